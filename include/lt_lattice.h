@@ -1,0 +1,154 @@
+/*
+ * lt_lattice.h -- C ABI of the MI355X (gfx950) recognition-lattice kernels.
+ *
+ * This is the drop-in boundary for the hot path of theadamsabra/last_torch:
+ * the semiring shortest distance / forward-backward over a GNAT recognition
+ * lattice built from alignments.FrameDependent x contexts.FullNGram, under
+ * semirings.Log / MaxTropical (and Real for the forward KATs).
+ *
+ * The reference has no FFI (it is pure PyTorch); every entry point below
+ * replaces one method of last_torch/lattices.py.RecognitionLattice and is the
+ * function that method's drop-in binds to (ctypes stub: INTEGRATION.md).
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers (caller-owned, e.g. from the PyTorch
+ *     caching allocator or hipMalloc). The library keeps no allocations.
+ *   - Arc weights W are one contiguous row-major tensor [B, T, C, V+1]:
+ *     W[b,t,p,0] = blank weight from context state p (weight_fns.py:69-71),
+ *     W[b,t,p,y] = lexical weight of label y in 1..V (weight_fns.py:72-75).
+ *     W must be 16-byte aligned; the 16-byte granule that holds its last byte
+ *     must be readable (always true for hipMalloc / torch allocations).
+ *     dtype: LT_DTYPE_F32 or LT_DTYPE_BF16; arithmetic is always fp32.
+ *   - C = sum_{i=0..n} V^i context states (contexts.py:181-182).
+ *   - Lengths (num_frames, num_labels) and labels are int32. Lengths are
+ *     clamped to [0, T] / labels outside [0, V] are treated as epsilon (0).
+ *   - Every call is asynchronous and ordered on `stream` (a hipStream_t;
+ *     NULL = legacy default stream). Calls are reentrant.
+ *   - Return value: LT_OK (0) or a negative LT_E* code; lt_last_error()
+ *     gives a thread-local message. No C++ exception crosses the ABI.
+ */
+#ifndef LT_LATTICE_H_
+#define LT_LATTICE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LT_OK 0
+#define LT_EINVAL (-1)       /* bad argument / shape */
+#define LT_EUNSUPPORTED (-2) /* configuration outside what the kernels do */
+#define LT_EHIP (-3)         /* HIP runtime error (launch, attribute) */
+
+#define LT_DTYPE_F32 0
+#define LT_DTYPE_BF16 1
+
+/* semirings.py: Log (184-305), MaxTropical (308-401), Real (143-173). */
+#define LT_SEMIRING_LOG 0
+#define LT_SEMIRING_MAX 1
+#define LT_SEMIRING_REAL 2
+
+/* shortest_path label convention.
+ * LT_LABELS_REFERENCE reproduces lattices.py:242-244 exactly: a lexical
+ * frame emits argmax over the 0-based vocab axis, i.e. label y as y-1.
+ * LT_LABELS_TRUE emits y (1..V) as documented at lattices.py:204-206. */
+#define LT_LABELS_TRUE 0
+#define LT_LABELS_REFERENCE 1
+
+typedef struct lt_problem {
+  int32_t batch;        /* B: number of utterances (flattened batch dims)  */
+  int32_t max_frames;   /* T: padded number of frames                      */
+  int32_t vocab_size;   /* V: lexical vocabulary size (FullNGram.vocab_size) */
+  int32_t context_size; /* n: FullNGram.context_size                       */
+  int32_t max_labels;   /* U: padded number of labels (0 if unused)        */
+  int32_t weight_dtype; /* LT_DTYPE_F32 or LT_DTYPE_BF16                    */
+} lt_problem;
+
+/* FullNGram.num_states() (contexts.py:181-182). */
+int lt_num_context_states(int32_t vocab_size, int32_t context_size,
+                          int64_t* num_states);
+
+/* RecognitionLattice._forward (lattices.py:379-496): shortest distance of the
+ * denominator lattice under `semiring`.
+ *   dist  [B]        out: (+)_q alpha_T[q]
+ *   alpha [B,T,C]    out (nullable): alpha_t before frame t, padding frames
+ *                    carry (lattices.py:460-462, 886-890). fp32. */
+int lt_den_forward(const lt_problem* pb, int32_t semiring, const void* W,
+                   const int32_t* num_frames, float* dist, float* alpha,
+                   void* stream);
+
+/* ForwardBackward.backward / _backward (lattices.py:514-642, 686-799) done
+ * right (reference defects D3/D4): backward weights + arc marginals.
+ *   dW[b,t,p,y] = grad[b] * exp(alpha_t[p] + W[b,t,p,y] + beta_{t+1}[next(p,y)]
+ *                 - log_z[b])   (alignments.py:300-318), 0 on padding frames.
+ *   log_z, alpha: outputs of lt_den_forward(LOG). grad nullable (= ones).
+ *   dW has W's dtype and shape. */
+int lt_den_backward(const lt_problem* pb, const void* W,
+                    const int32_t* num_frames, const float* log_z,
+                    const float* alpha, const float* grad, void* dW,
+                    void* stream);
+
+/* RecognitionLattice._string_forward (lattices.py:250-377): numerator
+ * (intersection with the label string) shortest distance.
+ *   labels [B,U] int32, num_labels [B] int32
+ *   num [B] out; alpha_num [B,T,U+1] out (nullable). */
+int lt_num_forward(const lt_problem* pb, int32_t semiring, const void* W,
+                   const int32_t* num_frames, const int32_t* labels,
+                   const int32_t* num_labels, float* num, float* alpha_num,
+                   void* stream);
+
+/* RecognitionLattice.forward (lattices.py:131-183), fused denominator +
+ * numerator in one launch (Log semiring).
+ *   local_norm != 0: LocallyNormalizedWeightFn (lattices.py:178-179),
+ *                    loss = -num and the denominator is skipped.
+ *   loss [B] out; log_z [B], num [B] out; alpha [B,T,C], alpha_num
+ *   [B,T,U+1] out (needed by lt_loss_backward; nullable otherwise). */
+int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
+                    const int32_t* num_frames, const int32_t* labels,
+                    const int32_t* num_labels, float* loss, float* log_z,
+                    float* num, float* alpha, float* alpha_num, void* stream);
+
+/* d loss / d W for lt_loss_forward (what loss.backward() in the reference
+ * should produce; it raises there, D1/D3):
+ *   dW = grad[b] * (den_marginals - num_marginals)   (global normalisation)
+ *   dW = -grad[b] * num_marginals                    (local_norm != 0)
+ * Utterances whose numerator is -inf (loss = +inf) get dW = 0.
+ * workspace: lt_loss_backward_workspace_bytes() bytes of device memory
+ * (0 for most shapes; then it may be NULL). */
+int lt_loss_backward_workspace_bytes(const lt_problem* pb, int32_t local_norm,
+                                     size_t* bytes);
+int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
+                     const int32_t* num_frames, const int32_t* labels,
+                     const int32_t* num_labels, const float* log_z,
+                     const float* num, const float* alpha,
+                     const float* alpha_num, const float* grad, void* dW,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* RecognitionLattice.shortest_path (lattices.py:185-247) without the
+ * cross-batch mask aliasing (D6): MaxTropical Viterbi with the reference's
+ * tie rules (blank wins ties, semirings.py:363; first argmax among lexical
+ * arcs and among final states, semirings.py:382).
+ *   labels [B,T] int64 out (0 = blank; lexical per label_convention; 0 on
+ *          padding frames), path_weight [B] out.
+ *   arcs   [B,T,C,V+1] (nullable, W's dtype): if given, receives grad[b] on
+ *          every arc of the best path and 0 elsewhere -- the vjp of
+ *          _forward(MaxTropical) (grad nullable = ones).
+ *   workspace: lt_viterbi_workspace_bytes() bytes of device memory. */
+int lt_viterbi_workspace_bytes(const lt_problem* pb, size_t* bytes);
+int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
+               int32_t label_convention, int64_t* labels, float* path_weight,
+               const float* grad, void* arcs, void* workspace,
+               size_t workspace_bytes, void* stream);
+
+/* Thread-local description of the last error; never NULL. */
+const char* lt_last_error(void);
+/* Library version string. */
+const char* lt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LT_LATTICE_H_ */

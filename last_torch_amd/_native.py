@@ -1,0 +1,204 @@
+"""ctypes binding of the HIP lattice library (liblt_lattice.so, include/lt_lattice.h).
+
+Every call is issued on ``torch.cuda.current_stream()`` and works on device
+tensors owned by the PyTorch caching allocator; the library never allocates.
+There is no CPU fallback: if the library is missing or no ROCm device is
+present, calls raise.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'liblt_lattice.so')
+
+LT_DTYPE_F32, LT_DTYPE_BF16 = 0, 1
+SEMIRING_LOG, SEMIRING_MAX, SEMIRING_REAL = 0, 1, 2
+LABELS_TRUE, LABELS_REFERENCE = 0, 1
+
+_lock = threading.Lock()
+_lib = None
+
+
+class LatticeLibraryError(RuntimeError):
+  """Raised when the HIP library is unavailable or a call fails."""
+
+
+class Problem(ctypes.Structure):
+  _fields_ = [('batch', ctypes.c_int32), ('max_frames', ctypes.c_int32),
+              ('vocab_size', ctypes.c_int32), ('context_size', ctypes.c_int32),
+              ('max_labels', ctypes.c_int32), ('weight_dtype', ctypes.c_int32)]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_SIG = {
+    'lt_num_context_states': [_I32, _I32, ctypes.POINTER(ctypes.c_int64)],
+    'lt_den_forward': [ctypes.POINTER(Problem), _I32, _P, _P, _P, _P, _P],
+    'lt_den_backward': [ctypes.POINTER(Problem), _P, _P, _P, _P, _P, _P, _P],
+    'lt_num_forward': [ctypes.POINTER(Problem), _I32, _P, _P, _P, _P, _P, _P, _P],
+    'lt_loss_forward': [ctypes.POINTER(Problem), _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    'lt_loss_backward_workspace_bytes': [ctypes.POINTER(Problem), _I32,
+                                         ctypes.POINTER(ctypes.c_size_t)],
+    'lt_loss_backward': [ctypes.POINTER(Problem), _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                         _P, _P, ctypes.c_size_t, _P],
+    'lt_viterbi_workspace_bytes': [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_size_t)],
+    'lt_viterbi': [ctypes.POINTER(Problem), _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t,
+                   _P],
+}
+EXPORTED = tuple(_SIG) + ('lt_last_error', 'lt_version')
+
+
+def lib():
+  """Loads liblt_lattice.so (built in-tree by __graft_entry__.build())."""
+  global _lib
+  with _lock:
+    if _lib is None:
+      if not os.path.exists(LIB_PATH):
+        raise LatticeLibraryError(
+            f'{LIB_PATH} is missing: build it with `python -c "import __graft_entry__ as g; '
+            'g.build()"` (hipcc --offload-arch=gfx950)')
+      l = ctypes.CDLL(LIB_PATH)
+      for name, argtypes in _SIG.items():
+        fn = getattr(l, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+      l.lt_last_error.restype = ctypes.c_char_p
+      l.lt_last_error.argtypes = []
+      l.lt_version.restype = ctypes.c_char_p
+      l.lt_version.argtypes = []
+      _lib = l
+  return _lib
+
+
+def version():
+  return lib().lt_version().decode()
+
+
+def _check(rc, what):
+  if rc != 0:
+    raise LatticeLibraryError(f'{what} failed ({rc}): {lib().lt_last_error().decode()}')
+
+
+def _ptr(t):
+  return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+  return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _problem(W, vocab_size, context_size, max_labels=0):
+  if W.dtype not in (torch.float32, torch.bfloat16):
+    raise TypeError(f'arc weights must be float32 or bfloat16, got {W.dtype}')
+  if not W.is_cuda:
+    raise LatticeLibraryError('lattice kernels need the arc weights on a ROCm device')
+  if not W.is_contiguous() or W.data_ptr() % 16:
+    raise ValueError('arc weights must be contiguous and 16-byte aligned')
+  B, T, C, R = W.shape
+  if R != vocab_size + 1:
+    raise ValueError(f'arc weights last dim {R} != vocab_size + 1 = {vocab_size + 1}')
+  return Problem(B, T, vocab_size, context_size, max_labels,
+                 LT_DTYPE_BF16 if W.dtype == torch.bfloat16 else LT_DTYPE_F32)
+
+
+def num_context_states(vocab_size, context_size):
+  out = ctypes.c_int64()
+  _check(lib().lt_num_context_states(vocab_size, context_size, ctypes.byref(out)),
+         'lt_num_context_states')
+  return out.value
+
+
+def _f32(shape, like):
+  return torch.empty(shape, dtype=torch.float32, device=like.device)
+
+
+def den_forward(W, num_frames, vocab_size, context_size, semiring, want_alpha=True):
+  """lt_den_forward: (dist [B], alpha [B,T,C] or None)."""
+  pb = _problem(W, vocab_size, context_size)
+  B, T, C, _ = W.shape
+  dist = _f32([B], W)
+  alpha = _f32([B, T, C], W) if want_alpha else None
+  _check(lib().lt_den_forward(ctypes.byref(pb), semiring, _ptr(W), _ptr(num_frames), _ptr(dist),
+                              _ptr(alpha), _stream()), 'lt_den_forward')
+  return dist, alpha
+
+
+def den_backward(W, num_frames, log_z, alpha, grad, vocab_size, context_size):
+  """lt_den_backward: grad-scaled arc marginals, W's dtype/shape."""
+  pb = _problem(W, vocab_size, context_size)
+  dW = torch.empty_like(W)
+  _check(lib().lt_den_backward(ctypes.byref(pb), _ptr(W), _ptr(num_frames), _ptr(log_z),
+                               _ptr(alpha), _ptr(grad), _ptr(dW), _stream()), 'lt_den_backward')
+  return dW
+
+
+def num_forward(W, num_frames, labels, num_labels, vocab_size, context_size, semiring,
+                want_alpha=True):
+  """lt_num_forward: (num [B], alpha_num [B,T,U+1] or None)."""
+  U = labels.shape[-1]
+  pb = _problem(W, vocab_size, context_size, U)
+  B, T = W.shape[:2]
+  num = _f32([B], W)
+  an = _f32([B, T, U + 1], W) if want_alpha else None
+  _check(lib().lt_num_forward(ctypes.byref(pb), semiring, _ptr(W), _ptr(num_frames),
+                              _ptr(labels), _ptr(num_labels), _ptr(num), _ptr(an), _stream()),
+         'lt_num_forward')
+  return num, an
+
+
+def loss_forward(W, num_frames, labels, num_labels, vocab_size, context_size, local_norm,
+                 want_alpha=True):
+  """lt_loss_forward: (loss, log_z, num, alpha, alpha_num)."""
+  U = labels.shape[-1]
+  pb = _problem(W, vocab_size, context_size, U)
+  B, T, C, _ = W.shape
+  loss, log_z, num = _f32([B], W), _f32([B], W), _f32([B], W)
+  alpha = _f32([B, T, C], W) if (want_alpha and not local_norm) else None
+  an = _f32([B, T, U + 1], W) if want_alpha else None
+  if local_norm:
+    log_z.zero_()
+  _check(lib().lt_loss_forward(ctypes.byref(pb), int(bool(local_norm)), _ptr(W),
+                               _ptr(num_frames), _ptr(labels), _ptr(num_labels), _ptr(loss),
+                               None if local_norm else _ptr(log_z), _ptr(num), _ptr(alpha),
+                               _ptr(an), _stream()), 'lt_loss_forward')
+  return loss, log_z, num, alpha, an
+
+
+def loss_backward(W, num_frames, labels, num_labels, log_z, num, alpha, alpha_num, grad,
+                  vocab_size, context_size, local_norm):
+  """lt_loss_backward: d loss / dW (scaled by grad), W's dtype/shape."""
+  U = labels.shape[-1]
+  pb = _problem(W, vocab_size, context_size, U)
+  ws_bytes = ctypes.c_size_t()
+  _check(lib().lt_loss_backward_workspace_bytes(ctypes.byref(pb), int(bool(local_norm)),
+                                                ctypes.byref(ws_bytes)),
+         'lt_loss_backward_workspace_bytes')
+  ws = (torch.empty([ws_bytes.value], dtype=torch.uint8, device=W.device)
+        if ws_bytes.value else None)
+  dW = torch.empty_like(W)
+  _check(lib().lt_loss_backward(ctypes.byref(pb), int(bool(local_norm)), _ptr(W),
+                                _ptr(num_frames), _ptr(labels), _ptr(num_labels), _ptr(log_z),
+                                _ptr(num), _ptr(alpha), _ptr(alpha_num), _ptr(grad), _ptr(dW),
+                                _ptr(ws), ws_bytes.value, _stream()), 'lt_loss_backward')
+  return dW
+
+
+def viterbi(W, num_frames, vocab_size, context_size, label_convention, grad=None,
+            want_arcs=False):
+  """lt_viterbi: (labels int64 [B,T], path_weight [B], arcs or None)."""
+  pb = _problem(W, vocab_size, context_size)
+  B, T = W.shape[:2]
+  ws_bytes = ctypes.c_size_t()
+  _check(lib().lt_viterbi_workspace_bytes(ctypes.byref(pb), ctypes.byref(ws_bytes)),
+         'lt_viterbi_workspace_bytes')
+  ws = torch.empty([max(ws_bytes.value, 1)], dtype=torch.uint8, device=W.device)
+  labels = torch.empty([B, T], dtype=torch.int64, device=W.device)
+  weight = _f32([B], W)
+  arcs = torch.empty_like(W) if want_arcs else None
+  _check(lib().lt_viterbi(ctypes.byref(pb), _ptr(W), _ptr(num_frames), label_convention,
+                          _ptr(labels), _ptr(weight), _ptr(grad), _ptr(arcs), _ptr(ws),
+                          ws_bytes.value, _stream()), 'lt_viterbi')
+  return labels, weight, arcs

@@ -1,0 +1,130 @@
+"""Context dependencies (mirrors last_torch/contexts.py).
+
+``FullNGram`` is the context DFA the HIP kernels implement natively (its
+index maps are evaluated in-kernel: DESIGN.md, "FullNGram index maps").
+The tensor methods below are the per-frame plugin surface
+(contexts.py:43-146); ``RecognitionLattice`` does not call them on its hot
+path.
+"""
+import abc
+import dataclasses
+
+import torch
+
+from last_torch_amd import semirings
+
+
+class ContextDependency(abc.ABC):
+  """A DFA over the lexical vocabulary whose states encode output history
+  (contexts.py:25-146). All states are final; label 0 is epsilon."""
+
+  @abc.abstractmethod
+  def shape(self) -> tuple[int, int]:
+    """(num_states, vocab_size)."""
+
+  @abc.abstractmethod
+  def start(self) -> int:
+    """Start state id."""
+
+  @abc.abstractmethod
+  def next_state(self, state: torch.Tensor, label: torch.Tensor) -> torch.Tensor:
+    """Transition; label 0 keeps the state (contexts.py:64-77)."""
+
+  @abc.abstractmethod
+  def forward_reduce(self, weights: torch.Tensor,
+                     semiring: semirings.Semiring) -> torch.Tensor:
+    """result[..., q] = (+)_{p -y-> q} weights[..., p, y-1] (contexts.py:79-94)."""
+
+  @abc.abstractmethod
+  def backward_broadcast(self, weights: torch.Tensor) -> torch.Tensor:
+    """result[..., p, y-1] = weights[..., next(p, y)] (contexts.py:96-107)."""
+
+  def walk_states(self, labels: torch.Tensor) -> torch.Tensor:
+    """States after each label prefix: [..., U] -> [..., U+1]
+    (contexts.py:109-146). states[..., 0] is the start state."""
+    labels = torch.as_tensor(labels)
+    states = [torch.full(labels.shape[:-1], self.start(), dtype=torch.int64,
+                         device=labels.device)]
+    for u in range(labels.shape[-1]):
+      states.append(self.next_state(states[-1], labels[..., u].to(torch.int64)))
+    return torch.stack(states, dim=-1)
+
+
+@dataclasses.dataclass(frozen=True)
+class FullNGram(ContextDependency):
+  """Every n-gram of length 0..context_size is a state, numbered in
+  lexicographic order; appending a label keeps the last context_size labels
+  (contexts.py:150-263, GNAT section 4.1)."""
+
+  vocab_size: int
+  context_size: int
+
+  def __post_init__(self):
+    if self.vocab_size <= 0:
+      raise ValueError(f'vocab_size should be > 0, but got vocab_size={self.vocab_size}')
+    if self.context_size < 0:
+      raise ValueError('context_size should be >= 0, but got '
+                       f'context_size={self.context_size}')
+
+  # sum_{i < k} V^i
+  def _geo(self, k: int) -> int:
+    return sum(self.vocab_size**i for i in range(max(k, 0)))
+
+  def num_states(self) -> int:
+    return self._geo(self.context_size + 1)
+
+  def shape(self) -> tuple[int, int]:
+    return self.num_states(), self.vocab_size
+
+  def start(self) -> int:
+    return 0
+
+  def next_state(self, state, label):
+    state = torch.as_tensor(state)
+    label = torch.as_tensor(label)
+    V, n = self.vocab_size, self.context_size
+    ascending = self._geo(n)  # histories shorter than n
+    grow = state * V + label
+    if n == 0:
+      full = torch.zeros_like(grow)
+    else:
+      full = torch.remainder(state - ascending, V**(n - 1)) * V + ascending + label - 1
+    nxt = torch.where(state < ascending, grow, full)
+    return torch.where(label == 0, state, nxt)
+
+  def next_state_table(self) -> torch.Tensor:
+    """[num_states, vocab_size]: table[p, y-1] = next_state(p, y) (contexts.py:258-263)."""
+    C, V = self.shape()
+    return self.next_state(torch.arange(C)[:, None], torch.arange(1, V + 1)[None, :])
+
+  def _arc_index(self, device):
+    # destination of arc (p, y) flattened as p*V + (y-1)
+    return self.next_state_table().reshape(-1).to(device)
+
+  def forward_reduce(self, weights, semiring):
+    if tuple(weights.shape[-2:]) != self.shape():
+      raise ValueError(f'weights.shape[-2:] should be {self.shape()} but got'
+                       f' {tuple(weights.shape[-2:])}')
+    C, V = self.shape()
+    batch = weights.shape[:-2]
+    dst = self._arc_index(weights.device)
+    flat = weights.reshape(*batch, C * V)
+    # group arcs by destination; every destination has the same in-degree
+    # except the start (none) and the ascending states (one).
+    out = []
+    for q in range(C):
+      idx = torch.nonzero(dst == q).flatten()
+      if idx.numel() == 0:
+        out.append(semiring.zeros(batch, weights.dtype, weights.device))
+      elif idx.numel() == 1:
+        out.append(flat[..., idx[0]])
+      else:
+        out.append(semiring.sum(flat[..., idx], dim=-1))
+    return torch.stack(out, dim=-1)
+
+  def backward_broadcast(self, weights):
+    C, V = self.shape()
+    if weights.shape[-1] != C:
+      raise ValueError(f'weights.shape[-1] should be {C} but got {weights.shape[-1]}')
+    dst = self._arc_index(weights.device)
+    return weights[..., dst].reshape(*weights.shape[:-1], C, V)

@@ -1,0 +1,370 @@
+"""Recognition lattice (mirrors last_torch/lattices.py).
+
+``RecognitionLattice`` keeps the reference's constructor and methods
+(lattices.py:103-247, 250-799). Each method materialises the frame's arc
+weights once through the ``WeightFn`` plugin as a contiguous
+[B, T, C, V+1] tensor and hands it to the HIP kernels in
+``liblt_lattice.so`` through ``_native`` (C ABI: include/lt_lattice.h):
+
+  forward         -> lt_loss_forward / lt_loss_backward   (one launch each)
+  _forward        -> lt_den_forward (Log, MaxTropical, Real);
+                     autograd: lt_den_backward (Log) / lt_viterbi arcs (Max)
+  _forward_backward -> lt_den_forward + lt_den_backward
+  _backward       -> lt_den_backward marginals, streamed to the callback
+  _string_forward -> lt_num_forward
+  shortest_path   -> lt_viterbi
+
+Supported: ``alignments.FrameDependent`` x ``contexts.FullNGram``. Anything
+else raises ``NotImplementedError`` -- there is no CPU fallback. Inputs on
+the CPU are moved to the current ROCm device and results moved back.
+Arbitrary batch dims are flattened (the reference's ``_string_forward``
+supports only one, D13).
+"""
+from collections.abc import Callable, Sequence
+from typing import Any, Generic, Optional, Protocol, TypeVar
+
+import torch
+import torch.nn as nn
+
+from last_torch_amd import _native
+from last_torch_amd import alignments
+from last_torch_amd import contexts
+from last_torch_amd import semirings
+from last_torch_amd import weight_fns
+
+T = TypeVar('T')
+
+_SEMIRING_IDS = {'Log': _native.SEMIRING_LOG, 'MaxTropical': _native.SEMIRING_MAX,
+                 'Real': _native.SEMIRING_REAL}
+
+
+def _semiring_id(semiring) -> int:
+  name = getattr(semiring, 'name', None)
+  if name not in _SEMIRING_IDS:
+    raise NotImplementedError(f'lattice kernels support Log, MaxTropical and Real, got {semiring!r}')
+  return _SEMIRING_IDS[name]
+
+
+def _compute_device(*tensors) -> torch.device:
+  for t in tensors:
+    if isinstance(t, torch.Tensor) and t.is_cuda:
+      return t.device
+  if not torch.cuda.is_available():
+    raise _native.LatticeLibraryError(
+        'last_torch_amd lattice operations run on a ROCm GPU (no CPU fallback); '
+        'no device is available')
+  return torch.device('cuda', torch.cuda.current_device())
+
+
+def _lengths(x, batch_numel, device) -> torch.Tensor:
+  return torch.as_tensor(x).reshape(batch_numel).to(device=device, dtype=torch.int32)
+
+
+def _kernel_weights(W: torch.Tensor) -> torch.Tensor:
+  if W.dtype not in (torch.float32, torch.bfloat16):
+    W = W.float()
+  W = W.contiguous()
+  if W.data_ptr() % 16:
+    W = W.clone()
+  return W
+
+
+class _LossFn(torch.autograd.Function):
+  """loss = log_z - num (or -num): lt_loss_forward / lt_loss_backward."""
+
+  @staticmethod
+  def forward(ctx, W, nf, labels, nl, V, n, local):
+    loss, log_z, num, alpha, an = _native.loss_forward(W, nf, labels, nl, V, n, local)
+    ctx.save_for_backward(W, nf, labels, nl, log_z, num,
+                          alpha if alpha is not None else log_z, an)
+    ctx.cfg = (V, n, local)
+    return loss
+
+  @staticmethod
+  def backward(ctx, g):
+    W, nf, labels, nl, log_z, num, alpha, an = ctx.saved_tensors
+    V, n, local = ctx.cfg
+    dW = _native.loss_backward(W, nf, labels, nl, log_z, num, None if local else alpha, an,
+                               g.float().contiguous(), V, n, local)
+    return dW, None, None, None, None, None, None
+
+
+class _DenFn(torch.autograd.Function):
+  """Denominator shortest distance; gradient = arc marginals (Log) or the
+  best-path indicator (MaxTropical)."""
+
+  @staticmethod
+  def forward(ctx, W, nf, V, n, sid):
+    dist, alpha = _native.den_forward(W, nf, V, n, sid, want_alpha=True)
+    ctx.save_for_backward(W, nf, dist, alpha)
+    ctx.cfg = (V, n, sid)
+    ctx.mark_non_differentiable(alpha)
+    return dist, alpha
+
+  @staticmethod
+  def backward(ctx, g, g_alpha):
+    del g_alpha  # alpha_0..T-1 is a checkpoint, not differentiated
+    W, nf, dist, alpha = ctx.saved_tensors
+    V, n, sid = ctx.cfg
+    g = g.float().contiguous()
+    if sid == _native.SEMIRING_LOG:
+      dW = _native.den_backward(W, nf, dist, alpha, g, V, n)
+    elif sid == _native.SEMIRING_MAX:
+      _, _, dW = _native.viterbi(W, nf, V, n, _native.LABELS_TRUE, grad=g, want_arcs=True)
+    else:
+      raise NotImplementedError('gradients of the Real-semiring distance are not supported')
+    return dW, None, None, None, None
+
+
+class _NumFn(torch.autograd.Function):
+  """Numerator (string) shortest distance; Log gradient = string marginals."""
+
+  @staticmethod
+  def forward(ctx, W, nf, labels, nl, V, n, sid):
+    num, an = _native.num_forward(W, nf, labels, nl, V, n, sid, want_alpha=True)
+    ctx.save_for_backward(W, nf, labels, nl, num, an)
+    ctx.cfg = (V, n, sid)
+    return num
+
+  @staticmethod
+  def backward(ctx, g):
+    W, nf, labels, nl, num, an = ctx.saved_tensors
+    V, n, sid = ctx.cfg
+    if sid != _native.SEMIRING_LOG:
+      raise NotImplementedError('string-distance gradients are supported for Log only')
+    # local-norm loss backward gives -grad * num marginals; feed -g.
+    dW = _native.loss_backward(W, nf, labels, nl, None, num, None, an,
+                               (-g).float().contiguous(), V, n, True)
+    return dW, None, None, None, None, None, None
+
+
+class RecognitionLattice(nn.Module, Generic[T]):
+  """GNAT recognition lattice = context dependency x alignment lattice, with
+  arc weights from a weight function (lattices.py:35-116)."""
+
+  def __init__(self, context: contexts.ContextDependency,
+               alignment: alignments.TimeSyncAlignmentLattice,
+               weight_fn_cacher_factory: Callable[[contexts.ContextDependency],
+                                                  weight_fns.WeightFnCacher[T]],
+               weight_fn_factory: Callable[[contexts.ContextDependency], weight_fns.WeightFn[T]]):
+    super().__init__()
+    self.context = context
+    self.alignment = alignment
+    self.weight_fn_cacher_factory = weight_fn_cacher_factory
+    self.weight_fn_factory = weight_fn_factory
+    self.weight_fn_cacher = weight_fn_cacher_factory(context)
+    self.weight_fn = weight_fn_factory(context)
+
+  # -- helpers -------------------------------------------------------------
+  def _ngram(self) -> tuple[int, int]:
+    if not isinstance(self.context, contexts.FullNGram):
+      raise NotImplementedError(f'lattice kernels implement FullNGram contexts, got '
+                                f'{type(self.context).__name__}')
+    if not isinstance(self.alignment, alignments.FrameDependent):
+      raise NotImplementedError(f'lattice kernels implement FrameDependent alignments, got '
+                                f'{type(self.alignment).__name__}')
+    return self.context.vocab_size, self.context.context_size
+
+  def build_cache(self) -> T:
+    """Builds the weight function cache (lattices.py:118-129)."""
+    return self.weight_fn_cacher()
+
+  def arc_weights(self, cache: T, frames: torch.Tensor) -> torch.Tensor:
+    """All arc weights [batch..., T, C, V+1]: [..., 0] blank, [..., y] label y.
+
+    Calls ``weight_fn(cache, frame)`` vectorised over time (the reference
+    vmaps weight_fn the same way, lattices.py:308-313), falling back to one
+    call per frame for weight functions vmap cannot trace.
+    """
+    tdim = frames.ndim - 2
+
+    def frame_weights(frame):
+      blank, lexical = self.weight_fn(cache, frame)
+      return torch.cat([blank[..., None], lexical], dim=-1)
+
+    try:
+      return torch.vmap(frame_weights, in_dims=tdim, out_dims=tdim, randomness='same')(frames)
+    except Exception:  # pylint: disable=broad-except
+      return torch.stack([frame_weights(frames[..., t, :]) for t in range(frames.shape[-2])],
+                         dim=tdim)
+
+  def _prepare(self, cache, frames, num_frames):
+    batch_dims = tuple(num_frames.shape)
+    if tuple(frames.shape[:-2]) != batch_dims:
+      raise ValueError('frames and num_frames have different batch_dims: '
+                       f'{tuple(frames.shape[:-2])} vs {batch_dims}')
+    V, n = self._ngram()
+    if cache is None:
+      cache = self.weight_fn_cacher()
+    W = self.arc_weights(cache, frames)
+    B = 1
+    for d in batch_dims:
+      B *= d
+    dev = _compute_device(W, frames, num_frames)
+    W = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
+    nf = _lengths(num_frames, B, dev)
+    return W, nf, batch_dims, B, V, n, cache
+
+  @staticmethod
+  def _home(x, like):
+    return x.to(like.device) if isinstance(like, torch.Tensor) else x
+
+  # -- public API ------------------------------------------------------------
+  def forward(self, frames: torch.Tensor, num_frames: torch.Tensor, labels: torch.Tensor,
+              num_labels: torch.Tensor, cache: Optional[T] = None) -> torch.Tensor:
+    """Negative sequence log-probability -log P(labels | frames)
+    (lattices.py:131-183); differentiable w.r.t. the weight function."""
+    batch_dims = tuple(num_frames.shape)
+    if tuple(frames.shape[:-2]) != batch_dims:
+      raise ValueError('frames and num_frames have different batch_dims: '
+                       f'{tuple(frames.shape[:-2])} vs {batch_dims}')
+    if tuple(labels.shape[:-1]) != batch_dims:
+      raise ValueError('labels and num_frames have different batch_dims: '
+                       f'{tuple(labels.shape[:-1])} vs {batch_dims}')
+    if tuple(num_labels.shape) != batch_dims:
+      raise ValueError('num_labels and num_frames have different batch_dims: '
+                       f'{tuple(num_labels.shape)} vs {batch_dims}')
+    W, nf, batch_dims, B, V, n, cache = self._prepare(cache, frames, num_frames)
+    lab = torch.as_tensor(labels).reshape(B, -1).to(device=W.device, dtype=torch.int32)
+    nl = _lengths(num_labels, B, W.device)
+    local = isinstance(self.weight_fn, weight_fns.LocallyNormalizedWeightFn)
+    loss = _LossFn.apply(W, nf, lab.contiguous(), nl, V, n, local)
+    return self._home(loss.reshape(batch_dims), frames)
+
+  def shortest_path(self, frames: torch.Tensor, num_frames: torch.Tensor,
+                    cache: Optional[T] = None, label_convention: str = 'reference'):
+    """Best alignment path (lattices.py:185-247).
+
+    Returns (alignment_labels [batch..., T], num_alignment_labels, path_weights).
+    ``label_convention='reference'`` (default) emits lexical label y as y-1
+    exactly like the reference (lattices.py:242-244);
+    ``'true'`` emits y. Unlike the reference, every utterance of a batch is
+    decoded independently (D6).
+    """
+    conv = {'reference': _native.LABELS_REFERENCE, 'true': _native.LABELS_TRUE}[label_convention]
+    W, nf, batch_dims, B, V, n, _ = self._prepare(cache, frames, num_frames)
+    with torch.no_grad():
+      labels, weights, _ = _native.viterbi(W.detach(), nf, V, n, conv)
+    labels = self._home(labels.reshape(*batch_dims, -1), frames)
+    num_alignment_labels = self.alignment.num_states() * num_frames
+    return labels, num_alignment_labels, self._home(weights.reshape(batch_dims), frames)
+
+  def _string_forward(self, cache: T, frames: torch.Tensor, num_frames: torch.Tensor,
+                      labels: torch.Tensor, num_labels: torch.Tensor,
+                      semiring: semirings.Semiring) -> torch.Tensor:
+    """Shortest distance on the lattice intersected with the label string
+    (lattices.py:250-377)."""
+    batch_dims = tuple(num_frames.shape)
+    if tuple(frames.shape[:-2]) != batch_dims:
+      raise ValueError('frames and num_frames have different batch_dims: '
+                       f'{tuple(frames.shape[:-2])} vs {batch_dims}')
+    if tuple(labels.shape[:-1]) != batch_dims:
+      raise ValueError('labels and num_frames have different batch_dims: '
+                       f'{tuple(labels.shape[:-1])} vs {batch_dims}')
+    if tuple(num_labels.shape) != batch_dims:
+      raise ValueError('num_labels and num_frames have different batch_dims: '
+                       f'{tuple(num_labels.shape)} vs {batch_dims}')
+    sid = _semiring_id(semiring)
+    W, nf, batch_dims, B, V, n, _ = self._prepare(cache, frames, num_frames)
+    lab = torch.as_tensor(labels).reshape(B, -1).to(device=W.device, dtype=torch.int32)
+    nl = _lengths(num_labels, B, W.device)
+    num = _NumFn.apply(W, nf, lab.contiguous(), nl, V, n, sid)
+    return self._home(num.reshape(batch_dims), frames)
+
+  def _forward(self, cache: T, frames: torch.Tensor, num_frames: torch.Tensor,
+               semiring: semirings.Semiring,
+               blank_mask: Optional[Sequence[torch.Tensor]] = None,
+               lexical_mask: Optional[Sequence[torch.Tensor]] = None):
+    """Shortest distance and alpha_0..T-1 (lattices.py:379-496).
+
+    Masks are added to the arc weights (lattices.py:450-453), so their
+    gradients are the arc marginals (Log) or the best-path indicator
+    (MaxTropical) -- per utterance, without the batch aliasing of D6.
+    """
+    for name, mask in (('blank_mask', blank_mask), ('lexical_mask', lexical_mask)):
+      if mask is not None and len(mask) != self.alignment.num_states():
+        raise ValueError(f'The length of {name} should be equal to '
+                         f'{self.alignment.num_states()} (the number of alignment states), '
+                         f'but is {len(mask)}')
+    sid = _semiring_id(semiring)
+    batch_dims = tuple(num_frames.shape)
+    if tuple(frames.shape[:-2]) != batch_dims:
+      raise ValueError('frames and num_frames have different batch_dims: '
+                       f'{tuple(frames.shape[:-2])} vs {batch_dims}')
+    V, n = self._ngram()
+    if cache is None:
+      cache = self.weight_fn_cacher()
+    W = self.arc_weights(cache, frames)
+    if blank_mask is not None:
+      W = torch.cat([W[..., :1] + blank_mask[0].to(W.device)[..., None], W[..., 1:]], dim=-1)
+    if lexical_mask is not None:
+      W = torch.cat([W[..., :1], W[..., 1:] + lexical_mask[0].to(W.device)], dim=-1)
+    B = 1
+    for d in batch_dims:
+      B *= d
+    dev = _compute_device(W, frames, num_frames)
+    Wk = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
+    nf = _lengths(num_frames, B, dev)
+    dist, alpha = _DenFn.apply(Wk, nf, V, n, sid)
+    C = alpha.shape[-1]
+    return (self._home(dist.reshape(batch_dims), frames),
+            self._home(alpha.reshape(*batch_dims, frames.shape[-2], C), frames))
+
+  def _forward_backward(self, cache: T, frames: torch.Tensor, num_frames: torch.Tensor):
+    """log_z with gradients from the backward algorithm (lattices.py:498-642;
+    the reference's backward raises, D3). Returns (log_z, alpha_0..T-1)."""
+    return self._forward(cache, frames, num_frames, semirings.Log)
+
+  class BackwardStepCallback(Protocol):
+    """Callback of the backward algorithm loop (lattices.py:644-684)."""
+
+    def __call__(self, weight_vjp_fn, carry, blank_marginal: torch.Tensor,
+                 lexical_marginals: torch.Tensor) -> tuple[Any, Any]:
+      raise NotImplementedError
+
+  def _backward(self, cache: T, frames: torch.Tensor, num_frames: torch.Tensor,
+                log_z: torch.Tensor, alpha_0_to_T_minus_1: torch.Tensor,
+                init_callback_carry: Any, callback: BackwardStepCallback):
+    """Arc marginals by the backward algorithm (lattices.py:686-799).
+
+    The marginals of every frame come from one ``lt_den_backward`` launch;
+    the callback then runs frame by frame from T-1 down to 0 (the reference
+    iterates in the wrong direction, D4) with ``weight_vjp_fn`` for that
+    frame. Outputs are stacked in time order along the frame axis.
+    """
+    batch_dims = tuple(num_frames.shape)
+    if tuple(frames.shape[:-2]) != batch_dims:
+      raise ValueError('frames and num_frames have different batch_dims: '
+                       f'{tuple(frames.shape[:-2])} vs {batch_dims}')
+    if tuple(log_z.shape) != batch_dims:
+      raise ValueError('log_z and num_frames have different batch_dims: '
+                       f'{tuple(log_z.shape)} vs {batch_dims}')
+    if tuple(alpha_0_to_T_minus_1.shape[:-2]) != batch_dims:
+      raise ValueError('alpha_0_to_T_minus_1 and num_frames have different '
+                       f'batch_dims: {tuple(alpha_0_to_T_minus_1.shape[:-2])} vs {batch_dims}')
+    V, n = self._ngram()
+    with torch.no_grad():
+      W = self.arc_weights(cache, frames)
+      B = 1
+      for d in batch_dims:
+        B *= d
+      dev = _compute_device(W, frames, num_frames)
+      Wk = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
+      nf = _lengths(num_frames, B, dev)
+      lz = log_z.detach().reshape(B).to(dev, torch.float32).contiguous()
+      al = alpha_0_to_T_minus_1.detach().reshape(B, Wk.shape[1], -1).to(dev, torch.float32)
+      marg = _native.den_backward(Wk, nf, lz, al.contiguous(), None, V, n).float()
+      marg = self._home(marg.reshape(*batch_dims, *marg.shape[1:]), frames)
+    tdim = len(batch_dims)
+    carry, outs = init_callback_carry, []
+    for t in reversed(range(frames.shape[-2])):
+      frame = frames.select(tdim, t)
+      _, vjp_fn = torch.func.vjp(lambda c, f: self.weight_fn(c, f), cache, frame)
+      m = marg.select(tdim, t)
+      carry, out = callback(weight_vjp_fn=vjp_fn, carry=carry, blank_marginal=m[..., 0],
+                            lexical_marginals=m[..., 1:])
+      outs.append(out)
+    outs.reverse()
+    stacked = torch.utils._pytree.tree_map(lambda *xs: torch.stack(xs, dim=tdim), *outs) \
+        if outs else None
+    return carry, stacked

@@ -1,0 +1,241 @@
+"""Semirings (mirrors last_torch/semirings.py).
+
+Plugin surface of the lattice path: ``Semiring`` with ``zeros / ones /
+times / plus / prod / sum`` (semirings.py:80-141). ``RecognitionLattice``
+selects its HIP kernel by semiring identity (``Log``, ``MaxTropical``,
+``Real``); the methods here are the per-element algebra used by the
+per-frame plugin methods (``FrameDependent.forward`` etc.).
+
+Differences from the reference, all bug fixes:
+  * ``Log.plus`` / ``Log.sum`` have working, NaN-safe gradients (the
+    reference's ``_LogAddExp.backward`` raises and ``_LogSumExp.backward``
+    returns zeros: SURVEY.md D1/D2).
+  * ``zeros`` / ``ones`` accept a ``device``.
+"""
+from collections.abc import Sequence
+from typing import Any, Generic, Optional, TypeVar
+
+import torch
+import torch.utils._pytree as pytree
+
+DType = Any
+T = TypeVar('T')
+
+
+def value_shape(x) -> tuple[int, ...]:
+  """Common shape of the leaves of a semiring value (semirings.py:30-62)."""
+  leaves = pytree.tree_leaves(x)
+  if not leaves or any(leaf is None for leaf in leaves):
+    raise ValueError(f'No common shape can be derived for an empty PyTree: {x!r}')
+  shapes = {tuple(leaf.shape) for leaf in leaves}
+  if len(shapes) != 1:
+    raise ValueError('A semiring value must consist of ndarrays of a common shape. '
+                     f'Got inconsistent shapes {sorted(shapes)} for PyTree: {x!r}')
+  return shapes.pop()
+
+
+def value_dtype(x):
+  """dtypes of a semiring value, in its PyTree structure (semirings.py:64-78)."""
+  return pytree.tree_map(lambda leaf: leaf.dtype, x)
+
+
+class Semiring(Generic[T]):
+  """Semiring interface (semirings.py:80-141). Unimplemented ops raise."""
+
+  def zeros(self, shape: Sequence[int], dtype: Optional[DType] = None, device=None) -> T:
+    raise NotImplementedError
+
+  def ones(self, shape: Sequence[int], dtype: Optional[DType] = None, device=None) -> T:
+    raise NotImplementedError
+
+  def times(self, a: T, b: T) -> T:
+    raise NotImplementedError
+
+  def plus(self, a: T, b: T) -> T:
+    raise NotImplementedError
+
+  def prod(self, a: T, dim: int) -> T:
+    raise NotImplementedError
+
+  def sum(self, a: T, dim: int) -> T:
+    raise NotImplementedError
+
+
+def _check_axis(a: torch.Tensor, dim: int) -> None:
+  if not isinstance(dim, int):
+    raise ValueError(f'Only int axis is supported, got axis={dim!r}')
+  if not -a.ndim <= dim < a.ndim:
+    raise ValueError(f'Invalid reduction axis={dim!r} for input shape {tuple(a.shape)}')
+
+
+def _empty_reduce_shape(a, dim):
+  dim = dim % a.ndim
+  return a.shape[:dim] + a.shape[dim + 1:]
+
+
+class _RealSemiring(Semiring[torch.Tensor]):
+  """(+, x) over the reals (semirings.py:143-173)."""
+
+  name = 'Real'
+
+  def zeros(self, shape, dtype=None, device=None):
+    return torch.zeros(tuple(shape), dtype=dtype, device=device)
+
+  def ones(self, shape, dtype=None, device=None):
+    return torch.ones(tuple(shape), dtype=dtype, device=device)
+
+  def times(self, a, b):
+    return a * b
+
+  def plus(self, a, b):
+    return a + b
+
+  def prod(self, a, dim):
+    return torch.prod(a, dim)
+
+  def sum(self, a, dim):
+    return torch.sum(a, dim)
+
+
+Real = _RealSemiring()
+
+
+def _safe_shift(m: torch.Tensor) -> torch.Tensor:
+  # semirings.py:248-255: a non-finite max is replaced by 0 before exp/log,
+  # so all -inf operands give -inf (gradient 0) and +inf propagates.
+  return torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+
+
+class _LogSumExpFn(torch.autograd.Function):
+  """logsumexp along ``dim`` with the reference's safe max.
+
+  Gradient: softmax weights; 0 for -inf operands, NaN where an operand is
+  +inf (an overflow upstream should not be silenced).
+  """
+
+  @staticmethod
+  def forward(ctx, a, dim):
+    c = _safe_shift(torch.amax(a, dim=dim, keepdim=True))
+    e = torch.exp(a - c)
+    z = torch.sum(e, dim=dim, keepdim=True)
+    ctx.save_for_backward(e, z)
+    ctx.dim = dim
+    return torch.squeeze(c + torch.log(z), dim)
+
+  @staticmethod
+  def backward(ctx, g):
+    e, z = ctx.saved_tensors
+    z = torch.where(z != 0, z, torch.ones_like(z))
+    return torch.unsqueeze(g, ctx.dim) * e / z, None
+
+
+class _LogAddExpFn(torch.autograd.Function):
+  """Binary logaddexp with the same safety rules (semirings.py:244-272)."""
+
+  @staticmethod
+  def forward(ctx, a, b):
+    c = _safe_shift(torch.maximum(a, b))
+    ea, eb = torch.exp(a - c), torch.exp(b - c)
+    z = ea + eb
+    ctx.save_for_backward(ea, eb, z)
+    return c + torch.log(z)
+
+  @staticmethod
+  def backward(ctx, g):
+    ea, eb, z = ctx.saved_tensors
+    s = g / torch.where(z != 0, z, torch.ones_like(z))
+    return s * ea, s * eb
+
+
+class _LogSemiring(Semiring[torch.Tensor]):
+  """(logaddexp, +) with zero = -inf, one = 0 (semirings.py:184-220)."""
+
+  name = 'Log'
+
+  def zeros(self, shape, dtype=None, device=None):
+    return torch.full(tuple(shape), -torch.inf, dtype=dtype, device=device)
+
+  def ones(self, shape, dtype=None, device=None):
+    return torch.zeros(tuple(shape), dtype=dtype, device=device)
+
+  def times(self, a, b):
+    return a + b
+
+  def plus(self, a, b):
+    a, b = torch.broadcast_tensors(a, b)
+    return _LogAddExpFn.apply(a, b)
+
+  def prod(self, a, dim):
+    return torch.sum(a, dim)
+
+  def sum(self, a, dim):
+    _check_axis(a, dim)
+    if a.numel() == 0:
+      return self.zeros(_empty_reduce_shape(a, dim), a.dtype, a.device)
+    return _LogSumExpFn.apply(a, dim % a.ndim)
+
+
+Log = _LogSemiring()
+
+
+class _MaximumFn(torch.autograd.Function):
+  """max(a, b); the gradient goes to ``a`` iff a >= b (semirings.py:354-371)."""
+
+  @staticmethod
+  def forward(ctx, a, b):
+    ctx.save_for_backward(a >= b)
+    return torch.maximum(a, b)
+
+  @staticmethod
+  def backward(ctx, g):
+    (choose_a,) = ctx.saved_tensors
+    return torch.where(choose_a, g, torch.zeros_like(g)), torch.where(choose_a, torch.zeros_like(g), g)
+
+
+class _MaxFn(torch.autograd.Function):
+  """max along dim; gradient one-hot on the first argmax (semirings.py:373-401)."""
+
+  @staticmethod
+  def forward(ctx, a, dim):
+    idx = torch.argmax(a, dim=dim, keepdim=True)
+    ctx.save_for_backward(idx)
+    ctx.shape, ctx.dim = a.shape, dim
+    return torch.squeeze(torch.gather(a, dim, idx), dim)
+
+  @staticmethod
+  def backward(ctx, g):
+    (idx,) = ctx.saved_tensors
+    out = torch.zeros(ctx.shape, dtype=g.dtype, device=g.device)
+    return out.scatter(ctx.dim, idx, torch.unsqueeze(g, ctx.dim)), None
+
+
+class _MaxTropicalSemiring(Semiring[torch.Tensor]):
+  """(max, +) with exactly one nonzero gradient per reduction, ties included
+  (semirings.py:308-351)."""
+
+  name = 'MaxTropical'
+
+  def zeros(self, shape, dtype=None, device=None):
+    return torch.full(tuple(shape), -torch.inf, dtype=dtype, device=device)
+
+  def ones(self, shape, dtype=None, device=None):
+    return torch.zeros(tuple(shape), dtype=dtype, device=device)
+
+  def times(self, a, b):
+    return a + b
+
+  def plus(self, a, b):
+    a, b = torch.broadcast_tensors(a, b)
+    return _MaximumFn.apply(a, b)
+
+  def prod(self, a, dim):
+    return torch.sum(a, dim)
+
+  def sum(self, a, dim):
+    _check_axis(a, dim)
+    if a.numel() == 0:
+      return self.zeros(_empty_reduce_shape(a, dim), a.dtype, a.device)
+    return _MaxFn.apply(a, dim % a.ndim)
+
+
+MaxTropical = _MaxTropicalSemiring()

@@ -1,0 +1,184 @@
+"""Weight functions (mirrors last_torch/weight_fns.py).
+
+A ``WeightFn`` produces the arc weights of one frame; it is the producer side
+of the lattice boundary (weight_fns.py:42-83). ``RecognitionLattice``
+materialises them once per call as one contiguous [B, T, C, V+1] tensor that
+the HIP kernels stream from HBM.
+
+Differences from the reference, all bug fixes:
+  * ``JointWeightFn`` owns its projections (created once, trainable,
+    deterministic) instead of building fresh random ``nn.Linear`` layers on
+    every call.
+  * ``SharedEmbCacher`` returns the embedding table tensor, not the module.
+  * ``SharedRNNCacher`` creates its default ``LSTMCell`` once.
+"""
+import abc
+from typing import Callable, Generic, Optional, TypeVar
+
+import einops
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+T = TypeVar('T')
+
+
+class WeightFn(nn.Module, Generic[T], abc.ABC):
+  """Computes (blank, lexical) arc weights for a frame (weight_fns.py:42-83).
+
+  state=None: blank [batch..., C], lexical [batch..., C, V].
+  state given: blank [batch...], lexical [batch..., V] for that state.
+  """
+
+  @abc.abstractmethod
+  def forward(self, cache: T, frame: torch.Tensor,
+              state: Optional[torch.Tensor] = None) -> tuple[torch.Tensor, torch.Tensor]:
+    raise NotImplementedError
+
+
+class WeightFnCacher(nn.Module, Generic[T], abc.ABC):
+  """Builds the static data a WeightFn reuses across frames (weight_fns.py:86-96)."""
+
+  @abc.abstractmethod
+  def forward(self) -> T:
+    """Builds the cached data."""
+
+
+def hat_normalize(blank: torch.Tensor, lexical: torch.Tensor):
+  """HAT local normalisation: sigmoid(blank) is P(blank), the lexical weights
+  are a log-softmax scaled by P(not blank) (weight_fns.py:99-117)."""
+  z = F.softplus(blank)  # log(1 + exp(blank)); log P(not blank) = -z
+  return blank - z, F.log_softmax(lexical, dim=-1) - z[..., None]
+
+
+def log_softmax_normalize(blank: torch.Tensor, lexical: torch.Tensor):
+  """Joint log-softmax over [blank, lexical] (weight_fns.py:120-136)."""
+  z = torch.logsumexp(torch.cat([blank[..., None], lexical], dim=-1), dim=-1)
+  return blank - z, lexical - z[..., None]
+
+
+class LocallyNormalizedWeightFn(WeightFn[T]):
+  """Wraps a WeightFn with a local normaliser. ``RecognitionLattice`` skips
+  the denominator for this type (lattices.py:178-179)."""
+
+  def __init__(self, weight_fn: WeightFn[T],
+               normalize: Callable[[torch.Tensor, torch.Tensor],
+                                   tuple[torch.Tensor, torch.Tensor]] = hat_normalize):
+    super().__init__()
+    self.weight_fn = weight_fn
+    self.normalize = normalize
+
+  def forward(self, cache, frame, state=None):
+    return self.normalize(*self.weight_fn(cache, frame, state))
+
+
+class JointWeightFn(WeightFn[torch.Tensor]):
+  """tanh(P_c ctx_emb[c] + P_f frame) -> (blank, V lexical) logits: the
+  shared-emb / shared-rnn weight function (weight_fns.py:174-227)."""
+
+  def __init__(self, vocab_size: int, hidden_size: int, device=None):
+    super().__init__()
+    self.vocab_size = vocab_size
+    self.hidden_size = hidden_size
+    self.context_projection = nn.LazyLinear(hidden_size, bias=False, device=device)
+    self.frame_projection = nn.LazyLinear(hidden_size, bias=False, device=device)
+    self.to_blank = nn.Linear(hidden_size, 1, device=device)
+    self.to_vocab = nn.Linear(hidden_size, vocab_size, device=device)
+
+  def forward(self, cache, frame, state=None):
+    ctx = cache
+    if state is None:
+      joint = self.context_projection(ctx) + self.frame_projection(frame)[..., None, :]
+    else:
+      ctx = torch.index_select(ctx, 0, state.reshape(-1).long()).reshape(
+          *state.shape, ctx.shape[-1])
+      joint = self.context_projection(ctx) + self.frame_projection(frame)
+    joint = torch.tanh(joint)
+    return self.to_blank(joint)[..., 0], self.to_vocab(joint)
+
+
+class SharedEmbCacher(WeightFnCacher[torch.Tensor]):
+  """An independent trainable [num_context_states, embedding_size] table
+  (weight_fns.py:230-242)."""
+
+  def __init__(self, num_context_states: int, embedding_size: int, device=None):
+    super().__init__()
+    self.num_context_states = num_context_states
+    self.embedding_size = embedding_size
+    self.embedding = nn.Embedding(num_context_states, embedding_size, device=device)
+
+  def forward(self):
+    return self.embedding.weight
+
+
+class SharedRNNCacher(WeightFnCacher[torch.Tensor]):
+  """Context embeddings from an RNN run over every n-gram history, in
+  FullNGram state order (weight_fns.py:245-294). LSTM cells contribute their
+  cell state, other cells their output."""
+
+  def __init__(self, vocab_size: int, context_size: int, rnn_size: int,
+               rnn_embedding_size: int, rnn_cell: Optional[nn.RNNCellBase] = None):
+    super().__init__()
+    self.vocab_size = vocab_size
+    self.context_size = context_size
+    self.rnn_size = rnn_size
+    self.rnn_embedding_size = rnn_embedding_size
+    self.embedding = nn.Embedding(vocab_size + 1, rnn_embedding_size)
+    self.rnn_cell = rnn_cell if rnn_cell is not None else nn.LSTMCell(
+        rnn_embedding_size, rnn_size)
+
+  def _step(self, inputs, state):
+    out = self.rnn_cell(inputs, state) if state is not None else self.rnn_cell(inputs)
+    if isinstance(out, tuple):  # LSTMCell: (h, c); the embedding is c
+      return out, out[1]
+    return out, out
+
+  def forward(self):
+    dev = self.embedding.weight.device
+    state, emb = self._step(self.embedding(torch.zeros([1], dtype=torch.long, device=dev)), None)
+    parts = [emb]
+    labels = self.embedding(torch.arange(1, self.vocab_size + 1, device=dev))
+    inputs = None
+    for order in range(self.context_size):
+      # histories of length order+1: prefix state (n) x appended label (v)
+      inputs = labels if order == 0 else einops.repeat(inputs, 'n ... -> (v n) ...',
+                                                       v=self.vocab_size)
+      tile = lambda x: einops.repeat(x, 'n ... -> (n v) ...', v=self.vocab_size)
+      state = tuple(tile(s) for s in state) if isinstance(state, tuple) else tile(state)
+      state, emb = self._step(inputs, state)
+      parts.append(emb)
+    return torch.cat(parts, dim=0)
+
+
+class NullCacher(WeightFnCacher[type(None)]):
+  """Returns None; pairs with TableWeightFn (weight_fns.py:297-304)."""
+
+  def forward(self):
+    return None
+
+
+class TableWeightFn(WeightFn[type(None)]):
+  """Looks arc weights up in a fixed table (weight_fns.py:307-342).
+
+  table: [batch..., input_vocab, C, 1+V]; frame[..., 0] is the integer row.
+  Weights are returned in float32 like the reference (weight_fns.py:333).
+  """
+
+  def __init__(self, table: torch.Tensor):
+    super().__init__()
+    self.table = table
+
+  def forward(self, cache, frame, state=None):
+    del cache
+    *batch, x, c, _ = self.table.shape
+    if tuple(frame.shape[:-1]) != tuple(batch):
+      raise ValueError(f'frame should have batch_dims={tuple(batch)} but '
+                       f'got ({tuple(frame.shape[:-1])})')
+    table = self.table.to(frame.device).float()
+    row = frame[..., 0].long()[..., None, None, None]
+    w = torch.take_along_dim(table, row.expand(*batch, 1, c, table.shape[-1]), dim=-3)[..., 0, :, :]
+    if state is not None:
+      st = torch.broadcast_to(torch.as_tensor(state, device=w.device), tuple(batch)).long()
+      w = torch.take_along_dim(w, st[..., None, None].expand(*batch, 1, w.shape[-1]),
+                               dim=-2)[..., 0, :]
+    return w[..., 0], w[..., 1:]
