@@ -1,19 +1,52 @@
 # Builds the HIP library (gfx950) and the CPU oracle. __graft_entry__.build() runs this.
+# The frame-recursion kernels are instantiated once per terms-per-lane value
+# (lt_inst.hip -DLT_P=..) so the objects compile in parallel (make -j).
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-HIPFLAGS ?= -O3 -std=c++17 -fPIC -shared --offload-arch=$(ARCH) -Wall
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall
+CSRC := last_torch_amd/csrc
+OBJ := build/obj
+# kernel variants LG_P (LG = log2 lanes per group, M1 = runtime); keep in sync
+# with LT_VARIANTS in lt_kernels.h
+VARIANTS := 3_5 2_9 1_4 1_3 2_5 3_3 2_3 M1_4 M1_8 M1_16
+INST_OBJS := $(foreach v,$(VARIANTS),$(OBJ)/lt_inst_$(v).o)
+lg_of = $(subst M1,-1,$(word 1,$(subst _, ,$(1))))
+lgn_of = $(word 1,$(subst _, ,$(1)))
+p_of = $(word 2,$(subst _, ,$(1)))
 LIB := last_torch_amd/liblt_lattice.so
+DEPS := $(CSRC)/lt_kernels.h include/lt_lattice.h
 
 all: $(LIB) oracle
 
-$(LIB): last_torch_amd/csrc/lt_lattice.hip include/lt_lattice.h
-	$(HIPCC) $(HIPFLAGS) -o $@ $<
+$(OBJ)/lt_inst_%.o: $(CSRC)/lt_inst.hip $(DEPS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DLT_LG=$(call lg_of,$*) -DLT_LGN=$(call lgn_of,$*) -DLT_P=$(call p_of,$*) -c -o $@ $<
+
+$(OBJ)/lt_lattice.o: $(CSRC)/lt_lattice.hip $(DEPS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJ)/lt_lattice.o $(INST_OBJS)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
 oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -f $(LIB)
+	rm -rf $(OBJ) $(LIB)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean
+
+# Diagnostic build with in-kernel s_memtime stamps (never shipped / loaded by
+# the package): build/stamps/liblt_lattice_stamps.so
+STAMP_OBJ := build/stamps
+$(STAMP_OBJ)/lt_inst_%.o: $(CSRC)/lt_inst.hip $(DEPS)
+	@mkdir -p $(STAMP_OBJ)
+	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -DLT_LG=$(call lg_of,$*) -DLT_LGN=$(call lgn_of,$*) -DLT_P=$(call p_of,$*) -c -o $@ $<
+$(STAMP_OBJ)/lt_lattice.o: $(CSRC)/lt_lattice.hip $(DEPS)
+	@mkdir -p $(STAMP_OBJ)
+	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -c -o $@ $<
+stamps: $(STAMP_OBJ)/lt_lattice.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(STAMP_OBJ)/liblt_lattice_stamps.so $^
+.PHONY: stamps

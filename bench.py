@@ -1,0 +1,246 @@
+"""Benchmark: Log-semiring lattice forward-backward (loss + dW) on MI355X.
+
+One step = one pass of the hot path over one batch of synthetic arc weights
+already resident in HBM: lt_loss_forward (fused denominator + numerator
+alpha) then lt_loss_backward (beta + arc marginals -> dW), plus, for N > 1,
+the single RCCL all-reduce of the summed loss.
+
+Workload (BASELINE.json configs[1], weak-scaled per GPU as configs[2]):
+B=64 utterances per GPU, T=1000 frames, U=100 labels, V=32, bigram FullNGram
+(C=33 context states), fp32. Metric: nominal lattice cells/s = B*T*U*C / s.
+
+Run: python bench.py [--gpus N --steps K --warmup W]
+     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from last_torch_amd import _native  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = 'lattice cells/s (B·T·U·|ctx|) at T=1000,U=100; 1/2/4/8-GPU scaling'
+
+
+def algorithmic_bytes(T, U, V, C, es=4):
+  """Per-frame algorithmic HBM bytes, split per kernel.
+
+  forward : W read once (C*(V+1)*es) + den alpha checkpoint write (4C)
+            + numerator gathers (2(U+1)*es) + numerator alpha write (4(U+1))
+  backward: W read + dW write (2*C*(V+1)*es) + den alpha read (4C)
+            + numerator gathers (2(U+1)*es) + numerator alpha read (4(U+1))
+  Sum = A_w(2 s_w + s_g) + 8C + (U+1)(4 s_w + 8): 15,756 B/frame for the
+  bigram fp32 U=100 workload.
+  """
+  Aw = C * (V + 1)
+  fwd = Aw * es + 4 * C + (U + 1) * (2 * es + 4)
+  bwd = 2 * Aw * es + 4 * C + (U + 1) * (2 * es + 4)
+  return fwd, bwd
+
+
+def make_inputs(B, T, U, V, C, device, seed, dtype=torch.float32):
+  g = torch.Generator(device=device)
+  g.manual_seed(seed)
+  W = torch.randn([B, T, C, V + 1], generator=g, device=device, dtype=torch.float32).to(dtype)
+  labels = torch.randint(1, V + 1, [B, U], generator=g, device=device, dtype=torch.int32)
+  nf = torch.full([B], T, dtype=torch.int32, device=device)
+  nl = torch.full([B], U, dtype=torch.int32, device=device)
+  return W, nf, labels, nl
+
+
+def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True):
+  """Returns (wall seconds over `steps`, fwd kernel ms list, bwd kernel ms list)."""
+  grad = torch.ones([W.shape[0]], dtype=torch.float32, device=W.device)
+  red = torch.zeros([1], dtype=torch.float32, device=W.device)
+
+  def step(ev=None):
+    if ev is not None:
+      ev[0].record()
+    loss, log_z, num, alpha, an = _native.loss_forward(W, nf, labels, nl, V, n, False)
+    if ev is not None:
+      ev[1].record()
+    dW = _native.loss_backward(W, nf, labels, nl, log_z, num, alpha, an, grad, V, n, False)
+    if ev is not None:
+      ev[2].record()
+    if dist_on:
+      red.copy_(loss.sum().reshape(1))
+      torch.distributed.all_reduce(red)
+    return dW
+
+  for _ in range(warmup):
+    step()
+  torch.cuda.synchronize()
+  if dist_on:
+    torch.distributed.barrier()
+  torch.cuda.synchronize()
+  evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)] \
+      if events else [None] * steps
+  t0 = time.perf_counter()
+  for i in range(steps):
+    step(evs[i])
+  torch.cuda.synchronize()
+  if dist_on:
+    torch.distributed.barrier()
+  torch.cuda.synchronize()
+  wall = time.perf_counter() - t0
+  fwd_ms = [e[0].elapsed_time(e[1]) for e in evs] if events else []
+  bwd_ms = [e[1].elapsed_time(e[2]) for e in evs] if events else []
+  return wall, fwd_ms, bwd_ms
+
+
+def cpu_baseline(T, U, V, n, C, sample_utts):
+  """The C oracle (single-threaded restatement of the reference) on a
+  bounded sample of the same workload: loss + dW for `sample_utts`
+  utterances of shape (T, U, V, n)."""
+  from oracle import oracle as orc
+  rng = np.random.default_rng(0)
+  W = rng.standard_normal((sample_utts, T, C, V + 1)).astype(np.float32)
+  nf = np.full([sample_utts], T, np.int32)
+  lab = rng.integers(1, V + 1, (sample_utts, U)).astype(np.int32)
+  nl = np.full([sample_utts], U, np.int32)
+  t0 = time.perf_counter()
+  orc.loss_grad(W, nf, lab, nl, V, n)
+  dt = time.perf_counter() - t0
+  return {
+      'value': sample_utts * T * U * C / dt,
+      'unit': 'cells/s',
+      'cores': 1,
+      'kind': 'port',
+      'sample': (f'oracle/lattice_oracle.c loss+dW (double precision, 1 thread) on '
+                 f'{sample_utts} utterances of T={T} U={U} V={V} n={n}: {dt:.2f} s'),
+  }
+
+
+def read_traffic(profile_json, kernel, B, T):
+  """HBM bytes per launch of `kernel` from a committed PMC summary
+  (profiles/*pmc*.json written by tools/pmc_summary.py), or None."""
+  try:
+    with open(profile_json) as f:
+      d = json.load(f)
+    k = d['kernels'][kernel]
+    if k.get('batch') != B or k.get('frames') != T:
+      return None
+    return k['hbm_bytes_per_launch']
+  except (OSError, KeyError, ValueError):
+    return None
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--gpus', type=int, default=1)
+  ap.add_argument('--steps', type=int, default=20)
+  ap.add_argument('--warmup', type=int, default=3)
+  ap.add_argument('--batch', type=int, default=64, help='utterances per GPU')
+  ap.add_argument('--frames', type=int, default=1000)
+  ap.add_argument('--labels', type=int, default=100)
+  ap.add_argument('--vocab', type=int, default=32)
+  ap.add_argument('--context', type=int, default=1)
+  ap.add_argument('--cpu-utts', type=int, default=int(os.environ.get('LT_BENCH_CPU_UTTS', 128)))
+  ap.add_argument('--no-north-star', action='store_true')
+  ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'))
+  args = ap.parse_args()
+
+  world = int(os.environ.get('WORLD_SIZE', '1'))
+  rank = int(os.environ.get('RANK', '0'))
+  local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+  dist_on = world > 1
+  torch.cuda.set_device(local_rank)
+  device = torch.device('cuda', local_rank)
+  if dist_on:
+    torch.distributed.init_process_group('nccl', device_id=device)
+
+  B, T, U, V, n = args.batch, args.frames, args.labels, args.vocab, args.context
+  C = _native.num_context_states(V, n)
+  W, nf, labels, nl = make_inputs(B, T, U, V, C, device, seed=1234 + rank)
+  wall, fwd_ms, bwd_ms = run_steps(W, nf, labels, nl, V, n, args.steps, args.warmup, dist_on)
+
+  t = torch.tensor([wall], dtype=torch.float64, device=device)
+  if dist_on:
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+  wall = float(t.item())
+  cells_per_step = world * B * T * U * C
+  value = cells_per_step * args.steps / wall
+
+  fwd_b, bwd_b = algorithmic_bytes(T, U, V, C)
+  fwd_avg = float(np.mean(fwd_ms)) * 1e-3
+  bwd_avg = float(np.mean(bwd_ms)) * 1e-3
+  dominant, dom_bytes, dom_s = ('loss_backward', bwd_b * B * T, bwd_avg) \
+      if bwd_avg >= fwd_avg else ('loss_forward', fwd_b * B * T, fwd_avg)
+  achieved = dom_bytes / dom_s / 1e9
+  kname = 'bwd_kernel' if dominant == 'loss_backward' else 'fwd_kernel'
+  traffic = read_traffic(args.pmc, kname, B, T)
+
+  result = None
+  if rank == 0:
+    result = {
+        'metric': METRIC,
+        'value': value,
+        'unit': 'cells/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': wall / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'synthetic (randn arc weights, uniform labels, full-length utterances)',
+        'config': {
+            'workload': (f'Log-semiring forward-backward (loss + dW), B={B}/GPU, T={T}, '
+                         f'U={U}, V={V}, FullNGram n={n} (C={C}), fp32 (BASELINE configs[1]; '
+                         f'configs[2] at 8 GPUs)'),
+            'batch_per_gpu': B, 'global_batch': B * world, 'frames': T, 'labels': U,
+            'vocab': V, 'context_size': n, 'context_states': C,
+            'parallelism': f'utterance-sharded x{world}, RCCL all-reduce of summed loss',
+        },
+        'kernels_ms': {'loss_forward': fwd_avg * 1e3, 'loss_backward': bwd_avg * 1e3},
+        'roofline': {
+            'bound': 'hbm',
+            'kernel': dominant,
+            'achieved': achieved,
+            'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s',
+            'frac': achieved / HBM_PEAK_GBS,
+            'traffic': traffic,
+            'algorithmic_bytes_per_frame': {'loss_forward': fwd_b, 'loss_backward': bwd_b},
+        },
+    }
+    step_bytes = (fwd_b + bwd_b) * B * T * world
+    result['step_gbs'] = step_bytes / (wall / args.steps) / 1e9
+
+  # north-star shape (B=256 on one GPU), measured in the same run at N=1
+  if not dist_on and not args.no_north_star and B != 256:
+    del W
+    torch.cuda.empty_cache()
+    W2, nf2, lab2, nl2 = make_inputs(256, T, U, V, C, device, seed=99)
+    wall2, f2, b2 = run_steps(W2, nf2, lab2, nl2, V, n, max(5, args.steps // 2), 2, False)
+    steps2 = max(5, args.steps // 2)
+    ms2 = wall2 / steps2 * 1e3
+    result['north_star_b256'] = {
+        'value': 256 * T * U * C * steps2 / wall2,
+        'ms_per_step': ms2,
+        'hbm_frac_step': (fwd_b + bwd_b) * 256 * T / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        'kernels_ms': {'loss_forward': float(np.mean(f2)), 'loss_backward': float(np.mean(b2))},
+        'frac_loss_backward': bwd_b * 256 * T / (float(np.mean(b2)) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+    }
+    del W2
+
+  if rank == 0 and not dist_on and args.cpu_utts > 0:
+    result['cpu_baseline'] = cpu_baseline(T, U, V, n, C, args.cpu_utts)
+  if rank == 0:
+    print(json.dumps(result), flush=True)
+  if dist_on:
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+  main()

@@ -1,0 +1,1116 @@
+// lt_kernels.h -- device code shared by the kernel translation units.
+// Included by lt_inst.hip (compiled once per terms-per-lane value P, so the
+// template instantiations build in parallel) and by lt_lattice.hip (host
+// side, C ABI, scatter / backtrace kernels).
+#pragma once
+// MI355X (gfx950 / CDNA4) kernels for the GNAT recognition
+// lattice hot path of theadamsabra/last_torch, behind the C ABI declared in
+// include/lt_lattice.h.
+//
+// What is computed (reference file:line in last_torch/):
+//   * denominator forward  alpha_{t+1} = FrameDependent.forward(alpha_t, W_t)
+//       lattices.py:379-496, alignments.py:286-297, contexts.py:207-230
+//   * denominator backward beta_t + arc marginals (FrameDependent.backward)
+//       lattices.py:686-799, alignments.py:300-318, contexts.py:232-256
+//   * numerator (string) forward / backward
+//       lattices.py:250-377, alignments.py:320-329
+//   * MaxTropical Viterbi + backtrace (shortest_path)
+//       lattices.py:185-247, semirings.py:354-401 (tie rules)
+//
+// Execution design:
+//   One workgroup per utterance; the recursion over frames is serial, the
+//   live front (all C context states, all U+1 string positions) is spread
+//   over the workgroup:
+//     waves [0, den_waves)            : denominator front, L lanes per
+//                                       context state ("group"), each lane a
+//                                       slice of the state's in/out arcs;
+//                                       group reductions with DPP.
+//     waves [den, den+aux)            : numerator front (one lane per string
+//                                       position) + (backward) the coalesced
+//                                       dW store of the previous frame.
+//     waves [den+aux, +load)          : loaders: LDS-DMA (global_load_lds
+//                                       dwordx4) of frame t+P into a ring of
+//                                       S = P+1 slots while frame t computes.
+//   One LDS barrier per frame. HBM is touched only by the streamed W rows,
+//   the (small) alpha checkpoints and dW.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "../../include/lt_lattice.h"
+
+#define LT_DEVINL __device__ __forceinline__
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// FullNGram index maps (contexts.py:181-256)
+// ---------------------------------------------------------------------------
+struct NGram {
+  int V;    // vocab size
+  int n;    // context size (order)
+  int C;    // number of states  sum_{i<=n} V^i
+  int An;   // ascending states  sum_{i<n}  V^i
+  int Apn;  // sum_{i<n-1} V^i   (first source row feeding full-order states)
+  int Vn1;  // V^(n-1) (n >= 1), 0 for n == 0
+  int K;    // lexical in-arcs per full-order destination (V+1, or V for n=0)
+};
+
+enum { M_LOG = 0, M_MAX = 1, M_REAL = 2 };
+
+constexpr float kInf = __builtin_huge_valf();
+
+// Destination q's lexical in-arcs, as arithmetic progressions:
+//   source  p_k = a0 + k*astr,  W element  e_k = w0 + k*wstr,  k in [0, kq)
+// (term order index o = 0 is the blank self loop, o = k+1 lexical arc k; the
+//  reference reduces the V+1 sources in ascending p, contexts.py:226-229).
+struct DestDesc {
+  int kq, a0, astr, w0, wstr;
+};
+
+__host__ __device__ inline DestDesc dest_desc(const NGram& g, int q) {
+  DestDesc d;
+  const int R = g.V + 1;
+  if (g.n == 0) {  // single state, V lexical self loops y = 1..V
+    d.kq = g.V; d.a0 = 0; d.astr = 0; d.w0 = 1; d.wstr = 1;
+  } else if (q == 0) {  // start state: no lexical in-arc (contexts.py:216-217)
+    d.kq = 0; d.a0 = 0; d.astr = 0; d.w0 = 0; d.wstr = 0;
+  } else if (q < g.An) {  // ascending: unique in-arc (contexts.py:222-225)
+    const int p = (q - 1) / g.V, y = (q - 1) % g.V + 1;
+    d.kq = 1; d.a0 = p; d.astr = 0; d.w0 = p * R + y; d.wstr = 0;
+  } else {  // full order: V+1 sources, same label (contexts.py:226-229)
+    const int jq = q - g.An;
+    const int pb = g.Apn + jq / g.V, y = jq % g.V + 1;
+    d.kq = g.K; d.a0 = pb; d.astr = g.Vn1; d.w0 = pb * R + y; d.wstr = g.Vn1 * R;
+  }
+  return d;
+}
+
+// next(p, y) = nb + y for y >= 1 (contexts.py:190-205); returns nb, and
+// *zero = true for n == 0 (every lexical arc loops to state 0).
+__host__ __device__ inline int next_base(const NGram& g, int p, bool* zero) {
+  *zero = (g.n == 0);
+  if (g.n <= 1) return 0;  // n = 1: next(p, y) = y for every p
+  if (p < g.An) return p * g.V;
+  return ((p - g.An) % g.Vn1) * g.V + g.An - 1;
+}
+
+// ---------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------
+LT_DEVINL float lt_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+// Arguments are sums of exp() with the max term == 1 (>= 1) or exactly 0.
+LT_DEVINL float lt_log(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
+
+template <int CTRL>
+LT_DEVINL float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+LT_DEVINL int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+// Partner exchange for butterfly stage s of a power-of-two lane group.
+// Stages 0-3 stay inside a DPP row (quad_perm / half_mirror / mirror);
+// stages 4-5 go through ds_bpermute. Valid for max / sum / (max,idx) merges
+// because after stage s every lane of a 2^s block holds the same value.
+// Butterfly stages of a power-of-two lane group. Stages 0-3 stay inside a
+// DPP row (quad_perm / row_half_mirror / row_mirror); stages 4-5 go through
+// ds_bpermute. Valid for max / sum / (max,idx) merges because after stage s
+// every lane of a 2^s block already holds the same value.
+template <int S>
+LT_DEVINL float xchg(float v) {
+  if constexpr (S == 0) return dppf<0xB1>(v);
+  else if constexpr (S == 1) return dppf<0x4E>(v);
+  else if constexpr (S == 2) return dppf<0x141>(v);
+  else if constexpr (S == 3) return dppf<0x140>(v);
+  else return __shfl_xor(v, 1 << S);
+}
+template <int S>
+LT_DEVINL int xchgi(int v) {
+  if constexpr (S == 0) return dppi<0xB1>(v);
+  else if constexpr (S == 1) return dppi<0x4E>(v);
+  else if constexpr (S == 2) return dppi<0x141>(v);
+  else if constexpr (S == 3) return dppi<0x140>(v);
+  else return __shfl_xor(v, 1 << S);
+}
+#define LT_STAGES(OP) OP(0) OP(1) OP(2) OP(3) OP(4) OP(5)
+
+LT_DEVINL float grp_max(float v, int lg) {
+#define LT_MAXST(S) if (lg > S) v = fmaxf(v, xchg<S>(v));
+  LT_STAGES(LT_MAXST)
+#undef LT_MAXST
+  return v;
+}
+LT_DEVINL float grp_sum(float v, int lg) {
+#define LT_SUMST(S) if (lg > S) v += xchg<S>(v);
+  LT_STAGES(LT_SUMST)
+#undef LT_SUMST
+  return v;
+}
+// first-max (lowest index wins ties): semirings.py:363 (blank term has the
+// lowest index) and :382 (torch.argmax returns the first maximum).
+LT_DEVINL void grp_argmax(float& v, int& i, int lg) {
+#define LT_ARGST(S)                                   \
+  if (lg > S) {                                       \
+    const float pv = xchg<S>(v);                      \
+    const int pi = xchgi<S>(i);                       \
+    if (pv > v || (pv == v && pi < i)) { v = pv; i = pi; } \
+  }
+  LT_STAGES(LT_ARGST)
+#undef LT_ARGST
+}
+
+// Log-semiring plus exactly as _LogAddExp.forward (semirings.py:248-255):
+// c = max(a,b), non-finite c replaced by 0.
+LT_DEVINL float log_plus(float a, float b) {
+  float c = fmaxf(a, b);
+  if (!__builtin_isfinite(c)) c = 0.f;
+  return c + lt_log(lt_exp(a - c) + lt_exp(b - c));
+}
+
+template <int MODE>
+LT_DEVINL float s_zero() { return MODE == M_REAL ? 0.f : -kInf; }
+template <int MODE>
+LT_DEVINL float s_one() { return MODE == M_REAL ? 1.f : 0.f; }
+template <int MODE>
+LT_DEVINL float s_times(float a, float b) { return MODE == M_REAL ? a * b : a + b; }
+template <int MODE>
+LT_DEVINL float s_plus(float a, float b) {
+  if (MODE == M_LOG) return log_plus(a, b);
+  if (MODE == M_MAX) return (a >= b) ? a : b;  // Maximum: choose a iff a >= b
+  return a + b;
+}
+
+template <bool BF16, typename I>
+LT_DEVINL float ldw(const unsigned char* p, I e) {
+  if constexpr (BF16) {
+    return __uint_as_float(((unsigned)((const unsigned short*)p)[e]) << 16);
+  } else {
+    return ((const float*)p)[e];
+  }
+}
+LT_DEVINL unsigned short f2bf(float f) {  // round to nearest even, NaN kept
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+template <bool BF16>
+LT_DEVINL void stw(void* p, long long e, float v) {
+  if constexpr (BF16) ((unsigned short*)p)[e] = f2bf(v);
+  else ((float*)p)[e] = v;
+}
+
+#ifdef LT_STAMPS
+// Diagnostic build only: block 0 records s_memtime at three points of every
+// frame for one wave per role: [role][i][k], k = 0 loop top, 1 after the
+// barrier, 2 end of the frame's work. Never in the shipped library.
+#define LT_STAMP(a, is_stamper, role_, i_, k_)                                      \
+  do {                                                                             \
+    if (blockIdx.x == 0 && a.stamps && (is_stamper))                               \
+      a.stamps[((long long)(role_) * a.T + (i_)) * 4 + (k_)] =                      \
+          (long long)__builtin_amdgcn_s_memtime();                                  \
+  } while (0)
+#else
+#define LT_STAMP(a, is_stamper, role_, i_, k_) \
+  do {                                          \
+  } while (0)
+#endif
+
+// LDS barrier: drains this wave's LDS ops, then s_barrier. The asm has a
+// memory clobber so the compiler cannot move LDS accesses across it, and it
+// does NOT wait on vmcnt: loads in flight (LDS-DMA ring) and global stores
+// (checkpoints) survive the barrier.
+LT_DEVINL void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// One LDS-DMA wave instruction: 64 lanes x 16 B from per-lane global
+// addresses into the contiguous 1 KiB at LDS byte address `lds_addr`
+// (wave-uniform, passed in M0). Issued from inline asm so the compiler's
+// waitcnt pass does not drain it at unrelated LDS reads; the loader waits
+// for it with a counted vmcnt (wait_vmcnt) before the consuming barrier.
+LT_DEVINL void glds16(const void* gsrc, unsigned lds_addr) {
+  unsigned keep;
+  lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
+#define LT_VMCNT_CASE(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+LT_DEVINL void wait_vmcnt(int n) {
+  switch (n < 0 ? 0 : (n > 63 ? 63 : n)) {
+    LT_VMCNT_CASE(0) LT_VMCNT_CASE(1) LT_VMCNT_CASE(2) LT_VMCNT_CASE(3)
+    LT_VMCNT_CASE(4) LT_VMCNT_CASE(5) LT_VMCNT_CASE(6) LT_VMCNT_CASE(7)
+    LT_VMCNT_CASE(8) LT_VMCNT_CASE(9) LT_VMCNT_CASE(10) LT_VMCNT_CASE(11)
+    LT_VMCNT_CASE(12) LT_VMCNT_CASE(13) LT_VMCNT_CASE(14) LT_VMCNT_CASE(15)
+    LT_VMCNT_CASE(16) LT_VMCNT_CASE(17) LT_VMCNT_CASE(18) LT_VMCNT_CASE(19)
+    LT_VMCNT_CASE(20) LT_VMCNT_CASE(21) LT_VMCNT_CASE(22) LT_VMCNT_CASE(23)
+    LT_VMCNT_CASE(24) LT_VMCNT_CASE(25) LT_VMCNT_CASE(26) LT_VMCNT_CASE(27)
+    LT_VMCNT_CASE(28) LT_VMCNT_CASE(29) LT_VMCNT_CASE(30) LT_VMCNT_CASE(31)
+    LT_VMCNT_CASE(32) LT_VMCNT_CASE(33) LT_VMCNT_CASE(34) LT_VMCNT_CASE(35)
+    LT_VMCNT_CASE(36) LT_VMCNT_CASE(37) LT_VMCNT_CASE(38) LT_VMCNT_CASE(39)
+    LT_VMCNT_CASE(40) LT_VMCNT_CASE(41) LT_VMCNT_CASE(42) LT_VMCNT_CASE(43)
+    LT_VMCNT_CASE(44) LT_VMCNT_CASE(45) LT_VMCNT_CASE(46) LT_VMCNT_CASE(47)
+    LT_VMCNT_CASE(48) LT_VMCNT_CASE(49) LT_VMCNT_CASE(50) LT_VMCNT_CASE(51)
+    LT_VMCNT_CASE(52) LT_VMCNT_CASE(53) LT_VMCNT_CASE(54) LT_VMCNT_CASE(55)
+    LT_VMCNT_CASE(56) LT_VMCNT_CASE(57) LT_VMCNT_CASE(58) LT_VMCNT_CASE(59)
+    LT_VMCNT_CASE(60) LT_VMCNT_CASE(61) LT_VMCNT_CASE(62)
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel arguments (passed by value)
+// ---------------------------------------------------------------------------
+constexpr int kMaxStreams = 3;
+enum { F_DEN = 1, F_NUM = 2, F_LOCAL = 4, F_LOSS = 8 };
+
+struct KArgs {
+  const unsigned char* W;
+  const int* nfr;
+  const int* labels;
+  const int* nlab;
+  const float* grad;
+  const float* log_z_in;
+  const float* num_in;
+  float* dist;       // den result (log_z / path weight)
+  float* alpha;      // [B,T,C] den alpha history
+  float* num;        // [B]
+  float* alpha_num;  // [B,T,U+1]
+  float* loss;       // [B]
+  unsigned char* bp; // [B,T,C] Viterbi backpointers
+  int* qstar;        // [B] Viterbi final state
+  void* dW;          // [B,T,C,V+1]
+  float* nm_side;    // [B,T,U+1,2] numerator marginals (direct path)
+  int* ctx_side;     // [B,U+1,2]    numerator arc rows (direct path)
+  int B, T, U, flags;
+  long long* stamps; // diagnostic build (-DLT_STAMPS) only: per-step clocks
+  int dbg;           // ablation bitmask (LT_DBG, timing experiments only): 1 skip den
+                     // compute, 2 skip numerator, 4 loaders issue nothing, 8 no barrier
+  NGram g;
+  int FR;            // C*(V+1) elements per frame
+  int den_groups;    // denominator groups (forward: destinations, backward: sources)
+  int den_q0;        // state of group 0 (forward n >= 1: 1, the start state is extra0)
+  int extra0;        // forward n >= 1: den lane 0 also does the start state (blank only)
+  int den_fast;      // every den lane owns at most one group (slices precomputed)
+  int Pr;            // terms per lane (block size of the lane slice, <= template P)
+  // layout
+  int L, lgL, den_waves, aux_waves, load_waves;
+  int S, P, slot_bytes;
+  // staged streams, fixed slots: 0 = W rows, 1 = alpha rows, 2 = alpha_num
+  // rows; st_ninstr[s] == 0 means stream s is not staged. Only indexed with
+  // compile-time constants (runtime-indexed kernel-argument arrays would be
+  // copied to scratch).
+  const unsigned char* st_base[kMaxStreams];
+  long long st_row[kMaxStreams];   // bytes per frame row
+  int st_ninstr[kMaxStreams];      // LDS-DMA wave instructions per frame
+  int st_off[kMaxStreams];         // byte offset inside a slot
+  int gw0, gw1;                    // instructions per frame of loader wave 0 / 1
+  int off_ring, off_a, off_na, off_ctx, off_ylab, off_dbuf, off_nbuf, off_misc;
+};
+
+LT_DEVINL unsigned lds_base_addr(unsigned char* lds) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
+}
+
+// Issue loader wave `lw`'s LDS-DMA instructions for frame t into `slot`.
+// The frame's instructions are numbered across the streams in slot order
+// (stream 0 first); wave lw issues numbers lw, lw + load_waves, ...
+// Streams are visited with compile-time indices so every parameter stays in
+// SGPRs (a runtime-indexed kernel argument becomes a vector load whose
+// vmcnt wait would drain the DMA ring).
+template <int S>
+LT_DEVINL void issue_stream(const KArgs& a, long long bt, unsigned sbase, int first, int lw,
+                            int lane) {
+  const int ni = a.st_ninstr[S];
+  if (ni == 0) return;
+  const long long row = a.st_row[S];
+  const long long off = bt * row;
+  const long long g1 = (off + row + 15) >> 4;
+  const unsigned char* base = a.st_base[S];
+  const unsigned dst = sbase + a.st_off[S];
+  // first k with (first + k) % load_waves == lw
+  int k = lw - first % a.load_waves;
+  if (k < 0) k += a.load_waves;
+  for (; k < ni; k += a.load_waves) {
+    long long gg = (off >> 4) + (long long)k * 64 + lane;
+    if (gg > g1 - 1) gg = g1 - 1;  // in-bounds duplicate, lands past the row
+    glds16(base + gg * 16, dst + k * 1024);
+  }
+}
+LT_DEVINL void issue_frame(const KArgs& a, int b, int t, int slot, int lw, int lane,
+                           unsigned ldsb) {
+  const unsigned sbase = ldsb + a.off_ring + slot * a.slot_bytes;
+  const long long bt = (long long)b * a.T + t;
+  issue_stream<0>(a, bt, sbase, 0, lw, lane);
+  issue_stream<1>(a, bt, sbase, a.st_ninstr[0], lw, lane);
+  issue_stream<2>(a, bt, sbase, a.st_ninstr[0] + a.st_ninstr[1], lw, lane);
+}
+
+// Address (in LDS) of stream S's row for frame t held in `slot`.
+template <int S>
+LT_DEVINL const unsigned char* slot_row(unsigned char* lds, const KArgs& a, int b, int t,
+                                        int slot) {
+  const long long off = ((long long)b * a.T + t) * a.st_row[S];
+  return lds + a.off_ring + slot * a.slot_bytes + a.st_off[S] + (int)(off & 15);
+}
+
+// Walk the context DFA along the label string (contexts.py:109-146) and the
+// numerator gather indices (lattices.py:314-338): ctx[u] = c_u*(V+1),
+// ylab[u] = safe class of labels[u] (0 -> 1, lattices.py:314-315), u < U.
+// Phase 1 (all aux lanes): labels -> ylab (raw). Phase 2 (one lane, after a
+// barrier): the serial walk over LDS.
+LT_DEVINL void load_labels(const KArgs& a, int b, int* ylab, int al, int aux_lanes) {
+  for (int u = al; u < a.U; u += aux_lanes) ylab[u] = a.labels[(long long)b * a.U + u];
+}
+LT_DEVINL void walk_states(const KArgs& a, int* ctx, int* ylab) {
+  const NGram& g = a.g;
+  const int R = g.V + 1;
+  int c = 0;
+  for (int u = 0; u <= a.U; ++u) {
+    ctx[u] = c * R;
+    if (u < a.U) {
+      int y = ylab[u];
+      if (y < 0 || y > g.V) y = 0;
+      ylab[u] = y < 1 ? 1 : y;
+      if (y != 0) {
+        bool z;
+        const int nb = next_base(g, c, &z);
+        c = z ? 0 : nb + y;
+      }
+    } else {
+      ylab[u] = 1;
+    }
+  }
+}
+
+// Lane slice of a forward group (destination q): term order index
+// o in [j*P, j*P+P) of {blank, lexical k = o-1}; aoff = alpha index,
+// woff = W element of the frame. Returns the count of valid terms.
+template <int P>
+LT_DEVINL int fwd_slice(const NGram& g, int q, int j, int Pr, int* aoff, int* woff) {
+  const DestDesc d = dest_desc(g, q);
+  const int nterm = d.kq + 1, R = g.V + 1;
+  int nv = 0;
+#pragma unroll
+  for (int m = 0; m < P; ++m) {
+    const int o = j * Pr + m;
+    int ai = 0, wi = 0;
+    if (m < Pr && o < nterm) {
+      if (o == 0) { ai = q; wi = q * R; }
+      else { const int k = o - 1; ai = d.a0 + k * d.astr; wi = d.w0 + k * d.wstr; }
+      nv = m + 1;
+    }
+    aoff[m] = ai;
+    woff[m] = wi;
+  }
+  return nv;
+}
+
+// Lane slice of a backward group (source p): labels y in [j*P, j*P+P);
+// woff = W element p*(V+1)+y, boff = beta index of next(p, y).
+template <int P>
+LT_DEVINL int bwd_slice(const NGram& g, int p, int j, int Pr, int* woff, int* boff) {
+  bool zero;
+  const int nb = next_base(g, p, &zero);
+  const int R = g.V + 1;
+  int nv = 0;
+#pragma unroll
+  for (int m = 0; m < P; ++m) {
+    const int y = j * Pr + m;
+    int wi = 0, bi = 0;
+    if (m < Pr && y <= g.V) {
+      wi = p * R + y;
+      bi = (y == 0) ? p : (zero ? 0 : nb + y);
+      nv = m + 1;
+    }
+    woff[m] = wi;
+    boff[m] = bi;
+  }
+  return nv;
+}
+
+// Group reductions with a compile-time group size 2^LG (LG < 0: runtime lg).
+template <int LG>
+LT_DEVINL float gmax(float v, int lg) {
+  if constexpr (LG < 0) {
+    return grp_max(v, lg);
+  } else {
+    if constexpr (LG > 0) v = fmaxf(v, xchg<0>(v));
+    if constexpr (LG > 1) v = fmaxf(v, xchg<1>(v));
+    if constexpr (LG > 2) v = fmaxf(v, xchg<2>(v));
+    if constexpr (LG > 3) v = fmaxf(v, xchg<3>(v));
+    if constexpr (LG > 4) v = fmaxf(v, xchg<4>(v));
+    if constexpr (LG > 5) v = fmaxf(v, xchg<5>(v));
+    return v;
+  }
+}
+template <int LG>
+LT_DEVINL float gsum(float v, int lg) {
+  if constexpr (LG < 0) {
+    return grp_sum(v, lg);
+  } else {
+    if constexpr (LG > 0) v += xchg<0>(v);
+    if constexpr (LG > 1) v += xchg<1>(v);
+    if constexpr (LG > 2) v += xchg<2>(v);
+    if constexpr (LG > 3) v += xchg<3>(v);
+    if constexpr (LG > 4) v += xchg<4>(v);
+    if constexpr (LG > 5) v += xchg<5>(v);
+    return v;
+  }
+}
+template <int S>
+LT_DEVINL void argmax_stage(float& v, int& i) {
+  const float pv = xchg<S>(v);
+  const int pi = xchgi<S>(i);
+  if (pv > v || (pv == v && pi < i)) { v = pv; i = pi; }
+}
+template <int LG>
+LT_DEVINL void gargmax(float& v, int& i, int lg) {
+  if constexpr (LG < 0) {
+    grp_argmax(v, i, lg);
+  } else {
+    if constexpr (LG > 0) argmax_stage<0>(v, i);
+    if constexpr (LG > 1) argmax_stage<1>(v, i);
+    if constexpr (LG > 2) argmax_stage<2>(v, i);
+    if constexpr (LG > 3) argmax_stage<3>(v, i);
+    if constexpr (LG > 4) argmax_stage<4>(v, i);
+    if constexpr (LG > 5) argmax_stage<5>(v, i);
+  }
+}
+
+// Semiring reduction of a group's terms (x[m] for m >= nv already = zero).
+// Log follows _LogSumExp.forward (semirings.py:279-286); Max returns the
+// first maximum's term order index in *bi (semirings.py:363, :382).
+template <int MODE, int LG, int P>
+LT_DEVINL float group_reduce(const float* x, int lgL, int o0, int* bi) {
+  if constexpr (MODE == M_LOG) {
+    float mx = x[0];
+#pragma unroll
+    for (int m = 1; m < P; ++m) mx = fmaxf(mx, x[m]);
+    mx = gmax<LG>(mx, lgL);
+    const float c = __builtin_isfinite(mx) ? mx : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < P; ++m) s += lt_exp(x[m] - c);
+    s = gsum<LG>(s, lgL);
+    return c + lt_log(s);
+  } else if constexpr (MODE == M_MAX) {
+    float r = x[0];
+    int i = o0;
+#pragma unroll
+    for (int m = 1; m < P; ++m)
+      if (x[m] > r) { r = x[m]; i = o0 + m; }
+    gargmax<LG>(r, i, lgL);
+    *bi = i;
+    return r;
+  } else {
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < P; ++m) s += x[m];
+    return gsum<LG>(s, lgL);
+  }
+}
+
+// Per-role frame loops. Every role runs exactly nf iterations with one LDS
+// barrier each (the only cross-wave synchronisation); each loop carries only
+// its own loop state, and frame addresses advance incrementally.
+LT_DEVINL void idle_loop(int nf) {
+  for (int i = 0; i < nf; ++i) lds_barrier();
+}
+
+// Loader: frame f(i) = reverse ? nf-1-i : i goes to slot i % S; at step i
+// frame f(i+P) is issued after the barrier and frame f(i+1) is waited for
+// before the next one (counted vmcnt).
+LT_DEVINL void loader_loop(const KArgs& a, int b, int nf, bool reverse, int lw, int lane,
+                           unsigned ldsb) {
+  const int gw = lw == 0 ? a.gw0 : a.gw1;
+  int slot = 0;
+  const bool st = lw == 0 && lane == 0;
+  for (int i = 0; i < nf; ++i) {
+    LT_STAMP(a, st, 2, i, 0);
+    if (!(a.dbg & 4)) {
+      const int later = (a.P - 1 < nf - 1 - i) ? a.P - 1 : nf - 1 - i;
+      wait_vmcnt(later * gw);
+    }
+    lds_barrier();
+    LT_STAMP(a, st, 2, i, 1);
+    if (i + a.P < nf && !(a.dbg & 4)) {
+      const int s2 = slot + a.P >= a.S ? slot + a.P - a.S : slot + a.P;
+      const int f = reverse ? nf - 1 - (i + a.P) : i + a.P;
+      issue_frame(a, b, f, s2, lw, lane, ldsb);
+    }
+    slot = (slot + 1 == a.S) ? 0 : slot + 1;
+    LT_STAMP(a, st, 2, i, 2);
+  }
+}
+
+// Cursor over the rows of one stream for successive frames: LDS address of
+// the staged row (ring slot + 16-B misalignment) and the global row.
+struct Cursor {
+  int soff;        // slot * slot_bytes
+  int mis;         // global byte offset & 15
+  int dmis;        // row bytes & 15, signed step
+  long long goff;  // global byte offset of the row
+  long long step;  // +-row bytes
+};
+LT_DEVINL Cursor make_cursor(long long row, long long first_row_index, bool reverse) {
+  Cursor c;
+  c.soff = 0;
+  c.goff = first_row_index * row;
+  c.mis = (int)(c.goff & 15);
+  c.dmis = (int)(row & 15);
+  if (reverse) c.dmis = -c.dmis;
+  c.step = reverse ? -row : row;
+  return c;
+}
+LT_DEVINL void advance(Cursor& c, const KArgs& a) {
+  c.soff += a.slot_bytes;
+  if (c.soff == a.S * a.slot_bytes) c.soff = 0;
+  c.mis = (c.mis + c.dmis) & 15;
+  c.goff += c.step;
+}
+
+// ---------------------------------------------------------------------------
+// Forward kernel: denominator and/or numerator, Log / MaxTropical / Real.
+// ---------------------------------------------------------------------------
+template <int MODE, bool BF16, bool WST, int LG, int P>
+LT_DEVINL void den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int b, int nf,
+                            int tid) {
+  const NGram& g = a.g;
+  const int C = g.C;
+  const int lgL = LG >= 0 ? LG : a.lgL;
+  const int L = 1 << lgL;
+  const int j = tid & (L - 1);
+  const int grp = tid >> lgL;
+  const int ngrp = (a.den_waves * 64) >> lgL;
+  const bool fast = a.den_fast;
+  const bool has = grp < a.den_groups;
+  int aoff[P], woff[P];
+  int nv = 0;
+  const int q = a.den_q0 + grp;
+  if (fast && has) nv = fwd_slice<P>(g, q, j, a.Pr, aoff, woff);
+  const unsigned char* ring = lds + a.off_ring + a.st_off[0];
+  Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)a.FR * (BF16 ? 2 : 4),
+                          (long long)b * a.T, false);
+  float* hist = a.alpha ? a.alpha + (long long)b * a.T * C : nullptr;
+  unsigned char* bpp = a.bp ? a.bp + (long long)b * a.T * C : nullptr;
+  for (int i = 0; i < nf; ++i) {
+    LT_STAMP(a, tid == 0, 0, i, 0);
+    lds_barrier();
+    LT_STAMP(a, tid == 0, 0, i, 1);
+    const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
+    const float* acur = abuf + (i & 1) * C;
+    float* anxt = abuf + ((i + 1) & 1) * C;
+    for (int qq = fast ? q : a.den_q0 + grp; qq < C; qq += ngrp) {
+      if (fast && !has) break;
+      int ao[P], wo[P];
+      int n2 = nv;
+      if (fast) {
+#pragma unroll
+        for (int m = 0; m < P; ++m) { ao[m] = aoff[m]; wo[m] = woff[m]; }
+      } else {
+        n2 = fwd_slice<P>(g, qq, j, a.Pr, ao, wo);
+      }
+      float x[P];
+      float aself = 0.f;
+#pragma unroll
+      for (int m = 0; m < P; ++m) {
+        const float av = acur[ao[m]];
+        const float wv = ldw<BF16>(wrow, wo[m]);
+        if (m == 0) aself = av;
+        x[m] = m < n2 ? s_times<MODE>(av, wv) : s_zero<MODE>();
+      }
+      int bi = 0;
+      const float r = group_reduce<MODE, LG, P>(x, lgL, j * a.Pr, &bi);
+      if (j == 0) {
+        anxt[qq] = r;
+        if (hist) hist[qq] = aself;
+        if (MODE == M_MAX && bpp) bpp[qq] = (unsigned char)bi;
+      }
+      if (fast) break;
+    }
+    if (a.extra0 && tid == 0) {  // start state: blank self loop only
+      const float av = acur[0];
+      anxt[0] = s_times<MODE>(av, ldw<BF16>(wrow, 0));
+      if (hist) hist[0] = av;
+      if (MODE == M_MAX && bpp) bpp[0] = 0;
+    }
+    advance(cw, a);
+    if (hist) hist += C;
+    if (bpp) bpp += C;
+    LT_STAMP(a, tid == 0, 0, i, 2);
+  }
+}
+
+template <int MODE, bool BF16, bool WST>
+LT_DEVINL void num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, const int* ctx,
+                            const int* ylab, int b, int nf, int al, int aux_lanes) {
+  const int NP = a.U + 1;
+  int ob = 0, olm = 0;
+  if (al < NP) {
+    ob = ctx[al];
+    if (al >= 1) olm = ctx[al - 1] + ylab[al - 1];
+  }
+  const unsigned char* ring = lds + a.off_ring + a.st_off[0];
+  Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)a.FR * (BF16 ? 2 : 4),
+                          (long long)b * a.T, false);
+  float* hist = a.alpha_num ? a.alpha_num + (long long)b * a.T * NP : nullptr;
+  for (int i = 0; i < nf; ++i) {
+    LT_STAMP(a, al == 0, 1, i, 0);
+    lds_barrier();
+    LT_STAMP(a, al == 0, 1, i, 1);
+    const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
+    const float* ncur = nbuf + (i & 1) * NP;
+    float* nnxt = nbuf + ((i + 1) & 1) * NP;
+    for (int u = al; u < NP; u += aux_lanes) {
+      int o0 = ob, o2 = olm;
+      if (u != al) { o0 = ctx[u]; o2 = ctx[u - 1] + ylab[u - 1]; }
+      const float cu = ncur[u];
+      const float xb = s_times<MODE>(cu, ldw<BF16>(wrow, o0));
+      float xl = s_zero<MODE>();
+      if (u >= 1) xl = s_times<MODE>(ncur[u - 1], ldw<BF16>(wrow, o2));
+      if (hist) hist[u] = cu;
+      nnxt[u] = s_plus<MODE>(xb, xl);
+    }
+    advance(cw, a);
+    if (hist) hist += NP;
+    LT_STAMP(a, al == 0, 1, i, 2);
+  }
+}
+
+template <int MODE, bool BF16, bool WST, int LG, int P>
+__global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const NGram& g = a.g;
+  const int C = g.C, NP = a.U + 1;
+  const bool do_den = a.flags & F_DEN, do_num = a.flags & F_NUM;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+
+  float* abuf = (float*)(lds + a.off_a);    // [2][C]
+  float* nbuf = (float*)(lds + a.off_na);   // [2][NP]
+  int* ctx = (int*)(lds + a.off_ctx);
+  int* ylab = (int*)(lds + a.off_ylab);
+  float* misc = (float*)(lds + a.off_misc);
+  const unsigned ldsb = lds_base_addr(lds);
+
+  const int den_lanes = a.den_waves * 64;
+  const int aux_lanes = a.aux_waves * 64;
+  const int role = wave < a.den_waves ? 0 : (wave < a.den_waves + a.aux_waves ? 1 : 2);
+  const int lw = wave - a.den_waves - a.aux_waves;  // loader wave index
+  const int al = tid - den_lanes;                   // aux lane index
+
+  // ---- prologue
+  if (role == 2) {
+    const int pre = nf < a.P ? nf : a.P;
+    for (int f = 0; f < pre; ++f) issue_frame(a, b, f, f, lw, lane, ldsb);
+  } else if (role == 0) {
+    if (do_den)
+      for (int q = tid; q < C; q += den_lanes) abuf[q] = (q == 0) ? s_one<MODE>() : s_zero<MODE>();
+  } else if (do_num) {
+    for (int u = al; u < NP; u += aux_lanes) nbuf[u] = (u == 0) ? s_one<MODE>() : s_zero<MODE>();
+    load_labels(a, b, ylab, al, aux_lanes);
+  }
+  lds_barrier();
+  if (role == 1 && do_num && al == 0) walk_states(a, ctx, ylab);
+  lds_barrier();
+
+  // ---- frame loop (alignment scan, lattices.py:856-892), one loop per role
+  if (role == 2) {
+    loader_loop(a, b, nf, false, lw, lane, ldsb);
+  } else if (role == 0) {
+    if (do_den && !(a.dbg & 1)) den_fwd_loop<MODE, BF16, WST, LG, P>(a, lds, abuf, b, nf, tid);
+    else idle_loop(nf);
+  } else {
+    if (do_num && !(a.dbg & 2)) num_fwd_loop<MODE, BF16, WST>(a, lds, nbuf, ctx, ylab, b, nf, al, aux_lanes);
+    else idle_loop(nf);
+  }
+  lds_barrier();
+
+  // ---- finalize: shortest distance = (+)_q alpha_T[q] (lattices.py:496)
+  const int fin = nf & 1;
+  if (role == 0 && do_den) {
+    const float* af = abuf + fin * C;
+    if (wave == 0) {
+      float r;
+      int bi = 0x7fffffff;
+      if constexpr (MODE == M_LOG) {
+        float mx = -kInf;
+        for (int q = lane; q < C; q += 64) mx = fmaxf(mx, af[q]);
+        mx = gmax<6>(mx, 6);
+        const float c = __builtin_isfinite(mx) ? mx : 0.f;
+        float s = 0.f;
+        for (int q = lane; q < C; q += 64) s += lt_exp(af[q] - c);
+        s = gsum<6>(s, 6);
+        r = c + lt_log(s);
+      } else if constexpr (MODE == M_MAX) {
+        r = -kInf;
+        for (int q = lane; q < C; q += 64)
+          if (bi == 0x7fffffff || af[q] > r) { r = af[q]; bi = q; }
+        gargmax<6>(r, bi, 6);
+      } else {
+        float s = 0.f;
+        for (int q = lane; q < C; q += 64) s += af[q];
+        r = gsum<6>(s, 6);
+      }
+      if (lane == 0) {
+        misc[0] = r;
+        if (a.dist) a.dist[b] = r;
+        if (MODE == M_MAX && a.qstar) a.qstar[b] = bi;
+      }
+    }
+    if (a.alpha) {  // padding frames carry alpha (lattices.py:460-461)
+      const long long n = (long long)(a.T - nf) * C;
+      float* dst = a.alpha + ((long long)b * a.T + nf) * C;
+      for (long long e = tid; e < n; e += den_lanes) dst[e] = af[e % C];
+    }
+  } else if (role == 1 && do_num) {
+    const float* nfin = nbuf + fin * NP;
+    if (al == 0) {
+      const int nl = a.nlab[b];
+      // lattices.py:375-377: (+) over positions equal to num_labels
+      const float r = (nl >= 0 && nl <= a.U) ? nfin[nl] : s_zero<MODE>();
+      misc[1] = r;
+      if (a.num) a.num[b] = r;
+    }
+    if (a.alpha_num) {
+      const long long n = (long long)(a.T - nf) * NP;
+      float* dst = a.alpha_num + ((long long)b * a.T + nf) * NP;
+      for (long long e = al; e < n; e += aux_lanes) dst[e] = nfin[e % NP];
+    }
+  }
+  if (a.flags & F_LOSS) {
+    lds_barrier();
+    if (tid == 0) {
+      // lattices.py:178-183
+      const float num = misc[1];
+      a.loss[b] = (a.flags & F_LOCAL) ? -num : misc[0] - num;
+    }
+  }
+}
+
+// Store one dW frame from the LDS staging buffers: v = den - num marginals.
+// Element e of the frame sits at LDS float index e + sh, sh = (global element
+// offset of the frame) % 4, so 4-element chunks are 16 B aligned on both
+// sides (8 B for bf16). Re-zeroes the numerator buffer.
+template <bool BF16>
+LT_DEVINL void store_frame(const KArgs& a, long long gbase, const float* db, float* nb,
+                           bool do_den, bool do_num, int al, int aux_lanes) {
+  const int FR = a.FR;
+  const int sh = (int)(gbase & 3);
+  const int head = (4 - sh) & 3;  // elements before the first aligned chunk
+  const int nchunk = (FR - head) >> 2;
+  const int tail0 = head + 4 * nchunk;
+  for (int c = al; c < nchunk; c += aux_lanes) {
+    const int li = head + 4 * c + sh;  // multiple of 4
+    float4 v = do_den ? *(const float4*)(db + li) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (do_num) {
+      const float4 n = *(const float4*)(nb + li);
+      v.x -= n.x; v.y -= n.y; v.z -= n.z; v.w -= n.w;
+      *(float4*)(nb + li) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const long long ge = gbase + head + 4 * c;
+    if constexpr (BF16) {
+      ushort4 h;
+      h.x = f2bf(v.x); h.y = f2bf(v.y); h.z = f2bf(v.z); h.w = f2bf(v.w);
+      *(ushort4*)((unsigned short*)a.dW + ge) = h;
+    } else {
+      *(float4*)((float*)a.dW + ge) = v;
+    }
+  }
+  // unaligned head / tail elements
+  const int nedge = head + (FR - tail0);
+  for (int r = al; r < nedge; r += aux_lanes) {
+    const int e = r < head ? r : tail0 + (r - head);
+    float v = do_den ? db[e + sh] : 0.f;
+    if (do_num) { v -= nb[e + sh]; nb[e + sh] = 0.f; }
+    stw<BF16>(a.dW, gbase + e, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward kernel (Log): beta recursion + arc marginals -> dW.
+//   DST: dW frame staged in LDS (den marginals written by den lanes, numerator
+//        marginals LDS-atomically accumulated by aux lanes, stored coalesced
+//        one frame later by the aux lanes).
+//   !DST: den lanes store straight to HBM; numerator marginals go to a side
+//        buffer and a scatter kernel subtracts them (large C*(V+1)).
+// ---------------------------------------------------------------------------
+template <bool BF16, bool WST, bool DST, int LG, int P>
+LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, float* dbuf,
+                            int FRS, int b, int nf, int tid, float gb, float log_z) {
+  const NGram& g = a.g;
+  const int C = g.C, FR = a.FR;
+  const int lgL = LG >= 0 ? LG : a.lgL;
+  const int L = 1 << lgL;
+  const int j = tid & (L - 1);
+  const int grp = tid >> lgL;
+  const int ngrp = (a.den_waves * 64) >> lgL;
+  const bool fast = a.den_fast;
+  const bool has = grp < a.den_groups;
+  int woff[P], boff[P];
+  int nv = 0;
+  if (fast && has) nv = bwd_slice<P>(g, grp, j, a.Pr, woff, boff);
+  const unsigned char* ringw = lds + a.off_ring + a.st_off[0];
+  const unsigned char* ringa = lds + a.off_ring + a.st_off[1];
+  const long long es = BF16 ? 2 : 4;
+  const long long t_last = (long long)b * a.T + (nf - 1);
+  Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)FR * es, t_last, true);
+  Cursor ca = make_cursor(a.st_row[1], t_last, true);
+  long long gframe = t_last * FR;  // global element offset of the frame
+  for (int i = 0; i < nf; ++i) {
+    LT_STAMP(a, tid == 0, 0, i, 0);
+    lds_barrier();
+    LT_STAMP(a, tid == 0, 0, i, 1);
+    const int cur = i & 1;
+    const unsigned char* wrow = WST ? ringw + cw.soff + cw.mis : a.W + cw.goff;
+    const float* arow = (const float*)(ringa + ca.soff + ca.mis);
+    const float* bcur = bbuf + cur * C;
+    float* bnxt = bbuf + (cur ^ 1) * C;
+    float* dcur = dbuf + cur * FRS + (int)(gframe & 3);
+    for (int p = grp; p < C; p += ngrp) {
+      if (fast && !has) break;
+      int wo[P], bo[P];
+      int n2 = nv;
+      if (fast) {
+#pragma unroll
+        for (int m = 0; m < P; ++m) { wo[m] = woff[m]; bo[m] = boff[m]; }
+      } else {
+        n2 = bwd_slice<P>(g, p, j, a.Pr, wo, bo);
+      }
+      float x[P];
+#pragma unroll
+      for (int m = 0; m < P; ++m) {
+        const float wv = ldw<BF16>(wrow, wo[m]);
+        const float bv = bcur[bo[m]];
+        x[m] = m < n2 ? wv + bv : -kInf;
+      }
+      const float ap = arow[p];
+      float mx = x[0];
+#pragma unroll
+      for (int m = 1; m < P; ++m) mx = fmaxf(mx, x[m]);
+      mx = gmax<LG>(mx, lgL);
+      const float c = __builtin_isfinite(mx) ? mx : 0.f;
+      float s = 0.f;
+#pragma unroll
+      for (int m = 0; m < P; ++m) {
+        x[m] = lt_exp(x[m] - c);
+        s += x[m];
+      }
+      s = gsum<LG>(s, lgL);
+      if (j == 0) bnxt[p] = c + lt_log(s);
+      // marginal exp(alpha + w + beta' - log_z) = e * exp(c + alpha - log_z)
+      const float sp = (gb == 0.f) ? 0.f : lt_exp(c + ap - log_z) * gb;
+#pragma unroll
+      for (int m = 0; m < P; ++m) {
+        if (m < n2) {
+          const float v = x[m] * sp;
+          if constexpr (DST) dcur[wo[m]] = v;
+          else stw<BF16>(a.dW, gframe + wo[m], v);
+        }
+      }
+      if (fast) break;
+    }
+    advance(cw, a);
+    advance(ca, a);
+    gframe -= FR;
+    LT_STAMP(a, tid == 0, 0, i, 2);
+  }
+}
+
+template <bool BF16, bool WST, bool DST>
+LT_DEVINL void aux_bwd_loop(const KArgs& a, unsigned char* lds, float* nbb, float* dbuf,
+                            float* mbuf, int FRS, const int* ctx, const int* ylab, int b, int nf,
+                            int al, int aux_lanes, float gb, float numv, bool do_den,
+                            bool do_num) {
+  const int NP = a.U + 1, FR = a.FR;
+  int ob = 0, ol = 0;
+  if (do_num && al < NP) {
+    ob = ctx[al];
+    ol = al < a.U ? ob + ylab[al] : 0;
+  }
+  const unsigned char* ringw = lds + a.off_ring + a.st_off[0];
+  const unsigned char* ringn = lds + a.off_ring + a.st_off[2];
+  const long long es = BF16 ? 2 : 4;
+  const long long t_last = (long long)b * a.T + (nf - 1);
+  Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)FR * es, t_last, true);
+  Cursor cn = make_cursor(a.st_row[2], t_last, true);
+  long long gframe = t_last * FR;
+  for (int i = 0; i < nf; ++i) {
+    LT_STAMP(a, al == 0, 1, i, 0);
+    lds_barrier();
+    LT_STAMP(a, al == 0, 1, i, 1);
+    const int cur = i & 1;
+    if constexpr (DST) {
+      if (i >= 1) {  // store the frame computed last step (t+1)
+        const int pv = cur ^ 1;
+        store_frame<BF16>(a, gframe + FR, dbuf + pv * FRS, mbuf + pv * FRS, do_den, do_num, al,
+                          aux_lanes);
+      }
+    }
+    if (do_num) {
+      const unsigned char* wrow = WST ? ringw + cw.soff + cw.mis : a.W + cw.goff;
+      const float* anrow = (const float*)(ringn + cn.soff + cn.mis);
+      const float* ncur = nbb + cur * NP;
+      float* nnxt = nbb + (cur ^ 1) * NP;
+      float* mcur = mbuf + cur * FRS + (int)(gframe & 3);
+      for (int u = al; u < NP; u += aux_lanes) {
+        int o0 = ob, o1 = ol;
+        if (u != al) { o0 = ctx[u]; o1 = u < a.U ? o0 + ylab[u] : 0; }
+        const float xb = ldw<BF16>(wrow, o0) + ncur[u];
+        float xl = -kInf;
+        if (u < a.U) xl = ldw<BF16>(wrow, o1) + ncur[u + 1];
+        nnxt[u] = log_plus(xb, xl);
+        float mb = 0.f, ml = 0.f;
+        if (gb != 0.f) {
+          const float an = anrow[u] - numv;
+          mb = lt_exp(an + xb) * gb;
+          ml = lt_exp(an + xl) * gb;
+        }
+        if constexpr (DST) {
+          if (mb != 0.f) atomicAdd(&mcur[o0], mb);
+          if (ml != 0.f) atomicAdd(&mcur[o1], ml);
+        } else {
+          float* ns = a.nm_side + ((gframe / FR) * NP + u) * 2;
+          ns[0] = mb;
+          ns[1] = ml;
+        }
+      }
+    }
+    advance(cw, a);
+    advance(cn, a);
+    gframe -= FR;
+    LT_STAMP(a, al == 0, 1, i, 2);
+  }
+}
+
+template <bool BF16, bool WST, bool DST, int LG, int P>
+__global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const NGram& g = a.g;
+  const int C = g.C, NP = a.U + 1, FR = a.FR;
+  const int FRS = DST ? (FR + 4 + 3) & ~3 : 0;  // staged frame stride (floats)
+  const bool do_den = a.flags & F_DEN, do_num = a.flags & F_NUM;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+
+  float* bbuf = (float*)(lds + a.off_a);     // [2][C]  den beta
+  float* nbb = (float*)(lds + a.off_na);     // [2][NP] num beta
+  int* ctx = (int*)(lds + a.off_ctx);
+  int* ylab = (int*)(lds + a.off_ylab);
+  float* dbuf = (float*)(lds + a.off_dbuf);  // [2][FRS] den marginals
+  float* mbuf = (float*)(lds + a.off_nbuf);  // [2][FRS] num marginals
+  const unsigned ldsb = lds_base_addr(lds);
+
+  const int den_lanes = a.den_waves * 64;
+  const int aux_lanes = a.aux_waves * 64;
+  const int role = wave < a.den_waves ? 0 : (wave < a.den_waves + a.aux_waves ? 1 : 2);
+  const int lw = wave - a.den_waves - a.aux_waves;
+  const int al = tid - den_lanes;
+
+  float gb = a.grad ? a.grad[b] : 1.f;
+  const float log_z = do_den ? a.log_z_in[b] : 0.f;
+  const float numv = do_num ? a.num_in[b] : 0.f;
+  // unreachable label string (loss = +inf) or degenerate partition: dW = 0
+  if ((do_num && !__builtin_isfinite(numv)) || (do_den && !__builtin_isfinite(log_z))) gb = 0.f;
+  const int nl = do_num ? a.nlab[b] : 0;
+
+  // ---- prologue
+  if (role == 2) {
+    const int pre = nf < a.P ? nf : a.P;
+    for (int f = 0; f < pre; ++f) issue_frame(a, b, nf - 1 - f, f, lw, lane, ldsb);
+  } else if (role == 0) {
+    // beta_T = one for every state: all context states are final
+    // (lattices.py:788-790)
+    if (do_den) for (int p = tid; p < C; p += den_lanes) bbuf[p] = 0.f;
+  } else {
+    if (do_num) {
+      for (int u = al; u < NP; u += aux_lanes) nbb[u] = (u == nl) ? 0.f : -kInf;
+      load_labels(a, b, ylab, al, aux_lanes);
+    }
+    if (DST && do_num)
+      for (int e = al; e < 2 * FRS; e += aux_lanes) mbuf[e] = 0.f;
+  }
+  lds_barrier();
+  if (role == 1 && do_num && al == 0) walk_states(a, ctx, ylab);
+  lds_barrier();
+  if (!DST && do_num && role == 1 && a.ctx_side) {
+    for (int u = al; u < NP; u += aux_lanes) {
+      a.ctx_side[((long long)b * NP + u) * 2 + 0] = ctx[u];
+      a.ctx_side[((long long)b * NP + u) * 2 + 1] = ylab[u];
+    }
+  }
+
+  if (role == 2) {
+    loader_loop(a, b, nf, true, lw, lane, ldsb);
+  } else if (role == 0) {
+    if (do_den && !(a.dbg & 1))
+      den_bwd_loop<BF16, WST, DST, LG, P>(a, lds, bbuf, dbuf, FRS, b, nf, tid, gb, log_z);
+    else idle_loop(nf);
+  } else {
+    aux_bwd_loop<BF16, WST, DST>(a, lds, nbb, dbuf, mbuf, FRS, ctx, ylab, b, nf, al, aux_lanes,
+                                 gb, numv, do_den, do_num && !(a.dbg & 2));
+  }
+  lds_barrier();
+  if constexpr (DST) {
+    if (role == 1 && nf >= 1) {  // last processed frame: t = 0
+      const int pv = (nf - 1) & 1;
+      store_frame<BF16>(a, (long long)b * a.T * FR, dbuf + pv * FRS, mbuf + pv * FRS, do_den,
+                        do_num, al, aux_lanes);
+    }
+  }
+  // padding frames get zero marginals (lattices.py:775-779); with no
+  // denominator in the direct path nothing else wrote dW.
+  {
+    const int t0 = (!DST && !do_den) ? 0 : nf;
+    const long long n = (long long)(a.T - t0) * FR;
+    const long long base = ((long long)b * a.T + t0) * FR;
+    const int nthr = blockDim.x;
+    for (long long e = tid; e < n; e += nthr) stw<BF16>(a.dW, base + e, 0.f);
+  }
+}
+
+}  // namespace
+
+namespace lt_impl {
+struct Plan {
+  KArgs a;
+  int lg;    // template LG (log2 lanes per group), -1 = runtime
+  int tmax;  // template P (register slice size)
+  bool wst, dst;
+  int threads;
+  int lds_bytes;
+};
+// Defined in lt_inst.hip, one pair per P in LT_P_LIST.
+// (LG, P) pairs with a compile-time group size (LG = log2 lanes per group)
+// plus runtime-LG fallbacks (LG = -1, written M1 in names).
+#define LT_VARIANTS(X) \
+  X(3, 5) X(2, 9) X(1, 4) X(1, 3) X(2, 5) X(3, 3) X(2, 3) X(M1, 4) X(M1, 8) X(M1, 16)
+#define LT_DECL(LG, P)                                                                   \
+  int launch_fwd_##LG##_##P(int mode, const Plan& pl, bool bf16, int grid, hipStream_t st); \
+  int launch_bwd_##LG##_##P(const Plan& pl, bool bf16, int grid, hipStream_t st);
+LT_VARIANTS(LT_DECL)
+#undef LT_DECL
+int set_error(int code, const char* msg);
+}  // namespace lt_impl

@@ -1,756 +1,10 @@
-// lt_lattice.hip -- MI355X (gfx950 / CDNA4) kernels for the GNAT recognition
-// lattice hot path of theadamsabra/last_torch, behind the C ABI declared in
-// include/lt_lattice.h.
-//
-// What is computed (reference file:line in last_torch/):
-//   * denominator forward  alpha_{t+1} = FrameDependent.forward(alpha_t, W_t)
-//       lattices.py:379-496, alignments.py:286-297, contexts.py:207-230
-//   * denominator backward beta_t + arc marginals (FrameDependent.backward)
-//       lattices.py:686-799, alignments.py:300-318, contexts.py:232-256
-//   * numerator (string) forward / backward
-//       lattices.py:250-377, alignments.py:320-329
-//   * MaxTropical Viterbi + backtrace (shortest_path)
-//       lattices.py:185-247, semirings.py:354-401 (tie rules)
-//
-// Execution design:
-//   One workgroup per utterance; the recursion over frames is serial, the
-//   live front (all C context states, all U+1 string positions) is spread
-//   over the workgroup:
-//     waves [0, den_waves)            : denominator front, L lanes per
-//                                       context state ("group"), each lane a
-//                                       slice of the state's in/out arcs;
-//                                       group reductions with DPP.
-//     waves [den, den+aux)            : numerator front (one lane per string
-//                                       position) + (backward) the coalesced
-//                                       dW store of the previous frame.
-//     waves [den+aux, +load)          : loaders: LDS-DMA (global_load_lds
-//                                       dwordx4) of frame t+P into a ring of
-//                                       S = P+1 slots while frame t computes.
-//   One LDS barrier per frame. HBM is touched only by the streamed W rows,
-//   the (small) alpha checkpoints and dW.
-#include <hip/hip_runtime.h>
-
-#include <math.h>
-#include <stdint.h>
-#include <stdio.h>
-#include <string.h>
-
-#include <algorithm>
-#include <string>
-
-#include "../../include/lt_lattice.h"
-
-#define LT_DEVINL __device__ __forceinline__
+// lt_lattice.hip -- host side of the MI355X lattice library: C ABI
+// (include/lt_lattice.h), launch planning, and the small scatter / Viterbi
+// backtrace kernels. The frame-recursion kernels live in lt_kernels.h and
+// are instantiated per terms-per-lane value by lt_inst.hip.
+#include "lt_kernels.h"
 
 namespace {
-
-// ---------------------------------------------------------------------------
-// FullNGram index maps (contexts.py:181-256)
-// ---------------------------------------------------------------------------
-struct NGram {
-  int V;    // vocab size
-  int n;    // context size (order)
-  int C;    // number of states  sum_{i<=n} V^i
-  int An;   // ascending states  sum_{i<n}  V^i
-  int Apn;  // sum_{i<n-1} V^i   (first source row feeding full-order states)
-  int Vn1;  // V^(n-1) (n >= 1), 0 for n == 0
-  int K;    // lexical in-arcs per full-order destination (V+1, or V for n=0)
-};
-
-enum { M_LOG = 0, M_MAX = 1, M_REAL = 2 };
-
-constexpr float kInf = __builtin_huge_valf();
-
-// Destination q's lexical in-arcs, as arithmetic progressions:
-//   source  p_k = a0 + k*astr,  W element  e_k = w0 + k*wstr,  k in [0, kq)
-// (term order index o = 0 is the blank self loop, o = k+1 lexical arc k; the
-//  reference reduces the V+1 sources in ascending p, contexts.py:226-229).
-struct DestDesc {
-  int kq, a0, astr, w0, wstr;
-};
-
-__host__ __device__ inline DestDesc dest_desc(const NGram& g, int q) {
-  DestDesc d;
-  const int R = g.V + 1;
-  if (g.n == 0) {  // single state, V lexical self loops y = 1..V
-    d.kq = g.V; d.a0 = 0; d.astr = 0; d.w0 = 1; d.wstr = 1;
-  } else if (q == 0) {  // start state: no lexical in-arc (contexts.py:216-217)
-    d.kq = 0; d.a0 = 0; d.astr = 0; d.w0 = 0; d.wstr = 0;
-  } else if (q < g.An) {  // ascending: unique in-arc (contexts.py:222-225)
-    const int p = (q - 1) / g.V, y = (q - 1) % g.V + 1;
-    d.kq = 1; d.a0 = p; d.astr = 0; d.w0 = p * R + y; d.wstr = 0;
-  } else {  // full order: V+1 sources, same label (contexts.py:226-229)
-    const int jq = q - g.An;
-    const int pb = g.Apn + jq / g.V, y = jq % g.V + 1;
-    d.kq = g.K; d.a0 = pb; d.astr = g.Vn1; d.w0 = pb * R + y; d.wstr = g.Vn1 * R;
-  }
-  return d;
-}
-
-// next(p, y) = nb + y for y >= 1 (contexts.py:190-205); returns nb, and
-// *zero = true for n == 0 (every lexical arc loops to state 0).
-__host__ __device__ inline int next_base(const NGram& g, int p, bool* zero) {
-  *zero = (g.n == 0);
-  if (g.n == 0) return 0;
-  if (p < g.An) return p * g.V;
-  return ((p - g.An) % g.Vn1) * g.V + g.An - 1;
-}
-
-// ---------------------------------------------------------------------------
-// Device helpers
-// ---------------------------------------------------------------------------
-LT_DEVINL float lt_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
-// Arguments are sums of exp() with the max term == 1 (>= 1) or exactly 0.
-LT_DEVINL float lt_log(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
-
-template <int CTRL>
-LT_DEVINL float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-template <int CTRL>
-LT_DEVINL int dppi(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
-}
-// Partner exchange for butterfly stage s of a power-of-two lane group.
-// Stages 0-3 stay inside a DPP row (quad_perm / half_mirror / mirror);
-// stages 4-5 go through ds_bpermute. Valid for max / sum / (max,idx) merges
-// because after stage s every lane of a 2^s block holds the same value.
-// Butterfly stages of a power-of-two lane group. Stages 0-3 stay inside a
-// DPP row (quad_perm / row_half_mirror / row_mirror); stages 4-5 go through
-// ds_bpermute. Valid for max / sum / (max,idx) merges because after stage s
-// every lane of a 2^s block already holds the same value.
-template <int S>
-LT_DEVINL float xchg(float v) {
-  if constexpr (S == 0) return dppf<0xB1>(v);
-  else if constexpr (S == 1) return dppf<0x4E>(v);
-  else if constexpr (S == 2) return dppf<0x141>(v);
-  else if constexpr (S == 3) return dppf<0x140>(v);
-  else return __shfl_xor(v, 1 << S);
-}
-template <int S>
-LT_DEVINL int xchgi(int v) {
-  if constexpr (S == 0) return dppi<0xB1>(v);
-  else if constexpr (S == 1) return dppi<0x4E>(v);
-  else if constexpr (S == 2) return dppi<0x141>(v);
-  else if constexpr (S == 3) return dppi<0x140>(v);
-  else return __shfl_xor(v, 1 << S);
-}
-#define LT_STAGES(OP) OP(0) OP(1) OP(2) OP(3) OP(4) OP(5)
-
-LT_DEVINL float grp_max(float v, int lg) {
-#define LT_MAXST(S) if (lg > S) v = fmaxf(v, xchg<S>(v));
-  LT_STAGES(LT_MAXST)
-#undef LT_MAXST
-  return v;
-}
-LT_DEVINL float grp_sum(float v, int lg) {
-#define LT_SUMST(S) if (lg > S) v += xchg<S>(v);
-  LT_STAGES(LT_SUMST)
-#undef LT_SUMST
-  return v;
-}
-// first-max (lowest index wins ties): semirings.py:363 (blank term has the
-// lowest index) and :382 (torch.argmax returns the first maximum).
-LT_DEVINL void grp_argmax(float& v, int& i, int lg) {
-#define LT_ARGST(S)                                   \
-  if (lg > S) {                                       \
-    const float pv = xchg<S>(v);                      \
-    const int pi = xchgi<S>(i);                       \
-    if (pv > v || (pv == v && pi < i)) { v = pv; i = pi; } \
-  }
-  LT_STAGES(LT_ARGST)
-#undef LT_ARGST
-}
-
-// Log-semiring plus exactly as _LogAddExp.forward (semirings.py:248-255):
-// c = max(a,b), non-finite c replaced by 0.
-LT_DEVINL float log_plus(float a, float b) {
-  float c = fmaxf(a, b);
-  if (!__builtin_isfinite(c)) c = 0.f;
-  return c + lt_log(lt_exp(a - c) + lt_exp(b - c));
-}
-
-template <int MODE>
-LT_DEVINL float s_zero() { return MODE == M_REAL ? 0.f : -kInf; }
-template <int MODE>
-LT_DEVINL float s_one() { return MODE == M_REAL ? 1.f : 0.f; }
-template <int MODE>
-LT_DEVINL float s_times(float a, float b) { return MODE == M_REAL ? a * b : a + b; }
-template <int MODE>
-LT_DEVINL float s_plus(float a, float b) {
-  if (MODE == M_LOG) return log_plus(a, b);
-  if (MODE == M_MAX) return (a >= b) ? a : b;  // Maximum: choose a iff a >= b
-  return a + b;
-}
-
-template <bool BF16, typename I>
-LT_DEVINL float ldw(const unsigned char* p, I e) {
-  if constexpr (BF16) {
-    return __uint_as_float(((unsigned)((const unsigned short*)p)[e]) << 16);
-  } else {
-    return ((const float*)p)[e];
-  }
-}
-LT_DEVINL unsigned short f2bf(float f) {  // round to nearest even, NaN kept
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
-}
-template <bool BF16>
-LT_DEVINL void stw(void* p, long long e, float v) {
-  if constexpr (BF16) ((unsigned short*)p)[e] = f2bf(v);
-  else ((float*)p)[e] = v;
-}
-
-// LDS barrier: drains this wave's LDS ops, then s_barrier. The asm has a
-// memory clobber so the compiler cannot move LDS accesses across it, and it
-// does NOT wait on vmcnt: loads in flight (LDS-DMA ring) and global stores
-// (checkpoints) survive the barrier.
-LT_DEVINL void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// One LDS-DMA wave instruction: 64 lanes x 16 B from per-lane global
-// addresses into the contiguous 1 KiB at LDS byte address `lds_addr`
-// (wave-uniform, passed in M0). Issued from inline asm so the compiler's
-// waitcnt pass does not drain it at unrelated LDS reads; the loader waits
-// for it with a counted vmcnt (wait_vmcnt) before the consuming barrier.
-LT_DEVINL void glds16(const void* gsrc, unsigned lds_addr) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_addr)
-      : "memory");
-}
-
-#define LT_VMCNT_CASE(N) \
-  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-LT_DEVINL void wait_vmcnt(int n) {
-  switch (n < 0 ? 0 : (n > 63 ? 63 : n)) {
-    LT_VMCNT_CASE(0) LT_VMCNT_CASE(1) LT_VMCNT_CASE(2) LT_VMCNT_CASE(3)
-    LT_VMCNT_CASE(4) LT_VMCNT_CASE(5) LT_VMCNT_CASE(6) LT_VMCNT_CASE(7)
-    LT_VMCNT_CASE(8) LT_VMCNT_CASE(9) LT_VMCNT_CASE(10) LT_VMCNT_CASE(11)
-    LT_VMCNT_CASE(12) LT_VMCNT_CASE(13) LT_VMCNT_CASE(14) LT_VMCNT_CASE(15)
-    LT_VMCNT_CASE(16) LT_VMCNT_CASE(17) LT_VMCNT_CASE(18) LT_VMCNT_CASE(19)
-    LT_VMCNT_CASE(20) LT_VMCNT_CASE(21) LT_VMCNT_CASE(22) LT_VMCNT_CASE(23)
-    LT_VMCNT_CASE(24) LT_VMCNT_CASE(25) LT_VMCNT_CASE(26) LT_VMCNT_CASE(27)
-    LT_VMCNT_CASE(28) LT_VMCNT_CASE(29) LT_VMCNT_CASE(30) LT_VMCNT_CASE(31)
-    LT_VMCNT_CASE(32) LT_VMCNT_CASE(33) LT_VMCNT_CASE(34) LT_VMCNT_CASE(35)
-    LT_VMCNT_CASE(36) LT_VMCNT_CASE(37) LT_VMCNT_CASE(38) LT_VMCNT_CASE(39)
-    LT_VMCNT_CASE(40) LT_VMCNT_CASE(41) LT_VMCNT_CASE(42) LT_VMCNT_CASE(43)
-    LT_VMCNT_CASE(44) LT_VMCNT_CASE(45) LT_VMCNT_CASE(46) LT_VMCNT_CASE(47)
-    LT_VMCNT_CASE(48) LT_VMCNT_CASE(49) LT_VMCNT_CASE(50) LT_VMCNT_CASE(51)
-    LT_VMCNT_CASE(52) LT_VMCNT_CASE(53) LT_VMCNT_CASE(54) LT_VMCNT_CASE(55)
-    LT_VMCNT_CASE(56) LT_VMCNT_CASE(57) LT_VMCNT_CASE(58) LT_VMCNT_CASE(59)
-    LT_VMCNT_CASE(60) LT_VMCNT_CASE(61) LT_VMCNT_CASE(62)
-    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Kernel arguments (passed by value)
-// ---------------------------------------------------------------------------
-constexpr int kMaxStreams = 3;
-enum { F_DEN = 1, F_NUM = 2, F_LOCAL = 4, F_LOSS = 8 };
-
-struct KArgs {
-  const unsigned char* W;
-  const int* nfr;
-  const int* labels;
-  const int* nlab;
-  const float* grad;
-  const float* log_z_in;
-  const float* num_in;
-  float* dist;       // den result (log_z / path weight)
-  float* alpha;      // [B,T,C] den alpha history
-  float* num;        // [B]
-  float* alpha_num;  // [B,T,U+1]
-  float* loss;       // [B]
-  unsigned char* bp; // [B,T,C] Viterbi backpointers
-  int* qstar;        // [B] Viterbi final state
-  void* dW;          // [B,T,C,V+1]
-  float* nm_side;    // [B,T,U+1,2] numerator marginals (direct path)
-  int* ctx_side;     // [B,U+1,2]    numerator arc rows (direct path)
-  int B, T, U, flags;
-  NGram g;
-  int FR;            // C*(V+1) elements per frame
-  // layout
-  int L, lgL, den_waves, aux_waves, load_waves;
-  int S, P, slot_bytes;
-  // staged streams, fixed slots: 0 = W rows, 1 = alpha rows, 2 = alpha_num
-  // rows; st_ninstr[s] == 0 means stream s is not staged. Only indexed with
-  // compile-time constants (runtime-indexed kernel-argument arrays would be
-  // copied to scratch).
-  const unsigned char* st_base[kMaxStreams];
-  long long st_row[kMaxStreams];   // bytes per frame row
-  int st_ninstr[kMaxStreams];      // LDS-DMA wave instructions per frame
-  int st_off[kMaxStreams];         // byte offset inside a slot
-  int gw0, gw1;                    // instructions per frame of loader wave 0 / 1
-  int off_ring, off_a, off_na, off_ctx, off_ylab, off_dbuf, off_nbuf, off_misc;
-};
-
-LT_DEVINL unsigned lds_base_addr(unsigned char* lds) {
-  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
-}
-
-// Issue the LDS-DMA instructions of loader wave `lw` for frame t into `slot`.
-// Instruction gi of the frame (streams in slot order) belongs to loader wave
-// gi % load_waves.
-template <int S>
-LT_DEVINL void issue_stream(const KArgs& a, int b, int t, int slot, int lw, int lane,
-                            unsigned ldsb, int& gi) {
-  const int ni = a.st_ninstr[S];
-  if (ni == 0) return;
-  const long long row = a.st_row[S];
-  const long long off = ((long long)b * a.T + t) * row;
-  const long long g0 = off >> 4;
-  const long long g1 = (off + row + 15) >> 4;
-  const unsigned dst0 = ldsb + a.off_ring + slot * a.slot_bytes + a.st_off[S];
-  const unsigned char* base = a.st_base[S];
-  for (int k = 0; k < ni; ++k, ++gi) {
-    if (gi % a.load_waves != lw) continue;
-    long long gg = g0 + (long long)k * 64 + lane;
-    if (gg > g1 - 1) gg = g1 - 1;  // in-bounds duplicate, lands past the row
-    glds16(base + gg * 16, dst0 + k * 1024);
-  }
-}
-LT_DEVINL void issue_frame(const KArgs& a, int b, int t, int slot, int lw, int lane,
-                           unsigned ldsb) {
-  int gi = 0;
-  issue_stream<0>(a, b, t, slot, lw, lane, ldsb, gi);
-  issue_stream<1>(a, b, t, slot, lw, lane, ldsb, gi);
-  issue_stream<2>(a, b, t, slot, lw, lane, ldsb, gi);
-}
-
-// Address (in LDS) of stream S's row for frame t held in `slot`.
-template <int S>
-LT_DEVINL const unsigned char* slot_row(unsigned char* lds, const KArgs& a, int b, int t,
-                                        int slot) {
-  const long long off = ((long long)b * a.T + t) * a.st_row[S];
-  return lds + a.off_ring + slot * a.slot_bytes + a.st_off[S] + (int)(off & 15);
-}
-
-// Walk the context DFA along the label string (contexts.py:109-146) and the
-// numerator gather indices (lattices.py:314-338): ctx[u] = c_u*(V+1),
-// ylab[u] = safe class of labels[u] (0 -> 1, lattices.py:314-315), u < U.
-LT_DEVINL void walk_states(const KArgs& a, int b, int* ctx, int* ylab) {
-  const NGram& g = a.g;
-  const int R = g.V + 1;
-  int c = 0;
-  for (int u = 0; u <= a.U; ++u) {
-    ctx[u] = c * R;
-    if (u < a.U) {
-      int y = a.labels[(long long)b * a.U + u];
-      if (y < 0 || y > g.V) y = 0;
-      ylab[u] = y < 1 ? 1 : y;
-      if (y != 0) {
-        bool z;
-        const int nb = next_base(g, c, &z);
-        c = z ? 0 : nb + y;
-      }
-    } else {
-      ylab[u] = 1;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Forward kernel: denominator and/or numerator, Log / MaxTropical / Real.
-// ---------------------------------------------------------------------------
-template <int MODE, bool BF16, bool WST, int TMAX>
-__global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const NGram& g = a.g;
-  const int C = g.C, R = g.V + 1, NP = a.U + 1;
-  const bool do_den = a.flags & F_DEN, do_num = a.flags & F_NUM;
-  int nf = a.nfr[b];
-  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
-
-  float* abuf = (float*)(lds + a.off_a);    // [2][C]
-  float* nbuf = (float*)(lds + a.off_na);   // [2][NP]
-  int* ctx = (int*)(lds + a.off_ctx);
-  int* ylab = (int*)(lds + a.off_ylab);
-  float* misc = (float*)(lds + a.off_misc);
-  const unsigned ldsb = lds_base_addr(lds);
-
-  const int den_lanes = a.den_waves * 64;
-  const int aux_lanes = a.aux_waves * 64;
-  const int role = wave < a.den_waves ? 0 : (wave < a.den_waves + a.aux_waves ? 1 : 2);
-  const int lw = wave - a.den_waves - a.aux_waves;  // loader wave index
-
-  // ---- prologue
-  if (role == 2) {
-    const int pre = nf < a.P ? nf : a.P;
-    for (int f = 0; f < pre; ++f) issue_frame(a, b, f, f % a.S, lw, lane, ldsb);
-  } else if (role == 0) {
-    if (do_den)
-      for (int q = tid; q < C; q += den_lanes) abuf[q] = (q == 0) ? s_one<MODE>() : s_zero<MODE>();
-  } else {
-    const int al = tid - den_lanes;
-    if (do_num) {
-      for (int u = al; u < NP; u += aux_lanes) nbuf[u] = (u == 0) ? s_one<MODE>() : s_zero<MODE>();
-      if (al == 0) walk_states(a, b, ctx, ylab);
-    }
-  }
-  lds_barrier();
-
-  const int L = a.L, lgL = a.lgL;
-  const int j = tid & (L - 1);
-  const int grp0 = tid >> lgL;
-  const int ngrp = den_lanes >> lgL;
-
-  // ---- frame loop (alignment scan, lattices.py:856-892)
-  for (int i = 0; i < nf; ++i) {
-    const int t = i;
-    const int slot = i % a.S;
-    if (role == 2) {
-      const int later = (a.P - 1 < nf - 1 - i) ? a.P - 1 : nf - 1 - i;
-      wait_vmcnt(later * (lw == 0 ? a.gw0 : a.gw1));
-    }
-    lds_barrier();
-    if (role == 2) {
-      if (i + a.P < nf) issue_frame(a, b, i + a.P, (i + a.P) % a.S, lw, lane, ldsb);
-      continue;
-    }
-    const unsigned char* wrow;
-    if constexpr (WST) wrow = slot_row<0>(lds, a, b, t, slot);
-    else wrow = a.W + ((long long)b * a.T + t) * (long long)a.FR * (BF16 ? 2 : 4);
-
-    if (role == 0) {
-      if (!do_den) continue;
-      const float* acur = abuf + (i & 1) * C;
-      float* anxt = abuf + ((i + 1) & 1) * C;
-      for (int q = grp0; q < C; q += ngrp) {
-        const DestDesc d = dest_desc(g, q);
-        const int nterm = d.kq + 1;
-        float xv[TMAX];
-#pragma unroll
-        for (int m = 0; m < TMAX; ++m) {
-          const int o = j + m * L;
-          float x = s_zero<MODE>();
-          if (o < nterm) {
-            float av, wv;
-            if (o == 0) {
-              av = acur[q];
-              wv = ldw<BF16>(wrow, (long long)q * R);
-            } else {
-              const int k = o - 1;
-              av = acur[d.a0 + k * d.astr];
-              wv = ldw<BF16>(wrow, d.w0 + k * d.wstr);
-            }
-            x = s_times<MODE>(av, wv);
-          }
-          xv[m] = x;
-        }
-        float r;
-        int bi = j;
-        if constexpr (MODE == M_LOG) {
-          float mx = xv[0];
-#pragma unroll
-          for (int m = 1; m < TMAX; ++m) mx = fmaxf(mx, xv[m]);
-          mx = grp_max(mx, lgL);
-          const float c = __builtin_isfinite(mx) ? mx : 0.f;
-          float s = 0.f;
-#pragma unroll
-          for (int m = 0; m < TMAX; ++m) s += lt_exp(xv[m] - c);
-          s = grp_sum(s, lgL);
-          r = c + lt_log(s);
-        } else if constexpr (MODE == M_MAX) {
-          r = xv[0];
-#pragma unroll
-          for (int m = 1; m < TMAX; ++m)
-            if (xv[m] > r) { r = xv[m]; bi = j + m * L; }
-          grp_argmax(r, bi, lgL);
-        } else {
-          float s = 0.f;
-#pragma unroll
-          for (int m = 0; m < TMAX; ++m) s += xv[m];
-          r = grp_sum(s, lgL);
-        }
-        if (j == 0) {
-          const long long hb = ((long long)b * a.T + t) * C + q;
-          if (a.alpha) a.alpha[hb] = acur[q];
-          if (MODE == M_MAX && a.bp) a.bp[hb] = (unsigned char)bi;
-          anxt[q] = r;
-        }
-      }
-    } else {  // role 1: numerator positions (alignments.py:320-329)
-      if (!do_num) continue;
-      const float* ncur = nbuf + (i & 1) * NP;
-      float* nnxt = nbuf + ((i + 1) & 1) * NP;
-      for (int u = tid - den_lanes; u < NP; u += aux_lanes) {
-        const float xb = s_times<MODE>(ncur[u], ldw<BF16>(wrow, ctx[u]));
-        float xl = s_zero<MODE>();
-        if (u >= 1) xl = s_times<MODE>(ncur[u - 1], ldw<BF16>(wrow, ctx[u - 1] + ylab[u - 1]));
-        if (a.alpha_num) a.alpha_num[((long long)b * a.T + t) * NP + u] = ncur[u];
-        nnxt[u] = s_plus<MODE>(xb, xl);
-      }
-    }
-  }
-  lds_barrier();
-
-  // ---- finalize: shortest distance = (+)_q alpha_T[q] (lattices.py:496)
-  const int fin = nf & 1;
-  if (role == 0 && do_den) {
-    const float* af = abuf + fin * C;
-    if (wave == 0) {
-      float r;
-      int bi = 0x7fffffff;
-      if constexpr (MODE == M_LOG) {
-        float mx = -kInf;
-        for (int q = lane; q < C; q += 64) mx = fmaxf(mx, af[q]);
-        mx = grp_max(mx, 6);
-        const float c = __builtin_isfinite(mx) ? mx : 0.f;
-        float s = 0.f;
-        for (int q = lane; q < C; q += 64) s += lt_exp(af[q] - c);
-        s = grp_sum(s, 6);
-        r = c + lt_log(s);
-      } else if constexpr (MODE == M_MAX) {
-        r = -kInf;
-        for (int q = lane; q < C; q += 64)
-          if (bi == 0x7fffffff || af[q] > r) { r = af[q]; bi = q; }
-        grp_argmax(r, bi, 6);
-      } else {
-        float s = 0.f;
-        for (int q = lane; q < C; q += 64) s += af[q];
-        r = grp_sum(s, 6);
-      }
-      if (lane == 0) {
-        misc[0] = r;
-        if (a.dist) a.dist[b] = r;
-        if (MODE == M_MAX && a.qstar) a.qstar[b] = bi;
-      }
-    }
-    if (a.alpha) {  // padding frames carry alpha (lattices.py:460-461)
-      const long long n = (long long)(a.T - nf) * C;
-      float* dst = a.alpha + ((long long)b * a.T + nf) * C;
-      for (long long e = tid; e < n; e += den_lanes) dst[e] = af[e % C];
-    }
-  } else if (role == 1 && do_num) {
-    const float* nfin = nbuf + fin * NP;
-    const int al = tid - den_lanes;
-    if (al == 0) {
-      const int nl = a.nlab[b];
-      // lattices.py:375-377: (+) over positions equal to num_labels
-      const float r = (nl >= 0 && nl <= a.U) ? nfin[nl] : s_zero<MODE>();
-      misc[1] = r;
-      if (a.num) a.num[b] = r;
-    }
-    if (a.alpha_num) {
-      const long long n = (long long)(a.T - nf) * NP;
-      float* dst = a.alpha_num + ((long long)b * a.T + nf) * NP;
-      for (long long e = al; e < n; e += aux_lanes) dst[e] = nfin[e % NP];
-    }
-  }
-  if (a.flags & F_LOSS) {
-    lds_barrier();
-    if (tid == 0) {
-      // lattices.py:178-183
-      const float num = misc[1];
-      a.loss[b] = (a.flags & F_LOCAL) ? -num : misc[0] - num;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Backward kernel (Log): beta recursion + arc marginals -> dW.
-//   DST: dW frame staged in LDS (den marginals written by den lanes, numerator
-//        marginals LDS-atomically accumulated by aux lanes, stored coalesced
-//        one frame later by the aux lanes).
-//   !DST: den lanes store straight to HBM; numerator marginals go to a side
-//        buffer and a scatter kernel subtracts them (large C*(V+1)).
-// ---------------------------------------------------------------------------
-template <bool BF16, bool WST, bool DST, int TMAX>
-__global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const NGram& g = a.g;
-  const int C = g.C, R = g.V + 1, NP = a.U + 1, FR = a.FR;
-  const bool do_den = a.flags & F_DEN, do_num = a.flags & F_NUM;
-  int nf = a.nfr[b];
-  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
-
-  float* bbuf = (float*)(lds + a.off_a);     // [2][C]  den beta
-  float* nbb = (float*)(lds + a.off_na);     // [2][NP] num beta
-  int* ctx = (int*)(lds + a.off_ctx);
-  int* ylab = (int*)(lds + a.off_ylab);
-  float* dbuf = (float*)(lds + a.off_dbuf);  // [2][FR] den marginals
-  float* mbuf = (float*)(lds + a.off_nbuf);  // [2][FR] num marginals
-  const unsigned ldsb = lds_base_addr(lds);
-
-  const int den_lanes = a.den_waves * 64;
-  const int aux_lanes = a.aux_waves * 64;
-  const int role = wave < a.den_waves ? 0 : (wave < a.den_waves + a.aux_waves ? 1 : 2);
-  const int lw = wave - a.den_waves - a.aux_waves;
-  const int al = tid - den_lanes;
-
-  float gb = a.grad ? a.grad[b] : 1.f;
-  const float log_z = do_den ? a.log_z_in[b] : 0.f;
-  const float numv = do_num ? a.num_in[b] : 0.f;
-  // unreachable label string (loss = +inf) or degenerate partition: dW = 0
-  if ((do_num && !__builtin_isfinite(numv)) || (do_den && !__builtin_isfinite(log_z))) gb = 0.f;
-  const int nl = do_num ? a.nlab[b] : 0;
-
-  // ---- prologue
-  if (role == 2) {
-    const int pre = nf < a.P ? nf : a.P;
-    for (int f = 0; f < pre; ++f) issue_frame(a, b, nf - 1 - f, f % a.S, lw, lane, ldsb);
-  } else if (role == 0) {
-    // beta_T = one for every state: all context states are final
-    // (lattices.py:788-790)
-    if (do_den) for (int p = tid; p < C; p += den_lanes) bbuf[p] = 0.f;
-  } else {
-    if (do_num) {
-      for (int u = al; u < NP; u += aux_lanes) nbb[u] = (u == nl) ? 0.f : -kInf;
-      if (al == 0) walk_states(a, b, ctx, ylab);
-    }
-    if (DST && do_num)
-      for (int e = al; e < 2 * FR; e += aux_lanes) mbuf[e] = 0.f;
-  }
-  lds_barrier();
-  if (!DST && do_num && role == 1 && a.ctx_side) {
-    for (int u = al; u < NP; u += aux_lanes) {
-      a.ctx_side[((long long)b * NP + u) * 2 + 0] = ctx[u];
-      a.ctx_side[((long long)b * NP + u) * 2 + 1] = ylab[u];
-    }
-  }
-
-  const int L = a.L, lgL = a.lgL;
-  const int j = tid & (L - 1);
-  const int grp0 = tid >> lgL;
-  const int ngrp = den_lanes >> lgL;
-  const int es = BF16 ? 2 : 4;
-
-  for (int i = 0; i < nf; ++i) {
-    const int t = nf - 1 - i;
-    const int slot = i % a.S;
-    const int cur = i & 1;
-    if (role == 2) {
-      const int later = (a.P - 1 < nf - 1 - i) ? a.P - 1 : nf - 1 - i;
-      wait_vmcnt(later * (lw == 0 ? a.gw0 : a.gw1));
-    }
-    lds_barrier();
-    if (role == 2) {
-      if (i + a.P < nf) issue_frame(a, b, nf - 1 - (i + a.P), (i + a.P) % a.S, lw, lane, ldsb);
-      continue;
-    }
-    const unsigned char* wrow;
-    if constexpr (WST) wrow = slot_row<0>(lds, a, b, t, slot);
-    else wrow = a.W + ((long long)b * a.T + t) * (long long)FR * es;
-
-    if (role == 0) {
-      if (!do_den) continue;
-      const float* arow = (const float*)slot_row<1>(lds, a, b, t, slot);
-      const float* bcur = bbuf + cur * C;
-      float* bnxt = bbuf + (cur ^ 1) * C;
-      for (int p = grp0; p < C; p += ngrp) {
-        bool zero;
-        const int nb = next_base(g, p, &zero);
-        float xv[TMAX];
-#pragma unroll
-        for (int m = 0; m < TMAX; ++m) {
-          const int y = j + m * L;
-          float x = -kInf;
-          if (y <= g.V) {
-            const int dst = (y == 0) ? p : (zero ? 0 : nb + y);
-            x = ldw<BF16>(wrow, (long long)p * R + y) + bcur[dst];
-          }
-          xv[m] = x;
-        }
-        float mx = xv[0];
-#pragma unroll
-        for (int m = 1; m < TMAX; ++m) mx = fmaxf(mx, xv[m]);
-        mx = grp_max(mx, lgL);
-        const float c = __builtin_isfinite(mx) ? mx : 0.f;
-        float s = 0.f;
-#pragma unroll
-        for (int m = 0; m < TMAX; ++m) {
-          xv[m] = lt_exp(xv[m] - c);
-          s += xv[m];
-        }
-        s = grp_sum(s, lgL);
-        if (j == 0) bnxt[p] = c + lt_log(s);
-        // marginals exp(alpha + w + beta' - log_z) = e_y * exp(c + alpha - log_z)
-        const float sp = (gb == 0.f) ? 0.f : lt_exp(c + arow[p] - log_z) * gb;
-#pragma unroll
-        for (int m = 0; m < TMAX; ++m) {
-          const int y = j + m * L;
-          if (y <= g.V) {
-            const float v = xv[m] * sp;
-            const long long e = (long long)p * R + y;
-            if constexpr (DST) dbuf[cur * FR + e] = v;
-            else stw<BF16>(a.dW, ((long long)b * a.T + t) * FR + e, v);
-          }
-        }
-      }
-    } else {  // role 1
-      if constexpr (DST) {
-        if (i >= 1) {  // store frame t+1 (computed last step)
-          const int pv = cur ^ 1;
-          const long long base = ((long long)b * a.T + (t + 1)) * FR;
-          for (int e = al; e < FR; e += aux_lanes) {
-            float v = do_den ? dbuf[pv * FR + e] : 0.f;
-            if (do_num) { v -= mbuf[pv * FR + e]; mbuf[pv * FR + e] = 0.f; }
-            stw<BF16>(a.dW, base + e, v);
-          }
-        }
-      }
-      if (!do_num) continue;
-      const float* ncur = nbb + cur * NP;
-      float* nnxt = nbb + (cur ^ 1) * NP;
-      const float* anrow = (const float*)slot_row<2>(lds, a, b, t, slot);
-      for (int u = al; u < NP; u += aux_lanes) {
-        const float xb = ldw<BF16>(wrow, ctx[u]) + ncur[u];
-        float xl = -kInf;
-        if (u < a.U) xl = ldw<BF16>(wrow, ctx[u] + ylab[u]) + ncur[u + 1];
-        nnxt[u] = log_plus(xb, xl);
-        float mb = 0.f, ml = 0.f;
-        if (gb != 0.f) {
-          const float an = anrow[u] - numv;
-          mb = lt_exp(an + xb) * gb;
-          ml = lt_exp(an + xl) * gb;
-        }
-        if constexpr (DST) {
-          if (mb != 0.f) atomicAdd(&mbuf[cur * FR + ctx[u]], mb);
-          if (ml != 0.f) atomicAdd(&mbuf[cur * FR + ctx[u] + ylab[u]], ml);
-        } else {
-          float* ns = a.nm_side + (((long long)b * a.T + t) * NP + u) * 2;
-          ns[0] = mb;
-          ns[1] = ml;
-        }
-      }
-    }
-  }
-  lds_barrier();
-  if constexpr (DST) {
-    if (role == 1 && nf >= 1) {  // last processed frame: t = 0
-      const int pv = (nf - 1) & 1;
-      const long long base = ((long long)b * a.T) * FR;
-      for (int e = al; e < FR; e += aux_lanes) {
-        float v = do_den ? dbuf[pv * FR + e] : 0.f;
-        if (do_num) v -= mbuf[pv * FR + e];
-        stw<BF16>(a.dW, base + e, v);
-      }
-    }
-  }
-  // padding frames get zero marginals (lattices.py:775-779); with no
-  // denominator in the direct path nothing else wrote dW.
-  {
-    const int t0 = (!DST && !do_den) ? 0 : nf;
-    const long long n = (long long)(a.T - t0) * FR;
-    const long long base = ((long long)b * a.T + t0) * FR;
-    const int nthr = blockDim.x;
-    for (long long e = tid; e < n; e += nthr) stw<BF16>(a.dW, base + e, 0.f);
-  }
-}
-
 // Direct path: subtract numerator marginals (one thread per (b,t), fixed u
 // order, so the result is deterministic).
 template <bool BF16>
@@ -894,13 +148,7 @@ int env_int(const char* name, int dflt) {
 
 int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
-struct Plan {
-  KArgs a;
-  int tmax;
-  bool wst, dst;
-  int threads;
-  int lds_bytes;
-};
+using lt_impl::Plan;
 
 // Choose lanes-per-group, wave roles, LDS carve and ring depth.
 //   kind 0: forward, kind 1: backward
@@ -909,34 +157,60 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   memset(&a, 0, sizeof(a));
   a.B = pb->batch; a.T = pb->max_frames; a.U = pb->max_labels; a.g = g;
   a.flags = flags;
+  a.dbg = env_int("LT_DBG", 0);
+#ifdef LT_STAMPS
+  {
+    const char* sp = getenv("LT_STAMPS_PTR");
+    a.stamps = sp ? (long long*)strtoull(sp, nullptr, 0) : nullptr;
+  }
+#endif
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const int es = bf16 ? 2 : 4;
-  const int C = g.C, R = g.V + 1, NP = a.U + 1;
-  a.FR = C * R;
+  const int C = g.C, NP = a.U + 1;
+  a.FR = C * (g.V + 1);
   const long long FRB = (long long)a.FR * es;
   const bool do_den = flags & F_DEN, do_num = flags & F_NUM;
 
-  // terms per group: forward K+1 (blank + lexical in-arcs), backward V+1
-  const int nterm = kind == 0 ? g.K + 1 : g.V + 1;
+  a.aux_waves = do_num ? std::min(ceil_div(NP, 64), 4) : (kind == 1 ? 1 : 0);
+  a.load_waves = 2;
+  if (!do_den && a.aux_waves == 0) a.aux_waves = 1;
+  const int max_den = kMaxWaves - a.aux_waves - a.load_waves;
+
+  // Denominator groups. Forward: one group per destination with lexical
+  // in-arcs; for n >= 1 the start state (blank self loop only) is done on
+  // the side by den lane 0 (extra0). Backward: one group per source state.
+  int nterm;
+  if (kind == 0) {
+    nterm = g.K + 1;
+    if (g.n >= 1) { a.den_groups = C - 1; a.den_q0 = 1; a.extra0 = 1; }
+    else { a.den_groups = 1; a.den_q0 = 0; a.extra0 = 0; }
+  } else {
+    nterm = g.V + 1;
+    a.den_groups = C; a.den_q0 = 0; a.extra0 = 0;
+  }
   int L = 1;
-  while (L < 64 && (nterm + L - 1) / L > 16) L *= 2;
-  // prefer >= ~4 terms per lane while the groups fit in the den waves
-  while (L < 16 && nterm / (2 * L) >= 4 && (long long)C * 2 * L <= 64LL * 10) L *= 2;
+  while (L < 64 && ceil_div(nterm, L) > 16) L *= 2;
+  while (L < 16 && ceil_div(nterm, 2 * L) >= 3 &&
+         (long long)a.den_groups * 2 * L <= 64LL * std::min(max_den, 4))
+    L *= 2;
   const int envL = env_int("LT_DEN_LANES", 0);
-  if (envL > 0 && (envL & (envL - 1)) == 0 && (nterm + envL - 1) / envL <= 16) L = envL;
+  if (envL > 0 && (envL & (envL - 1)) == 0 && envL <= 64 && ceil_div(nterm, envL) <= 16) L = envL;
   a.L = L;
   a.lgL = 0;
   while ((1 << a.lgL) < L) ++a.lgL;
-  const int per = (nterm + L - 1) / L;
-  pl->tmax = per <= 4 ? 4 : (per <= 8 ? 8 : 16);
+  a.Pr = ceil_div(nterm, L);
+  // compiled (LG, P) variants: exact pairs, else runtime-LG with P >= Pr
+  static const int kFixed[][2] = {{3, 5}, {2, 9}, {1, 4}, {1, 3}, {2, 5}, {3, 3}, {2, 3}};
+  pl->lg = -1;
+  pl->tmax = a.Pr <= 4 ? 4 : (a.Pr <= 8 ? 8 : 16);
+  for (const auto& v : kFixed)
+    if (v[0] == a.lgL && v[1] == a.Pr) { pl->lg = v[0]; pl->tmax = v[1]; }
 
-  a.aux_waves = do_num ? std::min(ceil_div(NP, 64), 4) : (kind == 1 ? 1 : 0);
-  a.load_waves = 2;
-  int den = do_den ? ceil_div((long long)C * L, 64) : 0;
-  den = std::min(den, kMaxWaves - a.aux_waves - a.load_waves);
+  int den = do_den ? ceil_div((long long)a.den_groups * L, 64) : 0;
+  den = std::min(den, max_den);
   if (do_den && den < 1) den = 1;
   a.den_waves = den;
-  if (!do_den && a.aux_waves == 0) a.aux_waves = 1;
+  a.den_fast = (den * 64 / L) >= a.den_groups;
 
   // LDS carve (bytes, 16-aligned pieces)
   auto al16 = [](long long x) { return (int)((x + 15) & ~15LL); };
@@ -948,17 +222,18 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   a.off_ylab = off; off += al16((long long)NP * 4);
   int fixed = off;
 
-  // staged marginals (backward)
+  // staged marginals (backward): two frames each, stride FR+4 rounded to 4
   pl->dst = false;
   if (kind == 1) {
-    const long long need = (do_den ? 2LL * a.FR * 4 : 0) + (do_num ? 2LL * a.FR * 4 : 0);
+    const long long frs = ((long long)a.FR + 4 + 3) & ~3LL;
+    const long long need = (do_den ? 2 * frs * 4 : 0) + (do_num ? 2 * frs * 4 : 0);
     const int ring_min = 4 * 1024 * 4;  // leave room for a few ring slots
     if (fixed + need + ring_min <= kLdsMax && env_int("LT_FORCE_DIRECT", 0) == 0) {
       pl->dst = true;
       a.off_dbuf = fixed;
-      fixed += do_den ? al16(2LL * a.FR * 4) : 0;
+      fixed += do_den ? al16(2 * frs * 4) : 0;
       a.off_nbuf = fixed;
-      fixed += do_num ? al16(2LL * a.FR * 4) : 0;
+      fixed += do_num ? al16(2 * frs * 4) : 0;
     }
   }
 
@@ -1003,62 +278,31 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   if (pl->lds_bytes > kLdsMax) return fail(LT_EUNSUPPORTED, "LDS plan exceeds 160 KiB");
   pl->threads = 64 * (a.den_waves + a.aux_waves + a.load_waves);
   if (pl->threads > 1024) return fail(LT_EUNSUPPORTED, "too many waves");
+  if (env_int("LT_VERBOSE", 0))
+    fprintf(stderr,
+            "[lt] kind=%d C=%d V=%d L=%d Pr=%d P=%d lg=%d den=%d aux=%d load=%d groups=%d fast=%d "
+            "S=%d slot=%d lds=%d dst=%d wst=%d\n",
+            kind, C, g.V, a.L, a.Pr, pl->tmax, pl->lg, a.den_waves, a.aux_waves, a.load_waves,
+            a.den_groups, a.den_fast, a.S, a.slot_bytes, pl->lds_bytes, (int)pl->dst,
+            (int)pl->wst);
   return LT_OK;
 }
 
-template <typename K>
-int launch(K kernel, const Plan& pl, int grid, hipStream_t st) {
-  if (grid == 0) return LT_OK;
-  hipError_t e = hipFuncSetAttribute((const void*)kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, pl.lds_bytes);
-  if (e != hipSuccess) return hip_check(e, "hipFuncSetAttribute");
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(pl.threads), pl.lds_bytes, st, pl.a);
-  return hip_check(hipGetLastError(), "kernel launch");
-}
-
-template <int MODE, bool BF16, bool WST>
-int launch_fwd_t(const Plan& pl, int grid, hipStream_t st) {
-  switch (pl.tmax) {
-    case 4: return launch(fwd_kernel<MODE, BF16, WST, 4>, pl, grid, st);
-    case 8: return launch(fwd_kernel<MODE, BF16, WST, 8>, pl, grid, st);
-    default: return launch(fwd_kernel<MODE, BF16, WST, 16>, pl, grid, st);
-  }
-}
-template <int MODE>
-int launch_fwd_m(const Plan& pl, bool bf16, int grid, hipStream_t st) {
-  if (bf16) return pl.wst ? launch_fwd_t<MODE, true, true>(pl, grid, st)
-                          : launch_fwd_t<MODE, true, false>(pl, grid, st);
-  return pl.wst ? launch_fwd_t<MODE, false, true>(pl, grid, st)
-                : launch_fwd_t<MODE, false, false>(pl, grid, st);
-}
+constexpr int M1 = -1;
 int launch_fwd(int mode, const Plan& pl, bool bf16, int grid, hipStream_t st) {
-  switch (mode) {
-    case M_LOG: return launch_fwd_m<M_LOG>(pl, bf16, grid, st);
-    case M_MAX: return launch_fwd_m<M_MAX>(pl, bf16, grid, st);
-    case M_REAL: return launch_fwd_m<M_REAL>(pl, bf16, grid, st);
-  }
-  return fail(LT_EINVAL, "bad semiring");
+#define LT_CASE(LG, P) \
+  if (pl.lg == LG && pl.tmax == P) return lt_impl::launch_fwd_##LG##_##P(mode, pl, bf16, grid, st);
+  LT_VARIANTS(LT_CASE)
+#undef LT_CASE
+  return fail(LT_EINVAL, "no kernel variant for this slice size");
 }
 
-template <bool BF16, bool WST, bool DST>
-int launch_bwd_t(const Plan& pl, int grid, hipStream_t st) {
-  switch (pl.tmax) {
-    case 4: return launch(bwd_kernel<BF16, WST, DST, 4>, pl, grid, st);
-    case 8: return launch(bwd_kernel<BF16, WST, DST, 8>, pl, grid, st);
-    default: return launch(bwd_kernel<BF16, WST, DST, 16>, pl, grid, st);
-  }
-}
 int launch_bwd(const Plan& pl, bool bf16, int grid, hipStream_t st) {
-  if (bf16) {
-    if (pl.wst) return pl.dst ? launch_bwd_t<true, true, true>(pl, grid, st)
-                              : launch_bwd_t<true, true, false>(pl, grid, st);
-    return pl.dst ? launch_bwd_t<true, false, true>(pl, grid, st)
-                  : launch_bwd_t<true, false, false>(pl, grid, st);
-  }
-  if (pl.wst) return pl.dst ? launch_bwd_t<false, true, true>(pl, grid, st)
-                            : launch_bwd_t<false, true, false>(pl, grid, st);
-  return pl.dst ? launch_bwd_t<false, false, true>(pl, grid, st)
-                : launch_bwd_t<false, false, false>(pl, grid, st);
+#define LT_CASE(LG, P) \
+  if (pl.lg == LG && pl.tmax == P) return lt_impl::launch_bwd_##LG##_##P(pl, bf16, grid, st);
+  LT_VARIANTS(LT_CASE)
+#undef LT_CASE
+  return fail(LT_EINVAL, "no kernel variant for this slice size");
 }
 
 void bind_streams(KArgs& a, const void* W, const float* alpha, const float* alpha_num) {
@@ -1078,6 +322,10 @@ size_t side_bytes(const lt_problem* pb) {
 }
 
 }  // namespace
+
+namespace lt_impl {
+int set_error(int code, const char* msg) { return fail(code, msg); }
+}  // namespace lt_impl
 
 // ---------------------------------------------------------------------------
 // C ABI
