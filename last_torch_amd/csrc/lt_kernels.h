@@ -104,7 +104,10 @@ __host__ __device__ inline int next_base(const NGram& g, int p, bool* zero) {
 // ---------------------------------------------------------------------------
 // Device helpers
 // ---------------------------------------------------------------------------
-LT_DEVINL float lt_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+constexpr float kLog2e = 1.4426950408889634f;
+LT_DEVINL float lt_exp(float x) { return __builtin_amdgcn_exp2f(x * kLog2e); }
+// exp(x - c) with cl = c * log2(e) precomputed: one FMA + v_exp_f32.
+LT_DEVINL float lt_exp_off(float x, float cl) { return __builtin_amdgcn_exp2f(__builtin_fmaf(x, kLog2e, -cl)); }
 // Arguments are sums of exp() with the max term == 1 (>= 1) or exactly 0.
 LT_DEVINL float lt_log(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
 
@@ -493,21 +496,43 @@ LT_DEVINL void gargmax(float& v, int& i, int lg) {
   }
 }
 
+// Balanced reductions over a lane's register slice (short dependency chains).
+template <int P>
+LT_DEVINL float tree_max(const float* x) {
+  float t[P];
+#pragma unroll
+  for (int m = 0; m < P; ++m) t[m] = x[m];
+#pragma unroll
+  for (int w = 1; w < P; w *= 2)
+#pragma unroll
+    for (int m = 0; m + w < P; m += 2 * w) t[m] = fmaxf(t[m], t[m + w]);
+  return t[0];
+}
+template <int P>
+LT_DEVINL float tree_sum(const float* x) {
+  float t[P];
+#pragma unroll
+  for (int m = 0; m < P; ++m) t[m] = x[m];
+#pragma unroll
+  for (int w = 1; w < P; w *= 2)
+#pragma unroll
+    for (int m = 0; m + w < P; m += 2 * w) t[m] = t[m] + t[m + w];
+  return t[0];
+}
+
 // Semiring reduction of a group's terms (x[m] for m >= nv already = zero).
 // Log follows _LogSumExp.forward (semirings.py:279-286); Max returns the
 // first maximum's term order index in *bi (semirings.py:363, :382).
 template <int MODE, int LG, int P>
 LT_DEVINL float group_reduce(const float* x, int lgL, int o0, int* bi) {
   if constexpr (MODE == M_LOG) {
-    float mx = x[0];
-#pragma unroll
-    for (int m = 1; m < P; ++m) mx = fmaxf(mx, x[m]);
-    mx = gmax<LG>(mx, lgL);
+    float mx = gmax<LG>(tree_max<P>(x), lgL);
     const float c = __builtin_isfinite(mx) ? mx : 0.f;
-    float s = 0.f;
+    const float cl = c * kLog2e;
+    float e[P];
 #pragma unroll
-    for (int m = 0; m < P; ++m) s += lt_exp(x[m] - c);
-    s = gsum<LG>(s, lgL);
+    for (int m = 0; m < P; ++m) e[m] = lt_exp_off(x[m], cl);
+    const float s = gsum<LG>(tree_sum<P>(e), lgL);
     return c + lt_log(s);
   } else if constexpr (MODE == M_MAX) {
     float r = x[0];
@@ -519,10 +544,7 @@ LT_DEVINL float group_reduce(const float* x, int lgL, int o0, int* bi) {
     *bi = i;
     return r;
   } else {
-    float s = 0.f;
-#pragma unroll
-    for (int m = 0; m < P; ++m) s += x[m];
-    return gsum<LG>(s, lgL);
+    return gsum<LG>(tree_sum<P>(x), lgL);
   }
 }
 
@@ -537,15 +559,17 @@ LT_DEVINL void idle_loop(int nf) {
 // frame f(i+P) is issued after the barrier and frame f(i+1) is waited for
 // before the next one (counted vmcnt).
 LT_DEVINL void loader_loop(const KArgs& a, int b, int nf, bool reverse, int lw, int lane,
-                           unsigned ldsb) {
+                           unsigned ldsb, int ahead = 0) {
   const int gw = lw == 0 ? a.gw0 : a.gw1;
   int slot = 0;
   const bool st = lw == 0 && lane == 0;
   for (int i = 0; i < nf; ++i) {
     LT_STAMP(a, st, 2, i, 0);
     if (!(a.dbg & 4)) {
-      const int later = (a.P - 1 < nf - 1 - i) ? a.P - 1 : nf - 1 - i;
-      wait_vmcnt(later * gw);
+      // frame i + ahead must have landed by this barrier
+      int later = (a.P - 1 < nf - 1 - i) ? a.P - 1 : nf - 1 - i;
+      later -= ahead;
+      wait_vmcnt(later < 0 ? 0 : later * gw);
     }
     lds_barrier();
     LT_STAMP(a, st, 2, i, 1);
@@ -609,51 +633,65 @@ LT_DEVINL void den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int
                           (long long)b * a.T, false);
   float* hist = a.alpha ? a.alpha + (long long)b * a.T * C : nullptr;
   unsigned char* bpp = a.bp ? a.bp + (long long)b * a.T * C : nullptr;
-  for (int i = 0; i < nf; ++i) {
-    LT_STAMP(a, tid == 0, 0, i, 0);
-    lds_barrier();
-    LT_STAMP(a, tid == 0, 0, i, 1);
-    const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
-    const float* acur = abuf + (i & 1) * C;
-    float* anxt = abuf + ((i + 1) & 1) * C;
-    for (int qq = fast ? q : a.den_q0 + grp; qq < C; qq += ngrp) {
-      if (fast && !has) break;
-      int ao[P], wo[P];
-      int n2 = nv;
-      if (fast) {
+  // one destination group: terms -> semiring sum -> alpha_{t+1}[q]
+  auto group = [&](int qq, const int* ao, const int* wo, int n2, const unsigned char* wrow,
+                   const float* acur, float* anxt) {
+    float x[P];
+    float aself = 0.f;
 #pragma unroll
-        for (int m = 0; m < P; ++m) { ao[m] = aoff[m]; wo[m] = woff[m]; }
-      } else {
-        n2 = fwd_slice<P>(g, qq, j, a.Pr, ao, wo);
-      }
-      float x[P];
-      float aself = 0.f;
-#pragma unroll
-      for (int m = 0; m < P; ++m) {
-        const float av = acur[ao[m]];
-        const float wv = ldw<BF16>(wrow, wo[m]);
-        if (m == 0) aself = av;
-        x[m] = m < n2 ? s_times<MODE>(av, wv) : s_zero<MODE>();
-      }
-      int bi = 0;
-      const float r = group_reduce<MODE, LG, P>(x, lgL, j * a.Pr, &bi);
-      if (j == 0) {
-        anxt[qq] = r;
-        if (hist) hist[qq] = aself;
-        if (MODE == M_MAX && bpp) bpp[qq] = (unsigned char)bi;
-      }
-      if (fast) break;
+    for (int m = 0; m < P; ++m) {
+      const float av = acur[ao[m]];
+      const float wv = ldw<BF16>(wrow, wo[m]);
+      if (m == 0) aself = av;
+      x[m] = m < n2 ? s_times<MODE>(av, wv) : s_zero<MODE>();
     }
-    if (a.extra0 && tid == 0) {  // start state: blank self loop only
+    int bi = 0;
+    const float r = group_reduce<MODE, LG, P>(x, lgL, j * a.Pr, &bi);
+    if (j == 0) {
+      anxt[qq] = r;
+      if (hist) hist[qq] = aself;
+      if (MODE == M_MAX && bpp) bpp[qq] = (unsigned char)bi;
+    }
+  };
+  auto start_state = [&](const unsigned char* wrow, const float* acur, float* anxt) {
+    if (a.extra0 && tid == 0) {  // blank self loop only
       const float av = acur[0];
       anxt[0] = s_times<MODE>(av, ldw<BF16>(wrow, 0));
       if (hist) hist[0] = av;
       if (MODE == M_MAX && bpp) bpp[0] = 0;
     }
-    advance(cw, a);
-    if (hist) hist += C;
-    if (bpp) bpp += C;
-    LT_STAMP(a, tid == 0, 0, i, 2);
+  };
+  if (fast) {
+    for (int i = 0; i < nf; ++i) {
+      LT_STAMP(a, tid == 0, 0, i, 0);
+      lds_barrier();
+      LT_STAMP(a, tid == 0, 0, i, 1);
+      const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
+      const float* acur = abuf + (i & 1) * C;
+      float* anxt = abuf + ((i + 1) & 1) * C;
+      if (has) group(q, aoff, woff, nv, wrow, acur, anxt);
+      start_state(wrow, acur, anxt);
+      advance(cw, a);
+      if (hist) hist += C;
+      if (bpp) bpp += C;
+      LT_STAMP(a, tid == 0, 0, i, 2);
+    }
+  } else {
+    for (int i = 0; i < nf; ++i) {
+      lds_barrier();
+      const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
+      const float* acur = abuf + (i & 1) * C;
+      float* anxt = abuf + ((i + 1) & 1) * C;
+      for (int qq = a.den_q0 + grp; qq < C; qq += ngrp) {
+        int ao[P], wo[P];
+        const int n2 = fwd_slice<P>(g, qq, j, a.Pr, ao, wo);
+        group(qq, ao, wo, n2, wrow, acur, anxt);
+      }
+      start_state(wrow, acur, anxt);
+      advance(cw, a);
+      if (hist) hist += C;
+      if (bpp) bpp += C;
+    }
   }
 }
 
@@ -807,56 +845,19 @@ __global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
   }
 }
 
-// Store one dW frame from the LDS staging buffers: v = den - num marginals.
-// Element e of the frame sits at LDS float index e + sh, sh = (global element
-// offset of the frame) % 4, so 4-element chunks are 16 B aligned on both
-// sides (8 B for bf16). Re-zeroes the numerator buffer.
-template <bool BF16>
-LT_DEVINL void store_frame(const KArgs& a, long long gbase, const float* db, float* nb,
-                           bool do_den, bool do_num, int al, int aux_lanes) {
-  const int FR = a.FR;
-  const int sh = (int)(gbase & 3);
-  const int head = (4 - sh) & 3;  // elements before the first aligned chunk
-  const int nchunk = (FR - head) >> 2;
-  const int tail0 = head + 4 * nchunk;
-  for (int c = al; c < nchunk; c += aux_lanes) {
-    const int li = head + 4 * c + sh;  // multiple of 4
-    float4 v = do_den ? *(const float4*)(db + li) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (do_num) {
-      const float4 n = *(const float4*)(nb + li);
-      v.x -= n.x; v.y -= n.y; v.z -= n.z; v.w -= n.w;
-      *(float4*)(nb + li) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    const long long ge = gbase + head + 4 * c;
-    if constexpr (BF16) {
-      ushort4 h;
-      h.x = f2bf(v.x); h.y = f2bf(v.y); h.z = f2bf(v.z); h.w = f2bf(v.w);
-      *(ushort4*)((unsigned short*)a.dW + ge) = h;
-    } else {
-      *(float4*)((float*)a.dW + ge) = v;
-    }
-  }
-  // unaligned head / tail elements
-  const int nedge = head + (FR - tail0);
-  for (int r = al; r < nedge; r += aux_lanes) {
-    const int e = r < head ? r : tail0 + (r - head);
-    float v = do_den ? db[e + sh] : 0.f;
-    if (do_num) { v -= nb[e + sh]; nb[e + sh] = 0.f; }
-    stw<BF16>(a.dW, gbase + e, v);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Backward kernel (Log): beta recursion + arc marginals -> dW.
-//   DST: dW frame staged in LDS (den marginals written by den lanes, numerator
-//        marginals LDS-atomically accumulated by aux lanes, stored coalesced
-//        one frame later by the aux lanes).
-//   !DST: den lanes store straight to HBM; numerator marginals go to a side
-//        buffer and a scatter kernel subtracts them (large C*(V+1)).
+//   Den lanes store dW straight to HBM, once per element.
+//   DST: the numerator marginals of the den lanes' frame are already in a
+//        3-deep LDS buffer (numerator lanes run one frame ahead) and are
+//        subtracted before the store.
+//   !DST (large C*(V+1)): numerator marginals go to a side buffer and a
+//        scatter kernel subtracts them afterwards.
 // ---------------------------------------------------------------------------
 template <bool BF16, bool WST, bool DST, int LG, int P>
-LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, float* dbuf,
-                            int FRS, int b, int nf, int tid, float gb, float log_z) {
+LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, float* nbuf3,
+                            int b, int nf, int tid, float gb, float log_z, bool do_den,
+                            bool do_num) {
   const NGram& g = a.g;
   const int C = g.C, FR = a.FR;
   const int lgL = LG >= 0 ? LG : a.lgL;
@@ -866,6 +867,7 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
   const int ngrp = (a.den_waves * 64) >> lgL;
   const bool fast = a.den_fast;
   const bool has = grp < a.den_groups;
+  const bool sub_num = DST && do_num;
   int woff[P], boff[P];
   int nv = 0;
   if (fast && has) nv = bwd_slice<P>(g, grp, j, a.Pr, woff, boff);
@@ -874,8 +876,58 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
   const long long es = BF16 ? 2 : 4;
   const long long t_last = (long long)b * a.T + (nf - 1);
   Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)FR * es, t_last, true);
-  Cursor ca = make_cursor(a.st_row[1], t_last, true);
+  Cursor ca = make_cursor(a.st_row[1] > 0 ? a.st_row[1] : (long long)C * 4, t_last, true);
   long long gframe = t_last * FR;  // global element offset of the frame
+  // one source group: beta_t[p] and the marginals of its out-arcs -> dW
+  auto group = [&](int p, const int* wo, const int* bo, int n2, const unsigned char* wrow,
+                   const float* arow, const float* bcur, float* bnxt, const float* ncur,
+                   void* dWf) {
+      // every LDS read of the step first
+      float wv[P], bv[P], nm[P];
+#pragma unroll
+      for (int m = 0; m < P; ++m) {
+        wv[m] = ldw<BF16>(wrow, wo[m]);
+        bv[m] = bcur[bo[m]];
+        nm[m] = sub_num ? ncur[wo[m]] : 0.f;
+      }
+      const float ap = do_den ? arow[p] : 0.f;
+      float v[P];
+      if (do_den) {
+        float x[P];
+#pragma unroll
+        for (int m = 0; m < P; ++m) x[m] = m < n2 ? wv[m] + bv[m] : -kInf;
+        const float mx = gmax<LG>(tree_max<P>(x), lgL);
+        const float c = __builtin_isfinite(mx) ? mx : 0.f;
+        const float cl = c * kLog2e;
+#pragma unroll
+        for (int m = 0; m < P; ++m) x[m] = lt_exp_off(x[m], cl);
+        const float s = gsum<LG>(tree_sum<P>(x), lgL);
+        if (j == 0) bnxt[p] = c + lt_log(s);
+        // marginal exp(alpha + w + beta' - log_z) = e * exp(c + alpha - log_z)
+        const float sp = (gb == 0.f) ? 0.f : lt_exp(c + ap - log_z) * gb;
+#pragma unroll
+        for (int m = 0; m < P; ++m) v[m] = x[m] * sp - nm[m];
+      } else {
+#pragma unroll
+        for (int m = 0; m < P; ++m) v[m] = -nm[m];
+      }
+      // branch-free stores: slots past the lane's slice rewrite the last valid
+      // element with its own value
+      if (n2 > 0) {
+        const int wl = wo[0];
+        float vl = v[0];
+        int wlast = wl;
+#pragma unroll
+        for (int m = 1; m < P; ++m)
+          if (m < n2) { wlast = wo[m]; vl = v[m]; }
+#pragma unroll
+        for (int m = 0; m < P; ++m) {
+          const bool ok = m < n2;
+          stw<BF16>(dWf, (ok ? wo[m] : wlast), ok ? v[m] : vl);
+        }
+      }
+  };
+  int k3 = 0;  // numerator marginal buffer of this frame (i % 3)
   for (int i = 0; i < nf; ++i) {
     LT_STAMP(a, tid == 0, 0, i, 0);
     lds_barrier();
@@ -885,65 +937,75 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
     const float* arow = (const float*)(ringa + ca.soff + ca.mis);
     const float* bcur = bbuf + cur * C;
     float* bnxt = bbuf + (cur ^ 1) * C;
-    float* dcur = dbuf + cur * FRS + (int)(gframe & 3);
-    for (int p = grp; p < C; p += ngrp) {
-      if (fast && !has) break;
-      int wo[P], bo[P];
-      int n2 = nv;
-      if (fast) {
-#pragma unroll
-        for (int m = 0; m < P; ++m) { wo[m] = woff[m]; bo[m] = boff[m]; }
-      } else {
-        n2 = bwd_slice<P>(g, p, j, a.Pr, wo, bo);
+    const float* ncur = nbuf3 + k3 * FR;
+    void* dWf = BF16 ? (void*)((unsigned short*)a.dW + gframe) : (void*)((float*)a.dW + gframe);
+    if (fast) {
+      if (has) group(grp, woff, boff, nv, wrow, arow, bcur, bnxt, ncur, dWf);
+    } else {
+      for (int p = grp; p < C; p += ngrp) {
+        int wo[P], bo[P];
+        const int n2 = bwd_slice<P>(g, p, j, a.Pr, wo, bo);
+        group(p, wo, bo, n2, wrow, arow, bcur, bnxt, ncur, dWf);
       }
-      float x[P];
-#pragma unroll
-      for (int m = 0; m < P; ++m) {
-        const float wv = ldw<BF16>(wrow, wo[m]);
-        const float bv = bcur[bo[m]];
-        x[m] = m < n2 ? wv + bv : -kInf;
-      }
-      const float ap = arow[p];
-      float mx = x[0];
-#pragma unroll
-      for (int m = 1; m < P; ++m) mx = fmaxf(mx, x[m]);
-      mx = gmax<LG>(mx, lgL);
-      const float c = __builtin_isfinite(mx) ? mx : 0.f;
-      float s = 0.f;
-#pragma unroll
-      for (int m = 0; m < P; ++m) {
-        x[m] = lt_exp(x[m] - c);
-        s += x[m];
-      }
-      s = gsum<LG>(s, lgL);
-      if (j == 0) bnxt[p] = c + lt_log(s);
-      // marginal exp(alpha + w + beta' - log_z) = e * exp(c + alpha - log_z)
-      const float sp = (gb == 0.f) ? 0.f : lt_exp(c + ap - log_z) * gb;
-#pragma unroll
-      for (int m = 0; m < P; ++m) {
-        if (m < n2) {
-          const float v = x[m] * sp;
-          if constexpr (DST) dcur[wo[m]] = v;
-          else stw<BF16>(a.dW, gframe + wo[m], v);
-        }
-      }
-      if (fast) break;
     }
     advance(cw, a);
     advance(ca, a);
     gframe -= FR;
+    k3 = (k3 == 2) ? 0 : k3 + 1;
     LT_STAMP(a, tid == 0, 0, i, 2);
   }
 }
 
+// Numerator beta + marginals for one frame (the reverse of
+// alignments.py:320-329): beta^n_t[u] from beta^n_{t+1}; marginals
+// exp(alpha^n_t[u] + w + beta^n_{t+1} - num) * g accumulated (LDS atomics:
+// several positions can share an arc) into `mdst` or written to the side
+// buffer `side` (direct path).
+template <bool BF16, bool DST>
+LT_DEVINL void num_bwd_frame(const KArgs& a, const unsigned char* wrow, const float* anrow,
+                             const float* ncur, float* nnxt, float* mdst, float* side,
+                             const int* ctx, const int* ylab, int al, int num_lanes, int ob,
+                             int ol, float gb, float numv) {
+  const int NP = a.U + 1;
+  for (int u = al; u < NP; u += num_lanes) {
+    int o0 = ob, o1 = ol;
+    if (u != al) { o0 = ctx[u]; o1 = u < a.U ? o0 + ylab[u] : 0; }
+    const bool lex = u < a.U;
+    // all reads first (o1 = 0 and the u+1 clamp are in-bounds dummies)
+    const float wb = ldw<BF16>(wrow, o0);
+    const float wl = ldw<BF16>(wrow, o1);
+    const float bu = ncur[u];
+    const float bu1 = ncur[lex ? u + 1 : u];
+    const float an = anrow[u] - numv;
+    const float xb = wb + bu;
+    const float xl = lex ? wl + bu1 : -kInf;
+    nnxt[u] = log_plus(xb, xl);
+    float mb = 0.f, ml = 0.f;
+    if (gb != 0.f) {
+      mb = lt_exp(an + xb) * gb;
+      ml = lt_exp(an + xl) * gb;
+    }
+    if constexpr (DST) {
+      if (mb != 0.f) atomicAdd(&mdst[o0], mb);
+      if (ml != 0.f) atomicAdd(&mdst[o1], ml);
+    } else {
+      side[u * 2 + 0] = mb;
+      side[u * 2 + 1] = ml;
+    }
+  }
+}
+
+// Numerator lanes of the backward. DST: they run one frame AHEAD of the
+// denominator (frame nf-1 in the prologue, frame nf-2-i at step i) so that
+// the den lanes can subtract the numerator marginals of their frame from
+// the 3-deep LDS buffer and store dW once, straight to HBM.
 template <bool BF16, bool WST, bool DST>
-LT_DEVINL void aux_bwd_loop(const KArgs& a, unsigned char* lds, float* nbb, float* dbuf,
-                            float* mbuf, int FRS, const int* ctx, const int* ylab, int b, int nf,
-                            int al, int aux_lanes, float gb, float numv, bool do_den,
-                            bool do_num) {
+LT_DEVINL void num_bwd_loop(const KArgs& a, unsigned char* lds, float* nbb, float* nbuf3,
+                            const int* ctx, const int* ylab, int b, int nf, int al, int num_lanes,
+                            float gb, float numv) {
   const int NP = a.U + 1, FR = a.FR;
   int ob = 0, ol = 0;
-  if (do_num && al < NP) {
+  if (al < NP) {
     ob = ctx[al];
     ol = al < a.U ? ob + ylab[al] : 0;
   }
@@ -953,52 +1015,47 @@ LT_DEVINL void aux_bwd_loop(const KArgs& a, unsigned char* lds, float* nbb, floa
   const long long t_last = (long long)b * a.T + (nf - 1);
   Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)FR * es, t_last, true);
   Cursor cn = make_cursor(a.st_row[2], t_last, true);
-  long long gframe = t_last * FR;
-  for (int i = 0; i < nf; ++i) {
-    LT_STAMP(a, al == 0, 1, i, 0);
-    lds_barrier();
-    LT_STAMP(a, al == 0, 1, i, 1);
-    const int cur = i & 1;
-    if constexpr (DST) {
-      if (i >= 1) {  // store the frame computed last step (t+1)
-        const int pv = cur ^ 1;
-        store_frame<BF16>(a, gframe + FR, dbuf + pv * FRS, mbuf + pv * FRS, do_den, do_num, al,
-                          aux_lanes);
-      }
-    }
-    if (do_num) {
-      const unsigned char* wrow = WST ? ringw + cw.soff + cw.mis : a.W + cw.goff;
-      const float* anrow = (const float*)(ringn + cn.soff + cn.mis);
-      const float* ncur = nbb + cur * NP;
-      float* nnxt = nbb + (cur ^ 1) * NP;
-      float* mcur = mbuf + cur * FRS + (int)(gframe & 3);
-      for (int u = al; u < NP; u += aux_lanes) {
-        int o0 = ob, o1 = ol;
-        if (u != al) { o0 = ctx[u]; o1 = u < a.U ? o0 + ylab[u] : 0; }
-        const float xb = ldw<BF16>(wrow, o0) + ncur[u];
-        float xl = -kInf;
-        if (u < a.U) xl = ldw<BF16>(wrow, o1) + ncur[u + 1];
-        nnxt[u] = log_plus(xb, xl);
-        float mb = 0.f, ml = 0.f;
-        if (gb != 0.f) {
-          const float an = anrow[u] - numv;
-          mb = lt_exp(an + xb) * gb;
-          ml = lt_exp(an + xl) * gb;
-        }
-        if constexpr (DST) {
-          if (mb != 0.f) atomicAdd(&mcur[o0], mb);
-          if (ml != 0.f) atomicAdd(&mcur[o1], ml);
-        } else {
-          float* ns = a.nm_side + ((gframe / FR) * NP + u) * 2;
-          ns[0] = mb;
-          ns[1] = ml;
-        }
-      }
-    }
+  float* side = a.nm_side ? a.nm_side + t_last * NP * 2 : nullptr;
+  const int lead = DST ? 1 : 0;  // frames ahead of the den lanes
+  int nb = 0;                    // beta^n buffer parity
+  int k3 = 0;                    // marginal buffer of the frame being computed
+  if (DST && nf > 0) {           // prologue frame nf-1 (after the caller's barrier)
+    const unsigned char* wrow = WST ? ringw + cw.soff + cw.mis : a.W + cw.goff;
+    const float* anrow = (const float*)(ringn + cn.soff + cn.mis);
+    num_bwd_frame<BF16, DST>(a, wrow, anrow, nbb, nbb + NP, nbuf3, nullptr, ctx, ylab, al,
+                             num_lanes, ob, ol, gb, numv);
     advance(cw, a);
     advance(cn, a);
-    gframe -= FR;
-    LT_STAMP(a, al == 0, 1, i, 2);
+    nb = 1;
+    k3 = 1;
+  }
+  const bool stamper = al == 0;
+  for (int i = 0; i < nf; ++i) {
+    LT_STAMP(a, stamper, 1, i, 0);
+    lds_barrier();
+    LT_STAMP(a, stamper, 1, i, 1);
+    if (i + lead < nf) {
+      float* mdst = nbuf3 + k3 * FR;
+      if constexpr (DST) {  // re-zero the buffer the den lanes read last step
+        float* stale = nbuf3 + ((k3 == 2) ? 0 : k3 + 1) * FR;
+        for (int u = al; u < NP; u += num_lanes) {
+          int o0 = ob, o1 = ol;
+          if (u != al) { o0 = ctx[u]; o1 = u < a.U ? o0 + ylab[u] : 0; }
+          stale[o0] = 0.f;
+          stale[o1] = 0.f;
+        }
+      }
+      const unsigned char* wrow = WST ? ringw + cw.soff + cw.mis : a.W + cw.goff;
+      const float* anrow = (const float*)(ringn + cn.soff + cn.mis);
+      num_bwd_frame<BF16, DST>(a, wrow, anrow, nbb + nb * NP, nbb + (nb ^ 1) * NP, mdst, side,
+                               ctx, ylab, al, num_lanes, ob, ol, gb, numv);
+      advance(cw, a);
+      advance(cn, a);
+      if (side) side -= NP * 2;
+      nb ^= 1;
+      k3 = (k3 == 2) ? 0 : k3 + 1;
+    }
+    LT_STAMP(a, stamper, 1, i, 2);
   }
 }
 
@@ -1010,7 +1067,6 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const NGram& g = a.g;
   const int C = g.C, NP = a.U + 1, FR = a.FR;
-  const int FRS = DST ? (FR + 4 + 3) & ~3 : 0;  // staged frame stride (floats)
   const bool do_den = a.flags & F_DEN, do_num = a.flags & F_NUM;
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
@@ -1019,8 +1075,7 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
   float* nbb = (float*)(lds + a.off_na);     // [2][NP] num beta
   int* ctx = (int*)(lds + a.off_ctx);
   int* ylab = (int*)(lds + a.off_ylab);
-  float* dbuf = (float*)(lds + a.off_dbuf);  // [2][FRS] den marginals
-  float* mbuf = (float*)(lds + a.off_nbuf);  // [2][FRS] num marginals
+  float* nbuf3 = (float*)(lds + a.off_nbuf); // [3][FR] num marginals (DST)
   const unsigned ldsb = lds_base_addr(lds);
 
   const int den_lanes = a.den_waves * 64;
@@ -1050,10 +1105,15 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
       load_labels(a, b, ylab, al, aux_lanes);
     }
     if (DST && do_num)
-      for (int e = al; e < 2 * FRS; e += aux_lanes) mbuf[e] = 0.f;
+      for (int e = al; e < 3 * FR; e += aux_lanes) nbuf3[e] = 0.f;
   }
   lds_barrier();
   if (role == 1 && do_num && al == 0) walk_states(a, ctx, ylab);
+  if (role == 2 && DST && do_num && nf > 0) {
+    // the numerator lanes start one frame early: frame nf-1 must have landed
+    const int pre = nf < a.P ? nf : a.P;
+    wait_vmcnt((pre - 1) * (lw == 0 ? a.gw0 : a.gw1));
+  }
   lds_barrier();
   if (!DST && do_num && role == 1 && a.ctx_side) {
     for (int u = al; u < NP; u += aux_lanes) {
@@ -1063,29 +1123,22 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
   }
 
   if (role == 2) {
-    loader_loop(a, b, nf, true, lw, lane, ldsb);
+    loader_loop(a, b, nf, true, lw, lane, ldsb, DST && do_num ? 1 : 0);
   } else if (role == 0) {
-    if (do_den && !(a.dbg & 1))
-      den_bwd_loop<BF16, WST, DST, LG, P>(a, lds, bbuf, dbuf, FRS, b, nf, tid, gb, log_z);
+    if (!(a.dbg & 1))
+      den_bwd_loop<BF16, WST, DST, LG, P>(a, lds, bbuf, nbuf3, b, nf, tid, gb, log_z, do_den,
+                                          do_num);
     else idle_loop(nf);
   } else {
-    aux_bwd_loop<BF16, WST, DST>(a, lds, nbb, dbuf, mbuf, FRS, ctx, ylab, b, nf, al, aux_lanes,
-                                 gb, numv, do_den, do_num && !(a.dbg & 2));
+    if (do_num && !(a.dbg & 2))
+      num_bwd_loop<BF16, WST, DST>(a, lds, nbb, nbuf3, ctx, ylab, b, nf, al, aux_lanes, gb, numv);
+    else idle_loop(nf);
   }
   lds_barrier();
-  if constexpr (DST) {
-    if (role == 1 && nf >= 1) {  // last processed frame: t = 0
-      const int pv = (nf - 1) & 1;
-      store_frame<BF16>(a, (long long)b * a.T * FR, dbuf + pv * FRS, mbuf + pv * FRS, do_den,
-                        do_num, al, aux_lanes);
-    }
-  }
-  // padding frames get zero marginals (lattices.py:775-779); with no
-  // denominator in the direct path nothing else wrote dW.
+  // padding frames get zero marginals (lattices.py:775-779)
   {
-    const int t0 = (!DST && !do_den) ? 0 : nf;
-    const long long n = (long long)(a.T - t0) * FR;
-    const long long base = ((long long)b * a.T + t0) * FR;
+    const long long n = (long long)(a.T - nf) * FR;
+    const long long base = ((long long)b * a.T + nf) * FR;
     const int nthr = blockDim.x;
     for (long long e = tid; e < n; e += nthr) stw<BF16>(a.dW, base + e, 0.f);
   }

@@ -171,7 +171,8 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   const long long FRB = (long long)a.FR * es;
   const bool do_den = flags & F_DEN, do_num = flags & F_NUM;
 
-  a.aux_waves = do_num ? std::min(ceil_div(NP, 64), 4) : (kind == 1 ? 1 : 0);
+  a.aux_waves = do_num ? std::min(ceil_div(NP, 64), 4) : 0;
+  if (kind == 1 && do_num) a.aux_waves = std::max(a.aux_waves, env_int("LT_BWD_AUX", 0));
   a.load_waves = 2;
   if (!do_den && a.aux_waves == 0) a.aux_waves = 1;
   const int max_den = kMaxWaves - a.aux_waves - a.load_waves;
@@ -190,8 +191,9 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   }
   int L = 1;
   while (L < 64 && ceil_div(nterm, L) > 16) L *= 2;
+  const int den_cap = std::min(max_den, env_int("LT_MAX_DEN_WAVES", kind == 1 ? 5 : 4));
   while (L < 16 && ceil_div(nterm, 2 * L) >= 3 &&
-         (long long)a.den_groups * 2 * L <= 64LL * std::min(max_den, 4))
+         (long long)a.den_groups * 2 * L <= 64LL * den_cap)
     L *= 2;
   const int envL = env_int("LT_DEN_LANES", 0);
   if (envL > 0 && (envL & (envL - 1)) == 0 && envL <= 64 && ceil_div(nterm, envL) <= 16) L = envL;
@@ -206,9 +208,11 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   for (const auto& v : kFixed)
     if (v[0] == a.lgL && v[1] == a.Pr) { pl->lg = v[0]; pl->tmax = v[1]; }
 
-  int den = do_den ? ceil_div((long long)a.den_groups * L, 64) : 0;
+  // backward: the den lanes also store dW, so they exist without a denominator
+  const bool den_role = do_den || kind == 1;
+  int den = den_role ? ceil_div((long long)a.den_groups * L, 64) : 0;
   den = std::min(den, max_den);
-  if (do_den && den < 1) den = 1;
+  if (den_role && den < 1) den = 1;
   a.den_waves = den;
   a.den_fast = (den * 64 / L) >= a.den_groups;
 
@@ -222,18 +226,16 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   a.off_ylab = off; off += al16((long long)NP * 4);
   int fixed = off;
 
-  // staged marginals (backward): two frames each, stride FR+4 rounded to 4
+  // staged numerator marginals (backward): 3 frames of FR floats
   pl->dst = false;
   if (kind == 1) {
-    const long long frs = ((long long)a.FR + 4 + 3) & ~3LL;
-    const long long need = (do_den ? 2 * frs * 4 : 0) + (do_num ? 2 * frs * 4 : 0);
+    const long long need = do_num ? 3LL * a.FR * 4 : 0;
     const int ring_min = 4 * 1024 * 4;  // leave room for a few ring slots
     if (fixed + need + ring_min <= kLdsMax && env_int("LT_FORCE_DIRECT", 0) == 0) {
       pl->dst = true;
-      a.off_dbuf = fixed;
-      fixed += do_den ? al16(2 * frs * 4) : 0;
       a.off_nbuf = fixed;
-      fixed += do_num ? al16(2 * frs * 4) : 0;
+      a.off_dbuf = fixed;
+      fixed += al16(need);
     }
   }
 
