@@ -25,6 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from last_torch_amd import _native  # noqa: E402
+from last_torch_amd import sharding  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = 'lattice cells/s (B·T·U·|ctx|) at T=1000,U=100; 1/2/4/8-GPU scaling'
@@ -59,7 +60,10 @@ def make_inputs(B, T, U, V, C, device, seed, dtype=torch.float32):
 def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True):
   """Returns (wall seconds over `steps`, fwd kernel ms list, bwd kernel ms list)."""
   grad = torch.ones([W.shape[0]], dtype=torch.float32, device=W.device)
-  red = torch.zeros([1], dtype=torch.float32, device=W.device)
+  # stand-in weight-fn projection head (512 x 33 fp32, SURVEY 8e) so the
+  # step's one collective carries [loss sum || parameter grads]
+  head = torch.nn.Parameter(torch.zeros([512, 33], device=W.device))
+  head.grad = torch.zeros_like(head)
 
   def step(ev=None):
     if ev is not None:
@@ -71,8 +75,7 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True):
     if ev is not None:
       ev[2].record()
     if dist_on:
-      red.copy_(loss.sum().reshape(1))
-      torch.distributed.all_reduce(red)
+      sharding.all_reduce_step(loss, [head])
     return dW
 
   for _ in range(warmup):
@@ -143,7 +146,7 @@ def main():
   ap.add_argument('--labels', type=int, default=100)
   ap.add_argument('--vocab', type=int, default=32)
   ap.add_argument('--context', type=int, default=1)
-  ap.add_argument('--cpu-utts', type=int, default=int(os.environ.get('LT_BENCH_CPU_UTTS', 128)))
+  ap.add_argument('--cpu-utts', type=int, default=int(os.environ.get('LT_BENCH_CPU_UTTS', 512)))
   ap.add_argument('--no-north-star', action='store_true')
   ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'))
   args = ap.parse_args()

@@ -101,6 +101,10 @@ __global__ __launch_bounds__(256) void backtrace_kernel(const BtArgs a) {
 // ---------------------------------------------------------------------------
 thread_local std::string g_err = "ok";
 
+// Frame-indexed buffers ([B, T, ...]) may be null when T == 0 (an empty
+// tensor has no storage); the kernels never touch them then.
+#define LT_NEED(p) (!(p) && pb->max_frames > 0)
+
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -352,7 +356,7 @@ int lt_den_forward(const lt_problem* pb, int32_t semiring, const void* W,
   if (rc) return rc;
   if (semiring < 0 || semiring > 2) return fail(LT_EINVAL, "bad semiring");
   if (pb->batch == 0) return LT_OK;
-  if (!W || !num_frames || !dist) return fail(LT_EINVAL, "null pointer");
+  if (LT_NEED(W) || !num_frames || !dist) return fail(LT_EINVAL, "null pointer");
   if (misaligned(W)) return fail(LT_EINVAL, "W must be 16-byte aligned");
   lt_problem p2 = *pb;
   p2.max_labels = 0;
@@ -374,7 +378,7 @@ int lt_num_forward(const lt_problem* pb, int32_t semiring, const void* W,
   if (rc) return rc;
   if (semiring < 0 || semiring > 2) return fail(LT_EINVAL, "bad semiring");
   if (pb->batch == 0) return LT_OK;
-  if (!W || !num_frames || !num_labels || !num || (pb->max_labels > 0 && !labels))
+  if (LT_NEED(W) || !num_frames || !num_labels || !num || (pb->max_labels > 0 && !labels))
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W)) return fail(LT_EINVAL, "W must be 16-byte aligned");
   Plan pl;
@@ -397,7 +401,7 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   int rc = check_problem(pb, &g);
   if (rc) return rc;
   if (pb->batch == 0) return LT_OK;
-  if (!W || !num_frames || !num_labels || !loss || (pb->max_labels > 0 && !labels))
+  if (LT_NEED(W) || !num_frames || !num_labels || !loss || (pb->max_labels > 0 && !labels))
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W)) return fail(LT_EINVAL, "W must be 16-byte aligned");
   const int flags = F_NUM | F_LOSS | (local_norm ? F_LOCAL : F_DEN);
@@ -423,7 +427,8 @@ int lt_den_backward(const lt_problem* pb, const void* W, const int32_t* num_fram
   int rc = check_problem(pb, &g);
   if (rc) return rc;
   if (pb->batch == 0) return LT_OK;
-  if (!W || !num_frames || !log_z || !alpha || !dW) return fail(LT_EINVAL, "null pointer");
+  if (LT_NEED(W) || !num_frames || !log_z || LT_NEED(alpha) || LT_NEED(dW))
+    return fail(LT_EINVAL, "null pointer");
   if (misaligned(W) || misaligned(alpha)) return fail(LT_EINVAL, "W/alpha must be 16-byte aligned");
   lt_problem p2 = *pb;
   p2.max_labels = 0;
@@ -457,8 +462,8 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
   int rc = check_problem(pb, &g);
   if (rc) return rc;
   if (pb->batch == 0) return LT_OK;
-  if (!W || !num_frames || !num_labels || !num || !alpha_num || !dW ||
-      (pb->max_labels > 0 && !labels) || (!local_norm && (!log_z || !alpha)))
+  if (LT_NEED(W) || !num_frames || !num_labels || !num || LT_NEED(alpha_num) || LT_NEED(dW) ||
+      (pb->max_labels > 0 && !labels) || (!local_norm && (!log_z || LT_NEED(alpha))))
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W) || (alpha && misaligned(alpha)) || misaligned(alpha_num))
     return fail(LT_EINVAL, "W/alpha/alpha_num must be 16-byte aligned");
@@ -514,7 +519,7 @@ int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
   int rc = check_problem(pb, &g);
   if (rc) return rc;
   if (pb->batch == 0) return LT_OK;
-  if (!W || !num_frames || !labels || !path_weight || !workspace)
+  if (LT_NEED(W) || !num_frames || LT_NEED(labels) || !path_weight || !workspace)
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W)) return fail(LT_EINVAL, "W must be 16-byte aligned");
   if (g.K + 1 > 255) return fail(LT_EUNSUPPORTED, "vocab too large for 8-bit backpointers");

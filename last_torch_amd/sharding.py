@@ -1,0 +1,63 @@
+"""Utterance sharding for data-parallel lattice losses.
+
+Utterances are independent lattices, so the path shards with no data-path
+collective: each rank runs the HIP kernels on its own utterances, and dW
+stays utterance-local. The only exchange is one all-reduce(SUM) per step of
+a flat fp32 bucket [sum of losses || weight-fn parameter grads], which on
+ROCm is RCCL over xGMI (torch.distributed backend "nccl") and gloo on CPU.
+
+Partitioning is longest-processing-time (LPT) with equal utterance counts:
+utterances are visited longest first and each goes to the least-loaded rank
+that still has room, so every rank gets B/N (+-1) utterances and the
+frame totals are balanced against length stragglers.
+"""
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_utterances(num_frames: Sequence[int], world_size: int) -> list[np.ndarray]:
+  """Returns, per rank, the ascending utterance indices it owns."""
+  nf = np.asarray(num_frames, dtype=np.int64).reshape(-1)
+  if world_size < 1:
+    raise ValueError(f'world_size must be >= 1, got {world_size}')
+  B = nf.shape[0]
+  cap = [B // world_size + (1 if r < B % world_size else 0) for r in range(world_size)]
+  load = np.zeros(world_size, np.int64)
+  owned: list[list[int]] = [[] for _ in range(world_size)]
+  for i in np.argsort(-nf, kind='stable'):
+    open_ranks = [r for r in range(world_size) if len(owned[r]) < cap[r]]
+    r = min(open_ranks, key=lambda k: (load[k], len(owned[k]), k))
+    owned[r].append(int(i))
+    load[r] += nf[i]
+  return [np.asarray(sorted(o), dtype=np.int64) for o in owned]
+
+
+def local_shard(num_frames, rank: int, world_size: int) -> np.ndarray:
+  """Indices of the utterances `rank` owns (see shard_utterances)."""
+  nf = num_frames.detach().cpu().numpy() if torch.is_tensor(num_frames) else num_frames
+  return shard_utterances(nf, world_size)[rank]
+
+
+def all_reduce_step(loss: torch.Tensor, params: Iterable[torch.nn.Parameter] = (),
+                    group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+  """The step's single collective: all-reduce(SUM) of [loss.sum() || grads].
+
+  Parameter gradients are summed in place (callers that want the mean
+  divide by the global utterance count). Returns the global loss sum.
+  Without an initialised process group this is the identity.
+  """
+  grads = [p.grad for p in params if p.grad is not None]
+  total = loss.detach().sum().reshape(1).to(torch.float32)
+  if not (dist.is_available() and dist.is_initialized()):
+    return total[0]
+  flat = torch.cat([total] + [g.reshape(-1).to(torch.float32) for g in grads])
+  dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+  off = 1
+  for g in grads:
+    k = g.numel()
+    g.copy_(flat[off:off + k].view_as(g).to(g.dtype))
+    off += k
+  return flat[0]

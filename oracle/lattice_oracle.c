@@ -285,12 +285,14 @@ static double num_forward_one(const ngram_t* g, int T, int U, const float* W, in
     const float* w = W + (long long)t * C * R;
     for (int u = 0; u < NP; ++u) {
       const double wb = w[ctx[u] * R];
-      const double bt = semiring == ORC_REAL ? a[u] * wb : a[u] + wb;
+      double bt = semiring == ORC_REAL ? a[u] * wb : a[u] + wb;
       double lx = zero; /* shift_down: position 0 gets semiring zero */
       if (u >= 1) {
         const double wl = w[ctx[u - 1] * R + yn[u - 1]];
         lx = semiring == ORC_REAL ? a[u - 1] * wl : a[u - 1] + wl;
       }
+      /* MaxTropical runs in float like the reference (exact, same operand order). */
+      if (semiring == ORC_MAX) { bt = (float)bt; lx = (float)lx; }
       if (semiring == ORC_REAL) na[u] = bt + lx;
       else if (semiring == ORC_MAX) na[u] = (bt >= lx) ? bt : lx;
       else na[u] = d_logaddexp(bt, lx);

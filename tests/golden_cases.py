@@ -1,0 +1,67 @@
+"""Loader for the golden fixtures written by tests/golden/make_golden.py."""
+import glob
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+LATTICE_CASES = sorted(
+    os.path.basename(p)[len('lattice_'):-len('.npz')]
+    for p in glob.glob(os.path.join(GOLDEN, 'lattice_*.npz')))
+SEMIRINGS = ('Log', 'MaxTropical', 'Real')
+
+
+def load(name):
+  with np.load(os.path.join(GOLDEN, f'lattice_{name}.npz')) as d:
+    c = {k: d[k] for k in d.files}
+  c['V'] = int(c.pop('vocab_size'))
+  c['n'] = int(c.pop('context_size'))
+  c['bf16'] = bool(c['bf16'])
+  return c
+
+
+def load_npz(stem):
+  with np.load(os.path.join(GOLDEN, f'{stem}.npz')) as d:
+    return {k: d[k] for k in d.files}
+
+
+def loss_tol(ref):
+  """|got - ref| <= 1e-4 * max(1, |ref|) (BASELINE north_star tolerance)."""
+  return 1e-4 * np.maximum(1.0, np.abs(ref))
+
+
+def assert_loss_close(got, ref):
+  got = np.asarray(got, np.float64)
+  ref = np.asarray(ref, np.float64)
+  fin = np.isfinite(ref)
+  np.testing.assert_array_equal(np.isfinite(got), fin)
+  np.testing.assert_array_equal(got[~fin], ref[~fin])
+  err = np.abs(got[fin] - ref[fin])
+  assert (err <= loss_tol(ref[fin])).all(), (got, ref, err)
+
+
+def assert_values_close(got, ref, rtol=1e-5, atol=1e-5):
+  got = np.asarray(got, np.float64)
+  ref = np.asarray(ref, np.float64)
+  np.testing.assert_array_equal(np.isneginf(got), np.isneginf(ref))
+  np.testing.assert_array_equal(np.isposinf(got), np.isposinf(ref))
+  fin = np.isfinite(ref)
+  np.testing.assert_allclose(got[fin], ref[fin], rtol=rtol, atol=atol)
+
+
+def assert_grad_close(got, ref, log_z, bf16=False):
+  """Arc-marginal gradients: per utterance b,
+  |got - ref| <= 1e-5 + 1e-6 * max(1, |log_z_b|) (+ 8e-3 relative for bf16 dW).
+  The fp32 log-space arguments alpha + w + beta - log_z are sums of terms
+  of magnitude ~|log_z|, each rounded at |log_z| * 2^-24, so a marginal near
+  1 carries an absolute error proportional to |log_z| (the reference, which
+  runs in fp32, carries the same); the float64 fixtures are exact."""
+  got = np.asarray(got, np.float64)
+  ref = np.asarray(ref, np.float64)
+  lz = np.abs(np.where(np.isfinite(log_z), log_z, 0.0)).astype(np.float64)
+  atol = 1e-5 + 1e-6 * np.maximum(1.0, lz)
+  tol = atol.reshape([-1] + [1] * (ref.ndim - 1)) + (8e-3 if bf16 else 1e-4) * np.abs(ref)
+  err = np.abs(got - ref)
+  bad = err > tol
+  assert not bad.any(), (f'{int(bad.sum())} of {bad.size} beyond tolerance; '
+                         f'max err {float(err.max()):.3g} at {np.argwhere(bad)[0].tolist()}')

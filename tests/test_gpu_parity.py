@@ -1,0 +1,360 @@
+"""GPU parity: the HIP kernels (through the C ABI and through the
+RecognitionLattice plugin API) against the reference's golden fixtures and
+the pinned C oracle.
+
+Tolerances (BASELINE.json north_star):
+  * Log loss / log_z / numerator: |got - ref| <= 1e-4 * max(1, |ref|);
+    alpha histories rtol 1e-4, atol 1e-4.
+  * dW (arc marginals, in [0, 1] per arc): per utterance
+    1e-5 + 1e-6 * max(1, |log_z|) absolute + 1e-4 relative (bf16 dW: 8e-3
+    relative, about one bf16 ulp); see golden_cases.assert_grad_close.
+  * MaxTropical distances, alpha histories and Viterbi labels/path weights:
+    bit-exact (same fp32 adds, same tie rules).
+"""
+import numpy as np
+import pytest
+import torch
+
+import last_torch_amd as lt
+from last_torch_amd import _native as nat
+from golden_cases import (LATTICE_CASES, assert_grad_close, assert_loss_close, assert_values_close,
+                          load)
+
+pytestmark = pytest.mark.gpu
+
+SID = {'Log': nat.SEMIRING_LOG, 'MaxTropical': nat.SEMIRING_MAX, 'Real': nat.SEMIRING_REAL}
+
+
+def _orc():
+  from oracle import oracle as orc  # test infrastructure only
+  return orc
+
+
+def _dev(c, cuda, key='W'):
+  dt = torch.bfloat16 if c['bf16'] else torch.float32
+  W = torch.tensor(c[key]).to(dt).to(cuda)
+  nf = torch.tensor(c['num_frames']).to(cuda)
+  lab = torch.tensor(c['labels']).to(cuda)
+  nl = torch.tensor(c['num_labels']).to(cuda)
+  return W, nf, lab, nl
+
+
+# ---------------------------------------------------------------------------
+# golden fixtures (reference outputs) through the C ABI
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize('case', LATTICE_CASES)
+@pytest.mark.parametrize('semiring', ['Log', 'MaxTropical', 'Real'])
+def test_golden_den_forward(cuda, case, semiring):
+  c = load(case)
+  W, nf, _, _ = _dev(c, cuda)
+  d, a = nat.den_forward(W, nf, c['V'], c['n'], SID[semiring])
+  d, a = d.cpu().numpy(), a.cpu().numpy()
+  if semiring == 'MaxTropical':
+    np.testing.assert_array_equal(d, c['den_MaxTropical'])
+    np.testing.assert_array_equal(a, c['alpha_MaxTropical'])
+  elif semiring == 'Log':
+    assert_loss_close(d, c['den_Log'])
+    assert_values_close(a, c['alpha_Log'], rtol=1e-4, atol=1e-4)
+  else:
+    ref = c['den_Real']
+    scale = max(1.0, float(np.abs(ref).max()))
+    assert_values_close(d, ref, rtol=1e-4, atol=1e-5 * scale)
+
+
+@pytest.mark.parametrize('case', LATTICE_CASES)
+@pytest.mark.parametrize('semiring', ['Log', 'MaxTropical', 'Real'])
+def test_golden_num_forward(cuda, case, semiring):
+  c = load(case)
+  W, nf, lab, nl = _dev(c, cuda)
+  num, _ = nat.num_forward(W, nf, lab, nl, c['V'], c['n'], SID[semiring])
+  num = num.cpu().numpy()
+  ref = c[f'num_{semiring}']
+  if semiring == 'MaxTropical':
+    np.testing.assert_array_equal(num, ref)
+  elif semiring == 'Log':
+    assert_loss_close(num, ref)
+  else:
+    scale = max(1.0, float(np.abs(ref).max()))
+    assert_values_close(num, ref, rtol=1e-4, atol=1e-5 * scale)
+
+
+@pytest.mark.parametrize('case', LATTICE_CASES)
+@pytest.mark.parametrize('local', [False, True])
+def test_golden_loss_and_grad(cuda, case, local):
+  c = load(case)
+  W, nf, lab, nl = _dev(c, cuda, 'W_local' if local else 'W')
+  loss, lz, num, al, an = nat.loss_forward(W, nf, lab, nl, c['V'], c['n'], local)
+  dW = nat.loss_backward(W, nf, lab, nl, lz, num, al, an, None, c['V'], c['n'], local)
+  torch.cuda.synchronize()
+  assert_loss_close(loss.cpu().numpy(), c['loss_local' if local else 'loss'])
+  if not local:
+    assert_loss_close(lz.cpu().numpy(), c['den_Log'])
+  ref = c['loss_local_grad' if local else 'loss_grad']
+  assert_grad_close(dW.float().cpu().numpy(), ref, c['den_Log'], c['bf16'])
+
+
+@pytest.mark.parametrize('case', LATTICE_CASES)
+def test_golden_den_grad(cuda, case):
+  c = load(case)
+  W, nf, _, _ = _dev(c, cuda)
+  lz, al = nat.den_forward(W, nf, c['V'], c['n'], nat.SEMIRING_LOG)
+  dW = nat.den_backward(W, nf, lz, al, None, c['V'], c['n'])
+  assert_grad_close(dW.float().cpu().numpy(), c['den_grad'], c['den_Log'], c['bf16'])
+
+
+@pytest.mark.parametrize('case', LATTICE_CASES)
+@pytest.mark.parametrize('convention', ['reference', 'true'])
+def test_golden_viterbi_bit_exact(cuda, case, convention):
+  c = load(case)
+  W, nf, _, _ = _dev(c, cuda)
+  conv = nat.LABELS_REFERENCE if convention == 'reference' else nat.LABELS_TRUE
+  labels, weights, _ = nat.viterbi(W, nf, c['V'], c['n'], conv)
+  np.testing.assert_array_equal(labels.cpu().numpy(), c[f'vit_labels_{convention}'])
+  np.testing.assert_array_equal(weights.cpu().numpy(), c['vit_weights'])
+
+
+# ---------------------------------------------------------------------------
+# golden fixtures through the plugin API (RecognitionLattice + TableWeightFn)
+# ---------------------------------------------------------------------------
+def _table_lattice(c, table):
+  return lt.RecognitionLattice(
+      context=lt.contexts.FullNGram(vocab_size=c['V'], context_size=c['n']),
+      alignment=lt.alignments.FrameDependent(),
+      weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+      weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(table))
+
+
+def _frames(B, T):
+  return torch.arange(T, dtype=torch.float32)[None, :, None].expand(B, T, 1).contiguous()
+
+
+@pytest.mark.parametrize('case', [k for k in LATTICE_CASES if not k.startswith('bf16')])
+def test_golden_recognition_lattice_api(cuda, case):
+  c = load(case)
+  B, T = c['W'].shape[:2]
+  table = torch.tensor(c['W'], device=cuda, requires_grad=True)
+  lat = _table_lattice(c, table)
+  frames = _frames(B, T).to(cuda)
+  nf = torch.tensor(c['num_frames'], dtype=torch.float32)  # float lengths, as the reference tests
+  labels = torch.tensor(c['labels'], dtype=torch.float32)
+  nl = torch.tensor(c['num_labels'], dtype=torch.float32)
+  loss = lat(frames, nf, labels, nl)
+  assert_loss_close(loss.detach().cpu().numpy(), c['loss'])
+  fin = torch.isfinite(loss)
+  loss.masked_fill(~fin, 0).sum().backward()
+  assert_grad_close(table.grad.cpu().numpy(), c['loss_grad'], c['den_Log'])
+  for sname in ('Log', 'MaxTropical'):
+    d, a = lat._forward(None, frames, nf, getattr(lt.semirings, sname))
+    if sname == 'MaxTropical':
+      np.testing.assert_array_equal(d.detach().cpu().numpy(), c['den_MaxTropical'])
+      np.testing.assert_array_equal(a.detach().cpu().numpy(), c['alpha_MaxTropical'])
+    else:
+      assert_loss_close(d.detach().cpu().numpy(), c['den_Log'])
+    s = lat._string_forward(None, frames, nf, labels, nl, getattr(lt.semirings, sname))
+    if sname == 'MaxTropical':
+      np.testing.assert_array_equal(s.detach().cpu().numpy(), c['num_MaxTropical'])
+    else:
+      assert_loss_close(s.detach().cpu().numpy(), c['num_Log'])
+  for conv in ('reference', 'true'):
+    al, nal, pw = lat.shortest_path(frames, nf, label_convention=conv)
+    np.testing.assert_array_equal(al.cpu().numpy(), c[f'vit_labels_{conv}'])
+    np.testing.assert_array_equal(pw.cpu().numpy(), c['vit_weights'])
+    np.testing.assert_array_equal(nal.cpu().numpy(), c['num_frames'])
+
+
+def test_locally_normalised_weight_fn_api(cuda):
+  """LocallyNormalizedWeightFn(hat_normalize) switches the loss to -numerator
+  (lattices.py:178-179); its gradient flows back through the normaliser."""
+  c = load('locally_normalised')
+  B, T = c['W'].shape[:2]
+  table = torch.tensor(c['W'], device=cuda, requires_grad=True)
+  lat = lt.RecognitionLattice(
+      context=lt.contexts.FullNGram(vocab_size=c['V'], context_size=c['n']),
+      alignment=lt.alignments.FrameDependent(),
+      weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+      weight_fn_factory=lambda _: lt.weight_fns.LocallyNormalizedWeightFn(
+          lt.weight_fns.TableWeightFn(table)))
+  frames = _frames(B, T).to(cuda)
+  loss = lat(frames, torch.tensor(c['num_frames']), torch.tensor(c['labels']),
+             torch.tensor(c['num_labels']))
+  assert_loss_close(loss.detach().cpu().numpy(), c['loss_local'])
+  loss.sum().backward()
+  # chain rule through hat_normalize, in float64 on the CPU
+  Wl = torch.tensor(c['W'], dtype=torch.float64, requires_grad=True)
+  hb, hl = lt.weight_fns.hat_normalize(Wl[..., 0], Wl[..., 1:])
+  Wn = torch.cat([hb[..., None], hl], dim=-1)
+  (Wn * torch.tensor(c['loss_local_grad'], dtype=torch.float64)).sum().backward()
+  np.testing.assert_allclose(table.grad.cpu().numpy(), Wl.grad.numpy(), atol=1e-5, rtol=1e-4)
+
+
+# ---------------------------------------------------------------------------
+# random problems against the oracle (sizes the oracle finishes in seconds)
+# ---------------------------------------------------------------------------
+RANDOM = [
+    # B, T, U, V, n, dtype
+    (8, 200, 30, 32, 1, 'f32'),
+    (8, 200, 30, 32, 1, 'bf16'),
+    (4, 64, 12, 8, 2, 'f32'),
+    (3, 40, 10, 16, 2, 'bf16'),
+    (2, 30, 8, 32, 2, 'bf16'),   # cfg5 shape class: trigram V=32 (C=1057), bf16
+    (2, 30, 8, 32, 2, 'f32'),    # trigram fp32: the wide-frame direct path
+    (6, 120, 20, 32, 0, 'f32'),
+    (4, 100, 20, 64, 1, 'f32'),
+    (5, 90, 15, 3, 3, 'f32'),
+    (1, 1, 1, 5, 1, 'f32'),
+]
+
+
+def _random_problem(B, T, U, V, n, seed):
+  orc = _orc()
+  rng = np.random.default_rng(seed)
+  C = orc.num_states(V, n)
+  W = rng.standard_normal((B, T, C, V + 1)).astype(np.float32)
+  nf = rng.integers(0, T + 1, B).astype(np.int32)
+  nf[0] = T
+  lab = rng.integers(0, V + 1, (B, U)).astype(np.int32)  # includes epsilon (0) labels
+  nl = rng.integers(0, U + 1, B).astype(np.int32)
+  nl[0] = min(U, T)
+  return W, nf, lab, nl
+
+
+@pytest.mark.parametrize('B,T,U,V,n,dt', RANDOM)
+def test_random_vs_oracle(cuda, B, T, U, V, n, dt):
+  orc = _orc()
+  W, nf, lab, nl = _random_problem(B, T, U, V, n, seed=B * 1000 + T + V + n)
+  bf16 = dt == 'bf16'
+  if bf16:
+    W = torch.tensor(W).bfloat16().float().numpy()
+  Wd = torch.tensor(W).to(torch.bfloat16 if bf16 else torch.float32).to(cuda)
+  nfd, labd, nld = (torch.tensor(x).to(cuda) for x in (nf, lab, nl))
+  loss, lz, num, al, an = nat.loss_forward(Wd, nfd, labd, nld, V, n, False)
+  dW = nat.loss_backward(Wd, nfd, labd, nld, lz, num, al, an, None, V, n, False)
+  rl, rlz, rnum, rdW = orc.loss_grad(W, nf, lab, nl, V, n)
+  assert_loss_close(loss.cpu().numpy(), rl)
+  assert_loss_close(lz.cpu().numpy(), rlz)
+  assert_grad_close(dW.float().cpu().numpy(), rdW, rlz, bf16)
+  for conv in (nat.LABELS_REFERENCE, nat.LABELS_TRUE):
+    labels, weights, arcs = nat.viterbi(Wd, nfd, V, n, conv, want_arcs=True)
+    rlab, rw, rarcs = orc.viterbi(W, nf, V, n, convention=conv, want_arcs=True)
+    np.testing.assert_array_equal(labels.cpu().numpy(), rlab)
+    np.testing.assert_array_equal(weights.cpu().numpy(), rw)
+    np.testing.assert_array_equal(arcs.float().cpu().numpy(), rarcs)
+  d, a = nat.den_forward(Wd, nfd, V, n, nat.SEMIRING_MAX)
+  rd, ra = orc.den_forward(W, nf, V, n, orc.MAX)
+  np.testing.assert_array_equal(d.cpu().numpy(), rd)
+  np.testing.assert_array_equal(a.cpu().numpy(), ra)
+
+
+def test_edge_cases(cuda):
+  """Empty utterances, T=0 and U=0, unreachable label strings (+inf loss,
+  zero gradient), lengths beyond max (clamped), labels all epsilon."""
+  orc = _orc()
+  V, n, T, U = 4, 1, 6, 5
+  C = orc.num_states(V, n)
+  rng = np.random.default_rng(11)
+  W = rng.standard_normal((6, T, C, V + 1)).astype(np.float32)
+  nf = np.array([0, 6, 2, 6, 9, 3], np.int32)           # 9 > T is clamped
+  nl = np.array([0, 5, 4, 0, 2, 3], np.int32)           # utt 2: 4 labels in 2 frames
+  lab = rng.integers(1, V + 1, (6, U)).astype(np.int32)
+  lab[5] = 0                                              # all-epsilon string
+  Wd = torch.tensor(W, device=cuda)
+  nfd, labd, nld = (torch.tensor(x, device=cuda) for x in (nf, lab, nl))
+  loss, lz, num, al, an = nat.loss_forward(Wd, nfd, labd, nld, V, n, False)
+  dW = nat.loss_backward(Wd, nfd, labd, nld, lz, num, al, an, None, V, n, False)
+  rl, _, _, rdW = orc.loss_grad(W, nf, lab, nl, V, n)
+  l = loss.cpu().numpy()
+  assert l[0] == 0.0                                      # T=0, U=0 -> 0 (lattices_test.py:286)
+  assert np.isposinf(l[2]) and np.isposinf(rl[2])        # unreachable -> +inf
+  assert (dW[2] == 0).all()
+  assert_loss_close(l, rl)
+  assert_grad_close(dW.cpu().numpy(), rdW, lz.cpu().numpy())
+  # T = 0 for the whole batch
+  W0 = torch.zeros([3, 0, C, V + 1], device=cuda)
+  z = torch.zeros([3], dtype=torch.int32, device=cuda)
+  d0, _ = nat.den_forward(W0, z, V, n, nat.SEMIRING_LOG)
+  np.testing.assert_array_equal(d0.cpu().numpy(), [0., 0., 0.])
+  lab0, w0, _ = nat.viterbi(W0, z, V, n, nat.LABELS_TRUE)
+  assert lab0.shape == (3, 0) and (w0.cpu().numpy() == 0).all()
+
+
+# ---------------------------------------------------------------------------
+# BASELINE sizes: size-independent properties + an oracle spot check
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope='module')
+def full_size(cuda):
+  B, T, U, V, n = 64, 1000, 100, 32, 1
+  g = torch.Generator(device=cuda)
+  g.manual_seed(0)
+  C = nat.num_context_states(V, n)
+  W = torch.randn([B, T, C, V + 1], generator=g, device=cuda)
+  nf = torch.randint(T // 2, T + 1, [B], generator=g, device=cuda, dtype=torch.int32)
+  nf[0] = T
+  lab = torch.randint(1, V + 1, [B, U], generator=g, device=cuda, dtype=torch.int32)
+  nl = torch.full([B], U, dtype=torch.int32, device=cuda)
+  return W, nf, lab, nl, V, n
+
+
+def test_full_size_marginals_sum_to_one(full_size):
+  W, nf, _, _, V, n = full_size
+  lz, al = nat.den_forward(W, nf, V, n, nat.SEMIRING_LOG)
+  dW = nat.den_backward(W, nf, lz, al, None, V, n)
+  s = dW.double().reshape(W.shape[0], W.shape[1], -1).sum(-1)
+  live = (torch.arange(W.shape[1], device=W.device)[None, :] < nf[:, None].long()).double()
+  # fp32 log-space rounding scales with |log_z| (~4e3 here); see assert_grad_close
+  tol = 1e-5 + 1e-6 * lz.abs().double().clamp(min=1.0)[:, None]
+  assert ((s - live).abs() <= tol).all(), float(((s - live).abs() / tol).max())
+
+
+def test_full_size_loss_properties_and_determinism(full_size):
+  W, nf, lab, nl, V, n = full_size
+  out1 = nat.loss_forward(W, nf, lab, nl, V, n, False)
+  dW1 = nat.loss_backward(W, nf, lab, nl, *out1[1:], None, V, n, False)
+  out2 = nat.loss_forward(W, nf, lab, nl, V, n, False)
+  dW2 = nat.loss_backward(W, nf, lab, nl, *out2[1:], None, V, n, False)
+  assert torch.equal(out1[0], out2[0])  # the loss is bitwise reproducible
+  # dW: numerator marginals of positions sharing an arc meet in LDS float
+  # atomics, so their summation order (last bits) may vary run to run
+  assert torch.allclose(dW1, dW2, atol=1e-6, rtol=0)
+  loss = out1[0]
+  assert torch.isfinite(loss).all() and (loss > -1e-3).all()    # log_z >= numerator
+  # linearity in the incoming gradient
+  g = torch.linspace(0.5, 2.0, W.shape[0], device=W.device)
+  dWg = nat.loss_backward(W, nf, lab, nl, *out1[1:], g, V, n, False)
+  assert torch.allclose(dWg, dW1 * g[:, None, None, None], atol=1e-6, rtol=1e-5)
+  # each live frame: den marginals sum to 1 and num marginals sum to 1
+  s = dW1.double().reshape(W.shape[0], W.shape[1], -1).sum(-1)
+  tol = 1e-5 + 2e-6 * out1[1].abs().double().clamp(min=1.0)[:, None]
+  assert (s.abs() <= tol).all(), float((s.abs() / tol).max())
+
+
+def test_full_size_oracle_spot_check(full_size):
+  """Two full-length utterances of the BASELINE workload against the oracle."""
+  orc = _orc()
+  W, nf, lab, nl, V, n = full_size
+  idx = [0, 7]
+  loss, lz, num, al, an = nat.loss_forward(W, nf, lab, nl, V, n, False)
+  dW = nat.loss_backward(W, nf, lab, nl, lz, num, al, an, None, V, n, False)
+  Wc = W[idx].cpu().numpy()
+  rl, rlz, _, rdW = orc.loss_grad(Wc, nf[idx].cpu().numpy(), lab[idx].cpu().numpy(),
+                                  nl[idx].cpu().numpy(), V, n)
+  assert_loss_close(loss[idx].cpu().numpy(), rl)
+  assert_grad_close(dW[idx].cpu().numpy(), rdW, rlz)
+
+
+def test_full_size_viterbi_properties(full_size):
+  """cfg4-class decode: the path weight is the MaxTropical distance, the
+  one-hot arcs re-sum to it, and labels match the oracle on a sample."""
+  orc = _orc()
+  W, nf, _, _, V, n = full_size
+  labels, weights, arcs = nat.viterbi(W, nf, V, n, nat.LABELS_TRUE, want_arcs=True)
+  d, _ = nat.den_forward(W, nf, V, n, nat.SEMIRING_MAX, want_alpha=False)
+  assert torch.equal(weights, d)
+  resum = (arcs.double() * W.double()).sum(dim=(1, 2, 3))
+  assert torch.allclose(resum, weights.double(), atol=1e-3, rtol=1e-6)
+  per_frame = arcs.reshape(W.shape[0], W.shape[1], -1).sum(-1)
+  live = (torch.arange(W.shape[1], device=W.device)[None, :] < nf[:, None].long()).float()
+  assert torch.equal(per_frame.float(), live)
+  idx = [0, 5]
+  rlab, rw, _ = orc.viterbi(W[idx].cpu().numpy(), nf[idx].cpu().numpy(), V, n, convention=0)
+  np.testing.assert_array_equal(labels[idx].cpu().numpy(), rlab)
+  np.testing.assert_array_equal(weights[idx].cpu().numpy(), rw)

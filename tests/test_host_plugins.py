@@ -1,0 +1,154 @@
+"""Host-side plugin surface (contexts / semirings / alignments / lattice
+validation) against the reference's golden tables. CPU only: these are the
+PyTorch-level mirrors of contexts.py, semirings.py and alignments.py that the
+HIP path plugs in behind; none of them touch the GPU."""
+import numpy as np
+import pytest
+import torch
+
+import last_torch_amd as lt
+from golden_cases import load_npz
+
+CTX_CONFIGS = [(3, 0), (3, 1), (3, 2), (2, 3), (5, 1), (4, 2)]
+SEMIRING_NAMES = ('Log', 'MaxTropical', 'Real')
+
+
+@pytest.fixture(scope='module')
+def ctx_tables():
+  return load_npz('contexts')
+
+
+@pytest.fixture(scope='module')
+def sr_tables():
+  return load_npz('semirings')
+
+
+@pytest.mark.parametrize('V,n', CTX_CONFIGS)
+def test_fullngram_next_state(ctx_tables, V, n):
+  ctx = lt.contexts.FullNGram(vocab_size=V, context_size=n)
+  C, vocab = ctx.shape()
+  assert vocab == V and C == ctx_tables[f'next_{V}_{n}'].shape[0]
+  st = torch.arange(C)[:, None].expand(C, V + 1)
+  y = torch.arange(V + 1)[None, :].expand(C, V + 1)
+  np.testing.assert_array_equal(ctx.next_state(st, y).numpy(), ctx_tables[f'next_{V}_{n}'])
+  # the dense table the kernels' arithmetic restates
+  np.testing.assert_array_equal(ctx.next_state_table().numpy(), ctx_tables[f'next_{V}_{n}'][:, 1:])
+
+
+@pytest.mark.parametrize('V,n', CTX_CONFIGS)
+@pytest.mark.parametrize('semiring', SEMIRING_NAMES)
+def test_fullngram_forward_reduce(ctx_tables, V, n, semiring):
+  ctx = lt.contexts.FullNGram(vocab_size=V, context_size=n)
+  x = torch.tensor(ctx_tables[f'reduce_in_{V}_{n}'])
+  got = ctx.forward_reduce(x, getattr(lt.semirings, semiring)).numpy()
+  ref = ctx_tables[f'reduce_{semiring}_{V}_{n}']
+  if semiring == 'MaxTropical':
+    np.testing.assert_array_equal(got, ref)
+  else:
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize('V,n', CTX_CONFIGS)
+def test_fullngram_backward_broadcast_and_walk(ctx_tables, V, n):
+  ctx = lt.contexts.FullNGram(vocab_size=V, context_size=n)
+  b = torch.tensor(ctx_tables[f'bcast_in_{V}_{n}'])
+  np.testing.assert_array_equal(ctx.backward_broadcast(b).numpy(), ctx_tables[f'bcast_{V}_{n}'])
+  labs = torch.tensor(ctx_tables[f'walk_in_{V}_{n}']).long()
+  np.testing.assert_array_equal(ctx.walk_states(labs).numpy(), ctx_tables[f'walk_{V}_{n}'])
+
+
+@pytest.mark.parametrize('semiring', SEMIRING_NAMES)
+def test_semiring_ops(sr_tables, semiring):
+  s = getattr(lt.semirings, semiring)
+  x, y = torch.tensor(sr_tables['x']), torch.tensor(sr_tables['y'])
+  for op, got in [('plus', s.plus(x, y)), ('times', s.times(x, y)), ('sum', s.sum(x, dim=-1)),
+                  ('prod', s.prod(x, dim=-1)), ('zeros', s.zeros([2])), ('ones', s.ones([2]))]:
+    np.testing.assert_allclose(got.numpy(), sr_tables[f'{op}_{semiring}'], rtol=1e-6,
+                               err_msg=f'{semiring}.{op}')
+
+
+def test_log_semiring_autograd_is_sound():
+  """The build's Log.plus/sum carry working gradients (reference D1/D2)."""
+  x = torch.tensor([1., 2., 3.], requires_grad=True)
+  lt.semirings.Log.sum(x, dim=-1).backward()
+  np.testing.assert_allclose(x.grad.numpy(), torch.softmax(x.detach(), -1).numpy(), rtol=1e-6)
+  a = torch.tensor([0.5, -np.inf], requires_grad=True)
+  b = torch.tensor([1.5, -np.inf], requires_grad=True)
+  lt.semirings.Log.plus(a, b).sum().backward()
+  assert torch.isfinite(a.grad).all() and torch.isfinite(b.grad).all()
+  np.testing.assert_allclose((a.grad + b.grad)[0].item(), 1.0, rtol=1e-6)
+
+
+def test_max_tropical_tie_rules():
+  """Maximum picks `a` on ties (semirings.py:363); Max the first argmax (:382)."""
+  a = torch.tensor([1., 2.], requires_grad=True)
+  b = torch.tensor([1., 3.], requires_grad=True)
+  lt.semirings.MaxTropical.plus(a, b).sum().backward()
+  np.testing.assert_array_equal(a.grad.numpy(), [1., 0.])
+  np.testing.assert_array_equal(b.grad.numpy(), [0., 1.])
+  x = torch.tensor([2., 5., 5., 1.], requires_grad=True)
+  lt.semirings.MaxTropical.sum(x, dim=-1).backward()
+  np.testing.assert_array_equal(x.grad.numpy(), [0., 1., 0., 0.])
+
+
+def test_frame_dependent_closed_forms():
+  """FrameDependent topology and step functions (alignments.py:250-329;
+  tests/alignments_test.py:49-207 closed forms)."""
+  fd = lt.alignments.FrameDependent()
+  assert fd.num_states() == 1 and fd.start() == 0
+  assert fd.blank_next(0) == 0 and fd.lexical_next(0) == 0
+  assert fd.topological_visit() == [0]
+  ctx = lt.contexts.FullNGram(vocab_size=2, context_size=1)
+  alpha = torch.tensor([0., 1., 2.])
+  blank = torch.tensor([3., 4., 5.])
+  lexical = torch.tensor([[6., 7.], [8., 9.], [10., 11.]])
+  r = fd.forward(alpha, [blank], [lexical], ctx, lt.semirings.Real)
+  # dest 0 only blank; dest y gathers all sources' label-y arcs
+  np.testing.assert_allclose(r.numpy(), [0 * 3, 1 * 4 + (0 * 6 + 1 * 8 + 2 * 10),
+                                         2 * 5 + (0 * 7 + 1 * 9 + 2 * 11)])
+  sf = fd.string_forward(torch.tensor([1., 2., 3.]), [torch.tensor([4., 5., 6.])],
+                         [torch.tensor([7., 8., 9.])], lt.semirings.Real)
+  np.testing.assert_allclose(sf.numpy(), [4., 2 * 5 + 7, 3 * 6 + 2 * 8])
+  with pytest.raises(ValueError):
+    fd.forward(alpha, [blank, blank], [lexical], ctx, lt.semirings.Real)
+
+
+def test_lattice_validates_batch_dims():
+  """RecognitionLattice.forward's shape checks (lattices.py:157-166) fire
+  before any device work, with the reference's messages."""
+  table = torch.zeros([4, 6, 3, 3])
+  lat = lt.RecognitionLattice(
+      context=lt.contexts.FullNGram(vocab_size=2, context_size=1),
+      alignment=lt.alignments.FrameDependent(),
+      weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+      weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(table))
+  frames = torch.zeros([4, 6, 1])
+  nf = torch.tensor([6, 3, 2, 1])
+  labels = torch.ones([4, 4])
+  nl = torch.tensor([4, 3, 1, 2])
+  with pytest.raises(ValueError, match='frames and num_frames have different batch_dims'):
+    lat(frames[:1], nf, labels, nl)
+  with pytest.raises(ValueError, match='labels and num_frames have different batch_dims'):
+    lat(frames, nf, labels[:1], nl)
+  with pytest.raises(ValueError, match='num_labels and num_frames have different batch_dims'):
+    lat(frames, nf, labels, nl[:1])
+  with pytest.raises(ValueError, match='frames and num_frames have different batch_dims'):
+    lat.shortest_path(frames[:1], nf)
+
+
+def test_lattice_without_gpu_fails_loudly():
+  """The product path has no CPU fallback: without a ROCm device the
+  lattice raises instead of computing anything."""
+  if torch.cuda.is_available():
+    pytest.skip('GPU present')
+  table = torch.zeros([2, 3, 3, 3])
+  lat = lt.RecognitionLattice(
+      context=lt.contexts.FullNGram(vocab_size=2, context_size=1),
+      alignment=lt.alignments.FrameDependent(),
+      weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+      weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(table))
+  frames = torch.arange(3.)[None, :, None].expand(2, 3, 1)
+  with pytest.raises(Exception):
+    lat(frames, torch.tensor([3, 2]), torch.ones([2, 2]), torch.tensor([1, 1]))
+  with pytest.raises(Exception):
+    lat.shortest_path(frames, torch.tensor([3, 2]))

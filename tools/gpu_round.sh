@@ -1,0 +1,59 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, kernel-trace profile, PMC passes.
+# Every GPU step has its own time limit; the first failure ends the script.
+# Usage (from the repo root on the box): bash tools/gpu_round.sh [round-tag] [steps...]
+set -euo pipefail
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-"test bench prof pmc"}
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+for s in $STEPS; do
+  case $s in
+    test)
+      echo "[gpu_round] pytest -m gpu"
+      timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 \
+        || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
+      tail -3 "$OUT/pytest_gpu.log"
+      ;;
+    smoke)
+      echo "[gpu_round] smoke"
+      timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > "$OUT/smoke.log" 2>&1 \
+        || { tail -40 "$OUT/smoke.log"; exit 1; }
+      tail -2 "$OUT/smoke.log"
+      ;;
+    bench)
+      echo "[gpu_round] bench"
+      timeout -k 10 600 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err" \
+        || { tail -40 "$OUT/bench_$TAG.err"; exit 1; }
+      cat "$OUT/bench_$TAG.json"
+      ;;
+    prof)
+      echo "[gpu_round] rocprofv3 kernel trace"
+      rm -rf "$OUT/prof_$TAG"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o "$TAG" \
+        --output-format csv -- python3 bench.py --steps 20 --warmup 3 --cpu-utts 0 \
+        > "$OUT/prof_$TAG.log" 2>&1 || { tail -40 "$OUT/prof_$TAG.log"; exit 1; }
+      find "$OUT/prof_$TAG" -name '*kernel_stats.csv' -exec cat {} \;
+      ;;
+    pmc)
+      echo "[gpu_round] PMC passes"
+      rm -rf "$OUT/pmc_fetch_$TAG" "$OUT/pmc_write_$TAG"
+      timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$TAG" -o fetch \
+        --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-utts 0 \
+        --no-north-star > "$OUT/pmc_fetch_$TAG.log" 2>&1 \
+        || { tail -40 "$OUT/pmc_fetch_$TAG.log"; exit 1; }
+      timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$TAG" -o write \
+        --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-utts 0 \
+        --no-north-star > "$OUT/pmc_write_$TAG.log" 2>&1 \
+        || { tail -40 "$OUT/pmc_write_$TAG.log"; exit 1; }
+      python tools/pmc_summary.py --fetch "$OUT/pmc_fetch_$TAG" --write "$OUT/pmc_write_$TAG" \
+        --batch 64 --frames 1000 --out "$OUT/${TAG}_pmc_summary.json"
+      ;;
+    *)
+      echo "unknown step $s"; exit 2;;
+  esac
+done
+echo "[gpu_round] done"
