@@ -31,20 +31,32 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = 'lattice cells/s (B·T·U·|ctx|) at T=1000,U=100; 1/2/4/8-GPU scaling'
 
 
-def algorithmic_bytes(T, U, V, C, es=4):
-  """Per-frame algorithmic HBM bytes, split per kernel.
+def algorithmic_bytes(T, U, V, C, es=4, checkpoints=True):
+  """Per-frame HBM bytes each kernel must move.
 
-  forward : W read once (C*(V+1)*es) + den alpha checkpoint write (4C)
-            + numerator gathers (2(U+1)*es) + numerator alpha write (4(U+1))
-  backward: W read + dW write (2*C*(V+1)*es) + den alpha read (4C)
-            + numerator gathers (2(U+1)*es) + numerator alpha read (4(U+1))
-  Sum = A_w(2 s_w + s_g) + 8C + (U+1)(4 s_w + 8): 15,756 B/frame for the
-  bigram fp32 U=100 workload.
+  SURVEY.md 8d's design-independent step figure is
+  F_fb = A_w(2 s_w + s_g) + 8C + (U+1)(4 s_w + 8) = 15,756 B/frame (bigram
+  fp32, U=100); it is what hbm_frac_step is priced on.
+
+  checkpointing design (default):
+    loss_forward : alpha pass and beta pass each stream W (2 A_w s_w) and
+                   write their checkpoints alpha, beta (8C) and alpha_num,
+                   beta_num (8(U+1)); numerator gathers come from the LDS copy.
+    loss_backward: marginal pass reads W, writes dW (2 A_w s_w) and reads the
+                   four checkpoints (8C + 8(U+1)).
+  recursion design (--no-checkpoints):
+    loss_forward : A_w s_w + 4C + (U+1)(2 s_w + 4)
+    loss_backward: 2 A_w s_w + 4C + (U+1)(2 s_w + 4)
   """
   Aw = C * (V + 1)
-  fwd = Aw * es + 4 * C + (U + 1) * (2 * es + 4)
-  bwd = 2 * Aw * es + 4 * C + (U + 1) * (2 * es + 4)
-  return fwd, bwd
+  if checkpoints:
+    fwd = 2 * Aw * es + 8 * C + 8 * (U + 1)
+    bwd = 2 * Aw * es + 8 * C + 8 * (U + 1)
+  else:
+    fwd = Aw * es + 4 * C + (U + 1) * (2 * es + 4)
+    bwd = 2 * Aw * es + 4 * C + (U + 1) * (2 * es + 4)
+  survey = Aw * 3 * es + 8 * C + (U + 1) * (4 * es + 8)
+  return fwd, bwd, survey
 
 
 def make_inputs(B, T, U, V, C, device, seed, dtype=torch.float32):
@@ -57,7 +69,7 @@ def make_inputs(B, T, U, V, C, device, seed, dtype=torch.float32):
   return W, nf, labels, nl
 
 
-def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True):
+def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, checkpoints=True):
   """Returns (wall seconds over `steps`, fwd kernel ms list, bwd kernel ms list)."""
   grad = torch.ones([W.shape[0]], dtype=torch.float32, device=W.device)
   # stand-in weight-fn projection head (512 x 33 fp32, SURVEY 8e) so the
@@ -68,10 +80,12 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True):
   def step(ev=None):
     if ev is not None:
       ev[0].record()
-    loss, log_z, num, alpha, an = _native.loss_forward(W, nf, labels, nl, V, n, False)
+    out = _native.loss_forward(W, nf, labels, nl, V, n, False, checkpoints=checkpoints)
+    loss, log_z, num, alpha, an = out[:5]
     if ev is not None:
       ev[1].record()
-    dW = _native.loss_backward(W, nf, labels, nl, log_z, num, alpha, an, grad, V, n, False)
+    dW = _native.loss_backward(W, nf, labels, nl, log_z, num, alpha, an, grad, V, n, False,
+                               ck=out[5] if checkpoints else None)
     if ev is not None:
       ev[2].record()
     if dist_on:
@@ -148,6 +162,10 @@ def main():
   ap.add_argument('--context', type=int, default=1)
   ap.add_argument('--cpu-utts', type=int, default=int(os.environ.get('LT_BENCH_CPU_UTTS', 512)))
   ap.add_argument('--no-north-star', action='store_true')
+  ap.add_argument('--design', choices=['auto', 'checkpoints', 'recursion'], default='auto',
+                  help='loss backward: concurrent beta pass + marginal pass (checkpoints), '
+                       'beta recursion with fused marginals (recursion), or the library '
+                       'policy for the batch size (auto)')
   ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'))
   args = ap.parse_args()
 
@@ -163,7 +181,10 @@ def main():
   B, T, U, V, n = args.batch, args.frames, args.labels, args.vocab, args.context
   C = _native.num_context_states(V, n)
   W, nf, labels, nl = make_inputs(B, T, U, V, C, device, seed=1234 + rank)
-  wall, fwd_ms, bwd_ms = run_steps(W, nf, labels, nl, V, n, args.steps, args.warmup, dist_on)
+  ckpt = (_native.prefer_checkpoints(B, device) if args.design == 'auto'
+          else args.design == 'checkpoints')
+  wall, fwd_ms, bwd_ms = run_steps(W, nf, labels, nl, V, n, args.steps, args.warmup, dist_on,
+                                   checkpoints=ckpt)
 
   t = torch.tensor([wall], dtype=torch.float64, device=device)
   if dist_on:
@@ -172,13 +193,16 @@ def main():
   cells_per_step = world * B * T * U * C
   value = cells_per_step * args.steps / wall
 
-  fwd_b, bwd_b = algorithmic_bytes(T, U, V, C)
+  fwd_b, bwd_b, survey_b = algorithmic_bytes(T, U, V, C, checkpoints=ckpt)
   fwd_avg = float(np.mean(fwd_ms)) * 1e-3
   bwd_avg = float(np.mean(bwd_ms)) * 1e-3
   dominant, dom_bytes, dom_s = ('loss_backward', bwd_b * B * T, bwd_avg) \
       if bwd_avg >= fwd_avg else ('loss_forward', fwd_b * B * T, fwd_avg)
   achieved = dom_bytes / dom_s / 1e9
-  kname = 'bwd_kernel' if dominant == 'loss_backward' else 'fwd_kernel'
+  if ckpt:
+    kname = 'marg_kernel' if dominant == 'loss_backward' else 'loss_forward'
+  else:
+    kname = 'bwd_kernel' if dominant == 'loss_backward' else 'fwd_kernel'
   traffic = read_traffic(args.pmc, kname, B, T)
 
   result = None
@@ -213,26 +237,33 @@ def main():
             'unit': 'GB/s',
             'frac': achieved / HBM_PEAK_GBS,
             'traffic': traffic,
-            'algorithmic_bytes_per_frame': {'loss_forward': fwd_b, 'loss_backward': bwd_b},
+            'algorithmic_bytes_per_frame': {'loss_forward': fwd_b, 'loss_backward': bwd_b,
+                                            'survey_step': survey_b},
         },
+        'design': 'checkpointing (alpha || beta, then marginal pass)' if ckpt
+                  else 'recursion backward',
     }
-    step_bytes = (fwd_b + bwd_b) * B * T * world
-    result['step_gbs'] = step_bytes / (wall / args.steps) / 1e9
+    result['step_gbs'] = survey_b * B * T * world / (wall / args.steps) / 1e9
+    result['hbm_frac_step'] = result['step_gbs'] / HBM_PEAK_GBS
 
   # north-star shape (B=256 on one GPU), measured in the same run at N=1
   if not dist_on and not args.no_north_star and B != 256:
     del W
     torch.cuda.empty_cache()
     W2, nf2, lab2, nl2 = make_inputs(256, T, U, V, C, device, seed=99)
-    wall2, f2, b2 = run_steps(W2, nf2, lab2, nl2, V, n, max(5, args.steps // 2), 2, False)
     steps2 = max(5, args.steps // 2)
+    ck2 = (_native.prefer_checkpoints(256, device) if args.design == 'auto'
+           else args.design == 'checkpoints')
+    wall2, f2, b2 = run_steps(W2, nf2, lab2, nl2, V, n, steps2, 2, False, checkpoints=ck2)
+    fb2, bb2, _ = algorithmic_bytes(T, U, V, C, checkpoints=ck2)
     ms2 = wall2 / steps2 * 1e3
     result['north_star_b256'] = {
         'value': 256 * T * U * C * steps2 / wall2,
         'ms_per_step': ms2,
-        'hbm_frac_step': (fwd_b + bwd_b) * 256 * T / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        'hbm_frac_step': survey_b * 256 * T / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
         'kernels_ms': {'loss_forward': float(np.mean(f2)), 'loss_backward': float(np.mean(b2))},
-        'frac_loss_backward': bwd_b * 256 * T / (float(np.mean(b2)) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        'frac_loss_backward': bb2 * 256 * T / (float(np.mean(b2)) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        'design': 'checkpoints' if ck2 else 'recursion',
     }
     del W2
 

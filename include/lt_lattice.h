@@ -104,27 +104,41 @@ int lt_num_forward(const lt_problem* pb, int32_t semiring, const void* W,
  *   local_norm != 0: LocallyNormalizedWeightFn (lattices.py:178-179),
  *                    loss = -num and the denominator is skipped.
  *   loss [B] out; log_z [B], num [B] out; alpha [B,T,C], alpha_num
- *   [B,T,U+1] out (needed by lt_loss_backward; nullable otherwise). */
+ *   [B,T,U+1] out (needed by lt_loss_backward; nullable otherwise).
+ *   Checkpointing mode (beta_num and arcs non-NULL, and beta unless
+ *   local_norm): the backward recursion -- which depends only on W -- runs
+ *   concurrently with the forward (an internal per-thread auxiliary stream,
+ *   joined back into `stream` before return), writing
+ *     beta     [B,T,C]    beta_{t+1} of frame t (alignments.py:315-316)
+ *     beta_num [B,T,U+1]  numerator beta_{t+1} of frame t
+ *     arcs     [B,4(U+1)] int32 numerator arc table
+ *   so that lt_loss_backward is a single fully parallel streaming pass. */
 int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
                     const int32_t* num_frames, const int32_t* labels,
                     const int32_t* num_labels, float* loss, float* log_z,
-                    float* num, float* alpha, float* alpha_num, void* stream);
+                    float* num, float* alpha, float* alpha_num, float* beta,
+                    float* beta_num, int32_t* arcs, void* stream);
 
 /* d loss / d W for lt_loss_forward (what loss.backward() in the reference
  * should produce; it raises there, D1/D3):
  *   dW = grad[b] * (den_marginals - num_marginals)   (global normalisation)
  *   dW = -grad[b] * num_marginals                    (local_norm != 0)
  * Utterances whose numerator is -inf (loss = +inf) get dW = 0.
- * workspace: lt_loss_backward_workspace_bytes() bytes of device memory
- * (0 for most shapes; then it may be NULL). */
+ * With the checkpoints of lt_loss_forward (beta_num, arcs and, unless
+ * local_norm, beta non-NULL) this is one streaming pass over (b, t) tiles;
+ * otherwise the backward recursion runs here. workspace:
+ * lt_loss_backward_workspace_bytes() bytes of device memory (0 for most
+ * shapes and in checkpointing mode; then it may be NULL). */
 int lt_loss_backward_workspace_bytes(const lt_problem* pb, int32_t local_norm,
                                      size_t* bytes);
 int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
                      const int32_t* num_frames, const int32_t* labels,
                      const int32_t* num_labels, const float* log_z,
                      const float* num, const float* alpha,
-                     const float* alpha_num, const float* grad, void* dW,
-                     void* workspace, size_t workspace_bytes, void* stream);
+                     const float* alpha_num, const float* beta,
+                     const float* beta_num, const int32_t* arcs,
+                     const float* grad, void* dW, void* workspace,
+                     size_t workspace_bytes, void* stream);
 
 /* RecognitionLattice.shortest_path (lattices.py:185-247) without the
  * cross-batch mask aliasing (D6): MaxTropical Viterbi with the reference's

@@ -39,11 +39,10 @@ _SIG = {
     'lt_den_forward': [ctypes.POINTER(Problem), _I32, _P, _P, _P, _P, _P],
     'lt_den_backward': [ctypes.POINTER(Problem), _P, _P, _P, _P, _P, _P, _P],
     'lt_num_forward': [ctypes.POINTER(Problem), _I32, _P, _P, _P, _P, _P, _P, _P],
-    'lt_loss_forward': [ctypes.POINTER(Problem), _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    'lt_loss_forward': [ctypes.POINTER(Problem), _I32] + [_P] * 13,
     'lt_loss_backward_workspace_bytes': [ctypes.POINTER(Problem), _I32,
                                          ctypes.POINTER(ctypes.c_size_t)],
-    'lt_loss_backward': [ctypes.POINTER(Problem), _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                         _P, _P, ctypes.c_size_t, _P],
+    'lt_loss_backward': [ctypes.POINTER(Problem), _I32] + [_P] * 14 + [ctypes.c_size_t, _P],
     'lt_viterbi_workspace_bytes': [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_size_t)],
     'lt_viterbi': [ctypes.POINTER(Problem), _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t,
                    _P],
@@ -149,40 +148,69 @@ def num_forward(W, num_frames, labels, num_labels, vocab_size, context_size, sem
   return num, an
 
 
+def prefer_checkpoints(batch, device=None):
+  """Whether the checkpointing loss path is the faster one for `batch`
+  utterances: it runs the alpha and beta recursions as separate workgroups
+  (2 per utterance) and adds a streaming marginal pass, which pays off while
+  2*batch workgroups still find idle CUs; beyond that the single-workgroup
+  recursion backward (marginals fused into the beta recursion) is faster.
+  LT_CHECKPOINTS=0/1 forces the choice."""
+  env = os.environ.get('LT_CHECKPOINTS')
+  if env in ('0', '1'):
+    return env == '1'
+  cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
+  return 2 * batch <= cus
+
+
 def loss_forward(W, num_frames, labels, num_labels, vocab_size, context_size, local_norm,
-                 want_alpha=True):
-  """lt_loss_forward: (loss, log_z, num, alpha, alpha_num)."""
+                 want_alpha=True, checkpoints=False):
+  """lt_loss_forward: (loss, log_z, num, alpha, alpha_num), plus a 6th element
+  ``ck = (beta, beta_num, arcs)`` with ``checkpoints=True`` -- the backward
+  recursion then runs concurrently with the forward and loss_backward(ck=ck)
+  is one streaming pass."""
   U = labels.shape[-1]
   pb = _problem(W, vocab_size, context_size, U)
   B, T, C, _ = W.shape
   loss, log_z, num = _f32([B], W), _f32([B], W), _f32([B], W)
+  want_alpha = want_alpha or checkpoints
   alpha = _f32([B, T, C], W) if (want_alpha and not local_norm) else None
   an = _f32([B, T, U + 1], W) if want_alpha else None
+  beta = _f32([B, T, C], W) if (checkpoints and not local_norm) else None
+  beta_num = _f32([B, T, U + 1], W) if checkpoints else None
+  arcs = (torch.empty([B, 4 * (U + 1)], dtype=torch.int32, device=W.device)
+          if checkpoints else None)
   if local_norm:
     log_z.zero_()
   _check(lib().lt_loss_forward(ctypes.byref(pb), int(bool(local_norm)), _ptr(W),
                                _ptr(num_frames), _ptr(labels), _ptr(num_labels), _ptr(loss),
                                None if local_norm else _ptr(log_z), _ptr(num), _ptr(alpha),
-                               _ptr(an), _stream()), 'lt_loss_forward')
+                               _ptr(an), _ptr(beta), _ptr(beta_num), _ptr(arcs), _stream()),
+         'lt_loss_forward')
+  if checkpoints:
+    return loss, log_z, num, alpha, an, (beta, beta_num, arcs)
   return loss, log_z, num, alpha, an
 
 
 def loss_backward(W, num_frames, labels, num_labels, log_z, num, alpha, alpha_num, grad,
-                  vocab_size, context_size, local_norm):
-  """lt_loss_backward: d loss / dW (scaled by grad), W's dtype/shape."""
+                  vocab_size, context_size, local_norm, ck=None):
+  """lt_loss_backward: d loss / dW (scaled by grad), W's dtype/shape. With
+  ``ck`` from loss_forward(checkpoints=True) the marginal pass runs."""
   U = labels.shape[-1]
   pb = _problem(W, vocab_size, context_size, U)
-  ws_bytes = ctypes.c_size_t()
-  _check(lib().lt_loss_backward_workspace_bytes(ctypes.byref(pb), int(bool(local_norm)),
-                                                ctypes.byref(ws_bytes)),
-         'lt_loss_backward_workspace_bytes')
+  beta, beta_num, arcs = ck if ck is not None else (None, None, None)
+  ws_bytes = ctypes.c_size_t(0)
+  if ck is None:
+    _check(lib().lt_loss_backward_workspace_bytes(ctypes.byref(pb), int(bool(local_norm)),
+                                                  ctypes.byref(ws_bytes)),
+           'lt_loss_backward_workspace_bytes')
   ws = (torch.empty([ws_bytes.value], dtype=torch.uint8, device=W.device)
         if ws_bytes.value else None)
   dW = torch.empty_like(W)
   _check(lib().lt_loss_backward(ctypes.byref(pb), int(bool(local_norm)), _ptr(W),
                                 _ptr(num_frames), _ptr(labels), _ptr(num_labels), _ptr(log_z),
-                                _ptr(num), _ptr(alpha), _ptr(alpha_num), _ptr(grad), _ptr(dW),
-                                _ptr(ws), ws_bytes.value, _stream()), 'lt_loss_backward')
+                                _ptr(num), _ptr(alpha), _ptr(alpha_num), _ptr(beta),
+                                _ptr(beta_num), _ptr(arcs), _ptr(grad), _ptr(dW), _ptr(ws),
+                                ws_bytes.value, _stream()), 'lt_loss_backward')
   return dW
 
 

@@ -39,6 +39,12 @@ int LT_CAT4(launch_fwd_, LT_LGN, _, LT_P)(int mode, const Plan& pl, bool bf16, i
   }
 }
 int LT_CAT4(launch_bwd_, LT_LGN, _, LT_P)(const Plan& pl, bool bf16, int grid, hipStream_t st) {
+  if (pl.ck) {
+    if (bf16) return pl.wst ? launch_one(bwd_kernel<true, true, false, LT_LG, LT_P, true>, pl, grid, st)
+                            : launch_one(bwd_kernel<true, false, false, LT_LG, LT_P, true>, pl, grid, st);
+    return pl.wst ? launch_one(bwd_kernel<false, true, false, LT_LG, LT_P, true>, pl, grid, st)
+                  : launch_one(bwd_kernel<false, false, false, LT_LG, LT_P, true>, pl, grid, st);
+  }
   if (bf16) {
     if (pl.wst) return pl.dst ? launch_one(bwd_kernel<true, true, true, LT_LG, LT_P>, pl, grid, st)
                               : launch_one(bwd_kernel<true, true, false, LT_LG, LT_P>, pl, grid, st);

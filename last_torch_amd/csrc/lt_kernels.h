@@ -145,6 +145,56 @@ LT_DEVINL int xchgi(int v) {
 }
 #define LT_STAGES(OP) OP(0) OP(1) OP(2) OP(3) OP(4) OP(5)
 
+// Fused butterfly stage for stages 0-3: one v_max/v_add with a DPP source
+// operand (the compiler otherwise emits v_mov_dpp + canonicalize + max).
+// s_nop 1 covers the VALU-write -> DPP-read hazard of the input.
+#define LT_DPP_OP(NAME, OPC)                                                            \
+  template <int S>                                                                      \
+  LT_DEVINL float NAME(float v) {                                                       \
+    float r;                                                                            \
+    if constexpr (S == 0)                                                               \
+      asm("s_nop 1\n\t" OPC " %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" \
+          : "=v"(r) : "v"(v));                                                          \
+    else if constexpr (S == 1)                                                          \
+      asm("s_nop 1\n\t" OPC " %0, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" \
+          : "=v"(r) : "v"(v));                                                          \
+    else if constexpr (S == 2)                                                          \
+      asm("s_nop 1\n\t" OPC " %0, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf"     \
+          : "=v"(r) : "v"(v));                                                          \
+    else                                                                                \
+      asm("s_nop 1\n\t" OPC " %0, %1, %1 row_mirror row_mask:0xf bank_mask:0xf"          \
+          : "=v"(r) : "v"(v));                                                          \
+    return r;                                                                           \
+  }
+LT_DPP_OP(dpp_max, "v_max_f32_dpp")
+LT_DPP_OP(dpp_add, "v_add_f32_dpp")
+#undef LT_DPP_OP
+
+// max / sum over lanes 8k+7 (k = 0..7) of the wave, returned wave-uniform;
+// every other lane must hold the identity. row_shr:8 folds lane 7 into 15
+// of each row, row_bcast:15 rows 0/2 into 1/3, row_bcast:31 rows 0-1 into
+// 2-3; lane 63 ends with the total.
+template <bool MAX>
+LT_DEVINL float xlane_reduce(float v) {
+  float r1, r2, r3;
+  if constexpr (MAX) {
+    asm("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf"
+        : "=v"(r1) : "v"(v));
+    asm("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf"
+        : "=v"(r2) : "v"(r1));
+    asm("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf"
+        : "=v"(r3) : "v"(r2));
+  } else {
+    asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf"
+        : "=v"(r1) : "v"(v));
+    asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf"
+        : "=v"(r2) : "v"(r1));
+    asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf"
+        : "=v"(r3) : "v"(r2));
+  }
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r3), 63));
+}
+
 LT_DEVINL float grp_max(float v, int lg) {
 #define LT_MAXST(S) if (lg > S) v = fmaxf(v, xchg<S>(v));
   LT_STAGES(LT_MAXST)
@@ -213,12 +263,12 @@ LT_DEVINL void stw(void* p, long long e, float v) {
 
 #ifdef LT_STAMPS
 // Diagnostic build only: block 0 records s_memtime at three points of every
-// frame for one wave per role: [role][i][k], k = 0 loop top, 1 after the
+// frame for every wave (lane 0): [wave][i][k], k = 0 loop top, 1 after the
 // barrier, 2 end of the frame's work. Never in the shipped library.
 #define LT_STAMP(a, is_stamper, role_, i_, k_)                                      \
   do {                                                                             \
-    if (blockIdx.x == 0 && a.stamps && (is_stamper))                               \
-      a.stamps[((long long)(role_) * a.T + (i_)) * 4 + (k_)] =                      \
+    if (blockIdx.x == 0 && a.stamps && (threadIdx.x & 63) == 0)                    \
+      a.stamps[((long long)(threadIdx.x >> 6) * a.T + (i_)) * 4 + (k_)] =           \
           (long long)__builtin_amdgcn_s_memtime();                                  \
   } while (0)
 #else
@@ -300,6 +350,9 @@ struct KArgs {
   void* dW;          // [B,T,C,V+1]
   float* nm_side;    // [B,T,U+1,2] numerator marginals (direct path)
   int* ctx_side;     // [B,U+1,2]    numerator arc rows (direct path)
+  float* beta;       // [B,T,C]   den beta_{t+1} per frame t (checkpointing backward)
+  float* beta_num;   // [B,T,U+1] num beta_{t+1} per frame t
+  int* arcs;         // [B,4(U+1)] numerator arc table (forward writes, marginal pass reads)
   int B, T, U, flags;
   long long* stamps; // diagnostic build (-DLT_STAMPS) only: per-step clocks
   int dbg;           // ablation bitmask (LT_DBG, timing experiments only): 1 skip den
@@ -310,6 +363,7 @@ struct KArgs {
   int den_q0;        // state of group 0 (forward n >= 1: 1, the start state is extra0)
   int extra0;        // forward n >= 1: den lane 0 also does the start state (blank only)
   int den_fast;      // every den lane owns at most one group (slices precomputed)
+  int den_xg;        // backward: last source state reduced by wave 0's spare lanes
   int Pr;            // terms per lane (block size of the lane slice, <= template P)
   // layout
   int L, lgL, den_waves, aux_waves, load_waves;
@@ -325,6 +379,17 @@ struct KArgs {
   int gw0, gw1;                    // instructions per frame of loader wave 0 / 1
   int off_ring, off_a, off_na, off_ctx, off_ylab, off_dbuf, off_nbuf, off_misc;
 };
+
+// The kernel arguments re-read from the kernarg segment through a pointer
+// the compiler cannot see through: each role loop then loads only the
+// fields it uses (scalar loads at the use), instead of the whole KArgs being
+// hoisted to the kernel entry and kept live (SGPR spills) across all roles.
+LT_DEVINL const KArgs& fresh_args() {
+  typedef const __attribute__((address_space(4))) KArgs* KP;
+  KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const KArgs*)p;
+}
 
 LT_DEVINL unsigned lds_base_addr(unsigned char* lds) {
   return (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
@@ -401,6 +466,35 @@ LT_DEVINL void walk_states(const KArgs& a, int* ctx, int* ylab) {
   }
 }
 
+// Numerator arc table of utterance b for the marginal pass: entry k = 2u is
+// position u's blank arc (frame element c_u*(V+1)), k = 2u+1 its lexical arc
+// c_u*(V+1) + y_{u+1} (u < U; -1 for u = U). link[k] = head << 30 | (next+1):
+// entries sharing an element form a chain in ascending k whose head (lowest
+// k) sums it, so the subtraction order is fixed (deterministic dW).
+LT_DEVINL void write_arc_table(const KArgs& a, int b, const int* ctx, const int* ylab, int tid,
+                               int nthr) {
+  const int NP = a.U + 1, NK = 2 * NP;
+  int* off = a.arcs + (long long)b * 2 * NK;
+  int* link = off + NK;
+  auto arc = [&](int k) {
+    const int u = k >> 1;
+    return (k & 1) == 0 ? ctx[u] : (u < a.U ? ctx[u] + ylab[u] : -1);
+  };
+  for (int k = tid; k < NK; k += nthr) {
+    const int o = arc(k);
+    int head = o >= 0 ? 1 : 0, nxt = -1;
+    if (o >= 0) {
+      for (int k2 = 0; k2 < NK; ++k2) {
+        if (arc(k2) != o) continue;
+        if (k2 < k) head = 0;
+        else if (k2 > k && nxt < 0) nxt = k2;
+      }
+    }
+    off[k] = o;
+    link[k] = (head << 30) | (nxt + 1);
+  }
+}
+
 // Lane slice of a forward group (destination q): term order index
 // o in [j*P, j*P+P) of {blank, lexical k = o-1}; aoff = alpha index,
 // woff = W element of the frame. Returns the count of valid terms.
@@ -453,10 +547,10 @@ LT_DEVINL float gmax(float v, int lg) {
   if constexpr (LG < 0) {
     return grp_max(v, lg);
   } else {
-    if constexpr (LG > 0) v = fmaxf(v, xchg<0>(v));
-    if constexpr (LG > 1) v = fmaxf(v, xchg<1>(v));
-    if constexpr (LG > 2) v = fmaxf(v, xchg<2>(v));
-    if constexpr (LG > 3) v = fmaxf(v, xchg<3>(v));
+    if constexpr (LG > 0) v = dpp_max<0>(v);
+    if constexpr (LG > 1) v = dpp_max<1>(v);
+    if constexpr (LG > 2) v = dpp_max<2>(v);
+    if constexpr (LG > 3) v = dpp_max<3>(v);
     if constexpr (LG > 4) v = fmaxf(v, xchg<4>(v));
     if constexpr (LG > 5) v = fmaxf(v, xchg<5>(v));
     return v;
@@ -467,10 +561,10 @@ LT_DEVINL float gsum(float v, int lg) {
   if constexpr (LG < 0) {
     return grp_sum(v, lg);
   } else {
-    if constexpr (LG > 0) v += xchg<0>(v);
-    if constexpr (LG > 1) v += xchg<1>(v);
-    if constexpr (LG > 2) v += xchg<2>(v);
-    if constexpr (LG > 3) v += xchg<3>(v);
+    if constexpr (LG > 0) v = dpp_add<0>(v);
+    if constexpr (LG > 1) v = dpp_add<1>(v);
+    if constexpr (LG > 2) v = dpp_add<2>(v);
+    if constexpr (LG > 3) v = dpp_add<3>(v);
     if constexpr (LG > 4) v += xchg<4>(v);
     if constexpr (LG > 5) v += xchg<5>(v);
     return v;
@@ -562,7 +656,7 @@ LT_DEVINL void loader_loop(const KArgs& a, int b, int nf, bool reverse, int lw, 
                            unsigned ldsb, int ahead = 0) {
   const int gw = lw == 0 ? a.gw0 : a.gw1;
   int slot = 0;
-  const bool st = lw == 0 && lane == 0;
+  [[maybe_unused]] const bool st = lw == 0 && lane == 0;
   for (int i = 0; i < nf; ++i) {
     LT_STAMP(a, st, 2, i, 0);
     if (!(a.dbg & 4)) {
@@ -775,10 +869,12 @@ __global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
   if (role == 2) {
     loader_loop(a, b, nf, false, lw, lane, ldsb);
   } else if (role == 0) {
-    if (do_den && !(a.dbg & 1)) den_fwd_loop<MODE, BF16, WST, LG, P>(a, lds, abuf, b, nf, tid);
+    if (do_den && !(a.dbg & 1))
+      den_fwd_loop<MODE, BF16, WST, LG, P>(a, lds, abuf, b, nf, tid);
     else idle_loop(nf);
   } else {
-    if (do_num && !(a.dbg & 2)) num_fwd_loop<MODE, BF16, WST>(a, lds, nbuf, ctx, ylab, b, nf, al, aux_lanes);
+    if (do_num && !(a.dbg & 2))
+      num_fwd_loop<MODE, BF16, WST>(a, lds, nbuf, ctx, ylab, b, nf, al, aux_lanes);
     else idle_loop(nf);
   }
   lds_barrier();
@@ -843,6 +939,7 @@ __global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
       a.loss[b] = (a.flags & F_LOCAL) ? -num : misc[0] - num;
     }
   }
+  if (do_num && a.arcs) write_arc_table(a, b, ctx, ylab, tid, blockDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -854,7 +951,7 @@ __global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
 //   !DST (large C*(V+1)): numerator marginals go to a side buffer and a
 //        scatter kernel subtracts them afterwards.
 // ---------------------------------------------------------------------------
-template <bool BF16, bool WST, bool DST, int LG, int P>
+template <bool BF16, bool WST, bool DST, int LG, int P, bool CK>
 LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, float* nbuf3,
                             int b, int nf, int tid, float gb, float log_z, bool do_den,
                             bool do_num) {
@@ -868,9 +965,17 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
   const bool fast = a.den_fast;
   const bool has = grp < a.den_groups;
   const bool sub_num = DST && do_num;
+  // Spare-lane extra group (plan: den_xg): the last source state E = C-1 is
+  // reduced by the idle last lane (j = L-1) of every group in wave 0, so the
+  // den role needs no partly filled extra wave; its reduction runs over lanes
+  // 8k+7 with row_shr / row_bcast DPP and a readlane.
+  const int E = C - 1;
+  const bool xw = fast && a.den_xg && tid < 64;  // wave-uniform
+  const bool xl = xw && j == L - 1;
   int woff[P], boff[P];
   int nv = 0;
-  if (fast && has) nv = bwd_slice<P>(g, grp, j, a.Pr, woff, boff);
+  if (xl) nv = bwd_slice<P>(g, E, grp, a.Pr, woff, boff);
+  else if (fast && has) nv = bwd_slice<P>(g, grp, j, a.Pr, woff, boff);
   const unsigned char* ringw = lds + a.off_ring + a.st_off[0];
   const unsigned char* ringa = lds + a.off_ring + a.st_off[1];
   const long long es = BF16 ? 2 : 4;
@@ -878,31 +983,59 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
   Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)FR * es, t_last, true);
   Cursor ca = make_cursor(a.st_row[1] > 0 ? a.st_row[1] : (long long)C * 4, t_last, true);
   long long gframe = t_last * FR;  // global element offset of the frame
-  // one source group: beta_t[p] and the marginals of its out-arcs -> dW
+  // CK: beta_t (computed at step i for frame t = nf-1-i) is frame t-1's
+  // checkpoint row; the row of frame nf-1 (beta_nf = 0) is the prologue's.
+  float* brow = (CK && a.beta) ? a.beta + (t_last - 1) * C : nullptr;
+  // one source group: beta_t[p] (alignments.py:315-316) and, unless CK, the
+  // marginals of its out-arcs (alignments.py:311-314) -> dW
   auto group = [&](int p, const int* wo, const int* bo, int n2, const unsigned char* wrow,
                    const float* arow, const float* bcur, float* bnxt, const float* ncur,
-                   void* dWf) {
-      // every LDS read of the step first
+                   void* dWf, float* crow, bool xwv) {
+      // every LDS read first, unconditionally (slots past the slice read
+      // in-bounds dummies), so they issue back to back
       float wv[P], bv[P], nm[P];
 #pragma unroll
       for (int m = 0; m < P; ++m) {
         wv[m] = ldw<BF16>(wrow, wo[m]);
         bv[m] = bcur[bo[m]];
-        nm[m] = sub_num ? ncur[wo[m]] : 0.f;
+        nm[m] = (!CK && sub_num) ? ncur[wo[m]] : 0.f;
       }
-      const float ap = do_den ? arow[p] : 0.f;
+      const bool xlv = xwv && j == L - 1;
+      const int pl = xlv ? E : p;
+      const float ap = (!CK && do_den) ? arow[pl] : 0.f;
       float v[P];
-      if (do_den) {
+      if (CK || do_den) {
         float x[P];
 #pragma unroll
         for (int m = 0; m < P; ++m) x[m] = m < n2 ? wv[m] + bv[m] : -kInf;
-        const float mx = gmax<LG>(tree_max<P>(x), lgL);
+        const float lmax = tree_max<P>(x);
+        float mx;
+        if (xwv) {
+          const float gm = gmax<LG>(xlv ? -kInf : lmax, lgL);
+          const float em = xlane_reduce<true>(xlv ? lmax : -kInf);
+          mx = xlv ? em : gm;
+        } else {
+          mx = gmax<LG>(lmax, lgL);
+        }
         const float c = __builtin_isfinite(mx) ? mx : 0.f;
         const float cl = c * kLog2e;
 #pragma unroll
         for (int m = 0; m < P; ++m) x[m] = lt_exp_off(x[m], cl);
-        const float s = gsum<LG>(tree_sum<P>(x), lgL);
-        if (j == 0) bnxt[p] = c + lt_log(s);
+        const float ls = tree_sum<P>(x);
+        float s;
+        if (xwv) {
+          const float gs = gsum<LG>(xlv ? 0.f : ls, lgL);
+          const float es2 = xlane_reduce<false>(xlv ? ls : 0.f);
+          s = xlv ? es2 : gs;
+        } else {
+          s = gsum<LG>(ls, lgL);
+        }
+        if (j == 0 || (xwv && tid == L - 1)) {
+          const float bval = c + lt_log(s);
+          bnxt[pl] = bval;
+          if (CK && crow) crow[pl] = bval;
+        }
+        if constexpr (CK) return;
         // marginal exp(alpha + w + beta' - log_z) = e * exp(c + alpha - log_z)
         const float sp = (gb == 0.f) ? 0.f : lt_exp(c + ap - log_z) * gb;
 #pragma unroll
@@ -938,19 +1071,24 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
     const float* bcur = bbuf + cur * C;
     float* bnxt = bbuf + (cur ^ 1) * C;
     const float* ncur = nbuf3 + k3 * FR;
-    void* dWf = BF16 ? (void*)((unsigned short*)a.dW + gframe) : (void*)((float*)a.dW + gframe);
+    void* dWf = CK ? nullptr
+                   : (BF16 ? (void*)((unsigned short*)a.dW + gframe)
+                           : (void*)((float*)a.dW + gframe));
+    float* crow = (brow && i < nf - 1) ? brow : nullptr;
     if (fast) {
-      if (has) group(grp, woff, boff, nv, wrow, arow, bcur, bnxt, ncur, dWf);
+      if (xw) group(grp, woff, boff, nv, wrow, arow, bcur, bnxt, ncur, dWf, crow, true);
+      else if (has) group(grp, woff, boff, nv, wrow, arow, bcur, bnxt, ncur, dWf, crow, false);
     } else {
       for (int p = grp; p < C; p += ngrp) {
         int wo[P], bo[P];
         const int n2 = bwd_slice<P>(g, p, j, a.Pr, wo, bo);
-        group(p, wo, bo, n2, wrow, arow, bcur, bnxt, ncur, dWf);
+        group(p, wo, bo, n2, wrow, arow, bcur, bnxt, ncur, dWf, crow, false);
       }
     }
     advance(cw, a);
     advance(ca, a);
     gframe -= FR;
+    if (brow) brow -= C;
     k3 = (k3 == 2) ? 0 : k3 + 1;
     LT_STAMP(a, tid == 0, 0, i, 2);
   }
@@ -1029,7 +1167,7 @@ LT_DEVINL void num_bwd_loop(const KArgs& a, unsigned char* lds, float* nbb, floa
     nb = 1;
     k3 = 1;
   }
-  const bool stamper = al == 0;
+  [[maybe_unused]] const bool stamper = al == 0;
   for (int i = 0; i < nf; ++i) {
     LT_STAMP(a, stamper, 1, i, 0);
     lds_barrier();
@@ -1059,7 +1197,55 @@ LT_DEVINL void num_bwd_loop(const KArgs& a, unsigned char* lds, float* nbb, floa
   }
 }
 
-template <bool BF16, bool WST, bool DST, int LG, int P>
+// Numerator lanes of the checkpointing backward: beta^n only, one frame per
+// step in lockstep with the den lanes; beta^n_t is frame t-1's checkpoint row.
+template <bool BF16, bool WST>
+LT_DEVINL void num_beta_loop(const KArgs& a, unsigned char* lds, float* nbb, const int* ctx,
+                             const int* ylab, int b, int nf, int al, int num_lanes) {
+  const int NP = a.U + 1;
+  int ob = 0, ol = 0;
+  if (al < NP) {
+    ob = ctx[al];
+    ol = al < a.U ? ob + ylab[al] : 0;
+  }
+  const unsigned char* ringw = lds + a.off_ring + a.st_off[0];
+  const long long es = BF16 ? 2 : 4;
+  const long long t_last = (long long)b * a.T + (nf - 1);
+  Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)a.FR * es, t_last, true);
+  float* row = a.beta_num ? a.beta_num + (t_last - 1) * NP : nullptr;
+  int nb = 0;
+  for (int i = 0; i < nf; ++i) {
+    LT_STAMP(a, al == 0, 1, i, 0);
+    lds_barrier();
+    LT_STAMP(a, al == 0, 1, i, 1);
+    const unsigned char* wrow = WST ? ringw + cw.soff + cw.mis : a.W + cw.goff;
+    const float* ncur = nbb + nb * NP;
+    float* nnxt = nbb + (nb ^ 1) * NP;
+    float* crow = (row && i < nf - 1) ? row : nullptr;
+    for (int u = al; u < NP; u += num_lanes) {
+      int o0 = ob, o1 = ol;
+      if (u != al) { o0 = ctx[u]; o1 = u < a.U ? o0 + ylab[u] : 0; }
+      const bool lex = u < a.U;
+      const float wb = ldw<BF16>(wrow, o0);
+      const float wl = ldw<BF16>(wrow, o1);
+      const float bu = ncur[u];
+      const float bu1 = ncur[lex ? u + 1 : u];
+      const float v = log_plus(wb + bu, lex ? wl + bu1 : -kInf);
+      nnxt[u] = v;
+      if (crow) crow[u] = v;
+    }
+    advance(cw, a);
+    if (row) row -= NP;
+    nb ^= 1;
+    LT_STAMP(a, al == 0, 1, i, 2);
+  }
+}
+
+// CK = true: the checkpointing backward. Only beta (den) and beta^n (num)
+// are computed and written per frame (a.beta / a.beta_num); the arc
+// marginals come later from marg_kernel, so this kernel can run
+// concurrently with the forward (both depend only on W).
+template <bool BF16, bool WST, bool DST, int LG, int P, bool CK = false>
 __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int b = blockIdx.x;
@@ -1098,10 +1284,23 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
   } else if (role == 0) {
     // beta_T = one for every state: all context states are final
     // (lattices.py:788-790)
-    if (do_den) for (int p = tid; p < C; p += den_lanes) bbuf[p] = 0.f;
+    if (do_den) {
+      float* crow = (CK && a.beta && nf > 0) ? a.beta + ((long long)b * a.T + nf - 1) * C
+                                             : nullptr;
+      for (int p = tid; p < C; p += den_lanes) {
+        bbuf[p] = 0.f;
+        if (crow) crow[p] = 0.f;
+      }
+    }
   } else {
     if (do_num) {
-      for (int u = al; u < NP; u += aux_lanes) nbb[u] = (u == nl) ? 0.f : -kInf;
+      float* crow = (CK && a.beta_num && nf > 0)
+                        ? a.beta_num + ((long long)b * a.T + nf - 1) * NP : nullptr;
+      for (int u = al; u < NP; u += aux_lanes) {
+        const float v = (u == nl) ? 0.f : -kInf;
+        nbb[u] = v;
+        if (crow) crow[u] = v;
+      }
       load_labels(a, b, ylab, al, aux_lanes);
     }
     if (DST && do_num)
@@ -1125,15 +1324,22 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
   if (role == 2) {
     loader_loop(a, b, nf, true, lw, lane, ldsb, DST && do_num ? 1 : 0);
   } else if (role == 0) {
-    if (!(a.dbg & 1))
-      den_bwd_loop<BF16, WST, DST, LG, P>(a, lds, bbuf, nbuf3, b, nf, tid, gb, log_z, do_den,
-                                          do_num);
+    if (!(a.dbg & 1) && (!CK || do_den))
+      den_bwd_loop<BF16, WST, DST, LG, P, CK>(fresh_args(), lds, bbuf, nbuf3, b, nf, tid, gb,
+                                              log_z, do_den, do_num);
     else idle_loop(nf);
   } else {
-    if (do_num && !(a.dbg & 2))
-      num_bwd_loop<BF16, WST, DST>(a, lds, nbb, nbuf3, ctx, ylab, b, nf, al, aux_lanes, gb, numv);
-    else idle_loop(nf);
+    if (do_num && !(a.dbg & 2)) {
+      if constexpr (CK)
+        num_beta_loop<BF16, WST>(fresh_args(), lds, nbb, ctx, ylab, b, nf, al, aux_lanes);
+      else
+        num_bwd_loop<BF16, WST, DST>(fresh_args(), lds, nbb, nbuf3, ctx, ylab, b, nf, al,
+                                     aux_lanes, gb, numv);
+    } else {
+      idle_loop(nf);
+    }
   }
+  if constexpr (CK) return;
   lds_barrier();
   // padding frames get zero marginals (lattices.py:775-779)
   {
@@ -1152,6 +1358,7 @@ struct Plan {
   int lg;    // template LG (log2 lanes per group), -1 = runtime
   int tmax;  // template P (register slice size)
   bool wst, dst;
+  bool ck;   // checkpointing backward (beta rows only, no marginals)
   int threads;
   int lds_bytes;
 };

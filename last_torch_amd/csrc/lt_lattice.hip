@@ -29,6 +29,247 @@ __global__ void num_scatter_kernel(const KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Arc marginals from checkpoints (the checkpointing loss backward).
+//   dW[b,t,p,y] = g_b * ( exp(alpha_t[p] + W[p,y] + beta_{t+1}[next(p,y)] - log_z)
+//                         - sum of the numerator marginals on that arc )
+// (alignments.py:311-317 for the denominator; the numerator arcs are the
+// string arcs of lattices.py:314-338, Appendix A.4). Every (b,t) is
+// independent, so this is one streaming pass over W -> dW with the grid
+// spanning B x T: tiles of F whole frames (small frames) or one slice of a
+// frame (large frames). Numerator entries that share an arc are summed by
+// the chain head in ascending order (deterministic).
+// ---------------------------------------------------------------------------
+struct MgArgs {
+  const unsigned char* W;
+  const int* nfr;
+  const float* alpha;      // [B,T,C]
+  const float* beta;       // [B,T,C]   beta_{t+1} at frame t
+  const float* alpha_num;  // [B,T,NP]
+  const float* beta_num;   // [B,T,NP]  beta^n_{t+1} at frame t
+  const int* arcs;         // [B,2*NK]  (offsets, links), NK = 2*NP
+  const float* log_z;
+  const float* num;
+  const float* grad;
+  void* dW;
+  int B, T, U, FR, do_den, do_num;
+  NGram g;
+  int F;         // frames per tile (whole-frame tiles), 1 for slice tiles
+  int tpf;       // tiles per frame (1 = whole-frame tiles)
+  int TS;        // elements per slice tile (tpf > 1)
+  int tiles;     // tiles per utterance
+  unsigned mR, mF, mNK;  // magic multipliers for / (V+1), / FR, / NK
+  int off_a, off_b, off_an, off_bn, off_arc, off_sub, off_nb, lds_bytes;
+};
+
+// n / d from the magic m = ceil(2^32 / d), corrected to exact.
+LT_DEVINL unsigned fdiv(unsigned n, unsigned d, unsigned m) {
+  unsigned q = __umulhi(n, m);
+  if (q * d > n) --q;
+  else if ((q + 1) * d <= n) ++q;
+  return q;
+}
+inline unsigned magic_of(unsigned d) { return (unsigned)((0x100000000ULL + d - 1) / d); }
+
+constexpr int kMgUnits = 5;  // 16-byte units of W per thread and tile
+
+template <bool BF16>
+LT_DEVINL void load_unit(const unsigned char* p, float* w) {
+  const uint4 q = *(const uint4*)p;
+  if constexpr (BF16) {
+    const unsigned u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w[2 * i] = __uint_as_float(u[i] << 16);
+      w[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  } else {
+    w[0] = __uint_as_float(q.x); w[1] = __uint_as_float(q.y);
+    w[2] = __uint_as_float(q.z); w[3] = __uint_as_float(q.w);
+  }
+}
+template <bool BF16>
+LT_DEVINL void store_unit(unsigned char* p, const float* v) {
+  uint4 q;
+  if constexpr (BF16) {
+    q.x = f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    q.y = f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    q.z = f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+    q.w = f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+  } else {
+    q.x = __float_as_uint(v[0]); q.y = __float_as_uint(v[1]);
+    q.z = __float_as_uint(v[2]); q.w = __float_as_uint(v[3]);
+  }
+  *(uint4*)p = q;
+}
+
+// One tile: F whole frames (small frames) or one slice of a frame.
+//   phase 0: the tile's W as 16-B units into registers; alpha/beta (+num)
+//            rows, the arc table and a zeroed numerator buffer into LDS
+//   phase 1: each numerator chain head sums its arc's marginals -> Sub[e]
+//            (one writer per element); den marginals in registers
+//   phase 2: dW = den - Sub, 16-B stores. Misaligned tiles / the tail go
+//            element by element.
+template <bool BF16>
+__global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr int VE = BF16 ? 8 : 4;  // elements per 16-byte unit
+  constexpr int ES = BF16 ? 2 : 4;
+  const int tile = blockIdx.x % a.tiles;
+  const int b = blockIdx.x / a.tiles;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const NGram& g = a.g;
+  const int C = g.C, R = g.V + 1, NP = a.U + 1, NK = 2 * NP, FR = a.FR;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  int t0, Fh, e_lo, e_hi;
+  if (a.tpf == 1) {
+    t0 = tile * a.F;
+    Fh = min(a.F, a.T - t0);
+    e_lo = 0;
+    e_hi = FR;
+  } else {
+    t0 = tile / a.tpf;
+    Fh = 1;
+    e_lo = (tile % a.tpf) * a.TS;
+    e_hi = min(FR, e_lo + a.TS);
+  }
+  const int Ew = e_hi - e_lo;
+  const int E = Fh * Ew;
+  const long long base = ((long long)b * a.T + t0) * FR + e_lo;  // tile is contiguous
+  unsigned char* dWb = (unsigned char*)a.dW + base * ES;
+  const unsigned char* Wb = a.W + base * ES;
+  const bool vec = ((base * ES) & 15) == 0;
+  const int nunits = vec ? E / VE : 0;
+  float gb = a.grad ? a.grad[b] : 1.f;
+  const float lz = a.do_den ? a.log_z[b] : 0.f;
+  const float nm = a.do_num ? a.num[b] : 0.f;
+  if ((a.do_num && !__builtin_isfinite(nm)) || (a.do_den && !__builtin_isfinite(lz))) gb = 0.f;
+  const int Fl = max(0, min(Fh, nf - t0));  // live frames of the tile
+  if (Fl == 0 || gb == 0.f) {                // padding (lattices.py:775-779) / unreachable
+    const float z[VE] = {};
+    for (int u = tid; u < nunits; u += nthr) store_unit<BF16>(dWb + (long long)u * 16, z);
+    for (int e = nunits * VE + tid; e < E; e += nthr) stw<BF16>(a.dW, base + e, 0.f);
+    return;
+  }
+  float* A = (float*)(lds + a.off_a);     // [F][C]
+  float* Bt = (float*)(lds + a.off_b);    // [F][C]
+  float* AN = (float*)(lds + a.off_an);   // [F][NP]
+  float* BN = (float*)(lds + a.off_bn);   // [F][NP]
+  int* aoff = (int*)(lds + a.off_arc);    // [NK] offsets, then [NK] links
+  int* alink = aoff + NK;
+  float* Sub = (float*)(lds + a.off_sub); // [E] numerator marginals per element
+  int* nbt = (int*)(lds + a.off_nb);      // [C] next_base (n >= 2)
+
+  // ---- phase 0
+  float w[kMgUnits][VE];
+#pragma unroll
+  for (int r = 0; r < kMgUnits; ++r) {
+    const int u = tid + r * 256;
+    if (u < nunits) load_unit<BF16>(Wb + (long long)u * 16, w[r]);
+  }
+  const long long row0 = (long long)b * a.T + t0;
+  if (a.do_den) {
+    for (int e = tid; e < Fl * C; e += nthr) {
+      A[e] = a.alpha[row0 * C + e];
+      Bt[e] = a.beta[row0 * C + e];
+    }
+    if (g.n >= 2)
+      for (int p = tid; p < C; p += nthr) {
+        bool z;
+        nbt[p] = next_base(g, p, &z);
+      }
+  }
+  if (a.do_num) {
+    for (int e = tid; e < Fl * NP; e += nthr) {
+      AN[e] = a.alpha_num[row0 * NP + e];
+      BN[e] = a.beta_num[row0 * NP + e];
+    }
+    const int* src = a.arcs + (long long)b * 2 * NK;
+    for (int k = tid; k < 2 * NK; k += nthr) aoff[k] = src[k];
+    for (int e = tid; e < E; e += nthr) Sub[e] = 0.f;
+  }
+  __syncthreads();
+
+  // ---- phase 1: numerator chains (deterministic: chain order = ascending k)
+  if (a.do_num) {
+    for (int i = tid; i < Fl * NK; i += nthr) {
+      const int f = (int)fdiv((unsigned)i, (unsigned)NK, a.mNK);
+      const int k = i - f * NK;
+      const int o = aoff[k];
+      const int lk = alink[k];
+      if (!(lk >> 30) || o < e_lo || o >= e_hi) continue;
+      const int el = f * Ew + o - e_lo;
+      const float wv = ldw<BF16>(Wb, el);
+      float sacc = 0.f;
+      for (int kk = k; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
+        const int u = kk >> 1;
+        const float bn = BN[f * NP + ((kk & 1) ? u + 1 : u)];
+        sacc += lt_exp(AN[f * NP + u] + wv + bn - nm);
+      }
+      Sub[el] = gb * sacc;
+    }
+  }
+  // den marginals of the register units
+  const bool den = a.do_den;
+  const bool zero_next = g.n == 0, nb_table = g.n >= 2;
+  float v[kMgUnits][VE];
+#pragma unroll
+  for (int r = 0; r < kMgUnits; ++r) {
+    const int u = tid + r * 256;
+#pragma unroll
+    for (int c = 0; c < VE; ++c) v[r][c] = 0.f;
+    if (u < nunits && den) {
+      const int e0 = u * VE;
+      int f = a.tpf == 1 ? (int)fdiv((unsigned)e0, (unsigned)FR, a.mF) : 0;
+      const int el0 = e_lo + e0 - f * Ew;
+      int p = (int)fdiv((unsigned)el0, (unsigned)R, a.mR);
+      int y = el0 - p * R;
+#pragma unroll
+      for (int c = 0; c < VE; ++c) {
+        if (f < Fl) {
+          const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
+          v[r][c] = gb * lt_exp(A[f * C + p] + w[r][c] + Bt[f * C + q] - lz);
+        }
+        if (++y == R) {
+          y = 0;
+          if (++p == C) { p = 0; ++f; }
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2
+#pragma unroll
+  for (int r = 0; r < kMgUnits; ++r) {
+    const int u = tid + r * 256;
+    if (u < nunits) {
+      if (a.do_num) {
+#pragma unroll
+        for (int c = 0; c < VE; ++c) v[r][c] -= Sub[u * VE + c];
+      }
+      store_unit<BF16>(dWb + (long long)u * 16, v[r]);
+    }
+  }
+  // misaligned tile or tail: element by element
+  for (int e = nunits * VE + tid; e < E; e += nthr) {
+    const int f = a.tpf == 1 ? (int)fdiv((unsigned)e, (unsigned)FR, a.mF) : 0;
+    const int el = e_lo + e - f * Ew;
+    float x = 0.f;
+    if (f < Fl) {
+      if (den) {
+        const int p = (int)fdiv((unsigned)el, (unsigned)R, a.mR);
+        const int y = el - p * R;
+        const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
+        x = gb * lt_exp(A[f * C + p] + ldw<BF16>(Wb, e) + Bt[f * C + q] - lz);
+      }
+      if (a.do_num) x -= Sub[e];
+    }
+    stw<BF16>(a.dW, base + e, x);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Viterbi backtrace: follows the backpointers written by fwd_kernel<M_MAX>.
 // Equivalent to the vjp of _forward(MaxTropical) w.r.t. a zero lexical mask
 // (lattices.py:219-244): the chosen arc at each frame, blank when the blank
@@ -110,6 +351,29 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// Auxiliary stream + events of this host thread and device: the
+// checkpointing backward runs on it concurrently with the forward.
+struct Fork {
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+thread_local Fork g_fork[64];
+
+int get_fork(Fork** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return fail(LT_EHIP, std::string("hipGetDevice: ") + hipGetErrorString(e));
+  Fork& f = g_fork[dev & 63];
+  if (!f.s) {
+    if ((e = hipStreamCreateWithFlags(&f.s, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&f.e0, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&f.e1, hipEventDisableTiming)) != hipSuccess)
+      return fail(LT_EHIP, std::string("aux stream: ") + hipGetErrorString(e));
+  }
+  *out = &f;
+  return LT_OK;
+}
+
 int make_ngram(int V, int n, NGram* g) {
   if (V <= 0) return fail(LT_EINVAL, "vocab_size must be > 0");
   if (n < 0) return fail(LT_EINVAL, "context_size must be >= 0");
@@ -155,10 +419,14 @@ int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 using lt_impl::Plan;
 
 // Choose lanes-per-group, wave roles, LDS carve and ring depth.
-//   kind 0: forward, kind 1: backward
-int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
+//   kind 0: forward, kind 1: backward (beta + marginals), kind 2: checkpointing
+//   backward (beta rows only). lds_cap bounds the workgroup's LDS (the
+//   forward and the checkpointing backward share CUs when they run together).
+int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl,
+         int lds_cap = 160 * 1024) {
   KArgs& a = pl->a;
   memset(&a, 0, sizeof(a));
+  pl->ck = kind == 2;
   a.B = pb->batch; a.T = pb->max_frames; a.U = pb->max_labels; a.g = g;
   a.flags = flags;
   a.dbg = env_int("LT_DBG", 0);
@@ -195,7 +463,7 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   }
   int L = 1;
   while (L < 64 && ceil_div(nterm, L) > 16) L *= 2;
-  const int den_cap = std::min(max_den, env_int("LT_MAX_DEN_WAVES", kind == 1 ? 5 : 4));
+  const int den_cap = std::min(max_den, env_int("LT_MAX_DEN_WAVES", kind != 0 ? 5 : 4));
   while (L < 16 && ceil_div(nterm, 2 * L) >= 3 &&
          (long long)a.den_groups * 2 * L <= 64LL * den_cap)
     L *= 2;
@@ -214,11 +482,21 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
 
   // backward: the den lanes also store dW, so they exist without a denominator
   const bool den_role = do_den || kind == 1;
+  const int cap = std::min(lds_cap, kLdsMax);
   int den = den_role ? ceil_div((long long)a.den_groups * L, 64) : 0;
   den = std::min(den, max_den);
   if (den_role && den < 1) den = 1;
+  // backward: when exactly one group would spill into an extra, nearly empty
+  // wave, wave 0's idle last lanes (j = L-1 of its 64/L groups) reduce it
+  a.den_xg = 0;
+  if (kind != 0 && den >= 2 && (long long)a.den_groups * L == 64LL * (den - 1) + L &&
+      L >= 2 && L <= 8 && (L - 1) * a.Pr >= nterm && (64 / L) * a.Pr >= nterm &&
+      env_int("LT_NO_XG", 0) == 0) {
+    a.den_xg = 1;
+    --den;
+  }
   a.den_waves = den;
-  a.den_fast = (den * 64 / L) >= a.den_groups;
+  a.den_fast = (den * 64 / L) >= a.den_groups - a.den_xg;
 
   // LDS carve (bytes, 16-aligned pieces)
   auto al16 = [](long long x) { return (int)((x + 15) & ~15LL); };
@@ -235,7 +513,7 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   if (kind == 1) {
     const long long need = do_num ? 3LL * a.FR * 4 : 0;
     const int ring_min = 4 * 1024 * 4;  // leave room for a few ring slots
-    if (fixed + need + ring_min <= kLdsMax && env_int("LT_FORCE_DIRECT", 0) == 0) {
+    if (fixed + need + ring_min <= cap && env_int("LT_FORCE_DIRECT", 0) == 0) {
       pl->dst = true;
       a.off_nbuf = fixed;
       a.off_dbuf = fixed;
@@ -265,7 +543,7 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
     a.slot_bytes = slot;
     if (instr == 0) { a.S = 1; a.P = 0; break; }
     const int gmax = ceil_div(instr, a.load_waves);
-    int S = (kLdsMax - al16(fixed)) / slot;
+    int S = (cap - al16(fixed)) / slot;
     S = std::min(S, env_int("LT_RING_SLOTS", 24));
     // outstanding DMA instructions per loader wave must stay <= 63
     while (S >= 3 && (S - 2) * gmax > 63) --S;
@@ -281,7 +559,7 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl) {
   for (int k = 0; k < instr; ++k) (k % a.load_waves == 0 ? a.gw0 : a.gw1)++;
   a.off_ring = al16(fixed);
   pl->lds_bytes = a.off_ring + a.S * a.slot_bytes;
-  if (pl->lds_bytes > kLdsMax) return fail(LT_EUNSUPPORTED, "LDS plan exceeds 160 KiB");
+  if (pl->lds_bytes > cap) return fail(LT_EUNSUPPORTED, "LDS plan exceeds the LDS budget");
   pl->threads = 64 * (a.den_waves + a.aux_waves + a.load_waves);
   if (pl->threads > 1024) return fail(LT_EUNSUPPORTED, "too many waves");
   if (env_int("LT_VERBOSE", 0))
@@ -325,6 +603,59 @@ size_t side_bytes(const lt_problem* pb) {
   const long long nm = (long long)pb->batch * pb->max_frames * NP * 2 * 4;
   const long long cs = (long long)pb->batch * NP * 2 * 4;
   return (size_t)(((nm + 255) & ~255LL) + cs);
+}
+
+// Tiles of the marginal pass: at most kMgUnits 16-byte units per thread.
+// Whole-frame tiles take a multiple of the frames that keep every tile
+// 16-byte aligned when the frame size allows it.
+int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, MgArgs* m,
+              long long* grid) {
+  memset(m, 0, sizeof(*m));
+  const int C = g.C, R = g.V + 1, NP = pb->max_labels + 1, NK = 2 * NP;
+  const long long FR = (long long)C * R;
+  const int es = pb->weight_dtype == LT_DTYPE_BF16 ? 2 : 4;
+  const long long emax_cap = 256LL * kMgUnits * (16 / es);
+  m->B = pb->batch; m->T = pb->max_frames; m->U = pb->max_labels; m->FR = (int)FR; m->g = g;
+  m->do_den = do_den; m->do_num = do_num;
+  long long emax;
+  if (FR <= emax_cap) {
+    m->tpf = 1;
+    long long period = 1;  // frames per 16-byte-aligned run
+    while ((period * FR * es) % 16) ++period;
+    int F = (int)(emax_cap / FR);
+    if (F >= period) F -= F % period;
+    F = std::max(1, std::min(F, std::max(1, pb->max_frames)));
+    m->F = F;
+    m->TS = (int)FR;
+    m->tiles = std::max(1, ceil_div(pb->max_frames, F));
+    emax = F * FR;
+  } else {
+    m->tpf = (int)((FR + emax_cap - 1) / emax_cap);
+    long long ts = (FR + m->tpf - 1) / m->tpf;
+    ts = (ts + 15) & ~15LL;  // slice starts stay 16-byte aligned within a frame
+    m->TS = (int)std::min<long long>(ts, emax_cap);
+    m->tpf = (int)((FR + m->TS - 1) / m->TS);
+    m->F = 1;
+    m->tiles = std::max(1, pb->max_frames * m->tpf);
+    emax = m->TS;
+  }
+  m->mR = magic_of((unsigned)R);
+  m->mF = magic_of((unsigned)FR);
+  m->mNK = magic_of((unsigned)NK);
+  auto al16 = [](long long x) { return (int)((x + 15) & ~15LL); };
+  int off = 0;
+  m->off_a = off; off += do_den ? al16(4LL * m->F * C) : 0;
+  m->off_b = off; off += do_den ? al16(4LL * m->F * C) : 0;
+  m->off_nb = off; off += (do_den && g.n >= 2) ? al16(4LL * C) : 0;
+  m->off_an = off; off += do_num ? al16(4LL * m->F * NP) : 0;
+  m->off_bn = off; off += do_num ? al16(4LL * m->F * NP) : 0;
+  m->off_arc = off; off += do_num ? al16(8LL * NK) : 0;
+  m->off_sub = off; off += do_num ? al16(4 * emax) : 0;
+  m->lds_bytes = std::max(off, 16);
+  if (off > kLdsMax) return fail(LT_EUNSUPPORTED, "marginal tile exceeds LDS");
+  *grid = (long long)pb->batch * m->tiles;
+  if (*grid > 0x7fffffffLL) return fail(LT_EUNSUPPORTED, "marginal grid too large");
+  return LT_OK;
 }
 
 }  // namespace
@@ -396,7 +727,8 @@ int lt_num_forward(const lt_problem* pb, int32_t semiring, const void* W,
 int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
                     const int32_t* num_frames, const int32_t* labels,
                     const int32_t* num_labels, float* loss, float* log_z, float* num,
-                    float* alpha, float* alpha_num, void* stream) {
+                    float* alpha, float* alpha_num, float* beta, float* beta_num,
+                    int32_t* arcs, void* stream) {
   NGram g;
   int rc = check_problem(pb, &g);
   if (rc) return rc;
@@ -404,20 +736,55 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   if (LT_NEED(W) || !num_frames || !num_labels || !loss || (pb->max_labels > 0 && !labels))
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W)) return fail(LT_EINVAL, "W must be 16-byte aligned");
+  const bool ck = beta_num && arcs;
+  if (ck && !local_norm && LT_NEED(beta)) return fail(LT_EINVAL, "beta is null");
+  if (ck && (LT_NEED(alpha_num) || (!local_norm && LT_NEED(alpha))))
+    return fail(LT_EINVAL, "checkpoints need alpha / alpha_num");
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const int flags = F_NUM | F_LOSS | (local_norm ? F_LOCAL : F_DEN);
-  Plan pl;
-  if ((rc = plan(pb, g, 0, flags, &pl))) return rc;
-  bind_streams(pl.a, W, nullptr, nullptr);
-  pl.a.nfr = num_frames;
-  pl.a.labels = labels;
-  pl.a.nlab = num_labels;
-  pl.a.loss = loss;
-  pl.a.dist = log_z;
-  pl.a.num = num;
-  pl.a.alpha = alpha;
-  pl.a.alpha_num = alpha_num;
-  return launch_fwd(M_LOG, pl, pb->weight_dtype == LT_DTYPE_BF16, pb->batch,
-                    (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  // With checkpoints, the beta pass (independent of alpha) runs at the same
+  // time on an auxiliary stream; both workgroup kinds then share CUs, so
+  // each plan takes half the LDS when that still leaves a deep ring.
+  Plan pf, pbk;
+  int cap = kLdsMax;
+  if (ck) {
+    const int half = kLdsMax / 2;
+    Plan t1, t2;
+    const int bflags = F_NUM | (local_norm ? F_LOCAL : F_DEN);
+    if (env_int("LT_PAIR_LDS", 0) && plan(pb, g, 0, flags, &t1, half) == LT_OK &&
+        plan(pb, g, 2, bflags, &t2, half) == LT_OK && t1.a.S >= 6 && t2.a.S >= 6)
+      cap = half;
+    if ((rc = plan(pb, g, 2, bflags, &pbk, cap))) return rc;
+    bind_streams(pbk.a, W, nullptr, nullptr);
+    pbk.a.nfr = num_frames;
+    pbk.a.labels = labels;
+    pbk.a.nlab = num_labels;
+    pbk.a.beta = local_norm ? nullptr : beta;
+    pbk.a.beta_num = beta_num;
+  }
+  if ((rc = plan(pb, g, 0, flags, &pf, cap))) return rc;
+  bind_streams(pf.a, W, nullptr, nullptr);
+  pf.a.nfr = num_frames;
+  pf.a.labels = labels;
+  pf.a.nlab = num_labels;
+  pf.a.loss = loss;
+  pf.a.dist = log_z;
+  pf.a.num = num;
+  pf.a.alpha = alpha;
+  pf.a.alpha_num = alpha_num;
+  pf.a.arcs = ck ? arcs : nullptr;
+  if (!ck) return launch_fwd(M_LOG, pf, bf16, pb->batch, st);
+  Fork* f = nullptr;
+  if ((rc = get_fork(&f))) return rc;
+  if ((rc = hip_check(hipEventRecord(f->e0, st), "event record"))) return rc;
+  if ((rc = hip_check(hipStreamWaitEvent(f->s, f->e0, 0), "stream wait"))) return rc;
+  // LT_CK_SOLO (timing experiments only): 1 = beta pass only, 2 = alpha pass only
+  const int solo = env_int("LT_CK_SOLO", 0);
+  if (solo != 2 && (rc = launch_bwd(pbk, bf16, pb->batch, f->s))) return rc;
+  if (solo != 1 && (rc = launch_fwd(M_LOG, pf, bf16, pb->batch, st))) return rc;
+  if ((rc = hip_check(hipEventRecord(f->e1, f->s), "event record"))) return rc;
+  return hip_check(hipStreamWaitEvent(st, f->e1, 0), "stream wait");
 }
 
 int lt_den_backward(const lt_problem* pb, const void* W, const int32_t* num_frames,
@@ -456,12 +823,39 @@ int lt_loss_backward_workspace_bytes(const lt_problem* pb, int32_t local_norm, s
 int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
                      const int32_t* num_frames, const int32_t* labels,
                      const int32_t* num_labels, const float* log_z, const float* num,
-                     const float* alpha, const float* alpha_num, const float* grad, void* dW,
+                     const float* alpha, const float* alpha_num, const float* beta,
+                     const float* beta_num, const int32_t* arcs, const float* grad, void* dW,
                      void* workspace, size_t workspace_bytes, void* stream) {
   NGram g;
   int rc = check_problem(pb, &g);
   if (rc) return rc;
   if (pb->batch == 0) return LT_OK;
+  if (beta_num && arcs) {  // checkpoints from lt_loss_forward: one streaming pass
+    if (LT_NEED(W) || !num_frames || !num || LT_NEED(alpha_num) || LT_NEED(beta_num) ||
+        LT_NEED(dW) || (!local_norm && (!log_z || LT_NEED(alpha) || LT_NEED(beta))))
+      return fail(LT_EINVAL, "null pointer");
+    if (misaligned(W) || misaligned(dW)) return fail(LT_EINVAL, "W/dW must be 16-byte aligned");
+    MgArgs m;
+    long long grid = 0;
+    if ((rc = plan_marg(pb, g, !local_norm, true, &m, &grid))) return rc;
+    m.W = (const unsigned char*)W; m.nfr = num_frames;
+    m.alpha = alpha; m.beta = beta; m.alpha_num = alpha_num; m.beta_num = beta_num;
+    m.arcs = arcs; m.log_z = log_z; m.num = num; m.grad = grad; m.dW = dW;
+    if (grid == 0) return LT_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (m.lds_bytes > 64 * 1024) {
+      const void* k = pb->weight_dtype == LT_DTYPE_BF16 ? (const void*)marg_kernel<true>
+                                                         : (const void*)marg_kernel<false>;
+      if ((rc = hip_check(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              m.lds_bytes), "marginal LDS")))
+        return rc;
+    }
+    if (pb->weight_dtype == LT_DTYPE_BF16)
+      hipLaunchKernelGGL(marg_kernel<true>, dim3((unsigned)grid), dim3(256), m.lds_bytes, st, m);
+    else
+      hipLaunchKernelGGL(marg_kernel<false>, dim3((unsigned)grid), dim3(256), m.lds_bytes, st, m);
+    return hip_check(hipGetLastError(), "marginal launch");
+  }
   if (LT_NEED(W) || !num_frames || !num_labels || !num || LT_NEED(alpha_num) || LT_NEED(dW) ||
       (pb->max_labels > 0 && !labels) || (!local_norm && (!log_z || LT_NEED(alpha))))
     return fail(LT_EINVAL, "null pointer");

@@ -70,22 +70,34 @@ def _kernel_weights(W: torch.Tensor) -> torch.Tensor:
 
 
 class _LossFn(torch.autograd.Function):
-  """loss = log_z - num (or -num): lt_loss_forward / lt_loss_backward."""
+  """loss = log_z - num (or -num): lt_loss_forward / lt_loss_backward.
+
+  When a gradient is needed, the forward also runs the backward recursion
+  concurrently (checkpointing mode) so the backward is one streaming pass
+  over the arc marginals."""
 
   @staticmethod
   def forward(ctx, W, nf, labels, nl, V, n, local):
-    loss, log_z, num, alpha, an = _native.loss_forward(W, nf, labels, nl, V, n, local)
+    ck = ctx.needs_input_grad[0] and _native.prefer_checkpoints(W.shape[0], W.device)
+    out = _native.loss_forward(W, nf, labels, nl, V, n, local, checkpoints=ck)
+    loss, log_z, num, alpha, an = out[:5]
+    beta, beta_num, arcs = out[5] if ck else (None, None, None)
+    dummy = log_z
     ctx.save_for_backward(W, nf, labels, nl, log_z, num,
-                          alpha if alpha is not None else log_z, an)
-    ctx.cfg = (V, n, local)
+                          alpha if alpha is not None else dummy, an,
+                          beta if beta is not None else dummy,
+                          beta_num if beta_num is not None else dummy,
+                          arcs if arcs is not None else nf)
+    ctx.cfg = (V, n, local, ck)
     return loss
 
   @staticmethod
   def backward(ctx, g):
-    W, nf, labels, nl, log_z, num, alpha, an = ctx.saved_tensors
-    V, n, local = ctx.cfg
+    W, nf, labels, nl, log_z, num, alpha, an, beta, beta_num, arcs = ctx.saved_tensors
+    V, n, local, ck = ctx.cfg
+    cks = ((None if local else beta), beta_num, arcs) if ck else None
     dW = _native.loss_backward(W, nf, labels, nl, log_z, num, None if local else alpha, an,
-                               g.float().contiguous(), V, n, local)
+                               g.float().contiguous(), V, n, local, ck=cks)
     return dW, None, None, None, None, None, None
 
 

@@ -80,11 +80,14 @@ def test_golden_num_forward(cuda, case, semiring):
 
 @pytest.mark.parametrize('case', LATTICE_CASES)
 @pytest.mark.parametrize('local', [False, True])
-def test_golden_loss_and_grad(cuda, case, local):
+@pytest.mark.parametrize('ckpt', [False, True])
+def test_golden_loss_and_grad(cuda, case, local, ckpt):
   c = load(case)
   W, nf, lab, nl = _dev(c, cuda, 'W_local' if local else 'W')
-  loss, lz, num, al, an = nat.loss_forward(W, nf, lab, nl, c['V'], c['n'], local)
-  dW = nat.loss_backward(W, nf, lab, nl, lz, num, al, an, None, c['V'], c['n'], local)
+  out = nat.loss_forward(W, nf, lab, nl, c['V'], c['n'], local, checkpoints=ckpt)
+  loss, lz, num, al, an = out[:5]
+  dW = nat.loss_backward(W, nf, lab, nl, lz, num, al, an, None, c['V'], c['n'], local,
+                         ck=out[5] if ckpt else None)
   torch.cuda.synchronize()
   assert_loss_close(loss.cpu().numpy(), c['loss_local' if local else 'loss'])
   if not local:
@@ -219,6 +222,24 @@ def _random_problem(B, T, U, V, n, seed):
 
 
 @pytest.mark.parametrize('B,T,U,V,n,dt', RANDOM)
+def test_random_checkpointing_vs_oracle(cuda, B, T, U, V, n, dt):
+  """Checkpointing loss path: concurrent beta pass + streaming marginal pass."""
+  orc = _orc()
+  W, nf, lab, nl = _random_problem(B, T, U, V, n, seed=B * 1000 + T + V + n + 7)
+  bf16 = dt == 'bf16'
+  if bf16:
+    W = torch.tensor(W).bfloat16().float().numpy()
+  Wd = torch.tensor(W).to(torch.bfloat16 if bf16 else torch.float32).to(cuda)
+  nfd, labd, nld = (torch.tensor(x).to(cuda) for x in (nf, lab, nl))
+  for local in (False, True):
+    out = nat.loss_forward(Wd, nfd, labd, nld, V, n, local, checkpoints=True)
+    dW = nat.loss_backward(Wd, nfd, labd, nld, *out[1:5], None, V, n, local, ck=out[5])
+    rl, rlz, _, rdW = orc.loss_grad(W, nf, lab, nl, V, n, local_norm=local)
+    assert_loss_close(out[0].cpu().numpy(), rl)
+    assert_grad_close(dW.float().cpu().numpy(), rdW, rlz, bf16)
+
+
+@pytest.mark.parametrize('B,T,U,V,n,dt', RANDOM)
 def test_random_vs_oracle(cuda, B, T, U, V, n, dt):
   orc = _orc()
   W, nf, lab, nl = _random_problem(B, T, U, V, n, seed=B * 1000 + T + V + n)
@@ -312,9 +333,18 @@ def test_full_size_loss_properties_and_determinism(full_size):
   out2 = nat.loss_forward(W, nf, lab, nl, V, n, False)
   dW2 = nat.loss_backward(W, nf, lab, nl, *out2[1:], None, V, n, False)
   assert torch.equal(out1[0], out2[0])  # the loss is bitwise reproducible
-  # dW: numerator marginals of positions sharing an arc meet in LDS float
-  # atomics, so their summation order (last bits) may vary run to run
+  # dW (recursion backward): numerator marginals of positions sharing an arc
+  # meet in LDS float atomics, so their summation order may vary run to run
   assert torch.allclose(dW1, dW2, atol=1e-6, rtol=0)
+  # checkpointing path: fixed summation order -> bitwise reproducible, and
+  # equal to the recursion backward within rounding
+  c1 = nat.loss_forward(W, nf, lab, nl, V, n, False, checkpoints=True)
+  d1 = nat.loss_backward(W, nf, lab, nl, *c1[1:5], None, V, n, False, ck=c1[5])
+  c2 = nat.loss_forward(W, nf, lab, nl, V, n, False, checkpoints=True)
+  d2 = nat.loss_backward(W, nf, lab, nl, *c2[1:5], None, V, n, False, ck=c2[5])
+  assert torch.equal(c1[0], out1[0]) and torch.equal(c1[0], c2[0]) and torch.equal(d1, d2)
+  tol = 1e-5 + 2e-6 * out1[1].abs().clamp(min=1.0)[:, None, None, None]
+  assert ((d1 - dW1).abs() <= tol).all()
   loss = out1[0]
   assert torch.isfinite(loss).all() and (loss > -1e-3).all()    # log_z >= numerator
   # linearity in the incoming gradient

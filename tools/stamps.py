@@ -53,4 +53,5 @@ def main():
   cyc = s[0, T - 1, 0] - s[0, 0, 0]
   print('clock est GHz', cyc / (e0.elapsed_time(e1) * 1e-3) / 1e9, 'kernel ms', e0.elapsed_time(e1))
 
-main()
+if __name__ == "__main__":
+  main()
