@@ -1061,7 +1061,9 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
       }
   };
   int k3 = 0;  // numerator marginal buffer of this frame (i % 3)
-  for (int i = 0; i < nf; ++i) {
+  // per-frame pointers, then the role's work; fast and general paths are
+  // separate loops so each keeps only its own state live
+  auto step = [&](int i, auto&& work) {
     LT_STAMP(a, tid == 0, 0, i, 0);
     lds_barrier();
     LT_STAMP(a, tid == 0, 0, i, 1);
@@ -1075,22 +1077,36 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
                    : (BF16 ? (void*)((unsigned short*)a.dW + gframe)
                            : (void*)((float*)a.dW + gframe));
     float* crow = (brow && i < nf - 1) ? brow : nullptr;
-    if (fast) {
-      if (xw) group(grp, woff, boff, nv, wrow, arow, bcur, bnxt, ncur, dWf, crow, true);
-      else if (has) group(grp, woff, boff, nv, wrow, arow, bcur, bnxt, ncur, dWf, crow, false);
-    } else {
-      for (int p = grp; p < C; p += ngrp) {
-        int wo[P], bo[P];
-        const int n2 = bwd_slice<P>(g, p, j, a.Pr, wo, bo);
-        group(p, wo, bo, n2, wrow, arow, bcur, bnxt, ncur, dWf, crow, false);
-      }
-    }
+    work(wrow, arow, bcur, bnxt, ncur, dWf, crow);
     advance(cw, a);
-    advance(ca, a);
+    if (!CK) advance(ca, a);
     gframe -= FR;
     if (brow) brow -= C;
     k3 = (k3 == 2) ? 0 : k3 + 1;
     LT_STAMP(a, tid == 0, 0, i, 2);
+  };
+  if (fast && xw) {
+    for (int i = 0; i < nf; ++i)
+      step(i, [&](const unsigned char* wrow, const float* arow, const float* bcur, float* bnxt,
+                  const float* ncur, void* dWf, float* crow) {
+        group(grp, woff, boff, nv, wrow, arow, bcur, bnxt, ncur, dWf, crow, true);
+      });
+  } else if (fast) {
+    for (int i = 0; i < nf; ++i)
+      step(i, [&](const unsigned char* wrow, const float* arow, const float* bcur, float* bnxt,
+                  const float* ncur, void* dWf, float* crow) {
+        if (has) group(grp, woff, boff, nv, wrow, arow, bcur, bnxt, ncur, dWf, crow, false);
+      });
+  } else {
+    for (int i = 0; i < nf; ++i)
+      step(i, [&](const unsigned char* wrow, const float* arow, const float* bcur, float* bnxt,
+                  const float* ncur, void* dWf, float* crow) {
+        for (int p = grp; p < C; p += ngrp) {
+          int wo[P], bo[P];
+          const int n2 = bwd_slice<P>(g, p, j, a.Pr, wo, bo);
+          group(p, wo, bo, n2, wrow, arow, bcur, bnxt, ncur, dWf, crow, false);
+        }
+      });
   }
 }
 
