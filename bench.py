@@ -136,17 +136,21 @@ def cpu_baseline(T, U, V, n, C, sample_utts):
   }
 
 
-def read_traffic(profile_json, kernel, B, T):
-  """HBM bytes per launch of `kernel` from a committed PMC summary
-  (profiles/*pmc*.json written by tools/pmc_summary.py), or None."""
+def read_traffic(profile_json, kernels, B, T):
+  """HBM bytes per call summed over `kernels` (the launches one C-ABI call
+  makes) from a committed PMC summary (profiles/*pmc*.json written by
+  tools/pmc_summary.py), or None."""
   try:
     with open(profile_json) as f:
       d = json.load(f)
-    k = d['kernels'][kernel]
-    if k.get('batch') != B or k.get('frames') != T:
-      return None
-    return k['hbm_bytes_per_launch']
-  except (OSError, KeyError, ValueError):
+    total = 0.0
+    for kernel in kernels:
+      k = d['kernels'][kernel]
+      if k.get('batch') != B or k.get('frames') != T or k['hbm_bytes_per_launch'] is None:
+        return None
+      total += k['hbm_bytes_per_launch']
+    return total
+  except (OSError, KeyError, ValueError, TypeError):
     return None
 
 
@@ -166,7 +170,8 @@ def main():
                   help='loss backward: concurrent beta pass + marginal pass (checkpoints), '
                        'beta recursion with fused marginals (recursion), or the library '
                        'policy for the batch size (auto)')
-  ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'))
+  ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'),
+                  help='PMC summary of the checkpointing design; *_recursion.json for the other')
   args = ap.parse_args()
 
   world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -200,10 +205,11 @@ def main():
       if bwd_avg >= fwd_avg else ('loss_forward', fwd_b * B * T, fwd_avg)
   achieved = dom_bytes / dom_s / 1e9
   if ckpt:
-    kname = 'marg_kernel' if dominant == 'loss_backward' else 'loss_forward'
+    knames = ['marg_kernel'] if dominant == 'loss_backward' else ['fwd_kernel', 'bwd_kernel_ck']
   else:
-    kname = 'bwd_kernel' if dominant == 'loss_backward' else 'fwd_kernel'
-  traffic = read_traffic(args.pmc, kname, B, T)
+    knames = ['bwd_kernel'] if dominant == 'loss_backward' else ['fwd_kernel']
+  pmc = args.pmc if ckpt else args.pmc.replace('.json', '_recursion.json')
+  traffic = read_traffic(pmc, knames, B, T)
 
   result = None
   if rank == 0:
@@ -231,7 +237,7 @@ def main():
         'kernels_ms': {'loss_forward': fwd_avg * 1e3, 'loss_backward': bwd_avg * 1e3},
         'roofline': {
             'bound': 'hbm',
-            'kernel': dominant,
+            'kernel': f"{dominant} ({' || '.join(knames)})",
             'achieved': achieved,
             'peak': HBM_PEAK_GBS,
             'unit': 'GB/s',

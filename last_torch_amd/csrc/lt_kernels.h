@@ -1133,11 +1133,17 @@ LT_DEVINL void num_bwd_frame(const KArgs& a, const unsigned char* wrow, const fl
     const float an = anrow[u] - numv;
     const float xb = wb + bu;
     const float xl = lex ? wl + bu1 : -kInf;
-    nnxt[u] = log_plus(xb, xl);
+    // log_plus (semirings.py:248-255) sharing its exponentials with the
+    // marginals exp(an + x) = exp(x - c) * exp(an + c)
+    float c = fmaxf(xb, xl);
+    if (!__builtin_isfinite(c)) c = 0.f;
+    const float eb = lt_exp(xb - c), el = lt_exp(xl - c);
+    nnxt[u] = c + lt_log(eb + el);
     float mb = 0.f, ml = 0.f;
     if (gb != 0.f) {
-      mb = lt_exp(an + xb) * gb;
-      ml = lt_exp(an + xl) * gb;
+      const float sc = lt_exp(an + c) * gb;
+      mb = eb * sc;
+      ml = el * sc;
     }
     if constexpr (DST) {
       if (mb != 0.f) atomicAdd(&mdst[o0], mb);

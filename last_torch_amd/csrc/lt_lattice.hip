@@ -58,7 +58,7 @@ struct MgArgs {
   int TS;        // elements per slice tile (tpf > 1)
   int tiles;     // tiles per utterance
   unsigned mR, mF, mNK;  // magic multipliers for / (V+1), / FR, / NK
-  int off_a, off_b, off_an, off_bn, off_arc, off_sub, off_nb, lds_bytes;
+  int off_a, off_b, off_an, off_bn, off_arc, off_sub, off_nb, off_w, lds_bytes;
 };
 
 // n / d from the magic m = ceil(2^32 / d), corrected to exact.
@@ -73,8 +73,7 @@ inline unsigned magic_of(unsigned d) { return (unsigned)((0x100000000ULL + d - 1
 constexpr int kMgUnits = 5;  // 16-byte units of W per thread and tile
 
 template <bool BF16>
-LT_DEVINL void load_unit(const unsigned char* p, float* w) {
-  const uint4 q = *(const uint4*)p;
+LT_DEVINL void unpack_unit(const uint4 q, float* w) {
   if constexpr (BF16) {
     const unsigned u[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
@@ -159,13 +158,14 @@ __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
   int* alink = aoff + NK;
   float* Sub = (float*)(lds + a.off_sub); // [E] numerator marginals per element
   int* nbt = (int*)(lds + a.off_nb);      // [C] next_base (n >= 2)
+  unsigned char* Wl = lds + a.off_w;      // [E] the tile's W (numerator gathers)
 
   // ---- phase 0
-  float w[kMgUnits][VE];
+  uint4 wq[kMgUnits];
 #pragma unroll
   for (int r = 0; r < kMgUnits; ++r) {
     const int u = tid + r * 256;
-    if (u < nunits) load_unit<BF16>(Wb + (long long)u * 16, w[r]);
+    if (u < nunits) wq[r] = *(const uint4*)(Wb + (long long)u * 16);
   }
   const long long row0 = (long long)b * a.T + t0;
   if (a.do_den) {
@@ -187,6 +187,16 @@ __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
     const int* src = a.arcs + (long long)b * 2 * NK;
     for (int k = tid; k < 2 * NK; k += nthr) aoff[k] = src[k];
     for (int e = tid; e < E; e += nthr) Sub[e] = 0.f;
+    // the tile's W in LDS for the numerator gathers
+#pragma unroll
+    for (int r = 0; r < kMgUnits; ++r) {
+      const int u = tid + r * 256;
+      if (u < nunits) *(uint4*)(Wl + u * 16) = wq[r];
+    }
+    for (int e = nunits * VE + tid; e < E; e += nthr) {
+      if constexpr (BF16) ((unsigned short*)Wl)[e] = ((const unsigned short*)Wb)[e];
+      else ((float*)Wl)[e] = ((const float*)Wb)[e];
+    }
   }
   __syncthreads();
 
@@ -199,7 +209,7 @@ __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
       const int lk = alink[k];
       if (!(lk >> 30) || o < e_lo || o >= e_hi) continue;
       const int el = f * Ew + o - e_lo;
-      const float wv = ldw<BF16>(Wb, el);
+      const float wv = ldw<BF16>(Wl, el);
       float sacc = 0.f;
       for (int kk = k; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
         const int u = kk >> 1;
@@ -219,6 +229,8 @@ __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
 #pragma unroll
     for (int c = 0; c < VE; ++c) v[r][c] = 0.f;
     if (u < nunits && den) {
+      float w[VE];
+      unpack_unit<BF16>(wq[r], w);
       const int e0 = u * VE;
       int f = a.tpf == 1 ? (int)fdiv((unsigned)e0, (unsigned)FR, a.mF) : 0;
       const int el0 = e_lo + e0 - f * Ew;
@@ -228,7 +240,7 @@ __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
       for (int c = 0; c < VE; ++c) {
         if (f < Fl) {
           const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
-          v[r][c] = gb * lt_exp(A[f * C + p] + w[r][c] + Bt[f * C + q] - lz);
+          v[r][c] = gb * lt_exp(A[f * C + p] + w[c] + Bt[f * C + q] - lz);
         }
         if (++y == R) {
           y = 0;
@@ -614,7 +626,8 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
   const int C = g.C, R = g.V + 1, NP = pb->max_labels + 1, NK = 2 * NP;
   const long long FR = (long long)C * R;
   const int es = pb->weight_dtype == LT_DTYPE_BF16 ? 2 : 4;
-  const long long emax_cap = 256LL * kMgUnits * (16 / es);
+  const int units = std::max(1, std::min(kMgUnits, env_int("LT_MARG_UNITS", kMgUnits)));
+  const long long emax_cap = 256LL * units * (16 / es);
   m->B = pb->batch; m->T = pb->max_frames; m->U = pb->max_labels; m->FR = (int)FR; m->g = g;
   m->do_den = do_den; m->do_num = do_num;
   long long emax;
@@ -651,6 +664,7 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
   m->off_bn = off; off += do_num ? al16(4LL * m->F * NP) : 0;
   m->off_arc = off; off += do_num ? al16(8LL * NK) : 0;
   m->off_sub = off; off += do_num ? al16(4 * emax) : 0;
+  m->off_w = off; off += do_num ? al16((long long)es * emax) : 0;
   m->lds_bytes = std::max(off, 16);
   if (off > kLdsMax) return fail(LT_EUNSUPPORTED, "marginal tile exceeds LDS");
   *grid = (long long)pb->batch * m->tiles;

@@ -33,7 +33,12 @@ def _rows(path):
 
 
 def _kernel_key(name):
-  for k in ('bwd_kernel', 'fwd_kernel', 'backtrace_kernel', 'num_scatter_kernel'):
+  """Kernel family: fwd_kernel, bwd_kernel (beta + marginals), bwd_kernel_ck
+  (checkpointing beta pass: last template argument true), marg_kernel, ..."""
+  if 'bwd_kernel' in name:
+    args = name.split('bwd_kernel<', 1)[-1].split('>', 1)[0].split(',')
+    return 'bwd_kernel_ck' if len(args) >= 6 and args[5].strip() == 'true' else 'bwd_kernel'
+  for k in ('fwd_kernel', 'marg_kernel', 'backtrace_kernel', 'num_scatter_kernel'):
     if k in name:
       return k
   return None
