@@ -26,7 +26,11 @@ $(OBJ)/lt_lattice.o: $(CSRC)/lt_lattice.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB): $(OBJ)/lt_lattice.o $(INST_OBJS)
+$(OBJ)/lt_pipe.o: $(CSRC)/lt_pipe.hip $(DEPS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(INST_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
 oracle:
@@ -47,6 +51,9 @@ $(STAMP_OBJ)/lt_inst_%.o: $(CSRC)/lt_inst.hip $(DEPS)
 $(STAMP_OBJ)/lt_lattice.o: $(CSRC)/lt_lattice.hip $(DEPS)
 	@mkdir -p $(STAMP_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -c -o $@ $<
-stamps: $(STAMP_OBJ)/lt_lattice.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
+$(STAMP_OBJ)/lt_pipe.o: $(CSRC)/lt_pipe.hip $(DEPS)
+	@mkdir -p $(STAMP_OBJ)
+	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -c -o $@ $<
+stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(STAMP_OBJ)/liblt_lattice_stamps.so $^
 .PHONY: stamps

@@ -205,7 +205,9 @@ def main():
       if bwd_avg >= fwd_avg else ('loss_forward', fwd_b * B * T, fwd_avg)
   achieved = dom_bytes / dom_s / 1e9
   if ckpt:
-    knames = ['marg_kernel'] if dominant == 'loss_backward' else ['fwd_kernel', 'bwd_kernel_ck']
+    fk = (['pipe_kernel'] if _native.pipe_path(B, T, U, V, n)
+          else ['fwd_kernel', 'bwd_kernel_ck'])
+    knames = ['marg_kernel'] if dominant == 'loss_backward' else fk
   else:
     knames = ['bwd_kernel'] if dominant == 'loss_backward' else ['fwd_kernel']
   pmc = args.pmc if ckpt else args.pmc.replace('.json', '_recursion.json')

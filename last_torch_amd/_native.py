@@ -162,6 +162,18 @@ def prefer_checkpoints(batch, device=None):
   return 2 * batch <= cus
 
 
+def pipe_path(batch, frames, labels, vocab_size, context_size, bf16=False):
+  """Whether lt_loss_forward with checkpoints runs the pipelined bigram
+  recursions (lt_pipe.hip, kernel ``pipe_kernel``) for this shape; mirrors
+  lt_impl::pipe_eligible. LT_NO_PIPE=1 turns them off."""
+  if os.environ.get('LT_NO_PIPE', '0') not in ('', '0'):
+    return False
+  if context_size != 1 or not 1 <= vocab_size <= 32 or labels + 1 > 256:
+    return False
+  C = vocab_size + 1
+  return batch * frames * C * C * (2 if bf16 else 4) < 0xFFFFFFF0
+
+
 def loss_forward(W, num_frames, labels, num_labels, vocab_size, context_size, local_norm,
                  want_alpha=True, checkpoints=False):
   """lt_loss_forward: (loss, log_z, num, alpha, alpha_num), plus a 6th element

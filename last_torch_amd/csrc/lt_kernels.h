@@ -1395,4 +1395,10 @@ struct Plan {
 LT_VARIANTS(LT_DECL)
 #undef LT_DECL
 int set_error(int code, const char* msg);
+// lt_pipe.hip: pipelined bigram Log recursions (alpha, and beta when dirs == 2)
+bool pipe_eligible(const lt_problem* pb);
+int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32_t* nfr,
+                const int32_t* labels, const int32_t* nlab, float* loss, float* log_z,
+                float* num, float* alpha, float* alpha_num, float* beta, float* beta_num,
+                int32_t* arcs, int dirs, int* err, void* stream);
 }  // namespace lt_impl

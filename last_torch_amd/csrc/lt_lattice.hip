@@ -757,6 +757,13 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const int flags = F_NUM | F_LOSS | (local_norm ? F_LOCAL : F_DEN);
   hipStream_t st = (hipStream_t)stream;
+  // bigram with checkpoints: the pipelined two-factor alpha and beta
+  // recursions in one launch (lt_pipe.hip). Without checkpoints the
+  // frame-barrier kernel below is the faster one (measured: 0.45 vs 0.52 ms
+  // at B=64), so the pipe only serves the checkpointing path.
+  if (ck && lt_impl::pipe_eligible(pb))
+    return lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
+                                num, alpha, alpha_num, beta, beta_num, arcs, 2, nullptr, stream);
   // With checkpoints, the beta pass (independent of alpha) runs at the same
   // time on an auxiliary stream; both workgroup kinds then share CUs, so
   // each plan takes half the LDS when that still leaves a deep ring.

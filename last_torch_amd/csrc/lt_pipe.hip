@@ -1,0 +1,934 @@
+// lt_pipe.hip -- barrier-free, producer/consumer pipelined recursions for the
+// bigram lattice (FullNGram context_size = 1, 1 <= V <= 32) under the Log
+// semiring: the alpha and beta passes of the checkpointing loss forward
+// (lt_loss_forward with checkpoints), one workgroup per (utterance, direction).
+//
+// What is computed (reference file:line in last_torch/):
+//   alpha_{t+1} = FrameDependent.forward(alpha_t, W_t)   alignments.py:286-297,
+//                 FullNGram.forward_reduce                  contexts.py:207-230
+//   beta_t      = FrameDependent.backward(beta_{t+1}, W_t) alignments.py:300-318,
+//                 FullNGram.backward_broadcast              contexts.py:232-256
+//   numerator alpha^n / beta^n over the label string       lattices.py:250-377,
+//                                                           alignments.py:320-329
+//   log_z, numerator, loss                                 lattices.py:131-183, 496
+//
+// Why a different kernel for this shape. With n = 1 every lexical arc with
+// label y lands in state y (contexts.py:190-205), so each frame is a dense
+// (V+1) x (V+1) log-semiring matrix-vector product. Written as per-destination
+// logsumexps it costs one exp per arc on the serial frame chain. Here it is
+// split into two factors,
+//     lse_k(v_k + W_k) = (M + c) + log sum_k exp(v_k - M) * exp(W_k - c),
+// with c the frame's max weight and M an upper bound of the state values:
+//   * E = exp(W - c) depends only on W. Helper waves compute it for frames
+//     ahead of the recursion (they also stage raw W for the numerator), so
+//     no arc exp is on the chain;
+//   * g_k = exp(v_k - M) is one exp per STATE, broadcast through LDS;
+//   * the chain per frame is then: one exp, an LDS round trip, J fused
+//     multiply-adds per lane, one DPP add and one log.
+// Exactness: every product is <= 1 and the sum is kept only when it lies in
+// [2^-60, 2^64]; dropped (underflowed) products are then < 2^-126, i.e.
+// below fp32 rounding of the sum. Any state whose sum leaves that range
+// (adversarial weight ranges, -inf / +inf arcs, dead lattices) makes the
+// wave recompute the frame with the exact safe-max logsumexp of
+// semirings.py:279-286 from the raw weights -- same results, slower.
+// State values are kept relative to a per-utterance float-float base, so the
+// chain accumulates no rounding; outputs are base + value rounded once.
+//
+// Execution: wave 0 = denominator (states 1..V on H lanes each, state 0
+// alongside), wave 1 = numerator (PN string positions per lane, neighbours
+// through DPP wave shifts), waves 2.. = helpers. Frames flow through a ring
+// of K LDS slots guarded by per-slot tags (producer) and done counters
+// (consumers); there is no workgroup barrier inside the frame loop. Every
+// wait is bounded: a stalled pipeline raises an abort flag and the kernel
+// drains instead of hanging.
+#include "lt_kernels.h"
+
+namespace {
+
+constexpr int kPipeMaxSlots = 32;
+constexpr int kPipeNL = 18;   // helper loads per lane per frame (FR <= 1152)
+constexpr int kPipeMaxHelpers = 6;
+constexpr float kLoTh = 8.673617379884035e-19f;  // 2^-60
+constexpr float kHiTh = 1.8446744073709552e19f;  // 2^64
+
+struct PArgs {
+  const unsigned char* W;
+  const int* nfr;
+  const int* labels;
+  const int* nlab;
+  float* loss;
+  float* log_z;
+  float* num;
+  float* alpha;      // [B,T,C]   alpha_t (pre-update) of frame t
+  float* alpha_num;  // [B,T,NP]
+  float* beta;       // [B,T,C]   beta_{t+1} of frame t
+  float* beta_num;   // [B,T,NP]
+  int* arcs;         // [B,4NP]
+  int* err;          // nullable: set to 1 if a pipeline wait timed out
+  int B, T, U, V, C, R, FR, flags;
+  int H, lgH;        // lanes per state
+  int J, JP, rowE;   // terms per lane part (<= template J), padded, floats per E row
+  int K, NH, NLr;    // ring slots, helper waves, loads per lane actually needed
+  int logn_x;        // unused (alignment)
+  float logn;        // log(number of terms per state) for the running bound
+  int off_ctl, off_g, off_u, off_ctx, off_ylab, off_ring, slot_bytes;
+  int soff_e, soff_eb, soff_c;  // offsets inside a slot
+  int dirs;          // 1: alpha only (blocks = B), 2: alpha + beta (blocks = 2B)
+  unsigned w_bytes;  // bytes of W (< 2^32)
+  long long* stamps; // diagnostic build (-DLT_STAMPS) only: [wave][T][4] s_memtime
+  int stamp_block;
+  int dbg;           // timing ablations (LT_PIPE_DBG): 1 no raw-W stores, 2 no E stores,
+                     // 4 no den history, 8 no num history
+};
+
+#ifdef LT_STAMPS
+#define PSTAMP(a, w, i, k)                                                         \
+  do {                                                                             \
+    if ((int)blockIdx.x == (a).stamp_block && (a).stamps && (threadIdx.x & 63) == 0) \
+      (a).stamps[((long long)(w) * (a).T + (i)) * 4 + (k)] =                        \
+          (long long)__builtin_amdgcn_s_memtime();                                  \
+  } while (0)
+#else
+#define PSTAMP(a, w, i, k) \
+  do {                     \
+  } while (0)
+#endif
+
+// control block (ints) at off_ctl
+enum { CTL_TAG = 0, CTL_DEN = kPipeMaxSlots, CTL_NUM, CTL_ABORT, CTL_FIN0, CTL_FIN1, CTL_N };
+
+typedef __attribute__((address_space(3))) volatile int lds_vint;
+typedef __attribute__((address_space(3))) float lds_float;
+typedef float lt_f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) lt_f4 lds_float4;
+typedef __attribute__((address_space(3))) int lds_int;
+
+LT_DEVINL __attribute__((address_space(3))) unsigned char* as3(unsigned char* p) {
+  return (__attribute__((address_space(3))) unsigned char*)p;
+}
+
+// Bounded wait until *p >= v (LDS word written by another wave). Returns
+// false (and raises the abort flag) on timeout or abort.
+LT_DEVINL bool wait_ge(lds_vint* p, int v, lds_vint* abort_flag, int* err) {
+  int n = 0;
+  while (*p < v) {
+    if (*abort_flag) return false;
+    __builtin_amdgcn_s_sleep(1);
+    if (++n > (1 << 21)) {
+      *abort_flag = 1;
+      if (err) atomicOr(err, 1);
+      return false;
+    }
+  }
+  asm volatile("" ::: "memory");
+  return true;
+}
+
+LT_DEVINL void lds_release_store(lds_vint* p, int v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  *p = v;
+}
+
+// ---- cross-lane helpers (full exec) -------------------------------------
+template <int CTRL>
+LT_DEVINL float dpp_mov(float v, float old) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v),
+                                                    CTRL, 0xF, 0xF, false));
+}
+// full-wave max / sum, result uniform
+LT_DEVINL float wave_max(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v, -kInf));
+  v = fmaxf(v, dpp_mov<0x4E>(v, -kInf));
+  v = fmaxf(v, dpp_mov<0x141>(v, -kInf));
+  v = fmaxf(v, dpp_mov<0x140>(v, -kInf));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-kInf),
+                                                          __float_as_int(v), 0x142, 0xA, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-kInf),
+                                                          __float_as_int(v), 0x143, 0xC, 0xF, false)));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+LT_DEVINL float wave_sum(float v) {
+  v += dpp_mov<0xB1>(v, 0.f);
+  v += dpp_mov<0x4E>(v, 0.f);
+  v += dpp_mov<0x141>(v, 0.f);
+  v += dpp_mov<0x140>(v, 0.f);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// sum / max over aligned groups of 2^lg lanes (all lanes of a group end equal)
+LT_DEVINL float group_sum_lg(float v, int lg) {
+  if (lg > 0) v += dpp_mov<0xB1>(v, 0.f);
+  if (lg > 1) v += dpp_mov<0x4E>(v, 0.f);
+  if (lg > 2) v += dpp_mov<0x141>(v, 0.f);
+  if (lg > 3) v += dpp_mov<0x140>(v, 0.f);
+  if (lg > 4) v += __shfl_xor(v, 16);
+  if (lg > 5) v += __shfl_xor(v, 32);
+  return v;
+}
+LT_DEVINL float group_max_lg(float v, int lg) {
+  if (lg > 0) v = fmaxf(v, dpp_mov<0xB1>(v, -kInf));
+  if (lg > 1) v = fmaxf(v, dpp_mov<0x4E>(v, -kInf));
+  if (lg > 2) v = fmaxf(v, dpp_mov<0x141>(v, -kInf));
+  if (lg > 3) v = fmaxf(v, dpp_mov<0x140>(v, -kInf));
+  if (lg > 4) v = fmaxf(v, __shfl_xor(v, 16));
+  if (lg > 5) v = fmaxf(v, __shfl_xor(v, 32));
+  return v;
+}
+// value of lane l-1 (lane 0 gets `fill`) / lane l+1 (lane 63 gets `fill`)
+LT_DEVINL float from_prev_lane(float v, float fill) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(fill), __float_as_int(v),
+                                                    0x138, 0xF, 0xF, false));
+}
+LT_DEVINL float from_next_lane(float v, float fill) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(fill), __float_as_int(v),
+                                                    0x130, 0xF, 0xF, false));
+}
+
+LT_DEVINL float safe(float x) { return __builtin_isfinite(x) ? x : 0.f; }
+
+// float-float accumulation of the per-utterance base (two-sum)
+LT_DEVINL void ff_add(float& hi, float& lo, float x) {
+  const float s = hi + x;
+  const float bb = s - hi;
+  const float e = (hi - (s - bb)) + (x - bb);
+  hi = s;
+  lo += e;
+}
+
+// ---- denominator wave ----------------------------------------------------
+// In-place DPP reductions: one VALU op per stage (s_nop 1 covers the
+// VALU-write -> DPP-read hazard); rows outside row_mask keep their value.
+LT_DEVINL float wave_max_dpp(float v) {
+  asm volatile(
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+      : "+v"(v));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+LT_DEVINL float wave_sum_dpp(float v) {
+  asm volatile(
+      "s_nop 1\n\tv_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+      : "+v"(v));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// sum over lane pairs (2l, 2l+1)
+LT_DEVINL float pair_sum_dpp(float v) {
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+               : "+v"(v));
+  return v;
+}
+
+typedef float lt_f2 __attribute__((ext_vector_type(2)));
+
+// fwd (REV = false): lane (d, h), d = 1 + (lane >> lgH) in [1, C): destination
+//   d, lexical terms from every source k in part h (k = h*J + j < C), plus the
+//   blank self loop on h == 0. State 0 (blank only, contexts.py:216-217) is
+//   kept exactly in log space on every lane.
+// bwd (REV = true): lane (p, h), p in [1, C): source p, lexical terms y = k+1
+//   (k = h*J + j < V) plus the blank on h == 0; state 0's V+1 terms are spread
+//   one per lane and wave-summed (no other state depends on it in-frame).
+//
+// Representation: the vector is base + log(g) with g the LINEAR values
+// published in gbuf (scaled forward algorithm). A frame is then
+//   S_d = sum_k g_k E[k,d]  (+ blank),  E = exp(W - c_t)  (helpers)
+//   g'_d = S_d * 2^-e,  base' = base + c_t + e ln 2,
+// with e the exponent of the previous frame's max S (lagged, off the chain):
+// no transcendental and no reduction on the chain. While every S lies in
+// [2^-60, 2^64] each dropped (underflowed) product is below fp32 rounding of
+// its sum and every published g >= 2^-124 is exact in log space; otherwise
+// the frame is recomputed with the exact safe-max logsumexp
+// (semirings.py:279-286) from log(g) (or the exact log values kept after a
+// previous fallback) and the raw weights, and the vector is republished
+// with its exact max as the new base.
+template <int J, bool REV>
+LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int lane) {
+  // reset the compiler's view of outstanding loads (other roles' paths):
+  // otherwise it waits for vmcnt(0) -- this wave's history stores -- in-loop
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
+  lds_float* gbuf = (lds_float*)(as3(lds) + a.off_g);
+  lds_float* ubuf = (lds_float*)(as3(lds) + a.off_u);
+  // lanes per state: compile-time for the J classes with a single H
+  constexpr int LGH = J == 17 ? 1 : (J == 5 ? 2 : (J == 2 ? 3 : -1));
+  const int C = a.C, V = a.V, R = a.R, JP = a.JP, rowE = a.rowE;
+  const int lgH = LGH >= 0 ? LGH : a.lgH;
+  const int H = 1 << lgH;
+  const int d = 1 + (lane >> lgH);
+  const int h = lane & (H - 1);
+  const bool act = d < C;
+  const int nlex = REV ? V : C;
+  auto pos = [&](int k) { return (k / J) * JP + (k % J); };
+  // each lane publishes one state: its own, or state 0 (fwd) / nothing
+  // (bwd: dummy slot rowE) for lane 1 and lanes without a state
+  const bool pub0 = lane == 1 || !act;
+  const int pub_pos = pub0 ? (REV ? rowE : 0) : pos(REV ? d - 1 : d);
+  const int hist_idx = pub0 ? 0 : d;
+  const int nvalid = max(0, min(J, nlex - h * J));  // valid terms of this part
+  const int rowi = act ? (REV ? d : d - 1) : 0;
+  const int eoff = rowi * rowE + h * JP;              // this lane's E part (floats)
+  const int ebi = act ? d : 0;
+  const int z_pos = (REV && lane < V) ? pos(lane) : 0;  // bwd state-0 spread
+  const lds_float* Gp = gbuf + h * JP;
+  // state (relative to base_hi + base_lo)
+  float g = (REV && act) ? 1.f : 0.f;  // own state, linear
+  float g0 = 1.f;                      // state 0, linear (bwd) / exp(u0) (fwd)
+  float u0 = 0.f;                      // fwd state 0, exact log (bwd: in mode 1)
+  float uo = (REV && act) ? 0.f : -kInf;  // own state, exact log (mode 1 only)
+  int mode = 1;                        // 1: ubuf holds exact logs (after init / fallback)
+  int esc = 0;                         // normaliser exponent (lagged)
+  float base_hi = 0.f, base_lo = 0.f;
+  gbuf[pub_pos] = pub0 ? g0 : g;
+  ubuf[pub_pos] = pub0 ? u0 : uo;
+  float* hrow = (REV ? a.beta : a.alpha);
+  const long long hstep = REV ? -(long long)C : (long long)C;
+  if (hrow) hrow += ((long long)b * a.T + (REV ? nf - 1 : 0)) * C + hist_idx;
+
+  // the current step's operands (software-pipelined: step i+1's are loaded
+  // while step i's off-chain work runs)
+  float gv[J], ev[J];
+  float ebl = 0.f, gz = 0.f, ez = 0.f, eb0 = 0.f, ct = 0.f, w00 = 0.f;
+  auto load_step = [&](int slot) {
+    unsigned char* sb = lds + a.off_ring + slot * a.slot_bytes;
+    const lds_float* E = (const lds_float*)(as3(sb) + a.soff_e);
+    const lds_float* Eb = (const lds_float*)(as3(sb) + a.soff_eb);
+#pragma unroll
+    for (int q = 0; q < J / 4; ++q) {
+      const lt_f4 g4 = *(const lds_float4*)(Gp + 4 * q);
+      const lt_f4 e4 = *(const lds_float4*)(E + eoff + 4 * q);
+      gv[4 * q] = g4.x; gv[4 * q + 1] = g4.y; gv[4 * q + 2] = g4.z; gv[4 * q + 3] = g4.w;
+      ev[4 * q] = e4.x; ev[4 * q + 1] = e4.y; ev[4 * q + 2] = e4.z; ev[4 * q + 3] = e4.w;
+    }
+#pragma unroll
+    for (int j = 4 * (J / 4); j < J; ++j) {
+      gv[j] = Gp[j];
+      ev[j] = E[eoff + j];
+    }
+    ebl = Eb[ebi];
+    if constexpr (REV) {
+      gz = gbuf[z_pos];
+      ez = E[z_pos];
+      eb0 = Eb[0];
+    }
+    ct = *(const lds_float*)(as3(sb) + a.soff_c);
+    w00 = *(const lds_float*)as3(sb);
+  };
+  int slot = 0;
+  bool live = nf > 0;
+  if (live) {
+    live = wait_ge(ctl + CTL_TAG, 1, ctl + CTL_ABORT, a.err);
+    asm volatile("" ::: "memory");
+    if (live) load_step(0);
+  }
+  int tag_pref = nf > 1 ? ctl[CTL_TAG + (a.K > 1 ? 1 : 0)] : 0;
+  int i = 0;
+  for (; live && i < nf; ++i) {
+    PSTAMP(a, 0, i, 0);
+    const int nslot = (slot + 1 == a.K) ? 0 : slot + 1;
+    // ---- the chain: S_d = sum_k g_k E[k,d] over part h (+ blank on h == 0)
+    lt_f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < J / 4; ++q) {
+      const lt_f2 g01 = {gv[4 * q], gv[4 * q + 1]}, g23 = {gv[4 * q + 2], gv[4 * q + 3]};
+      const lt_f2 e01 = {ev[4 * q], ev[4 * q + 1]}, e23 = {ev[4 * q + 2], ev[4 * q + 3]};
+      acc0 = __builtin_elementwise_fma(g01, e01, acc0);
+      acc1 = __builtin_elementwise_fma(g23, e23, acc1);
+    }
+    float st = __builtin_fmaf(g, h == 0 ? ebl : 0.f, 0.f);
+#pragma unroll
+    for (int j = 4 * (J / 4); j < J; ++j) st = __builtin_fmaf(gv[j], ev[j], st);
+    float S = ((acc0.x + acc0.y) + (acc1.x + acc1.y)) + st;
+    if (a.dbg & 64) S = gv[0] + ev[0];  // timing ablation
+    S = act ? S : 0.f;
+    if constexpr (LGH == 1) S = pair_sum_dpp(S);
+    else S = group_sum_lg(S, lgH);
+    float S0 = 0.f;
+    if constexpr (REV) {
+      const float tz = __builtin_fmaf(g0, lane == 0 ? eb0 : 0.f, lane < V ? gz * ez : 0.f);
+      S0 = wave_sum_dpp(tz);
+    }
+    // range check: positive finite floats order like their bit patterns
+    const unsigned lo_b = 0x21800000u, span = 0x5f800000u - 0x21800000u;
+    const bool bad_l = act && ((unsigned)__float_as_uint(S) - lo_b > span);
+    bool bad = __builtin_amdgcn_ballot_w64(bad_l) != 0;
+    if constexpr (REV) bad = bad || ((unsigned)__float_as_uint(S0) - lo_b > span);
+    PSTAMP(a, 0, i, 1);
+    // history value of row t: the pre-update vector (lattices.py:462)
+    const float hlo = pub0 ? ((REV && !mode) ? lt_log(g0) : u0) : (mode ? uo : lt_log(g));
+    const float hval = base_hi + (base_lo + hlo);
+    float shift, gn, g0n;
+    if (!bad) {
+      // fast path: publish g' = S 2^-e (exact scaling), base += c + e ln2
+      gn = __builtin_amdgcn_ldexpf(S, -esc);
+      const float esh = (float)esc * 0.6931471805599453f;
+      if constexpr (REV) {
+        g0n = __builtin_amdgcn_ldexpf(S0, -esc);
+      } else {
+        u0 = ((u0 + w00) - ct) - esh;  // exact blank self loop of state 0
+        g0n = lt_exp(u0);
+      }
+      gbuf[pub_pos] = pub0 ? g0n : gn;
+      shift = ct + esh;
+    } else {
+      // exact frame from log values (relative to base) and the raw weights
+      const lds_float* Wr = (const lds_float*)as3(lds + a.off_ring + slot * a.slot_bytes);
+      float x[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int k = h * J + j;
+        float xv = -kInf;
+        if (act && j < nvalid) {
+          float uk = mode ? ubuf[h * JP + j] : lt_log(gv[j]);
+          if (!REV && k == 0) uk = u0;
+          xv = REV ? uk + Wr[d * R + k + 1] : uk + Wr[k * R + d];
+        }
+        x[j] = xv;
+      }
+      const float uown = mode ? uo : lt_log(g);
+      const float xb = (act && h == 0) ? uown + Wr[d * R] : -kInf;
+      float m1 = xb;
+#pragma unroll
+      for (int j = 0; j < J; ++j) m1 = fmaxf(m1, x[j]);
+      m1 = group_max_lg(m1, lgH);
+      const float c1 = safe(m1);
+      float s1 = (act && h == 0) ? lt_exp(xb - c1) : 0.f;
+#pragma unroll
+      for (int j = 0; j < J; ++j) s1 += lt_exp(x[j] - c1);
+      s1 = group_sum_lg(s1, lgH);
+      const float un = act ? c1 + lt_log(s1) : -kInf;  // relative to base
+      float u0n;
+      if constexpr (REV) {
+        const float u0c = mode ? u0 : lt_log(g0);
+        float xz = -kInf;
+        if (lane == 0) xz = u0c + Wr[0];
+        else if (lane <= V) {
+          const int zp = pos(lane - 1);
+          xz = (mode ? ubuf[zp] : lt_log(gbuf[zp])) + Wr[lane];
+        }
+        const float cz = safe(wave_max(xz));
+        const float sz = wave_sum(lane <= V ? lt_exp(xz - cz) : 0.f);
+        u0n = cz + lt_log(sz);
+      } else {
+        u0n = u0 + w00;
+      }
+      // republish relative to the exact max of the new vector
+      const float mnew = safe(wave_max(fmaxf(un, u0n)));
+      const float unr = un - mnew, u0r = u0n - mnew;
+      gn = act ? lt_exp(unr) : 0.f;
+      g0n = lt_exp(u0r);
+      gbuf[pub_pos] = pub0 ? g0n : gn;
+      ubuf[pub_pos] = pub0 ? u0r : unr;
+      uo = unr;
+      u0 = u0r;
+      shift = mnew;
+    }
+    // ---- next step's operands (after the publish: LDS is in order per wave)
+    if (i + 1 < nf) {
+      if (tag_pref < i + 2 && !wait_ge(ctl + CTL_TAG + nslot, i + 2, ctl + CTL_ABORT, a.err))
+        live = false;
+      asm volatile("" ::: "memory");
+      if (live) {
+        load_step(nslot);
+        tag_pref = ctl[CTL_TAG + ((nslot + 1 == a.K) ? 0 : nslot + 1)];
+      }
+    }
+    // ---- off-chain work of step i
+    if (hrow && !(a.dbg & 4)) {
+      *hrow = hval;
+      hrow += hstep;
+    }
+    if (!bad) {
+      // next normaliser: exponent of this frame's max S
+      float mx = act ? S : 0.f;
+      if constexpr (REV) mx = fmaxf(mx, S0);
+      if (a.dbg & 32)  // timing ablation: cheap normaliser
+        esc = __builtin_amdgcn_frexp_expf(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(S))));
+      else
+        esc = __builtin_amdgcn_frexp_expf(wave_max_dpp(mx));
+      mode = 0;
+    } else {
+      esc = 0;
+      mode = 1;
+    }
+    g = act ? gn : 0.f;
+    g0 = g0n;
+    if (!(a.dbg & 32)) ff_add(base_hi, base_lo, shift);
+    // slot of step i consumed (its reads were used above)
+    asm volatile("" ::: "memory");
+    if (lane == 0) *(ctl + CTL_DEN) = i + 1;
+    PSTAMP(a, 0, i, 2);
+    slot = nslot;
+  }
+  // final vector: padding rows (fwd, lattices.py:460-461) and log_z
+  if (!REV) {
+    const float lown = mode ? uo : lt_log(g);
+    if (a.alpha) {
+      const long long r0 = (long long)b * a.T;
+      for (int t = nf; t < a.T; ++t)
+        a.alpha[(r0 + t) * C + hist_idx] = base_hi + (base_lo + (pub0 ? u0 : lown));
+    }
+    // (+)_q alpha_T[q] (lattices.py:496): safe-max logsumexp
+    const bool own = act && h == 0;
+    const float mx = wave_max(fmaxf(own ? lown : -kInf, lane == 0 ? u0 : -kInf));
+    const float c = safe(mx);
+    float e = 0.f;
+    if (own) e += lt_exp(lown - c);
+    if (lane == 0) e += lt_exp(u0 - c);
+    const float s = wave_sum(e);
+    // log_z = base + c + log(s) (the base only shifts finite values)
+    const float rel = c + lt_log(s);
+    const float lz = __builtin_isfinite(rel) ? base_hi + (base_lo + rel) : rel;
+    if (lane == 0) {
+      ((lds_float*)(as3(lds) + a.off_ctl))[CTL_FIN0] = lz;
+      if (a.log_z) a.log_z[b] = lz;
+    }
+  }
+}
+
+// _LogAddExp.forward (semirings.py:248-255) with one exp: the max term's
+// exp(a - c) is exactly 1, so c + log(1 + exp(min - c)) is the same value;
+// a non-finite max is returned as is (= the reference's safe-max result).
+LT_DEVINL float log_plus2(float a, float b) {
+  const float m = fmaxf(a, b), n = fminf(a, b);
+  const float r = m + lt_log(1.f + lt_exp(n - m));
+  return __builtin_isfinite(m) ? r : m;
+}
+
+// ---- numerator wave --------------------------------------------------------
+// Positions u = PN*lane + s. fwd: a'[u] = a[u] W[c_u,0] (+) a[u-1] W[c_{u-1},y_u]
+// (alignments.py:320-329, lattices.py:314-338); bwd is its transpose.
+template <int PN, bool REV>
+LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int lane) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // see den_pipe
+  lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
+  const lds_int* ctx = (const lds_int*)(as3(lds) + a.off_ctx);
+  const lds_int* ylab = (const lds_int*)(as3(lds) + a.off_ylab);
+  const int NP = a.U + 1, U = a.U;
+  int ob[PN], ol[PN];
+  float v[PN];
+  const int nl = a.nlab[b];
+#pragma unroll
+  for (int s = 0; s < PN; ++s) {
+    const int u = PN * lane + s;
+    ob[s] = 0;
+    ol[s] = 0;
+    if (u < NP) {
+      ob[s] = ctx[u];
+      if (!REV) ol[s] = u >= 1 ? ctx[u - 1] + ylab[u - 1] : 0;
+      else ol[s] = u < U ? ctx[u] + ylab[u] : 0;
+    }
+    if (!REV) v[s] = (u == 0) ? 0.f : -kInf;
+    else v[s] = (u == nl) ? 0.f : -kInf;
+  }
+  float* hist = REV ? a.beta_num : a.alpha_num;
+  int tag_next = nf > 0 ? ctl[CTL_TAG] : 0;
+  const long long row0 = (long long)b * a.T;
+  int slot = 0;
+  for (int i = 0; i < nf; ++i, slot = (slot + 1 == a.K) ? 0 : slot + 1) {
+    const int t = REV ? nf - 1 - i : i;
+    PSTAMP(a, 1, i, 0);
+    if (tag_next < i + 1 && !wait_ge(ctl + CTL_TAG + slot, i + 1, ctl + CTL_ABORT, a.err)) break;
+    asm volatile("" ::: "memory");
+    PSTAMP(a, 1, i, 1);
+    const lds_float* Wr = (const lds_float*)as3(lds + a.off_ring + slot * a.slot_bytes);
+    tag_next = ctl[CTL_TAG + ((slot + 1 == a.K) ? 0 : slot + 1)];
+    float wb[PN], wl[PN];
+#pragma unroll
+    for (int s = 0; s < PN; ++s) {
+      wb[s] = Wr[ob[s]];
+      wl[s] = Wr[ol[s]];
+    }
+    if (hist && !(a.dbg & 8)) {
+      float* hr = hist + (row0 + t) * NP;
+#pragma unroll
+      for (int s = 0; s < PN; ++s)
+        if (PN * lane + s < NP) hr[PN * lane + s] = v[s];
+    }
+    float nv[PN];
+    if (a.dbg & 16) {  // timing ablation: no numerator arithmetic
+#pragma unroll
+      for (int s = 0; s < PN; ++s) nv[s] = v[s] + wb[s] + wl[s];
+    } else
+    if constexpr (!REV) {
+      const float prev = from_prev_lane(v[PN - 1], -kInf);
+#pragma unroll
+      for (int s = 0; s < PN; ++s) {
+        const int u = PN * lane + s;
+        const float left = s == 0 ? prev : v[s - 1];
+        const float xl = u >= 1 ? left + wl[s] : -kInf;
+        nv[s] = u < NP ? log_plus2(v[s] + wb[s], xl) : -kInf;
+      }
+    } else {
+      const float next = from_next_lane(v[0], -kInf);
+#pragma unroll
+      for (int s = 0; s < PN; ++s) {
+        const int u = PN * lane + s;
+        const float right = s == PN - 1 ? next : v[s + 1];
+        const float xl = u < U ? wl[s] + right : -kInf;
+        nv[s] = u < NP ? log_plus2(wb[s] + v[s], xl) : -kInf;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < PN; ++s) v[s] = nv[s];
+    asm volatile("" ::: "memory");  // LDS is in order per wave: no wait
+    if (lane == 0) *(ctl + CTL_NUM) = i + 1;
+    PSTAMP(a, 1, i, 2);
+  }
+  if (!REV) {
+    if (a.alpha_num) {
+      for (int t = nf; t < a.T; ++t) {
+        float* hr = a.alpha_num + (row0 + t) * NP;
+#pragma unroll
+        for (int s = 0; s < PN; ++s)
+          if (PN * lane + s < NP) hr[PN * lane + s] = v[s];
+      }
+    }
+    // lattices.py:375-377
+#pragma unroll
+    for (int s = 0; s < PN; ++s) {
+      const int u = PN * lane + s;
+      if (u < NP && u == nl) {
+        ((lds_float*)(as3(lds) + a.off_ctl))[CTL_FIN1] = v[s];
+        if (a.num) a.num[b] = v[s];
+      }
+    }
+    if (lane == 0 && !(nl >= 0 && nl <= U)) {
+      ((lds_float*)(as3(lds) + a.off_ctl))[CTL_FIN1] = -kInf;
+      if (a.num) a.num[b] = -kInf;
+    }
+  }
+}
+
+// ---- helper waves ----------------------------------------------------------
+// Helper hw handles steps hw, hw + NH, ...: loads frame t's weights (element
+// e = lane + 64k, coalesced), the frame max c, E = exp(W - c) scattered into
+// the consumer layout, raw W (fp32) for the numerator, then the slot tag.
+// Loads are unconditional (NL per lane, a compile-time count) and every
+// step issues exactly NL of them, so the compiler's in-order vmcnt waits
+// leave the D-1 younger frames in flight; elements past the frame go to
+// padding / a trash word, so the per-element work is branch-free.
+template <bool BF16, int NL, bool REV>
+LT_DEVINL void helper_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int hw, int lane) {
+  constexpr int D = 60 / NL < 8 ? 60 / NL : 8;  // frames in flight per helper (vmcnt <= 63)
+  lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
+  const int FR = a.FR, R = a.R, NH = a.NH;
+  const int es = BF16 ? 2 : 4;
+  // scattered E offsets (bytes inside a slot) of this lane's elements
+  int pe[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int e = lane + 64 * k;
+    int o = a.soff_c + 8;  // trash word
+    if (e < FR) {
+      const int p = e / R, y = e - (e / R) * R;
+      if (y == 0) {
+        o = a.soff_eb + 4 * p;
+      } else {
+        const int row = REV ? p : y - 1;
+        const int kk = REV ? y - 1 : p;
+        o = a.soff_e + 4 * (row * a.rowE + (kk / a.J) * a.JP + (kk % a.J));
+      }
+    }
+    pe[k] = o;
+  }
+  // W through a buffer descriptor: the frame's byte offset in soffset, the
+  // lane's element in voffset; reads past the tensor return 0 (range check),
+  // reads past the frame are ignored below
+  const unsigned nbytes = (unsigned)__builtin_amdgcn_readfirstlane((int)a.w_bytes);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.W, (short)0, (int)nbytes, 0x00020000);
+  const long long ub = (long long)b * a.T;
+  if (nf <= 0) return;
+  auto issue = [&](float* w, int i) {
+    int ii = i < nf ? i : nf - 1;
+    const int t = REV ? nf - 1 - ii : ii;
+    // frame offset in the voffset (the range check covers voffset + imm)
+    const unsigned foff =
+        (unsigned)__builtin_amdgcn_readfirstlane((int)((ub + t) * (long long)FR * es));
+    const unsigned vb = foff + (unsigned)(lane * es);
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const int vo = (int)(vb + (unsigned)(64 * k * es));
+      if constexpr (BF16)
+        w[k] = __uint_as_float(((unsigned)__builtin_amdgcn_raw_buffer_load_b16(rsrc, vo, 0, 0))
+                               << 16);
+      else
+        w[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vo, 0, 0));
+    }
+    asm volatile("" ::: "memory");
+  };
+  int seen_den = 0, seen_num = 0;
+  int slot = hw;  // slot of step i (advanced by NH per processed step; NH <= K)
+  auto process = [&](const float* w, int i) -> bool {
+    // the slot's previous frame (step i-K) must be consumed
+    const int need = i - a.K + 1;
+    PSTAMP(a, 2 + hw, i, 0);
+    if (need > 0) {
+      if (seen_den < need) {
+        if (!wait_ge(ctl + CTL_DEN, need, ctl + CTL_ABORT, a.err)) return false;
+        seen_den = ctl[CTL_DEN];
+      }
+      if (seen_num < need) {
+        if (!wait_ge(ctl + CTL_NUM, need, ctl + CTL_ABORT, a.err)) return false;
+        seen_num = ctl[CTL_NUM];
+      }
+    }
+    PSTAMP(a, 2 + hw, i, 1);
+    float mx = -kInf;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) mx = fmaxf(mx, lane + 64 * k < FR ? w[k] : -kInf);
+    const float c = safe(wave_max(mx));
+    const float cl = c * kLog2e;
+    unsigned char* sb = lds + a.off_ring + slot * a.slot_bytes;
+    lds_float* Wr = (lds_float*)as3(sb);
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      if (!(a.dbg & 1)) Wr[lane + 64 * k] = w[k];
+      if (!(a.dbg & 2)) *(lds_float*)(as3(sb) + pe[k]) = lt_exp_off(w[k], cl);
+    }
+    if (lane == 0) {
+      *(lds_float*)(as3(sb) + a.soff_c) = c;
+      lds_release_store(ctl + CTL_TAG + slot, i + 1);
+    }
+    PSTAMP(a, 2 + hw, i, 2);
+    return true;
+  };
+  float wv[D][NL];
+#pragma unroll
+  for (int r = 0; r < D; ++r) issue(wv[r], hw + r * NH);
+  bool ok = true;
+  for (int i0 = hw; i0 < nf; i0 += NH * D) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      const int i = i0 + r * NH;
+      if (ok && i < nf) {
+        ok = process(wv[r], i);
+        slot += NH;
+        if (slot >= a.K) slot -= a.K;
+      }
+      issue(wv[r], i + NH * D);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int J, bool BF16, int PN, int D>
+__global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers)) void pipe_kernel(const PArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const bool rev = a.dirs == 2 && (int)blockIdx.x >= a.B;
+  const int b = rev ? (int)blockIdx.x - a.B : (int)blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nthr = blockDim.x;
+  const bool do_den = a.flags & F_DEN;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int NP = a.U + 1;
+
+  // ---- prologue: control block, zeroed ring (E padding stays 0), labels
+  lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
+  for (int k = tid; k < CTL_N; k += nthr) ctl[k] = 0;
+  {
+    const int n16 = (a.K * a.slot_bytes) / 16;
+    lds_float4* ring = (lds_float4*)(as3(lds) + a.off_ring);
+    for (int k = tid; k < n16; k += nthr) ring[k] = lt_f4{0.f, 0.f, 0.f, 0.f};
+    lds_float* gb = (lds_float*)(as3(lds) + a.off_g);
+    lds_float* ubf = (lds_float*)(as3(lds) + a.off_u);
+    for (int k = tid; k < a.rowE + 4; k += nthr) {
+      gb[k] = 0.f;
+      ubf[k] = -kInf;
+    }
+  }
+  int* ctx = (int*)(lds + a.off_ctx);
+  int* ylab = (int*)(lds + a.off_ylab);
+  for (int u = tid; u < a.U; u += nthr) ylab[u] = a.labels[(long long)b * a.U + u];
+  __syncthreads();
+  if (tid == 0) {
+    // walk_states (contexts.py:109-146) with the lattices.py:314-338 label rules
+    const int R = a.R;
+    int c = 0;
+    for (int u = 0; u <= a.U; ++u) {
+      ctx[u] = c * R;
+      if (u < a.U) {
+        int y = ylab[u];
+        if (y < 0 || y > a.V) y = 0;
+        ylab[u] = y < 1 ? 1 : y;
+        if (y != 0) c = y;  // n = 1: next(p, y) = y
+      } else {
+        ylab[u] = 1;
+      }
+    }
+  }
+  if (!do_den && tid == 0) ctl[CTL_DEN] = 0x3fffffff;
+  __syncthreads();
+
+  if (wave == 0) {
+    __builtin_amdgcn_s_setprio(3);
+    if (do_den) {
+      if (rev) den_pipe<J, true>(a, lds, b, nf, lane);
+      else den_pipe<J, false>(a, lds, b, nf, lane);
+    }
+  } else if (wave == 1) {
+    __builtin_amdgcn_s_setprio(2);
+    if (rev) num_pipe<PN, true>(a, lds, b, nf, lane);
+    else num_pipe<PN, false>(a, lds, b, nf, lane);
+  } else if (wave - 2 < a.NH) {
+    constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
+    if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, wave - 2, lane);
+    else helper_pipe<BF16, NL, false>(a, lds, b, nf, wave - 2, lane);
+  }
+  __syncthreads();
+  if (!rev) {
+    if (tid == 0 && a.loss) {
+      const lds_float* fin = (const lds_float*)(as3(lds) + a.off_ctl);
+      const float num = fin[CTL_FIN1];
+      a.loss[b] = (a.flags & F_LOCAL) ? -num : fin[CTL_FIN0] - num;
+    }
+    if (a.arcs) {
+      KArgs ka;
+      ka.arcs = a.arcs;
+      ka.U = a.U;
+      write_arc_table(ka, b, ctx, ylab, tid, nthr);
+    }
+  }
+  (void)NP;
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+int pipe_env(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return (s && *s) ? atoi(s) : dflt;
+}
+
+template <int J, bool BF16, int PN>
+int launch_pipe_t(const PArgs& a, int grid, int threads, int lds, hipStream_t st) {
+  constexpr int D = 4;
+  const void* k = (const void*)pipe_kernel<J, BF16, PN, D>;
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  hipLaunchKernelGGL((pipe_kernel<J, BF16, PN, D>), dim3(grid), dim3(threads), lds, st, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  return LT_OK;
+}
+
+template <int J, bool BF16>
+int launch_pipe_pn(int PN, const PArgs& a, int grid, int threads, int lds, hipStream_t st) {
+  if (PN == 1) return launch_pipe_t<J, BF16, 1>(a, grid, threads, lds, st);
+  if (PN == 2) return launch_pipe_t<J, BF16, 2>(a, grid, threads, lds, st);
+  return launch_pipe_t<J, BF16, 4>(a, grid, threads, lds, st);
+}
+
+template <bool BF16>
+int launch_pipe_j(int J, int PN, const PArgs& a, int grid, int threads, int lds, hipStream_t st) {
+  switch (J) {
+    case 17: return launch_pipe_pn<17, BF16>(PN, a, grid, threads, lds, st);
+    case 5: return launch_pipe_pn<5, BF16>(PN, a, grid, threads, lds, st);
+    case 2: return launch_pipe_pn<2, BF16>(PN, a, grid, threads, lds, st);
+    default: return launch_pipe_pn<1, BF16>(PN, a, grid, threads, lds, st);
+  }
+}
+
+}  // namespace
+
+namespace lt_impl {
+
+bool pipe_eligible(const lt_problem* pb) {
+  if (pipe_env("LT_NO_PIPE", 0)) return false;
+  if (pb->context_size != 1 || pb->vocab_size < 1 || pb->vocab_size > 32) return false;
+  if (pb->max_labels + 1 > 256) return false;
+  const long long C = pb->vocab_size + 1;
+  const long long es = pb->weight_dtype == LT_DTYPE_BF16 ? 2 : 4;
+  const long long bytes = (long long)pb->batch * pb->max_frames * C * C * es;
+  return bytes < 0xFFFFFFF0LL;
+}
+
+int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32_t* nfr,
+                const int32_t* labels, const int32_t* nlab, float* loss, float* log_z,
+                float* num, float* alpha, float* alpha_num, float* beta, float* beta_num,
+                int32_t* arcs, int dirs, int* err, void* stream) {
+  if (!pipe_eligible(pb)) return set_error(LT_EUNSUPPORTED, "pipe: shape not eligible");
+  PArgs a;
+  memset(&a, 0, sizeof(a));
+  const int V = pb->vocab_size, C = V + 1, R = V + 1, FR = C * R, U = pb->max_labels;
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  const int es = bf16 ? 2 : 4;
+  a.W = (const unsigned char*)W;
+  a.nfr = nfr; a.labels = labels; a.nlab = nlab;
+  a.loss = loss; a.log_z = log_z; a.num = num;
+  a.alpha = alpha; a.alpha_num = alpha_num; a.beta = beta; a.beta_num = beta_num;
+  a.arcs = arcs; a.err = err;
+  a.B = pb->batch; a.T = pb->max_frames; a.U = U; a.V = V; a.C = C; a.R = R; a.FR = FR;
+  a.flags = F_NUM | F_LOSS | (local_norm ? F_LOCAL : F_DEN);
+  int p2 = 1;
+  while (p2 < V) p2 *= 2;
+  a.H = 64 / p2;
+  a.lgH = 0;
+  while ((1 << a.lgH) < a.H) ++a.lgH;
+  a.J = V > 16 ? 17 : (V > 8 ? 5 : (V > 4 ? 2 : 1));
+  a.JP = a.J >= 4 ? (a.J + 3) / 4 * 4 : a.J;
+  a.rowE = a.H * a.JP;
+  if (a.H * a.J < C) return set_error(LT_EUNSUPPORTED, "pipe: lane plan");
+  a.NLr = (FR + 63) / 64;
+  a.NH = std::max(1, std::min(kPipeMaxHelpers, pipe_env("LT_PIPE_HELPERS", 4)));
+  a.logn = logf((float)(V + 2));
+  a.dirs = dirs;
+  a.dbg = pipe_env("LT_PIPE_DBG", 0);
+#ifdef LT_STAMPS
+  {
+    const char* sp = getenv("LT_STAMPS_PTR");
+    a.stamps = sp ? (long long*)strtoull(sp, nullptr, 0) : nullptr;
+    a.stamp_block = pipe_env("LT_STAMP_BLOCK", 0);
+  }
+#endif
+  a.w_bytes = (unsigned)((long long)pb->batch * pb->max_frames * FR * es);
+  const int PN = U + 1 <= 64 ? 1 : (U + 1 <= 128 ? 2 : 4);
+  const int NP = U + 1;
+  auto al16 = [](long long x) { return (int)((x + 15) & ~15LL); };
+  int off = 0;
+  a.off_ctl = off; off += al16(CTL_N * 4);
+  a.off_g = off; off += al16((a.rowE + 4) * 4);
+  a.off_u = off; off += al16((a.rowE + 4) * 4);
+  a.off_ctx = off; off += al16(NP * 4);
+  a.off_ylab = off; off += al16(NP * 4);
+  a.off_ring = off;
+  int so = 0;
+  const int NLc = a.J == 17 ? 18 : (a.J == 5 ? 5 : (a.J == 2 ? 2 : 1));
+  if (NLc * 64 < FR) return set_error(LT_EUNSUPPORTED, "pipe: helper load plan");
+  so += al16(NLc * 64 * 4);  // raw W, padded to the helpers' load footprint
+  a.soff_e = so; so += al16((long long)C * a.rowE * 4);
+  a.soff_eb = so; so += al16(C * 4);
+  a.soff_c = so; so += 16;
+  a.slot_bytes = so;
+  // LDS budget: two workgroups per CU when the grid exceeds the CU count
+  const int grid = dirs * pb->batch;
+  int cap = grid > 256 ? 80 * 1024 : 160 * 1024;
+  cap = pipe_env("LT_PIPE_LDS", cap);
+  int K = (cap - off) / so;
+  K = std::min(K, std::min(kPipeMaxSlots, pipe_env("LT_PIPE_SLOTS", 16)));
+  if (K < 2) return set_error(LT_EUNSUPPORTED, "pipe: ring does not fit in LDS");
+  a.K = K;
+  a.NH = std::min(a.NH, K);
+  const int lds = off + K * so;
+  const int threads = 64 * (2 + a.NH);
+  if (grid == 0) return LT_OK;
+  if (pipe_env("LT_VERBOSE", 0))
+    fprintf(stderr, "[lt pipe] V=%d H=%d J=%d JP=%d PN=%d NH=%d K=%d slot=%d lds=%d grid=%d\n",
+            V, a.H, a.J, a.JP, PN, a.NH, K, so, lds, grid);
+  hipStream_t st = (hipStream_t)stream;
+  return bf16 ? launch_pipe_j<true>(a.J, PN, a, grid, threads, lds, st)
+              : launch_pipe_j<false>(a.J, PN, a, grid, threads, lds, st);
+}
+
+}  // namespace lt_impl

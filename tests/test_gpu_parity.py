@@ -337,12 +337,14 @@ def test_full_size_loss_properties_and_determinism(full_size):
   # meet in LDS float atomics, so their summation order may vary run to run
   assert torch.allclose(dW1, dW2, atol=1e-6, rtol=0)
   # checkpointing path: fixed summation order -> bitwise reproducible, and
-  # equal to the recursion backward within rounding
+  # equal to the recursion path within rounding (for the bigram it runs the
+  # scaled linear-space recursions of lt_pipe.hip, a different rounding)
   c1 = nat.loss_forward(W, nf, lab, nl, V, n, False, checkpoints=True)
   d1 = nat.loss_backward(W, nf, lab, nl, *c1[1:5], None, V, n, False, ck=c1[5])
   c2 = nat.loss_forward(W, nf, lab, nl, V, n, False, checkpoints=True)
   d2 = nat.loss_backward(W, nf, lab, nl, *c2[1:5], None, V, n, False, ck=c2[5])
-  assert torch.equal(c1[0], out1[0]) and torch.equal(c1[0], c2[0]) and torch.equal(d1, d2)
+  assert torch.equal(c1[0], c2[0]) and torch.equal(d1, d2)
+  assert ((c1[0] - out1[0]).abs() <= 1e-5 + 1e-6 * out1[0].abs()).all()
   tol = 1e-5 + 2e-6 * out1[1].abs().clamp(min=1.0)[:, None, None, None]
   assert ((d1 - dW1).abs() <= tol).all()
   loss = out1[0]

@@ -38,7 +38,7 @@ def _kernel_key(name):
   if 'bwd_kernel' in name:
     args = name.split('bwd_kernel<', 1)[-1].split('>', 1)[0].split(',')
     return 'bwd_kernel_ck' if len(args) >= 6 and args[5].strip() == 'true' else 'bwd_kernel'
-  for k in ('fwd_kernel', 'marg_kernel', 'backtrace_kernel', 'num_scatter_kernel'):
+  for k in ('fwd_kernel', 'marg_kernel', 'backtrace_kernel', 'num_scatter_kernel', 'pipe_kernel'):
     if k in name:
       return k
   return None
