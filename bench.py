@@ -1,9 +1,12 @@
 """Benchmark: Log-semiring lattice forward-backward (loss + dW) on MI355X.
 
 One step = one pass of the hot path over one batch of synthetic arc weights
-already resident in HBM: lt_loss_forward (fused denominator + numerator
-alpha) then lt_loss_backward (beta + arc marginals -> dW), plus, for N > 1,
-the single RCCL all-reduce of the summed loss.
+already resident in HBM: lt_loss_grad (loss and dW = d(sum loss)/dW; for the
+bigram at B=64 ONE launch in which the alpha and beta recursions run while
+other workgroups turn every frame both have passed into arc marginals), then
+lt_scale_grad with the incoming gradient (ones), plus, for N > 1, the single
+RCCL all-reduce of the summed loss. --design checkpoints /
+recursion time the two-call designs (lt_loss_forward + lt_loss_backward).
 
 Workload (BASELINE.json configs[1], weak-scaled per GPU as configs[2]):
 B=64 utterances per GPU, T=1000 frames, U=100 labels, V=32, bigram FullNGram
@@ -69,9 +72,15 @@ def make_inputs(B, T, U, V, C, device, seed, dtype=torch.float32):
   return W, nf, labels, nl
 
 
-def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, checkpoints=True):
-  """Returns (wall seconds over `steps`, fwd kernel ms list, bwd kernel ms list)."""
+def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, checkpoints=True,
+              fused=False):
+  """Returns (wall seconds over `steps`, fwd kernel ms list, bwd kernel ms list);
+  fused: lt_loss_grad (fwd list) + lt_scale_grad (bwd list)."""
   grad = torch.ones([W.shape[0]], dtype=torch.float32, device=W.device)
+  ws = None
+  if fused:
+    nbytes = _native.loss_grad_workspace_bytes(W, V, n, labels.shape[-1], False)
+    ws = torch.empty([max(nbytes, 1)], dtype=torch.uint8, device=W.device)
   # stand-in weight-fn projection head (512 x 33 fp32, SURVEY 8e) so the
   # step's one collective carries [loss sum || parameter grads]
   head = torch.nn.Parameter(torch.zeros([512, 33], device=W.device))
@@ -80,12 +89,18 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, chec
   def step(ev=None):
     if ev is not None:
       ev[0].record()
-    out = _native.loss_forward(W, nf, labels, nl, V, n, False, checkpoints=checkpoints)
-    loss, log_z, num, alpha, an = out[:5]
-    if ev is not None:
-      ev[1].record()
-    dW = _native.loss_backward(W, nf, labels, nl, log_z, num, alpha, an, grad, V, n, False,
-                               ck=out[5] if checkpoints else None)
+    if fused:
+      loss, _, _, dW = _native.loss_grad(W, nf, labels, nl, V, n, False, workspace=ws)
+      if ev is not None:
+        ev[1].record()
+      _native.scale_grad(dW, grad, V, n)
+    else:
+      out = _native.loss_forward(W, nf, labels, nl, V, n, False, checkpoints=checkpoints)
+      loss, log_z, num, alpha, an = out[:5]
+      if ev is not None:
+        ev[1].record()
+      dW = _native.loss_backward(W, nf, labels, nl, log_z, num, alpha, an, grad, V, n, False,
+                                 ck=out[5] if checkpoints else None)
     if ev is not None:
       ev[2].record()
     if dist_on:
@@ -167,9 +182,10 @@ def main():
   ap.add_argument('--cpu-utts', type=int, default=int(os.environ.get('LT_BENCH_CPU_UTTS', 512)))
   ap.add_argument('--no-north-star', action='store_true')
   ap.add_argument('--design', choices=['auto', 'checkpoints', 'recursion'], default='auto',
-                  help='loss backward: concurrent beta pass + marginal pass (checkpoints), '
-                       'beta recursion with fused marginals (recursion), or the library '
-                       'policy for the batch size (auto)')
+                  help='auto: lt_loss_grad (one fused launch where eligible, else the '
+                       'library policy below); checkpoints: lt_loss_forward with the '
+                       'concurrent beta pass + lt_loss_backward marginal pass; recursion: '
+                       'lt_loss_forward + beta recursion with fused marginals')
   ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'),
                   help='PMC summary of the checkpointing design; *_recursion.json for the other')
   args = ap.parse_args()
@@ -188,8 +204,9 @@ def main():
   W, nf, labels, nl = make_inputs(B, T, U, V, C, device, seed=1234 + rank)
   ckpt = (_native.prefer_checkpoints(B, device) if args.design == 'auto'
           else args.design == 'checkpoints')
+  fused = args.design == 'auto' and _native.fused_path(B, T, U, V, n, device)
   wall, fwd_ms, bwd_ms = run_steps(W, nf, labels, nl, V, n, args.steps, args.warmup, dist_on,
-                                   checkpoints=ckpt)
+                                   checkpoints=ckpt, fused=fused)
 
   t = torch.tensor([wall], dtype=torch.float64, device=device)
   if dist_on:
@@ -201,16 +218,22 @@ def main():
   fwd_b, bwd_b, survey_b = algorithmic_bytes(T, U, V, C, checkpoints=ckpt)
   fwd_avg = float(np.mean(fwd_ms)) * 1e-3
   bwd_avg = float(np.mean(bwd_ms)) * 1e-3
+  if fused:  # one launch does both passes' work (fwd list = lt_loss_grad)
+    fwd_b, bwd_b = fwd_b + bwd_b, 0
   dominant, dom_bytes, dom_s = ('loss_backward', bwd_b * B * T, bwd_avg) \
       if bwd_avg >= fwd_avg else ('loss_forward', fwd_b * B * T, fwd_avg)
   achieved = dom_bytes / dom_s / 1e9
-  if ckpt:
+  if fused:
+    dominant = 'loss_grad'
+    knames = ['pipe_kernel']
+  elif ckpt:
     fk = (['pipe_kernel'] if _native.pipe_path(B, T, U, V, n)
           else ['fwd_kernel', 'bwd_kernel_ck'])
     knames = ['marg_kernel'] if dominant == 'loss_backward' else fk
   else:
     knames = ['bwd_kernel'] if dominant == 'loss_backward' else ['fwd_kernel']
-  pmc = args.pmc if ckpt else args.pmc.replace('.json', '_recursion.json')
+  pmc = (args.pmc.replace('.json', '_fused.json') if fused else
+         args.pmc if ckpt else args.pmc.replace('.json', '_recursion.json'))
   traffic = read_traffic(pmc, knames, B, T)
 
   result = None
@@ -236,7 +259,8 @@ def main():
             'vocab': V, 'context_size': n, 'context_states': C,
             'parallelism': f'utterance-sharded x{world}, RCCL all-reduce of summed loss',
         },
-        'kernels_ms': {'loss_forward': fwd_avg * 1e3, 'loss_backward': bwd_avg * 1e3},
+        'kernels_ms': ({'loss_grad': fwd_avg * 1e3, 'scale_grad': bwd_avg * 1e3} if fused else
+                       {'loss_forward': fwd_avg * 1e3, 'loss_backward': bwd_avg * 1e3}),
         'roofline': {
             'bound': 'hbm',
             'kernel': f"{dominant} ({' || '.join(knames)})",
@@ -248,8 +272,10 @@ def main():
             'algorithmic_bytes_per_frame': {'loss_forward': fwd_b, 'loss_backward': bwd_b,
                                             'survey_step': survey_b},
         },
-        'design': 'checkpointing (alpha || beta, then marginal pass)' if ckpt
-                  else 'recursion backward',
+        'design': ('fused (alpha || beta recursions with concurrent marginal workgroups, '
+                   'one launch)' if fused else
+                   'checkpointing (alpha || beta, then marginal pass)' if ckpt
+                   else 'recursion backward'),
     }
     result['step_gbs'] = survey_b * B * T * world / (wall / args.steps) / 1e9
     result['hbm_frac_step'] = result['step_gbs'] / HBM_PEAK_GBS

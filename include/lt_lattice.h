@@ -140,6 +140,30 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
                      const float* grad, void* dW, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* Loss and its gradient in one call: loss, log_z, num as lt_loss_forward and
+ *   dW = d(sum_b loss_b)/dW   (grad = ones; lt_scale_grad applies another)
+ * -- what RecognitionLattice.forward followed by loss.sum().backward() means
+ * to produce (lattices.py:131-183 with the backward of alignments.py:300-318;
+ * D1/D3 in the reference). Utterances with num = -inf get dW = 0.
+ * For the bigram (FullNGram n = 1, V <= 32, U < 256) with 2B below the CU
+ * count this is ONE launch: the alpha and beta recursions plus workgroups
+ * that turn every frame into marginals as soon as both recursions have
+ * passed it (each frame normalised by its own total, = log_z up to
+ * rounding). Otherwise lt_loss_forward + lt_loss_backward run in turn.
+ *   workspace: lt_loss_grad_workspace_bytes() bytes of device memory. */
+int lt_loss_grad_workspace_bytes(const lt_problem* pb, int32_t local_norm,
+                                 size_t* bytes);
+int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
+                 const int32_t* num_frames, const int32_t* labels,
+                 const int32_t* num_labels, float* loss, float* log_z,
+                 float* num, void* dW, void* workspace, size_t workspace_bytes,
+                 void* stream);
+/* dW[b,...] *= grad[b] in place (grad [B] fp32), the chain rule for an
+ * incoming gradient after lt_loss_grad; utterances with grad[b] == 1 cost
+ * nothing. */
+int lt_scale_grad(const lt_problem* pb, const float* grad, void* dW,
+                  void* stream);
+
 /* RecognitionLattice.shortest_path (lattices.py:185-247) without the
  * cross-batch mask aliasing (D6): MaxTropical Viterbi with the reference's
  * tie rules (blank wins ties, semirings.py:363; first argmax among lexical

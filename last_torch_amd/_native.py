@@ -43,6 +43,10 @@ _SIG = {
     'lt_loss_backward_workspace_bytes': [ctypes.POINTER(Problem), _I32,
                                          ctypes.POINTER(ctypes.c_size_t)],
     'lt_loss_backward': [ctypes.POINTER(Problem), _I32] + [_P] * 14 + [ctypes.c_size_t, _P],
+    'lt_loss_grad_workspace_bytes': [ctypes.POINTER(Problem), _I32,
+                                     ctypes.POINTER(ctypes.c_size_t)],
+    'lt_loss_grad': [ctypes.POINTER(Problem), _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
+    'lt_scale_grad': [ctypes.POINTER(Problem), _P, _P, _P],
     'lt_viterbi_workspace_bytes': [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_size_t)],
     'lt_viterbi': [ctypes.POINTER(Problem), _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t,
                    _P],
@@ -223,6 +227,74 @@ def loss_backward(W, num_frames, labels, num_labels, log_z, num, alpha, alpha_nu
                                 _ptr(num), _ptr(alpha), _ptr(alpha_num), _ptr(beta),
                                 _ptr(beta_num), _ptr(arcs), _ptr(grad), _ptr(dW), _ptr(ws),
                                 ws_bytes.value, _stream()), 'lt_loss_backward')
+  return dW
+
+
+def fused_path(batch, frames, labels, vocab_size, context_size, device=None, bf16=False):
+  """Whether lt_loss_grad runs as ONE fused launch for this shape (mirrors
+  lt_loss_grad: checkpointing batch size, 2B below the CU count, pipe shape;
+  LT_FUSED=0 turns it off)."""
+  if os.environ.get('LT_FUSED', '1') == '0':
+    return False
+  cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
+  return (prefer_checkpoints(batch, device) and 2 * batch < cus and
+          pipe_path(batch, frames, labels, vocab_size, context_size, bf16))
+
+
+def loss_grad_workspace_bytes(W, vocab_size, context_size, max_labels, local_norm):
+  pb = _problem(W, vocab_size, context_size, max_labels)
+  out = ctypes.c_size_t(0)
+  _check(lib().lt_loss_grad_workspace_bytes(ctypes.byref(pb), int(bool(local_norm)),
+                                            ctypes.byref(out)), 'lt_loss_grad_workspace_bytes')
+  return out.value
+
+
+def loss_grad(W, num_frames, labels, num_labels, vocab_size, context_size, local_norm,
+              workspace=None):
+  """lt_loss_grad: (loss, log_z, num, dW) with dW = d(sum loss)/dW in one call
+  (for the bigram a single launch: recursions and marginals overlapped).
+  ``workspace`` (uint8 device tensor of lt_loss_grad_workspace_bytes) is
+  allocated when not given."""
+  U = labels.shape[-1]
+  pb = _problem(W, vocab_size, context_size, U)
+  B = W.shape[0]
+  ws_bytes = ctypes.c_size_t(0)
+  _check(lib().lt_loss_grad_workspace_bytes(ctypes.byref(pb), int(bool(local_norm)),
+                                            ctypes.byref(ws_bytes)),
+         'lt_loss_grad_workspace_bytes')
+  if workspace is None or workspace.numel() < ws_bytes.value:
+    workspace = torch.empty([max(ws_bytes.value, 1)], dtype=torch.uint8, device=W.device)
+  loss, log_z, num = _f32([B], W), _f32([B], W), _f32([B], W)
+  log_z.zero_()
+  dW = torch.empty_like(W)
+  _check(lib().lt_loss_grad(ctypes.byref(pb), int(bool(local_norm)), _ptr(W), _ptr(num_frames),
+                            _ptr(labels), _ptr(num_labels), _ptr(loss), _ptr(log_z), _ptr(num),
+                            _ptr(dW), _ptr(workspace), workspace.numel(), _stream()),
+         'lt_loss_grad')
+  return loss, log_z, num, dW
+
+
+def grad_workspace_errors(workspace, W, vocab_size, context_size, max_labels, local_norm):
+  """The hand-off error word of a fused lt_loss_grad workspace (0 = no
+  timed-out wait); test / diagnostic use, synchronises."""
+  pb = _problem(W, vocab_size, context_size, max_labels)
+  C = num_context_states(vocab_size, context_size)
+  B, T = W.shape[:2]
+  NP = max_labels + 1
+  up = lambda x: (x + 255) & ~255
+  off = 0
+  if not local_norm:
+    off += 2 * up(4 * B * T * C)
+  off += 2 * up(4 * B * T * NP) + up(4 * B * 4 * NP)
+  del pb
+  return int(workspace[off + 8:off + 12].view(torch.int32).item())
+
+
+def scale_grad(dW, grad, vocab_size, context_size):
+  """lt_scale_grad: dW[b] *= grad[b] in place (no work where grad[b] == 1)."""
+  pb = _problem(dW, vocab_size, context_size)
+  _check(lib().lt_scale_grad(ctypes.byref(pb), _ptr(grad.float().contiguous()), _ptr(dW),
+                             _stream()), 'lt_scale_grad')
   return dW
 
 

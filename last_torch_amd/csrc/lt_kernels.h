@@ -1400,5 +1400,6 @@ bool pipe_eligible(const lt_problem* pb);
 int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32_t* nfr,
                 const int32_t* labels, const int32_t* nlab, float* loss, float* log_z,
                 float* num, float* alpha, float* alpha_num, float* beta, float* beta_num,
-                int32_t* arcs, int dirs, int* err, void* stream);
+                int32_t* arcs, int dirs, int* err, void* stream, void* dW = nullptr,
+                int* fctl = nullptr);
 }  // namespace lt_impl

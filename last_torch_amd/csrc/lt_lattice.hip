@@ -672,6 +672,57 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
   return LT_OK;
 }
 
+// dW[b] *= grad[b] for lt_scale_grad (the incoming gradient of a fused
+// lt_loss_grad); workgroups of utterances with grad[b] == 1 return at once.
+template <bool BF16>
+__global__ __launch_bounds__(256) void scale_kernel(void* dW, const float* grad, long long per,
+                                                    int chunks) {
+  const int b = blockIdx.x / chunks, c = blockIdx.x - (blockIdx.x / chunks) * chunks;
+  const float g = grad[b];
+  if (g == 1.f) return;
+  const long long lo = per * c / chunks, hi = per * (c + 1) / chunks;
+  const long long base = (long long)b * per;
+  for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) {
+    if constexpr (BF16) {
+      unsigned short* p = (unsigned short*)dW + base + e;
+      *p = f2bf(__uint_as_float((unsigned)*p << 16) * g);
+    } else {
+      float* p = (float*)dW + base + e;
+      *p *= g;
+    }
+  }
+}
+
+int cu_count() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return cus;
+}
+
+// lt_loss_grad workspace: checkpoints, arc table, hand-off counters and the
+// recursion backward's side buffer, each 256-byte aligned
+struct GradWs {
+  size_t alpha, beta, an, bn, arcs, ctl, side, total;
+};
+GradWs grad_ws(const lt_problem* pb, int local_norm) {
+  GradWs w;
+  const long long B = pb->batch, T = pb->max_frames, NP = pb->max_labels + 1;
+  NGram g;
+  make_ngram(pb->vocab_size, pb->context_size, &g);
+  auto up = [](long long x) { return (size_t)((x + 255) & ~255LL); };
+  size_t o = 0;
+  w.alpha = o; o += local_norm ? 0 : up(4 * B * T * g.C);
+  w.beta = o; o += local_norm ? 0 : up(4 * B * T * g.C);
+  w.an = o; o += up(4 * B * T * NP);
+  w.bn = o; o += up(4 * B * T * NP);
+  w.arcs = o; o += up(4 * B * 4 * NP);
+  w.ctl = o; o += up(4 * (4 + 4 * B));
+  w.side = o; o += up((long long)side_bytes(pb));
+  w.total = o;
+  return w;
+}
+
 }  // namespace
 
 namespace lt_impl {
@@ -967,6 +1018,81 @@ int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
   if (bf16) hipLaunchKernelGGL(backtrace_kernel<true>, dim3(pb->batch), dim3(256), shm, st, bt);
   else hipLaunchKernelGGL(backtrace_kernel<false>, dim3(pb->batch), dim3(256), shm, st, bt);
   return hip_check(hipGetLastError(), "backtrace launch");
+}
+
+int lt_loss_grad_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_t* bytes) {
+  NGram g;
+  int rc = check_problem(pb, &g);
+  if (rc) return rc;
+  if (bytes) *bytes = grad_ws(pb, local_norm).total;
+  return LT_OK;
+}
+
+int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
+                 const int32_t* num_frames, const int32_t* labels, const int32_t* num_labels,
+                 float* loss, float* log_z, float* num, void* dW, void* workspace,
+                 size_t workspace_bytes, void* stream) {
+  NGram g;
+  int rc = check_problem(pb, &g);
+  if (rc) return rc;
+  if (pb->batch == 0) return LT_OK;
+  if (LT_NEED(W) || !num_frames || !num_labels || !loss || !log_z || !num || LT_NEED(dW) ||
+      (pb->max_labels > 0 && !labels))
+    return fail(LT_EINVAL, "null pointer");
+  if (misaligned(W) || misaligned(dW)) return fail(LT_EINVAL, "W/dW must be 16-byte aligned");
+  const GradWs w = grad_ws(pb, local_norm);
+  if (!workspace || workspace_bytes < w.total) return fail(LT_EINVAL, "workspace too small");
+  char* ws = (char*)workspace;
+  float* alpha = local_norm ? nullptr : (float*)(ws + w.alpha);
+  float* beta = local_norm ? nullptr : (float*)(ws + w.beta);
+  float* an = (float*)(ws + w.an);
+  float* bn = (float*)(ws + w.bn);
+  int32_t* arcs = (int32_t*)(ws + w.arcs);
+  const long long ptrs = (long long)pb->batch * pb->max_frames;
+  if (ptrs == 0) {  // T = 0: loss from the empty lattice, dW is empty
+    return lt_loss_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z, num,
+                           alpha, an, nullptr, nullptr, nullptr, stream);
+  }
+  const int cus = cu_count();
+  const bool ck = env_int("LT_CHECKPOINTS", 2 * pb->batch <= cus ? 1 : 0) != 0;
+  // fused: the recursions and the marginal pass in one launch (lt_pipe.hip)
+  if (ck && env_int("LT_FUSED", 1) && 2 * pb->batch < cus && lt_impl::pipe_eligible(pb))
+    return lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
+                                num, alpha, an, beta, bn, arcs, 2, nullptr, stream, dW,
+                                (int*)(ws + w.ctl));
+  if (ck) {
+    if ((rc = lt_loss_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
+                              num, alpha, an, beta, bn, arcs, stream)))
+      return rc;
+    return lt_loss_backward(pb, local_norm, W, num_frames, labels, num_labels, log_z, num,
+                            alpha, an, beta, bn, arcs, nullptr, dW, nullptr, 0, stream);
+  }
+  if ((rc = lt_loss_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z, num,
+                            alpha, an, nullptr, nullptr, nullptr, stream)))
+    return rc;
+  return lt_loss_backward(pb, local_norm, W, num_frames, labels, num_labels, log_z, num, alpha,
+                          an, nullptr, nullptr, nullptr, nullptr, dW, ws + w.side,
+                          workspace_bytes - w.side, stream);
+}
+
+int lt_scale_grad(const lt_problem* pb, const float* grad, void* dW, void* stream) {
+  NGram g;
+  int rc = check_problem(pb, &g);
+  if (rc) return rc;
+  const long long per = (long long)pb->max_frames * g.C * (g.V + 1);
+  if (pb->batch == 0 || per == 0) return LT_OK;
+  if (!grad || LT_NEED(dW)) return fail(LT_EINVAL, "null pointer");
+  const int chunks = (int)std::max<long long>(1, std::min<long long>(64, per / 4096));
+  const long long grid = (long long)pb->batch * chunks;
+  if (grid > 0x7fffffffLL) return fail(LT_EUNSUPPORTED, "grid too large");
+  hipStream_t st = (hipStream_t)stream;
+  if (pb->weight_dtype == LT_DTYPE_BF16)
+    hipLaunchKernelGGL(scale_kernel<true>, dim3((unsigned)grid), dim3(256), 0, st, dW, grad, per,
+                       chunks);
+  else
+    hipLaunchKernelGGL(scale_kernel<false>, dim3((unsigned)grid), dim3(256), 0, st, dW, grad,
+                       per, chunks);
+  return hip_check(hipGetLastError(), "scale launch");
 }
 
 }  // extern "C"

@@ -47,7 +47,7 @@ namespace {
 
 constexpr int kPipeMaxSlots = 32;
 constexpr int kPipeNL = 18;   // helper loads per lane per frame (FR <= 1152)
-constexpr int kPipeMaxHelpers = 6;
+constexpr int kPipeMaxHelpers = 4;  // 6 waves: two workgroups per CU at <= 168 VGPRs
 constexpr float kLoTh = 8.673617379884035e-19f;  // 2^-60
 constexpr float kHiTh = 1.8446744073709552e19f;  // 2^64
 
@@ -79,6 +79,18 @@ struct PArgs {
   int stamp_block;
   int dbg;           // timing ablations (LT_PIPE_DBG): 1 no raw-W stores, 2 no E stores,
                      // 4 no den history, 8 no num history
+  // ---- fused loss + gradient (lt_loss_grad): marginal workgroups in the
+  // same launch consume frames as soon as both recursions have passed them
+  int fused;         // 0: recursions only; 1: + marginal roles (grid > dirs * B)
+  int* prog;         // [4][B] published steps: alpha den, alpha num, beta den, beta num
+  int* qctr;         // [0] role ticket, [1] marginal tile queue
+  void* dW;          // [B,T,C,V+1], W's dtype
+  const char* wsbase;  // workspace holding alpha, beta, alpha_num, beta_num, arcs (< 4 GB)
+  int FW, FT, NB, ntiles;  // frames per marginal wave / tile, tiles per utterance, tiles
+  int moff_ctl, moff_arc, moff_wave, mwave_bytes;  // marginal-role LDS layout
+  int mC4, mNP4, mFR4;     // padded row lengths (floats) in a wave's region
+  long long* trace;  // LT_FUSED_TRACE (diagnostics): [dirs*B][2] recursion start/end,
+                     // then [ntiles][4] tile grab/ready/done/role (s_memrealtime)
 };
 
 #ifdef LT_STAMPS
@@ -128,6 +140,35 @@ LT_DEVINL void lds_release_store(lds_vint* p, int v) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   *p = v;
 }
+
+// ---- cross-workgroup hand-off (fused mode) --------------------------------
+// The recursions' history rows are written with sc1 (write-through) stores and
+// published per direction and wave through an sc1 flag store of the number of
+// completed steps; consumers poll with sc1 loads and read the rows with sc1
+// loads only (MI355X_MICROARCH.md, hand-off table row 1). A step's row is
+// published once the wave's vmcnt shows it complete: vmcnt decrements in
+// issue order, so `s_waitcnt vmcnt(n)` leaves only the n youngest stores
+// outstanding. Publications run every kPubEvery steps, kPubLag steps behind.
+typedef __attribute__((address_space(1))) float g_float;
+typedef __attribute__((address_space(1))) int g_int;
+constexpr int kPubEvery = 16, kPubLag = 8;
+LT_DEVINL void st_sc1(float* p, float v) {
+  __hip_atomic_store((g_float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+LT_DEVINL void st_sc1(int* p, int v) {
+  __hip_atomic_store((g_int*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+LT_DEVINL float ld_sc1(const float* p) {
+  return __hip_atomic_load((g_float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+LT_DEVINL int ld_sc1(const int* p) {
+  return __hip_atomic_load((g_int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#ifdef LT_STAMPS
+#define LT_PUB_WAIT(n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define LT_PUB_WAIT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+#endif
 
 // ---- cross-lane helpers (full exec) -------------------------------------
 template <int CTRL>
@@ -291,6 +332,7 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
   ubuf[pub_pos] = pub0 ? u0 : uo;
   float* hrow = (REV ? a.beta : a.alpha);
   const long long hstep = REV ? -(long long)C : (long long)C;
+  int* pub = a.fused ? a.prog + (REV ? 2 : 0) * a.B + b : nullptr;
   if (hrow) hrow += ((long long)b * a.T + (REV ? nf - 1 : 0)) * C + hist_idx;
 
   // the current step's operands (software-pipelined: step i+1's are loaded
@@ -443,8 +485,13 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     }
     // ---- off-chain work of step i
     if (hrow && !(a.dbg & 4)) {
-      *hrow = hval;
+      st_sc1(hrow, hval);
       hrow += hstep;
+    }
+    if (pub && ((i + 1) % kPubEvery) == 0) {
+      // one store per step: the kPubLag youngest are steps i-7..i
+      LT_PUB_WAIT(8);
+      if (lane == 0) st_sc1(pub, i + 1 - kPubLag);
     }
     if (!bad) {
       // next normaliser: exponent of this frame's max S
@@ -467,6 +514,10 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     if (lane == 0) *(ctl + CTL_DEN) = i + 1;
     PSTAMP(a, 0, i, 2);
     slot = nslot;
+  }
+  if (pub) {  // every step (also after an abort: consumers must not wait forever)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) st_sc1(pub, nf);
   }
   // final vector: padding rows (fwd, lattices.py:460-461) and log_z
   if (!REV) {
@@ -530,6 +581,7 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     else v[s] = (u == nl) ? 0.f : -kInf;
   }
   float* hist = REV ? a.beta_num : a.alpha_num;
+  int* pub = a.fused ? a.prog + (REV ? 3 : 1) * a.B + b : nullptr;
   int tag_next = nf > 0 ? ctl[CTL_TAG] : 0;
   const long long row0 = (long long)b * a.T;
   int slot = 0;
@@ -551,7 +603,7 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
       float* hr = hist + (row0 + t) * NP;
 #pragma unroll
       for (int s = 0; s < PN; ++s)
-        if (PN * lane + s < NP) hr[PN * lane + s] = v[s];
+        if (PN * lane + s < NP) st_sc1(hr + PN * lane + s, v[s]);
     }
     float nv[PN];
     if (a.dbg & 16) {  // timing ablation: no numerator arithmetic
@@ -581,7 +633,18 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     for (int s = 0; s < PN; ++s) v[s] = nv[s];
     asm volatile("" ::: "memory");  // LDS is in order per wave: no wait
     if (lane == 0) *(ctl + CTL_NUM) = i + 1;
+    if (pub && ((i + 1) % kPubEvery) == 0) {
+      // PN stores per step: the kPubLag * PN youngest are steps i-7..i
+      if constexpr (PN == 1) LT_PUB_WAIT(8);
+      else if constexpr (PN == 2) LT_PUB_WAIT(16);
+      else LT_PUB_WAIT(32);
+      if (lane == 0) st_sc1(pub, i + 1 - kPubLag);
+    }
     PSTAMP(a, 1, i, 2);
+  }
+  if (pub) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) st_sc1(pub, nf);
   }
   if (!REV) {
     if (a.alpha_num) {
@@ -721,12 +784,323 @@ LT_DEVINL void helper_pipe(const PArgs& a, unsigned char* lds, int b, int nf, in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---- marginal role (fused mode) ----------------------------------------------
+// dW[b,t,p,y] = den - num marginals of frame t (alignments.py:311-317 for the
+// denominator, the string arcs of lattices.py:314-338 for the numerator), for
+// the gradient of sum_b loss_b. Tiles of FT frames are taken from a queue in
+// the order the two recursions make them ready (middle of the utterance
+// first); each wave of the workgroup then runs FW frames on its own.
+//
+// Normalisers: each frame is normalised by its own total,
+//   log_z = logsumexp_{p,y} alpha_t[p] + W_t[p,y] + beta_{t+1}[next(p,y)]
+// (the forward-backward identity holds at every live frame), and likewise the
+// numerator, so no frame waits for the end of the alpha pass. A frame whose
+// total is zero (log_z = -inf, or an unreachable string: num = -inf at every
+// frame) gets dW = 0, as lt_loss_backward does for those utterances.
+LT_DEVINL int mid_out(int k, int nb) {
+  const int mid = nb >> 1;
+  return (k & 1) ? mid - ((k + 1) >> 1) : mid + (k >> 1);
+}
+
+template <bool BF16, int NL, int PN>
+LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
+  const int tid = threadIdx.x, lane = tid & 63, nthr = blockDim.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int C = a.C, R = a.R, FR = a.FR, NP = a.U + 1, NK = 2 * NP, T = a.T, B = a.B;
+  const bool do_den = a.flags & F_DEN;
+  const int es = BF16 ? 2 : 4;
+  constexpr int PNW = PN;      // numerator row values per lane (NP <= 64 PN)
+  constexpr int NKL = 2 * PN;  // numerator arc slots per lane (NK <= 128 PN)
+  constexpr int D = NL * 64;   // dummy element: Wl[D] = -inf
+  lds_vint* sh = (lds_vint*)(as3(lds) + a.moff_ctl);
+  lds_int* aoff = (lds_int*)(as3(lds) + a.moff_arc);  // [NKL*64] arc element (or D)
+  // this wave's region (padded so that every lane's accesses are in range)
+  lds_float* A = (lds_float*)(as3(lds) + a.moff_wave + wave * a.mwave_bytes);
+  lds_float* Bt = A + 64;
+  lds_float* AN = Bt + 64;
+  lds_float* BN = AN + a.mNP4;
+  lds_float* Wl = BN + a.mNP4;
+  lds_float* Sub = Wl + a.mFR4;
+  if (lane == 0) Wl[D] = -kInf;
+  // this lane's elements e = lane + 64k: source p, destination q (n = 1:
+  // blank stays in p, label y goes to state y; contexts.py:190-205)
+  int pq[NL];  // p | q << 16
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int e = lane + 64 * k;
+    const int p = e / R, y = e - (e / R) * R;
+    pq[k] = e < FR ? (p | ((y == 0 ? p : y) << 16)) : 0;
+  }
+  // numerator arc slots kk = lane + 64s: positions u and u or u+1 (clamped;
+  // invalid slots point at the dummy element, whose -inf term vanishes)
+  int uab[NKL];  // u | (u or u+1) << 16
+#pragma unroll
+  for (int s2 = 0; s2 < NKL; ++s2) {
+    const int kk = lane + 64 * s2;
+    const int u = min(kk >> 1, NP - 1);
+    uab[s2] = u | (min((kk & 1) ? u + 1 : u, NP - 1) << 16);
+  }
+  // buffer descriptors: out-of-range offsets (kOff) read 0 / drop the store,
+  // so the per-element accesses need no branches. The handed-off rows and the
+  // arc table (all in one workspace, < 4 GB) are read with sc1 loads (cache
+  // policy 16): plain buffer loads, not atomics, so nothing orders them
+  // behind this wave's stores.
+  const unsigned nbytes = (unsigned)__builtin_amdgcn_readfirstlane((int)a.w_bytes);
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.W, (short)0, (int)nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr =
+      __builtin_amdgcn_make_buffer_rsrc(a.dW, (short)0, (int)nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wsbase, (short)0, (int)0xFFFFFFF0u, 0x00020000);
+  const unsigned o_al = (unsigned)((const char*)a.alpha - a.wsbase);
+  const unsigned o_be = (unsigned)((const char*)a.beta - a.wsbase);
+  const unsigned o_an = (unsigned)((const char*)a.alpha_num - a.wsbase);
+  const unsigned o_bn = (unsigned)((const char*)a.beta_num - a.wsbase);
+  const unsigned o_ar = (unsigned)((const char*)a.arcs - a.wsbase);
+  constexpr unsigned kOff = 0xFFFFFFF0u;
+  constexpr int kSc1 = 16;
+  for (;;) {
+    if (tid == 0) *sh = atomicAdd(a.qctr + 1, 1);
+    __syncthreads();
+    const int j = *sh;
+    if (j >= a.ntiles) break;
+    long long* tr = a.trace ? a.trace + 2LL * a.dirs * B + 4LL * j : nullptr;
+    if (tr && tid == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
+    const int kb = j / B, b = j - kb * B;
+    const int t0 = mid_out(kb, a.NB) * a.FT, t1 = min(T, t0 + a.FT);
+    int nf = a.nfr[b];
+    nf = nf < 0 ? 0 : (nf > T ? T : nf);
+    const int tl = min(t1, nf);  // live frames of the tile: [t0, tl)
+    if (t0 < tl) {
+      if (tid == 0) {
+        // alpha rows [0, tl) and beta rows [t0, nf) published
+        const int* pg = a.prog;
+        int n = 0;
+        bool ok = true;
+        for (int r = do_den ? 0 : 1; r < 4 && ok; r += do_den ? 1 : 2) {
+          const int need = (r < 2) ? tl : nf - t0;
+          while (ld_sc1(pg + r * B + b) < need) {
+            __builtin_amdgcn_s_sleep(8);
+            if (++n > (1 << 22)) {
+              if (a.err) atomicOr(a.err, 2);
+              ok = false;
+              break;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (tr && tid == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+      for (int k = tid; k < NKL * 64; k += nthr) {
+        const int ro = (int)(k < NK ? o_ar + (unsigned)(((long long)b * 2 * NK + k) * 4) : kOff);
+        const int o = (int)__builtin_amdgcn_raw_buffer_load_b32(xr, ro, 0, kSc1);
+        aoff[k] = (k < NK && o >= 0) ? o : D;
+      }
+      __syncthreads();
+    }
+    // ---- this wave's frames (the next one in flight)
+    const int tw0 = t0 + wave * a.FW, tw1 = min(t1, tw0 + a.FW);
+    const int twl = min(tw1, tl);  // this wave's live frames end
+    const long long ub = (long long)b * T;
+    struct Buf {
+      float w[NL], ra, rb, ran[PNW], rbn[PNW];
+    };
+    Buf X;
+    auto fetch = [&](Buf& f, int t) {
+      if (t >= twl) return;
+      const unsigned vb = (unsigned)__builtin_amdgcn_readfirstlane(
+          (int)((ub + t) * (long long)FR * es)) + (unsigned)(lane * es);
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        const int vo = (int)(lane + 64 * k < FR && !(a.dbg & 2048) ? vb + (unsigned)(64 * k * es)
+                                                                    : kOff);
+        if constexpr (BF16)
+          f.w[k] = __uint_as_float(
+              ((unsigned)__builtin_amdgcn_raw_buffer_load_b16(wr, vo, 0, 0)) << 16);
+        else
+          f.w[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wr, vo, 0, 0));
+      }
+      const unsigned rc = (unsigned)__builtin_amdgcn_readfirstlane((int)((ub + t) * C * 4));
+      const unsigned rn = (unsigned)__builtin_amdgcn_readfirstlane((int)((ub + t) * NP * 4));
+      if (a.dbg & 1024) return;
+      if (do_den) {
+        const unsigned ro = lane < C ? rc + lane * 4 : kOff;
+        f.ra = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(lane < C ? o_al + ro : kOff), 0, kSc1));
+        f.rb = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(lane < C ? o_be + ro : kOff), 0, kSc1));
+      }
+#pragma unroll
+      for (int s = 0; s < PNW; ++s) {
+        const int u = lane + 64 * s;
+        const unsigned ro = rn + u * 4;
+        f.ran[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            xr, (int)(u < NP ? o_an + ro : kOff), 0, kSc1));
+        f.rbn[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            xr, (int)(u < NP ? o_bn + ro : kOff), 0, kSc1));
+      }
+    };
+    auto process = [&](Buf& f, int t) {
+      if (t >= tw1) return;
+      const unsigned vb = (unsigned)__builtin_amdgcn_readfirstlane(
+          (int)((ub + t) * (long long)FR * es)) + (unsigned)(lane * es);
+      float x[NL];  // denominator terms, then the frame's dW values
+#pragma unroll
+      for (int k = 0; k < NL; ++k) x[k] = 0.f;
+      bool zero = t >= tl;
+      if (!zero) {
+        // frame t's operands into this wave's (padded) LDS region
+        A[lane] = f.ra;
+        Bt[lane] = f.rb;
+#pragma unroll
+        for (int s = 0; s < PNW; ++s) {
+          AN[lane + 64 * s] = f.ran[s];
+          BN[lane + 64 * s] = f.rbn[s];
+        }
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+          Wl[lane + 64 * k] = f.w[k];
+          Sub[lane + 64 * k] = 0.f;
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        // denominator terms and the frame total
+        float m = -kInf;
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+          const float xv = A[pq[k] & 0xffff] + f.w[k] + Bt[pq[k] >> 16];
+          x[k] = (do_den && lane + 64 * k < FR) ? xv : -kInf;
+          m = fmaxf(m, x[k]);
+        }
+        fetch(f, t + 1);  // the next frame's loads overlap this one
+        const float md = safe(wave_max(m));
+        float sd = 0.f;
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+          x[k] = lt_exp(x[k] - md);
+          sd += x[k];
+        }
+        sd = wave_sum(sd);
+        const float rd = (sd > 0.f && sd < kInf) ? __builtin_amdgcn_rcpf(sd) : 0.f;
+        // numerator arc terms and their total
+        float xn[NKL];
+        int on[NKL];
+        float mn = -kInf;
+#pragma unroll
+        for (int s = 0; s < NKL; ++s) {
+          on[s] = aoff[lane + 64 * s];
+          xn[s] = AN[uab[s] & 0xffff] + Wl[on[s]] + BN[uab[s] >> 16];
+          mn = fmaxf(mn, xn[s]);
+        }
+        const float mns = safe(wave_max(mn));
+        float sn = 0.f;
+#pragma unroll
+        for (int s = 0; s < NKL; ++s) {
+          xn[s] = lt_exp(xn[s] - mns);
+          sn += xn[s];
+        }
+        sn = wave_sum(sn);
+        const float rn = (sn > 0.f && sn < kInf) ? __builtin_amdgcn_rcpf(sn) : 0.f;
+        zero = (do_den && rd == 0.f) || rn == 0.f;
+        if (a.dbg & 256) zero = false;
+        if (!zero) {
+          // string arcs sharing a lattice arc meet in LDS float adds; one
+          // wave's adds apply in program and lane order (deterministic)
+#pragma unroll
+          for (int s = 0; s < NKL; ++s)
+            __hip_atomic_fetch_add(Sub + on[s], xn[s] * rn, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int k = 0; k < NL; ++k) x[k] = x[k] * rd - Sub[lane + 64 * k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        const float val = zero ? 0.f : x[k];
+        const int vo = (int)(lane + 64 * k < FR && !(a.dbg & 4096) ? vb + (unsigned)(64 * k * es)
+                                                                    : kOff);
+        if constexpr (BF16)
+          __builtin_amdgcn_raw_buffer_store_b16(f2bf(val), dr, vo, 0, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), dr, vo, 0, 0);
+      }
+    };
+    fetch(X, tw0);
+    for (int t = tw0; t < tw1; ++t) process(X, t);
+    __syncthreads();
+    if (tr && tid == 0) {
+      tr[2] = __builtin_amdgcn_s_memrealtime();
+      tr[3] = (long long)blockIdx.x;
+    }
+  }
+}
+
+// arc table of utterance b (lattices.py:314-338 arcs of the string; chains
+// link the string arcs that share a lattice arc) with sc1 stores, for the
+// marginal roles (fused mode)
+LT_DEVINL void write_arcs_sc1(const PArgs& a, int b, const int* ctx, const int* ylab, int tid,
+                              int nthr) {
+  const int NP = a.U + 1, NK = 2 * NP;
+  int* off = a.arcs + (long long)b * 2 * NK;
+  int* link = off + NK;
+  auto arc = [&](int k) {
+    const int u = k >> 1;
+    return (k & 1) == 0 ? ctx[u] : (u < a.U ? ctx[u] + ylab[u] : -1);
+  };
+  for (int k = tid; k < NK; k += nthr) {
+    const int o = arc(k);
+    int head = o >= 0 ? 1 : 0, nxt = -1;
+    if (o >= 0) {
+      for (int k2 = 0; k2 < NK; ++k2) {
+        if (arc(k2) != o) continue;
+        if (k2 < k) head = 0;
+        else if (k2 > k && nxt < 0) nxt = k2;
+      }
+    }
+    st_sc1(off + k, o);
+    st_sc1(link + k, (head << 30) | (nxt + 1));
+  }
+}
+
 template <int J, bool BF16, int PN, int D>
-__global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers)) void pipe_kernel(const PArgs a) {
+__global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers), 4) void pipe_kernel(const PArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const bool rev = a.dirs == 2 && (int)blockIdx.x >= a.B;
-  const int b = rev ? (int)blockIdx.x - a.B : (int)blockIdx.x;
+  int blk = (int)blockIdx.x;
+  if (a.fused) {
+    // roles by arrival: the first dirs*B workgroups to start run the
+    // recursions, so every recursion is resident before any marginal
+    // workgroup waits on it (no dependence on the dispatch order)
+    if (threadIdx.x == 0) *(lds_vint*)as3(lds) = atomicAdd(a.qctr, 1);
+    __syncthreads();
+    blk = *(lds_vint*)as3(lds);
+    __syncthreads();
+    if (a.trace && threadIdx.x == 0) {
+      // [grid][2] after the tile records: start time, (XCC, SE/SH/CU) ids
+      long long* tw = a.trace + 2LL * a.dirs * a.B + 4LL * a.ntiles + 2LL * blockIdx.x;
+      tw[0] = __builtin_amdgcn_s_memrealtime();
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      tw[1] = ((long long)xcc << 32) | hw | ((long long)blk << 40);
+    }
+    if (blk >= a.dirs * a.B) {
+      constexpr int NLm = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
+      marg_role<BF16, NLm, PN>(a, lds);
+      return;
+    }
+  }
+  const bool rev = a.dirs == 2 && blk >= a.B;
+  const int b = rev ? blk - a.B : blk;
   const int tid = threadIdx.x, lane = tid & 63;
+  if (a.fused && (a.dbg & 128)) {  // timing ablation: marginal roles alone
+    if (threadIdx.x < 2) st_sc1(a.prog + ((rev ? 2 : 0) + threadIdx.x) * a.B + b, a.T);
+    return;
+  }
+  if (a.trace && threadIdx.x == 0) a.trace[2 * blk] = __builtin_amdgcn_s_memrealtime();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nthr = blockDim.x;
   const bool do_den = a.flags & F_DEN;
@@ -770,6 +1144,13 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers)) void pipe_kernel(const 
   }
   if (!do_den && tid == 0) ctl[CTL_DEN] = 0x3fffffff;
   __syncthreads();
+  if (a.fused && !rev) {
+    // published with the first steps: every storing wave's stores complete
+    // before the barrier, the publications come after it
+    write_arcs_sc1(a, b, ctx, ylab, tid, nthr);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
 
   if (wave == 0) {
     __builtin_amdgcn_s_setprio(3);
@@ -783,17 +1164,20 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers)) void pipe_kernel(const 
     else num_pipe<PN, false>(a, lds, b, nf, lane);
   } else if (wave - 2 < a.NH) {
     constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
+    // above the marginal roles (priority 0) that share the CU in fused mode
+    if (a.fused && !(a.dbg & 8192)) __builtin_amdgcn_s_setprio(1);
     if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, wave - 2, lane);
     else helper_pipe<BF16, NL, false>(a, lds, b, nf, wave - 2, lane);
   }
   __syncthreads();
+  if (a.trace && tid == 0) a.trace[2 * blk + 1] = __builtin_amdgcn_s_memrealtime();
   if (!rev) {
     if (tid == 0 && a.loss) {
       const lds_float* fin = (const lds_float*)(as3(lds) + a.off_ctl);
       const float num = fin[CTL_FIN1];
       a.loss[b] = (a.flags & F_LOCAL) ? -num : fin[CTL_FIN0] - num;
     }
-    if (a.arcs) {
+    if (a.arcs && !a.fused) {
       KArgs ka;
       ka.arcs = a.arcs;
       ka.U = a.U;
@@ -817,6 +1201,11 @@ int launch_pipe_t(const PArgs& a, int grid, int threads, int lds, hipStream_t st
   const void* k = (const void*)pipe_kernel<J, BF16, PN, D>;
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  if (pipe_env("LT_VERBOSE", 0)) {
+    int occ = -1;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, threads, lds);
+    fprintf(stderr, "[lt pipe] occupancy %d blocks/CU (threads %d, lds %d)\n", occ, threads, lds);
+  }
   hipLaunchKernelGGL((pipe_kernel<J, BF16, PN, D>), dim3(grid), dim3(threads), lds, st, a);
   e = hipGetLastError();
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
@@ -851,14 +1240,17 @@ bool pipe_eligible(const lt_problem* pb) {
   const long long C = pb->vocab_size + 1;
   const long long es = pb->weight_dtype == LT_DTYPE_BF16 ? 2 : 4;
   const long long bytes = (long long)pb->batch * pb->max_frames * C * C * es;
-  return bytes < 0xFFFFFFF0LL;
+  const long long rows = (long long)pb->batch * pb->max_frames * (pb->max_labels + 1) * 4;
+  return bytes < 0xFFFFFFF0LL && rows < 0xFFFFFFF0LL;
 }
 
 int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32_t* nfr,
                 const int32_t* labels, const int32_t* nlab, float* loss, float* log_z,
                 float* num, float* alpha, float* alpha_num, float* beta, float* beta_num,
-                int32_t* arcs, int dirs, int* err, void* stream) {
+                int32_t* arcs, int dirs, int* err, void* stream, void* dW, int* fctl) {
   if (!pipe_eligible(pb)) return set_error(LT_EUNSUPPORTED, "pipe: shape not eligible");
+  const bool fused = dW != nullptr;
+  if (fused && (dirs != 2 || !fctl)) return set_error(LT_EINVAL, "pipe: fused needs both directions");
   PArgs a;
   memset(&a, 0, sizeof(a));
   const int V = pb->vocab_size, C = V + 1, R = V + 1, FR = C * R, U = pb->max_labels;
@@ -912,21 +1304,68 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   a.soff_c = so; so += 16;
   a.slot_bytes = so;
   // LDS budget: two workgroups per CU when the grid exceeds the CU count
-  const int grid = dirs * pb->batch;
-  int cap = grid > 256 ? 80 * 1024 : 160 * 1024;
+  // (fused: always -- marginal workgroups share the CUs)
+  int grid = dirs * pb->batch;
+  int cap = (grid > 256 || fused) ? 80 * 1024 : 160 * 1024;
   cap = pipe_env("LT_PIPE_LDS", cap);
   int K = (cap - off) / so;
   K = std::min(K, std::min(kPipeMaxSlots, pipe_env("LT_PIPE_SLOTS", 16)));
   if (K < 2) return set_error(LT_EUNSUPPORTED, "pipe: ring does not fit in LDS");
   a.K = K;
   a.NH = std::min(a.NH, K);
-  const int lds = off + K * so;
+  int lds = off + K * so;
   const int threads = 64 * (2 + a.NH);
   if (grid == 0) return LT_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (fused) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    a.fused = 1;
+    a.dW = dW;
+    a.qctr = fctl;
+    a.err = fctl + 2;
+    a.prog = fctl + 4;
+    const int nw = threads / 64;
+    a.FW = std::max(1, pipe_env("LT_FUSED_FW", 4));
+    a.FT = a.FW * nw;
+    a.NB = (a.T + a.FT - 1) / a.FT;
+    a.ntiles = a.NB * a.B;
+    const int NK = 2 * NP;
+    a.mC4 = 64;
+    a.moff_ctl = 0;
+    a.moff_arc = 16;
+    const int NLm = a.J == 17 ? 18 : (a.J == 5 ? 5 : (a.J == 2 ? 2 : 1));
+    a.mNP4 = 64 * PN;
+    a.mFR4 = 64 * NLm + 4;
+    a.moff_wave = al16(16 + 4LL * 128 * PN);
+    a.mwave_bytes = 4 * (128 + 2 * a.mNP4 + 2 * a.mFR4);
+    // the recursions' rows and the arc table are read through one descriptor
+    const char* lo = (const char*)alpha_num;
+    const char* hi = (const char*)alpha_num;
+    for (const void* p : {(const void*)alpha, (const void*)beta, (const void*)beta_num,
+                          (const void*)arcs})
+      if (p) {
+        lo = std::min(lo, (const char*)p);
+        hi = std::max(hi, (const char*)p);
+      }
+    const long long span = (hi - lo) + (long long)pb->batch * pb->max_frames * 4 *
+                                           std::max(C, NP) + 4LL * pb->batch * 2 * NK;
+    if (span >= 0xFFFFFFF0LL) return set_error(LT_EUNSUPPORTED, "pipe: fused workspace span");
+    a.wsbase = lo;
+    lds = std::max(lds, a.moff_wave + nw * a.mwave_bytes);
+    lds = std::max(lds, pipe_env("LT_FUSED_LDS", 0));  // e.g. > 80 KB: one workgroup per CU
+    if (const char* tp = getenv("LT_FUSED_TRACE")) a.trace = (long long*)strtoull(tp, nullptr, 0);
+    if (lds > 160 * 1024) return set_error(LT_EUNSUPPORTED, "pipe: fused LDS");
+    const int marg = std::max(1, pipe_env("LT_FUSED_MARG", 2 * cus - grid));
+    grid += marg;
+    const hipError_t e =
+        hipMemsetAsync(fctl, 0, sizeof(int) * (4 + 4LL * pb->batch), st);
+    if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
+  }
   if (pipe_env("LT_VERBOSE", 0))
     fprintf(stderr, "[lt pipe] V=%d H=%d J=%d JP=%d PN=%d NH=%d K=%d slot=%d lds=%d grid=%d\n",
             V, a.H, a.J, a.JP, PN, a.NH, K, so, lds, grid);
-  hipStream_t st = (hipStream_t)stream;
   return bf16 ? launch_pipe_j<true>(a.J, PN, a, grid, threads, lds, st)
               : launch_pipe_j<false>(a.J, PN, a, grid, threads, lds, st);
 }

@@ -70,34 +70,34 @@ def _kernel_weights(W: torch.Tensor) -> torch.Tensor:
 
 
 class _LossFn(torch.autograd.Function):
-  """loss = log_z - num (or -num): lt_loss_forward / lt_loss_backward.
+  """loss = log_z - num (or -num), lattices.py:131-183.
 
-  When a gradient is needed, the forward also runs the backward recursion
-  concurrently (checkpointing mode) so the backward is one streaming pass
-  over the arc marginals."""
+  When W needs a gradient the forward calls lt_loss_grad, which returns the
+  loss together with d(sum loss)/dW -- for the bigram ONE launch in which the
+  alpha and beta recursions run while other workgroups turn every frame they
+  have both passed into arc marginals. The backward then only applies the
+  incoming gradient (lt_scale_grad, in place; free where it is 1). Without a
+  gradient only lt_loss_forward runs."""
 
   @staticmethod
   def forward(ctx, W, nf, labels, nl, V, n, local):
-    ck = ctx.needs_input_grad[0] and _native.prefer_checkpoints(W.shape[0], W.device)
-    out = _native.loss_forward(W, nf, labels, nl, V, n, local, checkpoints=ck)
-    loss, log_z, num, alpha, an = out[:5]
-    beta, beta_num, arcs = out[5] if ck else (None, None, None)
-    dummy = log_z
-    ctx.save_for_backward(W, nf, labels, nl, log_z, num,
-                          alpha if alpha is not None else dummy, an,
-                          beta if beta is not None else dummy,
-                          beta_num if beta_num is not None else dummy,
-                          arcs if arcs is not None else nf)
-    ctx.cfg = (V, n, local, ck)
-    return loss
+    ctx.cfg = (V, n)
+    if ctx.needs_input_grad[0]:
+      loss, _, _, dW = _native.loss_grad(W, nf, labels, nl, V, n, local)
+      ctx.dW = dW
+      return loss
+    ctx.dW = None
+    return _native.loss_forward(W, nf, labels, nl, V, n, local, want_alpha=False)[0]
 
   @staticmethod
   def backward(ctx, g):
-    W, nf, labels, nl, log_z, num, alpha, an, beta, beta_num, arcs = ctx.saved_tensors
-    V, n, local, ck = ctx.cfg
-    cks = ((None if local else beta), beta_num, arcs) if ck else None
-    dW = _native.loss_backward(W, nf, labels, nl, log_z, num, None if local else alpha, an,
-                               g.float().contiguous(), V, n, local, ck=cks)
+    dW = ctx.dW
+    if dW is None:
+      raise RuntimeError('the lattice loss gradient was already consumed: backward through '
+                         'RecognitionLattice.forward twice is not supported (call it again)')
+    ctx.dW = None
+    V, n = ctx.cfg
+    _native.scale_grad(dW, g, V, n)
     return dW, None, None, None, None, None, None
 
 

@@ -266,6 +266,113 @@ def test_random_vs_oracle(cuda, B, T, U, V, n, dt):
   np.testing.assert_array_equal(a.cpu().numpy(), ra)
 
 
+def _poisoned_ws(W, V, n, U, local):
+  # NaN bytes: a stale hand-off read of a checkpoint row would show in dW
+  nb = nat.loss_grad_workspace_bytes(W, V, n, U, local)
+  return torch.full([max(nb, 1)], 0xFF, dtype=torch.uint8, device=W.device)
+
+
+@pytest.mark.parametrize('case', LATTICE_CASES)
+@pytest.mark.parametrize('local', [False, True])
+@pytest.mark.parametrize('fused', ['1', '0'])
+def test_golden_loss_grad(cuda, case, local, fused, monkeypatch):
+  """lt_loss_grad (one launch for the bigram; LT_FUSED=0: the two-call
+  path) against the reference's fixtures."""
+  monkeypatch.setenv('LT_FUSED', fused)
+  c = load(case)
+  W, nf, lab, nl = _dev(c, cuda, 'W_local' if local else 'W')
+  U = lab.shape[-1]
+  ws = _poisoned_ws(W, c['V'], c['n'], U, local)
+  loss, lz, _, dW = nat.loss_grad(W, nf, lab, nl, c['V'], c['n'], local, workspace=ws)
+  torch.cuda.synchronize()
+  assert_loss_close(loss.cpu().numpy(), c['loss_local' if local else 'loss'])
+  if not local:
+    assert_loss_close(lz.cpu().numpy(), c['den_Log'])
+  ref = c['loss_local_grad' if local else 'loss_grad']
+  assert_grad_close(dW.float().cpu().numpy(), ref, c['den_Log'], c['bf16'])
+  if fused == '1' and nat.fused_path(W.shape[0], W.shape[1], U, c['V'], c['n'], cuda,
+                                     W.dtype == torch.bfloat16):
+    assert nat.grad_workspace_errors(ws, W, c['V'], c['n'], U, local) == 0
+
+
+FUSED_RANDOM = [
+    # B, T, U, V, dtype: bigram shapes of the fused launch (V <= 32, U < 256)
+    (8, 200, 30, 32, 'f32'),
+    (8, 200, 30, 32, 'bf16'),
+    (6, 150, 70, 32, 'f32'),    # 2 numerator values per lane
+    (4, 90, 140, 16, 'f32'),    # 4 numerator values per lane
+    (12, 80, 10, 8, 'f32'),
+    (9, 50, 6, 3, 'f32'),
+    (5, 33, 4, 1, 'bf16'),
+    (1, 1, 1, 5, 'f32'),
+]
+
+
+@pytest.mark.parametrize('B,T,U,V,dt', FUSED_RANDOM)
+def test_random_loss_grad_vs_oracle(cuda, B, T, U, V, dt):
+  orc = _orc()
+  n = 1
+  W, nf, lab, nl = _random_problem(B, T, U, V, n, seed=B * 100 + T + U + V)
+  bf16 = dt == 'bf16'
+  if bf16:
+    W = torch.tensor(W).bfloat16().float().numpy()
+  Wd = torch.tensor(W).to(torch.bfloat16 if bf16 else torch.float32).to(cuda)
+  nfd, labd, nld = (torch.tensor(x).to(cuda) for x in (nf, lab, nl))
+  assert nat.fused_path(B, T, U, V, n, cuda, bf16)
+  for local in (False, True):
+    ws = _poisoned_ws(Wd, V, n, U, local)
+    loss, lz, _, dW = nat.loss_grad(Wd, nfd, labd, nld, V, n, local, workspace=ws)
+    rl, rlz, _, rdW = orc.loss_grad(W, nf, lab, nl, V, n, local_norm=local)
+    assert_loss_close(loss.cpu().numpy(), rl)
+    assert_grad_close(dW.float().cpu().numpy(), rdW, rlz, bf16)
+    assert nat.grad_workspace_errors(ws, Wd, V, n, U, local) == 0
+    # deterministic: a second call gives the same bits
+    loss2, _, _, dW2 = nat.loss_grad(Wd, nfd, labd, nld, V, n, local)
+    assert torch.equal(loss, loss2) and torch.equal(dW, dW2)
+
+
+def test_scale_grad(cuda):
+  """lt_scale_grad: dW[b] *= g[b]; utterances with g == 1 are untouched."""
+  V, n = 5, 1
+  g = torch.Generator(device=cuda)
+  g.manual_seed(3)
+  for dt in (torch.float32, torch.bfloat16):
+    dW = torch.randn([5, 7, 6, 6], generator=g, device=cuda).to(dt)
+    ref = dW.clone()
+    gr = torch.tensor([1.0, 0.5, -2.0, 1.0, 0.0], device=cuda)
+    nat.scale_grad(dW, gr, V, n)
+    exp = (ref.float() * gr[:, None, None, None]).to(dt)
+    assert torch.equal(dW, exp)
+    assert torch.equal(dW[0], ref[0]) and torch.equal(dW[3], ref[3])
+
+
+def test_loss_grad_autograd_scaling(cuda):
+  """RecognitionLattice.forward -> (w * loss).sum().backward(): the fused
+  gradient times the incoming per-utterance weights, against the oracle."""
+  orc = _orc()
+  B, T, U, V, n = 6, 40, 8, 7, 1
+  W, nf, lab, nl = _random_problem(B, T, U, V, n, seed=5)
+  table = torch.tensor(W, device=cuda, requires_grad=True)
+  lat = lt.RecognitionLattice(
+      context=lt.contexts.FullNGram(vocab_size=V, context_size=n),
+      alignment=lt.alignments.FrameDependent(),
+      weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+      weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(table))
+  loss = lat(_frames(B, T).to(cuda), torch.tensor(nf), torch.tensor(lab), torch.tensor(nl))
+  w = torch.tensor([0.5, 1.0, 2.0, -1.0, 3.0, 1.0], device=cuda)
+  fin = torch.isfinite(loss.detach())
+  (w * loss.masked_fill(~fin, 0)).sum().backward()
+  rl, rlz, _, rdW = orc.loss_grad(W, nf, lab, nl, V, n)
+  assert_loss_close(loss.detach().cpu().numpy(), rl)
+  scale = (w * fin).cpu().numpy()[:, None, None, None]
+  assert_grad_close(table.grad.cpu().numpy(), rdW * scale, rlz)
+  with pytest.raises(RuntimeError):
+    loss2 = lat(_frames(B, T).to(cuda), torch.tensor(nf), torch.tensor(lab), torch.tensor(nl))
+    s2 = loss2.masked_fill(~fin, 0).sum()
+    s2.backward(retain_graph=True)
+    s2.backward()
+
+
 def test_edge_cases(cuda):
   """Empty utterances, T=0 and U=0, unreachable label strings (+inf loss,
   zero gradient), lengths beyond max (clamped), labels all epsilon."""
