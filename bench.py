@@ -187,7 +187,8 @@ def main():
                        'concurrent beta pass + lt_loss_backward marginal pass; recursion: '
                        'lt_loss_forward + beta recursion with fused marginals')
   ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'),
-                  help='PMC summary of the checkpointing design; *_recursion.json for the other')
+                  help='PMC summary of the checkpointing design; *_fused.json / '
+                       '*_recursion.json for the others')
   args = ap.parse_args()
 
   world = int(os.environ.get('WORLD_SIZE', '1'))

@@ -802,7 +802,9 @@ LT_DEVINL int mid_out(int k, int nb) {
   return (k & 1) ? mid - ((k + 1) >> 1) : mid + (k >> 1);
 }
 
-template <bool BF16, int NL, int PN>
+// EXACT: the frame fills exactly NL slots of 64 (ceil(FR / 64) == NL), so
+// only the last slot is partial; otherwise every slot is checked.
+template <bool BF16, int NL, int PN, bool EXACT>
 LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
   const int tid = threadIdx.x, lane = tid & 63, nthr = blockDim.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -829,8 +831,10 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
   for (int k = 0; k < NL; ++k) {
     const int e = lane + 64 * k;
     const int p = e / R, y = e - (e / R) * R;
-    pq[k] = e < FR ? (p | ((y == 0 ? p : y) << 16)) : 0;
+    pq[k] = e < FR ? (p | ((y == 0 ? p : y) << 16)) : (63 | (63 << 16));  // A[63] = -inf
   }
+  // slot k may hold lanes past the frame (partial)
+  auto partial = [&](int k) { return EXACT ? k == NL - 1 : 64 * (k + 1) > FR; };
   // numerator arc slots kk = lane + 64s: positions u and u or u+1 (clamped;
   // invalid slots point at the dummy element, whose -inf term vanishes)
   int uab[NKL];  // u | (u or u+1) << 16
@@ -910,10 +914,10 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
       if (t >= twl) return;
       const unsigned vb = (unsigned)__builtin_amdgcn_readfirstlane(
           (int)((ub + t) * (long long)FR * es)) + (unsigned)(lane * es);
+      // lanes past the frame read the next frame (or 0 past the tensor): unused
 #pragma unroll
       for (int k = 0; k < NL; ++k) {
-        const int vo = (int)(lane + 64 * k < FR && !(a.dbg & 2048) ? vb + (unsigned)(64 * k * es)
-                                                                    : kOff);
+        const int vo = (int)(vb + (unsigned)(64 * k * es));
         if constexpr (BF16)
           f.w[k] = __uint_as_float(
               ((unsigned)__builtin_amdgcn_raw_buffer_load_b16(wr, vo, 0, 0)) << 16);
@@ -950,8 +954,10 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
       bool zero = t >= tl;
       if (!zero) {
         // frame t's operands into this wave's (padded) LDS region
-        A[lane] = f.ra;
-        Bt[lane] = f.rb;
+        // A[63] = -inf serves the lanes past the frame (and every lane when
+        // there is no denominator)
+        A[lane] = (do_den && lane < C) ? f.ra : -kInf;
+        Bt[lane] = do_den ? f.rb : 0.f;
 #pragma unroll
         for (int s = 0; s < PNW; ++s) {
           AN[lane + 64 * s] = f.ran[s];
@@ -959,7 +965,7 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
         }
 #pragma unroll
         for (int k = 0; k < NL; ++k) {
-          Wl[lane + 64 * k] = f.w[k];
+            Wl[lane + 64 * k] = f.w[k];
           Sub[lane + 64 * k] = 0.f;
         }
         __builtin_amdgcn_wave_barrier();
@@ -968,8 +974,9 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
         float m = -kInf;
 #pragma unroll
         for (int k = 0; k < NL; ++k) {
-          const float xv = A[pq[k] & 0xffff] + f.w[k] + Bt[pq[k] >> 16];
-          x[k] = (do_den && lane + 64 * k < FR) ? xv : -kInf;
+            // past the frame: the next frame's weight (may be +inf) -> -inf
+          if (partial(k) && lane + 64 * k >= FR) f.w[k] = -kInf;
+          x[k] = A[pq[k] & 0xffff] + f.w[k] + Bt[pq[k] >> 16];
           m = fmaxf(m, x[k]);
         }
         fetch(f, t + 1);  // the next frame's loads overlap this one
@@ -977,11 +984,11 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
         float sd = 0.f;
 #pragma unroll
         for (int k = 0; k < NL; ++k) {
-          x[k] = lt_exp(x[k] - md);
+            x[k] = lt_exp(x[k] - md);
           sd += x[k];
         }
         sd = wave_sum(sd);
-        const float rd = (sd > 0.f && sd < kInf) ? __builtin_amdgcn_rcpf(sd) : 0.f;
+        const float rd = (do_den && sd > 0.f && sd < kInf) ? __builtin_amdgcn_rcpf(sd) : 0.f;
         // numerator arc terms and their total
         float xn[NKL];
         int on[NKL];
@@ -1013,20 +1020,27 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
           __builtin_amdgcn_wave_barrier();
           asm volatile("" ::: "memory");
 #pragma unroll
-          for (int k = 0; k < NL; ++k) x[k] = x[k] * rd - Sub[lane + 64 * k];
+          for (int k = 0; k < NL; ++k) {
+                x[k] = x[k] * rd - Sub[lane + 64 * k];
+          }
         }
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
       }
+      if (zero) {
+#pragma unroll
+        for (int k = 0; k < NL; ++k) x[k] = 0.f;
+      }
+      // full slots store as is; the partial last slot only from lanes in the frame
 #pragma unroll
       for (int k = 0; k < NL; ++k) {
-        const float val = zero ? 0.f : x[k];
-        const int vo = (int)(lane + 64 * k < FR && !(a.dbg & 4096) ? vb + (unsigned)(64 * k * es)
-                                                                    : kOff);
+        int vo = (int)(vb + (unsigned)(64 * k * es));
+        if (partial(k) && lane + 64 * k >= FR) vo = (int)kOff;
+        if (a.dbg & 4096) vo = (int)kOff;
         if constexpr (BF16)
-          __builtin_amdgcn_raw_buffer_store_b16(f2bf(val), dr, vo, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b16(f2bf(x[k]), dr, vo, 0, 0);
         else
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), dr, vo, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x[k]), dr, vo, 0, 0);
       }
     };
     fetch(X, tw0);
@@ -1089,7 +1103,8 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers), 4) void pipe_kernel(con
     }
     if (blk >= a.dirs * a.B) {
       constexpr int NLm = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
-      marg_role<BF16, NLm, PN>(a, lds);
+      if ((a.FR + 63) / 64 == NLm) marg_role<BF16, NLm, PN, true>(a, lds);
+      else marg_role<BF16, NLm, PN, false>(a, lds);
       return;
     }
   }

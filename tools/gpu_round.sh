@@ -5,7 +5,7 @@
 set -euo pipefail
 TAG=${1:-r01}
 shift || true
-STEPS=${*:-"test bench prof pmc pmcrec"}
+STEPS=${*:-"test bench prof pmc pmcck pmcrec"}
 OUT=gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -50,6 +50,20 @@ for s in $STEPS; do
         --no-north-star > "$OUT/pmc_write_$TAG.log" 2>&1 \
         || { tail -40 "$OUT/pmc_write_$TAG.log"; exit 1; }
       python tools/pmc_summary.py --fetch "$OUT/pmc_fetch_$TAG" --write "$OUT/pmc_write_$TAG" \
+        --batch 64 --frames 1000 --out "$OUT/${TAG}_pmc_summary_fused.json"
+      ;;
+    pmcck)
+      echo "[gpu_round] PMC passes, checkpointing two-call design"
+      rm -rf "$OUT/pmcc_fetch_$TAG" "$OUT/pmcc_write_$TAG"
+      timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcc_fetch_$TAG" -o fetch \
+        --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-utts 0 \
+        --no-north-star --design checkpoints > "$OUT/pmcc_fetch_$TAG.log" 2>&1 \
+        || { tail -40 "$OUT/pmcc_fetch_$TAG.log"; exit 1; }
+      timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcc_write_$TAG" -o write \
+        --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-utts 0 \
+        --no-north-star --design checkpoints > "$OUT/pmcc_write_$TAG.log" 2>&1 \
+        || { tail -40 "$OUT/pmcc_write_$TAG.log"; exit 1; }
+      python tools/pmc_summary.py --fetch "$OUT/pmcc_fetch_$TAG" --write "$OUT/pmcc_write_$TAG" \
         --batch 64 --frames 1000 --out "$OUT/${TAG}_pmc_summary.json"
       ;;
     pmcrec)
