@@ -46,6 +46,15 @@ def lib():
     for f in ('orc_den_forward', 'orc_num_forward', 'orc_viterbi', 'orc_den_grad',
               'orc_loss_grad'):
       getattr(l, f).restype = None
+    # table_oracle.c: any next-state table, FrameDependent (K=0) or
+    # FrameLabelDependent(K)
+    l.tab_den_forward.argtypes = [_c_int] * 5 + [_I, _F, _I, _c_int, _F, ctypes.c_void_p]
+    l.tab_num_forward.argtypes = [_c_int] * 6 + [_I, _F, _I, _I, _I, _c_int, _F]
+    l.tab_loss_grad.argtypes = ([_c_int] * 6 + [_I, _F, _I, _I, _I, _c_int, ctypes.c_void_p,
+                                                 _F, _F, _F, ctypes.c_void_p])
+    l.tab_viterbi.argtypes = [_c_int] * 5 + [_I, _F, _I, _c_int, _L, _F]
+    for f in ('tab_den_forward', 'tab_num_forward', 'tab_loss_grad', 'tab_viterbi'):
+      getattr(l, f).restype = None
     _lib = l
   return _lib
 
@@ -134,3 +143,64 @@ def loss_grad(W, num_frames, labels, num_labels, V, n, local_norm=False, grad=No
   lib().orc_loss_grad(B, T, U, V, n, W, _i32(num_frames), labels, _i32(num_labels),
                       int(bool(local_norm)), _ptr(g), loss, log_z, num, _ptr(dW))
   return loss, log_z, num, dW
+
+
+# ---------------------------------------------------------------------------
+# table_oracle.c: arbitrary next-state tables and FrameLabelDependent(K)
+# ---------------------------------------------------------------------------
+def full_ngram_table(V, n):
+  """FullNGram.next_state_table() (contexts.py:258-263): [C, V] int32,
+  entry [p, y-1] = next_state(p, y)."""
+  C = num_states(V, n)
+  return np.array([[next_state(V, n, p, y) for y in range(1, V + 1)] for p in range(C)],
+                  np.int32)
+
+
+def _tab(table, W):
+  table = _i32(table)
+  W = _f32(W)
+  C, V = table.shape
+  B, T = W.shape[:2]
+  assert W.shape[2:] == (C, V + 1), (W.shape, table.shape)
+  return table, W, B, T, C, V
+
+
+def tab_den_forward(table, W, num_frames, K, semiring=LOG, want_alpha=False):
+  table, W, B, T, C, V = _tab(table, W)
+  dist = np.zeros([B], np.float32)
+  alpha = np.zeros([B, T, C], np.float32) if want_alpha else None
+  lib().tab_den_forward(B, T, C, V, K, table, W, _i32(num_frames), semiring, dist, _ptr(alpha))
+  return (dist, alpha) if want_alpha else dist
+
+
+def tab_num_forward(table, W, num_frames, labels, num_labels, K, semiring=LOG):
+  table, W, B, T, C, V = _tab(table, W)
+  labels = _i32(labels)
+  U = labels.shape[1]
+  num = np.zeros([B], np.float32)
+  lib().tab_num_forward(B, T, U, C, V, K, table, W, _i32(num_frames), labels, _i32(num_labels),
+                        semiring, num)
+  return num
+
+
+def tab_loss_grad(table, W, num_frames, labels, num_labels, K, local_norm=False, grad=None):
+  """(loss, log_z, num, dW) for any next-state table and alignment K."""
+  table, W, B, T, C, V = _tab(table, W)
+  labels = _i32(labels)
+  U = labels.shape[1]
+  loss, lz, num = (np.zeros([B], np.float32) for _ in range(3))
+  dW = np.zeros_like(W)
+  g = None if grad is None else _f32(grad)
+  lib().tab_loss_grad(B, T, U, C, V, K, table, W, _i32(num_frames), labels, _i32(num_labels),
+                      int(bool(local_norm)), _ptr(g), loss, lz, num, _ptr(dW))
+  return loss, lz, num, dW
+
+
+def tab_viterbi(table, W, num_frames, K, convention=1):
+  """(labels int64 [B, T*A], path weights [B]); A = 1 (K = 0) or K + 1."""
+  table, W, B, T, C, V = _tab(table, W)
+  A = 1 if K == 0 else K + 1
+  labels = np.zeros([B, T * A], np.int64)
+  weight = np.zeros([B], np.float32)
+  lib().tab_viterbi(B, T, C, V, K, table, W, _i32(num_frames), convention, labels, weight)
+  return labels, weight

@@ -9,6 +9,9 @@ LATTICE_CASES = sorted(
     os.path.basename(p)[len('lattice_'):-len('.npz')]
     for p in glob.glob(os.path.join(GOLDEN, 'lattice_*.npz')))
 SEMIRINGS = ('Log', 'MaxTropical', 'Real')
+FLD_CASES = sorted(
+    os.path.basename(p)[len('fld_'):-len('.npz')]
+    for p in glob.glob(os.path.join(GOLDEN, 'fld_*.npz')))
 
 
 def load(name):
@@ -17,6 +20,16 @@ def load(name):
   c['V'] = int(c.pop('vocab_size'))
   c['n'] = int(c.pop('context_size'))
   c['bf16'] = bool(c['bf16'])
+  return c
+
+
+def load_fld(name):
+  """FrameLabelDependent(K) fixtures (tests/golden/make_golden_fld.py)."""
+  with np.load(os.path.join(GOLDEN, f'fld_{name}.npz')) as d:
+    c = {k: d[k] for k in d.files}
+  c['V'] = int(c.pop('vocab_size'))
+  c['n'] = int(c.pop('context_size'))
+  c['K'] = int(c['K'])
   return c
 
 
