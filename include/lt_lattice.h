@@ -180,6 +180,72 @@ int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
                const float* grad, void* arcs, void* workspace,
                size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * General lattices: any context dependency given as a next-state table and
+ * either alignment lattice (lt_table.hip).
+ *   context   contexts.NextStateTable (contexts.py:266-320), or any
+ *             ContextDependency through its next_state_table() (FullNGram:
+ *             contexts.py:258-263); forward_reduce is the (+) over in-arcs
+ *             (the reference's NextStateTable.forward_reduce is defect D8)
+ *   alignment expansions = 0: alignments.FrameDependent (alignments.py:250-329)
+ *             expansions = K >= 1: alignments.FrameLabelDependent(K)
+ *             (alignments.py:331-432), alignment-state-invariant weights
+ *             (lattices.py:444-447)
+ * W has the same [B, T, C, V+1] layout as above with C = num_states.
+ * ------------------------------------------------------------------------ */
+typedef struct lt_graph {
+  int32_t num_states;        /* C */
+  int32_t vocab_size;        /* V */
+  int32_t expansions;        /* K: 0 FrameDependent, K >= 1 FrameLabelDependent */
+  const int32_t* next_state; /* device [C, V]: next_state[p, y-1] (y = 1..V) */
+  const int32_t* in_offsets; /* device [C+1]  } the arcs into each state, from */
+  const int32_t* in_arcs;    /* device [C*V]  } lt_graph_in_arcs()            */
+} lt_graph;
+
+typedef struct lt_table_problem {
+  int32_t batch, max_frames, max_labels, weight_dtype;
+} lt_table_problem;
+
+/* HOST helper: the in-arc CSR of a next-state table (host arrays): arcs
+ * (id = p*V + y-1) grouped by next state, ascending (p, y) inside a group --
+ * the reduce order, which fixes MaxTropical's first-argmax tie rule. */
+int lt_graph_in_arcs(int32_t num_states, int32_t vocab_size, const int32_t* next_state,
+                     int32_t* in_offsets, int32_t* in_arcs);
+
+/* RecognitionLattice._forward (lattices.py:379-496): dist [B], alpha
+ * [B,T,C] (state before frame t; nullable). Log / MaxTropical / Real. */
+int lt_table_forward(const lt_graph* g, const lt_table_problem* pb, int32_t semiring,
+                     const void* W, const int32_t* num_frames, float* dist, float* alpha,
+                     void* stream);
+
+/* RecognitionLattice._string_forward (lattices.py:250-377): num [B]. */
+int lt_table_num_forward(const lt_graph* g, const lt_table_problem* pb, int32_t semiring,
+                         const void* W, const int32_t* num_frames, const int32_t* labels,
+                         const int32_t* num_labels, float* num, void* stream);
+
+/* RecognitionLattice.forward (lattices.py:131-183) and, when dW is non-NULL,
+ * d(sum_b loss_b)/dW (Log; local_norm: loss = -num). Unreachable strings:
+ * loss = +inf, dW = 0. workspace: lt_table_loss_grad_workspace_bytes(). */
+int lt_table_loss_grad_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
+                                       size_t* bytes);
+int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t local_norm,
+                       const void* W, const int32_t* num_frames, const int32_t* labels,
+                       const int32_t* num_labels, float* loss, float* log_z, float* num,
+                       void* dW, void* workspace, size_t workspace_bytes, void* stream);
+
+/* RecognitionLattice.shortest_path (lattices.py:185-247), per utterance (no
+ * D6 aliasing): labels [B, T*A] int64 with A = 1 (FrameDependent) or K+1
+ * (FrameLabelDependent): slot i of frame t = label of the (i+1)-th lexical
+ * arc of that frame (label_convention as lt_viterbi), else 0; the last slot
+ * of a FrameLabelDependent frame is always 0. path_weight [B] = the
+ * MaxTropical distance. workspace: lt_table_viterbi_workspace_bytes(). */
+int lt_table_viterbi_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
+                                     size_t* bytes);
+int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* W,
+                     const int32_t* num_frames, int32_t label_convention, int64_t* labels,
+                     float* path_weight, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
 /* Thread-local description of the last error; never NULL. */
 const char* lt_last_error(void);
 /* Library version string. */

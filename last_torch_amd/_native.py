@@ -32,8 +32,22 @@ class Problem(ctypes.Structure):
               ('max_labels', ctypes.c_int32), ('weight_dtype', ctypes.c_int32)]
 
 
+class Graph(ctypes.Structure):
+  """lt_graph: a next-state table and its in-arc CSR (device pointers)."""
+  _fields_ = [('num_states', ctypes.c_int32), ('vocab_size', ctypes.c_int32),
+              ('expansions', ctypes.c_int32), ('next_state', ctypes.c_void_p),
+              ('in_offsets', ctypes.c_void_p), ('in_arcs', ctypes.c_void_p)]
+
+
+class TableProblem(ctypes.Structure):
+  _fields_ = [('batch', ctypes.c_int32), ('max_frames', ctypes.c_int32),
+              ('max_labels', ctypes.c_int32), ('weight_dtype', ctypes.c_int32)]
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
+_G = ctypes.POINTER(Graph)
+_TP = ctypes.POINTER(TableProblem)
 _SIG = {
     'lt_num_context_states': [_I32, _I32, ctypes.POINTER(ctypes.c_int64)],
     'lt_den_forward': [ctypes.POINTER(Problem), _I32, _P, _P, _P, _P, _P],
@@ -47,6 +61,13 @@ _SIG = {
                                      ctypes.POINTER(ctypes.c_size_t)],
     'lt_loss_grad': [ctypes.POINTER(Problem), _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
     'lt_scale_grad': [ctypes.POINTER(Problem), _P, _P, _P],
+    'lt_graph_in_arcs': [_I32, _I32, _P, _P, _P],
+    'lt_table_forward': [_G, _TP, _I32, _P, _P, _P, _P, _P],
+    'lt_table_num_forward': [_G, _TP, _I32, _P, _P, _P, _P, _P, _P],
+    'lt_table_loss_grad_workspace_bytes': [_G, _TP, ctypes.POINTER(ctypes.c_size_t)],
+    'lt_table_loss_grad': [_G, _TP, _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
+    'lt_table_viterbi_workspace_bytes': [_G, _TP, ctypes.POINTER(ctypes.c_size_t)],
+    'lt_table_viterbi': [_G, _TP, _P, _P, _I32, _P, _P, _P, ctypes.c_size_t, _P],
     'lt_viterbi_workspace_bytes': [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_size_t)],
     'lt_viterbi': [ctypes.POINTER(Problem), _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t,
                    _P],
@@ -314,3 +335,105 @@ def viterbi(W, num_frames, vocab_size, context_size, label_convention, grad=None
                           _ptr(labels), _ptr(weight), _ptr(grad), _ptr(arcs), _ptr(ws),
                           ws_bytes.value, _stream()), 'lt_viterbi')
   return labels, weight, arcs
+
+
+# ---------------------------------------------------------------------------
+# General lattices (lt_table.hip): any next-state table, FrameDependent (K=0)
+# or FrameLabelDependent(K)
+# ---------------------------------------------------------------------------
+class TableGraph:
+  """Device copy of a next-state table [C, V] (entry [p, y-1] = next state)
+  with its in-arc CSR, for alignment expansions K (0 = FrameDependent)."""
+
+  def __init__(self, next_state_table, expansions, device):
+    import numpy as np
+    tab = torch.as_tensor(next_state_table).to(torch.int32).cpu().contiguous()
+    if tab.ndim != 2 or 0 in tab.shape:
+      raise ValueError(f'next_state_table must be a non-empty [C, V] table, got {tuple(tab.shape)}')
+    C, V = tab.shape
+    tab_np = tab.numpy()
+    in_off = np.zeros([C + 1], np.int32)
+    in_arc = np.zeros([C * V], np.int32)
+    _check(lib().lt_graph_in_arcs(C, V, tab_np.ctypes.data_as(_P), in_off.ctypes.data_as(_P),
+                                  in_arc.ctypes.data_as(_P)), 'lt_graph_in_arcs')
+    self.C, self.V, self.K = int(C), int(V), int(expansions)
+    self.table = tab.to(device)
+    self.in_off = torch.from_numpy(in_off).to(device)
+    self.in_arc = torch.from_numpy(in_arc).to(device)
+    self.g = Graph(self.C, self.V, self.K, self.table.data_ptr(), self.in_off.data_ptr(),
+                   self.in_arc.data_ptr())
+
+  def num_alignment_states(self):
+    return 1 if self.K == 0 else self.K + 1
+
+
+def _tproblem(graph, W, max_labels=0):
+  if W.dtype not in (torch.float32, torch.bfloat16):
+    raise TypeError(f'arc weights must be float32 or bfloat16, got {W.dtype}')
+  if not W.is_cuda:
+    raise LatticeLibraryError('lattice kernels need the arc weights on a ROCm device')
+  if not W.is_contiguous():
+    raise ValueError('arc weights must be contiguous')
+  B, T, C, R = W.shape
+  if C != graph.C or R != graph.V + 1:
+    raise ValueError(f'arc weights {tuple(W.shape)} do not match the graph (C={graph.C}, '
+                     f'V+1={graph.V + 1})')
+  return TableProblem(B, T, max_labels, LT_DTYPE_BF16 if W.dtype == torch.bfloat16 else LT_DTYPE_F32)
+
+
+def table_forward(graph, W, num_frames, semiring, want_alpha=True):
+  """lt_table_forward: (dist [B], alpha [B,T,C] or None)."""
+  pb = _tproblem(graph, W)
+  B, T = W.shape[:2]
+  dist = _f32([B], W)
+  alpha = _f32([B, T, graph.C], W) if want_alpha else None
+  _check(lib().lt_table_forward(ctypes.byref(graph.g), ctypes.byref(pb), semiring, _ptr(W),
+                                _ptr(num_frames), _ptr(dist), _ptr(alpha), _stream()),
+         'lt_table_forward')
+  return dist, alpha
+
+
+def table_num_forward(graph, W, num_frames, labels, num_labels, semiring):
+  pb = _tproblem(graph, W, labels.shape[-1])
+  num = _f32([W.shape[0]], W)
+  _check(lib().lt_table_num_forward(ctypes.byref(graph.g), ctypes.byref(pb), semiring, _ptr(W),
+                                    _ptr(num_frames), _ptr(labels), _ptr(num_labels), _ptr(num),
+                                    _stream()), 'lt_table_num_forward')
+  return num
+
+
+def table_loss_grad(graph, W, num_frames, labels, num_labels, local_norm, want_grad=True):
+  """lt_table_loss_grad: (loss, log_z, num, dW = d(sum loss)/dW or None)."""
+  pb = _tproblem(graph, W, labels.shape[-1])
+  B = W.shape[0]
+  nbytes = ctypes.c_size_t(0)
+  _check(lib().lt_table_loss_grad_workspace_bytes(ctypes.byref(graph.g), ctypes.byref(pb),
+                                                  ctypes.byref(nbytes)),
+         'lt_table_loss_grad_workspace_bytes')
+  ws = (torch.empty([max(nbytes.value, 1)], dtype=torch.uint8, device=W.device)
+        if want_grad else None)
+  loss, log_z, num = _f32([B], W), _f32([B], W), _f32([B], W)
+  dW = torch.empty_like(W) if want_grad else None
+  _check(lib().lt_table_loss_grad(ctypes.byref(graph.g), ctypes.byref(pb), int(bool(local_norm)),
+                                  _ptr(W), _ptr(num_frames), _ptr(labels), _ptr(num_labels),
+                                  _ptr(loss), _ptr(log_z), _ptr(num), _ptr(dW), _ptr(ws),
+                                  nbytes.value if want_grad else 0, _stream()),
+         'lt_table_loss_grad')
+  return loss, log_z, num, dW
+
+
+def table_viterbi(graph, W, num_frames, label_convention):
+  """lt_table_viterbi: (labels int64 [B, T*A], path weights [B])."""
+  pb = _tproblem(graph, W)
+  B, T = W.shape[:2]
+  nbytes = ctypes.c_size_t(0)
+  _check(lib().lt_table_viterbi_workspace_bytes(ctypes.byref(graph.g), ctypes.byref(pb),
+                                                ctypes.byref(nbytes)),
+         'lt_table_viterbi_workspace_bytes')
+  ws = torch.empty([max(nbytes.value, 1)], dtype=torch.uint8, device=W.device)
+  labels = torch.empty([B, T * graph.num_alignment_states()], dtype=torch.int64, device=W.device)
+  weight = _f32([B], W)
+  _check(lib().lt_table_viterbi(ctypes.byref(graph.g), ctypes.byref(pb), _ptr(W),
+                                _ptr(num_frames), label_convention, _ptr(labels), _ptr(weight),
+                                _ptr(ws), nbytes.value, _stream()), 'lt_table_viterbi')
+  return labels, weight

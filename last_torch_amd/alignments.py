@@ -1,10 +1,11 @@
 """Alignment lattices (mirrors last_torch/alignments.py).
 
-``FrameDependent`` is the alignment the HIP kernels implement: every arc
-advances one frame, so the recursion over frames is row-synchronous over
-the context states. The per-frame methods below are the
-plugin surface (alignments.py:54-230), evaluated with torch ops on any
-device; ``RecognitionLattice`` does not call them on its hot path.
+``FrameDependent`` and ``FrameLabelDependent(K)`` are both run by HIP
+kernels: FrameDependent x FullNGram by the tuned kernels (lt_lattice.hip,
+lt_pipe.hip), everything else by the general table kernels (lt_table.hip).
+The per-frame methods below are the plugin surface (alignments.py:54-230),
+evaluated with torch ops on any device; ``RecognitionLattice`` does not
+call them on its hot path.
 """
 import abc
 from collections.abc import Sequence
@@ -117,3 +118,72 @@ class FrameDependent(TimeSyncAlignmentLattice):
     check_num_weights(self, blank, lexical)
     return semiring.plus(semiring.times(alpha, blank[0]),
                          shift_down(semiring.times(alpha, lexical[0]), semiring))
+
+
+class FrameLabelDependent(TimeSyncAlignmentLattice):
+  """Each frame emits up to ``max_expansions`` lexical labels followed by one
+  blank (alignments.py:331-432). Alignment state i counts the lexical labels
+  emitted so far in the frame."""
+
+  def __init__(self, max_expansions: int) -> None:
+    super().__init__()
+    self.max_expansions = max_expansions
+
+  def num_states(self) -> int:
+    return self.max_expansions + 1
+
+  def start(self) -> int:
+    return 0
+
+  def blank_next(self, state: int) -> Optional[int]:
+    return 0
+
+  def lexical_next(self, state: int) -> Optional[int]:
+    nxt = state + 1
+    return nxt if nxt <= self.max_expansions else None
+
+  def topological_visit(self) -> list[int]:
+    return list(range(self.max_expansions + 1))
+
+  def forward(self, alpha, blank, lexical, context, semiring):
+    """alignments.py:363-377: sum_i (L^i alpha) (x) blank[i]."""
+    check_num_weights(self, blank, lexical)
+    terminated = [semiring.times(alpha, blank[0])]
+    last = alpha
+    for i in range(self.max_expansions):
+      last = context.forward_reduce(semiring.times(last[..., None], lexical[i]), semiring)
+      terminated.append(semiring.times(last, blank[i + 1]))
+    return semiring.sum(torch.stack(terminated), dim=0)
+
+  def backward(self, alpha, blank, lexical, beta, log_z, context):
+    """alignments.py:379-419: (beta_t, blank marginals [K+1], lexical
+    marginals [K+1], the last all zero) of one frame, Log semiring."""
+    check_num_weights(self, blank, lexical)
+    K = self.max_expansions
+    la = [alpha]
+    last = alpha
+    for i in range(K):
+      last = context.forward_reduce(last[..., None] + lexical[i], semirings.Log)
+      la.append(last)
+    scale = beta - log_z[..., None]
+    blank_marginals = [torch.exp(la[i] + blank[i] + scale) for i in range(K + 1)]
+    next_beta = blank[K] + beta
+    lexical_marginals = []
+    for i in range(K):
+      j = K - 1 - i
+      lexical_beta = lexical[j] + context.backward_broadcast(next_beta)
+      lexical_marginals.append(torch.exp(lexical_beta + (la[j] - log_z[..., None])[..., None]))
+      next_beta = semirings.Log.plus(blank[j] + beta, semirings.Log.sum(lexical_beta, dim=-1))
+    lexical_marginals.reverse()
+    lexical_marginals.append(torch.zeros_like(lexical[K]))
+    return next_beta, blank_marginals, lexical_marginals
+
+  def string_forward(self, alpha, blank, lexical, semiring):
+    """alignments.py:421-432 on the string acceptor (shift_down)."""
+    check_num_weights(self, blank, lexical)
+    terminated = [semiring.times(alpha, blank[0])]
+    last = alpha
+    for i in range(self.max_expansions):
+      last = shift_down(semiring.times(last, lexical[i]), semiring)
+      terminated.append(semiring.times(last, blank[i + 1]))
+    return semiring.sum(torch.stack(terminated), dim=0)

@@ -1,10 +1,11 @@
 """Context dependencies (mirrors last_torch/contexts.py).
 
-``FullNGram`` is the context DFA the HIP kernels implement natively (its
-index maps are evaluated in-kernel: DESIGN.md, "FullNGram index maps").
-The tensor methods below are the per-frame plugin surface
-(contexts.py:43-146); ``RecognitionLattice`` does not call them on its hot
-path.
+``FullNGram`` is the context DFA the tuned HIP kernels implement natively
+(its index maps are evaluated in-kernel: DESIGN.md). ``NextStateTable`` (any
+DFA as a transition table) runs on the general table kernels
+(lt_table.hip), which take any context through ``next_state_table()``. The
+tensor methods below are the per-frame plugin surface (contexts.py:43-146);
+``RecognitionLattice`` does not call them on its hot path.
 """
 import abc
 import dataclasses
@@ -128,3 +129,62 @@ class FullNGram(ContextDependency):
       raise ValueError(f'weights.shape[-1] should be {C} but got {weights.shape[-1]}')
     dst = self._arc_index(weights.device)
     return weights[..., dst].reshape(*weights.shape[:-1], C, V)
+
+
+@dataclasses.dataclass(frozen=True)
+class NextStateTable(ContextDependency):
+  """Context dependency described as a transition table (contexts.py:266-320).
+
+  next_state_table: [num_states, vocab_size] int32; entry [p, y-1] is the
+  state reached from p with label y.
+  """
+  next_state_table: torch.Tensor
+
+  def __post_init__(self):
+    t = self.next_state_table
+    if t.ndim != 2:
+      raise ValueError('next_state_table should have shape [num_states, vocab_size], but'
+                       f'got shape {t.shape}')
+    if 0 in t.size():
+      raise ValueError('next_state_table should have a non-zero size, but '
+                       f'got shape {t.shape}')
+    if t.dtype != torch.int32:
+      raise ValueError('next_state_table should be an int32 ndarray, but '
+                       f'got dtype {t.dtype}')
+
+  def shape(self) -> tuple[int, int]:
+    return tuple(self.next_state_table.shape)
+
+  def start(self) -> int:
+    return 0
+
+  def next_state(self, state, label):
+    """contexts.py:291-298: epsilon (0) stays."""
+    state = torch.as_tensor(state)
+    label = torch.as_tensor(label)
+    is_eps = label == 0
+    zb = torch.where(is_eps, 0, label - 1)
+    nxt = self.next_state_table[state.long(), zb.long()]
+    return torch.where(is_eps, state.to(nxt.dtype), nxt)
+
+  def forward_reduce(self, weights, semiring):
+    """(+) of weights[..., p, y-1] over the arcs into each state. The
+    reference scatters with 'sum' and then takes a max (contexts.py:300-313,
+    SURVEY D8), which is no semiring sum; this is the intended reduction."""
+    C, V = self.shape()
+    if tuple(weights.shape[-2:]) != (C, V):
+      raise ValueError(f'weights.shape[-2:] should be {(C, V)} but got {tuple(weights.shape[-2:])}')
+    table = self.next_state_table.to(weights.device)
+    flat = weights.reshape(*weights.shape[:-2], C * V)
+    out = []
+    for q in range(C):
+      idx = torch.nonzero(table.reshape(-1) == q).reshape(-1)  # ascending (p, y)
+      out.append(semiring.sum(flat.index_select(-1, idx), dim=-1))
+    return torch.stack(out, dim=-1)
+
+  def backward_broadcast(self, weights):
+    """contexts.py:315-320: [..., C] -> [..., C, V] = weights[next_state]."""
+    if weights.shape[-1] != self.shape()[0]:
+      raise ValueError(f'weights.shape[-1] should be {self.shape()[0]} but '
+                       f'got {weights.shape[-1]}')
+    return weights[..., self.next_state_table.to(weights.device).long()]

@@ -1,0 +1,734 @@
+// lt_table.hip -- recognition-lattice kernels for ANY context dependency given
+// as a next-state table and for both alignment lattices (reference
+// file:line in last_torch/):
+//   context   NextStateTable                       contexts.py:266-320
+//             (or FullNGram.next_state_table()     contexts.py:258-263)
+//   alignment FrameDependent          (K = 0)      alignments.py:250-329
+//             FrameLabelDependent(K)  (K >= 1)     alignments.py:331-432
+// driven as RecognitionLattice._forward / _string_forward / forward /
+// shortest_path do (lattices.py:131-496), with alignment-state-invariant
+// weights (lattices.py:444-447): every expansion of a frame uses the same W.
+//
+// forward_reduce is the (+) over each state's in-arcs (its intended
+// semantics; the reference's NextStateTable.forward_reduce is defect D8).
+// The in-arcs come as a CSR over the next state, ascending (source, label)
+// -- the order FullNGram.forward_reduce reduces in, which fixes the
+// MaxTropical tie rule (first argmax, semirings.py:382).
+//
+// One workgroup per utterance; the state vectors live in LDS and each frame
+// is a few barrier-separated sweeps over the states (one per expansion). The
+// FullNGram x FrameDependent shapes of the benchmark use the tuned kernels
+// of lt_lattice.hip / lt_pipe.hip; this file is the general path.
+#include <vector>
+
+#include "lt_kernels.h"
+
+namespace {
+
+struct TArgs {
+  const unsigned char* W;
+  const int* nfr;
+  const int* table;   // [C, V] next state of (p, y)
+  const int* in_off;  // [C+1]
+  const int* in_arc;  // [C*V] arc id p*V + (y-1), grouped by next state
+  const int* labels;  // [B, U]
+  const int* nlab;    // [B]
+  float* dist;        // den: distance [B]; num: numerator [B]
+  float* alpha;       // history [B,T,S] (state before frame t), nullable
+  float* loss;        // num forward with dist_in: loss [B]
+  const float* den_in;  // log_z [B] (num forward: loss = log_z - num)
+  const float* num_in;  // numerator [B] (backward)
+  const float* hist;    // backward: alpha history [B,T,S]
+  float* dW;            // fp32 gradient (bf16 W: a workspace copy, converted at the end)
+  int* bp;              // Viterbi: [B,T,KK,C] winning in-arc position (-1: blank)
+  unsigned char* win;   // Viterbi, K >= 1: [B,T,C] winning expansion count
+  int* qstar;           // Viterbi: [B] best final state
+  long long* vlabels;   // Viterbi: [B, T*A]
+  int B, T, U, C, V, R, K, conv, local;
+};
+
+LT_DEVINL float t_safe(float x) { return __builtin_isfinite(x) ? x : 0.f; }
+// _LogAddExp (semirings.py:248-255)
+LT_DEVINL float t_lae(float a, float b) {
+  const float m = fmaxf(a, b);
+  const float c = t_safe(m);
+  return c + lt_log(lt_exp(a - c) + lt_exp(b - c));
+}
+// running logsumexp (m, s): the result is m + log(s) with the safe max
+struct Lse {
+  float m = -kInf, s = 0.f;
+  LT_DEVINL void add(float x) {
+    if (x == -kInf) return;
+    if (x > m) {
+      s = s * lt_exp(m - x) + 1.f;
+      m = x;
+    } else {
+      s += lt_exp(x - m);
+    }
+  }
+  LT_DEVINL float get() const { return s > 0.f ? m + lt_log(s) : -kInf; }
+};
+
+template <int SR>
+LT_DEVINL float t_zero() { return SR == M_REAL ? 0.f : -kInf; }
+template <int SR>
+LT_DEVINL float t_one() { return SR == M_REAL ? 1.f : 0.f; }
+template <int SR>
+LT_DEVINL float t_times(float a, float b) { return SR == M_REAL ? a * b : a + b; }
+
+// Graph accessors: the context lattice (states p, in-arcs from the CSR) and
+// the string acceptor (positions u, one in-arc from u-1; lattices.py:314-338).
+struct DenGraph {
+  const int* in_off;
+  const int* in_arc;
+  int V, R;
+  LT_DEVINL int blank(int q) const { return q * R; }
+  LT_DEVINL int nin(int q) const { return in_off[q + 1] - in_off[q]; }
+  LT_DEVINL int pos0(int q) const { return in_off[q]; }
+  LT_DEVINL void arc(int pos, int q, int* src, int* widx) const {
+    (void)q;
+    const int id = in_arc[pos];
+    const int p = id / V;
+    *src = p;
+    *widx = p * R + (id - p * V) + 1;
+  }
+};
+struct NumGraph {
+  const int* ctx;  // [S] ctx state * R
+  const int* yn;   // [S] label class of the arc leaving u
+  LT_DEVINL int blank(int u) const { return ctx[u]; }
+  LT_DEVINL int nin(int u) const { return u >= 1 ? 1 : 0; }
+  LT_DEVINL int pos0(int u) const { return u - 1; }
+  LT_DEVINL void arc(int pos, int u, int* src, int* widx) const {
+    (void)pos;
+    *src = u - 1;
+    *widx = ctx[u - 1] + yn[u - 1];
+  }
+};
+
+// (+) over the in-arcs of q of x[src] (x) w; MaxTropical keeps the first max
+template <bool BF16, int SR, typename G>
+LT_DEVINL float t_reduce(const G& g, int q, const float* x, const unsigned char* wf, int* argpos) {
+  const int n = g.nin(q), p0 = g.pos0(q);
+  if constexpr (SR == M_LOG) {
+    Lse l;
+    for (int k = 0; k < n; ++k) {
+      int src, wi;
+      g.arc(p0 + k, q, &src, &wi);
+      l.add(x[src] + ldw<BF16>(wf, wi));
+    }
+    return l.get();
+  } else if constexpr (SR == M_MAX) {
+    float r = -kInf;
+    int ra = -1;
+    for (int k = 0; k < n; ++k) {
+      int src, wi;
+      g.arc(p0 + k, q, &src, &wi);
+      const float v = x[src] + ldw<BF16>(wf, wi);
+      if (ra < 0 || v > r) {
+        r = v;
+        ra = p0 + k;
+      }
+    }
+    if (argpos) *argpos = ra;
+    return r;
+  } else {
+    float r = 0.f;
+    for (int k = 0; k < n; ++k) {
+      int src, wi;
+      g.arc(p0 + k, q, &src, &wi);
+      r += x[src] * ldw<BF16>(wf, wi);
+    }
+    return r;
+  }
+}
+
+// context_states / next-label classes of the string (contexts.py:109-146,
+// lattices.py:314-315 and 336-338); one thread
+LT_DEVINL void t_walk(const TArgs& a, int b, int* ctx, int* yn) {
+  int c = 0;
+  for (int u = 0; u <= a.U; ++u) {
+    ctx[u] = c * a.R;
+    int y = u < a.U ? a.labels[(long long)b * a.U + u] : 1;
+    if (u < a.U && (y < 0 || y > a.V)) y = 0;
+    yn[u] = y < 1 ? 1 : y;
+    if (u < a.U && y != 0) c = a.table[c * a.V + y - 1];
+  }
+}
+
+// ---- forward: den (NUM = false) or string (NUM = true) shortest distance ----
+template <bool BF16, int SR, bool NUM, bool VIT>
+__global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  const int S = NUM ? a.U + 1 : a.C, K = a.K, R = a.R;
+  float* va = sm;
+  float* vl = va + S;
+  float* vn = vl + S;
+  float* acc = vn + S;
+  int* ctx = (int*)(acc + S);
+  int* yn = ctx + S;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  for (int q = tid; q < S; q += nthr) va[q] = q == 0 ? t_one<SR>() : t_zero<SR>();
+  if (NUM && tid == 0) t_walk(a, b, ctx, yn);
+  __syncthreads();
+  DenGraph dg{a.in_off, a.in_arc, a.V, R};
+  NumGraph ng{ctx, yn};
+  const long long FR = (long long)a.C * R;
+  const int KK = K > 0 ? K : 1;
+  for (int t = 0; t < a.T; ++t) {
+    if (a.alpha)
+      for (int q = tid; q < S; q += nthr) a.alpha[((long long)b * a.T + t) * S + q] = va[q];
+    if (t >= nf) continue;  // padding frames carry alpha (lattices.py:460-461)
+    const unsigned char* wf = a.W + ((long long)b * a.T + t) * FR * (BF16 ? 2 : 4);
+    int* bpt = VIT ? a.bp + (((long long)b * a.T + t) * KK) * a.C : nullptr;
+    if (K == 0) {  // FrameDependent.forward, alignments.py:286-297
+      for (int q = tid; q < S; q += nthr) {
+        const int bi = NUM ? ng.blank(q) : dg.blank(q);
+        const float bt = t_times<SR>(va[q], ldw<BF16>(wf, bi));
+        int ap = -1;
+        const float r = NUM ? t_reduce<BF16, SR>(ng, q, va, wf, &ap)
+                            : t_reduce<BF16, SR>(dg, q, va, wf, &ap);
+        float o;
+        if constexpr (SR == M_LOG) {
+          o = t_lae(bt, r);
+        } else if constexpr (SR == M_MAX) {
+          const bool keep = ap < 0 || bt >= r;  // Maximum keeps a iff a >= b
+          o = keep ? bt : r;
+          if (VIT) bpt[q] = keep ? -1 : ap;
+        } else {
+          o = bt + r;
+        }
+        vn[q] = o;
+      }
+      __syncthreads();
+      for (int q = tid; q < S; q += nthr) va[q] = vn[q];
+      __syncthreads();
+      continue;
+    }
+    // FrameLabelDependent.forward (alignments.py:363-377): terms (L^i a) (x)
+    // blank, i = 0..K, summed (MaxTropical: the first max term wins)
+    for (int q = tid; q < S; q += nthr) {
+      const int bi = NUM ? ng.blank(q) : dg.blank(q);
+      acc[q] = t_times<SR>(va[q], ldw<BF16>(wf, bi));
+      vl[q] = va[q];
+      if (VIT) a.win[((long long)b * a.T + t) * a.C + q] = 0;
+    }
+    __syncthreads();
+    for (int i = 1; i <= K; ++i) {
+      for (int q = tid; q < S; q += nthr) {
+        int ap = -1;
+        vn[q] = NUM ? t_reduce<BF16, SR>(ng, q, vl, wf, &ap) : t_reduce<BF16, SR>(dg, q, vl, wf, &ap);
+        if (VIT) bpt[(long long)(i - 1) * a.C + q] = ap;
+      }
+      __syncthreads();
+      for (int q = tid; q < S; q += nthr) {
+        const int bi = NUM ? ng.blank(q) : dg.blank(q);
+        const float term = t_times<SR>(vn[q], ldw<BF16>(wf, bi));
+        if constexpr (SR == M_LOG) {
+          acc[q] = t_lae(acc[q], term);
+        } else if constexpr (SR == M_MAX) {
+          if (term > acc[q]) {
+            acc[q] = term;
+            if (VIT) a.win[((long long)b * a.T + t) * a.C + q] = (unsigned char)i;
+          }
+        } else {
+          acc[q] += term;
+        }
+        vl[q] = vn[q];
+      }
+      __syncthreads();
+    }
+    for (int q = tid; q < S; q += nthr) va[q] = acc[q];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (NUM) {
+      const int nl = a.nlab[b];
+      const float r = (nl >= 0 && nl <= a.U) ? va[nl] : t_zero<SR>();
+      a.dist[b] = r;  // lattices.py:375-377
+      if (a.loss) a.loss[b] = a.local ? -r : a.den_in[b] - r;  // lattices.py:131-183
+    } else {
+      // (+)_q alpha_T[q] (lattices.py:496); MaxTropical: first max state
+      float r = t_zero<SR>();
+      int qs = 0;
+      if constexpr (SR == M_LOG) {
+        Lse l;
+        for (int q = 0; q < S; ++q) l.add(va[q]);
+        r = l.get();
+      } else if constexpr (SR == M_MAX) {
+        r = va[0];
+        for (int q = 1; q < S; ++q)
+          if (va[q] > r) {
+            r = va[q];
+            qs = q;
+          }
+      } else {
+        for (int q = 0; q < S; ++q) r += va[q];
+      }
+      a.dist[b] = r;
+      if (VIT) a.qstar[b] = qs;
+    }
+  }
+}
+
+// ---- Viterbi backtrace (lattices.py:185-247, per utterance: no D6) ----------
+__global__ void tab_backtrace_kernel(const TArgs a) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.B) return;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int K = a.K, KK = K > 0 ? K : 1, A = K > 0 ? K + 1 : 1;
+  long long* lab = a.vlabels + (long long)b * a.T * A;
+  for (long long i = 0; i < (long long)a.T * A; ++i) lab[i] = 0;
+  int q = a.qstar[b];
+  for (int t = nf - 1; t >= 0; --t) {
+    const int* bpt = a.bp + (((long long)b * a.T + t) * KK) * a.C;
+    const int i = K > 0 ? a.win[((long long)b * a.T + t) * a.C + q] : 1;
+    for (int j = i; j >= 1; --j) {
+      const int pos = bpt[(long long)(j - 1) * a.C + q];
+      if (pos < 0) break;  // FrameDependent: blank won
+      const int id = a.in_arc[pos];
+      const int p = id / a.V, y = id - p * a.V + 1;
+      lab[(long long)t * A + j - 1] = a.conv ? y - 1 : y;
+      q = p;
+    }
+  }
+}
+
+// ---- backward (Log): denominator marginals -> dW (written for every frame) --
+// FrameDependent.backward (alignments.py:300-318) / FrameLabelDependent.backward
+// (:379-419) in reverse frame order; the K+1 blank and K lexical marginals of
+// a frame add up on the shared weights. Utterances whose loss is not finite,
+// and padding frames, get dW = 0. do_den = 0 (local normalisation): zeros.
+template <bool BF16>
+__global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  const int C = a.C, V = a.V, R = a.R, K = a.K;
+  float* beta = sm;
+  float* nbA = beta + C;
+  float* nbB = nbA + C;
+  float* la = nbB + C;  // [K+1][C]
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const float lz = a.local ? 0.f : a.den_in[b];
+  const float nm = a.num_in[b];
+  const bool live = !a.local && __builtin_isfinite(nm) && __builtin_isfinite(lz);
+  const long long FR = (long long)C * R;
+  for (int q = tid; q < C; q += nthr) beta[q] = 0.f;  // every state final (Log.ones)
+  __syncthreads();
+  DenGraph dg{a.in_off, a.in_arc, V, R};
+  for (int t = a.T - 1; t >= 0; --t) {
+    const long long fo = ((long long)b * a.T + t) * FR;
+    if (t >= nf || !live) {
+      for (long long e = tid; e < FR; e += nthr) stw<false>(a.dW, fo + e, 0.f);
+      continue;
+    }
+    const unsigned char* wf = a.W + fo * (BF16 ? 2 : 4);
+    for (int q = tid; q < C; q += nthr) la[q] = a.hist[((long long)b * a.T + t) * C + q];
+    __syncthreads();
+    for (int i = 1; i <= K; ++i) {  // lexical_alphas
+      for (int q = tid; q < C; q += nthr)
+        la[(long long)i * C + q] = t_reduce<BF16, M_LOG>(dg, q, la + (long long)(i - 1) * C, wf, nullptr);
+      __syncthreads();
+    }
+    for (int p = tid; p < C; p += nthr) {
+      const float bb = ldw<BF16>(wf, p * R) + beta[p];
+      if (K == 0) {
+        stw<false>(a.dW, fo + p * R, lt_exp(la[p] + bb - lz));
+        Lse s;
+        for (int y = 1; y <= V; ++y) {
+          const float lb = ldw<BF16>(wf, p * R + y) + beta[a.table[p * V + y - 1]];
+          stw<false>(a.dW, fo + p * R + y, lt_exp(la[p] + lb - lz));
+          s.add(lb);
+        }
+        nbA[p] = t_lae(bb, s.get());
+      } else {
+        float mb = 0.f;
+        for (int i = 0; i <= K; ++i) mb += lt_exp(la[(long long)i * C + p] + bb - lz);
+        stw<false>(a.dW, fo + p * R, mb);
+        nbA[p] = bb;  // blank[K] + beta
+      }
+    }
+    __syncthreads();
+    float* cur = nbA;
+    float* nxt = nbB;
+    for (int j = K - 1; j >= 0; --j) {
+      for (int p = tid; p < C; p += nthr) {
+        Lse s;
+        const float lj = la[(long long)j * C + p] - lz;
+        for (int y = 1; y <= V; ++y) {
+          const float lb = ldw<BF16>(wf, p * R + y) + cur[a.table[p * V + y - 1]];
+          const float m = lt_exp(lb + lj);
+          const long long e = fo + p * R + y;
+          // the same thread owns (p, y) for every j: accumulate in place
+          stw<false>(a.dW, e, j == K - 1 ? m : ldw<false>((const unsigned char*)a.dW, e) + m);
+          s.add(lb);
+        }
+        nxt[p] = t_lae(ldw<BF16>(wf, p * R) + beta[p], s.get());
+      }
+      __syncthreads();
+      float* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+    }
+    for (int p = tid; p < C; p += nthr) beta[p] = cur[p];
+    __syncthreads();
+  }
+}
+
+// ---- backward (Log): numerator marginals subtracted from dW ----------------
+// The same recursion on the string acceptor; string arcs that share a lattice
+// arc are summed by their chain head in ascending order (one writer per
+// element and frame: deterministic).
+template <bool BF16>
+__global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  const int U = a.U, S = U + 1, K = a.K, NK = 2 * S;
+  float* beta = sm;
+  float* nbA = beta + S;
+  float* nbB = nbA + S;
+  float* mb = nbB + S;
+  float* ml = mb + S;
+  float* la = ml + S;  // [K+1][S]
+  int* ctx = (int*)(la + (long long)(K + 1) * S);
+  int* yn = ctx + S;
+  int* link = yn + S;  // [NK]: head << 30 | (next entry + 1)
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const float nm = a.num_in[b];
+  const float lz = a.local ? 0.f : a.den_in[b];
+  const bool live = __builtin_isfinite(nm) && (a.local || __builtin_isfinite(lz));
+  if (!live) return;  // the denominator kernel wrote zeros
+  const int nl = a.nlab[b];
+  if (tid == 0) t_walk(a, b, ctx, yn);
+  for (int u = tid; u < S; u += nthr) beta[u] = u == nl ? 0.f : -kInf;
+  __syncthreads();
+  auto elem = [&](int k) {  // W element of string entry k = 2u + kind, or -1
+    const int u = k >> 1;
+    return (k & 1) == 0 ? ctx[u] : (u < U ? ctx[u] + yn[u] : -1);
+  };
+  for (int k = tid; k < NK; k += nthr) {
+    const int o = elem(k);
+    int head = o >= 0 ? 1 : 0, nxt = -1;
+    if (o >= 0)
+      for (int k2 = 0; k2 < NK; ++k2) {
+        if (elem(k2) != o) continue;
+        if (k2 < k) head = 0;
+        else if (k2 > k && nxt < 0) nxt = k2;
+      }
+    link[k] = (head << 30) | (nxt + 1);
+  }
+  __syncthreads();
+  NumGraph ng{ctx, yn};
+  const long long FR = (long long)a.C * a.R;
+  for (int t = nf - 1; t >= 0; --t) {
+    const long long fo = ((long long)b * a.T + t) * FR;
+    const unsigned char* wf = a.W + fo * (BF16 ? 2 : 4);
+    for (int u = tid; u < S; u += nthr) la[u] = a.hist[((long long)b * a.T + t) * S + u];
+    __syncthreads();
+    for (int i = 1; i <= K; ++i) {
+      for (int u = tid; u < S; u += nthr)
+        la[(long long)i * S + u] = t_reduce<BF16, M_LOG>(ng, u, la + (long long)(i - 1) * S, wf, nullptr);
+      __syncthreads();
+    }
+    for (int u = tid; u < S; u += nthr) {
+      const float bb = ldw<BF16>(wf, ctx[u]) + beta[u];
+      if (K == 0) {
+        const float lb = u < U ? ldw<BF16>(wf, ctx[u] + yn[u]) + beta[u + 1] : -kInf;
+        mb[u] = lt_exp(la[u] + bb - nm);
+        ml[u] = lt_exp(la[u] + lb - nm);
+        nbA[u] = t_lae(bb, lb);
+      } else {
+        float s = 0.f;
+        for (int i = 0; i <= K; ++i) s += lt_exp(la[(long long)i * S + u] + bb - nm);
+        mb[u] = s;
+        ml[u] = 0.f;
+        nbA[u] = bb;
+      }
+    }
+    __syncthreads();
+    float* cur = nbA;
+    float* nxt = nbB;
+    for (int j = K - 1; j >= 0; --j) {
+      for (int u = tid; u < S; u += nthr) {
+        const float lb = u < U ? ldw<BF16>(wf, ctx[u] + yn[u]) + cur[u + 1] : -kInf;
+        ml[u] += lt_exp(lb + la[(long long)j * S + u] - nm);
+        nxt[u] = t_lae(ldw<BF16>(wf, ctx[u]) + beta[u], lb);
+      }
+      __syncthreads();
+      float* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+    }
+    for (int k = tid; k < NK; k += nthr) {
+      const int lk = link[k];
+      if (!(lk >> 30)) continue;
+      float s = 0.f;
+      for (int kk = k; kk >= 0; kk = (link[kk] & 0x3fffffff) - 1)
+        s += (kk & 1) ? ml[kk >> 1] : mb[kk >> 1];
+      const long long e = fo + elem(k);
+      stw<false>(a.dW, e, ldw<false>((const unsigned char*)a.dW, e) - s);
+    }
+    __syncthreads();
+    for (int u = tid; u < S; u += nthr) beta[u] = cur[u];
+    __syncthreads();
+  }
+}
+
+// fp32 gradient -> bf16 dW (one rounding of den - num, as the tuned kernels)
+__global__ __launch_bounds__(256) void tab_to_bf16_kernel(const float* src, unsigned short* dst,
+                                                          long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    dst[i] = f2bf(src[i]);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+int t_fail(int code, const char* msg) { return lt_impl::set_error(code, msg); }
+int t_hip(hipError_t e, const char* what) {
+  return e == hipSuccess ? LT_OK : lt_impl::set_error(LT_EHIP, what);
+}
+constexpr int kTabLds = 160 * 1024;
+
+int t_check(const lt_graph* g, const lt_table_problem* pb) {
+  if (!g || !pb) return t_fail(LT_EINVAL, "null graph / problem");
+  if (g->num_states < 1 || g->vocab_size < 1 || g->expansions < 0 || g->expansions > 255)
+    return t_fail(LT_EINVAL, "bad graph (states >= 1, vocab >= 1, 0 <= expansions <= 255)");
+  if (!g->next_state || !g->in_offsets || !g->in_arcs) return t_fail(LT_EINVAL, "null graph arrays");
+  if (pb->batch < 0 || pb->max_frames < 0 || pb->max_labels < 0)
+    return t_fail(LT_EINVAL, "negative shape");
+  if (pb->weight_dtype != LT_DTYPE_F32 && pb->weight_dtype != LT_DTYPE_BF16)
+    return t_fail(LT_EINVAL, "bad dtype");
+  return LT_OK;
+}
+
+TArgs t_args(const lt_graph* g, const lt_table_problem* pb, const void* W, const int32_t* nf) {
+  TArgs a;
+  memset(&a, 0, sizeof(a));
+  a.W = (const unsigned char*)W;
+  a.nfr = nf;
+  a.table = g->next_state;
+  a.in_off = g->in_offsets;
+  a.in_arc = g->in_arcs;
+  a.B = pb->batch;
+  a.T = pb->max_frames;
+  a.U = pb->max_labels;
+  a.C = g->num_states;
+  a.V = g->vocab_size;
+  a.R = g->vocab_size + 1;
+  a.K = g->expansions;
+  return a;
+}
+
+template <typename KF>
+int t_launch(KF k, int grid, int lds_bytes, hipStream_t st, const TArgs& a) {
+  if (lds_bytes > kTabLds) return t_fail(LT_EUNSUPPORTED, "table lattice state exceeds LDS");
+  if (lds_bytes > 64 * 1024)
+    if (int rc = t_hip(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           lds_bytes), "table LDS"))
+      return rc;
+  if (grid == 0) return LT_OK;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds_bytes, st, a);
+  return t_hip(hipGetLastError(), "table kernel launch");
+}
+
+int fwd_lds(int S, bool num) { return 4 * (4 * S) + (num ? 8 * S : 0); }
+
+template <bool BF16>
+int launch_t_fwd(int sr, bool num, bool vit, const TArgs& a, hipStream_t st) {
+  const int S = num ? a.U + 1 : a.C;
+  const int lds = fwd_lds(S, num);
+  if (vit) return t_launch(tab_fwd_kernel<BF16, M_MAX, false, true>, a.B, lds, st, a);
+  if (num) {
+    if (sr == M_LOG) return t_launch(tab_fwd_kernel<BF16, M_LOG, true, false>, a.B, lds, st, a);
+    if (sr == M_MAX) return t_launch(tab_fwd_kernel<BF16, M_MAX, true, false>, a.B, lds, st, a);
+    return t_launch(tab_fwd_kernel<BF16, M_REAL, true, false>, a.B, lds, st, a);
+  }
+  if (sr == M_LOG) return t_launch(tab_fwd_kernel<BF16, M_LOG, false, false>, a.B, lds, st, a);
+  if (sr == M_MAX) return t_launch(tab_fwd_kernel<BF16, M_MAX, false, false>, a.B, lds, st, a);
+  return t_launch(tab_fwd_kernel<BF16, M_REAL, false, false>, a.B, lds, st, a);
+}
+
+int t_fwd(int sr, bool num, bool vit, const TArgs& a, bool bf16, hipStream_t st) {
+  return bf16 ? launch_t_fwd<true>(sr, num, vit, a, st) : launch_t_fwd<false>(sr, num, vit, a, st);
+}
+
+struct GradLayout {
+  size_t hd, hn, dwf, total;
+};
+GradLayout grad_layout(const lt_graph* g, const lt_table_problem* pb) {
+  auto up = [](long long x) { return (size_t)((x + 255) & ~255LL); };
+  GradLayout l;
+  const long long BT = (long long)pb->batch * pb->max_frames;
+  l.hd = 0;
+  l.hn = up(4 * BT * g->num_states);
+  l.dwf = l.hn + up(4 * BT * (pb->max_labels + 1));
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  l.total = l.dwf + (bf16 ? up(4 * BT * g->num_states * (g->vocab_size + 1)) : 0);
+  return l;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lt_graph_in_arcs(int32_t num_states, int32_t vocab_size, const int32_t* next_state,
+                     int32_t* in_offsets, int32_t* in_arcs) {
+  if (num_states < 1 || vocab_size < 1 || !next_state || !in_offsets || !in_arcs)
+    return t_fail(LT_EINVAL, "lt_graph_in_arcs: bad arguments");
+  const int C = num_states, V = vocab_size;
+  for (int q = 0; q <= C; ++q) in_offsets[q] = 0;
+  for (long long i = 0; i < (long long)C * V; ++i) {
+    const int q = next_state[i];
+    if (q < 0 || q >= C) return t_fail(LT_EINVAL, "next_state entry out of range");
+    ++in_offsets[q + 1];
+  }
+  for (int q = 0; q < C; ++q) in_offsets[q + 1] += in_offsets[q];
+  std::vector<int> fill(in_offsets, in_offsets + C);
+  for (int p = 0; p < C; ++p)  // ascending (p, y) within each next state
+    for (int y = 0; y < V; ++y) {
+      const int q = next_state[(long long)p * V + y];
+      in_arcs[fill[q]++] = p * V + y;
+    }
+  return LT_OK;
+}
+
+int lt_table_forward(const lt_graph* g, const lt_table_problem* pb, int32_t semiring,
+                     const void* W, const int32_t* num_frames, float* dist, float* alpha,
+                     void* stream) {
+  if (int rc = t_check(g, pb)) return rc;
+  if (semiring < 0 || semiring > 2) return t_fail(LT_EINVAL, "bad semiring");
+  if (pb->batch == 0) return LT_OK;
+  if ((!W && pb->max_frames > 0) || !num_frames || !dist) return t_fail(LT_EINVAL, "null pointer");
+  TArgs a = t_args(g, pb, W, num_frames);
+  a.dist = dist;
+  a.alpha = alpha;
+  return t_fwd(semiring, false, false, a, pb->weight_dtype == LT_DTYPE_BF16, (hipStream_t)stream);
+}
+
+int lt_table_num_forward(const lt_graph* g, const lt_table_problem* pb, int32_t semiring,
+                         const void* W, const int32_t* num_frames, const int32_t* labels,
+                         const int32_t* num_labels, float* num, void* stream) {
+  if (int rc = t_check(g, pb)) return rc;
+  if (semiring < 0 || semiring > 2) return t_fail(LT_EINVAL, "bad semiring");
+  if (pb->batch == 0) return LT_OK;
+  if ((!W && pb->max_frames > 0) || !num_frames || !num_labels || !num ||
+      (pb->max_labels > 0 && !labels))
+    return t_fail(LT_EINVAL, "null pointer");
+  TArgs a = t_args(g, pb, W, num_frames);
+  a.labels = labels;
+  a.nlab = num_labels;
+  a.dist = num;
+  return t_fwd(semiring, true, false, a, pb->weight_dtype == LT_DTYPE_BF16, (hipStream_t)stream);
+}
+
+int lt_table_loss_grad_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
+                                       size_t* bytes) {
+  if (int rc = t_check(g, pb)) return rc;
+  if (bytes) *bytes = grad_layout(g, pb).total;
+  return LT_OK;
+}
+
+int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t local_norm,
+                       const void* W, const int32_t* num_frames, const int32_t* labels,
+                       const int32_t* num_labels, float* loss, float* log_z, float* num,
+                       void* dW, void* workspace, size_t workspace_bytes, void* stream) {
+  if (int rc = t_check(g, pb)) return rc;
+  if (pb->batch == 0) return LT_OK;
+  if ((!W && pb->max_frames > 0) || !num_frames || !num_labels || !loss || !log_z || !num ||
+      (pb->max_labels > 0 && !labels))
+    return t_fail(LT_EINVAL, "null pointer");
+  const GradLayout l = grad_layout(g, pb);
+  if (dW && (!workspace || workspace_bytes < l.total)) return t_fail(LT_EINVAL, "workspace too small");
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  hipStream_t st = (hipStream_t)stream;
+  float* hd = dW ? (float*)((char*)workspace + l.hd) : nullptr;
+  float* hn = dW ? (float*)((char*)workspace + l.hn) : nullptr;
+  TArgs a = t_args(g, pb, W, num_frames);
+  a.labels = labels;
+  a.nlab = num_labels;
+  a.local = local_norm ? 1 : 0;
+  int rc;
+  if (!local_norm) {  // log_z and the alpha history
+    a.dist = log_z;
+    a.alpha = hd;
+    if ((rc = t_fwd(M_LOG, false, false, a, bf16, st))) return rc;
+  } else {
+    if ((rc = t_hip(hipMemsetAsync(log_z, 0, sizeof(float) * pb->batch, st), "memset"))) return rc;
+  }
+  a.dist = num;
+  a.alpha = hn;
+  a.loss = loss;
+  a.den_in = log_z;
+  if ((rc = t_fwd(M_LOG, true, false, a, bf16, st))) return rc;
+  if (!dW) return LT_OK;
+  a.dist = nullptr;
+  a.alpha = nullptr;
+  a.loss = nullptr;
+  a.num_in = num;
+  float* dwf = bf16 ? (float*)((char*)workspace + l.dwf) : (float*)dW;
+  a.dW = dwf;
+  const int C = a.C, S = a.U + 1, K = a.K;
+  a.hist = hd;
+  const int lds_d = 4 * (3 * C + (K + 1) * C);
+  rc = bf16 ? t_launch(tab_bwd_den_kernel<true>, a.B, lds_d, st, a)
+            : t_launch(tab_bwd_den_kernel<false>, a.B, lds_d, st, a);
+  if (rc) return rc;
+  a.hist = hn;
+  const int lds_n = 4 * (5 * S + (K + 1) * S) + 4 * (2 * S + 2 * S);
+  rc = bf16 ? t_launch(tab_bwd_num_kernel<true>, a.B, lds_n, st, a)
+            : t_launch(tab_bwd_num_kernel<false>, a.B, lds_n, st, a);
+  if (rc || !bf16) return rc;
+  const long long n = (long long)a.B * a.T * C * a.R;
+  const int blocks = (int)std::min<long long>(4096, (n + 255) / 256);
+  if (blocks > 0)
+    hipLaunchKernelGGL(tab_to_bf16_kernel, dim3(blocks), dim3(256), 0, st, dwf,
+                       (unsigned short*)dW, n);
+  return t_hip(hipGetLastError(), "bf16 conversion launch");
+}
+
+int lt_table_viterbi_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
+                                     size_t* bytes) {
+  if (int rc = t_check(g, pb)) return rc;
+  const long long BT = (long long)pb->batch * pb->max_frames;
+  const int KK = g->expansions > 0 ? g->expansions : 1;
+  auto up = [](long long x) { return (size_t)((x + 255) & ~255LL); };
+  if (bytes) *bytes = up(4 * BT * KK * g->num_states) + up(BT * g->num_states) + up(4LL * pb->batch);
+  return LT_OK;
+}
+
+int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* W,
+                     const int32_t* num_frames, int32_t label_convention, int64_t* labels,
+                     float* path_weight, void* workspace, size_t workspace_bytes, void* stream) {
+  if (int rc = t_check(g, pb)) return rc;
+  if (pb->batch == 0) return LT_OK;
+  if ((!W && pb->max_frames > 0) || !num_frames || !path_weight || (!labels && pb->max_frames > 0))
+    return t_fail(LT_EINVAL, "null pointer");
+  size_t need = 0;
+  lt_table_viterbi_workspace_bytes(g, pb, &need);
+  if (!workspace || workspace_bytes < need) return t_fail(LT_EINVAL, "workspace too small");
+  const long long BT = (long long)pb->batch * pb->max_frames;
+  const int KK = g->expansions > 0 ? g->expansions : 1;
+  auto up = [](long long x) { return (size_t)((x + 255) & ~255LL); };
+  TArgs a = t_args(g, pb, W, num_frames);
+  a.bp = (int*)workspace;
+  a.win = (unsigned char*)workspace + up(4 * BT * KK * g->num_states);
+  a.qstar = (int*)((char*)a.win + up(BT * g->num_states));
+  a.dist = path_weight;
+  a.conv = label_convention;
+  a.vlabels = (long long*)labels;
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = t_fwd(M_MAX, false, true, a, pb->weight_dtype == LT_DTYPE_BF16, st)) return rc;
+  const int threads = 64;
+  hipLaunchKernelGGL(tab_backtrace_kernel, dim3((a.B + threads - 1) / threads), dim3(threads), 0,
+                     st, a);
+  return t_hip(hipGetLastError(), "backtrace launch");
+}
+
+}  // extern "C"

@@ -101,6 +101,28 @@ class _LossFn(torch.autograd.Function):
     return dW, None, None, None, None, None, None
 
 
+class _TableLossFn(torch.autograd.Function):
+  """loss for the general lattices (lt_table_loss_grad): any next-state
+  table, FrameDependent or FrameLabelDependent(K). The gradient of
+  sum(loss) comes with the forward; the backward scales it."""
+
+  @staticmethod
+  def forward(ctx, W, nf, labels, nl, graph, local):
+    want = ctx.needs_input_grad[0]
+    loss, _, _, dW = _native.table_loss_grad(graph, W, nf, labels, nl, local, want_grad=want)
+    ctx.dW = dW
+    return loss
+
+  @staticmethod
+  def backward(ctx, g):
+    dW = ctx.dW
+    if dW is None:
+      raise RuntimeError('the lattice loss gradient was already consumed: backward through '
+                         'RecognitionLattice.forward twice is not supported (call it again)')
+    ctx.dW = None
+    return (dW * g.to(dW.dtype)[:, None, None, None], None, None, None, None, None)
+
+
 class _DenFn(torch.autograd.Function):
   """Denominator shortest distance; gradient = arc marginals (Log) or the
   best-path indicator (MaxTropical)."""
@@ -168,6 +190,34 @@ class RecognitionLattice(nn.Module, Generic[T]):
     self.weight_fn = weight_fn_factory(context)
 
   # -- helpers -------------------------------------------------------------
+  def _table_path(self) -> bool:
+    """False: FullNGram x FrameDependent, the tuned kernels (lt_lattice.hip,
+    lt_pipe.hip). True: any other context (through its next-state table)
+    with FrameDependent or FrameLabelDependent -- the general table kernels
+    (lt_table.hip)."""
+    if not isinstance(self.alignment, (alignments.FrameDependent,
+                                       alignments.FrameLabelDependent)):
+      raise NotImplementedError(f'lattice kernels implement FrameDependent and '
+                                f'FrameLabelDependent alignments, got '
+                                f'{type(self.alignment).__name__}')
+    return not (isinstance(self.context, contexts.FullNGram) and
+                isinstance(self.alignment, alignments.FrameDependent))
+
+  def _graph(self, device) -> '_native.TableGraph':
+    cache = self.__dict__.setdefault('_graphs', {})
+    key = str(device)
+    if key not in cache:
+      if isinstance(self.context, contexts.NextStateTable):
+        table = self.context.next_state_table
+      elif hasattr(self.context, 'next_state_table'):
+        table = self.context.next_state_table()
+      else:
+        raise NotImplementedError(f'{type(self.context).__name__} has no next-state table')
+      K = (self.alignment.max_expansions
+           if isinstance(self.alignment, alignments.FrameLabelDependent) else 0)
+      cache[key] = _native.TableGraph(table, K, device)
+    return cache[key]
+
   def _ngram(self) -> tuple[int, int]:
     if not isinstance(self.context, contexts.FullNGram):
       raise NotImplementedError(f'lattice kernels implement FullNGram contexts, got '
@@ -205,7 +255,7 @@ class RecognitionLattice(nn.Module, Generic[T]):
     if tuple(frames.shape[:-2]) != batch_dims:
       raise ValueError('frames and num_frames have different batch_dims: '
                        f'{tuple(frames.shape[:-2])} vs {batch_dims}')
-    V, n = self._ngram()
+    V, n = self._ngram() if not self._table_path() else (None, None)
     if cache is None:
       cache = self.weight_fn_cacher()
     W = self.arc_weights(cache, frames)
@@ -240,7 +290,10 @@ class RecognitionLattice(nn.Module, Generic[T]):
     lab = torch.as_tensor(labels).reshape(B, -1).to(device=W.device, dtype=torch.int32)
     nl = _lengths(num_labels, B, W.device)
     local = isinstance(self.weight_fn, weight_fns.LocallyNormalizedWeightFn)
-    loss = _LossFn.apply(W, nf, lab.contiguous(), nl, V, n, local)
+    if self._table_path():
+      loss = _TableLossFn.apply(W, nf, lab.contiguous(), nl, self._graph(W.device), local)
+    else:
+      loss = _LossFn.apply(W, nf, lab.contiguous(), nl, V, n, local)
     return self._home(loss.reshape(batch_dims), frames)
 
   def shortest_path(self, frames: torch.Tensor, num_frames: torch.Tensor,
@@ -256,7 +309,11 @@ class RecognitionLattice(nn.Module, Generic[T]):
     conv = {'reference': _native.LABELS_REFERENCE, 'true': _native.LABELS_TRUE}[label_convention]
     W, nf, batch_dims, B, V, n, _ = self._prepare(cache, frames, num_frames)
     with torch.no_grad():
-      labels, weights, _ = _native.viterbi(W.detach(), nf, V, n, conv)
+      if self._table_path():
+        # A labels per frame: slot i = the (i+1)-th lexical label of the frame
+        labels, weights = _native.table_viterbi(self._graph(W.device), W.detach(), nf, conv)
+      else:
+        labels, weights, _ = _native.viterbi(W.detach(), nf, V, n, conv)
     labels = self._home(labels.reshape(*batch_dims, -1), frames)
     num_alignment_labels = self.alignment.num_states() * num_frames
     return labels, num_alignment_labels, self._home(weights.reshape(batch_dims), frames)
@@ -280,7 +337,11 @@ class RecognitionLattice(nn.Module, Generic[T]):
     W, nf, batch_dims, B, V, n, _ = self._prepare(cache, frames, num_frames)
     lab = torch.as_tensor(labels).reshape(B, -1).to(device=W.device, dtype=torch.int32)
     nl = _lengths(num_labels, B, W.device)
-    num = _NumFn.apply(W, nf, lab.contiguous(), nl, V, n, sid)
+    if self._table_path():  # values only: gradients come through forward()
+      num = _native.table_num_forward(self._graph(W.device), W.detach(), nf, lab.contiguous(),
+                                      nl, sid)
+    else:
+      num = _NumFn.apply(W, nf, lab.contiguous(), nl, V, n, sid)
     return self._home(num.reshape(batch_dims), frames)
 
   def _forward(self, cache: T, frames: torch.Tensor, num_frames: torch.Tensor,
@@ -303,7 +364,16 @@ class RecognitionLattice(nn.Module, Generic[T]):
     if tuple(frames.shape[:-2]) != batch_dims:
       raise ValueError('frames and num_frames have different batch_dims: '
                        f'{tuple(frames.shape[:-2])} vs {batch_dims}')
-    V, n = self._ngram()
+    table = self._table_path()
+    V, n = self._ngram() if not table else (None, None)
+    if table:
+      # alignment-state-invariant weights (lattices.py:444-447): one mask
+      # for every alignment state
+      for mask in (blank_mask, lexical_mask):
+        if mask is not None and any(m is not mask[0] and not torch.equal(m, mask[0])
+                                    for m in mask[1:]):
+          raise NotImplementedError('per-alignment-state masks differ: the kernels use '
+                                    'alignment-state-invariant weights')
     if cache is None:
       cache = self.weight_fn_cacher()
     W = self.arc_weights(cache, frames)
@@ -317,7 +387,10 @@ class RecognitionLattice(nn.Module, Generic[T]):
     dev = _compute_device(W, frames, num_frames)
     Wk = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
     nf = _lengths(num_frames, B, dev)
-    dist, alpha = _DenFn.apply(Wk, nf, V, n, sid)
+    if table:  # values only: gradients come through forward() / shortest_path()
+      dist, alpha = _native.table_forward(self._graph(Wk.device), Wk.detach(), nf, sid)
+    else:
+      dist, alpha = _DenFn.apply(Wk, nf, V, n, sid)
     C = alpha.shape[-1]
     return (self._home(dist.reshape(batch_dims), frames),
             self._home(alpha.reshape(*batch_dims, frames.shape[-2], C), frames))

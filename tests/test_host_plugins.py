@@ -152,3 +152,64 @@ def test_lattice_without_gpu_fails_loudly():
     lat(frames, torch.tensor([3, 2]), torch.ones([2, 2]), torch.tensor([1, 1]))
   with pytest.raises(Exception):
     lat.shortest_path(frames, torch.tensor([3, 2]))
+
+
+# ---------------------------------------------------------------------------
+# NextStateTable / FrameLabelDependent host classes
+# ---------------------------------------------------------------------------
+def test_next_state_table_validation_and_full_ngram():
+  """contexts_test.py:175-200: invalid tables raise; a FullNGram table gives
+  the same maps as FullNGram."""
+  import last_torch_amd as lt
+  with pytest.raises(ValueError, match='non-zero size'):
+    lt.contexts.NextStateTable(torch.zeros([1, 0], dtype=torch.int32))
+  with pytest.raises(ValueError, match='non-zero size'):
+    lt.contexts.NextStateTable(torch.zeros([0, 1], dtype=torch.int32))
+  with pytest.raises(ValueError, match='should have shape'):
+    lt.contexts.NextStateTable(torch.zeros([1], dtype=torch.int32))
+  with pytest.raises(ValueError, match='int32'):
+    lt.contexts.NextStateTable(torch.zeros([2, 3]))
+  full = lt.contexts.FullNGram(vocab_size=3, context_size=2)
+  table = full.next_state_table().to(torch.int32)
+  assert tuple(table.shape) == (13, 3)
+  ctx = lt.contexts.NextStateTable(table)
+  assert ctx.shape() == (13, 3) and ctx.start() == 0
+  states = torch.arange(13)[:, None]
+  for y in range(4):
+    np.testing.assert_array_equal(ctx.next_state(states, torch.full_like(states, y)).numpy(),
+                                  full.next_state(states, torch.full_like(states, y)).numpy())
+  w = torch.randn(2, 13, 3, dtype=torch.float64)
+  for sr in (lt.semirings.Log, lt.semirings.MaxTropical, lt.semirings.Real):
+    np.testing.assert_allclose(ctx.forward_reduce(w, sr).numpy(),
+                               full.forward_reduce(w, sr).numpy(), rtol=1e-12, atol=1e-12)
+  b = torch.randn(2, 13, dtype=torch.float64)
+  np.testing.assert_array_equal(ctx.backward_broadcast(b).numpy(),
+                                full.backward_broadcast(b).numpy())
+  labels = torch.tensor([2, 0, 0, 3, 1])
+  np.testing.assert_array_equal(ctx.walk_states(labels).numpy(), full.walk_states(labels).numpy())
+
+
+def test_frame_label_dependent_host_matches_reference_fixtures():
+  """The host FrameLabelDependent (the plugin surface) composed over frames
+  reproduces the reference's FLD fixtures (den Log / MaxTropical, and the
+  loss gradient through its backward)."""
+  import last_torch_amd as lt
+  from golden_cases import FLD_CASES, load_fld
+  for case in FLD_CASES:
+    c = load_fld(case)
+    V, n, K = c['V'], c['n'], c['K']
+    ctx = lt.contexts.FullNGram(vocab_size=V, context_size=n)
+    align = lt.alignments.FrameLabelDependent(max_expansions=K)
+    assert align.num_states() == K + 1 and align.lexical_next(K) is None
+    W = torch.tensor(c['W'], dtype=torch.float64)
+    nf = torch.tensor(c['num_frames'])
+    B, T, C, _ = W.shape
+    for sname in ('Log', 'MaxTropical'):
+      sr = getattr(lt.semirings, sname)
+      alpha = sr.ones([B, C], dtype=torch.float64)
+      alpha = torch.where(torch.arange(C) == 0, alpha, sr.zeros([B, C], dtype=torch.float64))
+      for t in range(T):
+        nxt = align.forward(alpha, [W[:, t, :, 0]] * (K + 1), [W[:, t, :, 1:]] * (K + 1), ctx, sr)
+        alpha = torch.where((t < nf)[:, None], nxt, alpha)
+      d = sr.sum(alpha, dim=-1).numpy()
+      np.testing.assert_allclose(d, c[f'den_{sname}'], rtol=1e-5, atol=1e-5)
