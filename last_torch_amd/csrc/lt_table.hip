@@ -45,7 +45,29 @@ struct TArgs {
   int* qstar;           // Viterbi: [B] best final state
   long long* vlabels;   // Viterbi: [B, T*A]
   int B, T, U, C, V, R, K, conv, local;
+  int gst;  // the graph (in_off, in_arc, table) is copied to LDS first
 };
+
+// Copies the graph arrays to LDS at g (ints: in_off [C+1], in_arc [C*V],
+// table [C*V]) when a.gst, and returns the arrays to use.
+LT_DEVINL void t_graph(const TArgs& a, int* g, const int** in_off, const int** in_arc,
+                       const int** table) {
+  if (!a.gst) {
+    *in_off = a.in_off;
+    *in_arc = a.in_arc;
+    *table = a.table;
+    return;
+  }
+  const int C = a.C, CV = a.C * a.V;
+  for (int i = threadIdx.x; i <= C; i += blockDim.x) g[i] = a.in_off[i];
+  for (int i = threadIdx.x; i < CV; i += blockDim.x) {
+    g[C + 1 + i] = a.in_arc[i];
+    g[C + 1 + CV + i] = a.table[i];
+  }
+  *in_off = g;
+  *in_arc = g + C + 1;
+  *table = g + C + 1 + CV;
+}
 
 LT_DEVINL float t_safe(float x) { return __builtin_isfinite(x) ? x : 0.f; }
 // _LogAddExp (semirings.py:248-255)
@@ -107,15 +129,15 @@ struct NumGraph {
 };
 
 // (+) over the in-arcs of q of x[src] (x) w; MaxTropical keeps the first max
-template <bool BF16, int SR, typename G>
-LT_DEVINL float t_reduce(const G& g, int q, const float* x, const unsigned char* wf, int* argpos) {
+template <int SR, typename G, typename WR>
+LT_DEVINL float t_reduce(const G& g, int q, const float* x, const WR& wr, int* argpos) {
   const int n = g.nin(q), p0 = g.pos0(q);
   if constexpr (SR == M_LOG) {
     Lse l;
     for (int k = 0; k < n; ++k) {
       int src, wi;
       g.arc(p0 + k, q, &src, &wi);
-      l.add(x[src] + ldw<BF16>(wf, wi));
+      l.add(x[src] + wr(wi));
     }
     return l.get();
   } else if constexpr (SR == M_MAX) {
@@ -124,7 +146,7 @@ LT_DEVINL float t_reduce(const G& g, int q, const float* x, const unsigned char*
     for (int k = 0; k < n; ++k) {
       int src, wi;
       g.arc(p0 + k, q, &src, &wi);
-      const float v = x[src] + ldw<BF16>(wf, wi);
+      const float v = x[src] + wr(wi);
       if (ra < 0 || v > r) {
         r = v;
         ra = p0 + k;
@@ -137,7 +159,7 @@ LT_DEVINL float t_reduce(const G& g, int q, const float* x, const unsigned char*
     for (int k = 0; k < n; ++k) {
       int src, wi;
       g.arc(p0 + k, q, &src, &wi);
-      r += x[src] * ldw<BF16>(wf, wi);
+      r += x[src] * wr(wi);
     }
     return r;
   }
@@ -157,39 +179,53 @@ LT_DEVINL void t_walk(const TArgs& a, int b, int* ctx, int* yn) {
 }
 
 // ---- forward: den (NUM = false) or string (NUM = true) shortest distance ----
-template <bool BF16, int SR, bool NUM, bool VIT>
+// STAGE: the frame's weights are copied to LDS once (coalesced) and the
+// in-arc gathers read LDS; otherwise they read W from global memory.
+template <bool BF16, int SR, bool NUM, bool VIT, bool STAGE>
 __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
   const int S = NUM ? a.U + 1 : a.C, K = a.K, R = a.R;
-  float* va = sm;
+  int* gsm = (int*)sm;  // graph copy (a.gst): C+1 + 2*C*V ints
+  const int* g_off;
+  const int* g_arc;
+  const int* g_tab;
+  t_graph(a, gsm, &g_off, &g_arc, &g_tab);
+  float* va = sm + (a.gst ? (a.C + 1 + 2 * a.C * a.V + 3) / 4 * 4 : 0);
   float* vl = va + S;
   float* vn = vl + S;
   float* acc = vn + S;
   int* ctx = (int*)(acc + S);
   int* yn = ctx + S;
+  float* wl = (float*)(yn + S);  // STAGE: [C*(V+1)]
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   for (int q = tid; q < S; q += nthr) va[q] = q == 0 ? t_one<SR>() : t_zero<SR>();
   if (NUM && tid == 0) t_walk(a, b, ctx, yn);
   __syncthreads();
-  DenGraph dg{a.in_off, a.in_arc, a.V, R};
+  DenGraph dg{g_off, g_arc, a.V, R};
   NumGraph ng{ctx, yn};
   const long long FR = (long long)a.C * R;
   const int KK = K > 0 ? K : 1;
+  (void)g_tab;
   for (int t = 0; t < a.T; ++t) {
     if (a.alpha)
       for (int q = tid; q < S; q += nthr) a.alpha[((long long)b * a.T + t) * S + q] = va[q];
     if (t >= nf) continue;  // padding frames carry alpha (lattices.py:460-461)
     const unsigned char* wf = a.W + ((long long)b * a.T + t) * FR * (BF16 ? 2 : 4);
+    if (STAGE) {
+      for (int e = tid; e < FR; e += nthr) wl[e] = ldw<BF16>(wf, e);
+      __syncthreads();
+    }
+    auto wr = [&](int i) { return STAGE ? wl[i] : ldw<BF16>(wf, i); };
     int* bpt = VIT ? a.bp + (((long long)b * a.T + t) * KK) * a.C : nullptr;
     if (K == 0) {  // FrameDependent.forward, alignments.py:286-297
       for (int q = tid; q < S; q += nthr) {
         const int bi = NUM ? ng.blank(q) : dg.blank(q);
-        const float bt = t_times<SR>(va[q], ldw<BF16>(wf, bi));
+        const float bt = t_times<SR>(va[q], wr(bi));
         int ap = -1;
-        const float r = NUM ? t_reduce<BF16, SR>(ng, q, va, wf, &ap)
-                            : t_reduce<BF16, SR>(dg, q, va, wf, &ap);
+        const float r = NUM ? t_reduce<SR>(ng, q, va, wr, &ap)
+                            : t_reduce<SR>(dg, q, va, wr, &ap);
         float o;
         if constexpr (SR == M_LOG) {
           o = t_lae(bt, r);
@@ -211,7 +247,7 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
     // blank, i = 0..K, summed (MaxTropical: the first max term wins)
     for (int q = tid; q < S; q += nthr) {
       const int bi = NUM ? ng.blank(q) : dg.blank(q);
-      acc[q] = t_times<SR>(va[q], ldw<BF16>(wf, bi));
+      acc[q] = t_times<SR>(va[q], wr(bi));
       vl[q] = va[q];
       if (VIT) a.win[((long long)b * a.T + t) * a.C + q] = 0;
     }
@@ -219,13 +255,13 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
     for (int i = 1; i <= K; ++i) {
       for (int q = tid; q < S; q += nthr) {
         int ap = -1;
-        vn[q] = NUM ? t_reduce<BF16, SR>(ng, q, vl, wf, &ap) : t_reduce<BF16, SR>(dg, q, vl, wf, &ap);
+        vn[q] = NUM ? t_reduce<SR>(ng, q, vl, wr, &ap) : t_reduce<SR>(dg, q, vl, wr, &ap);
         if (VIT) bpt[(long long)(i - 1) * a.C + q] = ap;
       }
       __syncthreads();
       for (int q = tid; q < S; q += nthr) {
         const int bi = NUM ? ng.blank(q) : dg.blank(q);
-        const float term = t_times<SR>(vn[q], ldw<BF16>(wf, bi));
+        const float term = t_times<SR>(vn[q], wr(bi));
         if constexpr (SR == M_LOG) {
           acc[q] = t_lae(acc[q], term);
         } else if constexpr (SR == M_MAX) {
@@ -302,15 +338,21 @@ __global__ void tab_backtrace_kernel(const TArgs a) {
 // (:379-419) in reverse frame order; the K+1 blank and K lexical marginals of
 // a frame add up on the shared weights. Utterances whose loss is not finite,
 // and padding frames, get dW = 0. do_den = 0 (local normalisation): zeros.
-template <bool BF16>
+template <bool BF16, bool STAGE>
 __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
   const int C = a.C, V = a.V, R = a.R, K = a.K;
-  float* beta = sm;
+  int* gsm = (int*)sm;
+  const int* g_off;
+  const int* g_arc;
+  const int* g_tab;
+  t_graph(a, gsm, &g_off, &g_arc, &g_tab);
+  float* beta = sm + (a.gst ? (C + 1 + 2 * C * V + 3) / 4 * 4 : 0);
   float* nbA = beta + C;
   float* nbB = nbA + C;
   float* la = nbB + C;  // [K+1][C]
+  float* wl = la + (long long)(K + 1) * C;  // STAGE: [C*(V+1)]
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const float lz = a.local ? 0.f : a.den_in[b];
@@ -319,7 +361,7 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
   const long long FR = (long long)C * R;
   for (int q = tid; q < C; q += nthr) beta[q] = 0.f;  // every state final (Log.ones)
   __syncthreads();
-  DenGraph dg{a.in_off, a.in_arc, V, R};
+  DenGraph dg{g_off, g_arc, V, R};
   for (int t = a.T - 1; t >= 0; --t) {
     const long long fo = ((long long)b * a.T + t) * FR;
     if (t >= nf || !live) {
@@ -327,20 +369,23 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
       continue;
     }
     const unsigned char* wf = a.W + fo * (BF16 ? 2 : 4);
+    if (STAGE)
+      for (long long e = tid; e < FR; e += nthr) wl[e] = ldw<BF16>(wf, e);
+    auto wr = [&](int i) { return STAGE ? wl[i] : ldw<BF16>(wf, i); };
     for (int q = tid; q < C; q += nthr) la[q] = a.hist[((long long)b * a.T + t) * C + q];
     __syncthreads();
     for (int i = 1; i <= K; ++i) {  // lexical_alphas
       for (int q = tid; q < C; q += nthr)
-        la[(long long)i * C + q] = t_reduce<BF16, M_LOG>(dg, q, la + (long long)(i - 1) * C, wf, nullptr);
+        la[(long long)i * C + q] = t_reduce<M_LOG>(dg, q, la + (long long)(i - 1) * C, wr, nullptr);
       __syncthreads();
     }
     for (int p = tid; p < C; p += nthr) {
-      const float bb = ldw<BF16>(wf, p * R) + beta[p];
+      const float bb = wr(p * R) + beta[p];
       if (K == 0) {
         stw<false>(a.dW, fo + p * R, lt_exp(la[p] + bb - lz));
         Lse s;
         for (int y = 1; y <= V; ++y) {
-          const float lb = ldw<BF16>(wf, p * R + y) + beta[a.table[p * V + y - 1]];
+          const float lb = wr(p * R + y) + beta[g_tab[p * V + y - 1]];
           stw<false>(a.dW, fo + p * R + y, lt_exp(la[p] + lb - lz));
           s.add(lb);
         }
@@ -360,14 +405,14 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
         Lse s;
         const float lj = la[(long long)j * C + p] - lz;
         for (int y = 1; y <= V; ++y) {
-          const float lb = ldw<BF16>(wf, p * R + y) + cur[a.table[p * V + y - 1]];
+          const float lb = wr(p * R + y) + cur[g_tab[p * V + y - 1]];
           const float m = lt_exp(lb + lj);
           const long long e = fo + p * R + y;
           // the same thread owns (p, y) for every j: accumulate in place
           stw<false>(a.dW, e, j == K - 1 ? m : ldw<false>((const unsigned char*)a.dW, e) + m);
           s.add(lb);
         }
-        nxt[p] = t_lae(ldw<BF16>(wf, p * R) + beta[p], s.get());
+        nxt[p] = t_lae(wr(p * R) + beta[p], s.get());
       }
       __syncthreads();
       float* tmp = cur;
@@ -428,11 +473,12 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
   for (int t = nf - 1; t >= 0; --t) {
     const long long fo = ((long long)b * a.T + t) * FR;
     const unsigned char* wf = a.W + fo * (BF16 ? 2 : 4);
+    auto wr = [&](int i) { return ldw<BF16>(wf, i); };
     for (int u = tid; u < S; u += nthr) la[u] = a.hist[((long long)b * a.T + t) * S + u];
     __syncthreads();
     for (int i = 1; i <= K; ++i) {
       for (int u = tid; u < S; u += nthr)
-        la[(long long)i * S + u] = t_reduce<BF16, M_LOG>(ng, u, la + (long long)(i - 1) * S, wf, nullptr);
+        la[(long long)i * S + u] = t_reduce<M_LOG>(ng, u, la + (long long)(i - 1) * S, wr, nullptr);
       __syncthreads();
     }
     for (int u = tid; u < S; u += nthr) {
@@ -538,21 +584,36 @@ int t_launch(KF k, int grid, int lds_bytes, hipStream_t st, const TArgs& a) {
   return t_hip(hipGetLastError(), "table kernel launch");
 }
 
-int fwd_lds(int S, bool num) { return 4 * (4 * S) + (num ? 8 * S : 0); }
+int fwd_lds(int S) { return 4 * (4 * S) + 8 * S; }
+// stage a frame in LDS when it fits beside the state vectors
+constexpr int kStageBudget = 144 * 1024;
+
+template <bool BF16, bool STG>
+int launch_t_fwd_s(int sr, bool num, bool vit, const TArgs& a, int lds, hipStream_t st) {
+  if (vit) return t_launch(tab_fwd_kernel<BF16, M_MAX, false, true, STG>, a.B, lds, st, a);
+  if (num) {
+    if (sr == M_LOG) return t_launch(tab_fwd_kernel<BF16, M_LOG, true, false, false>, a.B, lds, st, a);
+    if (sr == M_MAX) return t_launch(tab_fwd_kernel<BF16, M_MAX, true, false, false>, a.B, lds, st, a);
+    return t_launch(tab_fwd_kernel<BF16, M_REAL, true, false, false>, a.B, lds, st, a);
+  }
+  if (sr == M_LOG) return t_launch(tab_fwd_kernel<BF16, M_LOG, false, false, STG>, a.B, lds, st, a);
+  if (sr == M_MAX) return t_launch(tab_fwd_kernel<BF16, M_MAX, false, false, STG>, a.B, lds, st, a);
+  return t_launch(tab_fwd_kernel<BF16, M_REAL, false, false, STG>, a.B, lds, st, a);
+}
+
+int graph_lds(const TArgs& a) { return 4 * ((a.C + 1 + 2 * a.C * a.V + 3) / 4 * 4); }
 
 template <bool BF16>
-int launch_t_fwd(int sr, bool num, bool vit, const TArgs& a, hipStream_t st) {
+int launch_t_fwd(int sr, bool num, bool vit, const TArgs& a0, hipStream_t st) {
+  TArgs a = a0;
   const int S = num ? a.U + 1 : a.C;
-  const int lds = fwd_lds(S, num);
-  if (vit) return t_launch(tab_fwd_kernel<BF16, M_MAX, false, true>, a.B, lds, st, a);
-  if (num) {
-    if (sr == M_LOG) return t_launch(tab_fwd_kernel<BF16, M_LOG, true, false>, a.B, lds, st, a);
-    if (sr == M_MAX) return t_launch(tab_fwd_kernel<BF16, M_MAX, true, false>, a.B, lds, st, a);
-    return t_launch(tab_fwd_kernel<BF16, M_REAL, true, false>, a.B, lds, st, a);
-  }
-  if (sr == M_LOG) return t_launch(tab_fwd_kernel<BF16, M_LOG, false, false>, a.B, lds, st, a);
-  if (sr == M_MAX) return t_launch(tab_fwd_kernel<BF16, M_MAX, false, false>, a.B, lds, st, a);
-  return t_launch(tab_fwd_kernel<BF16, M_REAL, false, false>, a.B, lds, st, a);
+  const long long FR = (long long)a.C * a.R;
+  int lds = fwd_lds(S);
+  a.gst = (!num && (long long)lds + graph_lds(a) <= kStageBudget) ? 1 : 0;
+  if (a.gst) lds += graph_lds(a);
+  if (!num && lds + 4 * FR <= kStageBudget)
+    return launch_t_fwd_s<BF16, true>(sr, num, vit, a, (int)(lds + 4 * FR), st);
+  return launch_t_fwd_s<BF16, false>(sr, num, vit, a, lds, st);
 }
 
 int t_fwd(int sr, bool num, bool vit, const TArgs& a, bool bf16, hipStream_t st) {
@@ -676,9 +737,18 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   a.dW = dwf;
   const int C = a.C, S = a.U + 1, K = a.K;
   a.hist = hd;
-  const int lds_d = 4 * (3 * C + (K + 1) * C);
-  rc = bf16 ? t_launch(tab_bwd_den_kernel<true>, a.B, lds_d, st, a)
-            : t_launch(tab_bwd_den_kernel<false>, a.B, lds_d, st, a);
+  int lds_d = 4 * (3 * C + (K + 1) * C);
+  const long long FRd = (long long)C * a.R;
+  a.gst = ((long long)lds_d + graph_lds(a) <= kStageBudget) ? 1 : 0;
+  if (a.gst) lds_d += graph_lds(a);
+  if (lds_d + 4 * FRd <= kStageBudget) {
+    const int l2 = (int)(lds_d + 4 * FRd);
+    rc = bf16 ? t_launch(tab_bwd_den_kernel<true, true>, a.B, l2, st, a)
+              : t_launch(tab_bwd_den_kernel<false, true>, a.B, l2, st, a);
+  } else {
+    rc = bf16 ? t_launch(tab_bwd_den_kernel<true, false>, a.B, lds_d, st, a)
+              : t_launch(tab_bwd_den_kernel<false, false>, a.B, lds_d, st, a);
+  }
   if (rc) return rc;
   a.hist = hn;
   const int lds_n = 4 * (5 * S + (K + 1) * S) + 4 * (2 * S + 2 * S);
