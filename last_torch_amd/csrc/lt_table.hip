@@ -19,6 +19,7 @@
 // is a few barrier-separated sweeps over the states (one per expansion). The
 // FullNGram x FrameDependent shapes of the benchmark use the tuned kernels
 // of lt_lattice.hip / lt_pipe.hip; this file is the general path.
+#include <type_traits>
 #include <vector>
 
 #include "lt_kernels.h"
@@ -45,14 +46,15 @@ struct TArgs {
   int* qstar;           // Viterbi: [B] best final state
   long long* vlabels;   // Viterbi: [B, T*A]
   int B, T, U, C, V, R, K, conv, local;
-  int gst;  // the graph (in_off, in_arc, table) is copied to LDS first
 };
 
 // Copies the graph arrays to LDS at g (ints: in_off [C+1], in_arc [C*V],
-// table [C*V]) when a.gst, and returns the arrays to use.
+// table [C*V]) when GST, and returns the arrays to use (compile-time choice,
+// so the compiler knows which memory every access goes to).
+template <bool GST>
 LT_DEVINL void t_graph(const TArgs& a, int* g, const int** in_off, const int** in_arc,
                        const int** table) {
-  if (!a.gst) {
+  if constexpr (!GST) {
     *in_off = a.in_off;
     *in_arc = a.in_arc;
     *table = a.table;
@@ -61,7 +63,9 @@ LT_DEVINL void t_graph(const TArgs& a, int* g, const int** in_off, const int** i
   const int C = a.C, CV = a.C * a.V;
   for (int i = threadIdx.x; i <= C; i += blockDim.x) g[i] = a.in_off[i];
   for (int i = threadIdx.x; i < CV; i += blockDim.x) {
-    g[C + 1 + i] = a.in_arc[i];
+    const int id = a.in_arc[i];
+    const int p = id / a.V;
+    g[C + 1 + i] = p | ((id - p * a.V) << 16);  // DenGraphP packing
     g[C + 1 + CV + i] = a.table[i];
   }
   *in_off = g;
@@ -115,6 +119,22 @@ struct DenGraph {
     *widx = p * R + (id - p * V) + 1;
   }
 };
+// The LDS copy of the CSR holds src | (label - 1) << 16 (no division).
+struct DenGraphP {
+  const int* in_off;
+  const int* in_arc;
+  int V, R;
+  LT_DEVINL int blank(int q) const { return q * R; }
+  LT_DEVINL int nin(int q) const { return in_off[q + 1] - in_off[q]; }
+  LT_DEVINL int pos0(int q) const { return in_off[q]; }
+  LT_DEVINL void arc(int pos, int q, int* src, int* widx) const {
+    (void)q;
+    const int v = in_arc[pos];
+    const int p = v & 0xffff;
+    *src = p;
+    *widx = p * R + (v >> 16) + 1;
+  }
+};
 struct NumGraph {
   const int* ctx;  // [S] ctx state * R
   const int* yn;   // [S] label class of the arc leaving u
@@ -165,6 +185,77 @@ LT_DEVINL float t_reduce(const G& g, int q, const float* x, const WR& wr, int* a
   }
 }
 
+// Merge a running logsumexp over G aligned lanes (xor shuffles; every lane of
+// the wave takes part) -- the lanes then hold the group's total.
+template <int G>
+LT_DEVINL void lse_merge(Lse& l) {
+  for (int o = 1; o < G; o <<= 1) {
+    const float m2 = __shfl_xor(l.m, o, 64), s2 = __shfl_xor(l.s, o, 64);
+    const float M = fmaxf(l.m, m2);
+    if (M == -kInf) {
+      l.s = 0.f;
+    } else {
+      l.s = l.s * lt_exp(l.m - M) + s2 * lt_exp(m2 - M);
+      l.m = M;
+    }
+  }
+}
+
+// t_reduce with G lanes per state: lane j takes in-arcs j, j+G, ... and the
+// partials merge over the group (MaxTropical: the first max by CSR position,
+// as the serial reduce). `valid` false: the lane joins the shuffles only.
+template <int SR, int G, typename Gr, typename WR>
+LT_DEVINL float t_reduce_g(const Gr& g, int q, bool valid, const float* x, const WR& wr,
+                           int* argpos) {
+  if constexpr (G == 1) {
+    return valid ? t_reduce<SR>(g, q, x, wr, argpos) : t_zero<SR>();
+  } else {
+    const int j = threadIdx.x & (G - 1);
+    const int n = valid ? g.nin(q) : 0, p0 = valid ? g.pos0(q) : 0;
+    if constexpr (SR == M_LOG) {
+      Lse l;
+      for (int k = j; k < n; k += G) {
+        int src, wi;
+        g.arc(p0 + k, q, &src, &wi);
+        l.add(x[src] + wr(wi));
+      }
+      lse_merge<G>(l);
+      return l.get();
+    } else if constexpr (SR == M_MAX) {
+      float r = -kInf;
+      int ra = -1;
+      for (int k = j; k < n; k += G) {
+        int src, wi;
+        g.arc(p0 + k, q, &src, &wi);
+        const float v = x[src] + wr(wi);
+        if (ra < 0 || v > r) {
+          r = v;
+          ra = p0 + k;
+        }
+      }
+      for (int o = 1; o < G; o <<= 1) {
+        const float r2 = __shfl_xor(r, o, 64);
+        const int a2 = __shfl_xor(ra, o, 64);
+        if (a2 >= 0 && (ra < 0 || r2 > r || (r2 == r && a2 < ra))) {
+          r = r2;
+          ra = a2;
+        }
+      }
+      if (argpos) *argpos = ra;
+      return r;
+    } else {
+      float r = 0.f;
+      for (int k = j; k < n; k += G) {
+        int src, wi;
+        g.arc(p0 + k, q, &src, &wi);
+        r += x[src] * wr(wi);
+      }
+      for (int o = 1; o < G; o <<= 1) r += __shfl_xor(r, o, 64);
+      return r;
+    }
+  }
+}
+
 // context_states / next-label classes of the string (contexts.py:109-146,
 // lattices.py:314-315 and 336-338); one thread
 LT_DEVINL void t_walk(const TArgs& a, int b, int* ctx, int* yn) {
@@ -178,6 +269,42 @@ LT_DEVINL void t_walk(const TArgs& a, int b, int* ctx, int* yn) {
   }
 }
 
+// Frame staging: the first kPf*blockDim weights of frame t+1 are loaded into
+// registers while frame t is processed (one memory round trip per frame,
+// hidden), the rest of a large frame in batches of kPf loads per thread.
+constexpr int kPf = 8;
+template <bool BF16>
+struct FrameStage {
+  float r[kPf];
+  LT_DEVINL void fetch(const unsigned char* wf, long long FR) {
+#pragma unroll
+    for (int u = 0; u < kPf; ++u) {
+      const long long e = (long long)u * blockDim.x + threadIdx.x;
+      r[u] = (wf && e < FR) ? ldw<BF16>(wf, e) : 0.f;
+    }
+  }
+  LT_DEVINL void store(float* wl, const unsigned char* wf, long long FR) {
+#pragma unroll
+    for (int u = 0; u < kPf; ++u) {
+      const long long e = (long long)u * blockDim.x + threadIdx.x;
+      if (e < FR) wl[e] = r[u];
+    }
+    for (long long e0 = (long long)kPf * blockDim.x; e0 < FR; e0 += (long long)kPf * blockDim.x) {
+      float t[kPf];
+#pragma unroll
+      for (int u = 0; u < kPf; ++u) {
+        const long long e = e0 + (long long)u * blockDim.x + threadIdx.x;
+        t[u] = e < FR ? ldw<BF16>(wf, e) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kPf; ++u) {
+        const long long e = e0 + (long long)u * blockDim.x + threadIdx.x;
+        if (e < FR) wl[e] = t[u];
+      }
+    }
+  }
+};
+
 // ---- forward: den (NUM = false) or string (NUM = true) shortest distance ----
 // STAGE: the frame's weights are copied to LDS once (coalesced) and the
 // in-arc gathers read LDS; otherwise they read W from global memory.
@@ -186,12 +313,12 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
   const int S = NUM ? a.U + 1 : a.C, K = a.K, R = a.R;
-  int* gsm = (int*)sm;  // graph copy (a.gst): C+1 + 2*C*V ints
+  int* gsm = (int*)sm;  // graph copy (STAGE): C+1 + 2*C*V ints
   const int* g_off;
   const int* g_arc;
   const int* g_tab;
-  t_graph(a, gsm, &g_off, &g_arc, &g_tab);
-  float* va = sm + (a.gst ? (a.C + 1 + 2 * a.C * a.V + 3) / 4 * 4 : 0);
+  t_graph<STAGE>(a, gsm, &g_off, &g_arc, &g_tab);
+  float* va = sm + (STAGE ? (a.C + 1 + 2 * a.C * a.V + 3) / 4 * 4 : 0);
   float* vl = va + S;
   float* vn = vl + S;
   float* acc = vn + S;
@@ -203,29 +330,39 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
   for (int q = tid; q < S; q += nthr) va[q] = q == 0 ? t_one<SR>() : t_zero<SR>();
   if (NUM && tid == 0) t_walk(a, b, ctx, yn);
   __syncthreads();
-  DenGraph dg{g_off, g_arc, a.V, R};
+  using DG = typename std::conditional<STAGE, DenGraphP, DenGraph>::type;
+  DG dg{g_off, g_arc, a.V, R};
   NumGraph ng{ctx, yn};
   const long long FR = (long long)a.C * R;
   const int KK = K > 0 ? K : 1;
+  constexpr int G = NUM ? 1 : 8;  // lanes per state in the in-arc reductions
   (void)g_tab;
+  const long long fbytes = FR * (BF16 ? 2 : 4);
+  const unsigned char* wb = a.W + (long long)b * a.T * fbytes;
+  FrameStage<BF16> fs;
+  if (STAGE) fs.fetch(nf > 0 ? wb : nullptr, FR);
   for (int t = 0; t < a.T; ++t) {
     if (a.alpha)
       for (int q = tid; q < S; q += nthr) a.alpha[((long long)b * a.T + t) * S + q] = va[q];
     if (t >= nf) continue;  // padding frames carry alpha (lattices.py:460-461)
-    const unsigned char* wf = a.W + ((long long)b * a.T + t) * FR * (BF16 ? 2 : 4);
+    const unsigned char* wf = wb + t * fbytes;
     if (STAGE) {
-      for (int e = tid; e < FR; e += nthr) wl[e] = ldw<BF16>(wf, e);
+      fs.store(wl, wf, FR);
+      fs.fetch(t + 1 < nf ? wf + fbytes : nullptr, FR);  // next frame in flight
       __syncthreads();
     }
     auto wr = [&](int i) { return STAGE ? wl[i] : ldw<BF16>(wf, i); };
     int* bpt = VIT ? a.bp + (((long long)b * a.T + t) * KK) * a.C : nullptr;
     if (K == 0) {  // FrameDependent.forward, alignments.py:286-297
-      for (int q = tid; q < S; q += nthr) {
+      for (int q0 = 0; q0 < S; q0 += nthr / G) {
+        const int q = q0 + tid / G;
+        const bool valid = q < S;
+        int ap = -1;
+        const float r = NUM ? t_reduce_g<SR, G>(ng, q, valid, va, wr, &ap)
+                            : t_reduce_g<SR, G>(dg, q, valid, va, wr, &ap);
+        if (!valid || (tid & (G - 1))) continue;
         const int bi = NUM ? ng.blank(q) : dg.blank(q);
         const float bt = t_times<SR>(va[q], wr(bi));
-        int ap = -1;
-        const float r = NUM ? t_reduce<SR>(ng, q, va, wr, &ap)
-                            : t_reduce<SR>(dg, q, va, wr, &ap);
         float o;
         if constexpr (SR == M_LOG) {
           o = t_lae(bt, r);
@@ -253,9 +390,14 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
     }
     __syncthreads();
     for (int i = 1; i <= K; ++i) {
-      for (int q = tid; q < S; q += nthr) {
+      for (int q0 = 0; q0 < S; q0 += nthr / G) {
+        const int q = q0 + tid / G;
+        const bool valid = q < S;
         int ap = -1;
-        vn[q] = NUM ? t_reduce<SR>(ng, q, vl, wr, &ap) : t_reduce<SR>(dg, q, vl, wr, &ap);
+        const float r = NUM ? t_reduce_g<SR, G>(ng, q, valid, vl, wr, &ap)
+                            : t_reduce_g<SR, G>(dg, q, valid, vl, wr, &ap);
+        if (!valid || (tid & (G - 1))) continue;
+        vn[q] = r;
         if (VIT) bpt[(long long)(i - 1) * a.C + q] = ap;
       }
       __syncthreads();
@@ -347,8 +489,8 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
   const int* g_off;
   const int* g_arc;
   const int* g_tab;
-  t_graph(a, gsm, &g_off, &g_arc, &g_tab);
-  float* beta = sm + (a.gst ? (C + 1 + 2 * C * V + 3) / 4 * 4 : 0);
+  t_graph<STAGE>(a, gsm, &g_off, &g_arc, &g_tab);
+  float* beta = sm + (STAGE ? (C + 1 + 2 * C * V + 3) / 4 * 4 : 0);
   float* nbA = beta + C;
   float* nbB = nbA + C;
   float* la = nbB + C;  // [K+1][C]
@@ -361,7 +503,12 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
   const long long FR = (long long)C * R;
   for (int q = tid; q < C; q += nthr) beta[q] = 0.f;  // every state final (Log.ones)
   __syncthreads();
-  DenGraph dg{g_off, g_arc, V, R};
+  using DG = typename std::conditional<STAGE, DenGraphP, DenGraph>::type;
+  DG dg{g_off, g_arc, V, R};
+  constexpr int G = 8;  // lanes per state
+  FrameStage<BF16> fs;
+  if (STAGE && live && nf > 0)
+    fs.fetch(a.W + ((long long)b * a.T + nf - 1) * FR * (BF16 ? 2 : 4), FR);
   for (int t = a.T - 1; t >= 0; --t) {
     const long long fo = ((long long)b * a.T + t) * FR;
     if (t >= nf || !live) {
@@ -369,26 +516,40 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
       continue;
     }
     const unsigned char* wf = a.W + fo * (BF16 ? 2 : 4);
-    if (STAGE)
-      for (long long e = tid; e < FR; e += nthr) wl[e] = ldw<BF16>(wf, e);
+    if (STAGE) {
+      fs.store(wl, wf, FR);
+      fs.fetch(t >= 1 ? wf - FR * (BF16 ? 2 : 4) : nullptr, FR);  // frame t-1 in flight
+    }
     auto wr = [&](int i) { return STAGE ? wl[i] : ldw<BF16>(wf, i); };
     for (int q = tid; q < C; q += nthr) la[q] = a.hist[((long long)b * a.T + t) * C + q];
     __syncthreads();
     for (int i = 1; i <= K; ++i) {  // lexical_alphas
-      for (int q = tid; q < C; q += nthr)
-        la[(long long)i * C + q] = t_reduce<M_LOG>(dg, q, la + (long long)(i - 1) * C, wr, nullptr);
+      for (int q0 = 0; q0 < C; q0 += nthr / G) {
+        const int q = q0 + tid / G;
+        const bool valid = q < C;
+        const float r = t_reduce_g<M_LOG, G>(dg, q, valid, la + (long long)(i - 1) * C, wr, nullptr);
+        if (valid && !(tid & (G - 1))) la[(long long)i * C + q] = r;
+      }
       __syncthreads();
     }
-    for (int p = tid; p < C; p += nthr) {
-      const float bb = wr(p * R) + beta[p];
-      if (K == 0) {
-        stw<false>(a.dW, fo + p * R, lt_exp(la[p] + bb - lz));
-        Lse s;
-        for (int y = 1; y <= V; ++y) {
+    // G lanes per source state p: lane jg takes the labels y = jg+1, jg+1+G, ...
+    const int jg = tid & (G - 1);
+    for (int p0 = 0; p0 < C; p0 += nthr / G) {
+      const int p = p0 + tid / G;
+      const bool valid = p < C;
+      const float bb = valid ? wr(p * R) + beta[p] : 0.f;
+      Lse s;
+      if (K == 0 && valid) {
+        for (int y = 1 + jg; y <= V; y += G) {
           const float lb = wr(p * R + y) + beta[g_tab[p * V + y - 1]];
           stw<false>(a.dW, fo + p * R + y, lt_exp(la[p] + lb - lz));
           s.add(lb);
         }
+      }
+      lse_merge<G>(s);
+      if (!valid || jg) continue;
+      if (K == 0) {
+        stw<false>(a.dW, fo + p * R, lt_exp(la[p] + bb - lz));
         nbA[p] = t_lae(bb, s.get());
       } else {
         float mb = 0.f;
@@ -401,18 +562,23 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
     float* cur = nbA;
     float* nxt = nbB;
     for (int j = K - 1; j >= 0; --j) {
-      for (int p = tid; p < C; p += nthr) {
+      for (int p0 = 0; p0 < C; p0 += nthr / G) {
+        const int p = p0 + tid / G;
+        const bool valid = p < C;
         Lse s;
-        const float lj = la[(long long)j * C + p] - lz;
-        for (int y = 1; y <= V; ++y) {
-          const float lb = wr(p * R + y) + cur[g_tab[p * V + y - 1]];
-          const float m = lt_exp(lb + lj);
-          const long long e = fo + p * R + y;
-          // the same thread owns (p, y) for every j: accumulate in place
-          stw<false>(a.dW, e, j == K - 1 ? m : ldw<false>((const unsigned char*)a.dW, e) + m);
-          s.add(lb);
+        if (valid) {
+          const float lj = la[(long long)j * C + p] - lz;
+          for (int y = 1 + jg; y <= V; y += G) {
+            const float lb = wr(p * R + y) + cur[g_tab[p * V + y - 1]];
+            const float m = lt_exp(lb + lj);
+            const long long e = fo + p * R + y;
+            // the same lane owns (p, y) for every j: accumulate in place
+            stw<false>(a.dW, e, j == K - 1 ? m : ldw<false>((const unsigned char*)a.dW, e) + m);
+            s.add(lb);
+          }
         }
-        nxt[p] = t_lae(wr(p * R) + beta[p], s.get());
+        lse_merge<G>(s);
+        if (valid && !jg) nxt[p] = t_lae(wr(p * R) + beta[p], s.get());
       }
       __syncthreads();
       float* tmp = cur;
@@ -608,11 +774,12 @@ int launch_t_fwd(int sr, bool num, bool vit, const TArgs& a0, hipStream_t st) {
   TArgs a = a0;
   const int S = num ? a.U + 1 : a.C;
   const long long FR = (long long)a.C * a.R;
-  int lds = fwd_lds(S);
-  a.gst = (!num && (long long)lds + graph_lds(a) <= kStageBudget) ? 1 : 0;
-  if (a.gst) lds += graph_lds(a);
-  if (!num && lds + 4 * FR <= kStageBudget)
-    return launch_t_fwd_s<BF16, true>(sr, num, vit, a, (int)(lds + 4 * FR), st);
+  const int lds = fwd_lds(S);
+  // STAGE: graph and frame in LDS (when both fit; the string forward reads
+  // two weights per position and stages nothing)
+  const long long staged = (long long)lds + graph_lds(a) + 4 * FR;
+  if (!num && staged <= kStageBudget)
+    return launch_t_fwd_s<BF16, true>(sr, num, vit, a, (int)staged, st);
   return launch_t_fwd_s<BF16, false>(sr, num, vit, a, lds, st);
 }
 
@@ -737,12 +904,10 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   a.dW = dwf;
   const int C = a.C, S = a.U + 1, K = a.K;
   a.hist = hd;
-  int lds_d = 4 * (3 * C + (K + 1) * C);
+  const int lds_d = 4 * (3 * C + (K + 1) * C);
   const long long FRd = (long long)C * a.R;
-  a.gst = ((long long)lds_d + graph_lds(a) <= kStageBudget) ? 1 : 0;
-  if (a.gst) lds_d += graph_lds(a);
-  if (lds_d + 4 * FRd <= kStageBudget) {
-    const int l2 = (int)(lds_d + 4 * FRd);
+  if (lds_d + graph_lds(a) + 4 * FRd <= kStageBudget) {
+    const int l2 = (int)(lds_d + graph_lds(a) + 4 * FRd);
     rc = bf16 ? t_launch(tab_bwd_den_kernel<true, true>, a.B, l2, st, a)
               : t_launch(tab_bwd_den_kernel<false, true>, a.B, l2, st, a);
   } else {
