@@ -46,10 +46,9 @@
 namespace {
 
 constexpr int kPipeMaxSlots = 32;
-constexpr int kPipeNL = 18;   // helper loads per lane per frame (FR <= 1152)
-constexpr int kPipeMaxHelpers = 4;  // 6 waves: two workgroups per CU at <= 168 VGPRs
-constexpr float kLoTh = 8.673617379884035e-19f;  // 2^-60
-constexpr float kHiTh = 1.8446744073709552e19f;  // 2^64
+// 6 waves (den, num, 4 helpers); __launch_bounds__(384, 4) keeps them at
+// <= 128 VGPRs so that two workgroups share a CU in the fused launch
+constexpr int kPipeMaxHelpers = 4;
 
 struct PArgs {
   const unsigned char* W;
@@ -157,9 +156,6 @@ LT_DEVINL void st_sc1(float* p, float v) {
 }
 LT_DEVINL void st_sc1(int* p, int v) {
   __hip_atomic_store((g_int*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-LT_DEVINL float ld_sc1(const float* p) {
-  return __hip_atomic_load((g_float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 LT_DEVINL int ld_sc1(const int* p) {
   return __hip_atomic_load((g_int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
