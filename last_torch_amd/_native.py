@@ -254,11 +254,11 @@ def loss_backward(W, num_frames, labels, num_labels, log_z, num, alpha, alpha_nu
 def fused_path(batch, frames, labels, vocab_size, context_size, device=None, bf16=False):
   """Whether lt_loss_grad runs as ONE fused launch for this shape (mirrors
   lt_loss_grad: checkpointing batch size, 2B below the CU count, pipe shape;
-  LT_FUSED=0 turns it off)."""
-  if os.environ.get('LT_FUSED', '1') == '0':
-    return False
+  LT_FUSED=0/1 forces the choice)."""
   cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
-  return (prefer_checkpoints(batch, device) and 2 * batch < cus and
+  env = os.environ.get('LT_FUSED', '')
+  want = (env != '0') if env else 2 * batch < cus
+  return (want and prefer_checkpoints(batch, device) and
           pipe_path(batch, frames, labels, vocab_size, context_size, bf16))
 
 

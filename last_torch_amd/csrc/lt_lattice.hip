@@ -58,7 +58,7 @@ struct MgArgs {
   int TS;        // elements per slice tile (tpf > 1)
   int tiles;     // tiles per utterance
   unsigned mR, mF, mNK;  // magic multipliers for / (V+1), / FR, / NK
-  int off_a, off_b, off_an, off_bn, off_arc, off_sub, off_nb, off_w, lds_bytes;
+  int off_a, off_b, off_an, off_bn, off_arc, off_sub, off_nb, lds_bytes;
 };
 
 // n / d from the magic m = ceil(2^32 / d), corrected to exact.
@@ -98,23 +98,26 @@ LT_DEVINL void store_unit(unsigned char* p, const float* v) {
     q.x = __float_as_uint(v[0]); q.y = __float_as_uint(v[1]);
     q.z = __float_as_uint(v[2]); q.w = __float_as_uint(v[3]);
   }
-  *(uint4*)p = q;
+  __builtin_nontemporal_store(q.x, (unsigned*)p);  // dW is written once
+  __builtin_nontemporal_store(q.y, (unsigned*)p + 1);
+  __builtin_nontemporal_store(q.z, (unsigned*)p + 2);
+  __builtin_nontemporal_store(q.w, (unsigned*)p + 3);
 }
 
 // One tile: F whole frames (small frames) or one slice of a frame.
 //   phase 0: the tile's W as 16-B units into registers; alpha/beta (+num)
 //            rows, the arc table and a zeroed numerator buffer into LDS
 //   phase 1: each numerator chain head sums its arc's marginals -> Sub[e]
-//            (one writer per element); den marginals in registers
+//            (one writer per element; its W element comes from L2, the tile
+//            was just streamed); den marginals in registers
 //   phase 2: dW = den - Sub, 16-B stores. Misaligned tiles / the tail go
 //            element by element.
 template <bool BF16>
-__global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   constexpr int VE = BF16 ? 8 : 4;  // elements per 16-byte unit
   constexpr int ES = BF16 ? 2 : 4;
-  const int tile = blockIdx.x % a.tiles;
-  const int b = blockIdx.x / a.tiles;
+  const int tile = job % a.tiles;
+  const int b = job / a.tiles;
   const int tid = threadIdx.x, nthr = blockDim.x;
   const NGram& g = a.g;
   const int C = g.C, R = g.V + 1, NP = a.U + 1, NK = 2 * NP, FR = a.FR;
@@ -158,7 +161,6 @@ __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
   int* alink = aoff + NK;
   float* Sub = (float*)(lds + a.off_sub); // [E] numerator marginals per element
   int* nbt = (int*)(lds + a.off_nb);      // [C] next_base (n >= 2)
-  unsigned char* Wl = lds + a.off_w;      // [E] the tile's W (numerator gathers)
 
   // ---- phase 0
   uint4 wq[kMgUnits];
@@ -168,55 +170,84 @@ __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
     if (u < nunits) wq[r] = *(const uint4*)(Wb + (long long)u * 16);
   }
   const long long row0 = (long long)b * a.T + t0;
-  if (a.do_den) {
-    for (int e = tid; e < Fl * C; e += nthr) {
-      A[e] = a.alpha[row0 * C + e];
-      Bt[e] = a.beta[row0 * C + e];
-    }
-    if (g.n >= 2)
-      for (int p = tid; p < C; p += nthr) {
-        bool z;
-        nbt[p] = next_base(g, p, &z);
-      }
-  }
-  if (a.do_num) {
-    for (int e = tid; e < Fl * NP; e += nthr) {
-      AN[e] = a.alpha_num[row0 * NP + e];
-      BN[e] = a.beta_num[row0 * NP + e];
-    }
-    const int* src = a.arcs + (long long)b * 2 * NK;
-    for (int k = tid; k < 2 * NK; k += nthr) aoff[k] = src[k];
-    for (int e = tid; e < E; e += nthr) Sub[e] = 0.f;
-    // the tile's W in LDS for the numerator gathers
+  // every row load in flight at once (a strided load -> LDS loop would wait
+  // one memory latency per trip)
+  constexpr int NR = 2;  // rounds per thread covered in registers; the rest loop
+  const int nA = a.do_den ? Fl * C : 0, nN = a.do_num ? Fl * NP : 0, nK = a.do_num ? 2 * NK : 0;
+  const int* arcsrc = a.arcs + (long long)b * 2 * NK;
+  float ra[NR], rb[NR], rn[NR], rm[NR];
+  int rk[NR];
 #pragma unroll
-    for (int r = 0; r < kMgUnits; ++r) {
-      const int u = tid + r * 256;
-      if (u < nunits) *(uint4*)(Wl + u * 16) = wq[r];
+  for (int i = 0; i < NR; ++i) {
+    const int e = tid + i * 256;
+    if (e < nA) { ra[i] = a.alpha[row0 * C + e]; rb[i] = a.beta[row0 * C + e]; }
+    if (e < nN) { rn[i] = a.alpha_num[row0 * NP + e]; rm[i] = a.beta_num[row0 * NP + e]; }
+    if (e < nK) rk[i] = arcsrc[e];
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int e = tid + i * 256;
+    if (e < nA) { A[e] = ra[i]; Bt[e] = rb[i]; }
+    if (e < nN) { AN[e] = rn[i]; BN[e] = rm[i]; }
+    if (e < nK) aoff[e] = rk[i];
+  }
+  for (int e = tid + NR * 256; e < nA; e += nthr) {
+    A[e] = a.alpha[row0 * C + e];
+    Bt[e] = a.beta[row0 * C + e];
+  }
+  for (int e = tid + NR * 256; e < nN; e += nthr) {
+    AN[e] = a.alpha_num[row0 * NP + e];
+    BN[e] = a.beta_num[row0 * NP + e];
+  }
+  for (int e = tid + NR * 256; e < nK; e += nthr) aoff[e] = arcsrc[e];
+  if (a.do_den && g.n >= 2)
+    for (int p = tid; p < C; p += nthr) {
+      bool z;
+      nbt[p] = next_base(g, p, &z);
     }
-    for (int e = nunits * VE + tid; e < E; e += nthr) {
-      if constexpr (BF16) ((unsigned short*)Wl)[e] = ((const unsigned short*)Wb)[e];
-      else ((float*)Wl)[e] = ((const float*)Wb)[e];
-    }
+  if (a.do_num) {
+    float4* S4 = (float4*)Sub;  // the region is padded to 16 bytes
+    for (int e = tid; e < (E + 3) / 4; e += nthr) S4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
 
   // ---- phase 1: numerator chains (deterministic: chain order = ascending k)
   if (a.do_num) {
-    for (int i = tid; i < Fl * NK; i += nthr) {
-      const int f = (int)fdiv((unsigned)i, (unsigned)NK, a.mNK);
-      const int k = i - f * NK;
+    // chain i: head (el >= 0) of frame f, arc k; the heads' W elements (L2:
+    // the tile was just streamed) are gathered for NH rounds at once
+    auto head = [&](int i, int& f, int& k) {
+      f = (int)fdiv((unsigned)i, (unsigned)NK, a.mNK);
+      k = i - f * NK;
       const int o = aoff[k];
-      const int lk = alink[k];
-      if (!(lk >> 30) || o < e_lo || o >= e_hi) continue;
-      const int el = f * Ew + o - e_lo;
-      const float wv = ldw<BF16>(Wl, el);
+      if (!(alink[k] >> 30) || o < e_lo || o >= e_hi) return -1;
+      return f * Ew + o - e_lo;
+    };
+    auto chain = [&](int f, int k, float wv) {
       float sacc = 0.f;
       for (int kk = k; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
         const int u = kk >> 1;
         const float bn = BN[f * NP + ((kk & 1) ? u + 1 : u)];
         sacc += lt_exp(AN[f * NP + u] + wv + bn - nm);
       }
-      Sub[el] = gb * sacc;
+      return gb * sacc;
+    };
+    constexpr int NH = 4;
+    const int nI = Fl * NK;
+    int hel[NH], hf[NH], hk[NH];
+    float hw[NH];
+#pragma unroll
+    for (int r = 0; r < NH; ++r) {
+      const int i = tid + r * 256;
+      hel[r] = i < nI ? head(i, hf[r], hk[r]) : -1;
+      if (hel[r] >= 0) hw[r] = ldw<BF16>(Wb, hel[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < NH; ++r)
+      if (hel[r] >= 0) Sub[hel[r]] = chain(hf[r], hk[r], hw[r]);
+    for (int i = tid + NH * 256; i < nI; i += nthr) {
+      int f, k;
+      const int el = head(i, f, k);
+      if (el >= 0) Sub[el] = chain(f, k, ldw<BF16>(Wb, el));
     }
   }
   // den marginals of the register units
@@ -279,6 +310,12 @@ __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
     }
     stw<BF16>(a.dW, base + e, x);
   }
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  marg_tile<BF16>(a, (int)blockIdx.x, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -664,7 +701,6 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
   m->off_bn = off; off += do_num ? al16(4LL * m->F * NP) : 0;
   m->off_arc = off; off += do_num ? al16(8LL * NK) : 0;
   m->off_sub = off; off += do_num ? al16(4 * emax) : 0;
-  m->off_w = off; off += do_num ? al16((long long)es * emax) : 0;
   m->lds_bytes = std::max(off, 16);
   if (off > kLdsMax) return fail(LT_EUNSUPPORTED, "marginal tile exceeds LDS");
   *grid = (long long)pb->batch * m->tiles;
@@ -915,17 +951,16 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
     m.arcs = arcs; m.log_z = log_z; m.num = num; m.grad = grad; m.dW = dW;
     if (grid == 0) return LT_OK;
     hipStream_t st = (hipStream_t)stream;
-    if (m.lds_bytes > 64 * 1024) {
-      const void* k = pb->weight_dtype == LT_DTYPE_BF16 ? (const void*)marg_kernel<true>
-                                                         : (const void*)marg_kernel<false>;
-      if ((rc = hip_check(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              m.lds_bytes), "marginal LDS")))
-        return rc;
-    }
-    if (pb->weight_dtype == LT_DTYPE_BF16)
-      hipLaunchKernelGGL(marg_kernel<true>, dim3((unsigned)grid), dim3(256), m.lds_bytes, st, m);
-    else
-      hipLaunchKernelGGL(marg_kernel<false>, dim3((unsigned)grid), dim3(256), m.lds_bytes, st, m);
+    const void* k = pb->weight_dtype == LT_DTYPE_BF16 ? (const void*)marg_kernel<true>
+                                                       : (const void*)marg_kernel<false>;
+    if (m.lds_bytes > 64 * 1024 &&
+        (rc = hip_check(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            m.lds_bytes), "marginal LDS")))
+      return rc;
+    void* args[] = {&m};
+    if ((rc = hip_check(hipLaunchKernel(k, dim3((unsigned)grid), dim3(256), args, m.lds_bytes, st),
+                        "marginal launch")))
+      return rc;
     return hip_check(hipGetLastError(), "marginal launch");
   }
   if (LT_NEED(W) || !num_frames || !num_labels || !num || LT_NEED(alpha_num) || LT_NEED(dW) ||
@@ -1056,7 +1091,8 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
   const int cus = cu_count();
   const bool ck = env_int("LT_CHECKPOINTS", 2 * pb->batch <= cus ? 1 : 0) != 0;
   // fused: the recursions and the marginal pass in one launch (lt_pipe.hip)
-  if (ck && env_int("LT_FUSED", 1) && 2 * pb->batch < cus && lt_impl::pipe_eligible(pb))
+  const int fused = env_int("LT_FUSED", 2 * pb->batch < cus ? 1 : 0);
+  if (ck && fused && lt_impl::pipe_eligible(pb))
     return lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
                                 num, alpha, an, beta, bn, arcs, 2, nullptr, stream, dW,
                                 (int*)(ws + w.ctl));

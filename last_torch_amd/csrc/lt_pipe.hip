@@ -1368,7 +1368,9 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
     lds = std::max(lds, pipe_env("LT_FUSED_LDS", 0));  // e.g. > 80 KB: one workgroup per CU
     if (const char* tp = getenv("LT_FUSED_TRACE")) a.trace = (long long*)strtoull(tp, nullptr, 0);
     if (lds > 160 * 1024) return set_error(LT_EUNSUPPORTED, "pipe: fused LDS");
-    const int marg = std::max(1, pipe_env("LT_FUSED_MARG", 2 * cus - grid));
+    // marginal workgroups fill the second workgroup slot of the CUs the
+    // recursions leave; with no slot left they start as recursions retire
+    const int marg = std::max(1, pipe_env("LT_FUSED_MARG", grid < 2 * cus ? 2 * cus - grid : cus));
     grid += marg;
     const hipError_t e =
         hipMemsetAsync(fctl, 0, sizeof(int) * (4 + 4LL * pb->batch), st);
