@@ -203,7 +203,7 @@ def main():
   B, T, U, V, n = args.batch, args.frames, args.labels, args.vocab, args.context
   C = _native.num_context_states(V, n)
   W, nf, labels, nl = make_inputs(B, T, U, V, C, device, seed=1234 + rank)
-  ckpt = (_native.prefer_checkpoints(B, device) if args.design == 'auto'
+  ckpt = (_native.prefer_checkpoints(B, device, (T, U, V, n, False)) if args.design == 'auto'
           else args.design == 'checkpoints')
   fused = args.design == 'auto' and _native.fused_path(B, T, U, V, n, device)
   wall, fwd_ms, bwd_ms = run_steps(W, nf, labels, nl, V, n, args.steps, args.warmup, dist_on,
@@ -287,7 +287,7 @@ def main():
     torch.cuda.empty_cache()
     W2, nf2, lab2, nl2 = make_inputs(256, T, U, V, C, device, seed=99)
     steps2 = max(5, args.steps // 2)
-    ck2 = (_native.prefer_checkpoints(256, device) if args.design == 'auto'
+    ck2 = (_native.prefer_checkpoints(256, device, (T, U, V, n, False)) if args.design == 'auto'
            else args.design == 'checkpoints')
     wall2, f2, b2 = run_steps(W2, nf2, lab2, nl2, V, n, steps2, 2, False, checkpoints=ck2)
     fb2, bb2, _ = algorithmic_bytes(T, U, V, C, checkpoints=ck2)

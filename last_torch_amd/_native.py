@@ -173,18 +173,22 @@ def num_forward(W, num_frames, labels, num_labels, vocab_size, context_size, sem
   return num, an
 
 
-def prefer_checkpoints(batch, device=None):
+def prefer_checkpoints(batch, device=None, shape=None):
   """Whether the checkpointing loss path is the faster one for `batch`
   utterances: it runs the alpha and beta recursions as separate workgroups
   (2 per utterance) and adds a streaming marginal pass, which pays off while
-  2*batch workgroups still find idle CUs; beyond that the single-workgroup
+  2*batch workgroups still find idle CUs -- and, for shapes on the pipelined
+  bigram recursions (`shape` = (frames, labels, vocab_size, context_size,
+  bf16)), up to 1.5 CUs of utterances; beyond that the single-workgroup
   recursion backward (marginals fused into the beta recursion) is faster.
-  LT_CHECKPOINTS=0/1 forces the choice."""
+  Mirrors lt_loss_grad. LT_CHECKPOINTS=0/1 forces the choice."""
   env = os.environ.get('LT_CHECKPOINTS')
   if env in ('0', '1'):
     return env == '1'
   cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
-  return 2 * batch <= cus
+  if 2 * batch <= cus:
+    return True
+  return shape is not None and 2 * batch <= 3 * cus and pipe_path(batch, *shape)
 
 
 def pipe_path(batch, frames, labels, vocab_size, context_size, bf16=False):

@@ -1089,7 +1089,11 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
                            alpha, an, nullptr, nullptr, nullptr, stream);
   }
   const int cus = cu_count();
-  const bool ck = env_int("LT_CHECKPOINTS", 2 * pb->batch <= cus ? 1 : 0) != 0;
+  // checkpointing (alpha || beta, then the marginal pass) while 2B recursion
+  // workgroups find CUs; with the pipelined bigram recursions up to 1.5 CUs
+  // utterances (measured crossover ~1.75: tools/b256_check.py)
+  const bool ck_def = 2 * pb->batch <= cus || (lt_impl::pipe_eligible(pb) && 2 * pb->batch <= 3 * cus);
+  const bool ck = env_int("LT_CHECKPOINTS", ck_def ? 1 : 0) != 0;
   // fused: the recursions and the marginal pass in one launch (lt_pipe.hip)
   const int fused = env_int("LT_FUSED", 2 * pb->batch < cus ? 1 : 0);
   if (ck && fused && lt_impl::pipe_eligible(pb))
