@@ -4,7 +4,10 @@ Plugin surface of the lattice path: ``Semiring`` with ``zeros / ones /
 times / plus / prod / sum`` (semirings.py:80-141). ``RecognitionLattice``
 selects its HIP kernel by semiring identity (``Log``, ``MaxTropical``,
 ``Real``); the methods here are the per-element algebra used by the
-per-frame plugin methods (``FrameDependent.forward`` etc.).
+per-frame plugin methods (``FrameDependent.forward`` etc.). The tuple-valued
+semirings (``Expectation`` / ``LogLogExpectation``, ``Cartesian``) are host
+algebra only, as in the reference: the lattice's arc weights are single
+tensors, so ``RecognitionLattice`` rejects them.
 
 Differences from the reference, all bug fixes:
   * ``Log.plus`` / ``Log.sum`` have working, NaN-safe gradients (the
@@ -12,7 +15,8 @@ Differences from the reference, all bug fixes:
     returns zeros: SURVEY.md D1/D2).
   * ``zeros`` / ``ones`` accept a ``device``.
 """
-from collections.abc import Sequence
+import dataclasses
+from collections.abc import Callable, Sequence
 from typing import Any, Generic, Optional, TypeVar
 
 import torch
@@ -20,6 +24,7 @@ import torch.utils._pytree as pytree
 
 DType = Any
 T = TypeVar('T')
+S = TypeVar('S')
 
 
 def value_shape(x) -> tuple[int, ...]:
@@ -239,3 +244,78 @@ class _MaxTropicalSemiring(Semiring[torch.Tensor]):
 
 
 MaxTropical = _MaxTropicalSemiring()
+
+
+def _split_dtype(dtype):
+  return (None, None) if dtype is None else tuple(dtype)
+
+
+@dataclasses.dataclass(frozen=True)
+class Expectation(Generic[T, S], Semiring[tuple[T, S]]):
+  """Eisner's expectation semiring (semirings.py:404-479): values (w, x) with
+  w a weight in semiring ``w`` and x a weighted sum in semiring ``x``;
+  ``w_to_x`` maps a weight into ``x``. ``weighted(w, v)`` builds (w, w*v)
+  and maps v to 0 where w is the zero of ``w`` (so 0 * inf stays 0)."""
+
+  w: Semiring[T]
+  x: Semiring[S]
+  w_to_x: Callable[[T], S]
+
+  def weighted(self, w: T, v: S) -> tuple[T, S]:
+    w_is_zero = w == self.w.zeros([], w.dtype, w.device)
+    safe_v = torch.where(w_is_zero, torch.zeros_like(v), v)
+    return w, self.x.times(self.w_to_x(w), safe_v)
+
+  def zeros(self, shape, dtype=None, device=None):
+    dw, dx = _split_dtype(dtype)
+    return self.w.zeros(shape, dw, device), self.x.zeros(shape, dx, device)
+
+  def ones(self, shape, dtype=None, device=None):
+    dw, dx = _split_dtype(dtype)
+    return self.w.ones(shape, dw, device), self.x.zeros(shape, dx, device)
+
+  def times(self, a, b):
+    w_a, x_a = a
+    w_b, x_b = b
+    return (self.w.times(w_a, w_b),
+            self.x.plus(self.x.times(self.w_to_x(w_a), x_b),
+                        self.x.times(self.w_to_x(w_b), x_a)))
+
+  def plus(self, a, b):
+    return self.w.plus(a[0], b[0]), self.x.plus(a[1], b[1])
+
+  def sum(self, a, axis):  # `axis`, as the reference's tuple semirings name it
+    return self.w.sum(a[0], axis), self.x.sum(a[1], axis)
+
+
+# weight and weighted sum both in Log (semirings.py:482-484): only sums of
+# non-negative values are representable
+LogLogExpectation = Expectation(w=Log, x=Log, w_to_x=lambda x: x)
+
+
+@dataclasses.dataclass(frozen=True)
+class Cartesian(Generic[T, S], Semiring[tuple[T, S]]):
+  """Product of two semirings, componentwise (semirings.py:487-533)."""
+
+  x: Semiring[T]
+  y: Semiring[S]
+
+  def zeros(self, shape, dtype=None, device=None):
+    dx, dy = _split_dtype(dtype)
+    return self.x.zeros(shape, dx, device), self.y.zeros(shape, dy, device)
+
+  def ones(self, shape, dtype=None, device=None):
+    dx, dy = _split_dtype(dtype)
+    return self.x.ones(shape, dx, device), self.y.ones(shape, dy, device)
+
+  def times(self, a, b):
+    return self.x.times(a[0], b[0]), self.y.times(a[1], b[1])
+
+  def plus(self, a, b):
+    return self.x.plus(a[0], b[0]), self.y.plus(a[1], b[1])
+
+  def sum(self, a, axis):
+    return self.x.sum(a[0], axis), self.y.sum(a[1], axis)
+
+  def prod(self, a, axis):
+    return self.x.prod(a[0], axis), self.y.prod(a[1], axis)

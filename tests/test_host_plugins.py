@@ -213,3 +213,90 @@ def test_frame_label_dependent_host_matches_reference_fixtures():
         alpha = torch.where((t < nf)[:, None], nxt, alpha)
       d = sr.sum(alpha, dim=-1).numpy()
       np.testing.assert_allclose(d, c[f'den_{sname}'], rtol=1e-5, atol=1e-5)
+
+
+# ---- tuple semirings (semirings.py:404-533), the reference's own checks
+# (tests/semirings_test.py:256-385) restated
+def _tree_equal(a, b):
+  assert len(a) == len(b)
+  for x, y in zip(a, b):
+    np.testing.assert_array_equal(x.float().numpy(), y.float().numpy())
+
+
+def test_expectation_basics():
+  E = lt.semirings.LogLogExpectation
+  one, zero = E.ones([]), E.zeros([])
+  for wx in [E.weighted(torch.tensor([1.]), torch.tensor([2.])), one, zero]:
+    _tree_equal(E.times(wx, one), wx)
+    _tree_equal(E.times(one, wx), wx)
+    _tree_equal(E.plus(wx, zero), wx)
+    _tree_equal(E.plus(zero, wx), wx)
+
+
+def test_expectation_shape_dtypes():
+  E = lt.semirings.LogLogExpectation
+  one = E.ones([1, 2], (torch.float32, torch.bfloat16))
+  assert lt.semirings.value_shape(one) == (1, 2)
+  assert lt.semirings.value_dtype(one) == (torch.float32, torch.bfloat16)
+  zero = E.zeros([], (torch.bfloat16, torch.float32))
+  assert lt.semirings.value_shape(zero) == ()
+  assert lt.semirings.value_dtype(zero) == (torch.bfloat16, torch.float32)
+
+
+def test_expectation_weighted_and_safety():
+  E = lt.semirings.LogLogExpectation
+  w, x = E.weighted(torch.log(torch.tensor([0., 1., 2.])), torch.log(torch.tensor([3., 4., 5.])))
+  np.testing.assert_allclose(torch.exp(w), [0, 1, 2], rtol=1e-6)
+  np.testing.assert_allclose(torch.exp(x), [0 * 3, 1 * 4, 2 * 5], rtol=1e-6)
+  w, x = E.weighted(torch.tensor([-np.inf]), torch.tensor([np.inf]))
+  assert w.item() == -np.inf and x.item() == -np.inf
+
+
+def test_expectation_sum_and_entropy():
+  E = lt.semirings.LogLogExpectation
+  w, x = E.sum(E.weighted(torch.log(torch.tensor([[0., 1.], [2., 3.]])),
+                          torch.log(torch.tensor([[4., 5.], [6., 7.]]))), axis=1)
+  np.testing.assert_allclose(torch.exp(w), [1, 5], rtol=1e-6)
+  np.testing.assert_allclose(torch.exp(x), [5, 33], rtol=1e-6)
+  probs = torch.tensor([0.25, 0.25, 0.5])
+  lp = torch.log(probs)
+  wx = E.weighted(lp, torch.log(-lp))
+  log_z, log_sum = E.sum(wx, axis=0)
+  np.testing.assert_allclose(log_z, 0, atol=1e-7)
+  np.testing.assert_allclose(torch.exp(log_sum), -torch.sum(probs * lp), rtol=1e-6)
+  probs2 = torch.tensor([0.25, 0.5, 0.25])
+  lp2 = torch.log(probs2)
+  log_z, log_sum = E.sum(E.times(wx, E.weighted(lp2, torch.log(-lp2))), axis=0)
+  np.testing.assert_allclose(torch.exp(log_z), torch.sum(probs * probs2), rtol=1e-6)
+  entropy = log_z + torch.exp(log_sum - log_z)
+  np.testing.assert_allclose(
+      entropy, -torch.sum(probs * probs2 * torch.exp(-log_z) * (lp + lp2 - log_z)), rtol=0.2)
+
+
+def test_cartesian():
+  S = lt.semirings.Cartesian(lt.semirings.Real, lt.semirings.MaxTropical)
+  one, zero = S.ones([]), S.zeros([])
+  for wx in [(torch.tensor(1.0), torch.tensor(2.0)), one, zero]:
+    _tree_equal(S.times(wx, one), wx)
+    _tree_equal(S.times(one, wx), wx)
+    _tree_equal(S.plus(wx, zero), wx)
+    _tree_equal(S.plus(zero, wx), wx)
+  one = S.ones([1, 2], (torch.float32, torch.bfloat16))
+  assert lt.semirings.value_shape(one) == (1, 2)
+  assert lt.semirings.value_dtype(one) == (torch.float32, torch.bfloat16)
+  a, b = (torch.tensor(2.0), torch.tensor(1.0)), (torch.tensor(3.0), torch.tensor(4.0))
+  c = (torch.tensor([1.0, 2.0]), torch.tensor([3.0, 4.0]))
+  assert [v.item() for v in S.times(a, b)] == [6.0, 5.0]
+  assert [v.item() for v in S.plus(a, b)] == [5.0, 4.0]
+  assert [v.item() for v in S.sum(c, axis=0)] == [3.0, 4.0]
+  assert [v.item() for v in S.prod(c, axis=0)] == [2.0, 7.0]
+
+
+def test_tuple_semirings_rejected_by_lattice():
+  ctx = lt.contexts.FullNGram(vocab_size=2, context_size=1)
+  lat = lt.RecognitionLattice(context=ctx, alignment=lt.alignments.FrameDependent(),
+                              weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+                              weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(
+                                  torch.zeros([1, 3, 3])))
+  with pytest.raises(NotImplementedError):
+    lat._forward(None, torch.zeros([1, 1, 1]), torch.ones([1]), lt.semirings.LogLogExpectation)
