@@ -34,9 +34,17 @@ for s in $STEPS; do
       echo "[gpu_round] rocprofv3 kernel trace"
       rm -rf "$OUT/prof_$TAG"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o "$TAG" \
-        --output-format csv -- python3 bench.py --steps 20 --warmup 3 --cpu-utts 0 \
+        --output-format csv -- python3 bench.py --steps 20 --warmup 3 --cpu-utts 0 --no-north-star \
         > "$OUT/prof_$TAG.log" 2>&1 || { tail -40 "$OUT/prof_$TAG.log"; exit 1; }
       find "$OUT/prof_$TAG" -name '*kernel_stats.csv' -exec cat {} \;
+      ;;
+    profns)
+      echo "[gpu_round] rocprofv3 kernel trace, north-star shape (B=256)"
+      rm -rf "$OUT/profns_$TAG"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/profns_$TAG" -o "${TAG}_b256" \
+        --output-format csv -- python3 bench.py --batch 256 --steps 10 --warmup 2 --cpu-utts 0 \
+        --no-north-star > "$OUT/profns_$TAG.log" 2>&1 || { tail -40 "$OUT/profns_$TAG.log"; exit 1; }
+      find "$OUT/profns_$TAG" -name '*kernel_stats.csv' -exec cat {} \;
       ;;
     pmc)
       echo "[gpu_round] PMC passes"
