@@ -46,6 +46,7 @@ struct TArgs {
   int* qstar;           // Viterbi: [B] best final state
   long long* vlabels;   // Viterbi: [B, T*A]
   int B, T, U, C, V, R, K, conv, local;
+  int acc;  // tab_bwd_den_kernel: FrameLabelDependent dW sums in LDS
 };
 
 // Copies the graph arrays to LDS at g (ints: in_off [C+1], in_arc [C*V],
@@ -148,6 +149,45 @@ struct NumGraph {
   }
 };
 
+// The string acceptor over a compact per-frame copy of its weights:
+// wc[2u] = blank of u, wc[2u+1] = the arc leaving u (lattices.py:314-338)
+struct NumGraphC {
+  LT_DEVINL int blank(int u) const { return 2 * u; }
+  LT_DEVINL int nin(int u) const { return u >= 1 ? 1 : 0; }
+  LT_DEVINL int pos0(int u) const { return u - 1; }
+  LT_DEVINL void arc(int pos, int u, int* src, int* widx) const {
+    (void)pos;
+    *src = u - 1;
+    *widx = 2 * u - 1;
+  }
+};
+
+// Register staging of a strided per-frame gather (element e -> ld(e)): the
+// next frame's values are loaded while this frame computes, so a frame costs
+// no memory round trip of its own (N rounds per thread; the rest is loaded
+// directly when stored)
+template <int N>
+struct RegStage {
+  float r[N];
+  template <typename F>
+  LT_DEVINL void fetch(int n, const F& ld) {
+#pragma unroll
+    for (int u = 0; u < N; ++u) {
+      const int e = u * blockDim.x + threadIdx.x;
+      r[u] = e < n ? ld(e) : 0.f;
+    }
+  }
+  template <typename F>
+  LT_DEVINL void store(float* dst, int n, const F& ld) const {
+#pragma unroll
+    for (int u = 0; u < N; ++u) {
+      const int e = u * blockDim.x + threadIdx.x;
+      if (e < n) dst[e] = r[u];
+    }
+    for (int e = N * blockDim.x + threadIdx.x; e < n; e += blockDim.x) dst[e] = ld(e);
+  }
+};
+
 // (+) over the in-arcs of q of x[src] (x) w; MaxTropical keeps the first max
 template <int SR, typename G, typename WR>
 LT_DEVINL float t_reduce(const G& g, int q, const float* x, const WR& wr, int* argpos) {
@@ -210,29 +250,63 @@ LT_DEVINL float t_reduce_g(const Gr& g, int q, bool valid, const float* x, const
   if constexpr (G == 1) {
     return valid ? t_reduce<SR>(g, q, x, wr, argpos) : t_zero<SR>();
   } else {
+    // the lane's terms are gathered NU at a time (independent LDS reads in
+    // flight together), then folded in CSR order
+    constexpr int NU = 8;
     const int j = threadIdx.x & (G - 1);
     const int n = valid ? g.nin(q) : 0, p0 = valid ? g.pos0(q) : 0;
+    float acc = SR == M_REAL ? 0.f : -kInf;  // MAX: best; LOG: running max
+    float ls = 0.f;                          // LOG: running sum at `acc`
+    int ra = -1;
+    for (int k0 = j; k0 < n; k0 += G * NU) {
+      float v[NU];
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        const int k = k0 + G * i;
+        v[i] = SR == M_REAL ? 0.f : -kInf;
+        if (k < n) {
+          int src, wi;
+          g.arc(p0 + k, q, &src, &wi);
+          v[i] = SR == M_REAL ? x[src] * wr(wi) : x[src] + wr(wi);
+        }
+      }
+      if constexpr (SR == M_LOG) {
+        float cm = v[0];
+#pragma unroll
+        for (int i = 1; i < NU; ++i) cm = fmaxf(cm, v[i]);
+        if (cm == kInf) {  // +inf dominates (the reference's safe max)
+          acc = kInf;
+          ls = 1.f;
+        } else if (cm != -kInf && acc != kInf) {
+          float cs = 0.f;
+#pragma unroll
+          for (int i = 0; i < NU; ++i) cs += lt_exp(v[i] - cm);
+          const float M = fmaxf(acc, cm);
+          ls = ls * lt_exp(acc - M) + cs * lt_exp(cm - M);
+          acc = M;
+        }
+      } else if constexpr (SR == M_MAX) {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+          const int k = k0 + G * i;
+          if (k < n && (ra < 0 || v[i] > acc)) {
+            acc = v[i];
+            ra = p0 + k;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) acc += v[i];
+      }
+    }
     if constexpr (SR == M_LOG) {
       Lse l;
-      for (int k = j; k < n; k += G) {
-        int src, wi;
-        g.arc(p0 + k, q, &src, &wi);
-        l.add(x[src] + wr(wi));
-      }
+      l.m = acc;
+      l.s = ls;
       lse_merge<G>(l);
       return l.get();
     } else if constexpr (SR == M_MAX) {
-      float r = -kInf;
-      int ra = -1;
-      for (int k = j; k < n; k += G) {
-        int src, wi;
-        g.arc(p0 + k, q, &src, &wi);
-        const float v = x[src] + wr(wi);
-        if (ra < 0 || v > r) {
-          r = v;
-          ra = p0 + k;
-        }
-      }
+      float r = acc;
       for (int o = 1; o < G; o <<= 1) {
         const float r2 = __shfl_xor(r, o, 64);
         const int a2 = __shfl_xor(ra, o, 64);
@@ -244,12 +318,7 @@ LT_DEVINL float t_reduce_g(const Gr& g, int q, bool valid, const float* x, const
       if (argpos) *argpos = ra;
       return r;
     } else {
-      float r = 0.f;
-      for (int k = j; k < n; k += G) {
-        int src, wi;
-        g.arc(p0 + k, q, &src, &wi);
-        r += x[src] * wr(wi);
-      }
+      float r = acc;
       for (int o = 1; o < G; o <<= 1) r += __shfl_xor(r, o, 64);
       return r;
     }
@@ -324,7 +393,7 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
   float* acc = vn + S;
   int* ctx = (int*)(acc + S);
   int* yn = ctx + S;
-  float* wl = (float*)(yn + S);  // STAGE: [C*(V+1)]
+  float* wl = (float*)(yn + S);  // STAGE: [C*(V+1)]; NUM: the compact weights [2S]
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   for (int q = tid; q < S; q += nthr) va[q] = q == 0 ? t_one<SR>() : t_zero<SR>();
@@ -332,7 +401,7 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
   __syncthreads();
   using DG = typename std::conditional<STAGE, DenGraphP, DenGraph>::type;
   DG dg{g_off, g_arc, a.V, R};
-  NumGraph ng{ctx, yn};
+  NumGraphC ng;
   const long long FR = (long long)a.C * R;
   const int KK = K > 0 ? K : 1;
   constexpr int G = NUM ? 1 : 8;  // lanes per state in the in-arc reductions
@@ -341,6 +410,12 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
   const unsigned char* wb = a.W + (long long)b * a.T * fbytes;
   FrameStage<BF16> fs;
   if (STAGE) fs.fetch(nf > 0 ? wb : nullptr, FR);
+  // the string's two weights per position, gathered one frame ahead
+  auto ldc = [&](const unsigned char* w) {
+    return [=](int e) { return ldw<BF16>(w, ctx[e >> 1] + ((e & 1) ? yn[e >> 1] : 0)); };
+  };
+  RegStage<2> cs;
+  if (NUM) cs.fetch(nf > 0 ? 2 * S : 0, ldc(wb));
   for (int t = 0; t < a.T; ++t) {
     if (a.alpha)
       for (int q = tid; q < S; q += nthr) a.alpha[((long long)b * a.T + t) * S + q] = va[q];
@@ -351,7 +426,12 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
       fs.fetch(t + 1 < nf ? wf + fbytes : nullptr, FR);  // next frame in flight
       __syncthreads();
     }
-    auto wr = [&](int i) { return STAGE ? wl[i] : ldw<BF16>(wf, i); };
+    if (NUM) {
+      cs.store(wl, 2 * S, ldc(wf));
+      cs.fetch(t + 1 < nf ? 2 * S : 0, ldc(wf + fbytes));
+      __syncthreads();
+    }
+    auto wr = [&](int i) { return (STAGE || NUM) ? wl[i] : ldw<BF16>(wf, i); };
     int* bpt = VIT ? a.bp + (((long long)b * a.T + t) * KK) * a.C : nullptr;
     if (K == 0) {  // FrameDependent.forward, alignments.py:286-297
       for (int q0 = 0; q0 < S; q0 += nthr / G) {
@@ -495,6 +575,7 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
   float* nbB = nbA + C;
   float* la = nbB + C;  // [K+1][C]
   float* wl = la + (long long)(K + 1) * C;  // STAGE: [C*(V+1)]
+  float* dacc = wl + (long long)C * R;      // a.acc: the frame's lexical dW sums [C*(V+1)]
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const float lz = a.local ? 0.f : a.den_in[b];
@@ -509,6 +590,11 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
   FrameStage<BF16> fs;
   if (STAGE && live && nf > 0)
     fs.fetch(a.W + ((long long)b * a.T + nf - 1) * FR * (BF16 ? 2 : 4), FR);
+  auto ldh = [&](int t) {  // alpha row of frame t, gathered one frame ahead
+    return [=](int e) { return a.hist[((long long)b * a.T + t) * C + e]; };
+  };
+  RegStage<1> hs;
+  if (live && nf > 0) hs.fetch(C, ldh(nf - 1));
   for (int t = a.T - 1; t >= 0; --t) {
     const long long fo = ((long long)b * a.T + t) * FR;
     if (t >= nf || !live) {
@@ -521,7 +607,8 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
       fs.fetch(t >= 1 ? wf - FR * (BF16 ? 2 : 4) : nullptr, FR);  // frame t-1 in flight
     }
     auto wr = [&](int i) { return STAGE ? wl[i] : ldw<BF16>(wf, i); };
-    for (int q = tid; q < C; q += nthr) la[q] = a.hist[((long long)b * a.T + t) * C + q];
+    hs.store(la, C, ldh(t));
+    hs.fetch(t >= 1 ? C : 0, ldh(t - 1));
     __syncthreads();
     for (int i = 1; i <= K; ++i) {  // lexical_alphas
       for (int q0 = 0; q0 < C; q0 += nthr / G) {
@@ -540,6 +627,7 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
       const float bb = valid ? wr(p * R) + beta[p] : 0.f;
       Lse s;
       if (K == 0 && valid) {
+#pragma unroll 4
         for (int y = 1 + jg; y <= V; y += G) {
           const float lb = wr(p * R + y) + beta[g_tab[p * V + y - 1]];
           stw<false>(a.dW, fo + p * R + y, lt_exp(la[p] + lb - lz));
@@ -568,12 +656,20 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
         Lse s;
         if (valid) {
           const float lj = la[(long long)j * C + p] - lz;
+#pragma unroll 4
           for (int y = 1 + jg; y <= V; y += G) {
             const float lb = wr(p * R + y) + cur[g_tab[p * V + y - 1]];
             const float m = lt_exp(lb + lj);
             const long long e = fo + p * R + y;
             // the same lane owns (p, y) for every j: accumulate in place
-            stw<false>(a.dW, e, j == K - 1 ? m : ldw<false>((const unsigned char*)a.dW, e) + m);
+            // (in LDS when it fits; dW is written once, at j = 0)
+            if (STAGE && a.acc) {
+              const float v = (j == K - 1 ? 0.f : dacc[p * R + y]) + m;
+              if (j == 0) stw<false>(a.dW, e, v);
+              else dacc[p * R + y] = v;
+            } else {
+              stw<false>(a.dW, e, j == K - 1 ? m : ldw<false>((const unsigned char*)a.dW, e) + m);
+            }
             s.add(lb);
           }
         }
@@ -608,6 +704,8 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
   int* ctx = (int*)(la + (long long)(K + 1) * S);
   int* yn = ctx + S;
   int* link = yn + S;  // [NK]: head << 30 | (next entry + 1)
+  float* wc = (float*)(link + NK);  // [2S] the frame's string weights (NumGraphC)
+  float* dh = wc + 2 * S;           // [NK] dW at the chain heads' elements
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const float nm = a.num_in[b];
@@ -634,13 +732,39 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
     link[k] = (head << 30) | (nxt + 1);
   }
   __syncthreads();
-  NumGraph ng{ctx, yn};
+  NumGraphC ng;
   const long long FR = (long long)a.C * a.R;
+  // every global read of a frame (alpha_num row, the string's weights, dW at
+  // the heads) is gathered one frame ahead into registers
+  auto ldh = [&](int t) {
+    return [=](int e) { return a.hist[((long long)b * a.T + t) * S + e]; };
+  };
+  auto ldc = [&](int t) {
+    const unsigned char* w = a.W + ((long long)b * a.T + t) * FR * (BF16 ? 2 : 4);
+    return [=](int e) { return ldw<BF16>(w, ctx[e >> 1] + ((e & 1) ? yn[e >> 1] : 0)); };
+  };
+  auto ldd = [&](int t) {
+    const long long fo = ((long long)b * a.T + t) * FR;
+    return [=](int k) {
+      return (link[k] >> 30) ? ldw<false>((const unsigned char*)a.dW, fo + elem(k)) : 0.f;
+    };
+  };
+  RegStage<1> hs;
+  RegStage<2> cs, ds;
+  if (nf > 0) {
+    hs.fetch(S, ldh(nf - 1));
+    cs.fetch(2 * S, ldc(nf - 1));
+    ds.fetch(NK, ldd(nf - 1));
+  }
   for (int t = nf - 1; t >= 0; --t) {
     const long long fo = ((long long)b * a.T + t) * FR;
-    const unsigned char* wf = a.W + fo * (BF16 ? 2 : 4);
-    auto wr = [&](int i) { return ldw<BF16>(wf, i); };
-    for (int u = tid; u < S; u += nthr) la[u] = a.hist[((long long)b * a.T + t) * S + u];
+    hs.store(la, S, ldh(t));
+    cs.store(wc, 2 * S, ldc(t));
+    ds.store(dh, NK, ldd(t));
+    hs.fetch(t >= 1 ? S : 0, ldh(t - 1));
+    cs.fetch(t >= 1 ? 2 * S : 0, ldc(t - 1));
+    ds.fetch(t >= 1 ? NK : 0, ldd(t - 1));
+    auto wr = [&](int i) { return wc[i]; };
     __syncthreads();
     for (int i = 1; i <= K; ++i) {
       for (int u = tid; u < S; u += nthr)
@@ -648,9 +772,9 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
       __syncthreads();
     }
     for (int u = tid; u < S; u += nthr) {
-      const float bb = ldw<BF16>(wf, ctx[u]) + beta[u];
+      const float bb = wc[2 * u] + beta[u];
       if (K == 0) {
-        const float lb = u < U ? ldw<BF16>(wf, ctx[u] + yn[u]) + beta[u + 1] : -kInf;
+        const float lb = u < U ? wc[2 * u + 1] + beta[u + 1] : -kInf;
         mb[u] = lt_exp(la[u] + bb - nm);
         ml[u] = lt_exp(la[u] + lb - nm);
         nbA[u] = t_lae(bb, lb);
@@ -667,9 +791,9 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
     float* nxt = nbB;
     for (int j = K - 1; j >= 0; --j) {
       for (int u = tid; u < S; u += nthr) {
-        const float lb = u < U ? ldw<BF16>(wf, ctx[u] + yn[u]) + cur[u + 1] : -kInf;
+        const float lb = u < U ? wc[2 * u + 1] + cur[u + 1] : -kInf;
         ml[u] += lt_exp(lb + la[(long long)j * S + u] - nm);
-        nxt[u] = t_lae(ldw<BF16>(wf, ctx[u]) + beta[u], lb);
+        nxt[u] = t_lae(wc[2 * u] + beta[u], lb);
       }
       __syncthreads();
       float* tmp = cur;
@@ -682,8 +806,7 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
       float s = 0.f;
       for (int kk = k; kk >= 0; kk = (link[kk] & 0x3fffffff) - 1)
         s += (kk & 1) ? ml[kk >> 1] : mb[kk >> 1];
-      const long long e = fo + elem(k);
-      stw<false>(a.dW, e, ldw<false>((const unsigned char*)a.dW, e) - s);
+      stw<false>(a.dW, fo + elem(k), dh[k] - s);
     }
     __syncthreads();
     for (int u = tid; u < S; u += nthr) beta[u] = cur[u];
@@ -774,7 +897,7 @@ int launch_t_fwd(int sr, bool num, bool vit, const TArgs& a0, hipStream_t st) {
   TArgs a = a0;
   const int S = num ? a.U + 1 : a.C;
   const long long FR = (long long)a.C * a.R;
-  const int lds = fwd_lds(S);
+  const int lds = fwd_lds(S) + (num ? 8 * S : 0);  // + the string's compact weights
   // STAGE: graph and frame in LDS (when both fit; the string forward reads
   // two weights per position and stages nothing)
   const long long staged = (long long)lds + graph_lds(a) + 4 * FR;
@@ -907,7 +1030,9 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   const int lds_d = 4 * (3 * C + (K + 1) * C);
   const long long FRd = (long long)C * a.R;
   if (lds_d + graph_lds(a) + 4 * FRd <= kStageBudget) {
-    const int l2 = (int)(lds_d + graph_lds(a) + 4 * FRd);
+    // + the lexical dW sums of FrameLabelDependent(K > 0) when they fit too
+    a.acc = K > 0 && lds_d + graph_lds(a) + 8 * FRd <= kStageBudget;
+    const int l2 = (int)(lds_d + graph_lds(a) + (a.acc ? 8 : 4) * FRd);
     rc = bf16 ? t_launch(tab_bwd_den_kernel<true, true>, a.B, l2, st, a)
               : t_launch(tab_bwd_den_kernel<false, true>, a.B, l2, st, a);
   } else {
@@ -916,7 +1041,7 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   }
   if (rc) return rc;
   a.hist = hn;
-  const int lds_n = 4 * (5 * S + (K + 1) * S) + 4 * (2 * S + 2 * S);
+  const int lds_n = 4 * (5 * S + (K + 1) * S) + 4 * (2 * S + 2 * S) + 4 * (2 * S + 2 * S);
   rc = bf16 ? t_launch(tab_bwd_num_kernel<true>, a.B, lds_n, st, a)
             : t_launch(tab_bwd_num_kernel<false>, a.B, lds_n, st, a);
   if (rc || !bf16) return rc;
