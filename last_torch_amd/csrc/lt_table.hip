@@ -47,6 +47,11 @@ struct TArgs {
   long long* vlabels;   // Viterbi: [B, T*A]
   int B, T, U, C, V, R, K, conv, local;
   int acc;  // tab_bwd_den_kernel: FrameLabelDependent dW sums in LDS
+  // numerator backward run beside the denominator's (lt_table_loss_grad):
+  // the chain heads' marginal sums go to nsub [B,T,2S] and their elements to
+  // ntab [B,2S] (-1: none), subtracted from dW afterwards (tab_apply_kernel)
+  float* nsub;
+  int* ntab;
 };
 
 // Copies the graph arrays to LDS at g (ints: in_off [C+1], in_arc [C*V],
@@ -378,9 +383,8 @@ struct FrameStage {
 // STAGE: the frame's weights are copied to LDS once (coalesced) and the
 // in-arc gathers read LDS; otherwise they read W from global memory.
 template <bool BF16, int SR, bool NUM, bool VIT, bool STAGE>
-__global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
   const int S = NUM ? a.U + 1 : a.C, K = a.K, R = a.R;
   int* gsm = (int*)sm;  // graph copy (STAGE): C+1 + 2*C*V ints
   const int* g_off;
@@ -531,6 +535,28 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
   }
 }
 
+template <bool BF16, int SR, bool NUM, bool VIT, bool STAGE>
+__global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  tab_fwd_body<BF16, SR, NUM, VIT, STAGE>(a, (int)blockIdx.x, sm);
+}
+
+// Log denominator (blocks [0, B)) and string (blocks [B, 2B)) forwards side
+// by side; the loss is formed afterwards (tab_loss_kernel)
+template <bool BF16, bool STAGE>
+__global__ __launch_bounds__(256) void tab_fwd2_kernel(const TArgs ad, const TArgs an) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int blk = (int)blockIdx.x;
+  if (blk < ad.B) tab_fwd_body<BF16, M_LOG, false, false, STAGE>(ad, blk, sm);
+  else tab_fwd_body<BF16, M_LOG, true, false, false>(an, blk - ad.B, sm);
+}
+
+__global__ void tab_loss_kernel(float* loss, const float* log_z, const float* num, int B,
+                                int local) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) loss[b] = local ? -num[b] : log_z[b] - num[b];  // lattices.py:131-183
+}
+
 // ---- Viterbi backtrace (lattices.py:185-247, per utterance: no D6) ----------
 __global__ void tab_backtrace_kernel(const TArgs a) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -561,9 +587,8 @@ __global__ void tab_backtrace_kernel(const TArgs a) {
 // a frame add up on the shared weights. Utterances whose loss is not finite,
 // and padding frames, get dW = 0. do_den = 0 (local normalisation): zeros.
 template <bool BF16, bool STAGE>
-__global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
   const int C = a.C, V = a.V, R = a.R, K = a.K;
   int* gsm = (int*)sm;
   const int* g_off;
@@ -690,10 +715,15 @@ __global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
 // The same recursion on the string acceptor; string arcs that share a lattice
 // arc are summed by their chain head in ascending order (one writer per
 // element and frame: deterministic).
-template <bool BF16>
-__global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
+template <bool BF16, bool STAGE>
+__global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  tab_bwd_den_body<BF16, STAGE>(a, (int)blockIdx.x, sm);
+}
+
+template <bool BF16>
+LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
   const int U = a.U, S = U + 1, K = a.K, NK = 2 * S;
   float* beta = sm;
   float* nbA = beta + S;
@@ -711,7 +741,11 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
   const float nm = a.num_in[b];
   const float lz = a.local ? 0.f : a.den_in[b];
   const bool live = __builtin_isfinite(nm) && (a.local || __builtin_isfinite(lz));
-  if (!live) return;  // the denominator kernel wrote zeros
+  if (!live) {  // the denominator kernel wrote zeros
+    if (a.ntab)
+      for (int k = tid; k < NK; k += nthr) a.ntab[(long long)b * NK + k] = -1;
+    return;
+  }
   const int nl = a.nlab[b];
   if (tid == 0) t_walk(a, b, ctx, yn);
   for (int u = tid; u < S; u += nthr) beta[u] = u == nl ? 0.f : -kInf;
@@ -730,6 +764,7 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
         else if (k2 > k && nxt < 0) nxt = k2;
       }
     link[k] = (head << 30) | (nxt + 1);
+    if (a.ntab) a.ntab[(long long)b * NK + k] = head ? o : -1;
   }
   __syncthreads();
   NumGraphC ng;
@@ -746,7 +781,8 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
   auto ldd = [&](int t) {
     const long long fo = ((long long)b * a.T + t) * FR;
     return [=](int k) {
-      return (link[k] >> 30) ? ldw<false>((const unsigned char*)a.dW, fo + elem(k)) : 0.f;
+      return (!a.nsub && (link[k] >> 30)) ? ldw<false>((const unsigned char*)a.dW, fo + elem(k))
+                                          : 0.f;
     };
   };
   RegStage<1> hs;
@@ -806,11 +842,46 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
       float s = 0.f;
       for (int kk = k; kk >= 0; kk = (link[kk] & 0x3fffffff) - 1)
         s += (kk & 1) ? ml[kk >> 1] : mb[kk >> 1];
-      stw<false>(a.dW, fo + elem(k), dh[k] - s);
+      if (a.nsub) a.nsub[((long long)b * a.T + t) * NK + k] = s;
+      else stw<false>(a.dW, fo + elem(k), dh[k] - s);
     }
     __syncthreads();
     for (int u = tid; u < S; u += nthr) beta[u] = cur[u];
     __syncthreads();
+  }
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  tab_bwd_num_body<BF16>(a, (int)blockIdx.x, sm);
+}
+
+// denominator (blocks [0, B)) and numerator (blocks [B, 2B)) backwards side
+// by side; the numerator's sums land in nsub
+template <bool BF16, bool STAGE>
+__global__ __launch_bounds__(256) void tab_bwd2_kernel(const TArgs ad, const TArgs an) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int blk = (int)blockIdx.x;
+  if (blk < ad.B) tab_bwd_den_body<BF16, STAGE>(ad, blk, sm);
+  else tab_bwd_num_body<BF16>(an, blk - ad.B, sm);
+}
+
+// dW -= the numerator's chain-head sums (one writer per element and frame)
+__global__ __launch_bounds__(256) void tab_apply_kernel(const TArgs a) {
+  const int NK = 2 * (a.U + 1);
+  const long long FR = (long long)a.C * a.R;
+  const long long n = (long long)a.B * a.T * NK;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % NK);
+    const long long bt = i / NK;
+    const int b = (int)(bt / a.T), t = (int)(bt - (long long)b * a.T);
+    const int el = a.ntab[(long long)b * NK + k];
+    int nf = a.nfr[b];
+    nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+    if (el < 0 || t >= nf) continue;
+    a.dW[bt * FR + el] -= a.nsub[i];
   }
 }
 
@@ -873,6 +944,18 @@ int t_launch(KF k, int grid, int lds_bytes, hipStream_t st, const TArgs& a) {
   return t_hip(hipGetLastError(), "table kernel launch");
 }
 
+template <typename KF>
+int t_launch2(KF k, int grid, int lds_bytes, hipStream_t st, const TArgs& a1, const TArgs& a2) {
+  if (lds_bytes > kTabLds) return t_fail(LT_EUNSUPPORTED, "table lattice state exceeds LDS");
+  if (lds_bytes > 64 * 1024)
+    if (int rc = t_hip(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           lds_bytes), "table LDS"))
+      return rc;
+  if (grid == 0) return LT_OK;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds_bytes, st, a1, a2);
+  return t_hip(hipGetLastError(), "table kernel launch");
+}
+
 int fwd_lds(int S) { return 4 * (4 * S) + 8 * S; }
 // stage a frame in LDS when it fits beside the state vectors
 constexpr int kStageBudget = 144 * 1024;
@@ -911,15 +994,17 @@ int t_fwd(int sr, bool num, bool vit, const TArgs& a, bool bf16, hipStream_t st)
 }
 
 struct GradLayout {
-  size_t hd, hn, dwf, total;
+  size_t hd, hn, nsub, ntab, dwf, total;
 };
 GradLayout grad_layout(const lt_graph* g, const lt_table_problem* pb) {
   auto up = [](long long x) { return (size_t)((x + 255) & ~255LL); };
   GradLayout l;
-  const long long BT = (long long)pb->batch * pb->max_frames;
+  const long long BT = (long long)pb->batch * pb->max_frames, NK = 2LL * (pb->max_labels + 1);
   l.hd = 0;
   l.hn = up(4 * BT * g->num_states);
-  l.dwf = l.hn + up(4 * BT * (pb->max_labels + 1));
+  l.nsub = l.hn + up(4 * BT * (pb->max_labels + 1));
+  l.ntab = l.nsub + up(4 * BT * NK);
+  l.dwf = l.ntab + up(4LL * pb->batch * NK);
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   l.total = l.dwf + (bf16 ? up(4 * BT * g->num_states * (g->vocab_size + 1)) : 0);
   return l;
@@ -1005,46 +1090,74 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   a.labels = labels;
   a.nlab = num_labels;
   a.local = local_norm ? 1 : 0;
+  const int C = a.C, S = a.U + 1, K = a.K;
+  const long long FR = (long long)C * a.R;
   int rc;
-  if (!local_norm) {  // log_z and the alpha history
-    a.dist = log_z;
-    a.alpha = hd;
-    if ((rc = t_fwd(M_LOG, false, false, a, bf16, st))) return rc;
+  // ---- forwards: denominator (log_z, alpha history) and string side by side
+  TArgs ad = a, an = a;
+  ad.dist = log_z;
+  ad.alpha = hd;
+  an.dist = num;
+  an.alpha = hn;
+  if (!local_norm) {
+    const int ln = fwd_lds(S) + 8 * S;
+    const int ld = fwd_lds(C);
+    const long long staged = (long long)ld + graph_lds(a) + 4 * FR;
+    if (staged <= kStageBudget) {
+      const int l2 = std::max((int)staged, ln);
+      rc = bf16 ? t_launch2(tab_fwd2_kernel<true, true>, 2 * a.B, l2, st, ad, an)
+                : t_launch2(tab_fwd2_kernel<false, true>, 2 * a.B, l2, st, ad, an);
+    } else {
+      const int l2 = std::max(ld, ln);
+      rc = bf16 ? t_launch2(tab_fwd2_kernel<true, false>, 2 * a.B, l2, st, ad, an)
+                : t_launch2(tab_fwd2_kernel<false, false>, 2 * a.B, l2, st, ad, an);
+    }
+    if (rc) return rc;
   } else {
     if ((rc = t_hip(hipMemsetAsync(log_z, 0, sizeof(float) * pb->batch, st), "memset"))) return rc;
+    if ((rc = t_fwd(M_LOG, true, false, an, bf16, st))) return rc;
   }
-  a.dist = num;
-  a.alpha = hn;
-  a.loss = loss;
-  a.den_in = log_z;
-  if ((rc = t_fwd(M_LOG, true, false, a, bf16, st))) return rc;
+  hipLaunchKernelGGL(tab_loss_kernel, dim3((pb->batch + 255) / 256), dim3(256), 0, st, loss,
+                     (const float*)log_z, (const float*)num, pb->batch, a.local);
+  if ((rc = t_hip(hipGetLastError(), "loss launch"))) return rc;
   if (!dW) return LT_OK;
+  // ---- backwards side by side; then dW -= the numerator's head sums
+  float* dwf = bf16 ? (float*)((char*)workspace + l.dwf) : (float*)dW;
   a.dist = nullptr;
   a.alpha = nullptr;
   a.loss = nullptr;
   a.num_in = num;
-  float* dwf = bf16 ? (float*)((char*)workspace + l.dwf) : (float*)dW;
+  a.den_in = log_z;
   a.dW = dwf;
-  const int C = a.C, S = a.U + 1, K = a.K;
-  a.hist = hd;
+  a.nsub = (float*)((char*)workspace + l.nsub);
+  a.ntab = (int*)((char*)workspace + l.ntab);
+  ad = a;
+  an = a;
+  ad.hist = hd;
+  ad.nsub = nullptr;
+  ad.ntab = nullptr;
+  an.hist = hn;
   const int lds_d = 4 * (3 * C + (K + 1) * C);
-  const long long FRd = (long long)C * a.R;
-  if (lds_d + graph_lds(a) + 4 * FRd <= kStageBudget) {
+  const int lds_n = 4 * (5 * S + (K + 1) * S) + 4 * (2 * S + 2 * S) + 4 * (2 * S + 2 * S);
+  if (lds_d + graph_lds(a) + 4 * FR <= kStageBudget) {
     // + the lexical dW sums of FrameLabelDependent(K > 0) when they fit too
-    a.acc = K > 0 && lds_d + graph_lds(a) + 8 * FRd <= kStageBudget;
-    const int l2 = (int)(lds_d + graph_lds(a) + (a.acc ? 8 : 4) * FRd);
-    rc = bf16 ? t_launch(tab_bwd_den_kernel<true, true>, a.B, l2, st, a)
-              : t_launch(tab_bwd_den_kernel<false, true>, a.B, l2, st, a);
+    ad.acc = K > 0 && lds_d + graph_lds(a) + 8 * FR <= kStageBudget;
+    const int l2 = std::max((int)(lds_d + graph_lds(a) + (ad.acc ? 8 : 4) * FR), lds_n);
+    rc = bf16 ? t_launch2(tab_bwd2_kernel<true, true>, 2 * a.B, l2, st, ad, an)
+              : t_launch2(tab_bwd2_kernel<false, true>, 2 * a.B, l2, st, ad, an);
   } else {
-    rc = bf16 ? t_launch(tab_bwd_den_kernel<true, false>, a.B, lds_d, st, a)
-              : t_launch(tab_bwd_den_kernel<false, false>, a.B, lds_d, st, a);
+    const int l2 = std::max(lds_d, lds_n);
+    rc = bf16 ? t_launch2(tab_bwd2_kernel<true, false>, 2 * a.B, l2, st, ad, an)
+              : t_launch2(tab_bwd2_kernel<false, false>, 2 * a.B, l2, st, ad, an);
   }
   if (rc) return rc;
-  a.hist = hn;
-  const int lds_n = 4 * (5 * S + (K + 1) * S) + 4 * (2 * S + 2 * S) + 4 * (2 * S + 2 * S);
-  rc = bf16 ? t_launch(tab_bwd_num_kernel<true>, a.B, lds_n, st, a)
-            : t_launch(tab_bwd_num_kernel<false>, a.B, lds_n, st, a);
-  if (rc || !bf16) return rc;
+  {
+    const long long n = (long long)a.B * a.T * 2 * S;
+    const int blocks = (int)std::min<long long>(4096, (n + 255) / 256);
+    if (blocks > 0) hipLaunchKernelGGL(tab_apply_kernel, dim3(blocks), dim3(256), 0, st, a);
+    if ((rc = t_hip(hipGetLastError(), "numerator apply launch"))) return rc;
+  }
+  if (!bf16) return LT_OK;
   const long long n = (long long)a.B * a.T * C * a.R;
   const int blocks = (int)std::min<long long>(4096, (n + 255) / 256);
   if (blocks > 0)
