@@ -108,6 +108,8 @@ LT_DEVINL float t_one() { return SR == M_REAL ? 1.f : 0.f; }
 template <int SR>
 LT_DEVINL float t_times(float a, float b) { return SR == M_REAL ? a * b : a + b; }
 
+constexpr int kTabMaxThreads = 512;
+
 // Graph accessors: the context lattice (states p, in-arcs from the CSR) and
 // the string acceptor (positions u, one in-arc from u-1; lattices.py:314-338).
 struct DenGraph {
@@ -536,7 +538,7 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
 }
 
 template <bool BF16, int SR, bool NUM, bool VIT, bool STAGE>
-__global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
+__global__ __launch_bounds__(kTabMaxThreads) void tab_fwd_kernel(const TArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   tab_fwd_body<BF16, SR, NUM, VIT, STAGE>(a, (int)blockIdx.x, sm);
 }
@@ -544,7 +546,7 @@ __global__ __launch_bounds__(256) void tab_fwd_kernel(const TArgs a) {
 // Log denominator (blocks [0, B)) and string (blocks [B, 2B)) forwards side
 // by side; the loss is formed afterwards (tab_loss_kernel)
 template <bool BF16, bool STAGE>
-__global__ __launch_bounds__(256) void tab_fwd2_kernel(const TArgs ad, const TArgs an) {
+__global__ __launch_bounds__(kTabMaxThreads) void tab_fwd2_kernel(const TArgs ad, const TArgs an) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int blk = (int)blockIdx.x;
   if (blk < ad.B) tab_fwd_body<BF16, M_LOG, false, false, STAGE>(ad, blk, sm);
@@ -716,7 +718,7 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
 // arc are summed by their chain head in ascending order (one writer per
 // element and frame: deterministic).
 template <bool BF16, bool STAGE>
-__global__ __launch_bounds__(256) void tab_bwd_den_kernel(const TArgs a) {
+__global__ __launch_bounds__(kTabMaxThreads) void tab_bwd_den_kernel(const TArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   tab_bwd_den_body<BF16, STAGE>(a, (int)blockIdx.x, sm);
 }
@@ -852,7 +854,7 @@ LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
 }
 
 template <bool BF16>
-__global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
+__global__ __launch_bounds__(kTabMaxThreads) void tab_bwd_num_kernel(const TArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   tab_bwd_num_body<BF16>(a, (int)blockIdx.x, sm);
 }
@@ -860,7 +862,7 @@ __global__ __launch_bounds__(256) void tab_bwd_num_kernel(const TArgs a) {
 // denominator (blocks [0, B)) and numerator (blocks [B, 2B)) backwards side
 // by side; the numerator's sums land in nsub
 template <bool BF16, bool STAGE>
-__global__ __launch_bounds__(256) void tab_bwd2_kernel(const TArgs ad, const TArgs an) {
+__global__ __launch_bounds__(kTabMaxThreads) void tab_bwd2_kernel(const TArgs ad, const TArgs an) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int blk = (int)blockIdx.x;
   if (blk < ad.B) tab_bwd_den_body<BF16, STAGE>(ad, blk, sm);
@@ -932,6 +934,14 @@ TArgs t_args(const lt_graph* g, const lt_table_problem* pb, const void* W, const
   return a;
 }
 
+// threads per utterance workgroup: the denominator reductions take 8 lanes
+// per state, so 512 threads cover up to 64 states in one pass
+int tab_threads(const TArgs& a) {
+  const char* e = getenv("LT_TAB_THREADS");
+  const int t = (e && *e) ? atoi(e) : (a.C > 32 ? 512 : 256);
+  return t >= 512 ? 512 : 256;
+}
+
 template <typename KF>
 int t_launch(KF k, int grid, int lds_bytes, hipStream_t st, const TArgs& a) {
   if (lds_bytes > kTabLds) return t_fail(LT_EUNSUPPORTED, "table lattice state exceeds LDS");
@@ -940,7 +950,7 @@ int t_launch(KF k, int grid, int lds_bytes, hipStream_t st, const TArgs& a) {
                                            lds_bytes), "table LDS"))
       return rc;
   if (grid == 0) return LT_OK;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds_bytes, st, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(tab_threads(a)), lds_bytes, st, a);
   return t_hip(hipGetLastError(), "table kernel launch");
 }
 
@@ -952,7 +962,7 @@ int t_launch2(KF k, int grid, int lds_bytes, hipStream_t st, const TArgs& a1, co
                                            lds_bytes), "table LDS"))
       return rc;
   if (grid == 0) return LT_OK;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds_bytes, st, a1, a2);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(tab_threads(a1)), lds_bytes, st, a1, a2);
   return t_hip(hipGetLastError(), "table kernel launch");
 }
 
