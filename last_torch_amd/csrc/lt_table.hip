@@ -560,6 +560,54 @@ __global__ void tab_loss_kernel(float* loss, const float* log_z, const float* nu
 }
 
 // ---- Viterbi backtrace (lattices.py:185-247, per utterance: no D6) ----------
+// One workgroup per utterance: chunks of backpointer rows (and the in-arc
+// table) are staged in LDS by the workgroup, one thread walks them (a frame
+// costs LDS latencies, not dependent global loads). `chunk` frames per stage;
+// `arcs_lds`: the in-arc table fits beside them.
+__global__ __launch_bounds__(256) void tab_backtrace_lds_kernel(const TArgs a, int chunk,
+                                                                 int arcs_lds) {
+  extern __shared__ __attribute__((aligned(16))) int lsm[];
+  const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int C = a.C, V = a.V, K = a.K, KK = K > 0 ? K : 1, A = K > 0 ? K + 1 : 1;
+  long long* lab = a.vlabels + (long long)b * a.T * A;
+  for (long long i = tid; i < (long long)a.T * A; i += nthr) lab[i] = 0;
+  int* arcs = lsm;                              // [C*V] (arcs_lds)
+  int* bpl = lsm + (arcs_lds ? C * V : 0);      // [chunk][KK][C]
+  unsigned char* wl = (unsigned char*)(bpl + (long long)chunk * KK * C);  // [chunk][C]
+  if (arcs_lds)
+    for (int i = tid; i < C * V; i += nthr) arcs[i] = a.in_arc[i];
+  const int* arc_tab = arcs_lds ? arcs : a.in_arc;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // zeros land before the walk's labels
+  __syncthreads();
+  int q = a.qstar[b];
+  for (int t1 = nf; t1 > 0; t1 -= chunk) {
+    const int t0 = t1 - chunk < 0 ? 0 : t1 - chunk;
+    const int* src = a.bp + ((long long)b * a.T + t0) * KK * C;
+    for (int e = tid; e < (t1 - t0) * KK * C; e += nthr) bpl[e] = src[e];
+    if (K > 0) {
+      const unsigned char* ws = a.win + ((long long)b * a.T + t0) * C;
+      for (int e = tid; e < (t1 - t0) * C; e += nthr) wl[e] = ws[e];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int t = t1 - 1; t >= t0; --t) {
+        const int i = K > 0 ? wl[(t - t0) * C + q] : 1;
+        for (int j = i; j >= 1; --j) {
+          const int pos = bpl[((t - t0) * KK + j - 1) * C + q];
+          if (pos < 0) break;  // FrameDependent: blank won
+          const int id = arc_tab[pos];
+          const int p = id / V, y = id - p * V + 1;
+          lab[(long long)t * A + j - 1] = a.conv ? y - 1 : y;
+          q = p;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void tab_backtrace_kernel(const TArgs a) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= a.B) return;
@@ -1208,9 +1256,22 @@ int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* 
   a.vlabels = (long long*)labels;
   hipStream_t st = (hipStream_t)stream;
   if (int rc = t_fwd(M_MAX, false, true, a, pb->weight_dtype == LT_DTYPE_BF16, st)) return rc;
-  const int threads = 64;
-  hipLaunchKernelGGL(tab_backtrace_kernel, dim3((a.B + threads - 1) / threads), dim3(threads), 0,
-                     st, a);
+  // staged walk when a frame's backpointers fit in LDS, else one thread per
+  // utterance straight from global memory
+  const long long per_frame = 4LL * KK * a.C + (a.K > 0 ? a.C : 0);
+  const long long arcs_bytes = 4LL * a.C * a.V;
+  const long long budget = 60 * 1024;
+  const int arcs_lds = arcs_bytes <= budget / 2 ? 1 : 0;
+  const long long room = budget - (arcs_lds ? arcs_bytes : 0);
+  const int chunk = (int)std::min<long long>(std::max(1, a.T), room / per_frame);
+  if (chunk >= 1 && !getenv("LT_TAB_BT_SERIAL")) {
+    const int lds = (int)((arcs_lds ? arcs_bytes : 0) + chunk * per_frame + 16);
+    hipLaunchKernelGGL(tab_backtrace_lds_kernel, dim3(a.B), dim3(256), lds, st, a, chunk, arcs_lds);
+  } else {
+    const int threads = 64;
+    hipLaunchKernelGGL(tab_backtrace_kernel, dim3((a.B + threads - 1) / threads), dim3(threads), 0,
+                       st, a);
+  }
   return t_hip(hipGetLastError(), "backtrace launch");
 }
 
