@@ -34,7 +34,11 @@ $(OBJ)/lt_table.o: $(CSRC)/lt_table.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_table.o $(INST_OBJS)
+$(OBJ)/lt_producer.o: $(CSRC)/lt_producer.hip $(DEPS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(INST_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
 oracle:
@@ -58,6 +62,6 @@ $(STAMP_OBJ)/lt_lattice.o: $(CSRC)/lt_lattice.hip $(DEPS)
 $(STAMP_OBJ)/lt_pipe.o: $(CSRC)/lt_pipe.hip $(DEPS)
 	@mkdir -p $(STAMP_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -c -o $@ $<
-stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_table.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
+stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(STAMP_OBJ)/liblt_lattice_stamps.so $^
 .PHONY: stamps

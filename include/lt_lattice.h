@@ -246,6 +246,18 @@ int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* 
                      float* path_weight, void* workspace, size_t workspace_bytes,
                      void* stream);
 
+/* Joint weight function on the matrix cores (replaces
+ * the hidden-tensor path of JointWeightFn.forward, weight_fns.py:174-227):
+ *   W[f, c, y] = out_bias[y] + sum_h out_weight[y, h] * tanh(ctx_proj[c, h] + frame_proj[f, h])
+ * for f < rows (= B*T), c < num_states, y < out_dim (= V+1; <= 64), h < hidden
+ * (a multiple of 16). ctx_proj [num_states, hidden], frame_proj [rows, hidden],
+ * out_weight [out_dim, hidden], out_bias [out_dim]: fp32, 16-byte aligned. W
+ * [rows, num_states, out_dim] in weight_dtype. The tanh values and out_weight
+ * enter the products as bf16, sums are fp32. */
+int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t out_dim,
+                     const float* ctx_proj, const float* frame_proj, const float* out_weight,
+                     const float* out_bias, void* W, int32_t weight_dtype, void* stream);
+
 /* Thread-local description of the last error; never NULL. */
 const char* lt_last_error(void);
 /* Library version string. */

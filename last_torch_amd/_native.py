@@ -68,6 +68,7 @@ _SIG = {
     'lt_table_loss_grad': [_G, _TP, _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
     'lt_table_viterbi_workspace_bytes': [_G, _TP, ctypes.POINTER(ctypes.c_size_t)],
     'lt_table_viterbi': [_G, _TP, _P, _P, _I32, _P, _P, _P, ctypes.c_size_t, _P],
+    'lt_joint_weights': [ctypes.c_int64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P],
     'lt_viterbi_workspace_bytes': [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_size_t)],
     'lt_viterbi': [ctypes.POINTER(Problem), _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t,
                    _P],
@@ -441,3 +442,25 @@ def table_viterbi(graph, W, num_frames, label_convention):
                                 _ptr(num_frames), label_convention, _ptr(labels), _ptr(weight),
                                 _ptr(ws), nbytes.value, _stream()), 'lt_table_viterbi')
   return labels, weight
+
+
+def joint_weights(ctx_proj, frame_proj, out_weight, out_bias, dtype=torch.float32):
+  """lt_joint_weights: W [..., C, R] = out_bias + tanh(ctx_proj[c] + frame_proj[...]) @
+  out_weight^T on the matrix cores (bf16 products, fp32 sums); frame_proj
+  [..., H], ctx_proj [C, H], out_weight [R, H], out_bias [R] (fp32)."""
+  for name, t in (('ctx_proj', ctx_proj), ('frame_proj', frame_proj),
+                  ('out_weight', out_weight), ('out_bias', out_bias)):
+    if not t.is_cuda:
+      raise LatticeLibraryError(f'lt_joint_weights: {name} must be on a ROCm device')
+    if t.dtype != torch.float32:
+      raise TypeError(f'lt_joint_weights: {name} must be float32, got {t.dtype}')
+  C, H = ctx_proj.shape
+  R = out_weight.shape[0]
+  pc = ctx_proj.contiguous()
+  pf = frame_proj.reshape(-1, H).contiguous()
+  wo, bo = out_weight.contiguous(), out_bias.contiguous()
+  W = torch.empty([*frame_proj.shape[:-1], C, R], dtype=dtype, device=frame_proj.device)
+  _check(lib().lt_joint_weights(pf.shape[0], C, H, R, _ptr(pc), _ptr(pf), _ptr(wo), _ptr(bo),
+                                _ptr(W), LT_DTYPE_BF16 if dtype == torch.bfloat16 else LT_DTYPE_F32,
+                                _stream()), 'lt_joint_weights')
+  return W

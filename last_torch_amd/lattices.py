@@ -239,6 +239,11 @@ class RecognitionLattice(nn.Module, Generic[T]):
     call per frame for weight functions vmap cannot trace.
     """
     tdim = frames.ndim - 2
+    if getattr(self.weight_fn, 'time_batched', False):
+      # the weight function takes any leading dims (JointWeightFn's
+      # matrix-core producer: one launch for every frame)
+      blank, lexical = self.weight_fn(cache, frames)
+      return torch.cat([blank[..., None], lexical], dim=-1)
 
     def frame_weights(frame):
       blank, lexical = self.weight_fn(cache, frame)

@@ -11,6 +11,12 @@ Differences from the reference, all bug fixes:
     every call.
   * ``SharedEmbCacher`` returns the embedding table tensor, not the module.
   * ``SharedRNNCacher`` creates its default ``LSTMCell`` once.
+
+``JointWeightFn`` on a ROCm device (all context states at once) runs the
+``lt_joint_weights`` matrix-core kernel (lt_producer.hip): the [..., C, H]
+hidden tensor is formed tile by tile in registers instead of in HBM; the
+tanh values and the output projection enter the products as bf16, the sums
+are fp32. Its backward recomputes the hidden tensor in fp32 in frame chunks.
 """
 import abc
 from typing import Callable, Generic, Optional, TypeVar
@@ -68,25 +74,82 @@ class LocallyNormalizedWeightFn(WeightFn[T]):
     self.weight_fn = weight_fn
     self.normalize = normalize
 
+  @property
+  def time_batched(self):
+    return getattr(self.weight_fn, 'time_batched', False)
+
   def forward(self, cache, frame, state=None):
     return self.normalize(*self.weight_fn(cache, frame, state))
 
 
+class _JointWeightsFn(torch.autograd.Function):
+  """W[..., c, :] = bias + tanh(pc[c] + pf[...]) @ wo^T via lt_joint_weights;
+  the backward recomputes tanh in fp32, `chunk` frame rows at a time."""
+
+  @staticmethod
+  def forward(ctx, pc, pf, wo, bias, chunk):
+    from last_torch_amd import _native
+    ctx.save_for_backward(pc, pf, wo)
+    ctx.chunk = chunk
+    return _native.joint_weights(pc, pf, wo, bias)
+
+  @staticmethod
+  def backward(ctx, gW):
+    pc, pf, wo = ctx.saved_tensors
+    C, H = pc.shape
+    R = wo.shape[0]
+    pf2 = pf.reshape(-1, H)
+    g2 = gW.reshape(-1, C, R).float()
+    dpc = torch.zeros_like(pc)
+    dpf = torch.empty_like(pf2)
+    dwo = torch.zeros_like(wo)
+    for s in range(0, pf2.shape[0], ctx.chunk):
+      hid = torch.tanh(pc[None] + pf2[s:s + ctx.chunk, None, :])  # [n, C, H]
+      g = g2[s:s + ctx.chunk]                                     # [n, C, R]
+      dwo += torch.einsum('ncr,nch->rh', g, hid)
+      dh = torch.matmul(g, wo) * (1.0 - hid * hid)
+      dpc += dh.sum(0)
+      dpf[s:s + ctx.chunk] = dh.sum(1)
+    return dpc, dpf.reshape(pf.shape), dwo, g2.sum((0, 1)), None
+
+
 class JointWeightFn(WeightFn[torch.Tensor]):
   """tanh(P_c ctx_emb[c] + P_f frame) -> (blank, V lexical) logits: the
-  shared-emb / shared-rnn weight function (weight_fns.py:174-227)."""
+  shared-emb / shared-rnn weight function (weight_fns.py:174-227).
 
-  def __init__(self, vocab_size: int, hidden_size: int, device=None):
+  ``fused`` (default): on a ROCm device, with all context states at once,
+  the logits come from the lt_joint_weights matrix-core kernel (bf16
+  products, fp32 sums; hidden_size a multiple of 16, vocab_size < 64)."""
+
+  def __init__(self, vocab_size: int, hidden_size: int, device=None, fused: bool = True,
+               backward_chunk: int = 16384):
     super().__init__()
     self.vocab_size = vocab_size
     self.hidden_size = hidden_size
+    self.fused = fused
+    self.backward_chunk = backward_chunk
     self.context_projection = nn.LazyLinear(hidden_size, bias=False, device=device)
     self.frame_projection = nn.LazyLinear(hidden_size, bias=False, device=device)
     self.to_blank = nn.Linear(hidden_size, 1, device=device)
     self.to_vocab = nn.Linear(hidden_size, vocab_size, device=device)
 
+  # forward() takes frames with any leading dims (RecognitionLattice calls it
+  # once for [batch..., T, F] instead of vmapping over T)
+  time_batched = True
+
+  def _use_kernel(self, frame):
+    return (self.fused and frame.is_cuda and frame.dtype == torch.float32 and
+            self.hidden_size % 16 == 0 and self.vocab_size + 1 <= 64)
+
   def forward(self, cache, frame, state=None):
     ctx = cache
+    if state is None and self._use_kernel(frame):
+      pc = self.context_projection(ctx)
+      pf = self.frame_projection(frame)
+      wo = torch.cat([self.to_blank.weight, self.to_vocab.weight], 0)
+      bias = torch.cat([self.to_blank.bias, self.to_vocab.bias], 0)
+      W = _JointWeightsFn.apply(pc, pf, wo, bias, self.backward_chunk)
+      return W[..., 0], W[..., 1:]
     if state is None:
       joint = self.context_projection(ctx) + self.frame_projection(frame)[..., None, :]
     else:

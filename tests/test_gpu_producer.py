@@ -1,0 +1,132 @@
+"""GPU tests of the joint weight function's matrix-core producer
+(lt_joint_weights, lt_producer.hip).
+
+Numerics reference: a plain PyTorch fp32 restatement of JointWeightFn
+(weight_fns.py:174-227): W = bias + tanh(pc[c] + pf[f]) @ wo^T. The kernel
+feeds the tanh values and wo to the matrix cores as bf16 (8 significant
+bits) and sums in fp32, so each logit may differ from fp32 by the bf16
+rounding of its products: |dW| <= 2^-7 * (|tanh| @ |wo|^T) + 1e-5 (written
+in `_tol`). Against a bf16-emulating reference (the same roundings, fp32
+sums) the difference is summation order plus the rare bf16 rounding flip
+of a tanh value: checked on the mean. The backward is fp32 (recomputed
+tanh): against torch autograd of the fp32 formula, 1e-4 relative.
+"""
+import pytest
+import torch
+
+import last_torch_amd as lt
+from last_torch_amd import _native as nat
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(pc, pf, wo, bias, bf16=False):
+  hid = torch.tanh(pc[None] + pf.reshape(-1, pf.shape[-1])[:, None, :])
+  w = wo
+  if bf16:
+    hid = hid.bfloat16().float()
+    w = wo.bfloat16().float()
+  W = torch.matmul(hid, w.t()) + bias
+  return W.reshape(*pf.shape[:-1], pc.shape[0], wo.shape[0]), hid
+
+
+def _tol(pc, pf, wo):
+  hid = torch.tanh(pc[None] + pf.reshape(-1, pf.shape[-1])[:, None, :]).abs()
+  return 2.0 ** -7 * torch.matmul(hid, wo.abs().t()).reshape(
+      *pf.shape[:-1], pc.shape[0], wo.shape[0]) + 1e-5
+
+
+def _inputs(cuda, lead, C, H, R, scale=1.0, seed=0):
+  g = torch.Generator(device=cuda)
+  g.manual_seed(seed)
+  pc = scale * torch.randn([C, H], generator=g, device=cuda)
+  pf = scale * torch.randn([*lead, H], generator=g, device=cuda)
+  wo = torch.randn([R, H], generator=g, device=cuda) / H ** 0.5
+  bias = torch.randn([R], generator=g, device=cuda)
+  return pc, pf, wo, bias
+
+
+@pytest.mark.parametrize('lead,C,H,R', [
+    ((4, 7), 33, 64, 33),     # bigram V=32 (two column tiles, the second with 1 column)
+    ((3, 5), 1, 16, 6),       # n = 0, V = 5
+    ((2, 9), 17, 48, 17),     # one column tile
+    ((1, 1), 33, 16, 64),     # full two tiles
+    ((5, 13), 21, 512, 33),   # H = 512 (the bench hidden size), ragged rows
+    ((37,), 33, 32, 33),      # rows * C not a multiple of 32
+])
+def test_forward_vs_torch(cuda, lead, C, H, R):
+  pc, pf, wo, bias = _inputs(cuda, lead, C, H, R)
+  W = nat.joint_weights(pc, pf, wo, bias)
+  torch.cuda.synchronize()
+  ref, _ = _ref(pc, pf, wo, bias)
+  assert W.shape == ref.shape
+  assert bool(((W - ref).abs() <= _tol(pc, pf, wo)).all())
+  emu, _ = _ref(pc, pf, wo, bias, bf16=True)
+  assert float((W - emu).abs().mean()) < 1e-4 * max(1.0, float(emu.abs().mean()))
+
+
+def test_forward_bf16_output_and_saturation(cuda):
+  pc, pf, wo, bias = _inputs(cuda, (3, 11), 33, 64, 33, scale=30.0)  # tanh saturates
+  W = nat.joint_weights(pc, pf, wo, bias, dtype=torch.bfloat16)
+  ref, _ = _ref(pc, pf, wo, bias)
+  assert W.dtype == torch.bfloat16
+  assert bool(torch.isfinite(W.float()).all())
+  tol = _tol(pc, pf, wo) + 2.0 ** -8 * ref.abs()
+  assert bool(((W.float() - ref).abs() <= tol).all())
+
+
+def test_empty_and_errors(cuda):
+  pc, pf, wo, bias = _inputs(cuda, (0, 5), 33, 16, 33)
+  assert nat.joint_weights(pc, pf, wo, bias).shape == (0, 5, 33, 33)
+  pc, pf, wo, bias = _inputs(cuda, (2, 3), 33, 20, 33)   # hidden not a multiple of 16
+  with pytest.raises(nat.LatticeLibraryError):
+    nat.joint_weights(pc, pf, wo, bias)
+  pc, pf, wo, bias = _inputs(cuda, (2, 3), 33, 16, 65)   # V + 1 > 64
+  with pytest.raises(nat.LatticeLibraryError):
+    nat.joint_weights(pc, pf, wo, bias)
+
+
+def test_backward_vs_torch(cuda):
+  lead, C, H, R = (3, 50), 33, 64, 33
+  pc, pf, wo, bias = _inputs(cuda, lead, C, H, R)
+  g = torch.randn([*lead, C, R], device=cuda)
+  leaves = [t.clone().requires_grad_(True) for t in (pc, pf, wo, bias)]
+  W = lt.weight_fns._JointWeightsFn.apply(*leaves, 37)   # several chunks, one ragged
+  (W * g).sum().backward()
+  ref_leaves = [t.clone().requires_grad_(True) for t in (pc, pf, wo, bias)]
+  ref, _ = _ref(*ref_leaves)
+  (ref * g).sum().backward()
+  for a, b in zip(leaves, ref_leaves):
+    scale = float(b.grad.abs().max())
+    assert float((a.grad - b.grad).abs().max()) <= 1e-4 * max(1.0, scale)
+
+
+def test_joint_weight_fn_in_lattice(cuda):
+  """RecognitionLattice with SharedEmbCacher + JointWeightFn: the fused
+  producer and the PyTorch path give the same loss within the bf16 product
+  tolerance, and gradients reach every parameter."""
+  torch.manual_seed(0)
+  V, n, H, B, T, U = 8, 1, 32, 3, 12, 4
+  ctx = lt.contexts.FullNGram(vocab_size=V, context_size=n)
+  cacher = lt.weight_fns.SharedEmbCacher(num_context_states=V + 1, embedding_size=16,
+                                         device=cuda)
+  fused = lt.weight_fns.JointWeightFn(vocab_size=V, hidden_size=H, device=cuda)
+  lat = lt.RecognitionLattice(context=ctx, alignment=lt.alignments.FrameDependent(),
+                              weight_fn_cacher_factory=lambda _: cacher,
+                              weight_fn_factory=lambda _: fused)
+  frames = torch.randn([B, T, 10], device=cuda)
+  nf = torch.tensor([T, T - 3, 5], device=cuda)
+  labels = torch.randint(1, V + 1, [B, U], device=cuda)
+  nl = torch.tensor([U, 2, 3], device=cuda)
+  loss = lat(frames=frames, num_frames=nf, labels=labels, num_labels=nl)
+  loss.sum().backward()
+  fused.fused = False
+  grads = {k: p.grad.clone() for k, p in fused.named_parameters()}
+  for p in fused.parameters():
+    p.grad = None
+  loss_ref = lat(frames=frames, num_frames=nf, labels=labels, num_labels=nl)
+  loss_ref.sum().backward()
+  assert torch.allclose(loss, loss_ref, rtol=2e-2, atol=2e-2), (loss, loss_ref)
+  for k, p in fused.named_parameters():
+    assert torch.isfinite(grads[k]).all() and grads[k].abs().sum() > 0, k
+    assert torch.allclose(grads[k], p.grad, rtol=5e-2, atol=5e-2 * float(p.grad.abs().max())), k
