@@ -14,7 +14,7 @@ for s in $STEPS; do
   case $s in
     test)
       echo "[gpu_round] pytest -m gpu"
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
         || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
       tail -3 "$OUT/pytest_gpu.log"
       ;;
