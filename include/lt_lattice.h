@@ -253,10 +253,39 @@ int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* 
  * (a multiple of 16). ctx_proj [num_states, hidden], frame_proj [rows, hidden],
  * out_weight [out_dim, hidden], out_bias [out_dim]: fp32, 16-byte aligned. W
  * [rows, num_states, out_dim] in weight_dtype. The tanh values and out_weight
- * enter the products as bf16, sums are fp32. */
+ * enter the products as bf16, sums are fp32. tanh(a + b) is formed from
+ * e^{2a} e^{2b} (both precomputed into the workspace) unless some |projection|
+ * exceeds 40, in which case the kernel evaluates e^{2(a+b)} directly.
+ * workspace: lt_joint_weights_workspace_bytes() bytes, 16-byte aligned. */
+int lt_joint_weights_workspace_bytes(int64_t rows, int32_t num_states, int32_t hidden,
+                                     size_t* bytes);
 int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t out_dim,
                      const float* ctx_proj, const float* frame_proj, const float* out_weight,
-                     const float* out_bias, void* W, int32_t weight_dtype, void* stream);
+                     const float* out_bias, void* W, int32_t weight_dtype, void* workspace,
+                     size_t workspace_bytes, void* stream);
+
+/* Adjoint of lt_joint_weights (JointWeightFn's parameter gradients; the
+ * reference gets them from autograd through weight_fns.py:174-227): with
+ * grad_W = dL/dW [rows, num_states, out_dim] fp32 and hid = tanh(ctx_proj[c] +
+ * frame_proj[f]) recomputed in fp32,
+ *   d_out_weight[y, h] = sum_{f,c} grad_W[f, c, y] hid[f, c, h]
+ *   d_out_bias[y]      = sum_{f,c} grad_W[f, c, y]
+ *   dh[f, c, h]        = (sum_y grad_W[f, c, y] out_weight[y, h]) (1 - hid^2)
+ *   d_ctx_proj[c, h]   = sum_f dh,   d_frame_proj[f, h] = sum_c dh
+ * Products are split-bf16 (about 16 mantissa bits), sums fp32. Needs
+ * hidden % 32 == 0, out_dim <= 64, rows * max(num_states, hidden) < 2^31 and
+ * the d_ctx_proj block of one workgroup (4 * num_states * 32 * waves bytes,
+ * waves = the largest of 8/4/2/1 dividing hidden / 32) plus 14 KB in LDS
+ * (<= 160 KB). All outputs are overwritten; d_frame_proj sums a frame's tiles
+ * with fp32 atomics (its low bits can vary run to run), the others are
+ * reduced in a fixed order. workspace: lt_joint_weights_backward_workspace_bytes(). */
+int lt_joint_weights_backward_workspace_bytes(int64_t rows, int32_t num_states, int32_t hidden,
+                                              int32_t out_dim, size_t* bytes);
+int lt_joint_weights_backward(int64_t rows, int32_t num_states, int32_t hidden, int32_t out_dim,
+                              const float* ctx_proj, const float* frame_proj,
+                              const float* out_weight, const float* grad_W, float* d_ctx_proj,
+                              float* d_frame_proj, float* d_out_weight, float* d_out_bias,
+                              void* workspace, size_t workspace_bytes, void* stream);
 
 /* Thread-local description of the last error; never NULL. */
 const char* lt_last_error(void);

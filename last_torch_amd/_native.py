@@ -68,7 +68,14 @@ _SIG = {
     'lt_table_loss_grad': [_G, _TP, _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
     'lt_table_viterbi_workspace_bytes': [_G, _TP, ctypes.POINTER(ctypes.c_size_t)],
     'lt_table_viterbi': [_G, _TP, _P, _P, _I32, _P, _P, _P, ctypes.c_size_t, _P],
-    'lt_joint_weights': [ctypes.c_int64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P],
+    'lt_joint_weights_workspace_bytes': [ctypes.c_int64, _I32, _I32,
+                                         ctypes.POINTER(ctypes.c_size_t)],
+    'lt_joint_weights': [ctypes.c_int64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P,
+                         ctypes.c_size_t, _P],
+    'lt_joint_weights_backward_workspace_bytes': [ctypes.c_int64, _I32, _I32, _I32,
+                                                  ctypes.POINTER(ctypes.c_size_t)],
+    'lt_joint_weights_backward': [ctypes.c_int64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P,
+                                  _P, _P, ctypes.c_size_t, _P],
     'lt_viterbi_workspace_bytes': [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_size_t)],
     'lt_viterbi': [ctypes.POINTER(Problem), _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t,
                    _P],
@@ -460,7 +467,46 @@ def joint_weights(ctx_proj, frame_proj, out_weight, out_bias, dtype=torch.float3
   pf = frame_proj.reshape(-1, H).contiguous()
   wo, bo = out_weight.contiguous(), out_bias.contiguous()
   W = torch.empty([*frame_proj.shape[:-1], C, R], dtype=dtype, device=frame_proj.device)
+  nbytes = ctypes.c_size_t(0)
+  _check(lib().lt_joint_weights_workspace_bytes(pf.shape[0], C, H, ctypes.byref(nbytes)),
+         'lt_joint_weights_workspace_bytes')
+  ws = torch.empty([(nbytes.value + 15) // 16 * 4], dtype=torch.float32, device=pf.device)
   _check(lib().lt_joint_weights(pf.shape[0], C, H, R, _ptr(pc), _ptr(pf), _ptr(wo), _ptr(bo),
                                 _ptr(W), LT_DTYPE_BF16 if dtype == torch.bfloat16 else LT_DTYPE_F32,
-                                _stream()), 'lt_joint_weights')
+                                _ptr(ws), ws.numel() * 4, _stream()), 'lt_joint_weights')
   return W
+
+
+def joint_weights_backward_supported(C, H, R, rows=0):
+  """Shapes lt_joint_weights_backward takes (its LDS holds a d_ctx_proj block)."""
+  if H % 32 or R > 64 or rows * max(C, H) >= 2 ** 31:
+    return False
+  n = H // 32
+  waves = 8 if n % 8 == 0 else 4 if n % 4 == 0 else 2 if n % 2 == 0 else 1
+  KB = (R + 15) // 16
+  return 4 * (2 * 32 * (16 * KB + 4) + 128 + C * 32 * waves) <= 160 * 1024
+
+
+def joint_weights_backward(ctx_proj, frame_proj, out_weight, grad_W):
+  """lt_joint_weights_backward: (d_ctx_proj [C, H], d_frame_proj [..., H],
+  d_out_weight [R, H], d_out_bias [R]) for grad_W = dL/dW [..., C, R] (fp32,
+  split-bf16 products on the matrix cores)."""
+  C, H = ctx_proj.shape
+  R = out_weight.shape[0]
+  pc = ctx_proj.contiguous()
+  pf = frame_proj.reshape(-1, H).contiguous()
+  wo = out_weight.contiguous()
+  g = grad_W.reshape(-1, C, R).float().contiguous()
+  rows = pf.shape[0]
+  dpc = torch.empty_like(pc)
+  dpf = torch.empty_like(pf)
+  dwo = torch.empty_like(wo)
+  dbias = torch.empty([R], dtype=torch.float32, device=pc.device)
+  nbytes = ctypes.c_size_t(0)
+  _check(lib().lt_joint_weights_backward_workspace_bytes(rows, C, H, R, ctypes.byref(nbytes)),
+         'lt_joint_weights_backward_workspace_bytes')
+  ws = torch.empty([max(1, nbytes.value // 4)], dtype=torch.float32, device=pc.device)
+  _check(lib().lt_joint_weights_backward(rows, C, H, R, _ptr(pc), _ptr(pf), _ptr(wo), _ptr(g),
+                                         _ptr(dpc), _ptr(dpf), _ptr(dwo), _ptr(dbias), _ptr(ws),
+                                         ws.numel() * 4, _stream()), 'lt_joint_weights_backward')
+  return dpc, dpf.reshape(frame_proj.shape), dwo, dbias

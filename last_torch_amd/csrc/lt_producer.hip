@@ -21,9 +21,17 @@
 
 namespace {
 
+// Projections beyond this magnitude take the direct path: e^{2x} of both
+// factors then stays within [e^-80, e^80], so their product is finite or
+// saturates to inf / 0 (tanh = +-1) without inf * 0.
+constexpr float kSplitMax = 40.f;
+
 struct JArgs {
   const float* pc;    // [C, H]
   const float* pf;    // [rows, H]
+  const float* ec;    // [C, H]    e^{2 pc} (workspace)
+  const float* ef;    // [rows, H] e^{2 pf} (workspace)
+  const int* big;     // != 0: some |projection| > kSplitMax, use the direct path
   const float* wo;    // [R, H]
   const float* bias;  // [R]
   void* W;            // [rows, C, R]
@@ -32,50 +40,111 @@ struct JArgs {
 };
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-// tanh(x) = 1 - 2 / (1 + e^{2x}): saturates to +-1 (exp over/underflow)
-LT_DEVINL float fast_tanh(float x) {
-  const float e = __expf(2.f * x);
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
+// two fp32 -> packed bf16 (v_cvt_pk_bf16_f32, round to nearest even)
+LT_DEVINL unsigned pk_bf16(f32x2 v) {
+  const bf16x2 h = {(__bf16)v.x, (__bf16)v.y};
+  return __builtin_bit_cast(unsigned, h);
 }
 
-template <bool OBF16>
+// tanh from p = e^{2x}: 1 - 2 / (1 + p) (p = inf -> 1, p = 0 -> -1)
+LT_DEVINL f32x2 tanh_from_exp(f32x2 p) {
+  const f32x2 one = {1.f, 1.f}, m2 = {-2.f, -2.f};
+  const f32x2 d = p + one;
+  const f32x2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  return r * m2 + one;
+}
+
+LT_DEVINL f32x2 exp2x(f32x2 x) {  // e^{2x}
+  const f32x2 k = {2.f * kLog2e, 2.f * kLog2e};
+  const f32x2 y = x * k;
+  return f32x2{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+}
+
+// e^{2x} of both projections, and the direct-path flag (rows * H and C * H
+// values, float4 per thread).
+__global__ __launch_bounds__(256) void joint_exp_kernel(const JArgs a, float* ec, float* ef,
+                                                        int* big) {
+  const long long nc = (long long)a.C * a.H / 4, nf = a.rows * a.H / 4;
+  bool over = false;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nc + nf;
+       i += (long long)gridDim.x * blockDim.x) {
+    const bool isc = i < nc;
+    const float4 x = isc ? ((const float4*)a.pc)[i] : ((const float4*)a.pf)[i - nc];
+    const float m = fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
+    over |= !(m <= kSplitMax);  // NaN counts as over
+    const f32x2 lo = exp2x(f32x2{x.x, x.y}), hi = exp2x(f32x2{x.z, x.w});
+    const float4 e = {lo.x, lo.y, hi.x, hi.y};
+    if (isc) ((float4*)ec)[i] = e;
+    else ((float4*)ef)[i - nc] = e;
+  }
+  if (__any(over) && (threadIdx.x & 63) == 0) atomicOr(big, 1);
+}
+
+// One wave: a 32-row tile of the flattened (f, c) rows against one or two
+// 32-column tiles of y (TWO: R > 32), K = H in steps of 16.
+template <bool OBF16, bool TWO>
 __global__ __launch_bounds__(256) void joint_weights_kernel(const JArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned short wol[];  // [R][H] bf16
+  extern __shared__ __attribute__((aligned(16))) unsigned short wol[];  // [R][H + 8] bf16
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int H = a.H, R = a.R, C = a.C;
-  for (int i = tid; i < R * H; i += blockDim.x) wol[i] = f2bf(a.wo[i]);
+  const int H = a.H, R = a.R, C = a.C, HP = H + 8;  // padded rows: no LDS bank conflicts
+  for (int i = tid; i < R * H; i += blockDim.x) {
+    const int y = i / H, h = i - y * H;
+    wol[y * HP + h] = f2bf(a.wo[i]);
+  }
   __syncthreads();
+  const bool split = *a.big == 0;
   const long long M = a.rows * C;
   const long long ntile = (M + 31) / 32;
   const int r = lane & 31, hk = 8 * (lane >> 5);
   const int y0 = r, y1 = 32 + r;
   const bool v0 = y0 < R, v1 = y1 < R;
   const float b0 = v0 ? a.bias[y0] : 0.f, b1 = v1 ? a.bias[y1] : 0.f;
-  const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  // columns past R read row R - 1 (valid) and are never stored
+  const unsigned short* w0 = wol + (v0 ? y0 : R - 1) * HP + hk;
+  const unsigned short* w1 = wol + (v1 ? y1 : R - 1) * HP + hk;
   for (long long tile = (long long)blockIdx.x * 4 + wave; tile < ntile;
        tile += (long long)gridDim.x * 4) {
     const long long m = tile * 32 + r;
-    const bool mv = m < M;
-    const long long f = mv ? m / C : 0;
-    const int c = mv ? (int)(m - f * C) : 0;
-    const float* pc = a.pc + (long long)c * H + hk;
-    const float* pf = a.pf + f * H + hk;
+    const long long mm = m < M ? m : M - 1;  // rows past M load row M - 1, never stored
+    const long long f = mm / C;
+    const int c = (int)(mm - f * C);
     f32x16 acc0 = {}, acc1 = {};
-    for (int k0 = 0; k0 < H; k0 += 16) {
-      const float4 c0 = *(const float4*)(pc + k0), c1 = *(const float4*)(pc + k0 + 4);
-      const float4 f0 = *(const float4*)(pf + k0), f1 = *(const float4*)(pf + k0 + 4);
-      const float x[8] = {c0.x + f0.x, c0.y + f0.y, c0.z + f0.z, c0.w + f0.w,
-                          c1.x + f1.x, c1.y + f1.y, c1.z + f1.z, c1.w + f1.w};
-      bf16x8 af;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) af[j] = (short)f2bf(mv ? fast_tanh(x[j]) : 0.f);
-      const bf16x8 bf0 = v0 ? *(const bf16x8*)(wol + y0 * H + k0 + hk) : zero8;
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf0, acc0, 0, 0, 0);
-      if (R > 32) {
-        const bf16x8 bf1 = v1 ? *(const bf16x8*)(wol + y1 * H + k0 + hk) : zero8;
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf1, acc1, 0, 0, 0);
+    if (split) {
+      const float* pc = a.ec + (long long)c * H + hk;
+      const float* pf = a.ef + f * H + hk;
+#pragma unroll 2
+      for (int k0 = 0; k0 < H; k0 += 16) {
+        const float4 c0 = *(const float4*)(pc + k0), c1 = *(const float4*)(pc + k0 + 4);
+        const float4 f0 = *(const float4*)(pf + k0), f1 = *(const float4*)(pf + k0 + 4);
+        const u32x4 t = {pk_bf16(tanh_from_exp(f32x2{c0.x, c0.y} * f32x2{f0.x, f0.y})),
+                         pk_bf16(tanh_from_exp(f32x2{c0.z, c0.w} * f32x2{f0.z, f0.w})),
+                         pk_bf16(tanh_from_exp(f32x2{c1.x, c1.y} * f32x2{f1.x, f1.y})),
+                         pk_bf16(tanh_from_exp(f32x2{c1.z, c1.w} * f32x2{f1.z, f1.w}))};
+        const bf16x8 af = __builtin_bit_cast(bf16x8, t);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w0 + k0), acc0, 0, 0, 0);
+        if (TWO)
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w1 + k0), acc1, 0, 0, 0);
+      }
+    } else {
+      const float* pc = a.pc + (long long)c * H + hk;
+      const float* pf = a.pf + f * H + hk;
+#pragma unroll 2
+      for (int k0 = 0; k0 < H; k0 += 16) {
+        const float4 c0 = *(const float4*)(pc + k0), c1 = *(const float4*)(pc + k0 + 4);
+        const float4 f0 = *(const float4*)(pf + k0), f1 = *(const float4*)(pf + k0 + 4);
+        const u32x4 t = {pk_bf16(tanh_from_exp(exp2x(f32x2{c0.x + f0.x, c0.y + f0.y}))),
+                         pk_bf16(tanh_from_exp(exp2x(f32x2{c0.z + f0.z, c0.w + f0.w}))),
+                         pk_bf16(tanh_from_exp(exp2x(f32x2{c1.x + f1.x, c1.y + f1.y}))),
+                         pk_bf16(tanh_from_exp(exp2x(f32x2{c1.z + f1.z, c1.w + f1.w})))};
+        const bf16x8 af = __builtin_bit_cast(bf16x8, t);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w0 + k0), acc0, 0, 0, 0);
+        if (TWO)
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w1 + k0), acc1, 0, 0, 0);
       }
     }
     // C/D: column y = lane & 31 (+32), row (i & 3) + 8 (i >> 2) + 4 (lane >> 5)
@@ -84,48 +153,403 @@ __global__ __launch_bounds__(256) void joint_weights_kernel(const JArgs a) {
       const long long mr = tile * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
       if (mr >= M) continue;
       if (v0) stw<OBF16>(a.W, mr * R + y0, acc0[i] + b0);
-      if (R > 32 && v1) stw<OBF16>(a.W, mr * R + y1, acc1[i] + b1);
+      if (TWO && v1) stw<OBF16>(a.W, mr * R + y1, acc1[i] + b1);
     }
   }
+}
+
+template <bool OBF16>
+const void* pick(bool two) {
+  return two ? (const void*)joint_weights_kernel<OBF16, true>
+             : (const void*)joint_weights_kernel<OBF16, false>;
+}
+
+size_t ws_bytes(long long rows, int C, int H) {
+  return 256 + 4 * (size_t)H * ((size_t)C + (size_t)rows);
 }
 
 }  // namespace
 
 extern "C" {
 
+int lt_joint_weights_workspace_bytes(int64_t rows, int32_t num_states, int32_t hidden,
+                                     size_t* bytes) {
+  if (!bytes || rows < 0 || num_states < 1 || hidden < 1)
+    return lt_impl::set_error(LT_EINVAL, "lt_joint_weights_workspace_bytes: bad arguments");
+  *bytes = ws_bytes(rows, num_states, hidden);
+  return LT_OK;
+}
+
 int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t out_dim,
                      const float* ctx_proj, const float* frame_proj, const float* out_weight,
-                     const float* out_bias, void* W, int32_t weight_dtype, void* stream) {
+                     const float* out_bias, void* W, int32_t weight_dtype, void* workspace,
+                     size_t workspace_bytes, void* stream) {
   if (rows < 0 || num_states < 1 || hidden < 1 || out_dim < 1)
     return lt_impl::set_error(LT_EINVAL, "lt_joint_weights: bad sizes");
   if (hidden % 16 || out_dim > 64)
     return lt_impl::set_error(LT_EUNSUPPORTED, "lt_joint_weights: needs hidden % 16 == 0, V+1 <= 64");
-  const long long lds = 2LL * out_dim * hidden;
+  const long long lds = 2LL * out_dim * (hidden + 8);
   if (lds > 128 * 1024)
     return lt_impl::set_error(LT_EUNSUPPORTED, "lt_joint_weights: output projection exceeds LDS");
   if (rows == 0) return LT_OK;
-  if (!ctx_proj || !frame_proj || !out_weight || !out_bias || !W)
+  if (!ctx_proj || !frame_proj || !out_weight || !out_bias || !W || !workspace)
     return lt_impl::set_error(LT_EINVAL, "lt_joint_weights: null pointer");
-  if (((uintptr_t)ctx_proj | (uintptr_t)frame_proj) & 15)
-    return lt_impl::set_error(LT_EINVAL, "lt_joint_weights: projections must be 16-byte aligned");
+  if (((uintptr_t)ctx_proj | (uintptr_t)frame_proj | (uintptr_t)workspace) & 15)
+    return lt_impl::set_error(LT_EINVAL, "lt_joint_weights: projections and workspace must be 16-byte aligned");
+  if (workspace_bytes < ws_bytes(rows, num_states, hidden))
+    return lt_impl::set_error(LT_EINVAL, "lt_joint_weights: workspace too small");
   JArgs a;
-  a.pc = ctx_proj; a.pf = frame_proj; a.wo = out_weight; a.bias = out_bias; a.W = W;
+  char* ws = (char*)workspace;
+  int* big = (int*)ws;
+  float* ec = (float*)(ws + 256);
+  float* ef = ec + (size_t)num_states * hidden;
+  a.pc = ctx_proj; a.pf = frame_proj; a.ec = ec; a.ef = ef; a.big = big;
+  a.wo = out_weight; a.bias = out_bias; a.W = W;
   a.rows = rows; a.C = num_states; a.H = hidden; a.R = out_dim;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(big, 0, sizeof(int), st);
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  {
+    const long long n4 = ((long long)num_states + rows) * hidden / 4;
+    const int grid = (int)std::min<long long>((n4 + 255) / 256, 8LL * cus);
+    void* args[] = {&a, &ec, &ef, &big};
+    e = hipLaunchKernel((const void*)joint_exp_kernel, dim3(grid), dim3(256), args, 0, st);
+    if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  }
   const long long tiles = (rows * num_states + 31) / 32;
   const long long want = (tiles + 3) / 4;
   const int grid = (int)std::min<long long>(want, 4LL * cus);  // persistent: Wo loaded once per WG
-  const bool bf = weight_dtype == LT_DTYPE_BF16;
-  const void* k = bf ? (const void*)joint_weights_kernel<true> : (const void*)joint_weights_kernel<false>;
-  hipStream_t st = (hipStream_t)stream;
+  const bool bf = weight_dtype == LT_DTYPE_BF16, two = out_dim > 32;
+  const void* k = bf ? pick<true>(two) : pick<false>(two);
   if (lds > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   }
   void* args[] = {&a};
-  const hipError_t e = hipLaunchKernel(k, dim3(grid), dim3(256), args, (size_t)lds, st);
+  e = hipLaunchKernel(k, dim3(grid), dim3(256), args, (size_t)lds, st);
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  return LT_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Backward of the joint weight function (the adjoint of lt_joint_weights):
+// with g = dL/dW [rows * C, R], hid = tanh(pc[c] + pf[f]) recomputed in fp32,
+//   gw[m, h]   = sum_r g[m, r] wo[r, h]          (MFMA, K = R)
+//   dh[m, h]   = gw[m, h] (1 - hid[m, h]^2)
+//   d_wo[r, h] = sum_m g[m, r] hid[m, h]          (MFMA, K = the tile's 32 rows)
+//   d_pf[f, h] = sum_c dh[(f, c), h]              (MFMA against a one-hot frame map)
+//   d_pc[c, h] = sum_f dh[(f, c), h]              (LDS fp32 adds)
+// Every product is split-bf16 (x = hi + lo; hi*hi + hi*lo + lo*hi, or exact
+// one-hot * (hi + lo)), about 16 mantissa bits, sums fp32. One workgroup of
+// H / 32 waves per CU: wave w owns the 32 hidden columns [32w, 32w + 32) for
+// every tile, so its d_wo block stays in registers for the whole launch;
+// the MFMA output layout of gw / dh / hid (row (i & 3) + 8 (i >> 2) + 4 half)
+// is used directly as the K operand of the next products (the K order only
+// has to agree between A and B).
+namespace {
+
+struct JBArgs {
+  const float* pc;   // [C, H]
+  const float* pf;   // [rows, H]
+  const float* wo;   // [R, H]
+  const float* g;    // [rows * C, R]
+  float* dpf;        // [rows, H], zeroed
+  float* part;       // [grid][C + R][H] per-workgroup d_pc, d_wo
+  long long rows;
+  int C, H, R;
+};
+
+LT_DEVINL void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+  u32x4 h, l;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const f32x2 x = {v[2 * p], v[2 * p + 1]};
+    const unsigned hp = pk_bf16(x);
+    const f32x2 xh = {__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
+    h[p] = hp;
+    l[p] = pk_bf16(x - xh);
+  }
+  hi = __builtin_bit_cast(bf16x8, h);
+  lo = __builtin_bit_cast(bf16x8, l);
+}
+
+LT_DEVINL f32x16 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+template <int KB, bool TWO, int NW>  // KB = ceil(R / 16) K blocks of gw; TWO: R > 32; NW waves
+__global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float bl[];
+  constexpr int GS = KB * 16 + 4;  // g tile row stride (floats)
+  constexpr int GN = 32 * KB * 16;  // g tile elements staged per tile
+  constexpr int nthr = 64 * NW, HW = 32 * NW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, R = a.R, C = a.C;
+  // this workgroup's hidden columns: [h0, h0 + HW)  // this workgroup's hidden columns [h0, h0 + HW)
+  const int h0 = blockIdx.y * HW;
+  float* gtb = bl;                    // [2][32][GS] double-buffered g tile
+  int* rinfo = (int*)(bl + 2 * 32 * GS);  // [2][32][2]: frame, context state (-1: past M)
+  float* dpc = bl + 2 * 32 * GS + 128;    // [C][HW]
+  for (int e = tid; e < C * HW; e += nthr) dpc[e] = 0.f;
+  const int half = lane >> 5, col = lane & 31;
+  const int hl = wave * 32 + col, h = h0 + hl;
+  const unsigned M = (unsigned)(a.rows * C);  // < 2^31 (host check)
+  const unsigned ntile = (M + 31) / 32;
+  bf16x8 woh[KB], wol[KB];  // B[k = r][n = h] of gw
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = 16 * kb + 8 * half + j;
+      v[j] = r < R ? a.wo[(long long)r * H + h] : 0.f;
+    }
+    split8(v, woh[kb], wol[kb]);
+  }
+  f32x16 dwo0 = {}, dwo1 = {};
+  float dbias = 0.f;  // thread tid < R of blockIdx.y == 0: sum of g[:, tid]
+  constexpr int GPT = (GN + nthr - 1) / nthr;  // staged g values per thread
+  float gnext[GPT];
+  auto load_g = [&](unsigned tile) {
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) {
+      const int e = tid + u * nthr;
+      const int m = e / (KB * 16), r = e - m * (KB * 16);
+      const unsigned mg = tile * 32 + m;
+      gnext[u] = (e < GN && tile < ntile && mg < M && r < R) ? a.g[(size_t)mg * R + r] : 0.f;
+    }
+  };
+  load_g(blockIdx.x);
+  int buf = 0;
+  for (unsigned tile = blockIdx.x; tile < ntile; tile += gridDim.x, buf ^= 1) {
+    float* gt = gtb + buf * 32 * GS;
+    int* ri = rinfo + buf * 64;
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) {
+      const int e = tid + u * nthr;
+      if (e < GN) {
+        const int m = e / (KB * 16), r = e - m * (KB * 16);
+        gt[m * GS + r] = gnext[u];
+      }
+    }
+    if (tid < 32) {
+      const unsigned mg = tile * 32 + tid;
+      const unsigned f = mg / (unsigned)C;
+      ri[2 * tid] = (int)f;
+      ri[2 * tid + 1] = mg < M ? (int)(mg - f * C) : -1;
+    }
+    __syncthreads();  // one barrier per tile: the other buffer is written next
+    load_g(tile + gridDim.x);  // in flight during this tile
+    if (blockIdx.y == 0 && tid < R)
+      for (int m = 0; m < 32; ++m) dbias += gt[m * GS + tid];
+    // x = pc[c] + pf[f] for this lane's 16 rows, loads issued before the gw products
+    float x[16];
+    int cc[16], ff[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
+      const int2 fc = *(const int2*)(ri + 2 * m);
+      ff[i] = fc.x;
+      cc[i] = fc.y;
+      const int c = fc.y < 0 ? 0 : fc.y;
+      const unsigned f = fc.y < 0 ? (unsigned)(a.rows - 1) : (unsigned)fc.x;
+      x[i] = a.pc[c * H + h] + a.pf[(size_t)f * H + h];
+    }
+    // gw: A[m = col][k = r]
+    f32x16 gw = {};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const float4 x0 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half);
+      const float4 x1 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half + 4);
+      const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      bf16x8 ah, al;
+      split8(v, ah, al);
+      gw = mfma3(ah, al, woh[kb], wol[kb], gw);
+    }
+    const int f0 = ri[0];
+    f32x16 dpfa = {};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      // K slot (half, j) <-> row m(i = 8q + j, half): this lane's own rows
+      float hv[8], dv[8], gv[8], oh[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * q + j;
+        const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
+        const bool ok = cc[i] >= 0;
+        const float e = __builtin_amdgcn_exp2f(x[i] * (2.f * kLog2e));
+        const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
+        hv[j] = ok ? t : 0.f;
+        dv[j] = ok ? gw[i] * (1.f - t * t) : 0.f;
+        oh[j] = ff[i] - f0 == col ? 1.f : 0.f;
+        atomicAdd(dpc + (ok ? cc[i] : 0) * HW + hl, dv[j]);
+        gv[j] = gt[m * GS + col];
+      }
+      bf16x8 hh, hlo, dhh, dhl, gh, glo, ohh, ohl;  // ohl = 0 (one-hot values are exact)
+      split8(hv, hh, hlo);
+      split8(dv, dhh, dhl);
+      split8(oh, ohh, ohl);
+      split8(gv, gh, glo);
+      dwo0 = mfma3(gh, glo, hh, hlo, dwo0);
+      if (TWO) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = 8 * q + j;
+          gv[j] = gt[((i & 3) + 8 * (i >> 2) + 4 * half) * GS + 32 + col];
+        }
+        split8(gv, gh, glo);
+        dwo1 = mfma3(gh, glo, hh, hlo, dwo1);
+      }
+      dpfa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ohh, dhl, dpfa, 0, 0, 0);
+      dpfa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ohh, dhh, dpfa, 0, 0, 0);
+    }
+    // frames in this tile: the last valid row's frame (row 31 or the last below M)
+    const int nf = (int)(min(tile * 32 + 31, M - 1) / (unsigned)C) - f0 + 1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int p = (i & 3) + 8 * (i >> 2) + 4 * half;
+      if (p < nf) atomicAdd(a.dpf + (size_t)(f0 + p) * H + h, dpfa[i]);
+    }
+  }
+  // per-workgroup partials: d_pc rows [0, C), d_wo rows [C, C + R), d_bias after them
+  float* part = a.part + (long long)blockIdx.x * ((long long)(C + R) * H + 64);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = (i & 3) + 8 * (i >> 2) + 4 * half;
+    if (r < R) part[(long long)(C + r) * H + h] = dwo0[i];
+    if (TWO && r + 32 < R) part[(long long)(C + r + 32) * H + h] = dwo1[i];
+  }
+  if (blockIdx.y == 0 && tid < R) part[(long long)(C + R) * H + tid] = dbias;
+  __syncthreads();
+  for (int e = tid; e < C * HW; e += nthr) {
+    const int c = e / HW;
+    part[(long long)c * H + h0 + (e - c * HW)] = dpc[e];
+  }
+}
+
+// out[e] = sum_g part[g][e] (fixed order: deterministic); part rows are
+// d_pc [C*H] | d_wo [R*H] | d_bias [R] with a per-workgroup stride
+__global__ __launch_bounds__(256) void joint_reduce_kernel(const float* part, int grid,
+                                                           long long stride, long long npc,
+                                                           long long nwo, int R, float* dpc,
+                                                           float* dwo, float* dbias) {
+  const long long n = npc + nwo + R;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int b = 0; b < grid; ++b) s += part[(long long)b * stride + e];
+    if (e < npc) dpc[e] = s;
+    else if (e < npc + nwo) dwo[e - npc] = s;
+    else dbias[e - npc - nwo] = s;
+  }
+}
+
+template <int KB, bool TWO>
+const void* pick_nw(int nw) {
+  return nw == 8 ? (const void*)joint_backward_kernel<KB, TWO, 8>
+       : nw == 4 ? (const void*)joint_backward_kernel<KB, TWO, 4>
+       : nw == 2 ? (const void*)joint_backward_kernel<KB, TWO, 2>
+                 : (const void*)joint_backward_kernel<KB, TWO, 1>;
+}
+
+// waves per workgroup: the largest of 8, 4, 2, 1 dividing hidden / 32
+int bwd_waves(int H) {
+  const int n = H / 32;
+  return n % 8 == 0 ? 8 : n % 4 == 0 ? 4 : n % 2 == 0 ? 2 : 1;
+}
+
+int bwd_grid(long long rows, int C, int H) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const long long tiles = (rows * C + 31) / 32;
+  const int gy = std::max(1, H / (32 * bwd_waves(H)));
+  // one resident workgroup per CU over the whole (x, y) grid
+  const long long gx = std::max<long long>(1, (cus * (bwd_waves(H) < 8 ? 2 : 1)) / gy);
+  return (int)std::max<long long>(1, std::min<long long>(tiles, gx));
+}
+
+long long bwd_lds(int C, int H, int R) {
+  const int KB = (R + 15) / 16;
+  return 4LL * (2 * 32 * (KB * 16 + 4) + 128 + (long long)C * 32 * bwd_waves(H));
+}
+
+long long bwd_stride(int C, int H, int R) { return (long long)(C + R) * H + 64; }
+
+}  // namespace
+
+extern "C" {
+
+int lt_joint_weights_backward_workspace_bytes(int64_t rows, int32_t num_states, int32_t hidden,
+                                              int32_t out_dim, size_t* bytes) {
+  if (!bytes || rows < 0 || num_states < 1 || hidden < 32 || out_dim < 1)
+    return lt_impl::set_error(LT_EINVAL, "lt_joint_weights_backward_workspace_bytes: bad arguments");
+  *bytes = 4 * (size_t)bwd_grid(rows, num_states, hidden) * bwd_stride(num_states, hidden, out_dim);
+  return LT_OK;
+}
+
+int lt_joint_weights_backward(int64_t rows, int32_t num_states, int32_t hidden, int32_t out_dim,
+                              const float* ctx_proj, const float* frame_proj,
+                              const float* out_weight, const float* grad_W, float* d_ctx_proj,
+                              float* d_frame_proj, float* d_out_weight, float* d_out_bias,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  const int C = num_states, H = hidden, R = out_dim;
+  if (rows < 0 || C < 1 || H < 1 || R < 1)
+    return lt_impl::set_error(LT_EINVAL, "lt_joint_weights_backward: bad sizes");
+  if (H % 32 || R > 64)
+    return lt_impl::set_error(LT_EUNSUPPORTED,
+                              "lt_joint_weights_backward: needs hidden % 32 == 0, V+1 <= 64");
+  const long long lds = bwd_lds(C, H, R);
+  if (lds > 160 * 1024)
+    return lt_impl::set_error(LT_EUNSUPPORTED, "lt_joint_weights_backward: d_ctx_proj block exceeds LDS");
+  if (rows * (long long)C >= (1LL << 31) || rows * (long long)H >= (1LL << 31))
+    return lt_impl::set_error(LT_EUNSUPPORTED, "lt_joint_weights_backward: rows * C or rows * H >= 2^31");
+  if (!ctx_proj || !out_weight || !d_ctx_proj || !d_out_weight || !d_out_bias ||
+      (rows > 0 && (!frame_proj || !grad_W || !d_frame_proj || !workspace)))
+    return lt_impl::set_error(LT_EINVAL, "lt_joint_weights_backward: null pointer");
+  size_t need = 0;
+  (void)lt_joint_weights_backward_workspace_bytes(rows, C, H, R, &need);
+  if (rows > 0 && workspace_bytes < need)
+    return lt_impl::set_error(LT_EINVAL, "lt_joint_weights_backward: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipSuccess;
+  if (rows == 0) {
+    e = hipMemsetAsync(d_ctx_proj, 0, 4 * (size_t)C * H, st);
+    if (e == hipSuccess) e = hipMemsetAsync(d_out_weight, 0, 4 * (size_t)R * H, st);
+    if (e == hipSuccess) e = hipMemsetAsync(d_out_bias, 0, 4 * (size_t)R, st);
+    return e == hipSuccess ? LT_OK : lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  }
+  e = hipMemsetAsync(d_frame_proj, 0, 4 * (size_t)rows * H, st);
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  JBArgs a;
+  a.pc = ctx_proj; a.pf = frame_proj; a.wo = out_weight; a.g = grad_W;
+  a.dpf = d_frame_proj; a.part = (float*)workspace;
+  a.rows = rows; a.C = C; a.H = H; a.R = R;
+  const int grid = bwd_grid(rows, C, H);
+  const int nw = bwd_waves(H);
+  const int KB = (R + 15) / 16;
+  const void* k = KB == 1 ? pick_nw<1, false>(nw) : KB == 2 ? pick_nw<2, false>(nw)
+                : KB == 3 ? pick_nw<3, true>(nw) : pick_nw<4, true>(nw);
+  if (lds > 64 * 1024) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  }
+  void* args[] = {&a};
+  e = hipLaunchKernel(k, dim3(grid, H / (32 * nw)), dim3(64 * nw), args, (size_t)lds, st);
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  long long stride = bwd_stride(C, H, R), npc = (long long)C * H, nwo = (long long)R * H;
+  int gridv = grid, Rv = R;
+  const int rg = (int)std::min<long long>((npc + nwo + R + 255) / 256, 4096);
+  void* rargs[] = {&a.part, &gridv, &stride, &npc, &nwo, &Rv, &d_ctx_proj, &d_out_weight,
+                   &d_out_bias};
+  e = hipLaunchKernel((const void*)joint_reduce_kernel, dim3(rg), dim3(256), rargs, 0, st);
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;
 }

@@ -16,7 +16,9 @@ Differences from the reference, all bug fixes:
 ``lt_joint_weights`` matrix-core kernel (lt_producer.hip): the [..., C, H]
 hidden tensor is formed tile by tile in registers instead of in HBM; the
 tanh values and the output projection enter the products as bf16, the sums
-are fp32. Its backward recomputes the hidden tensor in fp32 in frame chunks.
+are fp32. Its backward (``lt_joint_weights_backward``) recomputes the hidden
+tiles in fp32 and forms every gradient on the matrix cores with split-bf16
+products; shapes it cannot take fall back to PyTorch in frame chunks.
 """
 import abc
 from typing import Callable, Generic, Optional, TypeVar
@@ -84,7 +86,8 @@ class LocallyNormalizedWeightFn(WeightFn[T]):
 
 class _JointWeightsFn(torch.autograd.Function):
   """W[..., c, :] = bias + tanh(pc[c] + pf[...]) @ wo^T via lt_joint_weights;
-  the backward recomputes tanh in fp32, `chunk` frame rows at a time."""
+  the backward is lt_joint_weights_backward where its LDS holds d_ctx_proj,
+  else PyTorch recomputing tanh in fp32, `chunk` frame rows at a time."""
 
   @staticmethod
   def forward(ctx, pc, pf, wo, bias, chunk):
@@ -95,9 +98,13 @@ class _JointWeightsFn(torch.autograd.Function):
 
   @staticmethod
   def backward(ctx, gW):
+    from last_torch_amd import _native
     pc, pf, wo = ctx.saved_tensors
     C, H = pc.shape
     R = wo.shape[0]
+    if _native.joint_weights_backward_supported(C, H, R, pf.numel() // H):
+      dpc, dpf, dwo, dbias = _native.joint_weights_backward(pc, pf, wo, gW)
+      return dpc, dpf, dwo, dbias, None
     pf2 = pf.reshape(-1, H)
     g2 = gW.reshape(-1, C, R).float()
     dpc = torch.zeros_like(pc)

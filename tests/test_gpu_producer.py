@@ -65,14 +65,34 @@ def test_forward_vs_torch(cuda, lead, C, H, R):
   assert float((W - emu).abs().mean()) < 1e-4 * max(1.0, float(emu.abs().mean()))
 
 
-def test_forward_bf16_output_and_saturation(cuda):
-  pc, pf, wo, bias = _inputs(cuda, (3, 11), 33, 64, 33, scale=30.0)  # tanh saturates
+@pytest.mark.parametrize('scale', [8.0, 30.0])  # split path (|x| <= 40) / direct path
+def test_forward_bf16_output_and_saturation(cuda, scale):
+  pc, pf, wo, bias = _inputs(cuda, (3, 11), 33, 64, 33, scale=scale)  # tanh saturates
   W = nat.joint_weights(pc, pf, wo, bias, dtype=torch.bfloat16)
   ref, _ = _ref(pc, pf, wo, bias)
   assert W.dtype == torch.bfloat16
   assert bool(torch.isfinite(W.float()).all())
   tol = _tol(pc, pf, wo) + 2.0 ** -8 * ref.abs()
   assert bool(((W.float() - ref).abs() <= tol).all())
+
+
+def test_split_and_direct_paths_agree(cuda):
+  """One projection above 40 switches the whole call to the direct path; the
+  other rows must come out as on the split path up to bf16 rounding of tanh."""
+  pc, pf, wo, bias = _inputs(cuda, (2, 9), 33, 64, 33, scale=3.0)
+  W = nat.joint_weights(pc, pf, wo, bias)
+  pf2 = pf.clone()
+  pf2[1, 8, 0] = 50.0
+  W2 = nat.joint_weights(pc, pf2, wo, bias)
+  torch.cuda.synchronize()
+  assert bool(((W[:1] - W2[:1]).abs() <= _tol(pc, pf[:1], wo)).all())
+  ref, _ = _ref(pc, pf2, wo, bias)
+  assert bool(((W2 - ref).abs() <= _tol(pc, pf2, wo)).all())
+  pf3 = pf.clone()
+  pf3[0, 0, 0] = float('nan')
+  W3 = nat.joint_weights(pc, pf3, wo, bias)
+  torch.cuda.synchronize()
+  assert bool(torch.isnan(W3[0, 0]).all()) and bool(torch.isfinite(W3[1]).all())
 
 
 def test_empty_and_errors(cuda):
@@ -86,19 +106,66 @@ def test_empty_and_errors(cuda):
     nat.joint_weights(pc, pf, wo, bias)
 
 
-def test_backward_vs_torch(cuda):
-  lead, C, H, R = (3, 50), 33, 64, 33
+@pytest.mark.parametrize('lead,C,H,R', [
+    ((3, 50), 33, 64, 33),    # bigram V=32: second column block holds one row
+    ((2, 7), 1, 32, 6),       # n = 0, V = 5: 32 frames per tile
+    ((5, 9), 17, 96, 17),     # three waves, one K block pair
+    ((4, 3), 5, 32, 64),      # two full column blocks
+    ((2, 40), 33, 512, 33),   # bench hidden size: two workgroups per tile column
+    ((37,), 3, 288 - 32, 16), # hidden 256 exactly, rows * C not a multiple of 32
+    ((3, 11), 9, 320, 40),    # 2-wave workgroups over 5 column blocks, R in (32, 48]
+])
+@pytest.mark.parametrize('path', ['kernel', 'torch'])
+def test_backward_vs_torch(cuda, lead, C, H, R, path):
+  """lt_joint_weights_backward (split-bf16 products) and the chunked PyTorch
+  fallback both match fp32 autograd of the reference formula within 1e-4 of
+  each gradient's scale."""
   pc, pf, wo, bias = _inputs(cuda, lead, C, H, R)
   g = torch.randn([*lead, C, R], device=cuda)
   leaves = [t.clone().requires_grad_(True) for t in (pc, pf, wo, bias)]
-  W = lt.weight_fns._JointWeightsFn.apply(*leaves, 37)   # several chunks, one ragged
-  (W * g).sum().backward()
+  if path == 'kernel':
+    assert nat.joint_weights_backward_supported(C, H, R)
+    W = lt.weight_fns._JointWeightsFn.apply(*leaves, 37)
+    (W * g).sum().backward()
+  else:
+    grads = _torch_backward(pc, pf, wo, g, chunk=37)
+    for t, gr in zip(leaves, grads):
+      t.grad = gr
   ref_leaves = [t.clone().requires_grad_(True) for t in (pc, pf, wo, bias)]
   ref, _ = _ref(*ref_leaves)
   (ref * g).sum().backward()
-  for a, b in zip(leaves, ref_leaves):
+  for name, a, b in zip(('pc', 'pf', 'wo', 'bias'), leaves, ref_leaves):
     scale = float(b.grad.abs().max())
-    assert float((a.grad - b.grad).abs().max()) <= 1e-4 * max(1.0, scale)
+    err = float((a.grad - b.grad).abs().max())
+    assert err <= 1e-4 * max(1.0, scale), (name, err, scale)
+
+
+def _torch_backward(pc, pf, wo, g, chunk):
+  """The fallback branch of _JointWeightsFn.backward, forced."""
+  class Ctx:
+    pass
+  ctx = Ctx()
+  ctx.saved_tensors = (pc, pf, wo)
+  ctx.chunk = chunk
+  orig = nat.joint_weights_backward_supported
+  nat.joint_weights_backward_supported = lambda *a, **k: False
+  try:
+    return lt.weight_fns._JointWeightsFn.backward(ctx, g)[:4]
+  finally:
+    nat.joint_weights_backward_supported = orig
+
+
+def test_backward_errors_and_empty(cuda):
+  pc, pf, wo, bias = _inputs(cuda, (0, 4), 33, 64, 33)
+  dpc, dpf, dwo, db = nat.joint_weights_backward(pc, pf, wo, torch.zeros([0, 4, 33, 33], device=cuda))
+  assert dpf.shape == (0, 4, 64) and float(dpc.abs().sum()) == 0 and float(dwo.abs().sum()) == 0
+  assert db.shape == (33,) and float(db.abs().sum()) == 0
+  assert not nat.joint_weights_backward_supported(33, 48, 33)     # hidden % 32
+  assert nat.joint_weights_backward_supported(33, 320, 33)        # 10 column blocks: 5 x 2 waves
+  assert not nat.joint_weights_backward_supported(1057, 512, 33)  # d_ctx_proj exceeds LDS
+  pc, pf, wo, bias = _inputs(cuda, (2, 3), 33, 48, 33)
+  with pytest.raises(nat.LatticeLibraryError):
+    nat.joint_weights_backward(pc, pf, wo, torch.zeros([2, 3, 33, 33], device=cuda))
 
 
 def test_joint_weight_fn_in_lattice(cuda):

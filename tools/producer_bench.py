@@ -41,6 +41,11 @@ def main():
       return torch.matmul(torch.tanh(pc[None, None] + pf[:, :, None, :]), wo.t()) + bias
 
     kern = timeit(lambda: nat.joint_weights(pc, pf, wo, bias))
+    # |projection| > 40 somewhere: the kernel takes the direct e^{2(a+b)} path
+    pf_big = pf.clone()
+    pf_big.view(-1)[0] = 100.0
+    kern_direct = timeit(lambda: nat.joint_weights(pc, pf_big, wo, bias))
+    del pf_big
     ref = timeit(torch_fwd)
     leaves = [t.clone().requires_grad_(True) for t in (pc, pf, wo, bias)]
     gW = torch.randn([B, T, C, R], device='cuda')
@@ -54,13 +59,16 @@ def main():
                        leaves[2].t()) + leaves[3]
       torch.autograd.backward(W, gW)
 
+    kbwd = timeit(lambda: nat.joint_weights_backward(pc, pf, wo, gW), reps=3)
     kfb = timeit(kern_fb, reps=3)
     rfb = timeit(torch_fb, reps=3)
     flops = 2.0 * B * T * C * R * H
     print(json.dumps({'H': H, 'B': B, 'T': T, 'C': C, 'R': R,
-                      'producer_fwd_ms': kern, 'torch_fwd_ms': ref,
-                      'producer_fwd_bwd_ms': kfb, 'torch_fwd_bwd_ms': rfb,
+                      'producer_fwd_ms': kern, 'producer_fwd_direct_ms': kern_direct,
+                      'torch_fwd_ms': ref,
+                      'producer_bwd_kernel_ms': kbwd, 'producer_fwd_bwd_ms': kfb, 'torch_fwd_bwd_ms': rfb,
                       'producer_fwd_TFLOPs': flops / (kern * 1e-3) / 1e12,
+                      'producer_bwd_TFLOPs': 2 * flops / (kbwd * 1e-3) / 1e12,
                       'W_write_GBps': B * T * C * R * 4 / (kern * 1e-3) / 1e9}), flush=True)
     del leaves, gW
 
