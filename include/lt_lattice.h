@@ -276,9 +276,8 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
  * hidden % 32 == 0, out_dim <= 64, rows * max(num_states, hidden) < 2^31 and
  * the d_ctx_proj block of one workgroup (4 * num_states * 32 * waves bytes,
  * waves = the largest of 8/4/2/1 dividing hidden / 32) plus 14 KB in LDS
- * (<= 160 KB). All outputs are overwritten; d_frame_proj sums a frame's tiles
- * with fp32 atomics (its low bits can vary run to run), the others are
- * reduced in a fixed order. workspace: lt_joint_weights_backward_workspace_bytes(). */
+ * (<= 160 KB). All outputs are overwritten, every sum in a fixed order
+ * (deterministic). workspace: lt_joint_weights_backward_workspace_bytes(). */
 int lt_joint_weights_backward_workspace_bytes(int64_t rows, int32_t num_states, int32_t hidden,
                                               int32_t out_dim, size_t* bytes);
 int lt_joint_weights_backward(int64_t rows, int32_t num_states, int32_t hidden, int32_t out_dim,

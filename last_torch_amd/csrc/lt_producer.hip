@@ -164,6 +164,117 @@ const void* pick(bool two) {
              : (const void*)joint_weights_kernel<OBF16, false>;
 }
 
+// Frame-block form (used when a block fits LDS): a workgroup stages 32
+// frames' e^{2 pf} (or pf on the direct path) in LDS once and its waves walk
+// the context states, so the per-tile operands come from LDS plus one
+// broadcast row of e^{2 pc}; the row-tile form above re-reads both per tile.
+template <bool OBF16, bool TWO>
+__global__ __launch_bounds__(512) void joint_weights_fb_kernel(const JArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short wfl[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int H = a.H, R = a.R, C = a.C, HP = H + 8, FS = H + 4;
+  float* fb = (float*)(wfl + ((R * HP + 7) & ~7));  // [32][H + 4] fp32
+  float* crow = fb + 32 * FS + wave * H;             // [waves][H] fp32
+  for (int i = tid; i < R * H; i += blockDim.x) {
+    const int y = i / H, hh = i - y * H;
+    wfl[y * HP + hh] = f2bf(a.wo[i]);
+  }
+  const bool split = *a.big == 0;
+  const float* csrc = split ? a.ec : a.pc;
+  const float* fsrc = split ? a.ef : a.pf;
+  const int rows = (int)a.rows;  // < 2^31 / H (host check)
+  const int nblk = (rows + 31) / 32;
+  const int r = lane & 31, hk = 8 * (lane >> 5), half = lane >> 5;
+  const int y0 = r, y1 = 32 + r;
+  const bool v0 = y0 < R, v1 = y1 < R;
+  const float b0 = v0 ? a.bias[y0] : 0.f, b1 = v1 ? a.bias[y1] : 0.f;
+  const unsigned short* w0 = wfl + (v0 ? y0 : R - 1) * HP + hk;
+  const unsigned short* w1 = wfl + (v1 ? y1 : R - 1) * HP + hk;
+  const int h4 = H / 4;
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    __syncthreads();  // Wo staged / previous block's reads done
+    for (int e = tid; e < 32 * h4; e += blockDim.x) {
+      const int m = e / h4, k4 = e - m * h4;
+      const int f = 32 * blk + m;
+      const float4 v = f < rows ? ((const float4*)fsrc)[(size_t)f * h4 + k4]
+                                : float4{0.f, 0.f, 0.f, 0.f};
+      *(float4*)(fb + m * FS + 4 * k4) = v;
+    }
+    __syncthreads();
+    const float* fr = fb + r * FS + hk;
+    // this wave's context row (e^{2 pc[c]} or pc[c]) goes through a private
+    // LDS slice, loaded one tile ahead
+    float4 p0, p1, p2, p3;
+    const float4 z4 = {0.f, 0.f, 0.f, 0.f};
+    auto load_row = [&](int cc) {
+      const float4* src = (const float4*)(csrc + (size_t)cc * H);
+      p0 = lane < h4 ? src[lane] : z4;
+      p1 = lane + 64 < h4 ? src[lane + 64] : z4;
+      p2 = lane + 128 < h4 ? src[lane + 128] : z4;
+      p3 = lane + 192 < h4 ? src[lane + 192] : z4;
+    };
+    if (wave < C) load_row(wave);
+    for (int c = wave; c < C; c += nw) {
+      float4* cw = (float4*)crow;
+      if (lane < h4) cw[lane] = p0;
+      if (lane + 64 < h4) cw[lane + 64] = p1;
+      if (lane + 128 < h4) cw[lane + 128] = p2;
+      if (lane + 192 < h4) cw[lane + 192] = p3;
+      if (c + nw < C) load_row(c + nw);
+      const float* cr = crow + hk;
+      f32x16 acc0 = {}, acc1 = {};
+      if (split) {
+#pragma unroll 2
+        for (int k0 = 0; k0 < H; k0 += 16) {
+          const float4 c0 = *(const float4*)(cr + k0), c1 = *(const float4*)(cr + k0 + 4);
+          const float4 f0 = *(const float4*)(fr + k0), f1 = *(const float4*)(fr + k0 + 4);
+          const u32x4 t = {pk_bf16(tanh_from_exp(f32x2{c0.x, c0.y} * f32x2{f0.x, f0.y})),
+                           pk_bf16(tanh_from_exp(f32x2{c0.z, c0.w} * f32x2{f0.z, f0.w})),
+                           pk_bf16(tanh_from_exp(f32x2{c1.x, c1.y} * f32x2{f1.x, f1.y})),
+                           pk_bf16(tanh_from_exp(f32x2{c1.z, c1.w} * f32x2{f1.z, f1.w}))};
+          const bf16x8 af = __builtin_bit_cast(bf16x8, t);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w0 + k0), acc0, 0, 0, 0);
+          if (TWO)
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w1 + k0), acc1, 0, 0, 0);
+        }
+      } else {
+#pragma unroll 2
+        for (int k0 = 0; k0 < H; k0 += 16) {
+          const float4 c0 = *(const float4*)(cr + k0), c1 = *(const float4*)(cr + k0 + 4);
+          const float4 f0 = *(const float4*)(fr + k0), f1 = *(const float4*)(fr + k0 + 4);
+          const u32x4 t = {pk_bf16(tanh_from_exp(exp2x(f32x2{c0.x + f0.x, c0.y + f0.y}))),
+                           pk_bf16(tanh_from_exp(exp2x(f32x2{c0.z + f0.z, c0.w + f0.w}))),
+                           pk_bf16(tanh_from_exp(exp2x(f32x2{c1.x + f1.x, c1.y + f1.y}))),
+                           pk_bf16(tanh_from_exp(exp2x(f32x2{c1.z + f1.z, c1.w + f1.w})))};
+          const bf16x8 af = __builtin_bit_cast(bf16x8, t);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w0 + k0), acc0, 0, 0, 0);
+          if (TWO)
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w1 + k0), acc1, 0, 0, 0);
+        }
+      }
+      // C/D: column y = lane & 31 (+32), row = frame (i & 3) + 8 (i >> 2) + 4 half
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int f = 32 * blk + (i & 3) + 8 * (i >> 2) + 4 * half;
+        if (f >= rows) continue;
+        const long long mr = (long long)f * C + c;
+        if (v0) stw<OBF16>(a.W, mr * R + y0, acc0[i] + b0);
+        if (TWO && v1) stw<OBF16>(a.W, mr * R + y1, acc1[i] + b1);
+      }
+    }
+  }
+}
+
+template <bool OBF16>
+const void* pick_fb(bool two) {
+  return two ? (const void*)joint_weights_fb_kernel<OBF16, true>
+             : (const void*)joint_weights_fb_kernel<OBF16, false>;
+}
+
+long long fb_lds(int H, int R) {  // Wo bf16, the frame block, 8 context rows
+  return 2LL * (((long long)R * (H + 8) + 7) & ~7LL) + 4LL * 32 * (H + 4) + 4LL * 8 * H;
+}
+
 size_t ws_bytes(long long rows, int C, int H) {
   return 256 + 4 * (size_t)H * ((size_t)C + (size_t)rows);
 }
@@ -219,16 +330,29 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
     e = hipLaunchKernel((const void*)joint_exp_kernel, dim3(grid), dim3(256), args, 0, st);
     if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   }
+  const bool bf = weight_dtype == LT_DTYPE_BF16, two = out_dim > 32;
+  const long long lfb = fb_lds(hidden, out_dim);
+  void* args[] = {&a};
+  if (lfb <= 160 * 1024 && hidden <= 1024 && rows * (long long)hidden < (1LL << 31)) {
+    // frame-block form: one workgroup of 8 waves per CU
+    const void* k = bf ? pick_fb<true>(two) : pick_fb<false>(two);
+    if (lfb > 64 * 1024) {
+      e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfb);
+      if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+    }
+    const int grid = (int)std::min<long long>((rows + 31) / 32, cus);
+    e = hipLaunchKernel(k, dim3(grid), dim3(512), args, (size_t)lfb, st);
+    if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+    return LT_OK;
+  }
   const long long tiles = (rows * num_states + 31) / 32;
   const long long want = (tiles + 3) / 4;
   const int grid = (int)std::min<long long>(want, 4LL * cus);  // persistent: Wo loaded once per WG
-  const bool bf = weight_dtype == LT_DTYPE_BF16, two = out_dim > 32;
   const void* k = bf ? pick<true>(two) : pick<false>(two);
   if (lds > 64 * 1024) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   }
-  void* args[] = {&a};
   e = hipLaunchKernel(k, dim3(grid), dim3(256), args, (size_t)lds, st);
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;
@@ -242,15 +366,16 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
 //   gw[m, h]   = sum_r g[m, r] wo[r, h]          (MFMA, K = R)
 //   dh[m, h]   = gw[m, h] (1 - hid[m, h]^2)
 //   d_wo[r, h] = sum_m g[m, r] hid[m, h]          (MFMA, K = the tile's 32 rows)
-//   d_pf[f, h] = sum_c dh[(f, c), h]              (MFMA against a one-hot frame map)
-//   d_pc[c, h] = sum_f dh[(f, c), h]              (LDS fp32 adds)
-// Every product is split-bf16 (x = hi + lo; hi*hi + hi*lo + lo*hi, or exact
-// one-hot * (hi + lo)), about 16 mantissa bits, sums fp32. One workgroup of
-// H / 32 waves per CU: wave w owns the 32 hidden columns [32w, 32w + 32) for
-// every tile, so its d_wo block stays in registers for the whole launch;
-// the MFMA output layout of gw / dh / hid (row (i & 3) + 8 (i >> 2) + 4 half)
-// is used directly as the K operand of the next products (the K order only
-// has to agree between A and B).
+//   d_pf[f, h] = sum_c dh[(f, c), h]              (registers, over the C tiles)
+//   d_pc[c, h] = sum_f dh[(f, c), h]              (column sum per tile, LDS)
+// A tile is 32 frames x ONE context state c: a workgroup takes a block of 32
+// frames and walks c = 0..C-1, so pf stays in registers for the block, pc is
+// one value per lane and tile, and d_pf accumulates in registers (no atomics).
+// Products are split-bf16 (x = hi + lo; hi*hi + hi*lo + lo*hi), about 16
+// mantissa bits, sums fp32. Each wave owns 32 hidden columns for the whole
+// launch, so its d_wo block stays in registers; the MFMA output layout of
+// gw / hid (row (i & 3) + 8 (i >> 2) + 4 half) is used directly as the K
+// operand of d_wo (the K order only has to agree between A and B).
 namespace {
 
 struct JBArgs {
@@ -258,7 +383,7 @@ struct JBArgs {
   const float* pf;   // [rows, H]
   const float* wo;   // [R, H]
   const float* g;    // [rows * C, R]
-  float* dpf;        // [rows, H], zeroed
+  float* dpf;        // [rows, H]
   float* part;       // [grid][C + R][H] per-workgroup d_pc, d_wo
   long long rows;
   int C, H, R;
@@ -292,16 +417,15 @@ __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a)
   constexpr int nthr = 64 * NW, HW = 32 * NW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, R = a.R, C = a.C;
-  // this workgroup's hidden columns: [h0, h0 + HW)  // this workgroup's hidden columns [h0, h0 + HW)
+  // this workgroup's hidden columns: [h0, h0 + HW)
   const int h0 = blockIdx.y * HW;
-  float* gtb = bl;                    // [2][32][GS] double-buffered g tile
-  int* rinfo = (int*)(bl + 2 * 32 * GS);  // [2][32][2]: frame, context state (-1: past M)
-  float* dpc = bl + 2 * 32 * GS + 128;    // [C][HW]
+  float* gtb = bl;                  // [2][32][GS] double-buffered g tile
+  float* dpc = bl + 2 * 32 * GS;    // [C][HW]
   for (int e = tid; e < C * HW; e += nthr) dpc[e] = 0.f;
   const int half = lane >> 5, col = lane & 31;
   const int hl = wave * 32 + col, h = h0 + hl;
-  const unsigned M = (unsigned)(a.rows * C);  // < 2^31 (host check)
-  const unsigned ntile = (M + 31) / 32;
+  const int rows = (int)a.rows;  // rows * max(C, H) < 2^31 (host check)
+  const int nblk = (rows + 31) / 32;
   bf16x8 woh[KB], wol[KB];  // B[k = r][n = h] of gw
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
@@ -317,105 +441,92 @@ __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a)
   float dbias = 0.f;  // thread tid < R of blockIdx.y == 0: sum of g[:, tid]
   constexpr int GPT = (GN + nthr - 1) / nthr;  // staged g values per thread
   float gnext[GPT];
-  auto load_g = [&](unsigned tile) {
+  // tile (blk, c): rows (f = 32 blk + m, c), m < 32
+  auto load_g = [&](int blk, int c) {
 #pragma unroll
     for (int u = 0; u < GPT; ++u) {
       const int e = tid + u * nthr;
       const int m = e / (KB * 16), r = e - m * (KB * 16);
-      const unsigned mg = tile * 32 + m;
-      gnext[u] = (e < GN && tile < ntile && mg < M && r < R) ? a.g[(size_t)mg * R + r] : 0.f;
+      const int f = 32 * blk + m;
+      gnext[u] = (e < GN && blk < nblk && f < rows && r < R)
+                     ? a.g[((size_t)f * C + c) * R + r] : 0.f;
     }
   };
-  load_g(blockIdx.x);
   int buf = 0;
-  for (unsigned tile = blockIdx.x; tile < ntile; tile += gridDim.x, buf ^= 1) {
-    float* gt = gtb + buf * 32 * GS;
-    int* ri = rinfo + buf * 64;
-#pragma unroll
-    for (int u = 0; u < GPT; ++u) {
-      const int e = tid + u * nthr;
-      if (e < GN) {
-        const int m = e / (KB * 16), r = e - m * (KB * 16);
-        gt[m * GS + r] = gnext[u];
-      }
-    }
-    if (tid < 32) {
-      const unsigned mg = tile * 32 + tid;
-      const unsigned f = mg / (unsigned)C;
-      ri[2 * tid] = (int)f;
-      ri[2 * tid + 1] = mg < M ? (int)(mg - f * C) : -1;
-    }
-    __syncthreads();  // one barrier per tile: the other buffer is written next
-    load_g(tile + gridDim.x);  // in flight during this tile
-    if (blockIdx.y == 0 && tid < R)
-      for (int m = 0; m < 32; ++m) dbias += gt[m * GS + tid];
-    // x = pc[c] + pf[f] for this lane's 16 rows, loads issued before the gw products
-    float x[16];
-    int cc[16], ff[16];
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    // this lane's 16 frames (MFMA output rows) and their projections
+    float pfv[16], dpf[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
-      const int2 fc = *(const int2*)(ri + 2 * m);
-      ff[i] = fc.x;
-      cc[i] = fc.y;
-      const int c = fc.y < 0 ? 0 : fc.y;
-      const unsigned f = fc.y < 0 ? (unsigned)(a.rows - 1) : (unsigned)fc.x;
-      x[i] = a.pc[c * H + h] + a.pf[(size_t)f * H + h];
+      const int f = 32 * blk + (i & 3) + 8 * (i >> 2) + 4 * half;
+      pfv[i] = f < rows ? a.pf[(size_t)f * H + h] : 0.f;
+      dpf[i] = 0.f;
     }
-    // gw: A[m = col][k = r]
-    f32x16 gw = {};
+    load_g(blk, 0);
+    for (int c = 0; c < C; ++c, buf ^= 1) {
+      float* gt = gtb + buf * 32 * GS;
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      const float4 x0 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half);
-      const float4 x1 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half + 4);
-      const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      bf16x8 ah, al;
-      split8(v, ah, al);
-      gw = mfma3(ah, al, woh[kb], wol[kb], gw);
-    }
-    const int f0 = ri[0];
-    f32x16 dpfa = {};
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      // K slot (half, j) <-> row m(i = 8q + j, half): this lane's own rows
-      float hv[8], dv[8], gv[8], oh[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = 8 * q + j;
-        const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
-        const bool ok = cc[i] >= 0;
-        const float e = __builtin_amdgcn_exp2f(x[i] * (2.f * kLog2e));
-        const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
-        hv[j] = ok ? t : 0.f;
-        dv[j] = ok ? gw[i] * (1.f - t * t) : 0.f;
-        oh[j] = ff[i] - f0 == col ? 1.f : 0.f;
-        atomicAdd(dpc + (ok ? cc[i] : 0) * HW + hl, dv[j]);
-        gv[j] = gt[m * GS + col];
+      for (int u = 0; u < GPT; ++u) {
+        const int e = tid + u * nthr;
+        if (e < GN) {
+          const int m = e / (KB * 16), r = e - m * (KB * 16);
+          gt[m * GS + r] = gnext[u];
+        }
       }
-      bf16x8 hh, hlo, dhh, dhl, gh, glo, ohh, ohl;  // ohl = 0 (one-hot values are exact)
-      split8(hv, hh, hlo);
-      split8(dv, dhh, dhl);
-      split8(oh, ohh, ohl);
-      split8(gv, gh, glo);
-      dwo0 = mfma3(gh, glo, hh, hlo, dwo0);
-      if (TWO) {
+      __syncthreads();  // one barrier per tile: the other buffer is written next
+      if (c + 1 < C) load_g(blk, c + 1);  // in flight during this tile
+      if (blockIdx.y == 0 && tid < R)
+        for (int m = 0; m < 32; ++m) dbias += gt[m * GS + tid];
+      const float pcv = a.pc[c * H + h];
+      // gw: A[m = col][k = r]
+      f32x16 gw = {};
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const float4 x0 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half);
+        const float4 x1 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half + 4);
+        const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        bf16x8 ah, al;
+        split8(v, ah, al);
+        gw = mfma3(ah, al, woh[kb], wol[kb], gw);
+      }
+      float csum = 0.f;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        // K slot (half, j) <-> row m(i = 8q + j, half): this lane's own rows
+        float hv[8], gv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int i = 8 * q + j;
-          gv[j] = gt[((i & 3) + 8 * (i >> 2) + 4 * half) * GS + 32 + col];
+          const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
+          const float e = __builtin_amdgcn_exp2f((pcv + pfv[i]) * (2.f * kLog2e));
+          const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
+          hv[j] = t;  // rows past `rows` have g = 0: no contribution to d_wo
+          const float d = gw[i] * (1.f - t * t);
+          dpf[i] += d;
+          csum += d;
+          gv[j] = gt[m * GS + col];
         }
+        bf16x8 hh, hlo, gh, glo;
+        split8(hv, hh, hlo);
         split8(gv, gh, glo);
-        dwo1 = mfma3(gh, glo, hh, hlo, dwo1);
+        dwo0 = mfma3(gh, glo, hh, hlo, dwo0);
+        if (TWO) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int i = 8 * q + j;
+            gv[j] = gt[((i & 3) + 8 * (i >> 2) + 4 * half) * GS + 32 + col];
+          }
+          split8(gv, gh, glo);
+          dwo1 = mfma3(gh, glo, hh, hlo, dwo1);
+        }
       }
-      dpfa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ohh, dhl, dpfa, 0, 0, 0);
-      dpfa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ohh, dhh, dpfa, 0, 0, 0);
+      csum += __shfl_xor(csum, 32);
+      if (half == 0) dpc[c * HW + hl] += csum;  // this wave owns column hl
     }
-    // frames in this tile: the last valid row's frame (row 31 or the last below M)
-    const int nf = (int)(min(tile * 32 + 31, M - 1) / (unsigned)C) - f0 + 1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int p = (i & 3) + 8 * (i >> 2) + 4 * half;
-      if (p < nf) atomicAdd(a.dpf + (size_t)(f0 + p) * H + h, dpfa[i]);
+      const int f = 32 * blk + (i & 3) + 8 * (i >> 2) + 4 * half;
+      if (f < rows) a.dpf[(size_t)f * H + h] = dpf[i];
     }
   }
   // per-workgroup partials: d_pc rows [0, C), d_wo rows [C, C + R), d_bias after them
@@ -469,7 +580,7 @@ int bwd_grid(long long rows, int C, int H) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const long long tiles = (rows * C + 31) / 32;
+  const long long tiles = (rows + 31) / 32;  // blocks of 32 frames
   const int gy = std::max(1, H / (32 * bwd_waves(H)));
   // one resident workgroup per CU over the whole (x, y) grid
   const long long gx = std::max<long long>(1, (cus * (bwd_waves(H) < 8 ? 2 : 1)) / gy);
@@ -478,7 +589,7 @@ int bwd_grid(long long rows, int C, int H) {
 
 long long bwd_lds(int C, int H, int R) {
   const int KB = (R + 15) / 16;
-  return 4LL * (2 * 32 * (KB * 16 + 4) + 128 + (long long)C * 32 * bwd_waves(H));
+  return 4LL * (2 * 32 * (KB * 16 + 4) + (long long)C * 32 * bwd_waves(H));
 }
 
 long long bwd_stride(int C, int H, int R) { return (long long)(C + R) * H + 64; }
@@ -526,8 +637,6 @@ int lt_joint_weights_backward(int64_t rows, int32_t num_states, int32_t hidden, 
     if (e == hipSuccess) e = hipMemsetAsync(d_out_bias, 0, 4 * (size_t)R, st);
     return e == hipSuccess ? LT_OK : lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   }
-  e = hipMemsetAsync(d_frame_proj, 0, 4 * (size_t)rows * H, st);
-  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   JBArgs a;
   a.pc = ctx_proj; a.pf = frame_proj; a.wo = out_weight; a.g = grad_W;
   a.dpf = d_frame_proj; a.part = (float*)workspace;

@@ -53,6 +53,7 @@ def _inputs(cuda, lead, C, H, R, scale=1.0, seed=0):
     ((1, 1), 33, 16, 64),     # full two tiles
     ((5, 13), 21, 512, 33),   # H = 512 (the bench hidden size), ragged rows
     ((37,), 33, 32, 33),      # rows * C not a multiple of 32
+    ((2, 3), 5, 848, 33),     # frame block exceeds LDS: the row-tile kernel
 ])
 def test_forward_vs_torch(cuda, lead, C, H, R):
   pc, pf, wo, bias = _inputs(cuda, lead, C, H, R)
