@@ -484,7 +484,9 @@ def joint_weights_backward_supported(C, H, R, rows=0):
   n = H // 32
   waves = 8 if n % 8 == 0 else 4 if n % 4 == 0 else 2 if n % 2 == 0 else 1
   KB = (R + 15) // 16
-  return 4 * (2 * 32 * (16 * KB + 4) + C * 32 * waves) <= 160 * 1024
+  RB = 64 if R > 32 else 32
+  bufb = 4 * 32 * (16 * KB + 4) + 4 * 32 * (16 * KB + 8) + 4 * RB * 36
+  return 2 * bufb + 4 * C * 32 * waves <= 160 * 1024
 
 
 def joint_weights_backward(ctx_proj, frame_proj, out_weight, grad_W):

@@ -403,6 +403,13 @@ LT_DEVINL void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
   lo = __builtin_bit_cast(bf16x8, l);
 }
 
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+// 8 bf16: p[0..3] and p[8..11] (8-byte aligned)
+LT_DEVINL bf16x8 tpair(const unsigned short* p) {
+  const bf16x4 a = *(const bf16x4*)p, b = *(const bf16x4*)(p + 8);
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 LT_DEVINL f32x16 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 acc) {
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
@@ -412,15 +419,22 @@ LT_DEVINL f32x16 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 acc) {
 template <int KB, bool TWO, int NW>  // KB = ceil(R / 16) K blocks of gw; TWO: R > 32; NW waves
 __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a) {
   extern __shared__ __attribute__((aligned(16))) float bl[];
-  constexpr int GS = KB * 16 + 4;  // g tile row stride (floats)
+  constexpr int GS = KB * 16 + 4;   // fp32 g tile row stride (floats)
+  constexpr int GB = KB * 16 + 8;   // bf16 g tile row stride: [m][r]
+  constexpr int RB = TWO ? 64 : 32;  // rows of the transposed bf16 tile: [r][m]
+  constexpr int TS = 32 + 4;        // its row stride
   constexpr int GN = 32 * KB * 16;  // g tile elements staged per tile
+  // per buffer (bytes): fp32 [32][GS] | hi, lo [32][GB] | hi, lo [RB][TS]
+  constexpr int BUFB = 4 * 32 * GS + 2 * 2 * 32 * GB + 2 * 2 * RB * TS;
   constexpr int nthr = 64 * NW, HW = 32 * NW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, R = a.R, C = a.C;
   // this workgroup's hidden columns: [h0, h0 + HW)
   const int h0 = blockIdx.y * HW;
-  float* gtb = bl;                  // [2][32][GS] double-buffered g tile
-  float* dpc = bl + 2 * 32 * GS;    // [C][HW]
+  // double-buffered g tile: fp32 (bias sums), bf16 hi/lo splits [m][r] (gw's
+  // A operand) and transposed [r][m] (d_wo's A operand), split once here
+  // instead of in every wave
+  float* dpc = (float*)((char*)bl + 2 * BUFB);  // [C][HW]
   for (int e = tid; e < C * HW; e += nthr) dpc[e] = 0.f;
   const int half = lane >> 5, col = lane & 31;
   const int hl = wave * 32 + col, h = h0 + hl;
@@ -464,13 +478,28 @@ __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a)
     }
     load_g(blk, 0);
     for (int c = 0; c < C; ++c, buf ^= 1) {
-      float* gt = gtb + buf * 32 * GS;
+      char* bb = (char*)bl + buf * BUFB;
+      float* gt = (float*)bb;
+      unsigned short* gh = (unsigned short*)(bb + 4 * 32 * GS);
+      unsigned short* gl = gh + 32 * GB;
+      unsigned short* th = gl + 32 * GB;
+      unsigned short* tl = th + RB * TS;
 #pragma unroll
       for (int u = 0; u < GPT; ++u) {
         const int e = tid + u * nthr;
         if (e < GN) {
           const int m = e / (KB * 16), r = e - m * (KB * 16);
-          gt[m * GS + r] = gnext[u];
+          const float v = gnext[u];
+          const unsigned short hi = __builtin_bit_cast(unsigned short, (__bf16)v);
+          const unsigned short lo =
+              __builtin_bit_cast(unsigned short, (__bf16)(v - __uint_as_float((unsigned)hi << 16)));
+          gt[m * GS + r] = v;
+          gh[m * GB + r] = hi;
+          gl[m * GB + r] = lo;
+          if (r < RB) {
+            th[r * TS + m] = hi;
+            tl[r * TS + m] = lo;
+          }
         }
       }
       __syncthreads();  // one barrier per tile: the other buffer is written next
@@ -482,43 +511,34 @@ __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a)
       f32x16 gw = {};
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        const float4 x0 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half);
-        const float4 x1 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half + 4);
-        const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        bf16x8 ah, al;
-        split8(v, ah, al);
+        const bf16x8 ah = *(const bf16x8*)(gh + col * GB + 16 * kb + 8 * half);
+        const bf16x8 al = *(const bf16x8*)(gl + col * GB + 16 * kb + 8 * half);
         gw = mfma3(ah, al, woh[kb], wol[kb], gw);
       }
       float csum = 0.f;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         // K slot (half, j) <-> row m(i = 8q + j, half): this lane's own rows
-        float hv[8], gv[8];
+        float hv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int i = 8 * q + j;
-          const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
           const float e = __builtin_amdgcn_exp2f((pcv + pfv[i]) * (2.f * kLog2e));
           const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
           hv[j] = t;  // rows past `rows` have g = 0: no contribution to d_wo
           const float d = gw[i] * (1.f - t * t);
           dpf[i] += d;
           csum += d;
-          gv[j] = gt[m * GS + col];
         }
-        bf16x8 hh, hlo, gh, glo;
+        bf16x8 hh, hlo;
         split8(hv, hh, hlo);
-        split8(gv, gh, glo);
-        dwo0 = mfma3(gh, glo, hh, hlo, dwo0);
-        if (TWO) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int i = 8 * q + j;
-            gv[j] = gt[((i & 3) + 8 * (i >> 2) + 4 * half) * GS + 32 + col];
-          }
-          split8(gv, gh, glo);
-          dwo1 = mfma3(gh, glo, hh, hlo, dwo1);
-        }
+        // A[r][k slot (half, j)] = g[m][r], m = 16q + 4 half + (j & 3) + 8 (j >> 2):
+        // two runs of 4 in the transposed tile
+        const int tm = 16 * q + 4 * half;
+        dwo0 = mfma3(tpair(th + col * TS + tm), tpair(tl + col * TS + tm), hh, hlo, dwo0);
+        if (TWO)
+          dwo1 = mfma3(tpair(th + (32 + col) * TS + tm), tpair(tl + (32 + col) * TS + tm), hh,
+                       hlo, dwo1);
       }
       csum += __shfl_xor(csum, 32);
       if (half == 0) dpc[c * HW + hl] += csum;  // this wave owns column hl
@@ -587,9 +607,10 @@ int bwd_grid(long long rows, int C, int H) {
   return (int)std::max<long long>(1, std::min<long long>(tiles, gx));
 }
 
-long long bwd_lds(int C, int H, int R) {
-  const int KB = (R + 15) / 16;
-  return 4LL * (2 * 32 * (KB * 16 + 4) + (long long)C * 32 * bwd_waves(H));
+long long bwd_lds(int C, int H, int R) {  // keep in sync with BUFB
+  const int KB = (R + 15) / 16, RB = R > 32 ? 64 : 32;
+  const long long bufb = 4LL * 32 * (KB * 16 + 4) + 4LL * 32 * (KB * 16 + 8) + 4LL * RB * 36;
+  return 2 * bufb + 4LL * C * 32 * bwd_waves(H);
 }
 
 long long bwd_stride(int C, int H, int R) { return (long long)(C + R) * H + 64; }
