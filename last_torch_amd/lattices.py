@@ -242,6 +242,8 @@ class RecognitionLattice(nn.Module, Generic[T]):
     if getattr(self.weight_fn, 'time_batched', False):
       # the weight function takes any leading dims (JointWeightFn's
       # matrix-core producer: one launch for every frame)
+      if hasattr(self.weight_fn, 'forward_joint'):
+        return self.weight_fn.forward_joint(cache, frames)
       blank, lexical = self.weight_fn(cache, frames)
       return torch.cat([blank[..., None], lexical], dim=-1)
 

@@ -148,14 +148,23 @@ class JointWeightFn(WeightFn[torch.Tensor]):
     return (self.fused and frame.is_cuda and frame.dtype == torch.float32 and
             self.hidden_size % 16 == 0 and self.vocab_size + 1 <= 64)
 
-  def forward(self, cache, frame, state=None):
-    ctx = cache
-    if state is None and self._use_kernel(frame):
-      pc = self.context_projection(ctx)
+  def forward_joint(self, cache, frame):
+    """All context states' arc weights as ONE tensor [..., C, V+1] (blank at
+    [..., 0]), the layout RecognitionLattice hands to the lattice kernels:
+    with the matrix-core producer no split / concatenate round trip."""
+    if self._use_kernel(frame):
+      pc = self.context_projection(cache)
       pf = self.frame_projection(frame)
       wo = torch.cat([self.to_blank.weight, self.to_vocab.weight], 0)
       bias = torch.cat([self.to_blank.bias, self.to_vocab.bias], 0)
-      W = _JointWeightsFn.apply(pc, pf, wo, bias, self.backward_chunk)
+      return _JointWeightsFn.apply(pc, pf, wo, bias, self.backward_chunk)
+    blank, lexical = self.forward(cache, frame)
+    return torch.cat([blank[..., None], lexical], dim=-1)
+
+  def forward(self, cache, frame, state=None):
+    ctx = cache
+    if state is None and self._use_kernel(frame):
+      W = self.forward_joint(cache, frame)
       return W[..., 0], W[..., 1:]
     if state is None:
       joint = self.context_projection(ctx) + self.frame_projection(frame)[..., None, :]
