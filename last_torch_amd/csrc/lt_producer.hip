@@ -169,7 +169,7 @@ const void* pick(bool two) {
 // the context states, so the per-tile operands come from LDS plus one
 // broadcast row of e^{2 pc}; the row-tile form above re-reads both per tile.
 template <bool OBF16, bool TWO>
-__global__ __launch_bounds__(512) void joint_weights_fb_kernel(const JArgs a) {
+__global__ __launch_bounds__(1024) void joint_weights_fb_kernel(const JArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned short wfl[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int H = a.H, R = a.R, C = a.C, HP = H + 8, FS = H + 4;
@@ -271,8 +271,17 @@ const void* pick_fb(bool two) {
              : (const void*)joint_weights_fb_kernel<OBF16, false>;
 }
 
-long long fb_lds(int H, int R) {  // Wo bf16, the frame block, 8 context rows
-  return 2LL * (((long long)R * (H + 8) + 7) & ~7LL) + 4LL * 32 * (H + 4) + 4LL * 8 * H;
+long long fb_lds(int H, int R, int nw) {  // Wo bf16, the frame block, a context row per wave
+  return 2LL * (((long long)R * (H + 8) + 7) & ~7LL) + 4LL * 32 * (H + 4) + 4LL * nw * H;
+}
+
+// waves per frame-block workgroup: the fewest in [4, 16] that give the
+// fewest context tiles per wave (C = 33: 11 waves x 3 tiles, not 8 x 5)
+int fb_waves(int C) {
+  int best = 4;
+  for (int w = 5; w <= 16; ++w)
+    if ((C + w - 1) / w < (C + best - 1) / best) best = w;
+  return best;
 }
 
 size_t ws_bytes(long long rows, int C, int H) {
@@ -331,17 +340,18 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
     if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   }
   const bool bf = weight_dtype == LT_DTYPE_BF16, two = out_dim > 32;
-  const long long lfb = fb_lds(hidden, out_dim);
+  const int fnw = fb_waves(num_states);
+  const long long lfb = fb_lds(hidden, out_dim, fnw);
   void* args[] = {&a};
   if (lfb <= 160 * 1024 && hidden <= 1024 && rows * (long long)hidden < (1LL << 31)) {
-    // frame-block form: one workgroup of 8 waves per CU
+    // frame-block form: one workgroup of fnw waves per CU
     const void* k = bf ? pick_fb<true>(two) : pick_fb<false>(two);
     if (lfb > 64 * 1024) {
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfb);
       if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
     }
     const int grid = (int)std::min<long long>((rows + 31) / 32, cus);
-    e = hipLaunchKernel(k, dim3(grid), dim3(512), args, (size_t)lfb, st);
+    e = hipLaunchKernel(k, dim3(grid), dim3(64 * fnw), args, (size_t)lfb, st);
     if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
     return LT_OK;
   }
