@@ -300,3 +300,35 @@ def test_tuple_semirings_rejected_by_lattice():
                                   torch.zeros([1, 3, 3])))
   with pytest.raises(NotImplementedError):
     lat._forward(None, torch.zeros([1, 1, 1]), torch.ones([1]), lt.semirings.LogLogExpectation)
+
+
+def test_joint_weight_fn_host_paths():
+  """On the CPU JointWeightFn takes the PyTorch path: forward_joint is the
+  [..., C, V+1] concatenation of forward's (blank, lexical), and a per-state
+  call (state given) picks the same rows (weight_fns.py:174-227)."""
+  torch.manual_seed(0)
+  V, H, C = 5, 16, 6
+  wfn = lt.weight_fns.JointWeightFn(vocab_size=V, hidden_size=H)
+  ctx = torch.randn([C, 8])
+  frames = torch.randn([2, 7, 10])
+  blank, lexical = wfn(ctx, frames)
+  W = wfn.forward_joint(ctx, frames)
+  assert W.shape == (2, 7, C, V + 1)
+  assert torch.equal(W[..., 0], blank) and torch.equal(W[..., 1:], lexical)
+  state = torch.tensor([[3] * 7, [1] * 7])
+  b1, l1 = wfn(ctx, frames, state)
+  torch.testing.assert_close(b1, torch.stack([blank[0, :, 3], blank[1, :, 1]]))
+  torch.testing.assert_close(l1[1], lexical[1, :, 1])
+
+
+@pytest.mark.parametrize('C,H,R,rows,ok', [
+    (33, 512, 33, 64000, True),     # the bench head
+    (33, 48, 33, 10, False),        # hidden % 32
+    (33, 320, 33, 10, True),        # 10 column blocks of 2-wave workgroups
+    (1057, 512, 33, 10, False),     # trigram: d_ctx_proj block exceeds LDS
+    (33, 512, 65, 10, False),       # V + 1 > 64
+    (33, 512, 33, 2 ** 26, False),  # rows * H >= 2^31
+])
+def test_joint_weights_backward_supported(C, H, R, rows, ok):
+  from last_torch_amd import _native
+  assert _native.joint_weights_backward_supported(C, H, R, rows) is ok
