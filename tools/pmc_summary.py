@@ -38,7 +38,9 @@ def _kernel_key(name):
   if 'bwd_kernel' in name:
     args = name.split('bwd_kernel<', 1)[-1].split('>', 1)[0].split(',')
     return 'bwd_kernel_ck' if len(args) >= 6 and args[5].strip() == 'true' else 'bwd_kernel'
-  for k in ('fwd_kernel', 'marg_kernel', 'backtrace_kernel', 'num_scatter_kernel', 'pipe_kernel'):
+  for k in ('fwd_kernel', 'marg_kernel', 'backtrace_kernel', 'num_scatter_kernel', 'pipe_kernel',
+            'joint_weights_fb_kernel', 'joint_weights_kernel', 'joint_backward_kernel',
+            'joint_exp_kernel', 'joint_reduce_kernel'):
     if k in name:
       return k
   return None
@@ -78,6 +80,7 @@ def main():
         'batch': args.batch, 'frames': args.frames,
         'dispatches': {'fetch_pass': len(f), 'write_pass': len(w)},
         'fetch_bytes_per_launch': fb, 'write_bytes_per_launch': wb,
+        'fetch_bytes_per_launch_uncorrected': fb / 2 if fb is not None else None,
         'hbm_bytes_per_launch': (fb or 0) + (wb or 0) if (fb is not None and wb is not None)
         else None,
     }
