@@ -254,8 +254,9 @@ int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* 
  * out_weight [out_dim, hidden], out_bias [out_dim]: fp32, 16-byte aligned. W
  * [rows, num_states, out_dim] in weight_dtype. The tanh values and out_weight
  * enter the products as bf16, sums are fp32. tanh(a + b) is formed from
- * e^{2a} e^{2b} (both precomputed into the workspace) unless some |projection|
- * exceeds 40, in which case the kernel evaluates e^{2(a+b)} directly.
+ * e^{2a} e^{2b} (e^{2a} precomputed into the workspace, e^{2b} per block of
+ * 32 frames) unless some |ctx_proj| or a block's |frame_proj| exceeds 40, in
+ * which case that block evaluates e^{2(a+b)} directly.
  * workspace: lt_joint_weights_workspace_bytes() bytes, 16-byte aligned. */
 int lt_joint_weights_workspace_bytes(int64_t rows, int32_t num_states, int32_t hidden,
                                      size_t* bytes);

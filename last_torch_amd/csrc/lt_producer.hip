@@ -179,9 +179,7 @@ __global__ __launch_bounds__(1024) void joint_weights_fb_kernel(const JArgs a) {
     const int y = i / H, hh = i - y * H;
     wfl[y * HP + hh] = f2bf(a.wo[i]);
   }
-  const bool split = *a.big == 0;
-  const float* csrc = split ? a.ec : a.pc;
-  const float* fsrc = split ? a.ef : a.pf;
+  const bool csplit = *a.big == 0;  // every |pc| <= kSplitMax (the pre-pass's flag)
   const int rows = (int)a.rows;  // < 2^31 / H (host check)
   const int nblk = (rows + 31) / 32;
   const int r = lane & 31, hk = 8 * (lane >> 5), half = lane >> 5;
@@ -193,13 +191,29 @@ __global__ __launch_bounds__(1024) void joint_weights_fb_kernel(const JArgs a) {
   const int h4 = H / 4;
   for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
     __syncthreads();  // Wo staged / previous block's reads done
+    // stage pf, decide split vs direct for this block, then turn the block
+    // into e^{2 pf} in place (each thread its own elements)
+    bool over = false;
     for (int e = tid; e < 32 * h4; e += blockDim.x) {
       const int m = e / h4, k4 = e - m * h4;
       const int f = 32 * blk + m;
-      const float4 v = f < rows ? ((const float4*)fsrc)[(size_t)f * h4 + k4]
+      const float4 v = f < rows ? ((const float4*)a.pf)[(size_t)f * h4 + k4]
                                 : float4{0.f, 0.f, 0.f, 0.f};
+      const float mx = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+      over |= !(mx <= kSplitMax);  // NaN counts as over
       *(float4*)(fb + m * FS + 4 * k4) = v;
     }
+    const bool split = csplit && !__syncthreads_or(over);
+    if (split) {
+      for (int e = tid; e < 32 * h4; e += blockDim.x) {
+        const int m = e / h4, k4 = e - m * h4;
+        float4* q = (float4*)(fb + m * FS + 4 * k4);
+        const float4 v = *q;
+        const f32x2 lo = exp2x(f32x2{v.x, v.y}), hi = exp2x(f32x2{v.z, v.w});
+        *q = float4{lo.x, lo.y, hi.x, hi.y};
+      }
+    }
+    const float* csrc = split ? a.ec : a.pc;
     __syncthreads();
     const float* fr = fb + r * FS + hk;
     // this wave's context row (e^{2 pc[c]} or pc[c]) goes through a private
@@ -332,18 +346,22 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
   hipStream_t st = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(big, 0, sizeof(int), st);
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  const int fnw = fb_waves(num_states);
+  const long long lfb = fb_lds(hidden, out_dim, fnw);
+  const bool use_fb = lfb <= 160 * 1024 && hidden <= 1024 && rows * (long long)hidden < (1LL << 31);
   {
-    const long long n4 = ((long long)num_states + rows) * hidden / 4;
-    const int grid = (int)std::min<long long>((n4 + 255) / 256, 8LL * cus);
-    void* args[] = {&a, &ec, &ef, &big};
+    // the frame-block kernel forms e^{2 pf} itself: the pre-pass then covers pc only
+    JArgs ax = a;
+    if (use_fb) ax.rows = 0;
+    const long long n4 = ((long long)num_states + ax.rows) * hidden / 4;
+    const int grid = (int)std::max<long long>(1, std::min<long long>((n4 + 255) / 256, 8LL * cus));
+    void* args[] = {&ax, &ec, &ef, &big};
     e = hipLaunchKernel((const void*)joint_exp_kernel, dim3(grid), dim3(256), args, 0, st);
     if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   }
   const bool bf = weight_dtype == LT_DTYPE_BF16, two = out_dim > 32;
-  const int fnw = fb_waves(num_states);
-  const long long lfb = fb_lds(hidden, out_dim, fnw);
   void* args[] = {&a};
-  if (lfb <= 160 * 1024 && hidden <= 1024 && rows * (long long)hidden < (1LL << 31)) {
+  if (use_fb) {
     // frame-block form: one workgroup of fnw waves per CU
     const void* k = bf ? pick_fb<true>(two) : pick_fb<false>(two);
     if (lfb > 64 * 1024) {

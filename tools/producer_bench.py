@@ -41,11 +41,11 @@ def main():
       return torch.matmul(torch.tanh(pc[None, None] + pf[:, :, None, :]), wo.t()) + bias
 
     kern = timeit(lambda: nat.joint_weights(pc, pf, wo, bias))
-    # |projection| > 40 somewhere: the kernel takes the direct e^{2(a+b)} path
-    pf_big = pf.clone()
-    pf_big.view(-1)[0] = 100.0
-    kern_direct = timeit(lambda: nat.joint_weights(pc, pf_big, wo, bias))
-    del pf_big
+    # some |ctx projection| > 40: every block takes the direct e^{2(a+b)} path
+    pc_big = pc.clone()
+    pc_big.view(-1)[0] = 100.0
+    kern_direct = timeit(lambda: nat.joint_weights(pc_big, pf, wo, bias))
+    del pc_big
     ref = timeit(torch_fwd)
     leaves = [t.clone().requires_grad_(True) for t in (pc, pf, wo, bias)]
     gW = torch.randn([B, T, C, R], device='cuda')
