@@ -1,22 +1,29 @@
-// lt_producer.hip -- the joint weight function's arc weights on the matrix
-// cores (first step: the producer, not yet inside the
-// recursions). JointWeightFn (weight_fns.py:174-227) computes, for every
-// frame row f = (b, t) and context state c,
+// lt_producer.hip -- the joint weight function's arc weights and their
+// gradients on the matrix cores (first half: the
+// producer as its own launches, not yet inside the recursions).
+// JointWeightFn (weight_fns.py:174-227) computes, for every frame row
+// f = (b, t) and context state c,
 //
 //   W[f, c, y] = bias[y] + sum_h Wo[y, h] * tanh(Pc[c, h] + Pf[f, h])
 //
 // with Pc = context_projection(context embeddings) [C, H], Pf =
-// blank_projection(frames) [rows, H] (both plain GEMMs, left to the caller)
+// frame_projection(frames) [rows, H] (both plain GEMMs, left to the caller)
 // and Wo / bias the stacked (blank, vocab) output projections [R = V+1, H].
 // PyTorch materialises the [rows, C, H] hidden tensor (4.3 GB fp32 at the
 // bench shape with H = 512); here each hidden tile is formed in registers
-// as the A operand of v_mfma_f32_32x32x16_bf16 and never leaves the CU.
+// as an operand of v_mfma_f32_32x32x16_bf16 and never leaves the CU.
 //
-// Tiling: the flattened (f, c) rows are cut into 32-row wave tiles; a wave
-// computes its tile against one or two 32-column tiles of y (R <= 64), K = H
-// in steps of 16. Wo lives in LDS as bf16 [R][H] (loaded once per
-// persistent workgroup). Hidden values and Wo are rounded to bf16, products
-// accumulate in fp32 (MI355X_MICROARCH.md: dense bf16 MFMA).
+// Kernels:
+//   joint_exp_kernel         e^{2 Pc} (and e^{2 Pf} for the row-tile form), the
+//                            |projection| > 40 flag
+//   joint_weights_fb_kernel  forward, one workgroup per 32-frame block, waves
+//                            walk the context states (the default)
+//   joint_weights_kernel     forward, 32 flattened (f, c) rows per wave tile
+//                            (blocks that exceed LDS)
+//   joint_backward_kernel    d_wo, d_pf, d_pc (+ bias) per 32-frame block
+//   joint_reduce_kernel      fixed-order sum of the per-workgroup partials
+// Wo and the hidden values enter the forward products as bf16; the backward
+// uses split-bf16 products; all sums are fp32.
 #include "lt_kernels.h"
 
 namespace {
