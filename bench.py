@@ -128,6 +128,42 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, chec
   return wall, fwd_ms, bwd_ms
 
 
+def joint_step_leg(T, U, V, n, device, B=64, F=256, H=512, reps=5):
+  """a whole training step of RecognitionLattice driven
+  by SharedEmbCacher + JointWeightFn (weight_fns.py:174-242) at the bench
+  lattice shape, with the matrix-core producer (lt_joint_weights / _backward)
+  and with the PyTorch hidden tensor; the lattice kernels are the same in
+  both (tools/joint_step_bench.py has the H sweep)."""
+  import last_torch_amd as lt
+  torch.manual_seed(0)
+  ctx = lt.contexts.FullNGram(vocab_size=V, context_size=n)
+  cacher = lt.weight_fns.SharedEmbCacher(num_context_states=V + 1, embedding_size=128,
+                                         device=device)
+  wfn = lt.weight_fns.JointWeightFn(vocab_size=V, hidden_size=H, device=device)
+  lat = lt.RecognitionLattice(context=ctx, alignment=lt.alignments.FrameDependent(),
+                              weight_fn_cacher_factory=lambda _: cacher,
+                              weight_fn_factory=lambda _: wfn)
+  frames = torch.randn([B, T, F], device=device)
+  nf = torch.full([B], T, device=device)
+  labels = torch.randint(1, V + 1, [B, U], device=device)
+  nl = torch.full([B], U, device=device)
+  out = {'batch': B, 'frames': T, 'labels': U, 'features': F, 'hidden': H}
+  for name, fused in (('producer', True), ('pytorch_hidden', False)):
+    wfn.fused = fused
+    for _ in range(3):
+      lat(frames=frames, num_frames=nf, labels=labels, num_labels=nl).sum().backward()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+    e0.record()
+    for _ in range(reps):
+      lat(frames=frames, num_frames=nf, labels=labels, num_labels=nl).sum().backward()
+    e1.record()
+    torch.cuda.synchronize()
+    out[f'{name}_ms_per_step'] = e0.elapsed_time(e1) / reps
+  out['speedup'] = out['pytorch_hidden_ms_per_step'] / out['producer_ms_per_step']
+  return out
+
+
 def cpu_baseline(T, U, V, n, C, sample_utts):
   """The C oracle (single-threaded restatement of the reference) on a
   bounded sample of the same workload: loss + dW for `sample_utts`
@@ -301,6 +337,8 @@ def main():
         'design': 'checkpoints' if ck2 else 'recursion',
     }
     del W2
+    torch.cuda.empty_cache()
+    result['joint_weight_fn_step'] = joint_step_leg(T, U, V, n, device)
 
   if rank == 0 and not dist_on and args.cpu_utts > 0:
     result['cpu_baseline'] = cpu_baseline(T, U, V, n, C, args.cpu_utts)
