@@ -462,6 +462,9 @@ __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a)
   // per buffer (bytes): fp32 [32][GS] | hi, lo [32][GB] | hi, lo [RB][TS]
   constexpr int BUFB = 4 * 32 * GS + 2 * 2 * 32 * GB + 2 * 2 * RB * TS;
   constexpr int nthr = 64 * NW, HW = 32 * NW;
+  // 8 waves share each staged g value: split it once at staging (PRE);
+  // smaller workgroups split in each wave instead (fewer staging stores)
+  constexpr bool PRE = NW == 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, R = a.R, C = a.C;
   // this workgroup's hidden columns: [h0, h0 + HW)
@@ -529,11 +532,13 @@ __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a)
           const unsigned short lo =
               __builtin_bit_cast(unsigned short, (__bf16)(v - __uint_as_float((unsigned)hi << 16)));
           gt[m * GS + r] = v;
-          gh[m * GB + r] = hi;
-          gl[m * GB + r] = lo;
-          if (r < RB) {
-            th[r * TS + m] = hi;
-            tl[r * TS + m] = lo;
+          if constexpr (PRE) {
+            gh[m * GB + r] = hi;
+            gl[m * GB + r] = lo;
+            if (r < RB) {
+              th[r * TS + m] = hi;
+              tl[r * TS + m] = lo;
+            }
           }
         }
       }
@@ -546,8 +551,16 @@ __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a)
       f32x16 gw = {};
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        const bf16x8 ah = *(const bf16x8*)(gh + col * GB + 16 * kb + 8 * half);
-        const bf16x8 al = *(const bf16x8*)(gl + col * GB + 16 * kb + 8 * half);
+        bf16x8 ah, al;
+        if constexpr (PRE) {
+          ah = *(const bf16x8*)(gh + col * GB + 16 * kb + 8 * half);
+          al = *(const bf16x8*)(gl + col * GB + 16 * kb + 8 * half);
+        } else {
+          const float4 x0 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half);
+          const float4 x1 = *(const float4*)(gt + col * GS + 16 * kb + 8 * half + 4);
+          const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          split8(v, ah, al);
+        }
         gw = mfma3(ah, al, woh[kb], wol[kb], gw);
       }
       float csum = 0.f;
@@ -570,10 +583,25 @@ __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a)
         // A[r][k slot (half, j)] = g[m][r], m = 16q + 4 half + (j & 3) + 8 (j >> 2):
         // two runs of 4 in the transposed tile
         const int tm = 16 * q + 4 * half;
-        dwo0 = mfma3(tpair(th + col * TS + tm), tpair(tl + col * TS + tm), hh, hlo, dwo0);
-        if (TWO)
-          dwo1 = mfma3(tpair(th + (32 + col) * TS + tm), tpair(tl + (32 + col) * TS + tm), hh,
-                       hlo, dwo1);
+        if constexpr (PRE) {
+          dwo0 = mfma3(tpair(th + col * TS + tm), tpair(tl + col * TS + tm), hh, hlo, dwo0);
+          if (TWO)
+            dwo1 = mfma3(tpair(th + (32 + col) * TS + tm), tpair(tl + (32 + col) * TS + tm), hh,
+                         hlo, dwo1);
+        } else {  // split in this wave (fewer staging stores for small workgroups)
+          float gv[8];
+          bf16x8 gh8, gl8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gv[j] = gt[(tm + (j & 3) + 8 * (j >> 2)) * GS + col];
+          split8(gv, gh8, gl8);
+          dwo0 = mfma3(gh8, gl8, hh, hlo, dwo0);
+          if (TWO) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gv[j] = gt[(tm + (j & 3) + 8 * (j >> 2)) * GS + 32 + col];
+            split8(gv, gh8, gl8);
+            dwo1 = mfma3(gh8, gl8, hh, hlo, dwo1);
+          }
+        }
       }
       csum += __shfl_xor(csum, 32);
       if (half == 0) dpc[c * HW + hl] += csum;  // this wave owns column hl

@@ -115,6 +115,7 @@ def test_empty_and_errors(cuda):
     ((2, 40), 33, 512, 33),   # bench hidden size: two workgroups per tile column
     ((37,), 3, 288 - 32, 16), # hidden 256 exactly, rows * C not a multiple of 32
     ((3, 11), 9, 320, 40),    # 2-wave workgroups over 5 column blocks, R in (32, 48]
+    ((3, 20), 33, 128, 33),   # 4-wave workgroups (g split in each wave)
 ])
 @pytest.mark.parametrize('path', ['kernel', 'torch'])
 def test_backward_vs_torch(cuda, lead, C, H, R, path):
