@@ -88,6 +88,18 @@ for s in $STEPS; do
       python tools/pmc_summary.py --fetch "$OUT/pmcr_fetch_$TAG" --write "$OUT/pmcr_write_$TAG" \
         --batch 64 --frames 1000 --out "$OUT/${TAG}_pmc_summary_recursion.json"
       ;;
+    producer)
+      echo "[gpu_round] joint weight function: producer bench, training step, kernel trace"
+      rm -rf "$OUT/prodprof_$TAG"
+      HS=128,512 timeout -k 10 300 python tools/producer_bench.py > "$OUT/producer_$TAG.jsonl" \
+        || { tail -20 "$OUT/producer_$TAG.jsonl"; exit 1; }
+      HS=128,512 timeout -k 10 300 python tools/joint_step_bench.py > "$OUT/joint_step_$TAG.jsonl" \
+        || { tail -20 "$OUT/joint_step_$TAG.jsonl"; exit 1; }
+      HS=512 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prodprof_$TAG" -o prod \
+        --output-format csv -- python3 tools/producer_bench.py > "$OUT/prodprof_$TAG.log" 2>&1 \
+        || { tail -40 "$OUT/prodprof_$TAG.log"; exit 1; }
+      cat "$OUT/producer_$TAG.jsonl" "$OUT/joint_step_$TAG.jsonl"
+      ;;
     *)
       echo "unknown step $s"; exit 2;;
   esac
