@@ -34,11 +34,15 @@ $(OBJ)/lt_table.o: $(CSRC)/lt_table.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+$(OBJ)/lt_chunk.o: $(CSRC)/lt_chunk.hip $(DEPS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
 $(OBJ)/lt_producer.o: $(CSRC)/lt_producer.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(INST_OBJS)
+$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(INST_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
 oracle:
@@ -62,6 +66,19 @@ $(STAMP_OBJ)/lt_lattice.o: $(CSRC)/lt_lattice.hip $(DEPS)
 $(STAMP_OBJ)/lt_pipe.o: $(CSRC)/lt_pipe.hip $(DEPS)
 	@mkdir -p $(STAMP_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -c -o $@ $<
-stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
+stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(STAMP_OBJ)/liblt_lattice_stamps.so $^
 .PHONY: stamps
+
+# Diagnostic build (role ablations behind LT_DIAG; never loaded unless
+# LT_LIB_PATH points at it): build/diag/liblt_lattice_diag.so
+DIAG_OBJ := build/diag
+$(DIAG_OBJ)/lt_inst_%.o: $(CSRC)/lt_inst.hip $(DEPS)
+	@mkdir -p $(DIAG_OBJ)
+	$(HIPCC) $(HIPFLAGS) -DLT_DIAG -DLT_LG=$(call lg_of,$*) -DLT_LGN=$(call lgn_of,$*) -DLT_P=$(call p_of,$*) -c -o $@ $<
+$(DIAG_OBJ)/%.o: $(CSRC)/%.hip $(DEPS)
+	@mkdir -p $(DIAG_OBJ)
+	$(HIPCC) $(HIPFLAGS) -DLT_DIAG -c -o $@ $<
+diag: $(DIAG_OBJ)/lt_lattice.o $(DIAG_OBJ)/lt_pipe.o $(DIAG_OBJ)/lt_chunk.o $(DIAG_OBJ)/lt_table.o $(DIAG_OBJ)/lt_producer.o $(foreach v,$(VARIANTS),$(DIAG_OBJ)/lt_inst_$(v).o)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(DIAG_OBJ)/liblt_lattice_diag.so $^
+.PHONY: diag

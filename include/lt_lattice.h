@@ -164,6 +164,34 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
 int lt_scale_grad(const lt_problem* pb, const float* grad, void* dW,
                   void* stream);
 
+/* The bigram loss as a chunked two-level scan (lt_chunk.hip): FullNGram
+ * n = 1, 1 <= vocab_size <= 32, max_labels <= 124, Log semiring. Each
+ * utterance is cut into chunks of L frames (L from the LDS budget, 14 for
+ * V = 32 fp32); the serial chain is L + T/L steps instead of T.
+ *   lt_chunk_forward  = RecognitionLattice.forward (lattices.py:131-183):
+ *     loss [B] (log_z, num [B] nullable outputs); keeps the alpha / beta
+ *     values at every chunk boundary in `state`.
+ *   lt_chunk_backward = its gradient (alignments.py:300-318 composed in
+ *     reverse, D1-D4 in the reference): dW = grad[b] * (den - num marginals)
+ *     (grad nullable = ones), from `state` and W alone.
+ * `state` must live from the forward to the backward; `scratch` only during
+ * each call. Utterances with a frame whose weights are not all finite or
+ * span more than 60 (max - min) run through the frame-serial kernels inside
+ * the same calls (same results, slower). Sizes from
+ * lt_chunk_workspace_bytes(); both buffers 16-byte aligned.
+ * lt_loss_grad uses these two calls for every shape they take. */
+int lt_chunk_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_t* state_bytes,
+                             size_t* scratch_bytes);
+int lt_chunk_forward(const lt_problem* pb, int32_t local_norm, const void* W,
+                     const int32_t* num_frames, const int32_t* labels,
+                     const int32_t* num_labels, float* loss, float* log_z, float* num,
+                     void* state, size_t state_bytes, void* scratch, size_t scratch_bytes,
+                     void* stream);
+int lt_chunk_backward(const lt_problem* pb, int32_t local_norm, const void* W,
+                      const int32_t* num_frames, const int32_t* labels,
+                      const int32_t* num_labels, const float* grad, void* dW, void* state,
+                      size_t state_bytes, void* scratch, size_t scratch_bytes, void* stream);
+
 /* RecognitionLattice.shortest_path (lattices.py:185-247) without the
  * cross-batch mask aliasing (D6): MaxTropical Viterbi with the reference's
  * tie rules (blank wins ties, semirings.py:363; first argmax among lexical

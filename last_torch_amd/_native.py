@@ -12,7 +12,9 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'liblt_lattice.so')
+# LT_LIB_PATH: a diagnostic build of the same library (make diag); never set
+# in normal use
+LIB_PATH = os.environ.get('LT_LIB_PATH') or os.path.join(_HERE, 'liblt_lattice.so')
 
 LT_DTYPE_F32, LT_DTYPE_BF16 = 0, 1
 SEMIRING_LOG, SEMIRING_MAX, SEMIRING_REAL = 0, 1, 2
@@ -61,6 +63,12 @@ _SIG = {
                                      ctypes.POINTER(ctypes.c_size_t)],
     'lt_loss_grad': [ctypes.POINTER(Problem), _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
     'lt_scale_grad': [ctypes.POINTER(Problem), _P, _P, _P],
+    'lt_chunk_workspace_bytes': [ctypes.POINTER(Problem), _I32, ctypes.POINTER(ctypes.c_size_t),
+                                 ctypes.POINTER(ctypes.c_size_t)],
+    'lt_chunk_forward': [ctypes.POINTER(Problem), _I32] + [_P] * 8 + [ctypes.c_size_t, _P,
+                                                                    ctypes.c_size_t, _P],
+    'lt_chunk_backward': [ctypes.POINTER(Problem), _I32] + [_P] * 7 + [ctypes.c_size_t, _P,
+                                                                     ctypes.c_size_t, _P],
     'lt_graph_in_arcs': [_I32, _I32, _P, _P, _P],
     'lt_table_forward': [_G, _TP, _I32, _P, _P, _P, _P, _P],
     'lt_table_num_forward': [_G, _TP, _I32, _P, _P, _P, _P, _P, _P],
@@ -263,10 +271,23 @@ def loss_backward(W, num_frames, labels, num_labels, log_z, num, alpha, alpha_nu
   return dW
 
 
+def chunk_path(batch, frames, labels, vocab_size, context_size):
+  """Whether lt_loss_grad runs the chunked two-level scan (lt_chunk.hip) for
+  this shape; mirrors lt_impl::chunk_eligible. LT_CHUNK=0 turns it off."""
+  if os.environ.get('LT_CHUNK', '1') == '0':
+    return False
+  if context_size != 1 or not 1 <= vocab_size <= 32 or labels + 1 > 128 or frames < 1:
+    return False
+  C = vocab_size + 1
+  return batch * frames * C * C < 2 ** 31
+
+
 def fused_path(batch, frames, labels, vocab_size, context_size, device=None, bf16=False):
-  """Whether lt_loss_grad runs as ONE fused launch for this shape (mirrors
-  lt_loss_grad: checkpointing batch size, 2B below the CU count, pipe shape;
-  LT_FUSED=0/1 forces the choice)."""
+  """Whether lt_loss_grad runs as ONE fused pipe launch for this shape
+  (mirrors lt_loss_grad: not the chunked path, checkpointing batch size, 2B
+  below the CU count, pipe shape; LT_FUSED=0/1 forces the choice)."""
+  if chunk_path(batch, frames, labels, vocab_size, context_size):
+    return False
   cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
   env = os.environ.get('LT_FUSED', '')
   want = (env != '0') if env else 2 * batch < cus
@@ -305,6 +326,49 @@ def loss_grad(W, num_frames, labels, num_labels, vocab_size, context_size, local
                             _ptr(dW), _ptr(workspace), workspace.numel(), _stream()),
          'lt_loss_grad')
   return loss, log_z, num, dW
+
+
+def chunk_workspace_bytes(W, vocab_size, context_size, max_labels, local_norm):
+  """(state_bytes, scratch_bytes) of lt_chunk_forward / lt_chunk_backward."""
+  pb = _problem(W, vocab_size, context_size, max_labels)
+  st, sc = ctypes.c_size_t(0), ctypes.c_size_t(0)
+  _check(lib().lt_chunk_workspace_bytes(ctypes.byref(pb), int(bool(local_norm)), ctypes.byref(st),
+                                        ctypes.byref(sc)), 'lt_chunk_workspace_bytes')
+  return st.value, sc.value
+
+
+def chunk_forward(W, num_frames, labels, num_labels, vocab_size, context_size, local_norm):
+  """lt_chunk_forward: (loss, log_z, num, state); `state` (uint8 device
+  tensor) carries the chunk-boundary values to chunk_backward. The scratch
+  buffer lives only for the call."""
+  U = labels.shape[-1]
+  pb = _problem(W, vocab_size, context_size, U)
+  B = W.shape[0]
+  st, sc = chunk_workspace_bytes(W, vocab_size, context_size, U, local_norm)
+  state = torch.empty([max(st, 16)], dtype=torch.uint8, device=W.device)
+  scratch = torch.empty([max(sc, 16)], dtype=torch.uint8, device=W.device)
+  loss, log_z, num = _f32([B], W), _f32([B], W), _f32([B], W)
+  _check(lib().lt_chunk_forward(ctypes.byref(pb), int(bool(local_norm)), _ptr(W), _ptr(num_frames),
+                                _ptr(labels), _ptr(num_labels), _ptr(loss), _ptr(log_z), _ptr(num),
+                                _ptr(state), st, _ptr(scratch), sc, _stream()), 'lt_chunk_forward')
+  return loss, log_z, num, state
+
+
+def chunk_backward(W, num_frames, labels, num_labels, vocab_size, context_size, local_norm, state,
+                   grad=None):
+  """lt_chunk_backward: dW = grad[b] * d loss_b / dW (grad None = ones) from
+  the forward's `state`."""
+  U = labels.shape[-1]
+  pb = _problem(W, vocab_size, context_size, U)
+  st, sc = chunk_workspace_bytes(W, vocab_size, context_size, U, local_norm)
+  scratch = torch.empty([max(sc, 16)], dtype=torch.uint8, device=W.device)
+  dW = torch.empty_like(W)
+  g = None if grad is None else grad.float().contiguous()
+  _check(lib().lt_chunk_backward(ctypes.byref(pb), int(bool(local_norm)), _ptr(W),
+                                 _ptr(num_frames), _ptr(labels), _ptr(num_labels), _ptr(g),
+                                 _ptr(dW), _ptr(state), st, _ptr(scratch), sc, _stream()),
+         'lt_chunk_backward')
+  return dW
 
 
 def grad_workspace_errors(workspace, W, vocab_size, context_size, max_labels, local_norm):

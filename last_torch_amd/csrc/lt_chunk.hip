@@ -1,0 +1,1296 @@
+// lt_chunk.hip -- chunked-time two-level scan for the bigram Log lattice
+// (FullNGram n = 1, V <= 32, FrameDependent): loss and d(loss)/dW with
+// every utterance split into K chunks of L frames, so the serial chain per
+// utterance is L + K steps instead of T.
+//
+// Reference (last_torch/): the denominator recursion lattices.py:379-496
+// with FrameDependent.forward (alignments.py:286-297) and FullNGram
+// forward_reduce (contexts.py:207-230); the backward / marginals of
+// alignments.py:300-318 composed in reverse frame order (lattices.py:686-799,
+// defect D4 fixed); the numerator lattices.py:250-377 with
+// FrameDependent.string_forward (alignments.py:320-329); the loss
+// lattices.py:131-183. Log semiring semirings.py:184-305 (safe max).
+//
+// Bigram structure (contexts.py:190-205): next(p, y) = y for y >= 1, the
+// blank arc (y = 0) loops. States 1..V form a dense V x V "core"; state 0
+// (the start) has only its blank self loop as in-arc. So one frame is the
+// block matrix  M_t = [[w00, w0.], [0, Mc_t]]  in the log semiring, with
+// Mc_t[p][q] = W[p][q] (+) (p == q ? W[p][0] : zero).
+//
+// Three launches (one call of lt_loss_grad):
+//   A  ck_transfer_kernel  one wave per chunk: the chunk's transfer matrix
+//      P_k = M_{t0} ... M_{t1-1} in scaled linear space. The 32 x 32 core
+//      product runs on the matrix cores (v_mfma_f32_32x32x2_f32: exact f32
+//      FMA chains) as X <- E_t^T X with X = P^T, one column scale per start
+//      state; the state-0 row and the state-0 self loop on the side. Also
+//      gathers the numerator's two arc weights per string position and
+//      frame into G (the string lattice reads nothing else of W).
+//   B  ck_combine_kernel   one workgroup per utterance: the den alpha / beta
+//      vectors at every chunk boundary (K steps of a 33 x 33 log-semiring
+//      vector-matrix product each), the numerator alpha / beta over all
+//      frames from G (log space, exact per position) with the values at the
+//      chunk boundaries kept; log_z, num, loss.
+//   C  ck_marg_kernel      one workgroup per chunk: the chunk's W staged in
+//      LDS once; local den / num alpha and beta recursions from the
+//      boundary values (four waves side by side), then the arc marginals of
+//      every frame, normalised by the frame's own total (= Z up to
+//      rounding), den minus num, times the incoming gradient -> dW.
+// HBM traffic: W is read twice (A and C) and dW written once, plus G and the
+// chunk records (~10 % of W) -- the SURVEY 8(d) accounting.
+//
+// Exactness of the scaled linear spaces: with every weight of a frame finite
+// and max - min <= kRange (checked per frame in A; utterances that fail go
+// to the frame-serial kernels), every core state reaches every core state in
+// one frame with a weight within e^kRange of any other, so a value that
+// underflows relative to its vector's max (< 2^-126) carries a marginal below
+// e^(kRange - 87): nothing the tolerance can see. The start state, whose
+// alpha/beta can drift arbitrarily far from the core's, is kept in log space
+// throughout.
+#include "lt_kernels.h"
+
+namespace {
+
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+constexpr float kRange = 60.f;  // max - min of a frame's weights on the fast path
+constexpr int kRec = 1224;      // floats per chunk record (16-byte multiple)
+constexpr int kRowT = 36;       // row stride of the transposed core in a record
+// record layout (floats): [0, 1152) X^T rows: rec[i * 36 + j] = X[i][j] =
+// P_scaled[j][i] (start core state j -> end core state i); [1152, 1184)
+// per-start-state (column) power-of-two scales ej (int); [1184, 1216) the
+// state-0 row rt[i]; 1216 rho (int, log2 scale of rt); 1217 pi (log of
+// P00 relative to csum); 1218 csum (sum of the frames' offsets c_t);
+// 1219 flag (range violation); 1220 live frames.
+constexpr int kRecEj = 1152, kRecRt = 1184, kRecRho = 1216, kRecPi = 1217, kRecCs = 1218,
+              kRecFlag = 1219, kRecN = 1220;
+
+struct CkArgs {
+  const unsigned char* W;  // [B,T,C,R] fp32 / bf16
+  const int* nfr;
+  const int* labels;       // [B,U]
+  const int* nlab;
+  const float* grad;       // [B] nullable (ones)
+  float* rec;              // [B*K][kRec]
+  float* G;                // [B,T,NPG,2] numerator arc weights (log)
+  int* uflag;              // [B] 1: utterance goes to the frame-serial kernels
+  float* abd;              // [B,K+1,CP] den alpha at chunk starts (log)
+  float* bbd;              // [B,K+1,CP] den beta at chunk starts
+  float* nabd;             // [B,K+1,NPG] num alpha at chunk starts
+  float* nbbd;             // [B,K+1,NPG] num beta at chunk starts
+  float* loss;
+  float* log_z;            // state copies (read by C)
+  float* num;
+  float* lz_out;           // the caller's, nullable
+  float* num_out;
+  void* dW;
+  int B, T, U, V, C, R, FR, NP, NPG, PPL, CP;
+  int L, K;                // frames per chunk, chunks per utterance
+  int local;               // LocallyNormalizedWeightFn: no denominator
+  int dbg;                 // diagnostic builds (LT_DIAG) only: role ablations
+  long long FB;            // bytes per frame
+  // phase A per-wave LDS carve
+  int a_slots, a_ni, a_slot_bytes, a_wave_bytes, a_off_rt, a_off_tab;
+  // phase B LDS carve
+  int b_ni, b_slots, b_off_ra, b_off_rb, b_off_ga, b_off_gb, b_gslots, b_gslot, b_off_buf;
+  // phase C LDS carve
+  int c_ni, c_off_ad, c_off_bd, c_off_an, c_off_bn, c_off_tab, c_off_buf, c_off_fb;
+};
+
+LT_DEVINL float wmax(float v) {
+  v = fmaxf(v, xchg<0>(v));
+  v = fmaxf(v, xchg<1>(v));
+  v = fmaxf(v, xchg<2>(v));
+  v = fmaxf(v, xchg<3>(v));
+  v = fmaxf(v, xchg<4>(v));
+  v = fmaxf(v, xchg<5>(v));
+  return v;
+}
+LT_DEVINL float wmin(float v) {
+  v = fminf(v, xchg<0>(v));
+  v = fminf(v, xchg<1>(v));
+  v = fminf(v, xchg<2>(v));
+  v = fminf(v, xchg<3>(v));
+  v = fminf(v, xchg<4>(v));
+  v = fminf(v, xchg<5>(v));
+  return v;
+}
+LT_DEVINL float wsum(float v) {
+  v += xchg<0>(v);
+  v += xchg<1>(v);
+  v += xchg<2>(v);
+  v += xchg<3>(v);
+  v += xchg<4>(v);
+  v += xchg<5>(v);
+  return v;
+}
+// lanes l and l ^ 32 combined (v_permlane32_swap: both halves get both)
+LT_DEVINL float half_sum(float v) {
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(p[0]) + __int_as_float(p[1]);
+}
+LT_DEVINL float half_max(float v) {
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
+}
+// lane l gets v of lane l-1 (lane 0: fill)
+LT_DEVINL float from_prev(float v, float fill) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(__float_as_int(fill), __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+// lane 0 gets lane 63 (rotate right by one)
+LT_DEVINL float rot_prev(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x13C, 0xF, 0xF, false));
+}
+LT_DEVINL float rot_next(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xF, 0xF, false));
+}
+
+// Log-semiring plus of two terms, semirings.py:248-255 (non-finite max -> 0)
+LT_DEVINL float lse2(float a, float b) {
+  float c = fmaxf(a, b);
+  c = __builtin_isfinite(c) ? c : 0.f;
+  return c + lt_log(lt_exp(a - c) + lt_exp(b - c));
+}
+LT_DEVINL float safe_max(float m) { return __builtin_isfinite(m) ? m : 0.f; }
+// lane 0's float (readfirstlane is an int builtin: never pass it a float)
+LT_DEVINL float first_lane(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// k index of k-step s in lane half h (the rows register s of the 32x32
+// accumulator holds in that half): the MFMA's K order is free, so the
+// accumulator feeds the next product's B operand with no data movement
+LT_DEVINL int kstep(int s, int h) { return (s & 3) + 8 * (s >> 2) + 4 * h; }
+
+template <bool BF16>
+LT_DEVINL float ldsw(const unsigned char* fr, int e) {
+  if constexpr (BF16) return __uint_as_float(((unsigned)((const unsigned short*)fr)[e]) << 16);
+  else return ((const float*)fr)[e];
+}
+
+// LDS-DMA of `bytes` bytes at global byte offset `off` of `base` into LDS at
+// `lds_addr` (1 KiB per wave instruction, `ni` instructions; the copy starts
+// at the 16-byte granule holding `off`: the data sits at lds + (off & 15)).
+// Lanes past the end re-load the last granule into the slack.
+LT_DEVINL void dma_issue(const unsigned char* base, long long off, long long bytes,
+                         unsigned lds_addr, int ni, int lane, int wave0 = 0, int nwaves = 1) {
+  const long long a0 = off & ~15LL;
+  const int n16 = (int)((off + bytes - a0 + 15) >> 4);
+  for (int i = wave0; i < ni; i += nwaves) {
+    int g = lane + 64 * i;
+    g = g < n16 ? g : n16 - 1;
+    glds16(base + a0 + 16LL * g, lds_addr + 1024u * i);
+  }
+}
+
+// wave-uniform max / sum over all 64 lanes with DPP only (no LDS round trip):
+// butterflies inside each row of 16, then row_bcast:15 / row_bcast:31 fold
+// rows 0-1 into 2-3, and lane 63 holds the total
+template <bool MAX>
+LT_DEVINL float wred(float v) {
+  auto op = [](float x, float y) { return MAX ? fmaxf(x, y) : x + y; };
+  v = op(v, xchg<0>(v));
+  v = op(v, xchg<1>(v));
+  v = op(v, xchg<2>(v));
+  v = op(v, xchg<3>(v));
+  const float r15 = __int_as_float(__builtin_amdgcn_update_dpp(
+      MAX ? __float_as_int(v) : 0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+  v = op(v, r15);
+  const float r31 = __int_as_float(__builtin_amdgcn_update_dpp(
+      MAX ? __float_as_int(v) : 0, __float_as_int(v), 0x143, 0xC, 0xF, false));
+  v = op(v, r31);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+LT_DEVINL float wmax_u(float v) { return wred<true>(v); }
+LT_DEVINL float wsum_u(float v) { return wred<false>(v); }
+
+template <bool BF16>
+LT_DEVINL float ldg(const unsigned char* base, long long e) {
+  if constexpr (BF16) return __uint_as_float(((unsigned)((const unsigned short*)base)[e]) << 16);
+  else return ((const float*)base)[e];
+}
+
+// Numerator gather offsets of string position u (contexts.py:109-146
+// walk_states, lattices.py:314-338, bigram next(p, y) = y): boff = element of
+// a frame holding the blank weight of position u (state ctx_u = last valid
+// label before u, 0 if none), loff = element holding the weight of the arc
+// into u (from ctx_{u-1} with label y_u; epsilon / out-of-range labels read
+// label 1, make_safe_classes), -1 for u = 0 or u past the string. `lab` is
+// the utterance's labels staged in LDS.
+LT_DEVINL void string_offsets(const CkArgs& a, const int* lab, int u, int* boff, int* loff) {
+  auto valid = [&](int y) { return y >= 1 && y <= a.V; };
+  int ctx = 0, pc = 0;
+  int j = min(u, a.U) - 1;
+  for (; j >= 0; --j)
+    if (valid(lab[j])) { ctx = lab[j]; break; }
+  // ctx_{u-1}: the same scan one position earlier
+  if (u >= 1) {
+    if (j == u - 1) {  // label u-1 itself was the last valid one
+      for (int i = u - 2; i >= 0; --i)
+        if (valid(lab[i])) { pc = lab[i]; break; }
+    } else {
+      pc = ctx;
+    }
+  }
+  *boff = u < a.NP ? ctx * a.R : -1;
+  if (u == 0 || u >= a.NP) {
+    *loff = -1;
+  } else {
+    const int y = lab[u - 1];
+    *loff = pc * a.R + (valid(y) ? y : 1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// A: chunk transfer matrices (one wave per chunk). Frame data is loaded
+// straight into registers two frames ahead (the compiler's own waits).
+// ---------------------------------------------------------------------------
+template <bool BF16, int PPL>
+struct FrameRegs {
+  float w[16];      // W[k+1][i+1] for the lane's 16 k-steps
+  float wr0;        // W[0][i+1]
+  float wbl;        // W[lane][0]   (the blank column, lanes <= V)
+  float wdg;        // W[i+1][0]
+  float w00;        // W[0][0]
+  float gb[PPL], gl[PPL];  // numerator arc weights of the lane's positions
+};
+
+// Every lane issues every load (indices clamped into the frame, the unused
+// values replaced afterwards): no load sits under a branch, so the
+// compiler's vmcnt bookkeeping across the prefetch stays exact.
+template <bool BF16, int PPL>
+LT_DEVINL void load_frame(const CkArgs& a, const unsigned char* Wf, int lane, const int* boff,
+                          const int* loff, FrameRegs<BF16, PPL>& f) {
+  const int V = a.V, R = a.R, i = lane & 31, h = lane >> 5;
+  const int ic = min(i, V - 1);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int kk = min(kstep(s, h), V - 1);
+    f.w[s] = ldg<BF16>(Wf, (kk + 1) * R + ic + 1);
+  }
+  f.wr0 = ldg<BF16>(Wf, ic + 1);
+  f.wbl = ldg<BF16>(Wf, min(lane, V) * R);
+  f.wdg = ldg<BF16>(Wf, (ic + 1) * R);
+  f.w00 = ldg<BF16>(Wf, 0);
+#pragma unroll
+  for (int r = 0; r < PPL; ++r) {
+    f.gb[r] = ldg<BF16>(Wf, max(boff[r], 0));
+    f.gl[r] = ldg<BF16>(Wf, max(loff[r], 0));
+  }
+}
+// the values load_frame read for nothing
+template <bool BF16, int PPL>
+LT_DEVINL void mask_frame(int V, int lane, const int* boff, const int* loff,
+                          FrameRegs<BF16, PPL>& f) {
+  const int i = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+    if (!(kstep(s, h) < V && i < V)) f.w[s] = -kInf;
+  if (i >= V) { f.wr0 = -kInf; f.wdg = -kInf; }
+  if (lane > V) f.wbl = -kInf;
+#pragma unroll
+  for (int r = 0; r < PPL; ++r) {
+    if (boff[r] < 0) f.gb[r] = -kInf;
+    if (loff[r] < 0) f.gl[r] = -kInf;
+  }
+}
+
+template <bool BF16, int PPL>
+__global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_rt[4][32];
+  __shared__ int s_lab[4][128];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int id = blockIdx.x * 4 + wave;
+  if (id >= a.B * a.K) return;  // no workgroup barrier in this kernel
+  const int b = id / a.K, k = id - (id / a.K) * a.K;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int t0 = k * a.L;
+  const int t1 = min(t0 + a.L, nf);
+  if (t0 >= t1) return;  // no live frame: phase B never reads this record
+  const int V = a.V, NPG = a.NPG;
+  const int i = lane & 31, h = lane >> 5;
+  const int nt = t1 - t0;
+  float* rt = s_rt[wave];
+  int* lab = s_lab[wave];
+  for (int j = lane; j < a.U; j += 64) lab[j] = a.labels[(long long)b * a.U + j];
+  if (lane < 32) rt[lane] = 0.f;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  int boff[PPL], loff[PPL];
+#pragma unroll
+  for (int r = 0; r < PPL; ++r) {
+    const int u = lane + 64 * r;
+    boff[r] = -1;
+    loff[r] = -1;
+    if (u < NPG) string_offsets(a, lab, u, &boff[r], &loff[r]);
+  }
+  const long long es = BF16 ? 2 : 4;
+  const unsigned char* W0 = a.W + ((long long)b * a.T + t0) * a.FR * es;
+
+  v16f X;  // X = P^T, column j (lane & 31) = start state j+1; identity
+#pragma unroll
+  for (int r = 0; r < 16; ++r) X[r] = (kstep(r, h) == i && i < V) ? 1.f : 0.f;
+  int ej = 0;         // column power-of-two scale (lane's column)
+  int rho = -100000;  // rt scale (log2)
+  float pi = 0.f;     // log P00 - csum
+  float csum = 0.f;   // sum of c_t (integers)
+  int bad = 0;
+
+  // frames in registers two ahead; the loads are unconditional (clamped to
+  // the chunk's last frame) so the compiler's vmcnt tracking stays exact
+  FrameRegs<BF16, PPL> fr[2];
+  auto frame_ptr = [&](int f) { return W0 + (long long)min(f, nt - 1) * a.FR * es; };
+  auto step = [&](FrameRegs<BF16, PPL>& F, int f, bool reload) {
+    const int t = t0 + f;
+    mask_frame(V, lane, boff, loff, F);
+    // numerator arc weights of this frame -> G
+    float2* grow = (float2*)(a.G + ((long long)b * a.T + t) * NPG * 2);
+#pragma unroll
+    for (int r = 0; r < PPL; ++r) {
+      const int u = lane + 64 * r;
+      if (u < NPG) grow[u] = make_float2(F.gb[r], F.gl[r]);
+    }
+    // the frame's range (every weight finite, max - min <= kRange)
+    float mx = -kInf, mn = kInf;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int kk = kstep(s, h);
+      if (kk < V && i < V) { mx = fmaxf(mx, F.w[s]); mn = fminf(mn, F.w[s]); }
+    }
+    if (i < V) { mx = fmaxf(mx, F.wr0); mn = fminf(mn, F.wr0); }
+    if (lane <= V) { mx = fmaxf(mx, F.wbl); mn = fminf(mn, F.wbl); }
+    mx = wmax_u(mx);
+    mn = -wmax_u(-mn);
+    if (!(mx - mn <= kRange) || !__builtin_isfinite(mx) || !__builtin_isfinite(mn)) bad = 1;
+    const float c = __builtin_isfinite(mx) ? ceilf(mx) : 0.f;
+    const float cl = c * kLog2e;
+    // E_t^T as the A operand: lane (i, h), k-step s -> E[k][i]; the core
+    // diagonal also carries the blank self loop (alignments.py:294-297)
+    const float dgv = lt_exp_off(F.wdg, cl);
+    float A[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int kk = kstep(s, h);
+      float e = (kk < V && i < V) ? lt_exp_off(F.w[s], cl) : 0.f;
+      if (kk == i && i < V) e += dgv;
+      A[s] = e;
+    }
+    const float e0 = i < V ? lt_exp_off(F.wr0, cl) : 0.f;
+    const float w00 = F.w00;
+    if (reload) load_frame(a, frame_ptr(f + 2), lane, boff, loff, F);
+
+    // state-0 row: r' = p00 * e0 + r Ec (VALU, beside the MFMAs)
+    {
+      float part = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 r4 = *(const float4*)(rt + 8 * g + 4 * h);
+        part = __builtin_fmaf(A[4 * g + 0], r4.x, part);
+        part = __builtin_fmaf(A[4 * g + 1], r4.y, part);
+        part = __builtin_fmaf(A[4 * g + 2], r4.z, part);
+        part = __builtin_fmaf(A[4 * g + 3], r4.w, part);
+      }
+      const float y = half_sum(part);
+      const float lam = pi * kLog2e;
+      const int B0 = max(rho, (int)floorf(lam));
+      float nr = ldexpf(y, max(rho - B0, -200)) + e0 * __builtin_amdgcn_exp2f(lam - (float)B0);
+      nr = i < V ? nr : 0.f;
+      const float m = wmax_u(nr);
+      int e;
+      frexpf(m, &e);
+      e = m > 0.f ? e : 0;
+      nr = ldexpf(nr, -e);
+      rho = B0 + e;
+      if (lane < 32) rt[lane] = nr;
+    }
+    pi += w00 - c;
+    csum += c;
+
+    // core: X <- E^T X on the matrix cores (exact f32 FMA chains)
+    v16f D = {};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) D = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], X[s], D, 0, 0, 0);
+    float cm = 0.f;  // one power-of-two scale per column (start state)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cm = fmaxf(cm, D[r]);
+    cm = half_max(cm);
+    int e;
+    frexpf(cm, &e);
+    e = cm > 0.f ? e : 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) X[r] = ldexpf(D[r], -e);
+    ej += e;
+  };
+  load_frame(a, frame_ptr(0), lane, boff, loff, fr[0]);
+  load_frame(a, frame_ptr(1), lane, boff, loff, fr[1]);
+  const int nmain = nt & ~1;
+  for (int f0 = 0; f0 < nmain; f0 += 2) {
+    step(fr[0], f0, true);
+    step(fr[1], f0 + 1, true);
+  }
+  if (nt & 1) step(fr[0], nt - 1, false);
+
+  float* rec = a.rec + (long long)id * kRec;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) rec[kstep(r, h) * kRowT + i] = X[r];
+  if (lane < 32) {
+    ((int*)rec)[kRecEj + lane] = ej;
+    rec[kRecRt + lane] = rt[lane];
+  }
+  bad = __builtin_amdgcn_readfirstlane(bad);
+  if (lane == 0) {
+    ((int*)rec)[kRecRho] = rho;
+    rec[kRecPi] = pi;
+    rec[kRecCs] = csum;
+    ((int*)rec)[kRecFlag] = bad;
+    ((int*)rec)[kRecN] = nt;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// B: chunk boundaries (one workgroup per utterance, 4 waves). Records and
+// numerator rows are prefetched into registers (the compiler's own waits).
+// ---------------------------------------------------------------------------
+struct RecAlpha {  // what lane i (< 32) needs of one record for the alpha step
+  float4 x[8];     // X[i][0..31]
+  float rt, sc;    // rt[i]; the source-row scale of lane p (rho or ej[p-1], x ln2)
+  float pi, cs;
+};
+LT_DEVINL void load_rec_alpha(const float* rc, int lane, int V, RecAlpha& r) {
+  // unconditional loads (lanes >= 32 re-read row lane & 31): exact vmcnt
+#pragma unroll
+  for (int g = 0; g < 8; ++g) r.x[g] = *(const float4*)(rc + (lane & 31) * kRowT + 4 * g);
+  r.rt = rc[kRecRt + (lane & 31)];
+  const int si = lane == 0 ? kRecRho : kRecEj + min(lane, 32) - 1;
+  const int sc = ((const int*)rc)[si];
+  r.sc = lane <= V ? (float)sc * 0.6931471805599453f : 0.f;
+  r.pi = rc[kRecPi];
+  r.cs = rc[kRecCs];
+}
+struct RecBeta {   // lane (j, h): the rows of half h of column j
+  float x[16];
+  float rt, ej;    // rt[lane & 31], ej[j] x ln2
+  float rho, pi, cs;
+};
+LT_DEVINL void load_rec_beta(const float* rc, int lane, RecBeta& r) {
+  const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r.x[4 * g + q] = rc[(8 * g + 4 * h + q) * kRowT + j];
+  r.rt = rc[kRecRt + j];
+  r.ej = (float)((const int*)rc)[kRecEj + j] * 0.6931471805599453f;
+  r.rho = (float)((const int*)rc)[kRecRho] * 0.6931471805599453f;
+  r.pi = rc[kRecPi];
+  r.cs = rc[kRecCs];
+}
+
+// log-space plus in base-2 units: m + log2(1 + 2^(n - m)); both operands
+// -inf gives -inf (the clamp turns the NaN of -inf - -inf into -200)
+LT_DEVINL float lse2_b2(float x, float y) {
+  const float m = fmaxf(x, y), n = fminf(x, y);
+  return m + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(fmaxf(n - m, -200.f)));
+}
+
+template <int PPL>
+__global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_bc[2][64];
+  __shared__ int s_bad;
+  __shared__ float s_lz, s_num;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int Kl = (nf + a.L - 1) / a.L;  // live chunks
+  const int V = a.V, C = a.C, CP = a.CP, NPG = a.NPG;
+  const int nl = a.nlab[b];
+  const float* rec0 = a.rec + (long long)b * a.K * kRec;
+  constexpr float kLn2 = 0.6931471805599453f;
+
+  // any chunk out of the fast path's range (a weight not finite, or a frame
+  // spanning more than kRange): the frame-serial kernels take the utterance
+  if (threadIdx.x == 0) s_bad = 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < Kl; k += blockDim.x)
+    if (((const int*)(rec0 + (long long)k * kRec))[kRecFlag]) s_bad = 1;
+  __syncthreads();
+  if (s_bad) {
+    if (threadIdx.x == 0) a.uflag[b] = 1;
+    return;
+  }
+  if (threadIdx.x == 0) a.uflag[b] = 0;
+
+  if (wave == 0 && !a.local && !(a.dbg & 1)) {
+    // ---- den alpha across chunks (lattices.py:379-496 in chunk steps)
+    float* bc = s_bc[0];  // bc[j] = a_{j+1} (core source j), bc[32] = a_0
+    float al = lane == 0 ? 0.f : -kInf;  // lane p: alpha[p]
+    float* dst = a.abd + (long long)b * (a.K + 1) * CP;
+    if (lane < C) dst[lane] = al;
+    RecAlpha rr[2];
+    auto rec_ptr = [&](int k) { return rec0 + (long long)min(k, Kl - 1) * kRec; };
+    auto step = [&](RecAlpha& R, int k, bool reload) {
+      const float x = lane < C ? al + R.sc : -kInf;
+      const float M = safe_max(wmax_u(x));
+      const float av = lane < C ? lt_exp(x - M) : 0.f;
+      if (lane >= 1 && lane <= 32) bc[lane - 1] = av;
+      if (lane == 0) bc[32] = av;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; g += 2) {
+        const float4 a0 = *(const float4*)(bc + 4 * g);
+        const float4 a1 = *(const float4*)(bc + 4 * g + 4);
+        s0 = __builtin_fmaf(R.x[g].x, a0.x, s0);
+        s1 = __builtin_fmaf(R.x[g + 1].x, a1.x, s1);
+        s0 = __builtin_fmaf(R.x[g].y, a0.y, s0);
+        s1 = __builtin_fmaf(R.x[g + 1].y, a1.y, s1);
+        s0 = __builtin_fmaf(R.x[g].z, a0.z, s0);
+        s1 = __builtin_fmaf(R.x[g + 1].z, a1.z, s1);
+        s0 = __builtin_fmaf(R.x[g].w, a0.w, s0);
+        s1 = __builtin_fmaf(R.x[g + 1].w, a1.w, s1);
+      }
+      s0 = __builtin_fmaf(R.rt, bc[32], s0);
+      const float nq = M + R.cs + lt_log(s0 + s1);  // lane i < 32: alpha'[i+1]
+      const float n0 = first_lane(al) + R.pi + R.cs;
+      const float sh = from_prev(nq, -kInf);
+      al = lane == 0 ? n0 : (lane < C ? sh : -kInf);
+      if (lane < C) dst[(long long)(k + 1) * CP + lane] = al;
+      if (reload) load_rec_alpha(rec_ptr(k + 2), lane, V, R);
+      __builtin_amdgcn_wave_barrier();
+    };
+    if (Kl > 0) {
+      load_rec_alpha(rec_ptr(0), lane, V, rr[0]);
+      load_rec_alpha(rec_ptr(1), lane, V, rr[1]);
+      for (int k0 = 0; k0 < (Kl & ~1); k0 += 2) {
+        step(rr[0], k0, true);
+        step(rr[1], k0 + 1, true);
+      }
+      if (Kl & 1) step(rr[0], Kl - 1, false);
+    }
+    // log_z = (+)_q alpha_T[q] (lattices.py:496)
+    const float x = lane < C ? al : -kInf;
+    const float M = safe_max(wmax_u(x));
+    const float s = wsum_u(lane < C ? lt_exp(x - M) : 0.f);
+    if (lane == 0) s_lz = M + lt_log(s);
+  } else if (wave == 1 && !a.local && !(a.dbg & 1)) {
+    // ---- den beta across chunks: beta_T = one for every state (lattices.py:788-790)
+    float* bc = s_bc[1];
+    const int h = lane >> 5;
+    float be = lane < C ? 0.f : -kInf;  // lane p: beta[p]
+    float* dst = a.bbd + (long long)b * (a.K + 1) * CP;
+    if (lane < C) dst[(long long)Kl * CP + lane] = be;
+    RecBeta rr[2];
+    auto rec_ptr = [&](int k) { return rec0 + (long long)max(k, 0) * kRec; };
+    auto step = [&](RecBeta& R, int k, bool reload) {
+      const float xc = (lane >= 1 && lane < C) ? be : -kInf;  // core beta
+      const float Mc = safe_max(wmax_u(xc));
+      if (lane >= 1 && lane <= 32) bc[lane - 1] = lane < C ? lt_exp(xc - Mc) : 0.f;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      // lane (j, h): sum over end states i of half h of X[i][j] b_i
+      float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 b4 = *(const float4*)(bc + 8 * g + 4 * h);
+        p0 = __builtin_fmaf(R.x[4 * g + 0], b4.x, p0);
+        p1 = __builtin_fmaf(R.x[4 * g + 1], b4.y, p1);
+        p0 = __builtin_fmaf(R.x[4 * g + 2], b4.z, p0);
+        p1 = __builtin_fmaf(R.x[4 * g + 3], b4.w, p1);
+      }
+      const float tot = half_sum(p0 + p1);
+      const float nj = Mc + R.cs + R.ej + lt_log(tot);  // lane j: beta'[j+1]
+      // state 0: the rt row and its own self loop
+      const float rsum = wsum_u(lane < 32 ? R.rt * bc[lane & 31] : 0.f);
+      const float rterm = Mc + R.cs + R.rho + lt_log(rsum);
+      const float nb0 = lse2(first_lane(be) + R.pi + R.cs, rterm);
+      const float sh = from_prev(nj, -kInf);
+      be = lane == 0 ? nb0 : (lane < C ? sh : -kInf);
+      if (lane < C) dst[(long long)k * CP + lane] = be;
+      if (reload) load_rec_beta(rec_ptr(k - 2), lane, R);
+      __builtin_amdgcn_wave_barrier();
+    };
+    if (Kl > 0) {
+      load_rec_beta(rec_ptr(Kl - 1), lane, rr[0]);
+      load_rec_beta(rec_ptr(Kl - 2), lane, rr[1]);
+      for (int n0 = 0; n0 < (Kl & ~1); n0 += 2) {
+        step(rr[0], Kl - 1 - n0, true);
+        step(rr[1], Kl - 2 - n0, true);
+      }
+      if (Kl & 1) step(rr[0], 0, false);
+    }
+  } else if (wave == 2 && !(a.dbg & 2)) {
+    // ---- numerator alpha over frames (lattices.py:340-377), base-2 log space
+    constexpr int D = 8;
+    const float2* G0 = (const float2*)a.G + (long long)b * a.T * NPG;
+    float al[PPL];
+#pragma unroll
+    for (int r = 0; r < PPL; ++r) al[r] = (lane + 64 * r == 0) ? 0.f : -kInf;
+    float* dst = a.nabd + (long long)b * (a.K + 1) * NPG;
+    // rows in registers D frames ahead; unconditional loads (frame and
+    // position clamped) keep the compiler's vmcnt tracking exact
+    float2 gq[D][PPL];
+    auto gload = [&](int t, float2* g) {
+      const long long tt = min(t, max(nf - 1, 0));
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) g[r] = G0[tt * NPG + min(lane + 64 * r, NPG - 1)];
+    };
+    int kb = 0;  // next chunk boundary index
+    auto step = [&](float2* g, int t, bool reload) {
+      if (t == kb * a.L) {
+#pragma unroll
+        for (int r = 0; r < PPL; ++r)
+          if (lane + 64 * r < NPG) dst[(long long)kb * NPG + lane + 64 * r] = al[r] * kLn2;
+        ++kb;
+      }
+      float gb[PPL], gl[PPL];
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) {
+        const bool ok = lane + 64 * r < NPG;
+        gb[r] = ok ? g[r].x * kLog2e : -kInf;
+        gl[r] = ok ? g[r].y * kLog2e : -kInf;
+      }
+      if (reload) gload(t + D, g);
+      float prev = -kInf, nv[PPL];
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) {
+        const float x = rot_prev(al[r]);  // lane 0 gets lane 63's
+        const float pv = lane == 0 ? prev : x;
+        prev = x;
+        nv[r] = lse2_b2(al[r] + gb[r], pv + gl[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) al[r] = nv[r];
+    };
+    if (nf > 0) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) gload(d, gq[d]);
+      const int nmain = nf - nf % D;
+      for (int t0 = 0; t0 < nmain; t0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) step(gq[d], t0 + d, true);
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (nmain + d < nf) step(gq[d], nmain + d, false);
+    }
+    float nv = -kInf;
+#pragma unroll
+    for (int r = 0; r < PPL; ++r)
+      if (lane + 64 * r == nl) nv = al[r] * kLn2;
+    nv = wmax_u(nv);
+    if (lane == 0) s_num = (nl >= 0 && nl <= a.U) ? nv : -kInf;
+  } else if (wave == 3 && !(a.dbg & 2)) {
+    // ---- numerator beta (reverse of alignments.py:320-329), base-2 log space
+    constexpr int D = 8;
+    const float2* G0 = (const float2*)a.G + (long long)b * a.T * NPG;
+    float be[PPL];
+#pragma unroll
+    for (int r = 0; r < PPL; ++r) be[r] = (lane + 64 * r == nl) ? 0.f : -kInf;
+    float* dst = a.nbbd + (long long)b * (a.K + 1) * NPG;
+#pragma unroll
+    for (int r = 0; r < PPL; ++r)
+      if (lane + 64 * r < NPG) dst[(long long)Kl * NPG + lane + 64 * r] = be[r] * kLn2;
+    // row t: blank weight of u, weight of the arc into u+1; unconditional
+    // loads (frame and positions clamped)
+    float2 gq[D][PPL];
+    auto gload = [&](int t, float2* g) {
+      const long long tt = max(t, 0);
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) {
+        const int u = lane + 64 * r;
+        g[r].x = G0[tt * NPG + min(u, NPG - 1)].x;
+        g[r].y = G0[tt * NPG + min(u + 1, NPG - 1)].y;
+      }
+    };
+    int kb = Kl - 1;  // next chunk boundary index (descending)
+    auto step = [&](float2* g, int t, bool reload) {
+      float gb[PPL], gl[PPL];
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) {
+        const int u = lane + 64 * r;
+        gb[r] = u < NPG ? g[r].x * kLog2e : -kInf;
+        gl[r] = u + 1 < NPG ? g[r].y * kLog2e : -kInf;
+      }
+      if (reload) gload(t - D, g);
+      float nx[PPL], nv[PPL];
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) nx[r] = rot_next(be[r]);  // lane 63 gets lane 0's
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) {
+        // beta[u+1]: lane+1 of the same register; lane 63 -> lane 0 of r+1
+        const float nb = lane == 63 ? (r + 1 < PPL ? nx[r + 1 < PPL ? r + 1 : r] : -kInf)
+                                    : nx[r];
+        nv[r] = lse2_b2(gb[r] + be[r], gl[r] + nb);
+      }
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) be[r] = nv[r];
+      if (t == kb * a.L) {
+#pragma unroll
+        for (int r = 0; r < PPL; ++r)
+          if (lane + 64 * r < NPG) dst[(long long)kb * NPG + lane + 64 * r] = be[r] * kLn2;
+        --kb;
+      }
+    };
+    if (nf > 0) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) gload(nf - 1 - d, gq[d]);
+      const int nmain = nf - nf % D;
+      for (int n0 = 0; n0 < nmain; n0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) step(gq[d], nf - 1 - (n0 + d), true);
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (nmain + d < nf) step(gq[d], nf - 1 - (nmain + d), false);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float lz = a.local ? 0.f : s_lz;
+    const float nm = s_num;
+    a.log_z[b] = lz;
+    a.num[b] = nm;
+    if (a.lz_out) a.lz_out[b] = lz;
+    if (a.num_out) a.num_out[b] = nm;
+    a.loss[b] = a.local ? -nm : lz - nm;  // lattices.py:178-183
+  }
+}
+
+// Phase C's gather tables: per position, in LDS (labels staged by the whole
+// workgroup first).
+LT_DEVINL void gather_tables(const CkArgs& a, int b, int* lab, int* boff, int* loff, int tid,
+                             int nthr) {
+  for (int j = tid; j < a.U; j += nthr) lab[j] = a.labels[(long long)b * a.U + j];
+  __syncthreads();
+  for (int u = tid; u < a.NPG; u += nthr) {
+    int bo, lo;
+    string_offsets(a, lab, u, &bo, &lo);
+    boff[u] = bo < 0 ? 0 : bo;
+    loff[u] = lo;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// C: local recursions + marginals -> dW (one workgroup per chunk)
+// ---------------------------------------------------------------------------
+template <bool BF16>
+LT_DEVINL void store_dw(void* dW, long long e, float v) {
+  if constexpr (BF16) ((unsigned short*)dW)[e] = f2bf(v);
+  else ((float*)dW)[e] = v;
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int b = blockIdx.x / a.K, k = blockIdx.x - (blockIdx.x / a.K) * a.K;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a.uflag[b]) return;  // the frame-serial kernels own this utterance
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int t0 = k * a.L;
+  const int tend = min(t0 + a.L, a.T);
+  const int t1 = max(t0, min(t0 + a.L, nf));
+  const int V = a.V, C = a.C, R = a.R, FR = a.FR, CP = a.CP, NPG = a.NPG;
+  float g = a.grad ? a.grad[b] : 1.f;
+  const float lz = a.log_z[b], nm = a.num[b];
+  if (!__builtin_isfinite(nm) || (!a.local && !__builtin_isfinite(lz))) g = 0.f;
+  const long long e0 = ((long long)b * a.T + t0) * FR;
+  if (t1 <= t0 || g == 0.f) {  // padding chunk / unreachable string: dW = 0
+    const long long n = (long long)(tend - t0) * FR;
+    for (long long e = tid; e < n; e += blockDim.x) store_dw<BF16>(a.dW, e0 + e, 0.f);
+    return;
+  }
+  const int nt = t1 - t0;
+  // stage the chunk's live frames
+  const long long off = e0 * (BF16 ? 2 : 4);
+  dma_issue(a.W, off, (long long)nt * a.FB, lds_base_addr(lds), a.c_ni, lane, wave, 4);
+  const unsigned char* wch = lds + (off & 15);
+  float* ad = (float*)(lds + a.c_off_ad);  // [L][CP] alpha_t (log)
+  float* bd = (float*)(lds + a.c_off_bd);  // [L][CP] beta_{t+1}
+  float* an = (float*)(lds + a.c_off_an);  // [L][NPG]
+  float* bn = (float*)(lds + a.c_off_bn);  // [L][NPG]
+  int* boff = (int*)(lds + a.c_off_tab);
+  int* loff = boff + NPG;
+  int* labs = loff + NPG;
+  float* buf = (float*)(lds + a.c_off_buf) + 64 * wave;
+  gather_tables(a, b, labs, boff, loff, tid, blockDim.x);
+  wait_vmcnt(0);
+  __syncthreads();
+
+  if (wave == 0 && !a.local && !(a.dbg & 4)) {
+    // ---- den alpha (lane p: alpha[p]); per frame a linear-space step with
+    // the frame's W[0][0] as offset (range <= kRange) and the vector's max.
+    // Lane (q, h): destination q+1, sources p in [16h, 16h+16) (+ p = 32
+    // in h = 1), the blank self loop in h = 0; halves combined by permlane.
+    const int q = lane & 31, h = lane >> 5;
+    float al = lane < C ? a.abd[((long long)b * (a.K + 1) + k) * CP + lane] : -kInf;
+    for (int f = 0; f < nt; ++f) {
+      if (lane < C) ad[f * CP + lane] = al;
+      const unsigned char* fr = wch + f * a.FB;
+      const float c = ldsw<BF16>(fr, 0);
+      const float cl = c * kLog2e;
+      const float M = safe_max(wmax_u(lane < C ? al : -kInf));
+      if (lane < 36) buf[lane] = lane < C ? lt_exp(al - M) : 0.f;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      float s0 = 0.f, s1 = 0.f;
+      if (q < V) {
+        const int qe = q + 1;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 b4 = *(const float4*)(buf + 16 * h + 4 * g);
+          const int p0 = 16 * h + 4 * g;
+          s0 = __builtin_fmaf(b4.x, (p0 + 0 < C) ? lt_exp_off(ldsw<BF16>(fr, (p0 + 0) * R + qe), cl) : 0.f, s0);
+          s1 = __builtin_fmaf(b4.y, (p0 + 1 < C) ? lt_exp_off(ldsw<BF16>(fr, (p0 + 1) * R + qe), cl) : 0.f, s1);
+          s0 = __builtin_fmaf(b4.z, (p0 + 2 < C) ? lt_exp_off(ldsw<BF16>(fr, (p0 + 2) * R + qe), cl) : 0.f, s0);
+          s1 = __builtin_fmaf(b4.w, (p0 + 3 < C) ? lt_exp_off(ldsw<BF16>(fr, (p0 + 3) * R + qe), cl) : 0.f, s1);
+        }
+        if (h == 1) {
+          if (C > 32) s0 = __builtin_fmaf(buf[32], lt_exp_off(ldsw<BF16>(fr, 32 * R + qe), cl), s0);
+        } else {  // the blank self loop of qe
+          s1 = __builtin_fmaf(buf[qe], lt_exp_off(ldsw<BF16>(fr, qe * R), cl), s1);
+        }
+      }
+      const float nq = M + c + lt_log(half_sum(s0 + s1));
+      const float n0 = first_lane(al) + c;
+      const float sh = from_prev(nq, -kInf);
+      al = lane == 0 ? n0 : (lane < C ? sh : -kInf);
+      __builtin_amdgcn_wave_barrier();
+    }
+  } else if (wave == 1 && !a.local && !(a.dbg & 4)) {
+    // ---- den beta (lane p: beta[p]); bd[f] = beta_{f+1}. Lane (j, h): core
+    // source j+1 over labels y in [16h+1, 16h+16], the blank in h = 0; every
+    // lane also one term of state 0's sum
+    const int j = lane & 31, h = lane >> 5;
+    float be = lane < C ? a.bbd[((long long)b * (a.K + 1) + k + 1) * CP + lane] : -kInf;
+    for (int f = nt - 1; f >= 0; --f) {
+      if (lane < C) bd[f * CP + lane] = be;
+      const unsigned char* fr = wch + f * a.FB;
+      const float c = ldsw<BF16>(fr, 0);
+      const float cl = c * kLog2e;
+      const float Mc = safe_max(wmax_u((lane >= 1 && lane < C) ? be : -kInf));
+      // buf[y-1] = exp(beta[y] - Mc) for core y
+      if (lane >= 1 && lane <= 32) buf[lane - 1] = lane < C ? lt_exp(be - Mc) : 0.f;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      float s0 = 0.f, s1 = 0.f;
+      if (j < V) {
+        const int pe = j + 1;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 b4 = *(const float4*)(buf + 16 * h + 4 * g);
+          const int y0 = 16 * h + 4 * g + 1;
+          s0 = __builtin_fmaf(b4.x, (y0 + 0 <= V) ? lt_exp_off(ldsw<BF16>(fr, pe * R + y0 + 0), cl) : 0.f, s0);
+          s1 = __builtin_fmaf(b4.y, (y0 + 1 <= V) ? lt_exp_off(ldsw<BF16>(fr, pe * R + y0 + 1), cl) : 0.f, s1);
+          s0 = __builtin_fmaf(b4.z, (y0 + 2 <= V) ? lt_exp_off(ldsw<BF16>(fr, pe * R + y0 + 2), cl) : 0.f, s0);
+          s1 = __builtin_fmaf(b4.w, (y0 + 3 <= V) ? lt_exp_off(ldsw<BF16>(fr, pe * R + y0 + 3), cl) : 0.f, s1);
+        }
+        if (h == 0) s0 = __builtin_fmaf(buf[j], lt_exp_off(ldsw<BF16>(fr, pe * R), cl), s0);
+      }
+      const float nj = Mc + c + lt_log(half_sum(s0 + s1));  // lane j: beta'[j+1]
+      // state 0: sum over labels y of E[0][y] exp(beta[y] - Mc), then its self loop
+      const float t0v = (lane < 32 && lane < V) ? buf[lane] * lt_exp_off(ldsw<BF16>(fr, lane + 1), cl) : 0.f;
+      const float n0 = lse2(first_lane(be) + c, Mc + c + lt_log(wsum_u(t0v)));
+      const float sh = from_prev(nj, -kInf);
+      be = lane == 0 ? n0 : (lane < C ? sh : -kInf);
+      __builtin_amdgcn_wave_barrier();
+    }
+  } else if (wave == 2 && !(a.dbg & 8)) {
+    // ---- num alpha
+    float al[4];
+    const float* src = a.nabd + ((long long)b * (a.K + 1) + k) * NPG;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) al[r] = (r < a.PPL && lane + 64 * r < NPG) ? src[lane + 64 * r] : -kInf;
+    for (int f = 0; f < nt; ++f) {
+      const unsigned char* fr = wch + f * a.FB;
+      float prev = -kInf, nv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (r < a.PPL) {
+          const int u = lane + 64 * r;
+          if (u < NPG) an[f * NPG + u] = al[r];
+          const float x = rot_prev(al[r]);
+          const float pv = lane == 0 ? prev : x;
+          prev = x;
+          const float gb = u < a.NP ? ldsw<BF16>(fr, boff[u]) : -kInf;
+          const int lo = u < NPG ? loff[u] : -1;
+          const float gl = lo >= 0 ? ldsw<BF16>(fr, lo) : -kInf;
+          nv[r] = lse2(al[r] + gb, pv + gl);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r < a.PPL) al[r] = nv[r];
+      __builtin_amdgcn_wave_barrier();
+    }
+  } else if (wave == 3 && !(a.dbg & 8)) {
+    // ---- num beta; bn[f] = beta_{f+1}
+    float be[4];
+    const float* src = a.nbbd + ((long long)b * (a.K + 1) + k + 1) * NPG;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) be[r] = (r < a.PPL && lane + 64 * r < NPG) ? src[lane + 64 * r] : -kInf;
+    for (int f = nt - 1; f >= 0; --f) {
+      const unsigned char* fr = wch + f * a.FB;
+      float nxt[4], nv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) nxt[r] = rot_next(be[r]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (r < a.PPL) {
+          const int u = lane + 64 * r;
+          if (u < NPG) bn[f * NPG + u] = be[r];
+          const float nb = lane == 63 ? (r + 1 < a.PPL ? nxt[r + 1 < 4 ? r + 1 : 3] : -kInf) : nxt[r];
+          const float gb = u < a.NP ? ldsw<BF16>(fr, boff[u]) : -kInf;
+          const int lo = u + 1 < NPG ? loff[u + 1] : -1;
+          const float gl = lo >= 0 ? ldsw<BF16>(fr, lo) : -kInf;
+          nv[r] = lse2(gb + be[r], gl + nb);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r < a.PPL) be[r] = nv[r];
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  __syncthreads();
+
+  // ---- marginals, one wave per frame: den - num, each normalised by its
+  // frame total (alignments.py:311-317; numerator: reverse of :320-329).
+  // Element e = lane + 64 m of a frame is arc (p, y) into q = y ? y : p;
+  // p and q packed per m once.
+  constexpr int MFX = 18;  // ceil(33 * 33 / 64)
+  const int MF = (FR + 63) / 64;
+  int pq[MFX];
+#pragma unroll
+  for (int m = 0; m < MFX; ++m) {
+    const int e = lane + 64 * m;
+    const int p = e / R, y = e - p * R;
+    pq[m] = (m < MF && e < FR) ? (p | ((y ? y : p) << 8)) : -1;
+  }
+  for (int f = (a.dbg & 16) ? nt : wave; f < nt; f += 4) {
+    const unsigned char* fr = wch + f * a.FB;
+    float* fb = BF16 ? (float*)(lds + a.c_off_fb) + wave * ((FR + 3) & ~3) : (float*)fr;
+    // numerator terms first (they read W)
+    float sb[4], sl[4];
+    float mxn = -kInf;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sb[r] = -kInf;
+      sl[r] = -kInf;
+      const int u = lane + 64 * r;
+      if (r < a.PPL && u < a.NP) {
+        const float bu = bn[f * NPG + u];
+        sb[r] = an[f * NPG + u] + ldsw<BF16>(fr, boff[u]) + bu;
+        if (u >= 1) sl[r] = an[f * NPG + u - 1] + ldsw<BF16>(fr, loff[u]) + bu;
+        mxn = fmaxf(mxn, fmaxf(sb[r], sl[r]));
+      }
+    }
+    mxn = safe_max(wmax_u(mxn));
+    float zn = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sb[r] = lt_exp(sb[r] - mxn);
+      sl[r] = lt_exp(sl[r] - mxn);
+      zn += sb[r] + sl[r];
+    }
+    zn = wsum_u(zn);
+    const float gn = zn > 0.f ? g / zn : 0.f;
+    if (!a.local) {
+      const float* adf = ad + f * CP;
+      const float* bdf = bd + f * CP;
+      float sv[MFX];
+      float mx = -kInf;
+#pragma unroll
+      for (int m = 0; m < MFX; ++m) {
+        sv[m] = -kInf;
+        if (pq[m] >= 0) {
+          sv[m] = adf[pq[m] & 255] + ldsw<BF16>(fr, lane + 64 * m) + bdf[pq[m] >> 8];
+          mx = fmaxf(mx, sv[m]);
+        }
+      }
+      mx = safe_max(wmax_u(mx));
+      float z = 0.f;
+#pragma unroll
+      for (int m = 0; m < MFX; ++m) {
+        sv[m] = lt_exp(sv[m] - mx);
+        z += sv[m];
+      }
+      z = wsum_u(z);
+      const float gd = z > 0.f ? g / z : 0.f;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int m = 0; m < MFX; ++m)
+        if (pq[m] >= 0) fb[lane + 64 * m] = sv[m] * gd;
+    } else {
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      for (int e = lane; e < FR; e += 64) fb[e] = 0.f;
+    }
+    // string arcs sharing a lattice arc meet here (LDS adds, lane order)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int u = lane + 64 * r;
+      if (r < a.PPL && u < a.NP) {
+        atomicAdd(fb + boff[u], -sb[r] * gn);
+        if (u >= 1) atomicAdd(fb + loff[u], -sl[r] * gn);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const long long eb = e0 + (long long)f * FR;
+    for (int e = lane; e < FR; e += 64) store_dw<BF16>(a.dW, eb + e, fb[e]);
+  }
+  // padding frames of this chunk
+  {
+    const long long n = (long long)(tend - t1) * FR;
+    const long long base = e0 + (long long)nt * FR;
+    for (long long e = tid; e < n; e += blockDim.x) store_dw<BF16>(a.dW, base + e, 0.f);
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+namespace {
+
+int ck_env(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return (s && *s) ? atoi(s) : dflt;
+}
+long long up256(long long x) { return (x + 255) & ~255LL; }
+int al16(long long x) { return (int)((x + 15) & ~15LL); }
+
+struct CkLayout {
+  // state (kept from lt_chunk_forward to lt_chunk_backward)
+  size_t uflag, lz, num, abd, bbd, nabd, nbbd, state;
+  // scratch: forward = records + G; backward = the fallback's checkpoints
+  size_t rec, G, f_alpha, f_an, f_loss, f_lz, f_num, f_side, scratch;
+};
+
+int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
+  memset(a, 0, sizeof(*a));
+  const int V = pb->vocab_size;
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  const int es = bf16 ? 2 : 4;
+  a->B = pb->batch; a->T = pb->max_frames; a->U = pb->max_labels;
+  a->V = V; a->C = V + 1; a->R = V + 1; a->FR = a->C * a->R;
+  a->NP = a->U + 1; a->NPG = (a->NP + 1) & ~1; a->PPL = (a->NPG + 63) / 64;
+  a->CP = (a->C + 3) & ~3;
+  a->local = local_norm ? 1 : 0;
+#ifdef LT_DIAG
+  a->dbg = ck_env("LT_CK_DBG", 0);
+#endif
+  a->FB = (long long)a->FR * es;
+  // A: per wave a ring of frame slots, the state-0 row and the gather tables
+  const long long n16f = (a->FB + 30) / 16;
+  a->a_ni = (int)((n16f + 63) / 64);
+  a->a_slots = 3;
+  a->a_slot_bytes = a->a_ni * 1024;
+  a->a_off_rt = a->a_slots * a->a_slot_bytes;
+  a->a_off_tab = a->a_off_rt + 128;
+  a->a_wave_bytes = al16(a->a_off_tab + 8LL * a->NPG);
+  // B: record rings (den alpha, den beta), G rings (num alpha, num beta)
+  a->b_ni = (kRec * 4 + 15 + 1023) / 1024;
+  a->b_slots = 4;
+  a->b_off_ra = 0;
+  a->b_off_rb = a->b_slots * a->b_ni * 1024;
+  a->b_gslot = 1024;
+  a->b_gslots = 16;
+  a->b_off_ga = a->b_off_rb + a->b_slots * a->b_ni * 1024;
+  a->b_off_gb = a->b_off_ga + a->b_gslots * a->b_gslot;
+  a->b_off_buf = a->b_off_gb + a->b_gslots * a->b_gslot;
+  // C: the chunk's frames, per-frame alpha/beta vectors, tables; L frames
+  // per chunk chosen so that two workgroups share a CU
+  auto c_bytes = [&](int L, CkArgs* t) {
+    const long long n16 = ((long long)L * a->FB + 30) / 16;
+    t->c_ni = (int)((n16 + 63) / 64);
+    int off = t->c_ni * 1024;
+    t->c_off_ad = off; off += al16(4LL * L * a->CP);
+    t->c_off_bd = off; off += al16(4LL * L * a->CP);
+    t->c_off_an = off; off += al16(4LL * L * a->NPG);
+    t->c_off_bn = off; off += al16(4LL * L * a->NPG);
+    t->c_off_tab = off; off += al16(8LL * a->NPG + 4LL * a->U);
+    t->c_off_buf = off; off += 4 * 64 * 4;
+    t->c_off_fb = off; off += bf16 ? 4 * 4 * ((a->FR + 3) & ~3) : 0;
+    return off;
+  };
+  int L = std::max(1, std::min(32, ck_env("LT_CHUNK_LEN", 32)));
+  while (L > 4 && c_bytes(L, a) > 80 * 1024) --L;
+  if (c_bytes(L, a) > 160 * 1024) return lt_impl::set_error(LT_EUNSUPPORTED, "chunk: LDS");
+  c_bytes(L, a);
+  a->L = L;
+  a->K = std::max(1, (a->T + L - 1) / L);
+  // workspace
+  const long long B = a->B, K = a->K, T = a->T;
+  size_t o = 0;
+  w->uflag = o; o += up256(4 * B);
+  w->lz = o; o += up256(4 * B);
+  w->num = o; o += up256(4 * B);
+  w->abd = o; o += up256(4 * B * (K + 1) * a->CP);
+  w->bbd = o; o += up256(4 * B * (K + 1) * a->CP);
+  w->nabd = o; o += up256(4 * B * (K + 1) * a->NPG);
+  w->nbbd = o; o += up256(4 * B * (K + 1) * a->NPG);
+  w->state = o;
+  size_t s = 0;
+  w->rec = s; s += up256(4LL * B * K * kRec);
+  w->G = s; s += up256(8LL * B * T * a->NPG);
+  const size_t fwd = s;
+  s = 0;
+  w->f_alpha = s; s += up256(4LL * B * T * a->C);
+  w->f_an = s; s += up256(4LL * B * T * a->NP);
+  w->f_loss = s; s += up256(4 * B);
+  w->f_lz = s; s += up256(4 * B);
+  w->f_num = s; s += up256(4 * B);
+  w->f_side = s; s += up256((long long)lt_impl::serial_side_bytes(pb, local_norm));
+  w->scratch = std::max(fwd, s);
+  return LT_OK;
+}
+
+void ck_bind(CkArgs* a, const CkLayout& w, void* state, void* scratch) {
+  char* st = (char*)state;
+  char* sc = (char*)scratch;
+  a->uflag = (int*)(st + w.uflag);
+  a->log_z = (float*)(st + w.lz);
+  a->num = (float*)(st + w.num);
+  a->abd = (float*)(st + w.abd);
+  a->bbd = (float*)(st + w.bbd);
+  a->nabd = (float*)(st + w.nabd);
+  a->nbbd = (float*)(st + w.nbbd);
+  a->rec = sc ? (float*)(sc + w.rec) : nullptr;
+  a->G = sc ? (float*)(sc + w.G) : nullptr;
+}
+
+int ck_launch(const void* k, int grid, int lds, hipStream_t st, const CkArgs& a) {
+  if (grid <= 0) return LT_OK;
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  void* args[] = {(void*)&a};
+  e = hipLaunchKernel(k, dim3(grid), dim3(256), args, lds, st);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  return LT_OK;
+}
+
+int ck_check(const lt_problem* pb) {
+  if (!pb) return lt_impl::set_error(LT_EINVAL, "null problem");
+  if (pb->batch < 0 || pb->max_frames < 0 || pb->max_labels < 0)
+    return lt_impl::set_error(LT_EINVAL, "negative dimension");
+  if (pb->weight_dtype != LT_DTYPE_F32 && pb->weight_dtype != LT_DTYPE_BF16)
+    return lt_impl::set_error(LT_EINVAL, "weight_dtype must be LT_DTYPE_F32 or LT_DTYPE_BF16");
+  if (!lt_impl::chunk_eligible(pb))
+    return lt_impl::set_error(LT_EUNSUPPORTED,
+                              "chunked path: FullNGram n = 1, vocab_size <= 32, labels < 128");
+  return LT_OK;
+}
+
+}  // namespace
+
+namespace lt_impl {
+bool chunk_eligible(const lt_problem* pb) {
+  if (ck_env("LT_CHUNK", 1) == 0) return false;
+  if (pb->context_size != 1 || pb->vocab_size < 1 || pb->vocab_size > 32) return false;
+  if (pb->max_labels + 1 > 128) return false;  // <= 2 string positions per lane
+  const long long C = pb->vocab_size + 1;
+  if ((long long)pb->batch * pb->max_frames * C * C >= (1LL << 31)) return false;
+  return true;
+}
+}  // namespace lt_impl
+
+extern "C" {
+
+int lt_chunk_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_t* state_bytes,
+                             size_t* scratch_bytes) {
+  int rc = ck_check(pb);
+  if (rc) return rc;
+  CkArgs a;
+  CkLayout w;
+  if ((rc = ck_plan(pb, local_norm, &a, &w))) return rc;
+  if (state_bytes) *state_bytes = w.state;
+  if (scratch_bytes) *scratch_bytes = w.scratch;
+  return LT_OK;
+}
+
+int lt_chunk_forward(const lt_problem* pb, int32_t local_norm, const void* W,
+                     const int32_t* num_frames, const int32_t* labels, const int32_t* num_labels,
+                     float* loss, float* log_z, float* num, void* state, size_t state_bytes,
+                     void* scratch, size_t scratch_bytes, void* stream) {
+  int rc = ck_check(pb);
+  if (rc) return rc;
+  if (pb->batch == 0) return LT_OK;
+  CkArgs a;
+  CkLayout w;
+  if ((rc = ck_plan(pb, local_norm, &a, &w))) return rc;
+  if ((pb->max_frames > 0 && !W) || !num_frames || !num_labels || !loss ||
+      (pb->max_labels > 0 && !labels) || !state || !scratch)
+    return lt_impl::set_error(LT_EINVAL, "null pointer");
+  if (((uintptr_t)W & 15) || ((uintptr_t)state & 15) || ((uintptr_t)scratch & 15))
+    return lt_impl::set_error(LT_EINVAL, "W / workspaces must be 16-byte aligned");
+  if (state_bytes < w.state || scratch_bytes < w.scratch)
+    return lt_impl::set_error(LT_EINVAL, "workspace too small");
+  ck_bind(&a, w, state, scratch);
+  a.W = (const unsigned char*)W;
+  a.nfr = num_frames; a.labels = labels; a.nlab = num_labels;
+  a.loss = loss;
+  a.lz_out = log_z;
+  a.num_out = num;
+  hipStream_t st = (hipStream_t)stream;
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  const int grid_a = (int)(((long long)a.B * a.K + 3) / 4);
+  const void* ka = a.PPL == 1 ? (bf16 ? (const void*)ck_transfer_kernel<true, 1>
+                                      : (const void*)ck_transfer_kernel<false, 1>)
+                              : (bf16 ? (const void*)ck_transfer_kernel<true, 2>
+                                      : (const void*)ck_transfer_kernel<false, 2>);
+  const void* kb = a.PPL == 1 ? (const void*)ck_combine_kernel<1> : (const void*)ck_combine_kernel<2>;
+  if ((rc = ck_launch(ka, grid_a, 0, st, a))) return rc;
+  if ((rc = ck_launch(kb, a.B, 0, st, a))) return rc;
+  // utterances outside the fast path's range: the frame-serial kernels
+  // (their workgroups return at once for every other utterance)
+  return lt_impl::serial_loss(pb, local_norm, W, num_frames, labels, num_labels, a.uflag, loss,
+                              log_z ? log_z : a.log_z, num ? num : a.num, nullptr, nullptr,
+                              nullptr, nullptr, nullptr, stream);
+}
+
+int lt_chunk_backward(const lt_problem* pb, int32_t local_norm, const void* W,
+                      const int32_t* num_frames, const int32_t* labels, const int32_t* num_labels,
+                      const float* grad, void* dW, void* state, size_t state_bytes, void* scratch,
+                      size_t scratch_bytes, void* stream) {
+  int rc = ck_check(pb);
+  if (rc) return rc;
+  if (pb->batch == 0 || pb->max_frames == 0) return LT_OK;
+  CkArgs a;
+  CkLayout w;
+  if ((rc = ck_plan(pb, local_norm, &a, &w))) return rc;
+  if (!W || !num_frames || !num_labels || !dW || (pb->max_labels > 0 && !labels) || !state ||
+      !scratch)
+    return lt_impl::set_error(LT_EINVAL, "null pointer");
+  if (((uintptr_t)W & 15) || ((uintptr_t)state & 15) || ((uintptr_t)scratch & 15))
+    return lt_impl::set_error(LT_EINVAL, "W / workspaces must be 16-byte aligned");
+  if (state_bytes < w.state || scratch_bytes < w.scratch)
+    return lt_impl::set_error(LT_EINVAL, "workspace too small");
+  ck_bind(&a, w, state, nullptr);
+  a.W = (const unsigned char*)W;
+  a.nfr = num_frames; a.labels = labels; a.nlab = num_labels;
+  a.grad = grad;
+  a.dW = dW;
+  hipStream_t st = (hipStream_t)stream;
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  const int lds_c = a.c_off_fb + (bf16 ? 4 * 4 * ((a.FR + 3) & ~3) : 0);
+  if ((rc = ck_launch(bf16 ? (const void*)ck_marg_kernel<true> : (const void*)ck_marg_kernel<false>,
+                      a.B * a.K, lds_c, st, a)))
+    return rc;
+  char* sc = (char*)scratch;
+  return lt_impl::serial_loss(pb, local_norm, W, num_frames, labels, num_labels, a.uflag,
+                              (float*)(sc + w.f_loss), (float*)(sc + w.f_lz),
+                              (float*)(sc + w.f_num), (float*)(sc + w.f_alpha),
+                              (float*)(sc + w.f_an), grad, dW, sc + w.f_side, stream);
+}
+
+}  // extern "C"

@@ -354,6 +354,8 @@ struct KArgs {
   float* beta_num;   // [B,T,U+1] num beta_{t+1} per frame t
   int* arcs;         // [B,4(U+1)] numerator arc table (forward writes, marginal pass reads)
   int B, T, U, flags;
+  const int* only;   // nullable: only utterances with only[b] != 0 run (the chunked
+                     // path's fallback, lt_chunk.hip); the others return at once
   long long* stamps; // diagnostic build (-DLT_STAMPS) only: per-step clocks
   int dbg;           // ablation bitmask (LT_DBG, timing experiments only): 1 skip den
                      // compute, 2 skip numerator, 4 loaders issue nothing, 8 no barrier
@@ -834,6 +836,7 @@ __global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
   const NGram& g = a.g;
   const int C = g.C, NP = a.U + 1;
   const bool do_den = a.flags & F_DEN, do_num = a.flags & F_NUM;
+  if (a.only && !a.only[b]) return;
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
 
@@ -1276,6 +1279,7 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
   const NGram& g = a.g;
   const int C = g.C, NP = a.U + 1, FR = a.FR;
   const bool do_den = a.flags & F_DEN, do_num = a.flags & F_NUM;
+  if (a.only && !a.only[b]) return;
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
 
@@ -1395,6 +1399,14 @@ struct Plan {
 LT_VARIANTS(LT_DECL)
 #undef LT_DECL
 int set_error(int code, const char* msg);
+// lt_lattice.hip: frame-serial loss (+ dW) for the utterances with only[b] != 0
+size_t serial_side_bytes(const lt_problem* pb, int local_norm);
+int serial_loss(const lt_problem* pb, int local_norm, const void* W, const int32_t* num_frames,
+                const int32_t* labels, const int32_t* num_labels, const int* only, float* loss,
+                float* log_z, float* num, float* alpha, float* alpha_num, const float* grad,
+                void* dW, void* side, void* stream);
+// lt_chunk.hip: chunked two-level scan (bigram Log)
+bool chunk_eligible(const lt_problem* pb);
 // lt_pipe.hip: pipelined bigram Log recursions (alpha, and beta when dirs == 2)
 bool pipe_eligible(const lt_problem* pb);
 int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32_t* nfr,

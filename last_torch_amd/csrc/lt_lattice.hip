@@ -12,6 +12,7 @@ __global__ void num_scatter_kernel(const KArgs a) {
   const long long bt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (bt >= (long long)a.B * a.T) return;
   const int b = (int)(bt / a.T), t = (int)(bt % a.T);
+  if (a.only && !a.only[b]) return;
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   if (t >= nf) return;
@@ -478,7 +479,9 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl,
   pl->ck = kind == 2;
   a.B = pb->batch; a.T = pb->max_frames; a.U = pb->max_labels; a.g = g;
   a.flags = flags;
-  a.dbg = env_int("LT_DBG", 0);
+#ifdef LT_DIAG
+  a.dbg = env_int("LT_DBG", 0);  // timing ablations: diagnostic builds only
+#endif
 #ifdef LT_STAMPS
   {
     const char* sp = getenv("LT_STAMPS_PTR");
@@ -729,6 +732,15 @@ __global__ __launch_bounds__(256) void scale_kernel(void* dW, const float* grad,
   }
 }
 
+// After a fused lt_loss_grad launch: a hand-off wait that timed out (error
+// word non-zero, lt_pipe.hip) means some workgroup read rows that were never
+// published, so every loss of the batch is replaced by NaN -- the failure is
+// visible in the product path instead of a silently wrong dW.
+__global__ __launch_bounds__(256) void handoff_check_kernel(const int* err, float* loss, int B) {
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) loss[b] = __builtin_nanf("");
+}
+
 int cu_count() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
@@ -763,6 +775,65 @@ GradWs grad_ws(const lt_problem* pb, int local_norm) {
 
 namespace lt_impl {
 int set_error(int code, const char* msg) { return fail(code, msg); }
+
+size_t serial_side_bytes(const lt_problem* pb, int local_norm) {
+  size_t n = 0;
+  if (lt_loss_backward_workspace_bytes(pb, local_norm, &n) != LT_OK) return 0;
+  return n;
+}
+
+// The frame-serial recursion kernels (fwd_kernel, bwd_kernel) restricted to
+// the utterances with only[b] != 0: loss / log_z / num and, when dW is given,
+// alpha / alpha_num checkpoints plus the backward -> dW (scaled by grad).
+// The chunked path (lt_chunk.hip) sends utterances outside its range here.
+int serial_loss(const lt_problem* pb, int local_norm, const void* W, const int32_t* num_frames,
+                const int32_t* labels, const int32_t* num_labels, const int* only, float* loss,
+                float* log_z, float* num, float* alpha, float* alpha_num, const float* grad,
+                void* dW, void* side, void* stream) {
+  NGram g;
+  int rc = check_problem(pb, &g);
+  if (rc) return rc;
+  if (pb->batch == 0) return LT_OK;
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  hipStream_t st = (hipStream_t)stream;
+  Plan pf;
+  if ((rc = plan(pb, g, 0, F_NUM | F_LOSS | (local_norm ? F_LOCAL : F_DEN), &pf))) return rc;
+  bind_streams(pf.a, W, nullptr, nullptr);
+  pf.a.nfr = num_frames; pf.a.labels = labels; pf.a.nlab = num_labels;
+  pf.a.loss = loss; pf.a.dist = local_norm ? nullptr : log_z; pf.a.num = num;
+  pf.a.alpha = dW ? alpha : nullptr; pf.a.alpha_num = dW ? alpha_num : nullptr;
+  pf.a.only = only;
+  if (local_norm && log_z) {
+    if ((rc = hip_check(hipMemsetAsync(log_z, 0, sizeof(float) * pb->batch, st), "memset")))
+      return rc;
+  }
+  if ((rc = launch_fwd(M_LOG, pf, bf16, pb->batch, st))) return rc;
+  if (!dW) return LT_OK;
+  Plan pl;
+  if ((rc = plan(pb, g, 1, F_NUM | (local_norm ? F_LOCAL : F_DEN), &pl))) return rc;
+  bind_streams(pl.a, W, local_norm ? nullptr : alpha, alpha_num);
+  KArgs& a = pl.a;
+  a.nfr = num_frames; a.labels = labels; a.nlab = num_labels;
+  a.log_z_in = log_z; a.num_in = num; a.grad = grad; a.dW = dW;
+  a.only = only;
+  if (!pl.dst) {
+    const long long NP = pb->max_labels + 1;
+    const long long nm = (long long)pb->batch * pb->max_frames * NP * 2 * 4;
+    a.nm_side = (float*)side;
+    a.ctx_side = (int*)((char*)side + ((nm + 255) & ~255LL));
+  }
+  if ((rc = launch_bwd(pl, bf16, pb->batch, st))) return rc;
+  if (!pl.dst) {
+    const long long n = (long long)pb->batch * pb->max_frames;
+    const int blocks = (int)((n + 255) / 256);
+    if (blocks > 0) {
+      if (bf16) hipLaunchKernelGGL(num_scatter_kernel<true>, dim3(blocks), dim3(256), 0, st, a);
+      else hipLaunchKernelGGL(num_scatter_kernel<false>, dim3(blocks), dim3(256), 0, st, a);
+      if ((rc = hip_check(hipGetLastError(), "scatter launch"))) return rc;
+    }
+  }
+  return LT_OK;
+}
 }  // namespace lt_impl
 
 // ---------------------------------------------------------------------------
@@ -888,7 +959,11 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   if ((rc = hip_check(hipEventRecord(f->e0, st), "event record"))) return rc;
   if ((rc = hip_check(hipStreamWaitEvent(f->s, f->e0, 0), "stream wait"))) return rc;
   // LT_CK_SOLO (timing experiments only): 1 = beta pass only, 2 = alpha pass only
+#ifdef LT_DIAG
   const int solo = env_int("LT_CK_SOLO", 0);
+#else
+  const int solo = 0;
+#endif
   if (solo != 2 && (rc = launch_bwd(pbk, bf16, pb->batch, f->s))) return rc;
   if (solo != 1 && (rc = launch_fwd(M_LOG, pf, bf16, pb->batch, st))) return rc;
   if ((rc = hip_check(hipEventRecord(f->e1, f->s), "event record"))) return rc;
@@ -1059,6 +1134,12 @@ int lt_loss_grad_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_
   NGram g;
   int rc = check_problem(pb, &g);
   if (rc) return rc;
+  if (lt_impl::chunk_eligible(pb) && pb->max_frames > 0) {
+    size_t st = 0, sc = 0;
+    if ((rc = lt_chunk_workspace_bytes(pb, local_norm, &st, &sc))) return rc;
+    if (bytes) *bytes = ((st + 255) & ~(size_t)255) + sc;
+    return LT_OK;
+  }
   if (bytes) *bytes = grad_ws(pb, local_norm).total;
   return LT_OK;
 }
@@ -1075,6 +1156,20 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
       (pb->max_labels > 0 && !labels))
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W) || misaligned(dW)) return fail(LT_EINVAL, "W/dW must be 16-byte aligned");
+  if (lt_impl::chunk_eligible(pb) && pb->max_frames > 0) {
+    // bigram: the chunked two-level scan (lt_chunk.hip), three launches
+    size_t st = 0, sc = 0;
+    if ((rc = lt_chunk_workspace_bytes(pb, local_norm, &st, &sc))) return rc;
+    const size_t st_al = (st + 255) & ~(size_t)255;
+    if (!workspace || workspace_bytes < st_al + sc) return fail(LT_EINVAL, "workspace too small");
+    char* state = (char*)workspace;
+    char* scratch = state + st_al;
+    if ((rc = lt_chunk_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
+                               num, state, st, scratch, sc, stream)))
+      return rc;
+    return lt_chunk_backward(pb, local_norm, W, num_frames, labels, num_labels, nullptr, dW,
+                             state, st, scratch, sc, stream);
+  }
   const GradWs w = grad_ws(pb, local_norm);
   if (!workspace || workspace_bytes < w.total) return fail(LT_EINVAL, "workspace too small");
   char* ws = (char*)workspace;
@@ -1096,10 +1191,16 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
   const bool ck = env_int("LT_CHECKPOINTS", ck_def ? 1 : 0) != 0;
   // fused: the recursions and the marginal pass in one launch (lt_pipe.hip)
   const int fused = env_int("LT_FUSED", 2 * pb->batch < cus ? 1 : 0);
-  if (ck && fused && lt_impl::pipe_eligible(pb))
-    return lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
-                                num, alpha, an, beta, bn, arcs, 2, nullptr, stream, dW,
-                                (int*)(ws + w.ctl));
+  if (ck && fused && lt_impl::pipe_eligible(pb)) {
+    int* ctl = (int*)(ws + w.ctl);
+    if ((rc = lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss,
+                                   log_z, num, alpha, an, beta, bn, arcs, 2, nullptr, stream, dW,
+                                   ctl)))
+      return rc;
+    hipLaunchKernelGGL(handoff_check_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                       (const int*)(ctl + 2), loss, pb->batch);
+    return hip_check(hipGetLastError(), "hand-off check launch");
+  }
   if (ck) {
     if ((rc = lt_loss_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
                               num, alpha, an, beta, bn, arcs, stream)))

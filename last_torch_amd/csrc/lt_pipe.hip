@@ -1287,7 +1287,9 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   a.NH = std::max(1, std::min(kPipeMaxHelpers, pipe_env("LT_PIPE_HELPERS", 4)));
   a.logn = logf((float)(V + 2));
   a.dirs = dirs;
-  a.dbg = pipe_env("LT_PIPE_DBG", 0);
+#ifdef LT_DIAG
+  a.dbg = pipe_env("LT_PIPE_DBG", 0);  // timing ablations: diagnostic builds only
+#endif
 #ifdef LT_STAMPS
   {
     const char* sp = getenv("LT_STAMPS_PTR");
@@ -1366,7 +1368,9 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
     a.wsbase = lo;
     lds = std::max(lds, a.moff_wave + nw * a.mwave_bytes);
     lds = std::max(lds, pipe_env("LT_FUSED_LDS", 0));  // e.g. > 80 KB: one workgroup per CU
+#ifdef LT_DIAG
     if (const char* tp = getenv("LT_FUSED_TRACE")) a.trace = (long long*)strtoull(tp, nullptr, 0);
+#endif
     if (lds > 160 * 1024) return set_error(LT_EUNSUPPORTED, "pipe: fused LDS");
     // marginal workgroups fill the second workgroup slot of the CUs the
     // recursions leave; with no slot left they start as recursions retire

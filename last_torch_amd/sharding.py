@@ -49,10 +49,17 @@ def all_reduce_step(loss: torch.Tensor, params: Iterable[torch.nn.Parameter] = (
   divide by the global utterance count). Returns the global loss sum.
   Without an initialised process group this is the identity.
   """
-  grads = [p.grad for p in params if p.grad is not None]
   total = loss.detach().sum().reshape(1).to(torch.float32)
   if not (dist.is_available() and dist.is_initialized()):
     return total[0]
+  # every rank lays out the bucket from the full ordered parameter list: a
+  # parameter without a gradient on this rank (unused, or an empty shard)
+  # contributes zeros, so all ranks all-reduce buckets of the same layout
+  grads = []
+  for p in params:
+    if p.grad is None:
+      p.grad = torch.zeros_like(p)
+    grads.append(p.grad)
   flat = torch.cat([total] + [g.reshape(-1).to(torch.float32) for g in grads])
   dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
   off = 1

@@ -89,12 +89,18 @@ class _JointWeightsFn(torch.autograd.Function):
   the backward is lt_joint_weights_backward where its LDS holds d_ctx_proj,
   else PyTorch recomputing tanh in fp32, `chunk` frame rows at a time."""
 
+  # forward / setup_context split: torch.func transforms (the per-frame
+  # weight_vjp_fn of RecognitionLattice._backward) accept only this form
   @staticmethod
-  def forward(ctx, pc, pf, wo, bias, chunk):
+  def forward(pc, pf, wo, bias, chunk):
     from last_torch_amd import _native
+    return _native.joint_weights(pc, pf, wo, bias)
+
+  @staticmethod
+  def setup_context(ctx, inputs, output):
+    pc, pf, wo, _, chunk = inputs
     ctx.save_for_backward(pc, pf, wo)
     ctx.chunk = chunk
-    return _native.joint_weights(pc, pf, wo, bias)
 
   @staticmethod
   def backward(ctx, gW):

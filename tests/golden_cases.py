@@ -62,16 +62,20 @@ def assert_values_close(got, ref, rtol=1e-5, atol=1e-5):
   np.testing.assert_allclose(got[fin], ref[fin], rtol=rtol, atol=atol)
 
 
-def assert_grad_close(got, ref, log_z, bf16=False):
+def assert_grad_close(got, ref, log_z, bf16=False, num=None):
   """Arc-marginal gradients: per utterance b,
-  |got - ref| <= 1e-5 + 1e-6 * max(1, |log_z_b|) (+ 8e-3 relative for bf16 dW).
-  The fp32 log-space arguments alpha + w + beta - log_z are sums of terms
-  of magnitude ~|log_z|, each rounded at |log_z| * 2^-24, so a marginal near
-  1 carries an absolute error proportional to |log_z| (the reference, which
-  runs in fp32, carries the same); the float64 fixtures are exact."""
+  |got - ref| <= 1e-5 + 1e-6 * max(1, |log_z_b|, |num_b|) (+ 8e-3 relative
+  for bf16 dW). The fp32 log-space arguments alpha + w + beta - log_z (and
+  the numerator's alpha_num + w + beta_num - num) are sums of terms of
+  magnitude ~|log_z| (~|num|), each rounded at that magnitude * 2^-24, so a
+  marginal near 1 carries an absolute error proportional to it (the
+  reference, which runs in fp32, carries the same); the float64 fixtures are
+  exact. With locally normalised weights log_z is ~0 while |num| is not."""
   got = np.asarray(got, np.float64)
   ref = np.asarray(ref, np.float64)
   lz = np.abs(np.where(np.isfinite(log_z), log_z, 0.0)).astype(np.float64)
+  if num is not None:
+    lz = np.maximum(lz, np.abs(np.where(np.isfinite(num), num, 0.0)).astype(np.float64))
   atol = 1e-5 + 1e-6 * np.maximum(1.0, lz)
   tol = atol.reshape([-1] + [1] * (ref.ndim - 1)) + (8e-3 if bf16 else 1e-4) * np.abs(ref)
   err = np.abs(got - ref)

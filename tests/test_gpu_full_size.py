@@ -1,0 +1,190 @@
+"""GPU parity of the exact launches bench.py times, at the BASELINE sizes.
+
+* cfg2 (configs[1]): lt_loss_grad at B=64, T=1000, U=100, V=32 bigram fp32 --
+  the bench step's launch (the chunked two-level scan, lt_chunk.hip) -- every
+  utterance against the C oracle, plus size-independent properties
+  (per-frame marginal sums, determinism, linearity in the incoming gradient).
+* north star: B=256 of the same shape (sampled utterances + properties).
+* cfg4: MaxTropical Viterbi at B=64, T=2000: labels and path weights
+  bit-exact on every utterance.
+* cfg5: trigram (C = 1057) bf16 at B=32, T=1000, U=100: loss on a sample,
+  dW on two utterances.
+* the chunked path's fallback: utterances whose frames leave its range
+  (non-finite weights or max - min > 60) mixed into a batch.
+
+Tolerances as tests/test_gpu_parity.py (golden_cases.assert_*).
+"""
+import numpy as np
+import pytest
+import torch
+
+from last_torch_amd import _native as nat
+from golden_cases import assert_grad_close, assert_loss_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _orc():
+  from oracle import oracle as orc  # test infrastructure only
+  return orc
+
+
+def _bench_inputs(B, T, U, V, n, device, seed, dtype=torch.float32, varlen=False):
+  """bench.make_inputs: randn arc weights, uniform labels."""
+  g = torch.Generator(device=device)
+  g.manual_seed(seed)
+  C = nat.num_context_states(V, n)
+  W = torch.randn([B, T, C, V + 1], generator=g, device=device, dtype=torch.float32).to(dtype)
+  lab = torch.randint(1, V + 1, [B, U], generator=g, device=device, dtype=torch.int32)
+  if varlen:
+    nf = torch.randint(T // 2, T + 1, [B], generator=g, device=device, dtype=torch.int32)
+    nl = torch.randint(U // 2, U + 1, [B], generator=g, device=device, dtype=torch.int32)
+  else:
+    nf = torch.full([B], T, dtype=torch.int32, device=device)
+    nl = torch.full([B], U, dtype=torch.int32, device=device)
+  return W, nf, lab, nl
+
+
+def _np(*xs):
+  return [x.float().cpu().numpy() if x.is_floating_point() else x.cpu().numpy() for x in xs]
+
+
+def _frame_sums(dW, nf):
+  """Per (b, t): sum of dW over the frame's arcs (den marginals sum to 1,
+  num marginals to 1, so live frames give 0)."""
+  return dW.double().reshape(dW.shape[0], dW.shape[1], -1).sum(-1)
+
+
+@pytest.fixture(scope='module')
+def cfg2(cuda):
+  return _bench_inputs(64, 1000, 100, 32, 1, cuda, seed=1234)
+
+
+def test_cfg2_bench_launch_every_utterance(cfg2):
+  """The bench step (lt_loss_grad, B=64 T=1000 U=100 V=32 fp32): every
+  utterance's loss and dW against the oracle."""
+  W, nf, lab, nl = cfg2
+  V, n, U = 32, 1, lab.shape[1]
+  assert nat.chunk_path(W.shape[0], W.shape[1], U, V, n)
+  loss, lz, num, dW = nat.loss_grad(W, nf, lab, nl, V, n, False)
+  torch.cuda.synchronize()
+  Wc, nfc, labc, nlc = _np(W, nf, lab, nl)
+  rl, rlz, rnum, rdW = _orc().loss_grad(Wc, nfc, labc, nlc, V, n)
+  assert_loss_close(loss.cpu().numpy(), rl)
+  assert_loss_close(lz.cpu().numpy(), rlz)
+  assert_loss_close(num.cpu().numpy(), rnum)
+  assert_grad_close(dW.cpu().numpy(), rdW, rlz)
+
+
+def test_cfg2_properties(cfg2):
+  W, nf, lab, nl = cfg2
+  V, n = 32, 1
+  loss, lz, num, dW = nat.loss_grad(W, nf, lab, nl, V, n, False)
+  loss2, _, _, dW2 = nat.loss_grad(W, nf, lab, nl, V, n, False)
+  # deterministic: the same bits on a second call
+  assert torch.equal(loss, loss2) and torch.equal(dW, dW2)
+  assert torch.isfinite(loss).all() and (loss > -1e-3).all()  # log_z >= numerator
+  # each live frame: den marginals and num marginals both sum to 1
+  s = _frame_sums(dW, nf)
+  tol = 1e-5 + 2e-6 * lz.abs().double().clamp(min=1.0)[:, None]
+  assert (s.abs() <= tol).all(), float((s.abs() / tol).max())
+  # forward / backward split with an incoming gradient: linear in it
+  g = torch.linspace(-1.0, 2.0, W.shape[0], device=W.device)
+  l3, _, _, state = nat.chunk_forward(W, nf, lab, nl, V, n, False)
+  assert torch.equal(l3, loss)
+  dWg = nat.chunk_backward(W, nf, lab, nl, V, n, False, state, grad=g)
+  assert torch.allclose(dWg, dW * g[:, None, None, None], atol=1e-7, rtol=1e-6)
+  # the state serves a second backward (retain_graph semantics)
+  assert torch.equal(nat.chunk_backward(W, nf, lab, nl, V, n, False, state, grad=g), dWg)
+
+
+def test_cfg2_varlen_local_norm(cuda):
+  """Variable lengths and the locally normalised loss (numerator only) at
+  the bench shape: every utterance against the oracle."""
+  V, n = 32, 1
+  W, nf, lab, nl = _bench_inputs(16, 1000, 100, V, n, cuda, seed=7, varlen=True)
+  W = torch.log_softmax(W, dim=-1)
+  Wc, nfc, labc, nlc = _np(W, nf, lab, nl)
+  for local in (False, True):
+    loss, lz, _, dW = nat.loss_grad(W, nf, lab, nl, V, n, local)
+    rl, rlz, rnum, rdW = _orc().loss_grad(Wc, nfc, labc, nlc, V, n, local_norm=local)
+    assert_loss_close(loss.cpu().numpy(), rl)
+    # log-softmax weights: log_z ~ 0, the numerator's magnitude sets the tolerance
+    assert_grad_close(dW.cpu().numpy(), rdW, rlz, num=rnum)
+    pad = torch.arange(W.shape[1], device=cuda)[None, :] >= nf[:, None].long()
+    assert (dW[pad] == 0).all()
+
+
+def test_north_star_b256(cuda):
+  """B=256 (the north-star shape): sampled utterances against the oracle and
+  the per-frame marginal sums of all of them."""
+  V, n = 32, 1
+  W, nf, lab, nl = _bench_inputs(256, 1000, 100, V, n, cuda, seed=99)
+  loss, lz, _, dW = nat.loss_grad(W, nf, lab, nl, V, n, False)
+  s = _frame_sums(dW, nf)
+  tol = 1e-5 + 2e-6 * lz.abs().double().clamp(min=1.0)[:, None]
+  assert (s.abs() <= tol).all()
+  idx = [0, 1, 63, 64, 128, 200, 254, 255]
+  Wc, nfc, labc, nlc = _np(W[idx], nf[idx], lab[idx], nl[idx])
+  rl, rlz, _, rdW = _orc().loss_grad(Wc, nfc, labc, nlc, V, n)
+  assert_loss_close(loss[idx].cpu().numpy(), rl)
+  assert_grad_close(dW[idx].cpu().numpy(), rdW, rlz)
+
+
+def test_chunk_fallback_mixed_batch(cuda):
+  """Utterances outside the chunked path's range (a frame spanning more than
+  60, a -inf weight, a NaN-free +-30 peaked utterance) next to ordinary ones:
+  the frame-serial kernels take them inside the same call."""
+  V, n, T, U = 32, 1, 300, 40
+  rng = np.random.default_rng(21)
+  W = rng.standard_normal((6, T, V + 1, V + 1)).astype(np.float32)
+  W[1] *= 30.0                        # peaked: range ~ 200
+  W[3, 17, 5, 7] = -np.inf            # a masked arc
+  W[4, 250] *= 40.0                   # one wide frame late in the utterance
+  nf = np.array([300, 300, 123, 300, 280, 1], np.int32)
+  lab = rng.integers(1, V + 1, (6, U)).astype(np.int32)
+  nl = np.array([40, 35, 20, 40, 40, 0], np.int32)
+  Wd = torch.tensor(W, device=cuda)
+  nfd, labd, nld = (torch.tensor(x, device=cuda) for x in (nf, lab, nl))
+  assert nat.chunk_path(6, T, U, V, n)
+  for local in (False, True):
+    loss, lz, _, dW = nat.loss_grad(Wd, nfd, labd, nld, V, n, local)
+    rl, rlz, rnum, rdW = _orc().loss_grad(W, nf, lab, nl, V, n, local_norm=local)
+    assert_loss_close(loss.cpu().numpy(), rl)
+    assert_grad_close(dW.cpu().numpy(), rdW, rlz, num=rnum)
+
+
+def test_cfg4_viterbi_t2000_every_utterance(cuda):
+  """cfg4: MaxTropical shortest path at B=64, T=2000 (U=200 is unused by the
+  decode): labels and path weights bit-exact on every utterance, both label
+  conventions (reference y-1, D5; true y)."""
+  V, n = 32, 1
+  W, nf, _, _ = _bench_inputs(64, 2000, 200, V, n, cuda, seed=4)
+  Wc, nfc = _np(W, nf)
+  for conv in (nat.LABELS_REFERENCE, nat.LABELS_TRUE):
+    labels, weights, _ = nat.viterbi(W, nf, V, n, conv)
+    rlab, rw, _ = _orc().viterbi(Wc, nfc, V, n, convention=conv)
+    np.testing.assert_array_equal(labels.cpu().numpy(), rlab)
+    np.testing.assert_array_equal(weights.cpu().numpy(), rw)
+
+
+def test_cfg5_trigram_bf16(cuda):
+  """cfg5: trigram (|ctx| = 1057) bf16 arc weights at B=32, T=1000, U=100:
+  losses of a sample and dW of two utterances against the oracle on the
+  bf16-rounded weights; per-frame marginal sums of the whole batch."""
+  V, n = 32, 2
+  W, nf, lab, nl = _bench_inputs(32, 1000, 100, V, n, cuda, seed=5, dtype=torch.bfloat16)
+  loss, lz, _, dW = nat.loss_grad(W, nf, lab, nl, V, n, False)
+  s = _frame_sums(dW.float(), nf)
+  # bf16 dW: each element carries ~2^-9 relative rounding
+  tol = 1e-5 + 2e-6 * lz.abs().double().clamp(min=1.0)[:, None] + 2e-2
+  assert (s.abs() <= tol).all()
+  orc = _orc()
+  idx = [0, 17, 31]
+  Wc, nfc, labc, nlc = _np(W[idx], nf[idx], lab[idx], nl[idx])
+  rl, rlz, _, _ = orc.loss_grad(Wc, nfc, labc, nlc, V, n, want_grad=False)
+  assert_loss_close(loss[idx].cpu().numpy(), rl)
+  idx = [0, 31]
+  Wc, nfc, labc, nlc = _np(W[idx], nf[idx], lab[idx], nl[idx])
+  _, rlz, _, rdW = orc.loss_grad(Wc, nfc, labc, nlc, V, n)
+  assert_grad_close(dW[idx].float().cpu().numpy(), rdW, rlz, bf16=True)

@@ -272,13 +272,20 @@ def _poisoned_ws(W, V, n, U, local):
   return torch.full([max(nb, 1)], 0xFF, dtype=torch.uint8, device=W.device)
 
 
+# lt_loss_grad's designs: the chunked two-level scan (bigram default), the
+# fused pipe launch and the two-call path
+LOSS_GRAD_PATHS = {'chunk': {'LT_CHUNK': '1'}, 'fused': {'LT_CHUNK': '0', 'LT_FUSED': '1'},
+                   'two-call': {'LT_CHUNK': '0', 'LT_FUSED': '0'}}
+
+
 @pytest.mark.parametrize('case', LATTICE_CASES)
 @pytest.mark.parametrize('local', [False, True])
-@pytest.mark.parametrize('fused', ['1', '0'])
-def test_golden_loss_grad(cuda, case, local, fused, monkeypatch):
-  """lt_loss_grad (one launch for the bigram; LT_FUSED=0: the two-call
-  path) against the reference's fixtures."""
-  monkeypatch.setenv('LT_FUSED', fused)
+@pytest.mark.parametrize('path', list(LOSS_GRAD_PATHS))
+def test_golden_loss_grad(cuda, case, local, path, monkeypatch):
+  """lt_loss_grad against the reference's fixtures, on each design."""
+  for k, v in LOSS_GRAD_PATHS[path].items():
+    monkeypatch.setenv(k, v)
+  fused = '1' if path == 'fused' else '0'
   c = load(case)
   W, nf, lab, nl = _dev(c, cuda, 'W_local' if local else 'W')
   U = lab.shape[-1]
@@ -309,7 +316,10 @@ FUSED_RANDOM = [
 
 
 @pytest.mark.parametrize('B,T,U,V,dt', FUSED_RANDOM)
-def test_random_loss_grad_vs_oracle(cuda, B, T, U, V, dt):
+@pytest.mark.parametrize('path', ['chunk', 'fused'])
+def test_random_loss_grad_vs_oracle(cuda, B, T, U, V, dt, path, monkeypatch):
+  for k, v in LOSS_GRAD_PATHS[path].items():
+    monkeypatch.setenv(k, v)
   orc = _orc()
   n = 1
   W, nf, lab, nl = _random_problem(B, T, U, V, n, seed=B * 100 + T + U + V)
@@ -318,14 +328,18 @@ def test_random_loss_grad_vs_oracle(cuda, B, T, U, V, dt):
     W = torch.tensor(W).bfloat16().float().numpy()
   Wd = torch.tensor(W).to(torch.bfloat16 if bf16 else torch.float32).to(cuda)
   nfd, labd, nld = (torch.tensor(x).to(cuda) for x in (nf, lab, nl))
-  assert nat.fused_path(B, T, U, V, n, cuda, bf16)
+  if path == 'chunk' and not nat.chunk_path(B, T, U, V, n):
+    pytest.skip('shape outside the chunked path (U + 1 > 128)')
+  if path == 'fused':
+    assert nat.fused_path(B, T, U, V, n, cuda, bf16)
   for local in (False, True):
     ws = _poisoned_ws(Wd, V, n, U, local)
     loss, lz, _, dW = nat.loss_grad(Wd, nfd, labd, nld, V, n, local, workspace=ws)
     rl, rlz, _, rdW = orc.loss_grad(W, nf, lab, nl, V, n, local_norm=local)
     assert_loss_close(loss.cpu().numpy(), rl)
     assert_grad_close(dW.float().cpu().numpy(), rdW, rlz, bf16)
-    assert nat.grad_workspace_errors(ws, Wd, V, n, U, local) == 0
+    if path == 'fused':
+      assert nat.grad_workspace_errors(ws, Wd, V, n, U, local) == 0
     # deterministic: a second call gives the same bits
     loss2, _, _, dW2 = nat.loss_grad(Wd, nfd, labd, nld, V, n, local)
     assert torch.equal(loss, loss2) and torch.equal(dW, dW2)
