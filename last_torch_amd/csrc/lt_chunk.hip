@@ -55,6 +55,7 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr float kRange = 60.f;  // max - min of a frame's weights on the fast path
 constexpr int kRec = 1224;      // floats per chunk record (16-byte multiple)
 constexpr int kRowT = 36;       // row stride of the transposed core in a record
+constexpr int kGrp = 7;         // frames per numerator group (band offsets 0..kGrp)
 // record layout (floats): [0, 1152) X^T rows: rec[i * 36 + j] = X[i][j] =
 // P_scaled[j][i] (start core state j -> end core state i); [1152, 1184)
 // per-start-state (column) power-of-two scales ej (int); [1184, 1216) the
@@ -71,7 +72,7 @@ struct CkArgs {
   const int* nlab;
   const float* grad;       // [B] nullable (ones)
   float* rec;              // [B*K][kRec]
-  float* G;                // [B,T,NPG,2] numerator arc weights (log)
+  float* nb;               // [B,K,NGc,NPG,kGrp+1] numerator group bands (log2)
   int* uflag;              // [B] 1: utterance goes to the frame-serial kernels
   float* abd;              // [B,K+1,CP] den alpha at chunk starts (log)
   float* bbd;              // [B,K+1,CP] den beta at chunk starts
@@ -85,8 +86,10 @@ struct CkArgs {
   void* dW;
   int B, T, U, V, C, R, FR, NP, NPG, PPL, CP;
   int L, K;                // frames per chunk, chunks per utterance
+  int NGc;                 // numerator groups per chunk, ceil(L / kGrp)
   int local;               // LocallyNormalizedWeightFn: no denominator
   int dbg;                 // diagnostic builds (LT_DIAG) only: role ablations
+  long long* stamps;       // diagnostic builds only: per-workgroup s_memtime marks
   long long FB;            // bytes per frame
   // phase A per-wave LDS carve
   int a_slots, a_ni, a_slot_bytes, a_wave_bytes, a_off_rt, a_off_tab;
@@ -96,33 +99,6 @@ struct CkArgs {
   int c_ni, c_off_ad, c_off_bd, c_off_an, c_off_bn, c_off_tab, c_off_buf, c_off_fb;
 };
 
-LT_DEVINL float wmax(float v) {
-  v = fmaxf(v, xchg<0>(v));
-  v = fmaxf(v, xchg<1>(v));
-  v = fmaxf(v, xchg<2>(v));
-  v = fmaxf(v, xchg<3>(v));
-  v = fmaxf(v, xchg<4>(v));
-  v = fmaxf(v, xchg<5>(v));
-  return v;
-}
-LT_DEVINL float wmin(float v) {
-  v = fminf(v, xchg<0>(v));
-  v = fminf(v, xchg<1>(v));
-  v = fminf(v, xchg<2>(v));
-  v = fminf(v, xchg<3>(v));
-  v = fminf(v, xchg<4>(v));
-  v = fminf(v, xchg<5>(v));
-  return v;
-}
-LT_DEVINL float wsum(float v) {
-  v += xchg<0>(v);
-  v += xchg<1>(v);
-  v += xchg<2>(v);
-  v += xchg<3>(v);
-  v += xchg<4>(v);
-  v += xchg<5>(v);
-  return v;
-}
 // lanes l and l ^ 32 combined (v_permlane32_swap: both halves get both)
 LT_DEVINL float half_sum(float v) {
   auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
@@ -152,6 +128,25 @@ LT_DEVINL float lse2(float a, float b) {
   return c + lt_log(lt_exp(a - c) + lt_exp(b - c));
 }
 LT_DEVINL float safe_max(float m) { return __builtin_isfinite(m) ? m : 0.f; }
+#ifdef LT_DIAG
+#define CK_STAMP(k)                                                                  \
+  do {                                                                               \
+    if (a.stamps && !(a.dbg & 64) && threadIdx.x == 0)                                                \
+      a.stamps[(long long)blockIdx.x * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define CK_WSTAMP(k)                                                                 \
+  do {                                                                               \
+    if (a.stamps && (a.dbg & 64) && (threadIdx.x & 63) == 0)                                         \
+      a.stamps[(long long)blockIdx.x * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define CK_WSTAMP(k) \
+  do {               \
+  } while (0)
+#define CK_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 // lane 0's float (readfirstlane is an int builtin: never pass it a float)
 LT_DEVINL float first_lane(float v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
@@ -241,6 +236,13 @@ LT_DEVINL void string_offsets(const CkArgs& a, const int* lab, int u, int* boff,
   }
 }
 
+// log-space plus in base-2 units: m + log2(1 + 2^(n - m)); both operands
+// -inf gives -inf (the clamp turns the NaN of -inf - -inf into -200)
+LT_DEVINL float lse2_b2(float x, float y) {
+  const float m = fmaxf(x, y), n = fminf(x, y);
+  return m + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(fmaxf(n - m, -200.f)));
+}
+
 // ---------------------------------------------------------------------------
 // A: chunk transfer matrices (one wave per chunk). Frame data is loaded
 // straight into registers two frames ahead (the compiler's own waits).
@@ -299,6 +301,7 @@ template <bool BF16, int PPL>
 __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
   __shared__ __attribute__((aligned(16))) float s_rt[4][32];
   __shared__ int s_lab[4][128];
+  __shared__ __attribute__((aligned(16))) float2 s_g[4][128 + kGrp + 1];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int id = blockIdx.x * 4 + wave;
@@ -314,8 +317,10 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
   const int nt = t1 - t0;
   float* rt = s_rt[wave];
   int* lab = s_lab[wave];
+  float2* sg = s_g[wave];  // the frame's numerator arc weights (log2) by position
   for (int j = lane; j < a.U; j += 64) lab[j] = a.labels[(long long)b * a.U + j];
   if (lane < 32) rt[lane] = 0.f;
+  if (lane <= kGrp) sg[64 * PPL + lane] = make_float2(-kInf, -kInf);  // past the string
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
   int boff[PPL], loff[PPL];
@@ -337,20 +342,53 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
   float pi = 0.f;     // log P00 - csum
   float csum = 0.f;   // sum of c_t (integers)
   int bad = 0;
+  // numerator group bands: nbd[r][d] = log2 weight of the paths from
+  // position s = lane + 64 r at the group's first frame to s + d after its
+  // last (the string lattice's frame steps, lattices.py:340-377, composed)
+  float nbd[PPL][kGrp + 1];
 
   // frames in registers two ahead; the loads are unconditional (clamped to
   // the chunk's last frame) so the compiler's vmcnt tracking stays exact
   FrameRegs<BF16, PPL> fr[2];
   auto frame_ptr = [&](int f) { return W0 + (long long)min(f, nt - 1) * a.FR * es; };
   auto step = [&](FrameRegs<BF16, PPL>& F, int f, bool reload) {
-    const int t = t0 + f;
     mask_frame(V, lane, boff, loff, F);
-    // numerator arc weights of this frame -> G
-    float2* grow = (float2*)(a.G + ((long long)b * a.T + t) * NPG * 2);
+    // numerator: band step over the group (positions past the string read -inf)
+    {
+      const int j = f / kGrp, fl = f - j * kGrp;  // wave-uniform
 #pragma unroll
-    for (int r = 0; r < PPL; ++r) {
-      const int u = lane + 64 * r;
-      if (u < NPG) grow[u] = make_float2(F.gb[r], F.gl[r]);
+      for (int r = 0; r < PPL; ++r)
+        sg[lane + 64 * r] = make_float2(F.gb[r] * kLog2e, F.gl[r] * kLog2e);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      if (fl == 0) {
+#pragma unroll
+        for (int r = 0; r < PPL; ++r)
+#pragma unroll
+          for (int d = 0; d <= kGrp; ++d) nbd[r][d] = d ? -kInf : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) {
+        float2 gv[kGrp + 1];
+#pragma unroll
+        for (int d = 0; d <= kGrp; ++d) gv[d] = sg[lane + 64 * r + d];
+#pragma unroll
+        for (int d = kGrp; d >= 1; --d)
+          if (d <= fl + 1) nbd[r][d] = lse2_b2(nbd[r][d] + gv[d].x, nbd[r][d - 1] + gv[d].y);
+        nbd[r][0] += gv[0].x;
+      }
+      if (fl == kGrp - 1 || f == nt - 1) {  // source-major: 32 bytes per position
+        float4* dst = (float4*)(a.nb + (((long long)b * a.K + k) * a.NGc + j) * (kGrp + 1) * NPG);
+        static_assert(kGrp + 1 == 8, "two float4 per position");
+#pragma unroll
+        for (int r = 0; r < PPL; ++r)
+          if (lane + 64 * r < NPG) {
+            const int u = lane + 64 * r;
+            dst[2 * u] = make_float4(nbd[r][0], nbd[r][1], nbd[r][2], nbd[r][3]);
+            dst[2 * u + 1] = make_float4(nbd[r][4], nbd[r][5], nbd[r][6], nbd[r][7]);
+          }
+      }
+      __builtin_amdgcn_wave_barrier();
     }
     // the frame's range (every weight finite, max - min <= kRange)
     float mx = -kInf, mn = kInf;
@@ -487,11 +525,126 @@ LT_DEVINL void load_rec_beta(const float* rc, int lane, RecBeta& r) {
   r.cs = rc[kRecCs];
 }
 
-// log-space plus in base-2 units: m + log2(1 + 2^(n - m)); both operands
-// -inf gives -inf (the clamp turns the NaN of -inf - -inf into -200)
-LT_DEVINL float lse2_b2(float x, float y) {
-  const float m = fmaxf(x, y), n = fminf(x, y);
-  return m + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(fmaxf(n - m, -200.f)));
+// Phase B's numerator over the groups of kGrp frames (phase A's bands),
+// base-2 log space. FWD, alpha (lattices.py:340-377 composed per group):
+// al'[u] = (+)_d al[u - d] + N[u - d][d], scattered by destination through
+// an LDS table; !FWD, beta (the reverse of alignments.py:320-329):
+// be'[s] = (+)_d N[s][d] + be[s + d] from an LDS copy padded with -inf.
+// Boundary values at every chunk start -> nabd / nbbd (natural log).
+template <int PPL, bool FWD>
+LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl, float* lds,
+                        float* s_num) {
+  constexpr float kLn2 = 0.6931471805599453f;
+  const int NPG = a.NPG;
+  // ---- numerator over the groups of kGrp frames (phase A's bands), base-2
+  // log space. alpha (wave 2, lattices.py:340-377 composed per group):
+  // al'[u] = (+)_d al[u - d] + N[u - d][d]; beta (wave 3, the reverse of
+  // alignments.py:320-329): be'[s] = (+)_d N[s][d] + be[s + d]. The
+  // neighbours come from an LDS copy of the vector padded with -inf.
+  constexpr int D = 8;  // groups in registers ahead (4 loads each: vmcnt <= 63)
+  constexpr int NB = kGrp + 1;
+  constexpr int TS = NB + 1;  // alpha's scatter table row stride (odd: no bank conflicts)
+  const int NGc = a.NGc;
+  const int ntl = nf - (Kl - 1) * a.L;  // live frames of the last chunk
+  const int Q = Kl > 0 ? (Kl - 1) * NGc + (ntl + kGrp - 1) / kGrp : 0;
+  const float* nb0 = a.nb + (long long)b * a.K * NGc * NB * NPG;
+  // alpha: tab[u][d] = al[u - d] + N[u - d][d] (rows u < d stay -inf);
+  // beta: sv[s] = be[s] with sv[64 PPL, +NB) = -inf
+  float* tab = lds;
+  float* sv = lds;
+  if constexpr (FWD) {
+    for (int e = lane; e < (64 * PPL + NB) * TS; e += 64) tab[e] = -kInf;
+  } else if (lane < NB) {
+    sv[64 * PPL + lane] = -kInf;
+  }
+  float v[PPL];
+#pragma unroll
+  for (int r = 0; r < PPL; ++r) v[r] = (lane + 64 * r == (FWD ? 0 : nl)) ? 0.f : -kInf;
+  float* dst = (FWD ? a.nabd : a.nbbd) + (long long)b * (a.K + 1) * NPG;
+  if (!FWD) {
+#pragma unroll
+    for (int r = 0; r < PPL; ++r)
+      if (lane + 64 * r < NPG) dst[(long long)Kl * NPG + lane + 64 * r] = v[r] * kLn2;
+  }
+  // band rows N[s][0 .. kGrp] of group q for the lane's source positions
+  float4 gq[D][PPL][2];
+  auto bload = [&](int q, float4 (*g)[2]) {
+    const float4* row = (const float4*)(nb0 + (long long)min(max(q, 0), max(Q - 1, 0)) * NB * NPG);
+#pragma unroll
+    for (int r = 0; r < PPL; ++r) {
+      const int uc = min(lane + 64 * r, NPG - 1);
+      g[r][0] = row[2 * uc];
+      g[r][1] = row[2 * uc + 1];
+    }
+  };
+  auto step = [&](float4 (*g)[2], int q, int qn) {
+    if (FWD && q % NGc == 0) {  // a chunk starts here
+#pragma unroll
+      for (int r = 0; r < PPL; ++r)
+        if (lane + 64 * r < NPG) dst[(long long)(q / NGc) * NPG + lane + 64 * r] = v[r] * kLn2;
+    }
+    float n[PPL][NB];
+#pragma unroll
+    for (int r = 0; r < PPL; ++r) {
+      n[r][0] = g[r][0].x; n[r][1] = g[r][0].y; n[r][2] = g[r][0].z; n[r][3] = g[r][0].w;
+      n[r][4] = g[r][1].x; n[r][5] = g[r][1].y; n[r][6] = g[r][1].z; n[r][7] = g[r][1].w;
+    }
+    if constexpr (FWD) {
+#pragma unroll
+      for (int r = 0; r < PPL; ++r)
+#pragma unroll
+        for (int d = 0; d < NB; ++d) tab[(lane + 64 * r + d) * TS + d] = v[r] + n[r][d];
+    } else {
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) sv[lane + 64 * r] = v[r];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    float x[PPL][NB];
+#pragma unroll
+    for (int r = 0; r < PPL; ++r)
+#pragma unroll
+      for (int d = 0; d < NB; ++d)
+        x[r][d] = FWD ? tab[(lane + 64 * r) * TS + d] : n[r][d] + sv[lane + 64 * r + d];
+    bload(qn, g);
+#pragma unroll
+    for (int r = 0; r < PPL; ++r) {
+      float m = x[r][0];
+#pragma unroll
+      for (int d = 1; d < NB; ++d) m = fmaxf(m, x[r][d]);
+      const float ms = m == -kInf ? 0.f : m;
+      float sum = 0.f;
+#pragma unroll
+      for (int d = 0; d < NB; ++d) sum += __builtin_amdgcn_exp2f(x[r][d] - ms);
+      v[r] = lane + 64 * r < NPG ? ms + __builtin_amdgcn_logf(sum) : -kInf;
+    }
+    if (!FWD && q % NGc == 0) {  // beta at the chunk's first frame
+#pragma unroll
+      for (int r = 0; r < PPL; ++r)
+        if (lane + 64 * r < NPG) dst[(long long)(q / NGc) * NPG + lane + 64 * r] = v[r] * kLn2;
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  // alpha walks q = 0 .. Q-1, beta q = Q-1 .. 0
+  auto qof = [&](int n) { return FWD ? n : Q - 1 - n; };
+#pragma unroll
+  for (int d = 0; d < D; ++d) bload(qof(d), gq[d]);
+  const int nmain = Q - Q % D;
+  for (int n0 = 0; n0 < nmain; n0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) step(gq[d], qof(n0 + d), qof(n0 + d + D));
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (nmain + d < Q) step(gq[d], qof(nmain + d), qof(nmain + d));
+  if constexpr (FWD) {
+    float nv = -kInf;
+#pragma unroll
+    for (int r = 0; r < PPL; ++r)
+      if (lane + 64 * r == nl) nv = v[r] * kLn2;
+    nv = wmax_u(nv);
+    if (lane == 0) *s_num = (nl >= 0 && nl <= a.U) ? nv : -kInf;
+  }
 }
 
 template <int PPL>
@@ -499,16 +652,16 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
   __shared__ __attribute__((aligned(16))) float s_bc[2][64];
   __shared__ int s_bad;
   __shared__ float s_lz, s_num;
+  __shared__ float s_nv[2][(128 + kGrp + 1) * (kGrp + 2)];
   const int b = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const int Kl = (nf + a.L - 1) / a.L;  // live chunks
-  const int V = a.V, C = a.C, CP = a.CP, NPG = a.NPG;
+  const int V = a.V, C = a.C, CP = a.CP;
   const int nl = a.nlab[b];
   const float* rec0 = a.rec + (long long)b * a.K * kRec;
-  constexpr float kLn2 = 0.6931471805599453f;
 
   // any chunk out of the fast path's range (a weight not finite, or a frame
   // spanning more than kRange): the frame-serial kernels take the utterance
@@ -522,6 +675,7 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
     return;
   }
   if (threadIdx.x == 0) a.uflag[b] = 0;
+  CK_WSTAMP(2 * wave);
 
   if (wave == 0 && !a.local && !(a.dbg & 1)) {
     // ---- den alpha across chunks (lattices.py:379-496 in chunk steps)
@@ -622,132 +776,12 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
       }
       if (Kl & 1) step(rr[0], 0, false);
     }
-  } else if (wave == 2 && !(a.dbg & 2)) {
-    // ---- numerator alpha over frames (lattices.py:340-377), base-2 log space
-    constexpr int D = 8;
-    const float2* G0 = (const float2*)a.G + (long long)b * a.T * NPG;
-    float al[PPL];
-#pragma unroll
-    for (int r = 0; r < PPL; ++r) al[r] = (lane + 64 * r == 0) ? 0.f : -kInf;
-    float* dst = a.nabd + (long long)b * (a.K + 1) * NPG;
-    // rows in registers D frames ahead; unconditional loads (frame and
-    // position clamped) keep the compiler's vmcnt tracking exact
-    float2 gq[D][PPL];
-    auto gload = [&](int t, float2* g) {
-      const long long tt = min(t, max(nf - 1, 0));
-#pragma unroll
-      for (int r = 0; r < PPL; ++r) g[r] = G0[tt * NPG + min(lane + 64 * r, NPG - 1)];
-    };
-    int kb = 0;  // next chunk boundary index
-    auto step = [&](float2* g, int t, bool reload) {
-      if (t == kb * a.L) {
-#pragma unroll
-        for (int r = 0; r < PPL; ++r)
-          if (lane + 64 * r < NPG) dst[(long long)kb * NPG + lane + 64 * r] = al[r] * kLn2;
-        ++kb;
-      }
-      float gb[PPL], gl[PPL];
-#pragma unroll
-      for (int r = 0; r < PPL; ++r) {
-        const bool ok = lane + 64 * r < NPG;
-        gb[r] = ok ? g[r].x * kLog2e : -kInf;
-        gl[r] = ok ? g[r].y * kLog2e : -kInf;
-      }
-      if (reload) gload(t + D, g);
-      float prev = -kInf, nv[PPL];
-#pragma unroll
-      for (int r = 0; r < PPL; ++r) {
-        const float x = rot_prev(al[r]);  // lane 0 gets lane 63's
-        const float pv = lane == 0 ? prev : x;
-        prev = x;
-        nv[r] = lse2_b2(al[r] + gb[r], pv + gl[r]);
-      }
-#pragma unroll
-      for (int r = 0; r < PPL; ++r) al[r] = nv[r];
-    };
-    if (nf > 0) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) gload(d, gq[d]);
-      const int nmain = nf - nf % D;
-      for (int t0 = 0; t0 < nmain; t0 += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) step(gq[d], t0 + d, true);
-      }
-#pragma unroll
-      for (int d = 0; d < D; ++d)
-        if (nmain + d < nf) step(gq[d], nmain + d, false);
-    }
-    float nv = -kInf;
-#pragma unroll
-    for (int r = 0; r < PPL; ++r)
-      if (lane + 64 * r == nl) nv = al[r] * kLn2;
-    nv = wmax_u(nv);
-    if (lane == 0) s_num = (nl >= 0 && nl <= a.U) ? nv : -kInf;
+  } else if (wave == 2 && !(a.dbg & 2) && !(a.dbg & 128)) {
+    num_walk<PPL, true>(a, b, lane, nf, Kl, nl, s_nv[0], &s_num);
   } else if (wave == 3 && !(a.dbg & 2)) {
-    // ---- numerator beta (reverse of alignments.py:320-329), base-2 log space
-    constexpr int D = 8;
-    const float2* G0 = (const float2*)a.G + (long long)b * a.T * NPG;
-    float be[PPL];
-#pragma unroll
-    for (int r = 0; r < PPL; ++r) be[r] = (lane + 64 * r == nl) ? 0.f : -kInf;
-    float* dst = a.nbbd + (long long)b * (a.K + 1) * NPG;
-#pragma unroll
-    for (int r = 0; r < PPL; ++r)
-      if (lane + 64 * r < NPG) dst[(long long)Kl * NPG + lane + 64 * r] = be[r] * kLn2;
-    // row t: blank weight of u, weight of the arc into u+1; unconditional
-    // loads (frame and positions clamped)
-    float2 gq[D][PPL];
-    auto gload = [&](int t, float2* g) {
-      const long long tt = max(t, 0);
-#pragma unroll
-      for (int r = 0; r < PPL; ++r) {
-        const int u = lane + 64 * r;
-        g[r].x = G0[tt * NPG + min(u, NPG - 1)].x;
-        g[r].y = G0[tt * NPG + min(u + 1, NPG - 1)].y;
-      }
-    };
-    int kb = Kl - 1;  // next chunk boundary index (descending)
-    auto step = [&](float2* g, int t, bool reload) {
-      float gb[PPL], gl[PPL];
-#pragma unroll
-      for (int r = 0; r < PPL; ++r) {
-        const int u = lane + 64 * r;
-        gb[r] = u < NPG ? g[r].x * kLog2e : -kInf;
-        gl[r] = u + 1 < NPG ? g[r].y * kLog2e : -kInf;
-      }
-      if (reload) gload(t - D, g);
-      float nx[PPL], nv[PPL];
-#pragma unroll
-      for (int r = 0; r < PPL; ++r) nx[r] = rot_next(be[r]);  // lane 63 gets lane 0's
-#pragma unroll
-      for (int r = 0; r < PPL; ++r) {
-        // beta[u+1]: lane+1 of the same register; lane 63 -> lane 0 of r+1
-        const float nb = lane == 63 ? (r + 1 < PPL ? nx[r + 1 < PPL ? r + 1 : r] : -kInf)
-                                    : nx[r];
-        nv[r] = lse2_b2(gb[r] + be[r], gl[r] + nb);
-      }
-#pragma unroll
-      for (int r = 0; r < PPL; ++r) be[r] = nv[r];
-      if (t == kb * a.L) {
-#pragma unroll
-        for (int r = 0; r < PPL; ++r)
-          if (lane + 64 * r < NPG) dst[(long long)kb * NPG + lane + 64 * r] = be[r] * kLn2;
-        --kb;
-      }
-    };
-    if (nf > 0) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) gload(nf - 1 - d, gq[d]);
-      const int nmain = nf - nf % D;
-      for (int n0 = 0; n0 < nmain; n0 += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) step(gq[d], nf - 1 - (n0 + d), true);
-      }
-#pragma unroll
-      for (int d = 0; d < D; ++d)
-        if (nmain + d < nf) step(gq[d], nf - 1 - (nmain + d), false);
-    }
+    num_walk<PPL, false>(a, b, lane, nf, Kl, nl, s_nv[1], nullptr);
   }
+  CK_WSTAMP(2 * wave + 1);
   __syncthreads();
   if (threadIdx.x == 0) {
     const float lz = a.local ? 0.f : s_lz;
@@ -783,7 +817,7 @@ LT_DEVINL void store_dw(void* dW, long long e, float v) {
   else ((float*)dW)[e] = v;
 }
 
-template <bool BF16>
+template <bool BF16, int PPL>
 __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int b = blockIdx.x / a.K, k = blockIdx.x - (blockIdx.x / a.K) * a.K;
@@ -795,7 +829,7 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
   const int t0 = k * a.L;
   const int tend = min(t0 + a.L, a.T);
   const int t1 = max(t0, min(t0 + a.L, nf));
-  const int V = a.V, C = a.C, R = a.R, FR = a.FR, CP = a.CP, NPG = a.NPG;
+  const int V = a.V, C = a.C, R = a.R, FR = a.FR, CP = a.CP, NPG = a.NPG, NP = a.NP;
   float g = a.grad ? a.grad[b] : 1.f;
   const float lz = a.log_z[b], nm = a.num[b];
   if (!__builtin_isfinite(nm) || (!a.local && !__builtin_isfinite(lz))) g = 0.f;
@@ -806,6 +840,7 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
     return;
   }
   const int nt = t1 - t0;
+  CK_STAMP(0);
   // stage the chunk's live frames
   const long long off = e0 * (BF16 ? 2 : 4);
   dma_issue(a.W, off, (long long)nt * a.FB, lds_base_addr(lds), a.c_ni, lane, wave, 4);
@@ -821,6 +856,9 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
   gather_tables(a, b, labs, boff, loff, tid, blockDim.x);
   wait_vmcnt(0);
   __syncthreads();
+  CK_STAMP(1);
+  // every LDS load below is unconditional (clamped index, unused values
+  // masked afterwards): a load under a branch would pay its full latency
 
   if (wave == 0 && !a.local && !(a.dbg & 4)) {
     // ---- den alpha (lane p: alpha[p]); per frame a linear-space step with
@@ -828,34 +866,34 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
     // Lane (q, h): destination q+1, sources p in [16h, 16h+16) (+ p = 32
     // in h = 1), the blank self loop in h = 0; halves combined by permlane.
     const int q = lane & 31, h = lane >> 5;
+    const int qe = min(q, V - 1) + 1;
     float al = lane < C ? a.abd[((long long)b * (a.K + 1) + k) * CP + lane] : -kInf;
     for (int f = 0; f < nt; ++f) {
       if (lane < C) ad[f * CP + lane] = al;
       const unsigned char* fr = wch + f * a.FB;
       const float c = ldsw<BF16>(fr, 0);
       const float cl = c * kLog2e;
+      // transition weights first: they do not depend on alpha
+      float e[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) e[m] = lt_exp_off(ldsw<BF16>(fr, min(16 * h + m, C - 1) * R + qe), cl);
+      const float e32 = lt_exp_off(ldsw<BF16>(fr, min(32, C - 1) * R + qe), cl);
+      const float eb = lt_exp_off(ldsw<BF16>(fr, qe * R), cl);
       const float M = safe_max(wmax_u(lane < C ? al : -kInf));
-      if (lane < 36) buf[lane] = lane < C ? lt_exp(al - M) : 0.f;
+      if (lane < 36) buf[lane] = lane < C ? lt_exp(al - M) : 0.f;  // buf[p >= C] = 0
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       float s0 = 0.f, s1 = 0.f;
-      if (q < V) {
-        const int qe = q + 1;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 b4 = *(const float4*)(buf + 16 * h + 4 * g);
-          const int p0 = 16 * h + 4 * g;
-          s0 = __builtin_fmaf(b4.x, (p0 + 0 < C) ? lt_exp_off(ldsw<BF16>(fr, (p0 + 0) * R + qe), cl) : 0.f, s0);
-          s1 = __builtin_fmaf(b4.y, (p0 + 1 < C) ? lt_exp_off(ldsw<BF16>(fr, (p0 + 1) * R + qe), cl) : 0.f, s1);
-          s0 = __builtin_fmaf(b4.z, (p0 + 2 < C) ? lt_exp_off(ldsw<BF16>(fr, (p0 + 2) * R + qe), cl) : 0.f, s0);
-          s1 = __builtin_fmaf(b4.w, (p0 + 3 < C) ? lt_exp_off(ldsw<BF16>(fr, (p0 + 3) * R + qe), cl) : 0.f, s1);
-        }
-        if (h == 1) {
-          if (C > 32) s0 = __builtin_fmaf(buf[32], lt_exp_off(ldsw<BF16>(fr, 32 * R + qe), cl), s0);
-        } else {  // the blank self loop of qe
-          s1 = __builtin_fmaf(buf[qe], lt_exp_off(ldsw<BF16>(fr, qe * R), cl), s1);
-        }
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 b4 = *(const float4*)(buf + 16 * h + 4 * g4);
+        s0 = __builtin_fmaf(b4.x, e[4 * g4 + 0], s0);
+        s1 = __builtin_fmaf(b4.y, e[4 * g4 + 1], s1);
+        s0 = __builtin_fmaf(b4.z, e[4 * g4 + 2], s0);
+        s1 = __builtin_fmaf(b4.w, e[4 * g4 + 3], s1);
       }
+      // h = 1: source 32 (buf[32] = 0 unless C > 32); h = 0: the blank loop of qe
+      s0 = __builtin_fmaf(h ? buf[32] : buf[qe], h ? e32 : eb, s0);
       const float nq = M + c + lt_log(half_sum(s0 + s1));
       const float n0 = first_lane(al) + c;
       const float sh = from_prev(nq, -kInf);
@@ -867,133 +905,148 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
     // source j+1 over labels y in [16h+1, 16h+16], the blank in h = 0; every
     // lane also one term of state 0's sum
     const int j = lane & 31, h = lane >> 5;
+    const int pe = min(j, V - 1) + 1;
     float be = lane < C ? a.bbd[((long long)b * (a.K + 1) + k + 1) * CP + lane] : -kInf;
     for (int f = nt - 1; f >= 0; --f) {
       if (lane < C) bd[f * CP + lane] = be;
       const unsigned char* fr = wch + f * a.FB;
       const float c = ldsw<BF16>(fr, 0);
       const float cl = c * kLog2e;
+      float e[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) e[m] = lt_exp_off(ldsw<BF16>(fr, pe * R + min(16 * h + m + 1, V)), cl);
+      const float eb = lt_exp_off(ldsw<BF16>(fr, pe * R), cl);
+      const float e0y = lt_exp_off(ldsw<BF16>(fr, min(j, V - 1) + 1), cl);  // E[0][j+1]
       const float Mc = safe_max(wmax_u((lane >= 1 && lane < C) ? be : -kInf));
-      // buf[y-1] = exp(beta[y] - Mc) for core y
+      // buf[y-1] = exp(beta[y] - Mc) for core y; 0 past V
       if (lane >= 1 && lane <= 32) buf[lane - 1] = lane < C ? lt_exp(be - Mc) : 0.f;
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       float s0 = 0.f, s1 = 0.f;
-      if (j < V) {
-        const int pe = j + 1;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 b4 = *(const float4*)(buf + 16 * h + 4 * g);
-          const int y0 = 16 * h + 4 * g + 1;
-          s0 = __builtin_fmaf(b4.x, (y0 + 0 <= V) ? lt_exp_off(ldsw<BF16>(fr, pe * R + y0 + 0), cl) : 0.f, s0);
-          s1 = __builtin_fmaf(b4.y, (y0 + 1 <= V) ? lt_exp_off(ldsw<BF16>(fr, pe * R + y0 + 1), cl) : 0.f, s1);
-          s0 = __builtin_fmaf(b4.z, (y0 + 2 <= V) ? lt_exp_off(ldsw<BF16>(fr, pe * R + y0 + 2), cl) : 0.f, s0);
-          s1 = __builtin_fmaf(b4.w, (y0 + 3 <= V) ? lt_exp_off(ldsw<BF16>(fr, pe * R + y0 + 3), cl) : 0.f, s1);
-        }
-        if (h == 0) s0 = __builtin_fmaf(buf[j], lt_exp_off(ldsw<BF16>(fr, pe * R), cl), s0);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 b4 = *(const float4*)(buf + 16 * h + 4 * g4);
+        s0 = __builtin_fmaf(b4.x, e[4 * g4 + 0], s0);
+        s1 = __builtin_fmaf(b4.y, e[4 * g4 + 1], s1);
+        s0 = __builtin_fmaf(b4.z, e[4 * g4 + 2], s0);
+        s1 = __builtin_fmaf(b4.w, e[4 * g4 + 3], s1);
       }
+      const float bj = buf[j];
+      s0 = __builtin_fmaf(h ? 0.f : bj, eb, s0);
       const float nj = Mc + c + lt_log(half_sum(s0 + s1));  // lane j: beta'[j+1]
       // state 0: sum over labels y of E[0][y] exp(beta[y] - Mc), then its self loop
-      const float t0v = (lane < 32 && lane < V) ? buf[lane] * lt_exp_off(ldsw<BF16>(fr, lane + 1), cl) : 0.f;
+      const float t0v = lane < 32 ? bj * e0y : 0.f;
       const float n0 = lse2(first_lane(be) + c, Mc + c + lt_log(wsum_u(t0v)));
       const float sh = from_prev(nj, -kInf);
       be = lane == 0 ? n0 : (lane < C ? sh : -kInf);
       __builtin_amdgcn_wave_barrier();
     }
   } else if (wave == 2 && !(a.dbg & 8)) {
-    // ---- num alpha
-    float al[4];
+    // ---- num alpha (log space)
+    int bo[PPL], lo[PPL];
+    float al[PPL];
     const float* src = a.nabd + ((long long)b * (a.K + 1) + k) * NPG;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) al[r] = (r < a.PPL && lane + 64 * r < NPG) ? src[lane + 64 * r] : -kInf;
+    for (int r = 0; r < PPL; ++r) {
+      const int u = lane + 64 * r, uc = min(u, NPG - 1);
+      bo[r] = boff[uc];
+      lo[r] = max(loff[uc], 0);
+      const float v = src[uc];
+      al[r] = u < NPG ? v : -kInf;
+    }
     for (int f = 0; f < nt; ++f) {
       const unsigned char* fr = wch + f * a.FB;
-      float prev = -kInf, nv[4];
+      float prev = -kInf, nv[PPL];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (r < a.PPL) {
-          const int u = lane + 64 * r;
-          if (u < NPG) an[f * NPG + u] = al[r];
-          const float x = rot_prev(al[r]);
-          const float pv = lane == 0 ? prev : x;
-          prev = x;
-          const float gb = u < a.NP ? ldsw<BF16>(fr, boff[u]) : -kInf;
-          const int lo = u < NPG ? loff[u] : -1;
-          const float gl = lo >= 0 ? ldsw<BF16>(fr, lo) : -kInf;
-          nv[r] = lse2(al[r] + gb, pv + gl);
-        }
+      for (int r = 0; r < PPL; ++r) {
+        const int u = lane + 64 * r;
+        if (u < NPG) an[f * NPG + u] = al[r];
+        const float x = rot_prev(al[r]);
+        const float pv = lane == 0 ? prev : x;
+        prev = x;
+        const float wb = ldsw<BF16>(fr, bo[r]), wl = ldsw<BF16>(fr, lo[r]);
+        const float gb = u < NP ? wb : -kInf;
+        const float gl = (u >= 1 && u < NP) ? wl : -kInf;
+        nv[r] = lse2(al[r] + gb, pv + gl);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (r < a.PPL) al[r] = nv[r];
+      for (int r = 0; r < PPL; ++r) al[r] = nv[r];
       __builtin_amdgcn_wave_barrier();
     }
   } else if (wave == 3 && !(a.dbg & 8)) {
     // ---- num beta; bn[f] = beta_{f+1}
-    float be[4];
+    int bo[PPL], lo[PPL];
+    float be[PPL];
     const float* src = a.nbbd + ((long long)b * (a.K + 1) + k + 1) * NPG;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) be[r] = (r < a.PPL && lane + 64 * r < NPG) ? src[lane + 64 * r] : -kInf;
+    for (int r = 0; r < PPL; ++r) {
+      const int u = lane + 64 * r, uc = min(u, NPG - 1);
+      bo[r] = boff[uc];
+      lo[r] = max(loff[min(u + 1, NPG - 1)], 0);  // the arc into u+1
+      const float v = src[uc];
+      be[r] = u < NPG ? v : -kInf;
+    }
     for (int f = nt - 1; f >= 0; --f) {
       const unsigned char* fr = wch + f * a.FB;
-      float nxt[4], nv[4];
+      float nx[PPL], nv[PPL];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) nxt[r] = rot_next(be[r]);
+      for (int r = 0; r < PPL; ++r) nx[r] = rot_next(be[r]);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (r < a.PPL) {
-          const int u = lane + 64 * r;
-          if (u < NPG) bn[f * NPG + u] = be[r];
-          const float nb = lane == 63 ? (r + 1 < a.PPL ? nxt[r + 1 < 4 ? r + 1 : 3] : -kInf) : nxt[r];
-          const float gb = u < a.NP ? ldsw<BF16>(fr, boff[u]) : -kInf;
-          const int lo = u + 1 < NPG ? loff[u + 1] : -1;
-          const float gl = lo >= 0 ? ldsw<BF16>(fr, lo) : -kInf;
-          nv[r] = lse2(gb + be[r], gl + nb);
-        }
+      for (int r = 0; r < PPL; ++r) {
+        const int u = lane + 64 * r;
+        if (u < NPG) bn[f * NPG + u] = be[r];
+        const float nb = lane == 63 ? (r + 1 < PPL ? nx[r + 1 < PPL ? r + 1 : r] : -kInf) : nx[r];
+        const float wb = ldsw<BF16>(fr, bo[r]), wl = ldsw<BF16>(fr, lo[r]);
+        const float gb = u < NP ? wb : -kInf;
+        const float gl = u + 1 < NP ? wl : -kInf;
+        nv[r] = lse2(gb + be[r], gl + nb);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (r < a.PPL) be[r] = nv[r];
+      for (int r = 0; r < PPL; ++r) be[r] = nv[r];
       __builtin_amdgcn_wave_barrier();
     }
   }
   __syncthreads();
+  CK_STAMP(2);
 
   // ---- marginals, one wave per frame: den - num, each normalised by its
   // frame total (alignments.py:311-317; numerator: reverse of :320-329).
-  // Element e = lane + 64 m of a frame is arc (p, y) into q = y ? y : p;
-  // p and q packed per m once.
+  // Element e = lane + 64 m of a frame is arc (p, y) into q = y ? y : p.
   constexpr int MFX = 18;  // ceil(33 * 33 / 64)
-  const int MF = (FR + 63) / 64;
-  int pq[MFX];
+  int pq[MFX];             // p | q << 8 of the (clamped) element
 #pragma unroll
   for (int m = 0; m < MFX; ++m) {
-    const int e = lane + 64 * m;
+    const int e = min(lane + 64 * m, FR - 1);
     const int p = e / R, y = e - p * R;
-    pq[m] = (m < MF && e < FR) ? (p | ((y ? y : p) << 8)) : -1;
+    pq[m] = p | ((y ? y : p) << 8);
+  }
+  int bo[PPL], lo[PPL];
+#pragma unroll
+  for (int r = 0; r < PPL; ++r) {
+    const int uc = min(lane + 64 * r, NP - 1);
+    bo[r] = boff[uc];
+    lo[r] = max(loff[uc], 0);
   }
   for (int f = (a.dbg & 16) ? nt : wave; f < nt; f += 4) {
     const unsigned char* fr = wch + f * a.FB;
     float* fb = BF16 ? (float*)(lds + a.c_off_fb) + wave * ((FR + 3) & ~3) : (float*)fr;
     // numerator terms first (they read W)
-    float sb[4], sl[4];
+    float sb[PPL], sl[PPL];
     float mxn = -kInf;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      sb[r] = -kInf;
-      sl[r] = -kInf;
-      const int u = lane + 64 * r;
-      if (r < a.PPL && u < a.NP) {
-        const float bu = bn[f * NPG + u];
-        sb[r] = an[f * NPG + u] + ldsw<BF16>(fr, boff[u]) + bu;
-        if (u >= 1) sl[r] = an[f * NPG + u - 1] + ldsw<BF16>(fr, loff[u]) + bu;
-        mxn = fmaxf(mxn, fmaxf(sb[r], sl[r]));
-      }
+    for (int r = 0; r < PPL; ++r) {
+      const int u = lane + 64 * r, uc = min(u, NP - 1);
+      const float bu = bn[f * NPG + uc];
+      const float tb = an[f * NPG + uc] + ldsw<BF16>(fr, bo[r]) + bu;
+      const float tl = an[f * NPG + max(uc - 1, 0)] + ldsw<BF16>(fr, lo[r]) + bu;
+      sb[r] = u < NP ? tb : -kInf;
+      sl[r] = (u >= 1 && u < NP) ? tl : -kInf;
+      mxn = fmaxf(mxn, fmaxf(sb[r], sl[r]));
     }
     mxn = safe_max(wmax_u(mxn));
     float zn = 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < PPL; ++r) {
       sb[r] = lt_exp(sb[r] - mxn);
       sl[r] = lt_exp(sl[r] - mxn);
       zn += sb[r] + sl[r];
@@ -1003,15 +1056,20 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
     if (!a.local) {
       const float* adf = ad + f * CP;
       const float* bdf = bd + f * CP;
-      float sv[MFX];
+      // the three operand reads staged separately so they issue back to back
+      float sv[MFX], xa[MFX], xb[MFX];
+#pragma unroll
+      for (int m = 0; m < MFX; ++m) sv[m] = ldsw<BF16>(fr, min(lane + 64 * m, FR - 1));
+#pragma unroll
+      for (int m = 0; m < MFX; ++m) xa[m] = adf[pq[m] & 255];
+#pragma unroll
+      for (int m = 0; m < MFX; ++m) xb[m] = bdf[pq[m] >> 8];
       float mx = -kInf;
 #pragma unroll
       for (int m = 0; m < MFX; ++m) {
-        sv[m] = -kInf;
-        if (pq[m] >= 0) {
-          sv[m] = adf[pq[m] & 255] + ldsw<BF16>(fr, lane + 64 * m) + bdf[pq[m] >> 8];
-          mx = fmaxf(mx, sv[m]);
-        }
+        const float v = xa[m] + sv[m] + xb[m];
+        sv[m] = lane + 64 * m < FR ? v : -kInf;
+        mx = fmaxf(mx, sv[m]);
       }
       mx = safe_max(wmax_u(mx));
       float z = 0.f;
@@ -1026,7 +1084,7 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int m = 0; m < MFX; ++m)
-        if (pq[m] >= 0) fb[lane + 64 * m] = sv[m] * gd;
+        if (lane + 64 * m < FR) fb[lane + 64 * m] = sv[m] * gd;
     } else {
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
@@ -1034,18 +1092,51 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
     }
     // string arcs sharing a lattice arc meet here (LDS adds, lane order)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < PPL; ++r) {
       const int u = lane + 64 * r;
-      if (r < a.PPL && u < a.NP) {
-        atomicAdd(fb + boff[u], -sb[r] * gn);
-        if (u >= 1) atomicAdd(fb + loff[u], -sl[r] * gn);
+      if (u < NP) {
+        atomicAdd(fb + bo[r], -sb[r] * gn);
+        if (u >= 1) atomicAdd(fb + lo[r], -sl[r] * gn);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     const long long eb = e0 + (long long)f * FR;
-    for (int e = lane; e < FR; e += 64) store_dw<BF16>(a.dW, eb + e, fb[e]);
+    if constexpr (BF16) {  // the frame's dW, rounded once, over its own W bytes
+      float ov[MFX];
+#pragma unroll
+      for (int m = 0; m < MFX; ++m) ov[m] = fb[min(lane + 64 * m, FR - 1)];
+      unsigned short* fo = (unsigned short*)fr;
+#pragma unroll
+      for (int m = 0; m < MFX; ++m)
+        if (lane + 64 * m < FR) fo[lane + 64 * m] = f2bf(ov[m]);
+    }
+    (void)eb;
   }
+  // the chunk's dW sits in LDS in place of its W: one streaming pass of
+  // 16-byte stores (scalar stores only at the unaligned head and tail)
+  __syncthreads();
+  CK_STAMP(3);
+  {
+    const long long es = BF16 ? 2 : 4;
+    const long long bytes = (long long)nt * a.FB;
+    unsigned char* gdst = (unsigned char*)a.dW + off;  // same byte offset as W
+    const long long head = min((long long)((16 - (off & 15)) & 15), bytes);
+    const long long body = (bytes - head) & ~15LL;
+    const unsigned char* src = wch;  // LDS image, (off & 15)-shifted like W
+    for (long long x = tid; x < head / es; x += blockDim.x) {
+      if constexpr (BF16) ((unsigned short*)gdst)[x] = ((const unsigned short*)src)[x];
+      else ((float*)gdst)[x] = ((const float*)src)[x];
+    }
+    const uint4* s16 = (const uint4*)(src + head);
+    uint4* d16 = (uint4*)(gdst + head);
+    for (long long x = tid; x < body / 16; x += blockDim.x) d16[x] = s16[x];
+    for (long long x = head + body + tid * es; x < bytes; x += blockDim.x * es) {
+      if constexpr (BF16) *(unsigned short*)(gdst + x) = *(const unsigned short*)(src + x);
+      else *(float*)(gdst + x) = *(const float*)(src + x);
+    }
+  }
+  CK_STAMP(4);
   // padding frames of this chunk
   {
     const long long n = (long long)(tend - t1) * FR;
@@ -1071,8 +1162,8 @@ int al16(long long x) { return (int)((x + 15) & ~15LL); }
 struct CkLayout {
   // state (kept from lt_chunk_forward to lt_chunk_backward)
   size_t uflag, lz, num, abd, bbd, nabd, nbbd, state;
-  // scratch: forward = records + G; backward = the fallback's checkpoints
-  size_t rec, G, f_alpha, f_an, f_loss, f_lz, f_num, f_side, scratch;
+  // scratch: forward = records + numerator bands; backward = the fallback's checkpoints
+  size_t rec, nb, f_alpha, f_an, f_loss, f_lz, f_num, f_side, scratch;
 };
 
 int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
@@ -1087,6 +1178,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   a->local = local_norm ? 1 : 0;
 #ifdef LT_DIAG
   a->dbg = ck_env("LT_CK_DBG", 0);
+  if (const char* sp = getenv("LT_CK_STAMPS")) a->stamps = (long long*)strtoull(sp, nullptr, 0);
 #endif
   a->FB = (long long)a->FR * es;
   // A: per wave a ring of frame slots, the state-0 row and the gather tables
@@ -1128,6 +1220,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   c_bytes(L, a);
   a->L = L;
   a->K = std::max(1, (a->T + L - 1) / L);
+  a->NGc = (L + kGrp - 1) / kGrp;
   // workspace
   const long long B = a->B, K = a->K, T = a->T;
   size_t o = 0;
@@ -1141,7 +1234,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   w->state = o;
   size_t s = 0;
   w->rec = s; s += up256(4LL * B * K * kRec);
-  w->G = s; s += up256(8LL * B * T * a->NPG);
+  w->nb = s; s += up256(4LL * B * K * a->NGc * (kGrp + 1) * a->NPG);
   const size_t fwd = s;
   s = 0;
   w->f_alpha = s; s += up256(4LL * B * T * a->C);
@@ -1165,7 +1258,7 @@ void ck_bind(CkArgs* a, const CkLayout& w, void* state, void* scratch) {
   a->nabd = (float*)(st + w.nabd);
   a->nbbd = (float*)(st + w.nbbd);
   a->rec = sc ? (float*)(sc + w.rec) : nullptr;
-  a->G = sc ? (float*)(sc + w.G) : nullptr;
+  a->nb = sc ? (float*)(sc + w.nb) : nullptr;
 }
 
 int ck_launch(const void* k, int grid, int lds, hipStream_t st, const CkArgs& a) {
@@ -1283,9 +1376,11 @@ int lt_chunk_backward(const lt_problem* pb, int32_t local_norm, const void* W,
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const int lds_c = a.c_off_fb + (bf16 ? 4 * 4 * ((a.FR + 3) & ~3) : 0);
-  if ((rc = ck_launch(bf16 ? (const void*)ck_marg_kernel<true> : (const void*)ck_marg_kernel<false>,
-                      a.B * a.K, lds_c, st, a)))
-    return rc;
+  const void* kc = a.PPL == 1 ? (bf16 ? (const void*)ck_marg_kernel<true, 1>
+                                      : (const void*)ck_marg_kernel<false, 1>)
+                              : (bf16 ? (const void*)ck_marg_kernel<true, 2>
+                                      : (const void*)ck_marg_kernel<false, 2>);
+  if ((rc = ck_launch(kc, a.B * a.K, lds_c, st, a))) return rc;
   char* sc = (char*)scratch;
   return lt_impl::serial_loss(pb, local_norm, W, num_frames, labels, num_labels, a.uflag,
                               (float*)(sc + w.f_loss), (float*)(sc + w.f_lz),
