@@ -319,7 +319,6 @@ def loss_grad(W, num_frames, labels, num_labels, vocab_size, context_size, local
   if workspace is None or workspace.numel() < ws_bytes.value:
     workspace = torch.empty([max(ws_bytes.value, 1)], dtype=torch.uint8, device=W.device)
   loss, log_z, num = _f32([B], W), _f32([B], W), _f32([B], W)
-  log_z.zero_()
   dW = torch.empty_like(W)
   _check(lib().lt_loss_grad(ctypes.byref(pb), int(bool(local_norm)), _ptr(W), _ptr(num_frames),
                             _ptr(labels), _ptr(num_labels), _ptr(loss), _ptr(log_z), _ptr(num),

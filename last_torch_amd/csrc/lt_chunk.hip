@@ -53,8 +53,10 @@ namespace {
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr float kRange = 60.f;  // max - min of a frame's weights on the fast path
+constexpr float kLn2 = 0.6931471805599453f;
 constexpr int kRec = 1224;      // floats per chunk record (16-byte multiple)
 constexpr int kRowT = 36;       // row stride of the transposed core in a record
+constexpr int kMargWaves = 4;   // phase C: waves per workgroup (recursions on 0-3)
 constexpr int kGrp = 7;         // frames per numerator group (band offsets 0..kGrp)
 // record layout (floats): [0, 1152) X^T rows: rec[i * 36 + j] = X[i][j] =
 // P_scaled[j][i] (start core state j -> end core state i); [1152, 1184)
@@ -78,6 +80,7 @@ struct CkArgs {
   float* bbd;              // [B,K+1,CP] den beta at chunk starts
   float* nabd;             // [B,K+1,NPG] num alpha at chunk starts
   float* nbbd;             // [B,K+1,NPG] num beta at chunk starts
+  float* cf;               // [B,T] frame offsets c_t = ceil(max W_t) (phase A's)
   float* loss;
   float* log_z;            // state copies (read by C)
   float* num;
@@ -96,7 +99,7 @@ struct CkArgs {
   // phase B LDS carve
   int b_ni, b_slots, b_off_ra, b_off_rb, b_off_ga, b_off_gb, b_gslots, b_gslot, b_off_buf;
   // phase C LDS carve
-  int c_ni, c_off_ad, c_off_bd, c_off_an, c_off_bn, c_off_tab, c_off_buf, c_off_fb;
+  int c_ni, c_off_ad, c_off_bd, c_off_an, c_off_bn, c_off_tab, c_off_cf, c_off_buf, c_off_fb;
 };
 
 // lanes l and l ^ 32 combined (v_permlane32_swap: both halves get both)
@@ -131,12 +134,12 @@ LT_DEVINL float safe_max(float m) { return __builtin_isfinite(m) ? m : 0.f; }
 #ifdef LT_DIAG
 #define CK_STAMP(k)                                                                  \
   do {                                                                               \
-    if (a.stamps && !(a.dbg & 64) && threadIdx.x == 0)                                                \
+    if (a.stamps && !(a.dbg & 64) && threadIdx.x == 0)                               \
       a.stamps[(long long)blockIdx.x * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 #define CK_WSTAMP(k)                                                                 \
   do {                                                                               \
-    if (a.stamps && (a.dbg & 64) && (threadIdx.x & 63) == 0)                                         \
+    if (a.stamps && (a.dbg & 64) && (threadIdx.x & 63) == 0)                         \
       a.stamps[(long long)blockIdx.x * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
@@ -404,6 +407,7 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
     if (!(mx - mn <= kRange) || !__builtin_isfinite(mx) || !__builtin_isfinite(mn)) bad = 1;
     const float c = __builtin_isfinite(mx) ? ceilf(mx) : 0.f;
     const float cl = c * kLog2e;
+    if (lane == 0) a.cf[(long long)b * a.T + t0 + f] = c;
     // E_t^T as the A operand: lane (i, h), k-step s -> E[k][i]; the core
     // diagonal also carries the blank self loop (alignments.py:294-297)
     const float dgv = lt_exp_off(F.wdg, cl);
@@ -534,7 +538,6 @@ LT_DEVINL void load_rec_beta(const float* rc, int lane, RecBeta& r) {
 template <int PPL, bool FWD>
 LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl, float* lds,
                         float* s_num) {
-  constexpr float kLn2 = 0.6931471805599453f;
   const int NPG = a.NPG;
   // ---- numerator over the groups of kGrp frames (phase A's bands), base-2
   // log space. alpha (wave 2, lattices.py:340-377 composed per group):
@@ -818,7 +821,7 @@ LT_DEVINL void store_dw(void* dW, long long e, float v) {
 }
 
 template <bool BF16, int PPL>
-__global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
+__global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kernel(const CkArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int b = blockIdx.x / a.K, k = blockIdx.x - (blockIdx.x / a.K) * a.K;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -843,7 +846,7 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
   CK_STAMP(0);
   // stage the chunk's live frames
   const long long off = e0 * (BF16 ? 2 : 4);
-  dma_issue(a.W, off, (long long)nt * a.FB, lds_base_addr(lds), a.c_ni, lane, wave, 4);
+  dma_issue(a.W, off, (long long)nt * a.FB, lds_base_addr(lds), a.c_ni, lane, wave, kMargWaves);
   const unsigned char* wch = lds + (off & 15);
   float* ad = (float*)(lds + a.c_off_ad);  // [L][CP] alpha_t (log)
   float* bd = (float*)(lds + a.c_off_bd);  // [L][CP] beta_{t+1}
@@ -853,6 +856,8 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
   int* loff = boff + NPG;
   int* labs = loff + NPG;
   float* buf = (float*)(lds + a.c_off_buf) + 64 * wave;
+  float* cfl = (float*)(lds + a.c_off_cf);
+  if (tid < nt) cfl[tid] = a.cf[(long long)b * a.T + t0 + tid];
   gather_tables(a, b, labs, boff, loff, tid, blockDim.x);
   wait_vmcnt(0);
   __syncthreads();
@@ -861,26 +866,36 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
   // masked afterwards): a load under a branch would pay its full latency
 
   if (wave == 0 && !a.local && !(a.dbg & 4)) {
-    // ---- den alpha (lane p: alpha[p]); per frame a linear-space step with
-    // the frame's W[0][0] as offset (range <= kRange) and the vector's max.
-    // Lane (q, h): destination q+1, sources p in [16h, 16h+16) (+ p = 32
-    // in h = 1), the blank self loop in h = 0; halves combined by permlane.
+    // ---- den alpha in scaled linear space. Lane p in [1, V]: alpha[p] =
+    // al 2^S, renormalised every frame by a power of two so that state 1
+    // sits in [1/2, 1) (readfirstlane + frexp: no reduction on the chain).
+    // With E = exp(W - c), c = ceil(max W) (phase A's), every E is in
+    // [e^-61, 1] and the frame range bound keeps every core value within
+    // ~2^89 of state 1. The start state (only its blank loop in-arc) is a
+    // log2 scalar a0 beside the chain. Lane (q, h): destination q+1,
+    // sources p in [16h, 16h+16) (+ p = 32 in h = 1), the blank self loop
+    // in h = 0; halves combined by permlane.
     const int q = lane & 31, h = lane >> 5;
     const int qe = min(q, V - 1) + 1;
-    float al = lane < C ? a.abd[((long long)b * (a.K + 1) + k) * CP + lane] : -kInf;
+    const bool core = lane >= 1 && lane <= V;
+    const float x0 = lane < C ? a.abd[((long long)b * (a.K + 1) + k) * CP + lane] * kLog2e : -kInf;
+    float a0 = first_lane(x0);
+    float S = wmax_u(core ? x0 : -kInf);  // -inf: no core state reached yet
+    float al = (core && S != -kInf) ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     for (int f = 0; f < nt; ++f) {
-      if (lane < C) ad[f * CP + lane] = al;
+      if (lane < C) ad[f * CP + lane] = (lane == 0 ? a0 : S + __builtin_amdgcn_logf(al)) * kLn2;
       const unsigned char* fr = wch + f * a.FB;
-      const float c = ldsw<BF16>(fr, 0);
-      const float cl = c * kLog2e;
+      const float cl = cfl[f] * kLog2e;
+      const float w00 = ldsw<BF16>(fr, 0);
       // transition weights first: they do not depend on alpha
       float e[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) e[m] = lt_exp_off(ldsw<BF16>(fr, min(16 * h + m, C - 1) * R + qe), cl);
       const float e32 = lt_exp_off(ldsw<BF16>(fr, min(32, C - 1) * R + qe), cl);
       const float eb = lt_exp_off(ldsw<BF16>(fr, qe * R), cl);
-      const float M = safe_max(wmax_u(lane < C ? al : -kInf));
-      if (lane < 36) buf[lane] = lane < C ? lt_exp(al - M) : 0.f;  // buf[p >= C] = 0
+      const float M = fmaxf(a0, S);  // a0 is finite on the fast path
+      const float u = __builtin_amdgcn_exp2f(S - M), t = __builtin_amdgcn_exp2f(a0 - M);
+      if (lane < 36) buf[lane] = lane == 0 ? t : al * u;  // buf[p > V] = 0
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       float s0 = 0.f, s1 = 0.f;
@@ -894,32 +909,39 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
       }
       // h = 1: source 32 (buf[32] = 0 unless C > 32); h = 0: the blank loop of qe
       s0 = __builtin_fmaf(h ? buf[32] : buf[qe], h ? e32 : eb, s0);
-      const float nq = M + c + lt_log(half_sum(s0 + s1));
-      const float n0 = first_lane(al) + c;
-      const float sh = from_prev(nq, -kInf);
-      al = lane == 0 ? n0 : (lane < C ? sh : -kInf);
+      const float sq = half_sum(s0 + s1);  // lane q: alpha'[q+1] / (2^M e^c)
+      int ex;
+      (void)frexpf(first_lane(sq), &ex);  // state 1: > 0 on the fast path
+      S = M + cl + (float)ex;
+      a0 += w00 * kLog2e;
+      const float sh = from_prev(ldexpf(sq, -ex), 0.f);
+      al = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
     }
   } else if (wave == 1 && !a.local && !(a.dbg & 4)) {
-    // ---- den beta (lane p: beta[p]); bd[f] = beta_{f+1}. Lane (j, h): core
-    // source j+1 over labels y in [16h+1, 16h+16], the blank in h = 0; every
-    // lane also one term of state 0's sum
+    // ---- den beta, the same scaled linear space; bd[f] = beta_{f+1}. Lane
+    // (j, h): core source j+1 over labels y in [16h+1, 16h+16], the blank in
+    // h = 0; every lane also one term of the start state's sum (log2 scalar
+    // b0: no core state depends on it).
     const int j = lane & 31, h = lane >> 5;
     const int pe = min(j, V - 1) + 1;
-    float be = lane < C ? a.bbd[((long long)b * (a.K + 1) + k + 1) * CP + lane] : -kInf;
+    const bool core = lane >= 1 && lane <= V;
+    const float x0 = lane < C ? a.bbd[((long long)b * (a.K + 1) + k + 1) * CP + lane] * kLog2e : -kInf;
+    float b0 = first_lane(x0);
+    float S = safe_max(wmax_u(core ? x0 : -kInf));
+    float be = core ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     for (int f = nt - 1; f >= 0; --f) {
-      if (lane < C) bd[f * CP + lane] = be;
+      if (lane < C) bd[f * CP + lane] = (lane == 0 ? b0 : S + __builtin_amdgcn_logf(be)) * kLn2;
       const unsigned char* fr = wch + f * a.FB;
-      const float c = ldsw<BF16>(fr, 0);
-      const float cl = c * kLog2e;
+      const float cl = cfl[f] * kLog2e;
+      const float w00 = ldsw<BF16>(fr, 0);
       float e[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) e[m] = lt_exp_off(ldsw<BF16>(fr, pe * R + min(16 * h + m + 1, V)), cl);
       const float eb = lt_exp_off(ldsw<BF16>(fr, pe * R), cl);
       const float e0y = lt_exp_off(ldsw<BF16>(fr, min(j, V - 1) + 1), cl);  // E[0][j+1]
-      const float Mc = safe_max(wmax_u((lane >= 1 && lane < C) ? be : -kInf));
-      // buf[y-1] = exp(beta[y] - Mc) for core y; 0 past V
-      if (lane >= 1 && lane <= 32) buf[lane - 1] = lane < C ? lt_exp(be - Mc) : 0.f;
+      // buf[y-1] = beta[y] (scaled) for core y; 0 past V
+      if (lane >= 1 && lane <= 32) buf[lane - 1] = be;
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       float s0 = 0.f, s1 = 0.f;
@@ -933,12 +955,15 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
       }
       const float bj = buf[j];
       s0 = __builtin_fmaf(h ? 0.f : bj, eb, s0);
-      const float nj = Mc + c + lt_log(half_sum(s0 + s1));  // lane j: beta'[j+1]
-      // state 0: sum over labels y of E[0][y] exp(beta[y] - Mc), then its self loop
-      const float t0v = lane < 32 ? bj * e0y : 0.f;
-      const float n0 = lse2(first_lane(be) + c, Mc + c + lt_log(wsum_u(t0v)));
-      const float sh = from_prev(nj, -kInf);
-      be = lane == 0 ? n0 : (lane < C ? sh : -kInf);
+      const float sj = half_sum(s0 + s1);  // lane j: beta'[j+1] / (2^S e^c)
+      // start state: (+)_y E[0][y] beta[y], then its own blank loop
+      const float r0 = wsum_u(lane < 32 ? bj * e0y : 0.f);
+      b0 = lse2_b2(b0 + w00 * kLog2e, S + cl + __builtin_amdgcn_logf(r0));
+      int ex;
+      (void)frexpf(first_lane(sj), &ex);
+      S = S + cl + (float)ex;
+      const float sh = from_prev(ldexpf(sj, -ex), 0.f);
+      be = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
     }
   } else if (wave == 2 && !(a.dbg & 8)) {
@@ -1027,7 +1052,7 @@ __global__ __launch_bounds__(256, 2) void ck_marg_kernel(const CkArgs a) {
     bo[r] = boff[uc];
     lo[r] = max(loff[uc], 0);
   }
-  for (int f = (a.dbg & 16) ? nt : wave; f < nt; f += 4) {
+  for (int f = (a.dbg & 16) ? nt : wave; f < nt; f += kMargWaves) {
     const unsigned char* fr = wch + f * a.FB;
     float* fb = BF16 ? (float*)(lds + a.c_off_fb) + wave * ((FR + 3) & ~3) : (float*)fr;
     // numerator terms first (they read W)
@@ -1161,7 +1186,7 @@ int al16(long long x) { return (int)((x + 15) & ~15LL); }
 
 struct CkLayout {
   // state (kept from lt_chunk_forward to lt_chunk_backward)
-  size_t uflag, lz, num, abd, bbd, nabd, nbbd, state;
+  size_t uflag, lz, num, abd, bbd, nabd, nbbd, cf, state;
   // scratch: forward = records + numerator bands; backward = the fallback's checkpoints
   size_t rec, nb, f_alpha, f_an, f_loss, f_lz, f_num, f_side, scratch;
 };
@@ -1210,8 +1235,9 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
     t->c_off_an = off; off += al16(4LL * L * a->NPG);
     t->c_off_bn = off; off += al16(4LL * L * a->NPG);
     t->c_off_tab = off; off += al16(8LL * a->NPG + 4LL * a->U);
+    t->c_off_cf = off; off += al16(4LL * L);
     t->c_off_buf = off; off += 4 * 64 * 4;
-    t->c_off_fb = off; off += bf16 ? 4 * 4 * ((a->FR + 3) & ~3) : 0;
+    t->c_off_fb = off; off += bf16 ? kMargWaves * 4 * ((a->FR + 3) & ~3) : 0;
     return off;
   };
   int L = std::max(1, std::min(32, ck_env("LT_CHUNK_LEN", 32)));
@@ -1231,6 +1257,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   w->bbd = o; o += up256(4 * B * (K + 1) * a->CP);
   w->nabd = o; o += up256(4 * B * (K + 1) * a->NPG);
   w->nbbd = o; o += up256(4 * B * (K + 1) * a->NPG);
+  w->cf = o; o += up256(4 * B * T);
   w->state = o;
   size_t s = 0;
   w->rec = s; s += up256(4LL * B * K * kRec);
@@ -1257,16 +1284,18 @@ void ck_bind(CkArgs* a, const CkLayout& w, void* state, void* scratch) {
   a->bbd = (float*)(st + w.bbd);
   a->nabd = (float*)(st + w.nabd);
   a->nbbd = (float*)(st + w.nbbd);
+  a->cf = (float*)(st + w.cf);
   a->rec = sc ? (float*)(sc + w.rec) : nullptr;
   a->nb = sc ? (float*)(sc + w.nb) : nullptr;
 }
 
-int ck_launch(const void* k, int grid, int lds, hipStream_t st, const CkArgs& a) {
+int ck_launch(const void* k, int grid, int lds, hipStream_t st, const CkArgs& a,
+              int threads = 256) {
   if (grid <= 0) return LT_OK;
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   void* args[] = {(void*)&a};
-  e = hipLaunchKernel(k, dim3(grid), dim3(256), args, lds, st);
+  e = hipLaunchKernel(k, dim3(grid), dim3(threads), args, lds, st);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;
@@ -1284,6 +1313,29 @@ int ck_check(const lt_problem* pb) {
   return LT_OK;
 }
 
+const void* ck_kernel_a(int ppl, bool bf16) {
+  return ppl == 1 ? (bf16 ? (const void*)ck_transfer_kernel<true, 1>
+                          : (const void*)ck_transfer_kernel<false, 1>)
+                  : (bf16 ? (const void*)ck_transfer_kernel<true, 2>
+                          : (const void*)ck_transfer_kernel<false, 2>);
+}
+const void* ck_kernel_b(int ppl) {
+  return ppl == 1 ? (const void*)ck_combine_kernel<1> : (const void*)ck_combine_kernel<2>;
+}
+const void* ck_kernel_c(int ppl, bool bf16) {
+  return ppl == 1 ? (bf16 ? (const void*)ck_marg_kernel<true, 1>
+                          : (const void*)ck_marg_kernel<false, 1>)
+                  : (bf16 ? (const void*)ck_marg_kernel<true, 2>
+                          : (const void*)ck_marg_kernel<false, 2>);
+}
+int ck_lds_c(const CkArgs& a, bool bf16) {
+  int lds = a.c_off_fb + (bf16 ? kMargWaves * 4 * ((a.FR + 3) & ~3) : 0);
+#ifdef LT_DIAG
+  lds += ck_env("LT_CK_LDS_PAD", 0);  // occupancy experiments
+#endif
+  return lds;
+}
+
 }  // namespace
 
 namespace lt_impl {
@@ -1294,6 +1346,46 @@ bool chunk_eligible(const lt_problem* pb) {
   const long long C = pb->vocab_size + 1;
   if ((long long)pb->batch * pb->max_frames * C * C >= (1LL << 31)) return false;
   return true;
+}
+}  // namespace lt_impl
+
+namespace lt_impl {
+// lt_loss_grad's chunked route: A, B and C, then ONE frame-serial call for
+// the utterances outside the fast path's range (it writes their loss, log_z,
+// num and dW; its workgroups return at once for every other utterance).
+// `state` / `scratch` as lt_chunk_workspace_bytes; the scratch's records
+// and bands are dead once B has run, so the fallback reuses the region.
+int chunk_loss_grad(const lt_problem* pb, int local_norm, const void* W, const int32_t* num_frames,
+                    const int32_t* labels, const int32_t* num_labels, float* loss, float* log_z,
+                    float* num, void* dW, void* state, size_t state_bytes, void* scratch,
+                    size_t scratch_bytes, void* stream) {
+  int rc = ck_check(pb);
+  if (rc) return rc;
+  if (pb->batch == 0) return LT_OK;
+  CkArgs a;
+  CkLayout w;
+  if ((rc = ck_plan(pb, local_norm, &a, &w))) return rc;
+  if (state_bytes < w.state || scratch_bytes < w.scratch)
+    return set_error(LT_EINVAL, "workspace too small");
+  ck_bind(&a, w, state, scratch);
+  a.W = (const unsigned char*)W;
+  a.nfr = num_frames; a.labels = labels; a.nlab = num_labels;
+  a.loss = loss;
+  a.lz_out = log_z;
+  a.num_out = num;
+  a.dW = dW;
+  hipStream_t st = (hipStream_t)stream;
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  if ((rc = ck_launch(ck_kernel_a(a.PPL, bf16), (int)(((long long)a.B * a.K + 3) / 4), 0, st, a)))
+    return rc;
+  if ((rc = ck_launch(ck_kernel_b(a.PPL), a.B, 0, st, a))) return rc;
+  if ((rc = ck_launch(ck_kernel_c(a.PPL, bf16), a.B * a.K, ck_lds_c(a, bf16), st, a,
+                      64 * kMargWaves)))
+    return rc;
+  char* sc = (char*)scratch;
+  return serial_loss(pb, local_norm, W, num_frames, labels, num_labels, a.uflag, loss, log_z, num,
+                     (float*)(sc + w.f_alpha), (float*)(sc + w.f_an), nullptr, dW, sc + w.f_side,
+                     stream);
 }
 }  // namespace lt_impl
 
@@ -1336,14 +1428,9 @@ int lt_chunk_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   a.num_out = num;
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
-  const int grid_a = (int)(((long long)a.B * a.K + 3) / 4);
-  const void* ka = a.PPL == 1 ? (bf16 ? (const void*)ck_transfer_kernel<true, 1>
-                                      : (const void*)ck_transfer_kernel<false, 1>)
-                              : (bf16 ? (const void*)ck_transfer_kernel<true, 2>
-                                      : (const void*)ck_transfer_kernel<false, 2>);
-  const void* kb = a.PPL == 1 ? (const void*)ck_combine_kernel<1> : (const void*)ck_combine_kernel<2>;
-  if ((rc = ck_launch(ka, grid_a, 0, st, a))) return rc;
-  if ((rc = ck_launch(kb, a.B, 0, st, a))) return rc;
+  if ((rc = ck_launch(ck_kernel_a(a.PPL, bf16), (int)(((long long)a.B * a.K + 3) / 4), 0, st, a)))
+    return rc;
+  if ((rc = ck_launch(ck_kernel_b(a.PPL), a.B, 0, st, a))) return rc;
   // utterances outside the fast path's range: the frame-serial kernels
   // (their workgroups return at once for every other utterance)
   return lt_impl::serial_loss(pb, local_norm, W, num_frames, labels, num_labels, a.uflag, loss,
@@ -1375,12 +1462,9 @@ int lt_chunk_backward(const lt_problem* pb, int32_t local_norm, const void* W,
   a.dW = dW;
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
-  const int lds_c = a.c_off_fb + (bf16 ? 4 * 4 * ((a.FR + 3) & ~3) : 0);
-  const void* kc = a.PPL == 1 ? (bf16 ? (const void*)ck_marg_kernel<true, 1>
-                                      : (const void*)ck_marg_kernel<false, 1>)
-                              : (bf16 ? (const void*)ck_marg_kernel<true, 2>
-                                      : (const void*)ck_marg_kernel<false, 2>);
-  if ((rc = ck_launch(kc, a.B * a.K, lds_c, st, a))) return rc;
+  if ((rc = ck_launch(ck_kernel_c(a.PPL, bf16), a.B * a.K, ck_lds_c(a, bf16), st, a,
+                      64 * kMargWaves)))
+    return rc;
   char* sc = (char*)scratch;
   return lt_impl::serial_loss(pb, local_norm, W, num_frames, labels, num_labels, a.uflag,
                               (float*)(sc + w.f_loss), (float*)(sc + w.f_lz),

@@ -1157,18 +1157,17 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W) || misaligned(dW)) return fail(LT_EINVAL, "W/dW must be 16-byte aligned");
   if (lt_impl::chunk_eligible(pb) && pb->max_frames > 0) {
-    // bigram: the chunked two-level scan (lt_chunk.hip), three launches
+    // bigram: the chunked two-level scan (lt_chunk.hip), three launches (plus
+    // the frame-serial pair, whose workgroups exit at once unless an
+    // utterance is out of the fast path's range)
     size_t st = 0, sc = 0;
     if ((rc = lt_chunk_workspace_bytes(pb, local_norm, &st, &sc))) return rc;
     const size_t st_al = (st + 255) & ~(size_t)255;
     if (!workspace || workspace_bytes < st_al + sc) return fail(LT_EINVAL, "workspace too small");
     char* state = (char*)workspace;
     char* scratch = state + st_al;
-    if ((rc = lt_chunk_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
-                               num, state, st, scratch, sc, stream)))
-      return rc;
-    return lt_chunk_backward(pb, local_norm, W, num_frames, labels, num_labels, nullptr, dW,
-                             state, st, scratch, sc, stream);
+    return lt_impl::chunk_loss_grad(pb, local_norm, W, num_frames, labels, num_labels, loss,
+                                    log_z, num, dW, state, st, scratch, sc, stream);
   }
   const GradWs w = grad_ws(pb, local_norm);
   if (!workspace || workspace_bytes < w.total) return fail(LT_EINVAL, "workspace too small");

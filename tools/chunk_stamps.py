@@ -28,6 +28,14 @@ os.environ['LT_CK_STAMPS'] = hex(st.data_ptr())
 _native.loss_grad(W, nf, lab, nl, V, 1, False)
 torch.cuda.synchronize()
 del os.environ['LT_CK_STAMPS']
+if os.environ.get('LT_CK_LDS_PAD'):
+  e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+  e0.record()
+  for _ in range(10):
+    _native.loss_grad(W, nf, lab, nl, V, 1, False)
+  e1.record()
+  torch.cuda.synchronize()
+  print(f'LDS pad {os.environ["LT_CK_LDS_PAD"]}: {e0.elapsed_time(e1) / 10:.3f} ms per call')
 s = st.cpu().numpy().reshape(-1, 8)
 s = s[s[:, 0] > 0]
 names = ['DMA+tables', 'recursions', 'marginals', 'dW stream']
