@@ -53,9 +53,11 @@ namespace {
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr float kRange = 60.f;  // max - min of a frame's weights on the fast path
+constexpr float kEmin = 0x1p-88f;  // < e^-(kRange + 1): the exponential form of the range test
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr int kRec = 1224;      // floats per chunk record (16-byte multiple)
 constexpr int kRowT = 36;       // row stride of the transposed core in a record
+constexpr int kChunkLds = 40 * 1024;  // phase C LDS per workgroup (four per CU)
 constexpr int kMargWaves = 4;   // phase C: waves per workgroup (recursions on 0-3)
 constexpr int kGrp = 7;         // frames per numerator group (band offsets 0..kGrp)
 // record layout (floats): [0, 1152) X^T rows: rec[i * 36 + j] = X[i][j] =
@@ -99,7 +101,8 @@ struct CkArgs {
   // phase B LDS carve
   int b_ni, b_slots, b_off_ra, b_off_rb, b_off_ga, b_off_gb, b_gslots, b_gslot, b_off_buf;
   // phase C LDS carve
-  int c_ni, c_off_ad, c_off_bd, c_off_an, c_off_bn, c_off_tab, c_off_cf, c_off_buf, c_off_fb;
+  int c_ni, c_off_ad, c_off_bd, c_off_an, c_off_bn, c_off_nw, c_off_fs, c_off_tab, c_off_cf,
+      c_off_buf, c_off_e, c_bytes;
 };
 
 // lanes l and l ^ 32 combined (v_permlane32_swap: both halves get both)
@@ -107,9 +110,10 @@ LT_DEVINL float half_sum(float v) {
   auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
   return __int_as_float(p[0]) + __int_as_float(p[1]);
 }
-LT_DEVINL float half_max(float v) {
+// lane l & 31's value in both halves
+LT_DEVINL float half_lo(float v) {
   auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
-  return fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
+  return (threadIdx.x & 32) ? __int_as_float(p[0]) : v;
 }
 // lane l gets v of lane l-1 (lane 0: fill)
 LT_DEVINL float from_prev(float v, float fill) {
@@ -150,6 +154,13 @@ LT_DEVINL float safe_max(float m) { return __builtin_isfinite(m) ? m : 0.f; }
   do {              \
   } while (0)
 #endif
+// max of three with no NaN quieting of the operands (a NaN in W is caught
+// by the exponential test of phase A, not by the max)
+LT_DEVINL float max3_raw(float x, float y, float z) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+  return r;
+}
 // lane 0's float (readfirstlane is an int builtin: never pass it a float)
 LT_DEVINL float first_lane(float v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
@@ -283,15 +294,17 @@ LT_DEVINL void load_frame(const CkArgs& a, const unsigned char* Wf, int lane, co
     f.gl[r] = ldg<BF16>(Wf, max(loff[r], 0));
   }
 }
-// the values load_frame read for nothing
-template <bool BF16, int PPL>
+// the values load_frame read for nothing (FULL: V = 32, every core value live)
+template <bool BF16, int PPL, bool FULL>
 LT_DEVINL void mask_frame(int V, int lane, const int* boff, const int* loff,
                           FrameRegs<BF16, PPL>& f) {
   const int i = lane & 31, h = lane >> 5;
+  if constexpr (!FULL) {
 #pragma unroll
-  for (int s = 0; s < 16; ++s)
-    if (!(kstep(s, h) < V && i < V)) f.w[s] = -kInf;
-  if (i >= V) { f.wr0 = -kInf; f.wdg = -kInf; }
+    for (int s = 0; s < 16; ++s)
+      if (!(kstep(s, h) < V && i < V)) f.w[s] = -kInf;
+    if (i >= V) { f.wr0 = -kInf; f.wdg = -kInf; }
+  }
   if (lane > V) f.wbl = -kInf;
 #pragma unroll
   for (int r = 0; r < PPL; ++r) {
@@ -300,7 +313,7 @@ LT_DEVINL void mask_frame(int V, int lane, const int* boff, const int* loff,
   }
 }
 
-template <bool BF16, int PPL>
+template <bool BF16, int PPL, bool FULL>
 __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
   __shared__ __attribute__((aligned(16))) float s_rt[4][32];
   __shared__ int s_lab[4][128];
@@ -345,6 +358,11 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
   float pi = 0.f;     // log P00 - csum
   float csum = 0.f;   // sum of c_t (integers)
   int bad = 0;
+  // the lane's diagonal k-step (the blank self loop of state i+1 joins the
+  // core product there): 1 at s with kstep(s, h) == i, else 0
+  float dsel[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) dsel[s] = (kstep(s, h) == i && (FULL || i < V)) ? 1.f : 0.f;
   // numerator group bands: nbd[r][d] = log2 weight of the paths from
   // position s = lane + 64 r at the group's first frame to s + d after its
   // last (the string lattice's frame steps, lattices.py:340-377, composed)
@@ -355,7 +373,7 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
   FrameRegs<BF16, PPL> fr[2];
   auto frame_ptr = [&](int f) { return W0 + (long long)min(f, nt - 1) * a.FR * es; };
   auto step = [&](FrameRegs<BF16, PPL>& F, int f, bool reload) {
-    mask_frame(V, lane, boff, loff, F);
+    mask_frame<BF16, PPL, FULL>(V, lane, boff, loff, F);
     // numerator: band step over the group (positions past the string read -inf)
     {
       const int j = f / kGrp, fl = f - j * kGrp;  // wave-uniform
@@ -393,33 +411,33 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
       }
       __builtin_amdgcn_wave_barrier();
     }
-    // the frame's range (every weight finite, max - min <= kRange)
-    float mx = -kInf, mn = kInf;
+    // the frame's offset c = ceil(max W) (masked values are -inf)
+    float mx = max3_raw(F.wr0, F.wbl, F.w[15]);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int kk = kstep(s, h);
-      if (kk < V && i < V) { mx = fmaxf(mx, F.w[s]); mn = fminf(mn, F.w[s]); }
-    }
-    if (i < V) { mx = fmaxf(mx, F.wr0); mn = fminf(mn, F.wr0); }
-    if (lane <= V) { mx = fmaxf(mx, F.wbl); mn = fminf(mn, F.wbl); }
+    for (int s = 0; s < 15; s += 3) mx = max3_raw(mx, max3_raw(F.w[s], F.w[s + 1], F.w[s + 2]), mx);
     mx = wmax_u(mx);
-    mn = -wmax_u(-mn);
-    if (!(mx - mn <= kRange) || !__builtin_isfinite(mx) || !__builtin_isfinite(mn)) bad = 1;
-    const float c = __builtin_isfinite(mx) ? ceilf(mx) : 0.f;
+    const bool cfin = __builtin_isfinite(mx);
+    const float c = cfin ? ceilf(mx) : 0.f;
     const float cl = c * kLog2e;
     if (lane == 0) a.cf[(long long)b * a.T + t0 + f] = c;
     // E_t^T as the A operand: lane (i, h), k-step s -> E[k][i]; the core
-    // diagonal also carries the blank self loop (alignments.py:294-297)
+    // diagonal also carries the blank self loop (alignments.py:294-297).
+    // The range test rides on the exponentials: every live E >= e^-61
+    // (max - min <= kRange + 1; a NaN or -inf weight fails it, +inf fails cfin)
     const float dgv = lt_exp_off(F.wdg, cl);
     float A[16];
+    bool lbad = (lane <= V) && !(F.wbl >= c - (kRange + 1.f));
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const int kk = kstep(s, h);
-      float e = (kk < V && i < V) ? lt_exp_off(F.w[s], cl) : 0.f;
-      if (kk == i && i < V) e += dgv;
-      A[s] = e;
+      const bool live = FULL || (kstep(s, h) < V && i < V);
+      const float e = lt_exp_off(F.w[s], cl);
+      lbad = lbad || (live && !(e >= kEmin));
+      A[s] = live ? __builtin_fmaf(dsel[s], dgv, e) : 0.f;
     }
-    const float e0 = i < V ? lt_exp_off(F.wr0, cl) : 0.f;
+    const float e0r = lt_exp_off(F.wr0, cl);
+    const float e0 = (FULL || i < V) ? e0r : 0.f;
+    lbad = lbad || ((FULL || i < V) && !(e0r >= kEmin));
+    if (!cfin || __builtin_amdgcn_ballot_w64(lbad)) bad = 1;
     const float w00 = F.w00;
     if (reload) load_frame(a, frame_ptr(f + 2), lane, boff, loff, F);
 
@@ -438,8 +456,10 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
       const float lam = pi * kLog2e;
       const int B0 = max(rho, (int)floorf(lam));
       float nr = ldexpf(y, max(rho - B0, -200)) + e0 * __builtin_amdgcn_exp2f(lam - (float)B0);
-      nr = i < V ? nr : 0.f;
-      const float m = wmax_u(nr);
+      nr = (FULL || i < V) ? nr : 0.f;
+      // scale by state 1's entry (> 0: state 0 reaches every core state in
+      // one frame; the others stay within e^61 of it)
+      const float m = first_lane(nr);
       int e;
       frexpf(m, &e);
       e = m > 0.f ? e : 0;
@@ -454,10 +474,9 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
     v16f D = {};
 #pragma unroll
     for (int s = 0; s < 16; ++s) D = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], X[s], D, 0, 0, 0);
-    float cm = 0.f;  // one power-of-two scale per column (start state)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) cm = fmaxf(cm, D[r]);
-    cm = half_max(cm);
+    // one power-of-two scale per column (start state j): its end state 1
+    // (row 0, register 0 of half 0), within e^61 of the column's others
+    const float cm = half_lo(D[0]);
     int e;
     frexpf(cm, &e);
     e = cm > 0.f ? e : 0;
@@ -820,7 +839,11 @@ LT_DEVINL void store_dw(void* dW, long long e, float v) {
   else ((float*)dW)[e] = v;
 }
 
-template <bool BF16, int PPL>
+// per-frame scalars of phase C (log2): alpha's and beta's scales, the start
+// state's alpha and beta, W[0][0]
+constexpr int kFs = 8, kFsMa = 0, kFsA0 = 1, kFsMb = 2, kFsB0 = 3, kFsW00 = 4;
+
+template <bool BF16, int PPL, bool FULL>
 __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kernel(const CkArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int b = blockIdx.x / a.K, k = blockIdx.x - (blockIdx.x / a.K) * a.K;
@@ -832,7 +855,10 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   const int t0 = k * a.L;
   const int tend = min(t0 + a.L, a.T);
   const int t1 = max(t0, min(t0 + a.L, nf));
-  const int V = a.V, C = a.C, R = a.R, FR = a.FR, CP = a.CP, NPG = a.NPG, NP = a.NP;
+  // FULL: V = 32, every stride a compile-time constant
+  const int V = FULL ? 32 : a.V, C = V + 1, R = V + 1, FR = C * R, CP = FULL ? 36 : a.CP;
+  const int NPG = a.NPG, NP = a.NP;
+  const int FRP = (FR + 3) & ~3;
   float g = a.grad ? a.grad[b] : 1.f;
   const float lz = a.log_z[b], nm = a.num[b];
   if (!__builtin_isfinite(nm) || (!a.local && !__builtin_isfinite(lz))) g = 0.f;
@@ -847,11 +873,13 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   // stage the chunk's live frames
   const long long off = e0 * (BF16 ? 2 : 4);
   dma_issue(a.W, off, (long long)nt * a.FB, lds_base_addr(lds), a.c_ni, lane, wave, kMargWaves);
-  const unsigned char* wch = lds + (off & 15);
-  float* ad = (float*)(lds + a.c_off_ad);  // [L][CP] alpha_t (log)
-  float* bd = (float*)(lds + a.c_off_bd);  // [L][CP] beta_{t+1}
-  float* an = (float*)(lds + a.c_off_an);  // [L][NPG]
-  float* bn = (float*)(lds + a.c_off_bn);  // [L][NPG]
+  unsigned char* wch = lds + (off & 15);
+  float* xa = (float*)(lds + a.c_off_ad);  // [L][CP] alpha_f, linear, max 1 (scale fs Ma)
+  float* xb = (float*)(lds + a.c_off_bd);  // [L][CP] beta_{f+1} of the core, linear, max 1
+  float* an = (float*)(lds + a.c_off_an);  // [L][NPG] numerator alpha_f (log2)
+  float* bn = (float*)(lds + a.c_off_bn);  // [L][NPG] numerator beta_{f+1} (log2)
+  float2* nw = (float2*)(lds + a.c_off_nw);  // [L][NPG] (blank of u, arc into u), log2
+  float* fs = (float*)(lds + a.c_off_fs);    // [L][kFs]
   int* boff = (int*)(lds + a.c_off_tab);
   int* loff = boff + NPG;
   int* labs = loff + NPG;
@@ -862,6 +890,57 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   wait_vmcnt(0);
   __syncthreads();
   CK_STAMP(1);
+  // E_f = exp(W_f - c_f) (c_f = ceil(max W_f), so E <= 1): in place over
+  // the f32 image, in a region of its own for bf16
+  auto eptr = [&](int f) -> float* {
+    return BF16 ? (float*)(lds + a.c_off_e) + f * FRP : (float*)(wch + f * a.FB);
+  };
+  // the numerator's arc weights leave W first (exact, log2); every read of
+  // this pass issues before the barrier, every E store after it
+  {
+    float2 g2[4];
+    const int nnw = nt * NPG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int x = min(tid + 64 * kMargWaves * i, nnw - 1);
+      const int f = x / NPG, u = x - f * NPG;
+      const unsigned char* fr = wch + f * a.FB;
+      const int lo = loff[u];
+      const float wb = ldsw<BF16>(fr, boff[u]), wl = ldsw<BF16>(fr, max(lo, 0));
+      g2[i] = make_float2(u < NP ? wb * kLog2e : -kInf, (u >= 1 && u < NP) ? wl * kLog2e : -kInf);
+    }
+    for (int x = tid + 4 * 64 * kMargWaves; x < nnw; x += 64 * kMargWaves) {  // long strings
+      const int f = x / NPG, u = x - f * NPG;
+      const unsigned char* fr = wch + f * a.FB;
+      const int lo = loff[u];
+      const float wb = ldsw<BF16>(fr, boff[u]), wl = ldsw<BF16>(fr, max(lo, 0));
+      nw[x] = make_float2(u < NP ? wb * kLog2e : -kInf, (u >= 1 && u < NP) ? wl * kLog2e : -kInf);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (tid + 64 * kMargWaves * i < nnw) nw[tid + 64 * kMargWaves * i] = g2[i];
+  }
+  if (tid < nt) fs[tid * kFs + kFsW00] = ldsw<BF16>(wch + tid * a.FB, 0) * kLog2e;
+  __syncthreads();  // the gathers above read W; E overwrites it below
+  // E in place, frame by frame: each thread's elements of a frame loaded
+  // together (element-wise: no barrier between a thread's reads and stores)
+  constexpr int kEi = 5;  // ceil(33 * 33 / 256)
+  for (int f = 0; f < nt; ++f) {
+    const unsigned char* fr = wch + f * a.FB;
+    float* ef = eptr(f);
+    const float cl = cfl[f] * kLog2e;
+    float v[kEi];
+#pragma unroll
+    for (int i = 0; i < kEi; ++i) v[i] = ldsw<BF16>(fr, min(tid + 64 * kMargWaves * i, FR - 1));
+#pragma unroll
+    for (int i = 0; i < kEi; ++i)
+      if (tid + 64 * kMargWaves * i < FR) ef[tid + 64 * kMargWaves * i] =
+          __builtin_amdgcn_exp2f(__builtin_fmaf(v[i], kLog2e, -cl));
+    for (int e = tid + 64 * kMargWaves * kEi; e < FR; e += 64 * kMargWaves)  // V > 32 never
+      ef[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(ldsw<BF16>(fr, e), kLog2e, -cl));
+  }
+  __syncthreads();
+  CK_STAMP(5);
   // every LDS load below is unconditional (clamped index, unused values
   // masked afterwards): a load under a branch would pay its full latency
 
@@ -869,12 +948,12 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     // ---- den alpha in scaled linear space. Lane p in [1, V]: alpha[p] =
     // al 2^S, renormalised every frame by a power of two so that state 1
     // sits in [1/2, 1) (readfirstlane + frexp: no reduction on the chain).
-    // With E = exp(W - c), c = ceil(max W) (phase A's), every E is in
-    // [e^-61, 1] and the frame range bound keeps every core value within
-    // ~2^89 of state 1. The start state (only its blank loop in-arc) is a
-    // log2 scalar a0 beside the chain. Lane (q, h): destination q+1,
-    // sources p in [16h, 16h+16) (+ p = 32 in h = 1), the blank self loop
-    // in h = 0; halves combined by permlane.
+    // Every E is in [e^-61, 1] and the frame range bound keeps every core
+    // value within ~2^89 of state 1. The start state (only its blank loop
+    // in-arc) is a log2 scalar a0 beside the chain. Lane (q, h): destination
+    // q+1, sources p in [16h, 16h+16) (+ p = 32 in h = 1), the blank self
+    // loop in h = 0; halves combined by permlane. Per frame, off the chain:
+    // xa = alpha_f / its max (all states), Ma = log2 of that max.
     const int q = lane & 31, h = lane >> 5;
     const int qe = min(q, V - 1) + 1;
     const bool core = lane >= 1 && lane <= V;
@@ -883,19 +962,27 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     float S = wmax_u(core ? x0 : -kInf);  // -inf: no core state reached yet
     float al = (core && S != -kInf) ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     for (int f = 0; f < nt; ++f) {
-      if (lane < C) ad[f * CP + lane] = (lane == 0 ? a0 : S + __builtin_amdgcn_logf(al)) * kLn2;
-      const unsigned char* fr = wch + f * a.FB;
+      const float* ef = eptr(f);
       const float cl = cfl[f] * kLog2e;
-      const float w00 = ldsw<BF16>(fr, 0);
-      // transition weights first: they do not depend on alpha
+      const float w00 = fs[f * kFs + kFsW00];
       float e[16];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) e[m] = lt_exp_off(ldsw<BF16>(fr, min(16 * h + m, C - 1) * R + qe), cl);
-      const float e32 = lt_exp_off(ldsw<BF16>(fr, min(32, C - 1) * R + qe), cl);
-      const float eb = lt_exp_off(ldsw<BF16>(fr, qe * R), cl);
+      for (int m = 0; m < 16; ++m) e[m] = ef[min(16 * h + m, C - 1) * R + qe];
+      const float e32 = ef[min(32, C - 1) * R + qe];
+      const float eb = ef[qe * R];
       const float M = fmaxf(a0, S);  // a0 is finite on the fast path
       const float u = __builtin_amdgcn_exp2f(S - M), t = __builtin_amdgcn_exp2f(a0 - M);
       if (lane < 36) buf[lane] = lane == 0 ? t : al * u;  // buf[p > V] = 0
+      // alpha_f for the marginals
+      const float mc = wmax_u(core ? al : 0.f);
+      const float Ma = mc > 0.f ? fmaxf(a0, S + __builtin_amdgcn_logf(mc)) : a0;
+      if (lane < C)
+        xa[f * CP + lane] = lane == 0 ? __builtin_amdgcn_exp2f(a0 - Ma)
+                                      : al * __builtin_amdgcn_exp2f(S - Ma);
+      if (lane == 0) {
+        fs[f * kFs + kFsMa] = Ma;
+        fs[f * kFs + kFsA0] = a0;
+      }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       float s0 = 0.f, s1 = 0.f;
@@ -913,16 +1000,17 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       int ex;
       (void)frexpf(first_lane(sq), &ex);  // state 1: > 0 on the fast path
       S = M + cl + (float)ex;
-      a0 += w00 * kLog2e;
+      a0 += w00;
       const float sh = from_prev(ldexpf(sq, -ex), 0.f);
       al = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
     }
   } else if (wave == 1 && !a.local && !(a.dbg & 4)) {
-    // ---- den beta, the same scaled linear space; bd[f] = beta_{f+1}. Lane
-    // (j, h): core source j+1 over labels y in [16h+1, 16h+16], the blank in
-    // h = 0; every lane also one term of the start state's sum (log2 scalar
-    // b0: no core state depends on it).
+    // ---- den beta, the same scaled linear space; frame f gets beta_{f+1}.
+    // Lane (j, h): core source j+1 over labels y in [16h+1, 16h+16], the
+    // blank in h = 0; every lane also one term of the start state's sum
+    // (log2 scalar b0: no core state depends on it). Off the chain: xb =
+    // core beta / its max, Mb = log2 of that max.
     const int j = lane & 31, h = lane >> 5;
     const int pe = min(j, V - 1) + 1;
     const bool core = lane >= 1 && lane <= V;
@@ -931,17 +1019,22 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     float S = safe_max(wmax_u(core ? x0 : -kInf));
     float be = core ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     for (int f = nt - 1; f >= 0; --f) {
-      if (lane < C) bd[f * CP + lane] = (lane == 0 ? b0 : S + __builtin_amdgcn_logf(be)) * kLn2;
-      const unsigned char* fr = wch + f * a.FB;
+      const float* ef = eptr(f);
       const float cl = cfl[f] * kLog2e;
-      const float w00 = ldsw<BF16>(fr, 0);
+      const float w00 = fs[f * kFs + kFsW00];
       float e[16];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) e[m] = lt_exp_off(ldsw<BF16>(fr, pe * R + min(16 * h + m + 1, V)), cl);
-      const float eb = lt_exp_off(ldsw<BF16>(fr, pe * R), cl);
-      const float e0y = lt_exp_off(ldsw<BF16>(fr, min(j, V - 1) + 1), cl);  // E[0][j+1]
+      for (int m = 0; m < 16; ++m) e[m] = ef[pe * R + min(16 * h + m + 1, V)];
+      const float eb = ef[pe * R];
+      const float e0y = ef[min(j, V - 1) + 1];  // E[0][j+1]
       // buf[y-1] = beta[y] (scaled) for core y; 0 past V
       if (lane >= 1 && lane <= 32) buf[lane - 1] = be;
+      const float mc = wmax_u(be);  // > 0: every core beta is
+      if (lane < C) xb[f * CP + lane] = be * __builtin_amdgcn_rcpf(mc);
+      if (lane == 0) {
+        fs[f * kFs + kFsMb] = S + __builtin_amdgcn_logf(mc);
+        fs[f * kFs + kFsB0] = b0;
+      }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       float s0 = 0.f, s1 = 0.f;
@@ -958,7 +1051,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       const float sj = half_sum(s0 + s1);  // lane j: beta'[j+1] / (2^S e^c)
       // start state: (+)_y E[0][y] beta[y], then its own blank loop
       const float r0 = wsum_u(lane < 32 ? bj * e0y : 0.f);
-      b0 = lse2_b2(b0 + w00 * kLog2e, S + cl + __builtin_amdgcn_logf(r0));
+      b0 = lse2_b2(b0 + w00, S + cl + __builtin_amdgcn_logf(r0));
       int ex;
       (void)frexpf(first_lane(sj), &ex);
       S = S + cl + (float)ex;
@@ -967,20 +1060,16 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       __builtin_amdgcn_wave_barrier();
     }
   } else if (wave == 2 && !(a.dbg & 8)) {
-    // ---- num alpha (log space)
-    int bo[PPL], lo[PPL];
+    // ---- num alpha (log2): al'[u] = al[u] + blank(u) (+) al[u-1] + arc(u)
     float al[PPL];
     const float* src = a.nabd + ((long long)b * (a.K + 1) + k) * NPG;
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       const int u = lane + 64 * r, uc = min(u, NPG - 1);
-      bo[r] = boff[uc];
-      lo[r] = max(loff[uc], 0);
-      const float v = src[uc];
+      const float v = src[uc] * kLog2e;
       al[r] = u < NPG ? v : -kInf;
     }
     for (int f = 0; f < nt; ++f) {
-      const unsigned char* fr = wch + f * a.FB;
       float prev = -kInf, nv[PPL];
 #pragma unroll
       for (int r = 0; r < PPL; ++r) {
@@ -989,30 +1078,24 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         const float x = rot_prev(al[r]);
         const float pv = lane == 0 ? prev : x;
         prev = x;
-        const float wb = ldsw<BF16>(fr, bo[r]), wl = ldsw<BF16>(fr, lo[r]);
-        const float gb = u < NP ? wb : -kInf;
-        const float gl = (u >= 1 && u < NP) ? wl : -kInf;
-        nv[r] = lse2(al[r] + gb, pv + gl);
+        const float2 w = nw[f * NPG + min(u, NPG - 1)];
+        nv[r] = lse2_b2(al[r] + w.x, pv + w.y);
       }
 #pragma unroll
       for (int r = 0; r < PPL; ++r) al[r] = nv[r];
       __builtin_amdgcn_wave_barrier();
     }
   } else if (wave == 3 && !(a.dbg & 8)) {
-    // ---- num beta; bn[f] = beta_{f+1}
-    int bo[PPL], lo[PPL];
+    // ---- num beta (log2); frame f gets beta_{f+1}
     float be[PPL];
     const float* src = a.nbbd + ((long long)b * (a.K + 1) + k + 1) * NPG;
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       const int u = lane + 64 * r, uc = min(u, NPG - 1);
-      bo[r] = boff[uc];
-      lo[r] = max(loff[min(u + 1, NPG - 1)], 0);  // the arc into u+1
-      const float v = src[uc];
+      const float v = src[uc] * kLog2e;
       be[r] = u < NPG ? v : -kInf;
     }
     for (int f = nt - 1; f >= 0; --f) {
-      const unsigned char* fr = wch + f * a.FB;
       float nx[PPL], nv[PPL];
 #pragma unroll
       for (int r = 0; r < PPL; ++r) nx[r] = rot_next(be[r]);
@@ -1021,10 +1104,9 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         const int u = lane + 64 * r;
         if (u < NPG) bn[f * NPG + u] = be[r];
         const float nb = lane == 63 ? (r + 1 < PPL ? nx[r + 1 < PPL ? r + 1 : r] : -kInf) : nx[r];
-        const float wb = ldsw<BF16>(fr, bo[r]), wl = ldsw<BF16>(fr, lo[r]);
-        const float gb = u < NP ? wb : -kInf;
-        const float gl = u + 1 < NP ? wl : -kInf;
-        nv[r] = lse2(gb + be[r], gl + nb);
+        const float wb = nw[f * NPG + min(u, NPG - 1)].x;
+        const float wl = nw[f * NPG + min(u + 1, NPG - 1)].y;
+        nv[r] = lse2_b2(wb + be[r], (u + 1 < NP ? wl : -kInf) + nb);
       }
 #pragma unroll
       for (int r = 0; r < PPL; ++r) be[r] = nv[r];
@@ -1036,15 +1118,15 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
 
   // ---- marginals, one wave per frame: den - num, each normalised by its
   // frame total (alignments.py:311-317; numerator: reverse of :320-329).
-  // Element e = lane + 64 m of a frame is arc (p, y) into q = y ? y : p.
-  constexpr int MFX = 18;  // ceil(33 * 33 / 64)
-  int pq[MFX];             // p | q << 8 of the (clamped) element
-#pragma unroll
-  for (int m = 0; m < MFX; ++m) {
-    const int e = min(lane + 64 * m, FR - 1);
-    const int p = e / R, y = e - p * R;
-    pq[m] = p | ((y ? y : p) << 8);
-  }
+  // Den in rows: lane (y, h) = column y = lane & 31 of rows p = 2 m + h,
+  // then column 32 (lane p); arc (p, y) goes into q = y ? y : p. Den (p, y)
+  // = E[p][y] xa[p] xb[q] 2^(Ma + Mb + c - Z) except (0, 0), the only arc
+  // into the start state, taken in log2 (its beta may sit far above the
+  // core's; xb[0] = 0 keeps it out of the sum). Every other den term is
+  // <= 1 and the largest >= e^-61.
+  constexpr int NROW = 17;  // row pairs: p = 2 m + h <= 33
+  const int y = lane & 31, h = lane >> 5;
+  const bool ycol = y < R;  // FULL: every lane
   int bo[PPL], lo[PPL];
 #pragma unroll
   for (int r = 0; r < PPL; ++r) {
@@ -1053,17 +1135,17 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     lo[r] = max(loff[uc], 0);
   }
   for (int f = (a.dbg & 16) ? nt : wave; f < nt; f += kMargWaves) {
-    const unsigned char* fr = wch + f * a.FB;
-    float* fb = BF16 ? (float*)(lds + a.c_off_fb) + wave * ((FR + 3) & ~3) : (float*)fr;
-    // numerator terms first (they read W)
+    float* fb = eptr(f);  // E_f, then the frame's dW in place
+    // numerator terms (log2)
     float sb[PPL], sl[PPL];
     float mxn = -kInf;
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       const int u = lane + 64 * r, uc = min(u, NP - 1);
       const float bu = bn[f * NPG + uc];
-      const float tb = an[f * NPG + uc] + ldsw<BF16>(fr, bo[r]) + bu;
-      const float tl = an[f * NPG + max(uc - 1, 0)] + ldsw<BF16>(fr, lo[r]) + bu;
+      const float2 w = nw[f * NPG + uc];
+      const float tb = an[f * NPG + uc] + w.x + bu;
+      const float tl = an[f * NPG + max(uc - 1, 0)] + w.y + bu;
       sb[r] = u < NP ? tb : -kInf;
       sl[r] = (u >= 1 && u < NP) ? tl : -kInf;
       mxn = fmaxf(mxn, fmaxf(sb[r], sl[r]));
@@ -1072,44 +1154,54 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     float zn = 0.f;
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
-      sb[r] = lt_exp(sb[r] - mxn);
-      sl[r] = lt_exp(sl[r] - mxn);
+      sb[r] = __builtin_amdgcn_exp2f(sb[r] - mxn);
+      sl[r] = __builtin_amdgcn_exp2f(sl[r] - mxn);
       zn += sb[r] + sl[r];
     }
     zn = wsum_u(zn);
     const float gn = zn > 0.f ? g / zn : 0.f;
     if (!a.local) {
-      const float* adf = ad + f * CP;
-      const float* bdf = bd + f * CP;
-      // the three operand reads staged separately so they issue back to back
-      float sv[MFX], xa[MFX], xb[MFX];
+      const float* xaf = xa + f * CP;
+      const float* xbf = xb + f * CP;
+      const int yc = min(y, R - 1);
+      const float xby = xbf[yc];  // column y's beta (y >= 1)
+      // rows: E, xa[p] and xb[p] (the blank column's beta) for p = 2 m + h
+      float t[NROW], ra[NROW], rb[NROW];
 #pragma unroll
-      for (int m = 0; m < MFX; ++m) sv[m] = ldsw<BF16>(fr, min(lane + 64 * m, FR - 1));
+      for (int m = 0; m < NROW; ++m) t[m] = fb[min(2 * m + h, C - 1) * R + yc];
 #pragma unroll
-      for (int m = 0; m < MFX; ++m) xa[m] = adf[pq[m] & 255];
+      for (int m = 0; m < NROW; ++m) ra[m] = xaf[min(2 * m + h, C - 1)];
 #pragma unroll
-      for (int m = 0; m < MFX; ++m) xb[m] = bdf[pq[m] >> 8];
-      float mx = -kInf;
+      for (int m = 0; m < NROW; ++m) rb[m] = xbf[min(2 * m + h, C - 1)];
+      // column 32 (C = 33 only): lane p < 33
+      const int pc = min(lane, C - 1);
+      float tc = fb[pc * R + (R - 1)] * xaf[pc] * xbf[R - 1];
+      const bool colc = R == 33 && lane < 33;
+      tc = colc ? tc : 0.f;
+      float sum = tc;
 #pragma unroll
-      for (int m = 0; m < MFX; ++m) {
-        const float v = xa[m] + sv[m] + xb[m];
-        sv[m] = lane + 64 * m < FR ? v : -kInf;
-        mx = fmaxf(mx, sv[m]);
+      for (int m = 0; m < NROW; ++m) {
+        const bool live = ycol && 2 * m + h < C && (R < 33 || y < 32);
+        const float v = t[m] * ra[m] * (y ? xby : rb[m]);
+        t[m] = live ? v : 0.f;
+        sum += t[m];
       }
-      mx = safe_max(wmax_u(mx));
-      float z = 0.f;
-#pragma unroll
-      for (int m = 0; m < MFX; ++m) {
-        sv[m] = lt_exp(sv[m] - mx);
-        z += sv[m];
-      }
-      z = wsum_u(z);
-      const float gd = z > 0.f ? g / z : 0.f;
+      sum = wsum_u(sum);
+      const float* fsf = fs + f * kFs;
+      const float base = fsf[kFsMa] + fsf[kFsMb] + cfl[f] * kLog2e;
+      const float v00 = fsf[kFsA0] + fsf[kFsW00] + fsf[kFsB0];
+      const float zl = lse2_b2(base + __builtin_amdgcn_logf(sum), v00);
+      const float mult = g * __builtin_amdgcn_exp2f(base - zl);
+      const float m00 = g * __builtin_amdgcn_exp2f(v00 - zl);
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int m = 0; m < MFX; ++m)
-        if (lane + 64 * m < FR) fb[lane + 64 * m] = sv[m] * gd;
+      for (int m = 0; m < NROW; ++m) {
+        const int p = 2 * m + h;
+        if (ycol && p < C && (R < 33 || y < 32))
+          fb[p * R + y] = (m == 0 && lane == 0) ? m00 : t[m] * mult;
+      }
+      if (colc) fb[pc * R + (R - 1)] = tc * mult;
     } else {
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
@@ -1126,17 +1218,10 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    const long long eb = e0 + (long long)f * FR;
     if constexpr (BF16) {  // the frame's dW, rounded once, over its own W bytes
-      float ov[MFX];
-#pragma unroll
-      for (int m = 0; m < MFX; ++m) ov[m] = fb[min(lane + 64 * m, FR - 1)];
-      unsigned short* fo = (unsigned short*)fr;
-#pragma unroll
-      for (int m = 0; m < MFX; ++m)
-        if (lane + 64 * m < FR) fo[lane + 64 * m] = f2bf(ov[m]);
+      unsigned short* fo = (unsigned short*)(wch + f * a.FB);
+      for (int e = lane; e < FR; e += 64) fo[e] = f2bf(fb[e]);
     }
-    (void)eb;
   }
   // the chunk's dW sits in LDS in place of its W: one streaming pass of
   // 16-byte stores (scalar stores only at the unaligned head and tail)
@@ -1234,16 +1319,21 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
     t->c_off_bd = off; off += al16(4LL * L * a->CP);
     t->c_off_an = off; off += al16(4LL * L * a->NPG);
     t->c_off_bn = off; off += al16(4LL * L * a->NPG);
+    t->c_off_nw = off; off += al16(8LL * L * a->NPG);
+    t->c_off_fs = off; off += al16(4LL * L * kFs);
     t->c_off_tab = off; off += al16(8LL * a->NPG + 4LL * a->U);
     t->c_off_cf = off; off += al16(4LL * L);
     t->c_off_buf = off; off += 4 * 64 * 4;
-    t->c_off_fb = off; off += bf16 ? kMargWaves * 4 * ((a->FR + 3) & ~3) : 0;
+    t->c_off_e = off; off += bf16 ? al16(4LL * L * ((a->FR + 3) & ~3)) : 0;
     return off;
   };
   int L = std::max(1, std::min(32, ck_env("LT_CHUNK_LEN", 32)));
-  while (L > 4 && c_bytes(L, a) > 80 * 1024) --L;
+  // LDS per workgroup: kChunkLds lets four share a CU (the per-frame chains
+  // of phase C are latency-bound: more workgroups in flight beat longer chunks)
+  const int budget = ck_env("LT_CHUNK_LDS", kChunkLds);
+  while (L > 4 && c_bytes(L, a) > budget) --L;
   if (c_bytes(L, a) > 160 * 1024) return lt_impl::set_error(LT_EUNSUPPORTED, "chunk: LDS");
-  c_bytes(L, a);
+  a->c_bytes = c_bytes(L, a);
   a->L = L;
   a->K = std::max(1, (a->T + L - 1) / L);
   a->NGc = (L + kGrp - 1) / kGrp;
@@ -1313,23 +1403,34 @@ int ck_check(const lt_problem* pb) {
   return LT_OK;
 }
 
-const void* ck_kernel_a(int ppl, bool bf16) {
-  return ppl == 1 ? (bf16 ? (const void*)ck_transfer_kernel<true, 1>
-                          : (const void*)ck_transfer_kernel<false, 1>)
-                  : (bf16 ? (const void*)ck_transfer_kernel<true, 2>
-                          : (const void*)ck_transfer_kernel<false, 2>);
+const void* ck_kernel_a(int ppl, bool bf16, bool full) {
+  if (full)
+    return ppl == 1 ? (bf16 ? (const void*)ck_transfer_kernel<true, 1, true>
+                            : (const void*)ck_transfer_kernel<false, 1, true>)
+                    : (bf16 ? (const void*)ck_transfer_kernel<true, 2, true>
+                            : (const void*)ck_transfer_kernel<false, 2, true>);
+  return ppl == 1 ? (bf16 ? (const void*)ck_transfer_kernel<true, 1, false>
+                          : (const void*)ck_transfer_kernel<false, 1, false>)
+                  : (bf16 ? (const void*)ck_transfer_kernel<true, 2, false>
+                          : (const void*)ck_transfer_kernel<false, 2, false>);
 }
 const void* ck_kernel_b(int ppl) {
   return ppl == 1 ? (const void*)ck_combine_kernel<1> : (const void*)ck_combine_kernel<2>;
 }
-const void* ck_kernel_c(int ppl, bool bf16) {
-  return ppl == 1 ? (bf16 ? (const void*)ck_marg_kernel<true, 1>
-                          : (const void*)ck_marg_kernel<false, 1>)
-                  : (bf16 ? (const void*)ck_marg_kernel<true, 2>
-                          : (const void*)ck_marg_kernel<false, 2>);
+const void* ck_kernel_c(int ppl, bool bf16, bool full) {
+  if (full)
+    return ppl == 1 ? (bf16 ? (const void*)ck_marg_kernel<true, 1, true>
+                            : (const void*)ck_marg_kernel<false, 1, true>)
+                    : (bf16 ? (const void*)ck_marg_kernel<true, 2, true>
+                            : (const void*)ck_marg_kernel<false, 2, true>);
+  return ppl == 1 ? (bf16 ? (const void*)ck_marg_kernel<true, 1, false>
+                          : (const void*)ck_marg_kernel<false, 1, false>)
+                  : (bf16 ? (const void*)ck_marg_kernel<true, 2, false>
+                          : (const void*)ck_marg_kernel<false, 2, false>);
 }
 int ck_lds_c(const CkArgs& a, bool bf16) {
-  int lds = a.c_off_fb + (bf16 ? kMargWaves * 4 * ((a.FR + 3) & ~3) : 0);
+  (void)bf16;
+  int lds = a.c_bytes;
 #ifdef LT_DIAG
   lds += ck_env("LT_CK_LDS_PAD", 0);  // occupancy experiments
 #endif
@@ -1376,10 +1477,10 @@ int chunk_loss_grad(const lt_problem* pb, int local_norm, const void* W, const i
   a.dW = dW;
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
-  if ((rc = ck_launch(ck_kernel_a(a.PPL, bf16), (int)(((long long)a.B * a.K + 3) / 4), 0, st, a)))
+  if ((rc = ck_launch(ck_kernel_a(a.PPL, bf16, a.V == 32), (int)(((long long)a.B * a.K + 3) / 4), 0, st, a)))
     return rc;
   if ((rc = ck_launch(ck_kernel_b(a.PPL), a.B, 0, st, a))) return rc;
-  if ((rc = ck_launch(ck_kernel_c(a.PPL, bf16), a.B * a.K, ck_lds_c(a, bf16), st, a,
+  if ((rc = ck_launch(ck_kernel_c(a.PPL, bf16, a.V == 32), a.B * a.K, ck_lds_c(a, bf16), st, a,
                       64 * kMargWaves)))
     return rc;
   char* sc = (char*)scratch;
@@ -1428,7 +1529,7 @@ int lt_chunk_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   a.num_out = num;
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
-  if ((rc = ck_launch(ck_kernel_a(a.PPL, bf16), (int)(((long long)a.B * a.K + 3) / 4), 0, st, a)))
+  if ((rc = ck_launch(ck_kernel_a(a.PPL, bf16, a.V == 32), (int)(((long long)a.B * a.K + 3) / 4), 0, st, a)))
     return rc;
   if ((rc = ck_launch(ck_kernel_b(a.PPL), a.B, 0, st, a))) return rc;
   // utterances outside the fast path's range: the frame-serial kernels
@@ -1462,7 +1563,7 @@ int lt_chunk_backward(const lt_problem* pb, int32_t local_norm, const void* W,
   a.dW = dW;
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
-  if ((rc = ck_launch(ck_kernel_c(a.PPL, bf16), a.B * a.K, ck_lds_c(a, bf16), st, a,
+  if ((rc = ck_launch(ck_kernel_c(a.PPL, bf16, a.V == 32), a.B * a.K, ck_lds_c(a, bf16), st, a,
                       64 * kMargWaves)))
     return rc;
   char* sc = (char*)scratch;

@@ -38,9 +38,12 @@ if os.environ.get('LT_CK_LDS_PAD'):
   print(f'LDS pad {os.environ["LT_CK_LDS_PAD"]}: {e0.elapsed_time(e1) / 10:.3f} ms per call')
 s = st.cpu().numpy().reshape(-1, 8)
 s = s[s[:, 0] > 0]
-names = ['DMA+tables', 'recursions', 'marginals', 'dW stream']
-for k, nm in enumerate(names):
-  d = s[:, k + 1] - s[:, k]
+segs = [('DMA+tables', 0, 1), ('nw + E', 1, 5), ('recursions', 5, 2), ('marginals', 2, 3),
+        ('dW stream', 3, 4)]
+for nm, i, j in segs:
+  if not s[:, j].any():
+    continue
+  d = s[:, j] - s[:, i]
   print(f'{nm:12s} median {np.median(d):8.0f}  p90 {np.percentile(d, 90):8.0f} cycles')
 tot = s[:, 4] - s[:, 0]
 print(f'{"total":12s} median {np.median(tot):8.0f}  p90 {np.percentile(tot, 90):8.0f}; '
