@@ -15,6 +15,41 @@ import torch
 from last_torch_amd import semirings
 
 
+_IN_ARCS = {}
+
+
+def _in_arcs(table: torch.Tensor, device) -> torch.Tensor:
+  """[C, D] flat arc indices p * V + (y - 1) into each destination state,
+  ascending, padded with C * V (one past the last arc) where the in-degree
+  is below the maximum D."""
+  key = (table.shape, table.cpu().numpy().tobytes(), str(device))
+  idx = _IN_ARCS.get(key)
+  if idx is None:
+    C, V = table.shape
+    dst = table.reshape(-1).long().cpu()
+    order = torch.argsort(dst * (C * V) + torch.arange(C * V), stable=True)
+    counts = torch.bincount(dst, minlength=C)
+    D = max(int(counts.max()), 1)
+    idx = torch.full((C, D), C * V, dtype=torch.int64)
+    start = torch.cumsum(counts, 0) - counts
+    for q in range(C):
+      idx[q, :counts[q]] = order[start[q]:start[q] + counts[q]]
+    idx = idx.to(device)
+    _IN_ARCS[key] = idx
+  return idx
+
+
+def _reduce_by_table(weights: torch.Tensor, table: torch.Tensor, semiring) -> torch.Tensor:
+  """result[..., q] = (+)_{p -y-> q} weights[..., p, y-1]: one gather of
+  every state's in-arcs (ascending, so the semiring's own tie rules see the
+  arcs in the order a per-state loop would) and one semiring sum."""
+  C, V = table.shape
+  idx = _in_arcs(table, weights.device)
+  flat = weights.reshape(*weights.shape[:-2], C * V)
+  pad = semiring.zeros((*flat.shape[:-1], 1), flat.dtype, flat.device)
+  return semiring.sum(torch.cat([flat, pad], dim=-1)[..., idx], dim=-1)
+
+
 class ContextDependency(abc.ABC):
   """A DFA over the lexical vocabulary whose states encode output history
   (contexts.py:25-146). All states are final; label 0 is epsilon."""
@@ -106,22 +141,9 @@ class FullNGram(ContextDependency):
     if tuple(weights.shape[-2:]) != self.shape():
       raise ValueError(f'weights.shape[-2:] should be {self.shape()} but got'
                        f' {tuple(weights.shape[-2:])}')
-    C, V = self.shape()
-    batch = weights.shape[:-2]
-    dst = self._arc_index(weights.device)
-    flat = weights.reshape(*batch, C * V)
-    # group arcs by destination; every destination has the same in-degree
-    # except the start (none) and the ascending states (one).
-    out = []
-    for q in range(C):
-      idx = torch.nonzero(dst == q).flatten()
-      if idx.numel() == 0:
-        out.append(semiring.zeros(batch, weights.dtype, weights.device))
-      elif idx.numel() == 1:
-        out.append(flat[..., idx[0]])
-      else:
-        out.append(semiring.sum(flat[..., idx], dim=-1))
-    return torch.stack(out, dim=-1)
+    # every destination has the same in-degree except the start (none) and
+    # the ascending states (one)
+    return _reduce_by_table(weights, self.next_state_table(), semiring)
 
   def backward_broadcast(self, weights):
     C, V = self.shape()
@@ -174,13 +196,7 @@ class NextStateTable(ContextDependency):
     C, V = self.shape()
     if tuple(weights.shape[-2:]) != (C, V):
       raise ValueError(f'weights.shape[-2:] should be {(C, V)} but got {tuple(weights.shape[-2:])}')
-    table = self.next_state_table.to(weights.device)
-    flat = weights.reshape(*weights.shape[:-2], C * V)
-    out = []
-    for q in range(C):
-      idx = torch.nonzero(table.reshape(-1) == q).reshape(-1)  # ascending (p, y)
-      out.append(semiring.sum(flat.index_select(-1, idx), dim=-1))
-    return torch.stack(out, dim=-1)
+    return _reduce_by_table(weights, self.next_state_table, semiring)
 
   def backward_broadcast(self, weights):
     """contexts.py:315-320: [..., C] -> [..., C, V] = weights[next_state]."""

@@ -401,29 +401,6 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
-// Auxiliary stream + events of this host thread and device: the
-// checkpointing backward runs on it concurrently with the forward.
-struct Fork {
-  hipStream_t s = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-};
-thread_local Fork g_fork[64];
-
-int get_fork(Fork** out) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return fail(LT_EHIP, std::string("hipGetDevice: ") + hipGetErrorString(e));
-  Fork& f = g_fork[dev & 63];
-  if (!f.s) {
-    if ((e = hipStreamCreateWithFlags(&f.s, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&f.e0, hipEventDisableTiming)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&f.e1, hipEventDisableTiming)) != hipSuccess)
-      return fail(LT_EHIP, std::string("aux stream: ") + hipGetErrorString(e));
-  }
-  *out = &f;
-  return LT_OK;
-}
-
 int make_ngram(int V, int n, NGram* g) {
   if (V <= 0) return fail(LT_EINVAL, "vocab_size must be > 0");
   if (n < 0) return fail(LT_EINVAL, "context_size must be >= 0");
@@ -922,19 +899,13 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   if (ck && lt_impl::pipe_eligible(pb))
     return lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
                                 num, alpha, alpha_num, beta, beta_num, arcs, 2, nullptr, stream);
-  // With checkpoints, the beta pass (independent of alpha) runs at the same
-  // time on an auxiliary stream; both workgroup kinds then share CUs, so
-  // each plan takes half the LDS when that still leaves a deep ring.
+  // With checkpoints, the beta pass (independent of alpha) and then the
+  // alpha pass, both on the caller's stream (the library forks no stream:
+  // everything stays ordered on `stream` and capturable).
   Plan pf, pbk;
-  int cap = kLdsMax;
   if (ck) {
-    const int half = kLdsMax / 2;
-    Plan t1, t2;
     const int bflags = F_NUM | (local_norm ? F_LOCAL : F_DEN);
-    if (env_int("LT_PAIR_LDS", 0) && plan(pb, g, 0, flags, &t1, half) == LT_OK &&
-        plan(pb, g, 2, bflags, &t2, half) == LT_OK && t1.a.S >= 6 && t2.a.S >= 6)
-      cap = half;
-    if ((rc = plan(pb, g, 2, bflags, &pbk, cap))) return rc;
+    if ((rc = plan(pb, g, 2, bflags, &pbk, kLdsMax))) return rc;
     bind_streams(pbk.a, W, nullptr, nullptr);
     pbk.a.nfr = num_frames;
     pbk.a.labels = labels;
@@ -942,7 +913,7 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
     pbk.a.beta = local_norm ? nullptr : beta;
     pbk.a.beta_num = beta_num;
   }
-  if ((rc = plan(pb, g, 0, flags, &pf, cap))) return rc;
+  if ((rc = plan(pb, g, 0, flags, &pf, kLdsMax))) return rc;
   bind_streams(pf.a, W, nullptr, nullptr);
   pf.a.nfr = num_frames;
   pf.a.labels = labels;
@@ -953,21 +924,8 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   pf.a.alpha = alpha;
   pf.a.alpha_num = alpha_num;
   pf.a.arcs = ck ? arcs : nullptr;
-  if (!ck) return launch_fwd(M_LOG, pf, bf16, pb->batch, st);
-  Fork* f = nullptr;
-  if ((rc = get_fork(&f))) return rc;
-  if ((rc = hip_check(hipEventRecord(f->e0, st), "event record"))) return rc;
-  if ((rc = hip_check(hipStreamWaitEvent(f->s, f->e0, 0), "stream wait"))) return rc;
-  // LT_CK_SOLO (timing experiments only): 1 = beta pass only, 2 = alpha pass only
-#ifdef LT_DIAG
-  const int solo = env_int("LT_CK_SOLO", 0);
-#else
-  const int solo = 0;
-#endif
-  if (solo != 2 && (rc = launch_bwd(pbk, bf16, pb->batch, f->s))) return rc;
-  if (solo != 1 && (rc = launch_fwd(M_LOG, pf, bf16, pb->batch, st))) return rc;
-  if ((rc = hip_check(hipEventRecord(f->e1, f->s), "event record"))) return rc;
-  return hip_check(hipStreamWaitEvent(st, f->e1, 0), "stream wait");
+  if (ck && (rc = launch_bwd(pbk, bf16, pb->batch, st))) return rc;
+  return launch_fwd(M_LOG, pf, bf16, pb->batch, st);
 }
 
 int lt_den_backward(const lt_problem* pb, const void* W, const int32_t* num_frames,

@@ -14,11 +14,13 @@ weights once through the ``WeightFn`` plugin as a contiguous
   _string_forward -> lt_num_forward
   shortest_path   -> lt_viterbi
 
-Supported: ``alignments.FrameDependent`` x ``contexts.FullNGram``. Anything
-else raises ``NotImplementedError`` -- there is no CPU fallback. Inputs on
-the CPU are moved to the current ROCm device and results moved back.
-Arbitrary batch dims are flattened (the reference's ``_string_forward``
-supports only one, D13).
+The device of the arc weights picks the implementation, as in the
+reference: ROCm tensors run the HIP kernels (FrameDependent and
+FrameLabelDependent alignments, FullNGram or any next-state table), CPU
+tensors the PyTorch restatement in ``cpu.py`` (FrameDependent). There is no
+fallback between the two: a ROCm tensor never runs on the CPU, and a missing
+HIP library raises. Arbitrary batch dims are flattened (the reference's
+``_string_forward`` supports only one, D13).
 """
 from collections.abc import Callable, Sequence
 from typing import Any, Generic, Optional, Protocol, TypeVar
@@ -28,6 +30,7 @@ import torch.nn as nn
 
 from last_torch_amd import _native
 from last_torch_amd import alignments
+from last_torch_amd import cpu
 from last_torch_amd import contexts
 from last_torch_amd import semirings
 from last_torch_amd import weight_fns
@@ -45,15 +48,13 @@ def _semiring_id(semiring) -> int:
   return _SEMIRING_IDS[name]
 
 
-def _compute_device(*tensors) -> torch.device:
-  for t in tensors:
+def _compute_device(W, *tensors) -> torch.device:
+  """The arc weights' device (a ROCm device if any input is on one): ROCm
+  -> HIP kernels, CPU -> cpu.py."""
+  for t in (W, *tensors):
     if isinstance(t, torch.Tensor) and t.is_cuda:
       return t.device
-  if not torch.cuda.is_available():
-    raise _native.LatticeLibraryError(
-        'last_torch_amd lattice operations run on a ROCm GPU (no CPU fallback); '
-        'no device is available')
-  return torch.device('cuda', torch.cuda.current_device())
+  return torch.device('cpu')
 
 
 def _lengths(x, batch_numel, device) -> torch.Tensor:
@@ -70,34 +71,44 @@ def _kernel_weights(W: torch.Tensor) -> torch.Tensor:
 
 
 class _LossFn(torch.autograd.Function):
-  """loss = log_z - num (or -num), lattices.py:131-183.
+  """loss = log_z - num (or -num), lattices.py:131-183, on the HIP kernels.
 
-  When W needs a gradient the forward calls lt_loss_grad, which returns the
-  loss together with d(sum loss)/dW -- for the bigram ONE launch in which the
-  alpha and beta recursions run while other workgroups turn every frame they
-  have both passed into arc marginals. The backward then only applies the
-  incoming gradient (lt_scale_grad, in place; free where it is 1). Without a
-  gradient only lt_loss_forward runs."""
+  The forward keeps only what the backward needs: for the bigram (V <= 32)
+  the chunked scan's boundary state (lt_chunk_forward; ~12 MB at B=64,
+  T=1000 against dW's 279 MB), for other n-grams the forward alphas
+  (lt_loss_forward). dW is formed in the backward, already scaled by the
+  incoming gradient (lt_chunk_backward / lt_loss_backward): a forward that is
+  never differentiated costs no dW, and the graph can be backpropagated more
+  than once (retain_graph). Without a gradient only the loss is computed."""
 
   @staticmethod
   def forward(ctx, W, nf, labels, nl, V, n, local):
-    ctx.cfg = (V, n)
-    if ctx.needs_input_grad[0]:
-      loss, _, _, dW = _native.loss_grad(W, nf, labels, nl, V, n, local)
-      ctx.dW = dW
-      return loss
-    ctx.dW = None
-    return _native.loss_forward(W, nf, labels, nl, V, n, local, want_alpha=False)[0]
+    ctx.cfg = (V, n, local)
+    ctx.mode = None
+    if not ctx.needs_input_grad[0]:
+      return _native.loss_forward(W, nf, labels, nl, V, n, local, want_alpha=False)[0]
+    B, T = W.shape[:2]
+    if _native.chunk_path(B, T, labels.shape[-1], V, n):
+      loss, _, _, state = _native.chunk_forward(W, nf, labels, nl, V, n, local)
+      ctx.mode = 'chunk'
+      ctx.save_for_backward(W, nf, labels, nl, state)
+    else:
+      loss, lz, num, alpha, an = _native.loss_forward(W, nf, labels, nl, V, n, local,
+                                                      want_alpha=True)
+      ctx.mode = 'alpha'
+      ctx.save_for_backward(W, nf, labels, nl, lz, num, alpha, an)
+    return loss
 
   @staticmethod
   def backward(ctx, g):
-    dW = ctx.dW
-    if dW is None:
-      raise RuntimeError('the lattice loss gradient was already consumed: backward through '
-                         'RecognitionLattice.forward twice is not supported (call it again)')
-    ctx.dW = None
-    V, n = ctx.cfg
-    _native.scale_grad(dW, g, V, n)
+    V, n, local = ctx.cfg
+    g = g.float().contiguous()
+    if ctx.mode == 'chunk':
+      W, nf, labels, nl, state = ctx.saved_tensors
+      dW = _native.chunk_backward(W, nf, labels, nl, V, n, local, state, grad=g)
+    else:
+      W, nf, labels, nl, lz, num, alpha, an = ctx.saved_tensors
+      dW = _native.loss_backward(W, nf, labels, nl, lz, num, alpha, an, g, V, n, local)
     return dW, None, None, None, None, None, None
 
 
@@ -270,8 +281,11 @@ class RecognitionLattice(nn.Module, Generic[T]):
     for d in batch_dims:
       B *= d
     dev = _compute_device(W, frames, num_frames)
-    W = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
+    W = W.to(dev).reshape(B, *W.shape[-3:])
+    W = _kernel_weights(W) if dev.type == 'cuda' else W.float()
     nf = _lengths(num_frames, B, dev)
+    if dev.type != 'cuda':
+      nf = nf.long()
     return W, nf, batch_dims, B, V, n, cache
 
   @staticmethod
@@ -297,7 +311,9 @@ class RecognitionLattice(nn.Module, Generic[T]):
     lab = torch.as_tensor(labels).reshape(B, -1).to(device=W.device, dtype=torch.int32)
     nl = _lengths(num_labels, B, W.device)
     local = isinstance(self.weight_fn, weight_fns.LocallyNormalizedWeightFn)
-    if self._table_path():
+    if W.device.type == 'cpu':
+      loss = cpu.loss(W, nf, lab, nl.long(), self.context, self.alignment, local)
+    elif self._table_path():
       loss = _TableLossFn.apply(W, nf, lab.contiguous(), nl, self._graph(W.device), local)
     else:
       loss = _LossFn.apply(W, nf, lab.contiguous(), nl, V, n, local)
@@ -316,7 +332,9 @@ class RecognitionLattice(nn.Module, Generic[T]):
     conv = {'reference': _native.LABELS_REFERENCE, 'true': _native.LABELS_TRUE}[label_convention]
     W, nf, batch_dims, B, V, n, _ = self._prepare(cache, frames, num_frames)
     with torch.no_grad():
-      if self._table_path():
+      if W.device.type == 'cpu':
+        labels, weights = cpu.viterbi(W, nf, self.context, self.alignment, label_convention)
+      elif self._table_path():
         # A labels per frame: slot i = the (i+1)-th lexical label of the frame
         labels, weights = _native.table_viterbi(self._graph(W.device), W.detach(), nf, conv)
       else:
@@ -344,7 +362,9 @@ class RecognitionLattice(nn.Module, Generic[T]):
     W, nf, batch_dims, B, V, n, _ = self._prepare(cache, frames, num_frames)
     lab = torch.as_tensor(labels).reshape(B, -1).to(device=W.device, dtype=torch.int32)
     nl = _lengths(num_labels, B, W.device)
-    if self._table_path():  # values only: gradients come through forward()
+    if W.device.type == 'cpu':
+      num = cpu.num_forward(W, nf, lab, nl.long(), self.context, self.alignment, semiring)
+    elif self._table_path():  # values only: gradients come through forward()
       num = _native.table_num_forward(self._graph(W.device), W.detach(), nf, lab.contiguous(),
                                       nl, sid)
     else:
@@ -392,8 +412,14 @@ class RecognitionLattice(nn.Module, Generic[T]):
     for d in batch_dims:
       B *= d
     dev = _compute_device(W, frames, num_frames)
-    Wk = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
     nf = _lengths(num_frames, B, dev)
+    if dev.type == 'cpu':
+      dist, alpha = cpu.den_forward(W.reshape(B, *W.shape[-3:]).float(), nf.long(), self.context,
+                                    self.alignment, semiring)
+      C = alpha.shape[-1]
+      return (dist.reshape(batch_dims),
+              alpha.reshape(*batch_dims, frames.shape[-2], C))
+    Wk = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
     if table:  # values only: gradients come through forward() / shortest_path()
       dist, alpha = _native.table_forward(self._graph(Wk.device), Wk.detach(), nf, sid)
     else:
@@ -434,24 +460,45 @@ class RecognitionLattice(nn.Module, Generic[T]):
     if tuple(alpha_0_to_T_minus_1.shape[:-2]) != batch_dims:
       raise ValueError('alpha_0_to_T_minus_1 and num_frames have different '
                        f'batch_dims: {tuple(alpha_0_to_T_minus_1.shape[:-2])} vs {batch_dims}')
-    V, n = self._ngram()
     with torch.no_grad():
       W = self.arc_weights(cache, frames)
       B = 1
       for d in batch_dims:
         B *= d
       dev = _compute_device(W, frames, num_frames)
-      Wk = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
       nf = _lengths(num_frames, B, dev)
-      lz = log_z.detach().reshape(B).to(dev, torch.float32).contiguous()
-      al = alpha_0_to_T_minus_1.detach().reshape(B, Wk.shape[1], -1).to(dev, torch.float32)
-      marg = _native.den_backward(Wk, nf, lz, al.contiguous(), None, V, n).float()
-      marg = self._home(marg.reshape(*batch_dims, *marg.shape[1:]), frames)
+    if dev.type == 'cpu':
+      # arc marginals = d log_z / dW (the reference's backward algorithm
+      # computes the same quantities frame by frame)
+      with torch.enable_grad():
+        Wd = W.detach().reshape(B, *W.shape[-3:]).float().requires_grad_(True)
+        dist, _ = cpu.den_forward(Wd, nf.long(), self.context, self.alignment, semirings.Log)
+        (marg,) = torch.autograd.grad(dist.sum(), Wd)
+      marg = marg.reshape(*batch_dims, *marg.shape[1:])
+    else:
+      V, n = self._ngram()
+      with torch.no_grad():
+        Wk = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
+        lz = log_z.detach().reshape(B).to(dev, torch.float32).contiguous()
+        al = alpha_0_to_T_minus_1.detach().reshape(B, Wk.shape[1], -1).to(dev, torch.float32)
+        marg = _native.den_backward(Wk, nf, lz, al.contiguous(), None, V, n).float()
+        marg = self._home(marg.reshape(*batch_dims, *marg.shape[1:]), frames)
     tdim = len(batch_dims)
     carry, outs = init_callback_carry, []
+    # weight_vjp_fn(cotangent) -> (d cache, d frame); a cache that is not a
+    # tree of tensors (NullCacher: None) is held fixed and gets None
+    leaves = torch.utils._pytree.tree_leaves(cache)
+    cache_is_tensor = cache is not None and all(isinstance(x, torch.Tensor) for x in leaves)
+
+    def frame_vjp(frame):
+      if cache_is_tensor:
+        return torch.func.vjp(lambda c, f: self.weight_fn(c, f), cache, frame)[1]
+      fn = torch.func.vjp(lambda f: self.weight_fn(cache, f), frame)[1]
+      return lambda ct: (None, *fn(ct))
+
     for t in reversed(range(frames.shape[-2])):
       frame = frames.select(tdim, t)
-      _, vjp_fn = torch.func.vjp(lambda c, f: self.weight_fn(c, f), cache, frame)
+      vjp_fn = frame_vjp(frame)
       m = marg.select(tdim, t)
       carry, out = callback(weight_vjp_fn=vjp_fn, carry=carry, blank_marginal=m[..., 0],
                             lexical_marginals=m[..., 1:])

@@ -276,6 +276,11 @@ def main(ref_path):
   rand_case('unreachable', 3, 5, 6, 3, 1, nf=[5, 2, 0], nl=[6, 3, 1])
   rand_case('bf16_bigram', 2, 10, 4, 5, 1, nf=[10, 9], nl=[4, 3], bf16=True)
   rand_case('v1_bigram', 2, 6, 3, 1, 1, nf=[6, 4], nl=[3, 2])
+  # BASELINE.json configs[0] at its exact shape: B=2, T=8, U=4, vocab 5,
+  # FullNGram order 0 (its own generator: the fixtures above stay as they were)
+  rng_cfg1 = np.random.default_rng(1)
+  lattice_case('cfg1', rng_cfg1.standard_normal((2, 8, 1, 6)).astype(np.float32), [8, 8],
+               rng_cfg1.integers(1, 6, (2, 4)), [4, 4], 5, 0)
 
   # --- 2. FullNGram closed forms (contexts.py:181-256, 109-146)
   d = {}

@@ -136,22 +136,29 @@ def test_lattice_validates_batch_dims():
     lat.shortest_path(frames[:1], nf)
 
 
-def test_lattice_without_gpu_fails_loudly():
-  """The product path has no CPU fallback: without a ROCm device the
-  lattice raises instead of computing anything."""
-  if torch.cuda.is_available():
-    pytest.skip('GPU present')
-  table = torch.zeros([2, 3, 3, 3])
+def test_lattice_device_dispatch():
+  """The device of the arc weights picks the implementation: CPU tensors run
+  the PyTorch restatement (cpu.py) with no GPU involved; the HIP path is
+  taken only for ROCm tensors, and a ROCm tensor with the library missing
+  raises (tests/test_abi_and_sharding.py checks the loader)."""
+  table = torch.randn([2, 3, 3, 3])
   lat = lt.RecognitionLattice(
       context=lt.contexts.FullNGram(vocab_size=2, context_size=1),
       alignment=lt.alignments.FrameDependent(),
       weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
       weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(table))
   frames = torch.arange(3.)[None, :, None].expand(2, 3, 1)
-  with pytest.raises(Exception):
-    lat(frames, torch.tensor([3, 2]), torch.ones([2, 2]), torch.tensor([1, 1]))
-  with pytest.raises(Exception):
-    lat.shortest_path(frames, torch.tensor([3, 2]))
+  loss = lat(frames, torch.tensor([3, 2]), torch.ones([2, 2]), torch.tensor([1, 1]))
+  assert loss.device.type == 'cpu' and torch.isfinite(loss).all()
+  labels, _, weights = lat.shortest_path(frames, torch.tensor([3, 2]))
+  assert labels.shape == (2, 3) and weights.device.type == 'cpu'
+  fsa = lt.RecognitionLattice(
+      context=lt.contexts.FullNGram(vocab_size=2, context_size=1),
+      alignment=lt.alignments.FrameLabelDependent(max_expansions=2),
+      weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+      weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(table))
+  with pytest.raises(NotImplementedError, match='FrameDependent'):
+    fsa(frames, torch.tensor([3, 2]), torch.ones([2, 2]), torch.tensor([1, 1]))
 
 
 # ---------------------------------------------------------------------------
