@@ -1,12 +1,14 @@
 """Benchmark: Log-semiring lattice forward-backward (loss + dW) on MI355X.
 
 One step = one pass of the hot path over one batch of synthetic arc weights
-already resident in HBM: lt_loss_grad (loss and dW = d(sum loss)/dW; for the
-bigram at B=64 ONE launch in which the alpha and beta recursions run while
-other workgroups turn every frame both have passed into arc marginals), then
-lt_scale_grad with the incoming gradient (ones), plus, for N > 1, the single
-RCCL all-reduce of the summed loss. --design checkpoints /
-recursion time the two-call designs (lt_loss_forward + lt_loss_backward).
+already resident in HBM: lt_loss_grad, i.e. the loss and dW = d(sum
+loss)/dW (what loss.sum().backward() needs). For the bigram it is the
+chunked two-level scan (lt_chunk.hip: ck_transfer_kernel -> ck_combine_kernel
+-> ck_marg_kernel, plus the frame-serial pair whose workgroups exit at once
+unless an utterance is out of the fast path's range). For N > 1 the step
+adds the single RCCL all-reduce of the summed loss.
+--design checkpoints / recursion time the older two-call designs
+(lt_loss_forward + lt_loss_backward).
 
 Workload (BASELINE.json configs[1], weak-scaled per GPU as configs[2]):
 B=64 utterances per GPU, T=1000 frames, U=100 labels, V=32, bigram FullNGram
@@ -74,8 +76,9 @@ def make_inputs(B, T, U, V, C, device, seed, dtype=torch.float32):
 
 def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, checkpoints=True,
               fused=False):
-  """Returns (wall seconds over `steps`, fwd kernel ms list, bwd kernel ms list);
-  fused: lt_loss_grad (fwd list) + lt_scale_grad (bwd list)."""
+  """Returns (wall seconds over `steps`, fwd ms list, bwd ms list); fused:
+  lt_loss_grad in one C-ABI call (fwd list; bwd list empty), else
+  lt_loss_forward (fwd list) + lt_loss_backward (bwd list)."""
   grad = torch.ones([W.shape[0]], dtype=torch.float32, device=W.device)
   ws = None
   if fused:
@@ -93,7 +96,6 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, chec
       loss, _, _, dW = _native.loss_grad(W, nf, labels, nl, V, n, False, workspace=ws)
       if ev is not None:
         ev[1].record()
-      _native.scale_grad(dW, grad, V, n)
     else:
       out = _native.loss_forward(W, nf, labels, nl, V, n, False, checkpoints=checkpoints)
       loss, log_z, num, alpha, an = out[:5]
@@ -124,7 +126,7 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, chec
   torch.cuda.synchronize()
   wall = time.perf_counter() - t0
   fwd_ms = [e[0].elapsed_time(e[1]) for e in evs] if events else []
-  bwd_ms = [e[1].elapsed_time(e[2]) for e in evs] if events else []
+  bwd_ms = [e[1].elapsed_time(e[2]) for e in evs] if (events and not fused) else []
   return wall, fwd_ms, bwd_ms
 
 
@@ -162,6 +164,37 @@ def joint_step_leg(T, U, V, n, device, B=64, F=256, H=512, reps=5):
     out[f'{name}_ms_per_step'] = e0.elapsed_time(e1) / reps
   out['speedup'] = out['pytorch_hidden_ms_per_step'] / out['producer_ms_per_step']
   return out
+
+
+def cpu_ref(T, U, V, n, sample_utts):
+  """SURVEY 8(d) cpu_ref: the reference's own CPU formulation -- PyTorch on
+  the host, the per-frame recursion vectorised over the batch and the
+  states, dW by autograd (last_torch_amd/cpu.py, the drop-in's CPU path) --
+  at full thread count, on a bounded sample of the same workload."""
+  import last_torch_amd as lt
+  from last_torch_amd import cpu
+  g = torch.Generator().manual_seed(0)
+  W = torch.randn([sample_utts, T, V + 1, V + 1], generator=g).requires_grad_(True)
+  nf = torch.full([sample_utts], T)
+  lab = torch.randint(1, V + 1, (sample_utts, U), generator=g)
+  nl = torch.full([sample_utts], U)
+  ctx = lt.contexts.FullNGram(vocab_size=V, context_size=n)
+  t0 = time.perf_counter()
+  loss = cpu.loss(W, nf, lab, nl, ctx, lt.alignments.FrameDependent(), False)
+  loss.sum().backward()
+  dt = time.perf_counter() - t0
+  C = V + 1
+  return {
+      'value': sample_utts * T * U * C / dt,
+      'unit': 'cells/s',
+      'cores': torch.get_num_threads(),
+      'kind': 'port',
+      'affinity_cores': len(os.sched_getaffinity(0)),
+      'torch_threads': torch.get_num_threads(),
+      'sample': (f'PyTorch CPU (last_torch_amd/cpu.py, the reference per-frame algorithm, '
+                 f'fp32, autograd dW) loss+dW on {sample_utts} utterances of T={T} U={U} V={V} '
+                 f'n={n}: {dt:.2f} s on {torch.get_num_threads()} threads'),
+  }
 
 
 def cpu_baseline(T, U, V, n, C, sample_utts):
@@ -205,6 +238,39 @@ def read_traffic(profile_json, kernels, B, T):
     return None
 
 
+def chunk_design_bytes(T, U, V, L, es=4):
+  """Per-frame HBM bytes the chunked design moves:
+  W read by ck_transfer_kernel and again by ck_marg_kernel, dW written once;
+  per chunk of L frames a 1224-float record and the numerator group bands
+  (NPG x 8 floats per 7-frame group) written by A and read by B; the
+  boundary vectors written by B and read by C; the frame offsets c_t."""
+  Aw = (V + 1) * (V + 1)
+  NPG = (U + 2) & ~1
+  CP = (V + 4) & ~3
+  groups = -(-L // 7)
+  rec = 1224 * 4 * 2 / L
+  bands = groups * 8 * NPG * 4 * 2 / L
+  bound = 2 * (CP + NPG) * 4 * 2 / L
+  return Aw * es * 3 + rec + bands + bound + 4 * 2
+
+
+def chunk_len(B, T, U, V):
+  """The chunk length lt_chunk.hip picks (its LDS budget, mirrored)."""
+  FB = (V + 1) * (V + 1) * 4
+  NPG = (U + 2) & ~1
+  CP = (V + 4) & ~3
+  al16 = lambda x: (x + 15) & ~15
+  budget = int(os.environ.get('LT_CHUNK_LDS', 40 * 1024))
+  L = max(1, min(32, int(os.environ.get('LT_CHUNK_LEN', 32))))
+  while True:
+    n16 = (L * FB + 30) // 16
+    b = ((n16 + 63) // 64) * 1024 + 2 * al16(4 * L * CP) + 2 * al16(4 * L * NPG) + \
+        al16(8 * L * NPG) + al16(32 * L) + al16(8 * NPG + 4 * U) + al16(4 * L) + 1024
+    if L <= 4 or b <= budget:
+      return L
+    L -= 1
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
@@ -215,16 +281,18 @@ def main():
   ap.add_argument('--labels', type=int, default=100)
   ap.add_argument('--vocab', type=int, default=32)
   ap.add_argument('--context', type=int, default=1)
-  ap.add_argument('--cpu-utts', type=int, default=int(os.environ.get('LT_BENCH_CPU_UTTS', 512)))
+  ap.add_argument('--cpu-utts', type=int, default=int(os.environ.get('LT_BENCH_CPU_UTTS', 128)),
+                  help='utterances of the C-oracle baseline (0: skip)')
+  ap.add_argument('--cpu-ref-utts', type=int,
+                  default=int(os.environ.get('LT_BENCH_CPU_REF_UTTS', 8)),
+                  help='utterances of the PyTorch-CPU cpu_ref baseline (0: skip)')
   ap.add_argument('--no-north-star', action='store_true')
+  ap.add_argument('--no-joint', action='store_true')
   ap.add_argument('--design', choices=['auto', 'checkpoints', 'recursion'], default='auto',
-                  help='auto: lt_loss_grad (one fused launch where eligible, else the '
-                       'library policy below); checkpoints: lt_loss_forward with the '
-                       'concurrent beta pass + lt_loss_backward marginal pass; recursion: '
-                       'lt_loss_forward + beta recursion with fused marginals')
-  ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r01_pmc_summary.json'),
-                  help='PMC summary of the checkpointing design; *_fused.json / '
-                       '*_recursion.json for the others')
+                  help='auto: lt_loss_grad (the chunked scan for the bigram); checkpoints / '
+                       'recursion: the two-call lt_loss_forward + lt_loss_backward designs')
+  ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r02_pmc_summary.json'),
+                  help='PMC summary (tools/pmc_summary.py) the traffic figure is read from')
   args = ap.parse_args()
 
   world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -239,9 +307,8 @@ def main():
   B, T, U, V, n = args.batch, args.frames, args.labels, args.vocab, args.context
   C = _native.num_context_states(V, n)
   W, nf, labels, nl = make_inputs(B, T, U, V, C, device, seed=1234 + rank)
-  ckpt = (_native.prefer_checkpoints(B, device, (T, U, V, n, False)) if args.design == 'auto'
-          else args.design == 'checkpoints')
-  fused = args.design == 'auto' and _native.fused_path(B, T, U, V, n, device)
+  fused = args.design == 'auto'
+  ckpt = args.design == 'checkpoints'
   wall, fwd_ms, bwd_ms = run_steps(W, nf, labels, nl, V, n, args.steps, args.warmup, dist_on,
                                    checkpoints=ckpt, fused=fused)
 
@@ -253,25 +320,35 @@ def main():
   value = cells_per_step * args.steps / wall
 
   fwd_b, bwd_b, survey_b = algorithmic_bytes(T, U, V, C, checkpoints=ckpt)
-  fwd_avg = float(np.mean(fwd_ms)) * 1e-3
-  bwd_avg = float(np.mean(bwd_ms)) * 1e-3
-  if fused:  # one launch does both passes' work (fwd list = lt_loss_grad)
-    fwd_b, bwd_b = fwd_b + bwd_b, 0
-  dominant, dom_bytes, dom_s = ('loss_backward', bwd_b * B * T, bwd_avg) \
-      if bwd_avg >= fwd_avg else ('loss_forward', fwd_b * B * T, fwd_avg)
-  achieved = dom_bytes / dom_s / 1e9
+  chunk = fused and _native.chunk_path(B, T, U, V, n)
   if fused:
-    dominant = 'loss_grad'
-    knames = ['pipe_kernel']
-  elif ckpt:
-    fk = (['pipe_kernel'] if _native.pipe_path(B, T, U, V, n)
-          else ['fwd_kernel', 'bwd_kernel_ck'])
-    knames = ['marg_kernel'] if dominant == 'loss_backward' else fk
+    call_s = float(np.mean(fwd_ms)) * 1e-3
+    if chunk:
+      L = chunk_len(B, T, U, V)
+      knames = ['ck_transfer_kernel', 'ck_combine_kernel', 'ck_marg_kernel']
+      design = (f'chunked two-level scan, L={L} frames per chunk (lt_chunk.hip: '
+                f'ck_transfer_kernel -> ck_combine_kernel -> ck_marg_kernel)')
+      design_b = chunk_design_bytes(T, U, V, L)
+    else:
+      knames = ['pipe_kernel'] if _native.fused_path(B, T, U, V, n, device) else ['lt_loss_grad']
+      design = 'lt_loss_grad (fused pipe)' if knames == ['pipe_kernel'] else 'lt_loss_grad'
+      design_b = fwd_b + bwd_b
+    kernel = f"lt_loss_grad ({' + '.join(knames)})"
+    kernels_ms = {'loss_grad': call_s * 1e3}
   else:
-    knames = ['bwd_kernel'] if dominant == 'loss_backward' else ['fwd_kernel']
-  pmc = (args.pmc.replace('.json', '_fused.json') if fused else
-         args.pmc if ckpt else args.pmc.replace('.json', '_recursion.json'))
-  traffic = read_traffic(pmc, knames, B, T)
+    fwd_avg = float(np.mean(fwd_ms)) * 1e-3
+    bwd_avg = float(np.mean(bwd_ms)) * 1e-3
+    call_s = fwd_avg + bwd_avg
+    knames = ['fwd_kernel', 'bwd_kernel_ck' if ckpt else 'bwd_kernel', 'marg_kernel']
+    design = 'checkpointing (alpha || beta, then marginal pass)' if ckpt else 'recursion backward'
+    design_b = fwd_b + bwd_b
+    kernel = 'lt_loss_forward + lt_loss_backward'
+    kernels_ms = {'loss_forward': fwd_avg * 1e3, 'loss_backward': bwd_avg * 1e3}
+  # roofline: SURVEY 8(d)'s design-independent bytes per frame for every
+  # design (the design's own bytes are reported beside it), over the C-ABI
+  # call's own duration (HIP events on the stream the kernels run on)
+  achieved = survey_b * B * T / call_s / 1e9
+  traffic = read_traffic(args.pmc, knames, B, T)
 
   result = None
   if rank == 0:
@@ -296,23 +373,20 @@ def main():
             'vocab': V, 'context_size': n, 'context_states': C,
             'parallelism': f'utterance-sharded x{world}, RCCL all-reduce of summed loss',
         },
-        'kernels_ms': ({'loss_grad': fwd_avg * 1e3, 'scale_grad': bwd_avg * 1e3} if fused else
-                       {'loss_forward': fwd_avg * 1e3, 'loss_backward': bwd_avg * 1e3}),
+        'design': design,
+        'kernels_ms': kernels_ms,
         'roofline': {
             'bound': 'hbm',
-            'kernel': f"{dominant} ({' || '.join(knames)})",
+            'kernel': kernel,
             'achieved': achieved,
             'peak': HBM_PEAK_GBS,
             'unit': 'GB/s',
             'frac': achieved / HBM_PEAK_GBS,
             'traffic': traffic,
-            'algorithmic_bytes_per_frame': {'loss_forward': fwd_b, 'loss_backward': bwd_b,
-                                            'survey_step': survey_b},
+            'survey_bytes_per_frame': survey_b,
+            'design_bytes_per_frame': design_b,
+            'traffic_bytes_per_frame': traffic / (B * T) if traffic else None,
         },
-        'design': ('fused (alpha || beta recursions with concurrent marginal workgroups, '
-                   'one launch)' if fused else
-                   'checkpointing (alpha || beta, then marginal pass)' if ckpt
-                   else 'recursion backward'),
     }
     result['step_gbs'] = survey_b * B * T * world / (wall / args.steps) / 1e9
     result['hbm_frac_step'] = result['step_gbs'] / HBM_PEAK_GBS
@@ -323,25 +397,28 @@ def main():
     torch.cuda.empty_cache()
     W2, nf2, lab2, nl2 = make_inputs(256, T, U, V, C, device, seed=99)
     steps2 = max(5, args.steps // 2)
-    ck2 = (_native.prefer_checkpoints(256, device, (T, U, V, n, False)) if args.design == 'auto'
-           else args.design == 'checkpoints')
-    wall2, f2, b2 = run_steps(W2, nf2, lab2, nl2, V, n, steps2, 2, False, checkpoints=ck2)
-    fb2, bb2, _ = algorithmic_bytes(T, U, V, C, checkpoints=ck2)
+    wall2, f2, b2 = run_steps(W2, nf2, lab2, nl2, V, n, steps2, 2, False, checkpoints=ckpt,
+                              fused=fused)
     ms2 = wall2 / steps2 * 1e3
+    call2 = float(np.mean(f2)) + (float(np.mean(b2)) if b2 else 0.0)
     result['north_star_b256'] = {
         'value': 256 * T * U * C * steps2 / wall2,
         'ms_per_step': ms2,
+        'ms_per_call': call2,
         'hbm_frac_step': survey_b * 256 * T / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
-        'kernels_ms': {'loss_forward': float(np.mean(f2)), 'loss_backward': float(np.mean(b2))},
-        'frac_loss_backward': bb2 * 256 * T / (float(np.mean(b2)) * 1e-3) / 1e9 / HBM_PEAK_GBS,
-        'design': 'checkpoints' if ck2 else 'recursion',
+        'frac_call': survey_b * 256 * T / (call2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        'design': design if fused else ('checkpoints' if ckpt else 'recursion'),
     }
     del W2
     torch.cuda.empty_cache()
-    result['joint_weight_fn_step'] = joint_step_leg(T, U, V, n, device)
+    if not args.no_joint:
+      result['joint_weight_fn_step'] = joint_step_leg(T, U, V, n, device)
 
-  if rank == 0 and not dist_on and args.cpu_utts > 0:
-    result['cpu_baseline'] = cpu_baseline(T, U, V, n, C, args.cpu_utts)
+  if rank == 0 and not dist_on:
+    if args.cpu_ref_utts > 0:
+      result['cpu_baseline'] = cpu_ref(T, U, V, n, args.cpu_ref_utts)
+    if args.cpu_utts > 0:
+      result['cpu_baseline_oracle'] = cpu_baseline(T, U, V, n, C, args.cpu_utts)
   if rank == 0:
     print(json.dumps(result), flush=True)
   if dist_on:

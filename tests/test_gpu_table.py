@@ -152,7 +152,7 @@ def test_frame_label_dependent_api(cuda):
   table = torch.tensor(W, device=cuda, requires_grad=True)
   lat = _table_lattice(lt.contexts.FullNGram(vocab_size=V, context_size=n),
                        lt.alignments.FrameLabelDependent(max_expansions=K), table)
-  frames = torch.arange(T, dtype=torch.float32)[None, :, None].expand(B, T, 1).contiguous()
+  frames = torch.arange(T, dtype=torch.float32, device=cuda)[None, :, None].expand(B, T, 1).contiguous()
   num_frames = torch.tensor([6, 3, 2, 1])
   labels = torch.tensor([[1, 1, 1, 1], [2, 2, 2, 2], [1, 2, 1, 2], [2, 1, 2, 1]])
   num_labels = torch.tensor([4, 3, 4, 3])
@@ -193,7 +193,7 @@ def test_next_state_table_api(cuda):
   for K, align in ((0, lt.alignments.FrameDependent()),
                    (1, lt.alignments.FrameLabelDependent(max_expansions=1))):
     lat = _table_lattice(ctx, align, table)
-    frames = torch.arange(T, dtype=torch.float32)[None, :, None].expand(B, T, 1).contiguous()
+    frames = torch.arange(T, dtype=torch.float32, device=cuda)[None, :, None].expand(B, T, 1).contiguous()
     nf = np.array([12, 7, 3], np.int32)
     lab = rng.integers(1, V + 1, (B, U)).astype(np.int32)
     nl = np.array([4, 2, 1], np.int32)

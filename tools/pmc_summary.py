@@ -14,6 +14,10 @@ Corrections (MI355X_MICROARCH.md "HBM [CDNA4]"):
     kernels are 16 B/lane LDS-DMA reads, so FETCH_SIZE is doubled.
   * WRITE_SIZE (KiB) is exact for 16 B/lane streaming stores and dword
     float stores; it is taken as is.
+  * The chunked path's transfer kernel (ck_transfer_kernel) reads W with
+    dword loads, a width the guide leaves uncalibrated; it reads every frame
+    exactly once (B*T*FR*4 bytes), so its doubled FETCH_SIZE against that
+    count is the calibration, printed as ``fetch_vs_w``.
 """
 import argparse
 import csv
@@ -38,7 +42,8 @@ def _kernel_key(name):
   if 'bwd_kernel' in name:
     args = name.split('bwd_kernel<', 1)[-1].split('>', 1)[0].split(',')
     return 'bwd_kernel_ck' if len(args) >= 6 and args[5].strip() == 'true' else 'bwd_kernel'
-  for k in ('fwd_kernel', 'marg_kernel', 'backtrace_kernel', 'num_scatter_kernel', 'pipe_kernel',
+  for k in ('ck_transfer_kernel', 'ck_combine_kernel', 'ck_marg_kernel',
+            'fwd_kernel', 'marg_kernel', 'backtrace_kernel', 'num_scatter_kernel', 'pipe_kernel',
             'joint_weights_fb_kernel', 'joint_weights_kernel', 'joint_backward_kernel',
             'joint_exp_kernel', 'joint_reduce_kernel'):
     if k in name:
@@ -67,6 +72,8 @@ def main():
   ap.add_argument('--batch', type=int, required=True)
   ap.add_argument('--frames', type=int, required=True)
   ap.add_argument('--out', required=True)
+  ap.add_argument('--w-bytes', type=float, default=None,
+                  help='bytes of W per launch (B*T*C*(V+1)*4): fetch_vs_w calibration')
   args = ap.parse_args()
   fetch = collect(args.fetch, 'FETCH_SIZE')
   write = collect(args.write, 'WRITE_SIZE')
@@ -84,6 +91,8 @@ def main():
         'hbm_bytes_per_launch': (fb or 0) + (wb or 0) if (fb is not None and wb is not None)
         else None,
     }
+    if args.w_bytes and fb is not None:
+      kernels[k]['fetch_vs_w'] = fb / args.w_bytes
   res = {'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)',
          'corrections': 'FETCH_SIZE KiB x1024 x2 (gfx950 wide-read half count); '
                         'WRITE_SIZE KiB x1024',
