@@ -107,8 +107,8 @@ int lt_num_forward(const lt_problem* pb, int32_t semiring, const void* W,
  *   [B,T,U+1] out (needed by lt_loss_backward; nullable otherwise).
  *   Checkpointing mode (beta_num and arcs non-NULL, and beta unless
  *   local_norm): the backward recursion -- which depends only on W -- runs
- *   concurrently with the forward (an internal per-thread auxiliary stream,
- *   joined back into `stream` before return), writing
+ *   here too (for the bigram in the same launch as the forward; otherwise
+ *   launched before it on `stream`: the library forks no stream), writing
  *     beta     [B,T,C]    beta_{t+1} of frame t (alignments.py:315-316)
  *     beta_num [B,T,U+1]  numerator beta_{t+1} of frame t
  *     arcs     [B,4(U+1)] int32 numerator arc table
@@ -145,11 +145,14 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
  * -- what RecognitionLattice.forward followed by loss.sum().backward() means
  * to produce (lattices.py:131-183 with the backward of alignments.py:300-318;
  * D1/D3 in the reference). Utterances with num = -inf get dW = 0.
- * For the bigram (FullNGram n = 1, V <= 32, U < 256) with 2B below the CU
- * count this is ONE launch: the alpha and beta recursions plus workgroups
- * that turn every frame into marginals as soon as both recursions have
- * passed it (each frame normalised by its own total, = log_z up to
- * rounding). Otherwise lt_loss_forward + lt_loss_backward run in turn.
+ * For the bigram (FullNGram n = 1, V <= 32, U <= 127) this is the chunked
+ * two-level scan below (three launches, plus the frame-serial pair whose
+ * workgroups exit at once unless an utterance is out of its range). Other
+ * bigram shapes with 2B below the CU count run ONE fused launch (alpha and
+ * beta recursions plus workgroups that turn every frame into marginals as
+ * soon as both recursions have passed it; should a hand-off wait time out,
+ * the affected loss is NaN, never a silent wrong value). Otherwise
+ * lt_loss_forward + lt_loss_backward run in turn.
  *   workspace: lt_loss_grad_workspace_bytes() bytes of device memory. */
 int lt_loss_grad_workspace_bytes(const lt_problem* pb, int32_t local_norm,
                                  size_t* bytes);
@@ -165,9 +168,10 @@ int lt_scale_grad(const lt_problem* pb, const float* grad, void* dW,
                   void* stream);
 
 /* The bigram loss as a chunked two-level scan (lt_chunk.hip): FullNGram
- * n = 1, 1 <= vocab_size <= 32, max_labels <= 124, Log semiring. Each
- * utterance is cut into chunks of L frames (L from the LDS budget, 14 for
- * V = 32 fp32); the serial chain is L + T/L steps instead of T.
+ * n = 1, 1 <= vocab_size <= 32, max_labels <= 127, Log semiring. Each
+ * utterance is cut into chunks of L frames (L from a 40 KB LDS budget per
+ * workgroup: 6 for V = 32, U = 100, fp32); the serial chains are L frames
+ * and T/L chunk steps (T/7 numerator group steps) instead of T.
  *   lt_chunk_forward  = RecognitionLattice.forward (lattices.py:131-183):
  *     loss [B] (log_z, num [B] nullable outputs); keeps the alpha / beta
  *     values at every chunk boundary in `state`.
@@ -176,10 +180,10 @@ int lt_scale_grad(const lt_problem* pb, const float* grad, void* dW,
  *     (grad nullable = ones), from `state` and W alone.
  * `state` must live from the forward to the backward; `scratch` only during
  * each call. Utterances with a frame whose weights are not all finite or
- * span more than 60 (max - min) run through the frame-serial kernels inside
+ * span more than 61 (max - min) run through the frame-serial kernels inside
  * the same calls (same results, slower). Sizes from
  * lt_chunk_workspace_bytes(); both buffers 16-byte aligned.
- * lt_loss_grad uses these two calls for every shape they take. */
+ * lt_loss_grad runs the same three launches for every shape they take. */
 int lt_chunk_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_t* state_bytes,
                              size_t* scratch_bytes);
 int lt_chunk_forward(const lt_problem* pb, int32_t local_norm, const void* W,

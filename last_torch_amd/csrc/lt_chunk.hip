@@ -138,12 +138,12 @@ LT_DEVINL float safe_max(float m) { return __builtin_isfinite(m) ? m : 0.f; }
 #ifdef LT_DIAG
 #define CK_STAMP(k)                                                                  \
   do {                                                                               \
-    if (a.stamps && !(a.dbg & 64) && threadIdx.x == 0)                               \
+    if (a.stamps && !LT_ABL(a, 64) && threadIdx.x == 0)                               \
       a.stamps[(long long)blockIdx.x * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 #define CK_WSTAMP(k)                                                                 \
   do {                                                                               \
-    if (a.stamps && (a.dbg & 64) && (threadIdx.x & 63) == 0)                         \
+    if (a.stamps && LT_ABL(a, 64) && (threadIdx.x & 63) == 0)                         \
       a.stamps[(long long)blockIdx.x * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
@@ -699,7 +699,7 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
   if (threadIdx.x == 0) a.uflag[b] = 0;
   CK_WSTAMP(2 * wave);
 
-  if (wave == 0 && !a.local && !(a.dbg & 1)) {
+  if (wave == 0 && !a.local && !LT_ABL(a, 1)) {
     // ---- den alpha across chunks (lattices.py:379-496 in chunk steps)
     float* bc = s_bc[0];  // bc[j] = a_{j+1} (core source j), bc[32] = a_0
     float al = lane == 0 ? 0.f : -kInf;  // lane p: alpha[p]
@@ -752,7 +752,7 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
     const float M = safe_max(wmax_u(x));
     const float s = wsum_u(lane < C ? lt_exp(x - M) : 0.f);
     if (lane == 0) s_lz = M + lt_log(s);
-  } else if (wave == 1 && !a.local && !(a.dbg & 1)) {
+  } else if (wave == 1 && !a.local && !LT_ABL(a, 1)) {
     // ---- den beta across chunks: beta_T = one for every state (lattices.py:788-790)
     float* bc = s_bc[1];
     const int h = lane >> 5;
@@ -798,9 +798,9 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
       }
       if (Kl & 1) step(rr[0], 0, false);
     }
-  } else if (wave == 2 && !(a.dbg & 2) && !(a.dbg & 128)) {
+  } else if (wave == 2 && !LT_ABL(a, 2) && !LT_ABL(a, 128)) {
     num_walk<PPL, true>(a, b, lane, nf, Kl, nl, s_nv[0], &s_num);
-  } else if (wave == 3 && !(a.dbg & 2)) {
+  } else if (wave == 3 && !LT_ABL(a, 2)) {
     num_walk<PPL, false>(a, b, lane, nf, Kl, nl, s_nv[1], nullptr);
   }
   CK_WSTAMP(2 * wave + 1);
@@ -944,7 +944,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   // every LDS load below is unconditional (clamped index, unused values
   // masked afterwards): a load under a branch would pay its full latency
 
-  if (wave == 0 && !a.local && !(a.dbg & 4)) {
+  if (wave == 0 && !a.local && !LT_ABL(a, 4)) {
     // ---- den alpha in scaled linear space. Lane p in [1, V]: alpha[p] =
     // al 2^S, renormalised every frame by a power of two so that state 1
     // sits in [1/2, 1) (readfirstlane + frexp: no reduction on the chain).
@@ -1005,7 +1005,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       al = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
     }
-  } else if (wave == 1 && !a.local && !(a.dbg & 4)) {
+  } else if (wave == 1 && !a.local && !LT_ABL(a, 4)) {
     // ---- den beta, the same scaled linear space; frame f gets beta_{f+1}.
     // Lane (j, h): core source j+1 over labels y in [16h+1, 16h+16], the
     // blank in h = 0; every lane also one term of the start state's sum
@@ -1059,7 +1059,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       be = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
     }
-  } else if (wave == 2 && !(a.dbg & 8)) {
+  } else if (wave == 2 && !LT_ABL(a, 8)) {
     // ---- num alpha (log2): al'[u] = al[u] + blank(u) (+) al[u-1] + arc(u)
     float al[PPL];
     const float* src = a.nabd + ((long long)b * (a.K + 1) + k) * NPG;
@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       for (int r = 0; r < PPL; ++r) al[r] = nv[r];
       __builtin_amdgcn_wave_barrier();
     }
-  } else if (wave == 3 && !(a.dbg & 8)) {
+  } else if (wave == 3 && !LT_ABL(a, 8)) {
     // ---- num beta (log2); frame f gets beta_{f+1}
     float be[PPL];
     const float* src = a.nbbd + ((long long)b * (a.K + 1) + k + 1) * NPG;
@@ -1134,7 +1134,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     bo[r] = boff[uc];
     lo[r] = max(loff[uc], 0);
   }
-  for (int f = (a.dbg & 16) ? nt : wave; f < nt; f += kMargWaves) {
+  for (int f = LT_ABL(a, 16) ? nt : wave; f < nt; f += kMargWaves) {
     float* fb = eptr(f);  // E_f, then the frame's dW in place
     // numerator terms (log2)
     float sb[PPL], sl[PPL];

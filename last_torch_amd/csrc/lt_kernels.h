@@ -40,6 +40,15 @@
 #include <stdio.h>
 #include <string.h>
 
+// Timing-ablation switches: live only in diagnostic builds (make diag,
+// -DLT_DIAG); in the product build every LT_ABL is the constant false and
+// the compiler drops the branch.
+#ifdef LT_DIAG
+#define LT_ABL(args, bits) ((((args).dbg) & (bits)) != 0)
+#else
+#define LT_ABL(args, bits) false
+#endif
+
 #include <algorithm>
 #include <string>
 
@@ -661,7 +670,7 @@ LT_DEVINL void loader_loop(const KArgs& a, int b, int nf, bool reverse, int lw, 
   [[maybe_unused]] const bool st = lw == 0 && lane == 0;
   for (int i = 0; i < nf; ++i) {
     LT_STAMP(a, st, 2, i, 0);
-    if (!(a.dbg & 4)) {
+    if (!LT_ABL(a, 4)) {
       // frame i + ahead must have landed by this barrier
       int later = (a.P - 1 < nf - 1 - i) ? a.P - 1 : nf - 1 - i;
       later -= ahead;
@@ -669,7 +678,7 @@ LT_DEVINL void loader_loop(const KArgs& a, int b, int nf, bool reverse, int lw, 
     }
     lds_barrier();
     LT_STAMP(a, st, 2, i, 1);
-    if (i + a.P < nf && !(a.dbg & 4)) {
+    if (i + a.P < nf && !LT_ABL(a, 4)) {
       const int s2 = slot + a.P >= a.S ? slot + a.P - a.S : slot + a.P;
       const int f = reverse ? nf - 1 - (i + a.P) : i + a.P;
       issue_frame(a, b, f, s2, lw, lane, ldsb);
@@ -872,11 +881,11 @@ __global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
   if (role == 2) {
     loader_loop(a, b, nf, false, lw, lane, ldsb);
   } else if (role == 0) {
-    if (do_den && !(a.dbg & 1))
+    if (do_den && !LT_ABL(a, 1))
       den_fwd_loop<MODE, BF16, WST, LG, P>(a, lds, abuf, b, nf, tid);
     else idle_loop(nf);
   } else {
-    if (do_num && !(a.dbg & 2))
+    if (do_num && !LT_ABL(a, 2))
       num_fwd_loop<MODE, BF16, WST>(a, lds, nbuf, ctx, ylab, b, nf, al, aux_lanes);
     else idle_loop(nf);
   }
@@ -1350,12 +1359,12 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
   if (role == 2) {
     loader_loop(a, b, nf, true, lw, lane, ldsb, DST && do_num ? 1 : 0);
   } else if (role == 0) {
-    if (!(a.dbg & 1) && (!CK || do_den))
+    if (!LT_ABL(a, 1) && (!CK || do_den))
       den_bwd_loop<BF16, WST, DST, LG, P, CK>(fresh_args(), lds, bbuf, nbuf3, b, nf, tid, gb,
                                               log_z, do_den, do_num);
     else idle_loop(nf);
   } else {
-    if (do_num && !(a.dbg & 2)) {
+    if (do_num && !LT_ABL(a, 2)) {
       if constexpr (CK)
         num_beta_loop<BF16, WST>(fresh_args(), lds, nbb, ctx, ylab, b, nf, al, aux_lanes);
       else

@@ -385,7 +385,7 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
 #pragma unroll
     for (int j = 4 * (J / 4); j < J; ++j) st = __builtin_fmaf(gv[j], ev[j], st);
     float S = ((acc0.x + acc0.y) + (acc1.x + acc1.y)) + st;
-    if (a.dbg & 64) S = gv[0] + ev[0];  // timing ablation
+    if (LT_ABL(a, 64)) S = gv[0] + ev[0];  // timing ablation
     S = act ? S : 0.f;
     if constexpr (LGH == 1) S = pair_sum_dpp(S);
     else S = group_sum_lg(S, lgH);
@@ -480,7 +480,7 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
       }
     }
     // ---- off-chain work of step i
-    if (hrow && !(a.dbg & 4)) {
+    if (hrow && !LT_ABL(a, 4)) {
       st_sc1(hrow, hval);
       hrow += hstep;
     }
@@ -493,7 +493,7 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
       // next normaliser: exponent of this frame's max S
       float mx = act ? S : 0.f;
       if constexpr (REV) mx = fmaxf(mx, S0);
-      if (a.dbg & 32)  // timing ablation: cheap normaliser
+      if (LT_ABL(a, 32))  // timing ablation: cheap normaliser
         esc = __builtin_amdgcn_frexp_expf(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(S))));
       else
         esc = __builtin_amdgcn_frexp_expf(wave_max_dpp(mx));
@@ -504,7 +504,7 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     }
     g = act ? gn : 0.f;
     g0 = g0n;
-    if (!(a.dbg & 32)) ff_add(base_hi, base_lo, shift);
+    if (!LT_ABL(a, 32)) ff_add(base_hi, base_lo, shift);
     // slot of step i consumed (its reads were used above)
     asm volatile("" ::: "memory");
     if (lane == 0) *(ctl + CTL_DEN) = i + 1;
@@ -595,14 +595,14 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
       wb[s] = Wr[ob[s]];
       wl[s] = Wr[ol[s]];
     }
-    if (hist && !(a.dbg & 8)) {
+    if (hist && !LT_ABL(a, 8)) {
       float* hr = hist + (row0 + t) * NP;
 #pragma unroll
       for (int s = 0; s < PN; ++s)
         if (PN * lane + s < NP) st_sc1(hr + PN * lane + s, v[s]);
     }
     float nv[PN];
-    if (a.dbg & 16) {  // timing ablation: no numerator arithmetic
+    if (LT_ABL(a, 16)) {  // timing ablation: no numerator arithmetic
 #pragma unroll
       for (int s = 0; s < PN; ++s) nv[s] = v[s] + wb[s] + wl[s];
     } else
@@ -751,8 +751,8 @@ LT_DEVINL void helper_pipe(const PArgs& a, unsigned char* lds, int b, int nf, in
     lds_float* Wr = (lds_float*)as3(sb);
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
-      if (!(a.dbg & 1)) Wr[lane + 64 * k] = w[k];
-      if (!(a.dbg & 2)) *(lds_float*)(as3(sb) + pe[k]) = lt_exp_off(w[k], cl);
+      if (!LT_ABL(a, 1)) Wr[lane + 64 * k] = w[k];
+      if (!LT_ABL(a, 2)) *(lds_float*)(as3(sb) + pe[k]) = lt_exp_off(w[k], cl);
     }
     if (lane == 0) {
       *(lds_float*)(as3(sb) + a.soff_c) = c;
@@ -922,7 +922,7 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
       }
       const unsigned rc = (unsigned)__builtin_amdgcn_readfirstlane((int)((ub + t) * C * 4));
       const unsigned rn = (unsigned)__builtin_amdgcn_readfirstlane((int)((ub + t) * NP * 4));
-      if (a.dbg & 1024) return;
+      if (LT_ABL(a, 1024)) return;
       if (do_den) {
         const unsigned ro = lane < C ? rc + lane * 4 : kOff;
         f.ra = __uint_as_float(
@@ -1005,7 +1005,7 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
         sn = wave_sum(sn);
         const float rn = (sn > 0.f && sn < kInf) ? __builtin_amdgcn_rcpf(sn) : 0.f;
         zero = (do_den && rd == 0.f) || rn == 0.f;
-        if (a.dbg & 256) zero = false;
+        if (LT_ABL(a, 256)) zero = false;
         if (!zero) {
           // string arcs sharing a lattice arc meet in LDS float adds; one
           // wave's adds apply in program and lane order (deterministic)
@@ -1032,7 +1032,7 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
       for (int k = 0; k < NL; ++k) {
         int vo = (int)(vb + (unsigned)(64 * k * es));
         if (partial(k) && lane + 64 * k >= FR) vo = (int)kOff;
-        if (a.dbg & 4096) vo = (int)kOff;
+        if (LT_ABL(a, 4096)) vo = (int)kOff;
         if constexpr (BF16)
           __builtin_amdgcn_raw_buffer_store_b16(f2bf(x[k]), dr, vo, 0, 0);
         else
@@ -1107,7 +1107,7 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers), 4) void pipe_kernel(con
   const bool rev = a.dirs == 2 && blk >= a.B;
   const int b = rev ? blk - a.B : blk;
   const int tid = threadIdx.x, lane = tid & 63;
-  if (a.fused && (a.dbg & 128)) {  // timing ablation: marginal roles alone
+  if (a.fused && LT_ABL(a, 128)) {  // timing ablation: marginal roles alone
     if (threadIdx.x < 2) st_sc1(a.prog + ((rev ? 2 : 0) + threadIdx.x) * a.B + b, a.T);
     return;
   }
@@ -1176,7 +1176,7 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers), 4) void pipe_kernel(con
   } else if (wave - 2 < a.NH) {
     constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
     // above the marginal roles (priority 0) that share the CU in fused mode
-    if (a.fused && !(a.dbg & 8192)) __builtin_amdgcn_s_setprio(1);
+    if (a.fused && !LT_ABL(a, 8192)) __builtin_amdgcn_s_setprio(1);
     if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, wave - 2, lane);
     else helper_pipe<BF16, NL, false>(a, lds, b, nf, wave - 2, lane);
   }

@@ -6,9 +6,10 @@
  * load this library, and only as the checker / the timed CPU baseline. The
  * product path (last_torch_amd) never calls it.
  *
- * Pinned against the reference itself: the fixtures tests/golden/golden_*.npz are made by
- * tests/golden/make_golden.py importing /root/reference/last_torch, and
- * tests/test_oracle.py checks every function here against them.
+ * Pinned against the reference itself: the fixtures tests/golden/lattice_*.npz
+ * (and contexts.npz, semirings.npz) are made by tests/golden/make_golden.py
+ * importing /root/reference/last_torch, and tests/test_oracle_golden.py checks
+ * every function here against them.
  *
  * Restated, not re-derived: the per-frame steps follow the reference's own
  * tensor formulation, cited per function:
