@@ -3,8 +3,8 @@
 One step = one pass of the hot path over one batch of synthetic arc weights
 already resident in HBM: lt_loss_grad, i.e. the loss and dW = d(sum
 loss)/dW (what loss.sum().backward() needs). For the bigram it is the
-chunked two-level scan (lt_chunk.hip: ck_transfer_kernel -> ck_combine_kernel
--> ck_marg_kernel, plus the frame-serial pair whose workgroups exit at once
+chunked two-level scan (lt_chunk.hip: ck_ab_kernel -- the chunk transfers
+with the boundary walks in the same launch -- then ck_marg_kernel, plus the frame-serial pair whose workgroups exit at once
 unless an utterance is out of the fast path's range). For N > 1 the step
 adds the single RCCL all-reduce of the summed loss.
 --design checkpoints / recursion time the older two-call designs
@@ -240,16 +240,16 @@ def read_traffic(profile_json, kernels, B, T):
 
 def chunk_design_bytes(T, U, V, L, es=4):
   """Per-frame HBM bytes the chunked design moves:
-  W read by ck_transfer_kernel and again by ck_marg_kernel, dW written once;
-  per chunk of L frames a 1224-float record and the numerator group bands
+  W read by ck_ab_kernel and again by ck_marg_kernel, dW written once;
+  per chunk of L frames a 1248-float record and the numerator group bands
   (NPG x 8 floats per 7-frame group) written by A and read by B; the
   boundary vectors written by B and read by C; the frame offsets c_t."""
   Aw = (V + 1) * (V + 1)
   NPG = (U + 2) & ~1
   CP = (V + 4) & ~3
   groups = -(-L // 7)
-  rec = 1224 * 4 * 2 / L
-  bands = groups * 8 * NPG * 4 * 2 / L
+  rec = 1248 * 4 * 2 / L
+  bands = ((groups * 8 * NPG + 31) & ~31) * 4 * 2 / L
   bound = 2 * (CP + NPG) * 4 * 2 / L
   return Aw * es * 3 + rec + bands + bound + 4 * 2
 
@@ -325,9 +325,10 @@ def main():
     call_s = float(np.mean(fwd_ms)) * 1e-3
     if chunk:
       L = chunk_len(B, T, U, V)
-      knames = ['ck_transfer_kernel', 'ck_combine_kernel', 'ck_marg_kernel']
+      fuse_ab = B <= torch.cuda.get_device_properties(device).multi_processor_count
+      knames = ['ck_ab_kernel'] + ([] if fuse_ab else ['ck_combine_kernel']) + ['ck_marg_kernel']
       design = (f'chunked two-level scan, L={L} frames per chunk (lt_chunk.hip: '
-                f'ck_transfer_kernel -> ck_combine_kernel -> ck_marg_kernel)')
+                f"{' -> '.join(knames)})")
       design_b = chunk_design_bytes(T, U, V, L)
     else:
       knames = ['pipe_kernel'] if _native.fused_path(B, T, U, V, n, device) else ['lt_loss_grad']

@@ -17,19 +17,22 @@
 // block matrix  M_t = [[w00, w0.], [0, Mc_t]]  in the log semiring, with
 // Mc_t[p][q] = W[p][q] (+) (p == q ? W[p][0] : zero).
 //
-// Three launches (one call of lt_loss_grad):
-//   A  ck_transfer_kernel  one wave per chunk: the chunk's transfer matrix
+// Two launches (one call of lt_loss_grad):
+//   A  one wave per chunk: the chunk's transfer matrix
 //      P_k = M_{t0} ... M_{t1-1} in scaled linear space. The 32 x 32 core
 //      product runs on the matrix cores (v_mfma_f32_32x32x2_f32: exact f32
 //      FMA chains) as X <- E_t^T X with X = P^T, one column scale per start
 //      state; the state-0 row and the state-0 self loop on the side. Also
-//      gathers the numerator's two arc weights per string position and
-//      frame into G (the string lattice reads nothing else of W).
-//   B  ck_combine_kernel   one workgroup per utterance: the den alpha / beta
-//      vectors at every chunk boundary (K steps of a 33 x 33 log-semiring
-//      vector-matrix product each), the numerator alpha / beta over all
-//      frames from G (log space, exact per position) with the values at the
-//      chunk boundaries kept; log_z, num, loss.
+//      the numerator's group bands (the string lattice's frame steps
+//      composed over kGrp frames) and the frame offsets.
+//   B  one workgroup per utterance: the den alpha / beta vectors at every
+//      chunk boundary (K steps of a 33 x 33 log-semiring vector-matrix
+//      product each), the numerator alpha / beta over the groups with the
+//      values at the chunk boundaries kept; log_z, num, loss.
+//      A and B share ck_ab_kernel: the walks follow A's chunks through
+//      per-chunk ready flags (write-through stores, agent-scope acquire), so
+//      they run beside the transfers instead of after them (B > CUs or
+//      LT_CHUNK_FUSE=0: ck_combine_kernel after the launch).
 //   C  ck_marg_kernel      one workgroup per chunk: the chunk's W staged in
 //      LDS once; local den / num alpha and beta recursions from the
 //      boundary values (four waves side by side), then the arc marginals of
@@ -55,11 +58,12 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr float kRange = 60.f;  // max - min of a frame's weights on the fast path
 constexpr float kEmin = 0x1p-88f;  // < e^-(kRange + 1): the exponential form of the range test
 constexpr float kLn2 = 0.6931471805599453f;
-constexpr int kRec = 1224;      // floats per chunk record (16-byte multiple)
+constexpr int kRec = 1248;      // floats per chunk record (whole 128-byte lines)
 constexpr int kRowT = 36;       // row stride of the transposed core in a record
 constexpr int kChunkLds = 40 * 1024;  // phase C LDS per workgroup (four per CU)
 constexpr int kMargWaves = 4;   // phase C: waves per workgroup (recursions on 0-3)
 constexpr int kGrp = 7;         // frames per numerator group (band offsets 0..kGrp)
+constexpr unsigned kSpinMax = 1u << 20;  // phase B's bound on polls without progress (~1 s)
 // record layout (floats): [0, 1152) X^T rows: rec[i * 36 + j] = X[i][j] =
 // P_scaled[j][i] (start core state j -> end core state i); [1152, 1184)
 // per-start-state (column) power-of-two scales ej (int); [1184, 1216) the
@@ -83,6 +87,7 @@ struct CkArgs {
   float* nabd;             // [B,K+1,NPG] num alpha at chunk starts
   float* nbbd;             // [B,K+1,NPG] num beta at chunk starts
   float* cf;               // [B,T] frame offsets c_t = ceil(max W_t) (phase A's)
+  unsigned* ready;         // [B,K] chunk k's record and bands published (scratch, zeroed per call)
   float* loss;
   float* log_z;            // state copies (read by C)
   float* num;
@@ -92,6 +97,8 @@ struct CkArgs {
   int B, T, U, V, C, R, FR, NP, NPG, PPL, CP;
   int L, K;                // frames per chunk, chunks per utterance
   int NGc;                 // numerator groups per chunk, ceil(L / kGrp)
+  int nc, wpos;            // ck_ab_kernel: nc walking workgroups (B fused, 0 not) from block wpos
+  int nbs;                 // floats per chunk of numerator bands (whole 128-byte lines)
   int local;               // LocallyNormalizedWeightFn: no denominator
   int dbg;                 // diagnostic builds (LT_DIAG) only: role ablations
   long long* stamps;       // diagnostic builds only: per-workgroup s_memtime marks
@@ -313,16 +320,40 @@ LT_DEVINL void mask_frame(int V, int lane, const int* boff, const int* loff,
   }
 }
 
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// Write-through (sc1) stores for what phase B reads in the same launch: the
+// bytes leave the XCD's L2 with the store, so the publishing wave needs only
+// its own s_waitcnt vmcnt(0) before the flag -- no L2 write-back fence
+// (MI355X_MICROARCH.md: a per-wave release fence costs the whole L2's dirty
+// lines). A buffer resource per chunk region (bounds-checked).
+LT_DEVINL __amdgpu_buffer_rsrc_t wt_rsrc(void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, 0x00020000);
+}
+LT_DEVINL void st_wt(__amdgpu_buffer_rsrc_t r, int idx, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, 4 * idx, 0, 0x10);
+}
+LT_DEVINL void st_wt(__amdgpu_buffer_rsrc_t r, int idx, int v) {
+  __builtin_amdgcn_raw_buffer_store_b32((unsigned)v, r, 4 * idx, 0, 0x10);
+}
+LT_DEVINL void st_wt4(__amdgpu_buffer_rsrc_t r, int idx, float x, float y, float z, float w) {
+  const v4u v = {__float_as_uint(x), __float_as_uint(y), __float_as_uint(z), __float_as_uint(w)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, 4 * idx, 0, 0x10);
+}
+
+// Chunk k of utterance b: the transfer record, the numerator bands and the
+// frame offsets, then the hand-off to phase B: record and bands stored
+// write-through (sc1), the wave's s_waitcnt vmcnt(0), then one relaxed
+// agent-scope flag store (1, or 2 for a chunk outside the range); phase B
+// polls it and acquires (ChunkReady).
 template <bool BF16, int PPL, bool FULL>
-__global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
+LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   __shared__ __attribute__((aligned(16))) float s_rt[4][32];
   __shared__ int s_lab[4][128];
   __shared__ __attribute__((aligned(16))) float2 s_g[4][128 + kGrp + 1];
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int id = blockIdx.x * 4 + wave;
-  if (id >= a.B * a.K) return;  // no workgroup barrier in this kernel
-  const int b = id / a.K, k = id - (id / a.K) * a.K;
+  const int id = b * a.K + k;
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const int t0 = k * a.L;
@@ -367,6 +398,7 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
   // position s = lane + 64 r at the group's first frame to s + d after its
   // last (the string lattice's frame steps, lattices.py:340-377, composed)
   float nbd[PPL][kGrp + 1];
+  const __amdgpu_buffer_rsrc_t nbr = wt_rsrc(a.nb + (long long)id * a.nbs, 4 * a.nbs);
 
   // frames in registers two ahead; the loads are unconditional (clamped to
   // the chunk's last frame) so the compiler's vmcnt tracking stays exact
@@ -399,14 +431,14 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
         nbd[r][0] += gv[0].x;
       }
       if (fl == kGrp - 1 || f == nt - 1) {  // source-major: 32 bytes per position
-        float4* dst = (float4*)(a.nb + (((long long)b * a.K + k) * a.NGc + j) * (kGrp + 1) * NPG);
         static_assert(kGrp + 1 == 8, "two float4 per position");
+        const int g0 = j * (kGrp + 1) * NPG;
 #pragma unroll
         for (int r = 0; r < PPL; ++r)
           if (lane + 64 * r < NPG) {
             const int u = lane + 64 * r;
-            dst[2 * u] = make_float4(nbd[r][0], nbd[r][1], nbd[r][2], nbd[r][3]);
-            dst[2 * u + 1] = make_float4(nbd[r][4], nbd[r][5], nbd[r][6], nbd[r][7]);
+            st_wt4(nbr, g0 + 8 * u, nbd[r][0], nbd[r][1], nbd[r][2], nbd[r][3]);
+            st_wt4(nbr, g0 + 8 * u + 4, nbd[r][4], nbd[r][5], nbd[r][6], nbd[r][7]);
           }
       }
       __builtin_amdgcn_wave_barrier();
@@ -493,22 +525,88 @@ __global__ __launch_bounds__(256, 2) void ck_transfer_kernel(const CkArgs a) {
   }
   if (nt & 1) step(fr[0], nt - 1, false);
 
-  float* rec = a.rec + (long long)id * kRec;
+  const __amdgpu_buffer_rsrc_t rr = wt_rsrc(a.rec + (long long)id * kRec, 4 * kRec);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) rec[kstep(r, h) * kRowT + i] = X[r];
+  for (int r = 0; r < 16; ++r) st_wt(rr, kstep(r, h) * kRowT + i, X[r]);
   if (lane < 32) {
-    ((int*)rec)[kRecEj + lane] = ej;
-    rec[kRecRt + lane] = rt[lane];
+    st_wt(rr, kRecEj + lane, ej);
+    st_wt(rr, kRecRt + lane, rt[lane]);
   }
   bad = __builtin_amdgcn_readfirstlane(bad);
   if (lane == 0) {
-    ((int*)rec)[kRecRho] = rho;
-    rec[kRecPi] = pi;
-    rec[kRecCs] = csum;
-    ((int*)rec)[kRecFlag] = bad;
-    ((int*)rec)[kRecN] = nt;
+    st_wt(rr, kRecRho, rho);
+    st_wt(rr, kRecPi, pi);
+    st_wt(rr, kRecCs, csum);
+    st_wt(rr, kRecFlag, bad);
+    st_wt(rr, kRecN, nt);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0)
+    __hip_atomic_store((gu32*)(a.ready + id), bad ? 2u : 1u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// Phase B's side of the hand-off, one wave: chunks [0, hi] (forward walks)
+// or [lo, Kl) (backward walks) are known published. ensure() polls 64 flags
+// per pass with relaxed agent-scope loads (s_sleep between passes), and one
+// agent-scope acquire follows every pass that extends the range, so the
+// wave's own plain loads of the newly published records see them (no other
+// wave reads through this acquire). A flag of 2 marks a chunk outside the
+// fast path's range (bad). A bounded spin: on timeout (a placement that never
+// schedules the producer) ok = 0, the range is taken as covered, and the
+// utterance goes to the frame-serial kernels.
+struct ChunkReady {
+  const unsigned* f;
+  int lo, hi, Kl, ok, bad;
+  LT_DEVINL ChunkReady(const unsigned* flags, int kl) : f(flags), lo(kl), hi(-1), Kl(kl), ok(1), bad(0) {}
+  LT_DEVINL void take(unsigned v, int lane, int* c) {
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(v != 0);
+    *c = m == ~0ull ? 64 : __builtin_ctzll(~m);
+    const unsigned long long live = *c == 64 ? ~0ull : ((1ull << *c) - 1);
+    if (__builtin_amdgcn_ballot_w64(v == 2u) & live) bad = 1;
+  }
+  LT_DEVINL void timeout() {
+    ok = 0;
+    hi = Kl - 1;
+    lo = 0;
+  }
+  LT_DEVINL void ensure_fwd(int k, int lane) {
+    k = min(k, Kl - 1);
+    for (unsigned spins = 0; k > hi; ++spins) {
+      const int x = hi + 1 + lane;
+      const unsigned v = x < Kl ? __hip_atomic_load((const gu32*)(f + x), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      int c;
+      take(v, lane, &c);
+      if (c) {
+        hi += c;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      } else if (spins > kSpinMax) {
+        timeout();
+      } else {
+        __builtin_amdgcn_s_sleep(4);
+      }
+    }
+  }
+  LT_DEVINL void ensure_bwd(int k, int lane) {
+    k = max(k, 0);
+    for (unsigned spins = 0; k < lo; ++spins) {
+      const int x = lo - 1 - lane;
+      const unsigned v = x >= 0 ? __hip_atomic_load((const gu32*)(f + x), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      int c;
+      take(v, lane, &c);
+      if (c) {
+        lo -= c;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      } else if (spins > kSpinMax) {
+        timeout();
+      } else {
+        __builtin_amdgcn_s_sleep(4);
+      }
+    }
+  }
+};
 
 // ---------------------------------------------------------------------------
 // B: chunk boundaries (one workgroup per utterance, 4 waves). Records and
@@ -556,7 +654,7 @@ LT_DEVINL void load_rec_beta(const float* rc, int lane, RecBeta& r) {
 // Boundary values at every chunk start -> nabd / nbbd (natural log).
 template <int PPL, bool FWD>
 LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl, float* lds,
-                        float* s_num) {
+                        float* s_num, ChunkReady& rd) {
   const int NPG = a.NPG;
   // ---- numerator over the groups of kGrp frames (phase A's bands), base-2
   // log space. alpha (wave 2, lattices.py:340-377 composed per group):
@@ -569,7 +667,7 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
   const int NGc = a.NGc;
   const int ntl = nf - (Kl - 1) * a.L;  // live frames of the last chunk
   const int Q = Kl > 0 ? (Kl - 1) * NGc + (ntl + kGrp - 1) / kGrp : 0;
-  const float* nb0 = a.nb + (long long)b * a.K * NGc * NB * NPG;
+  const float* nb0 = a.nb + (long long)b * a.K * a.nbs;
   // alpha: tab[u][d] = al[u - d] + N[u - d][d] (rows u < d stay -inf);
   // beta: sv[s] = be[s] with sv[64 PPL, +NB) = -inf
   float* tab = lds;
@@ -591,7 +689,11 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
   // band rows N[s][0 .. kGrp] of group q for the lane's source positions
   float4 gq[D][PPL][2];
   auto bload = [&](int q, float4 (*g)[2]) {
-    const float4* row = (const float4*)(nb0 + (long long)min(max(q, 0), max(Q - 1, 0)) * NB * NPG);
+    const int qc = min(max(q, 0), max(Q - 1, 0));
+    if constexpr (FWD) rd.ensure_fwd(qc / NGc, lane);
+    else rd.ensure_bwd(qc / NGc, lane);
+    const int kc = qc / NGc;
+    const float4* row = (const float4*)(nb0 + (long long)kc * a.nbs + (qc - kc * NGc) * NB * NPG);
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       const int uc = min(lane + 64 * r, NPG - 1);
@@ -669,15 +771,15 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
   }
 }
 
+// Utterance b's walks, one per wave, each following phase A's progress
+// through the ready flags (ChunkReady) when A runs in the same launch.
 template <int PPL>
-__global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
+LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
   __shared__ __attribute__((aligned(16))) float s_bc[2][64];
   __shared__ int s_bad;
   __shared__ float s_lz, s_num;
   __shared__ float s_nv[2][(128 + kGrp + 1) * (kGrp + 2)];
-  const int b = blockIdx.x;
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const int Kl = (nf + a.L - 1) / a.L;  // live chunks
@@ -685,19 +787,10 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
   const int nl = a.nlab[b];
   const float* rec0 = a.rec + (long long)b * a.K * kRec;
 
-  // any chunk out of the fast path's range (a weight not finite, or a frame
-  // spanning more than kRange): the frame-serial kernels take the utterance
   if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
-  for (int k = threadIdx.x; k < Kl; k += blockDim.x)
-    if (((const int*)(rec0 + (long long)k * kRec))[kRecFlag]) s_bad = 1;
-  __syncthreads();
-  if (s_bad) {
-    if (threadIdx.x == 0) a.uflag[b] = 1;
-    return;
-  }
-  if (threadIdx.x == 0) a.uflag[b] = 0;
   CK_WSTAMP(2 * wave);
+  ChunkReady rd(a.ready + (long long)b * a.K, Kl);
 
   if (wave == 0 && !a.local && !LT_ABL(a, 1)) {
     // ---- den alpha across chunks (lattices.py:379-496 in chunk steps)
@@ -735,10 +828,14 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
       const float sh = from_prev(nq, -kInf);
       al = lane == 0 ? n0 : (lane < C ? sh : -kInf);
       if (lane < C) dst[(long long)(k + 1) * CP + lane] = al;
-      if (reload) load_rec_alpha(rec_ptr(k + 2), lane, V, R);
+      if (reload) {
+        rd.ensure_fwd(k + 2, lane);
+        load_rec_alpha(rec_ptr(k + 2), lane, V, R);
+      }
       __builtin_amdgcn_wave_barrier();
     };
     if (Kl > 0) {
+      rd.ensure_fwd(1, lane);
       load_rec_alpha(rec_ptr(0), lane, V, rr[0]);
       load_rec_alpha(rec_ptr(1), lane, V, rr[1]);
       for (int k0 = 0; k0 < (Kl & ~1); k0 += 2) {
@@ -786,10 +883,14 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
       const float sh = from_prev(nj, -kInf);
       be = lane == 0 ? nb0 : (lane < C ? sh : -kInf);
       if (lane < C) dst[(long long)k * CP + lane] = be;
-      if (reload) load_rec_beta(rec_ptr(k - 2), lane, R);
+      if (reload) {
+        rd.ensure_bwd(k - 2, lane);
+        load_rec_beta(rec_ptr(k - 2), lane, R);
+      }
       __builtin_amdgcn_wave_barrier();
     };
     if (Kl > 0) {
+      rd.ensure_bwd(Kl - 2, lane);
       load_rec_beta(rec_ptr(Kl - 1), lane, rr[0]);
       load_rec_beta(rec_ptr(Kl - 2), lane, rr[1]);
       for (int n0 = 0; n0 < (Kl & ~1); n0 += 2) {
@@ -799,13 +900,22 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
       if (Kl & 1) step(rr[0], 0, false);
     }
   } else if (wave == 2 && !LT_ABL(a, 2) && !LT_ABL(a, 128)) {
-    num_walk<PPL, true>(a, b, lane, nf, Kl, nl, s_nv[0], &s_num);
+    num_walk<PPL, true>(a, b, lane, nf, Kl, nl, s_nv[0], &s_num, rd);
   } else if (wave == 3 && !LT_ABL(a, 2)) {
-    num_walk<PPL, false>(a, b, lane, nf, Kl, nl, s_nv[1], nullptr);
+    num_walk<PPL, false>(a, b, lane, nf, Kl, nl, s_nv[1], nullptr, rd);
   }
+  // any chunk out of the fast path's range (a weight not finite, or a frame
+  // spanning more than kRange; every walk has seen every chunk's flag) or a
+  // hand-off timeout: the frame-serial kernels take the utterance
+  if (lane == 0 && (rd.bad || !rd.ok)) s_bad = 1;
   CK_WSTAMP(2 * wave + 1);
   __syncthreads();
+  if (s_bad) {
+    if (threadIdx.x == 0) a.uflag[b] = 1;
+    return;
+  }
   if (threadIdx.x == 0) {
+    a.uflag[b] = 0;
     const float lz = a.local ? 0.f : s_lz;
     const float nm = s_num;
     a.log_z[b] = lz;
@@ -814,6 +924,43 @@ __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
     if (a.num_out) a.num_out[b] = nm;
     a.loss[b] = a.local ? -nm : lz - nm;  // lattices.py:178-183
   }
+}
+
+// A and B in one launch: the nc = B workgroups at block indices [wpos, wpos
+// + nc) walk one utterance each (nc = 0: ck_combine_kernel walks after the
+// launch); every other wave computes one chunk, ordered outside-in -- level
+// m holds chunks m and Kl-1-m of every utterance -- so the forward walks
+// (chunk 0 up) and the backward walks (Kl-1 down) both find their next
+// chunks among the first published. The walks start part-way through the
+// chunks (wpos, host-chosen), so that they hold their wave slots only for
+// the stretch they can follow A's front. Dispatch order is not assumed for
+// correctness: a walk that never sees its chunk times out to the
+// frame-serial kernels.
+template <bool BF16, int PPL, bool FULL>
+__global__ __launch_bounds__(256, 2) void ck_ab_kernel(const CkArgs a) {
+  const int nc = a.nc;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int x = blockIdx.x;
+  if (x >= a.wpos && x < a.wpos + nc) {
+    combine_role<PPL>(a, x - a.wpos, wave);
+    return;
+  }
+  if (x >= a.wpos) x -= nc;
+  const long long j = (long long)x * 4 + wave;
+  const int m = (int)(j / (2 * a.B));
+  const int r = (int)(j - (long long)m * 2 * a.B);
+  const int b = r < a.B ? r : r - a.B;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int Kl = (nf + a.L - 1) / a.L;
+  const int k = r < a.B ? m : Kl - 1 - m;
+  if (r < a.B ? m > Kl - 1 - m : Kl - 1 - m <= m) return;  // past the middle (or no chunk)
+  transfer_role<BF16, PPL, FULL>(a, b, k, wave);
+}
+
+template <int PPL>
+__global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
+  combine_role<PPL>(a, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
 
 // Phase C's gather tables: per position, in LDS (labels staged by the whole
@@ -1273,7 +1420,7 @@ struct CkLayout {
   // state (kept from lt_chunk_forward to lt_chunk_backward)
   size_t uflag, lz, num, abd, bbd, nabd, nbbd, cf, state;
   // scratch: forward = records + numerator bands; backward = the fallback's checkpoints
-  size_t rec, nb, f_alpha, f_an, f_loss, f_lz, f_num, f_side, scratch;
+  size_t ready, rec, nb, f_alpha, f_an, f_loss, f_lz, f_num, f_side, scratch;
 };
 
 int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
@@ -1350,8 +1497,10 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   w->cf = o; o += up256(4 * B * T);
   w->state = o;
   size_t s = 0;
+  w->ready = s; s += up256(4LL * B * K);
   w->rec = s; s += up256(4LL * B * K * kRec);
-  w->nb = s; s += up256(4LL * B * K * a->NGc * (kGrp + 1) * a->NPG);
+  a->nbs = (a->NGc * (kGrp + 1) * a->NPG + 31) & ~31;
+  w->nb = s; s += up256(4LL * B * K * a->nbs);
   const size_t fwd = s;
   s = 0;
   w->f_alpha = s; s += up256(4LL * B * T * a->C);
@@ -1377,6 +1526,7 @@ void ck_bind(CkArgs* a, const CkLayout& w, void* state, void* scratch) {
   a->cf = (float*)(st + w.cf);
   a->rec = sc ? (float*)(sc + w.rec) : nullptr;
   a->nb = sc ? (float*)(sc + w.nb) : nullptr;
+  a->ready = sc ? (unsigned*)(sc + w.ready) : nullptr;
 }
 
 int ck_launch(const void* k, int grid, int lds, hipStream_t st, const CkArgs& a,
@@ -1403,19 +1553,50 @@ int ck_check(const lt_problem* pb) {
   return LT_OK;
 }
 
-const void* ck_kernel_a(int ppl, bool bf16, bool full) {
+const void* ck_kernel_ab(int ppl, bool bf16, bool full) {
   if (full)
-    return ppl == 1 ? (bf16 ? (const void*)ck_transfer_kernel<true, 1, true>
-                            : (const void*)ck_transfer_kernel<false, 1, true>)
-                    : (bf16 ? (const void*)ck_transfer_kernel<true, 2, true>
-                            : (const void*)ck_transfer_kernel<false, 2, true>);
-  return ppl == 1 ? (bf16 ? (const void*)ck_transfer_kernel<true, 1, false>
-                          : (const void*)ck_transfer_kernel<false, 1, false>)
-                  : (bf16 ? (const void*)ck_transfer_kernel<true, 2, false>
-                          : (const void*)ck_transfer_kernel<false, 2, false>);
+    return ppl == 1 ? (bf16 ? (const void*)ck_ab_kernel<true, 1, true>
+                            : (const void*)ck_ab_kernel<false, 1, true>)
+                    : (bf16 ? (const void*)ck_ab_kernel<true, 2, true>
+                            : (const void*)ck_ab_kernel<false, 2, true>);
+  return ppl == 1 ? (bf16 ? (const void*)ck_ab_kernel<true, 1, false>
+                          : (const void*)ck_ab_kernel<false, 1, false>)
+                  : (bf16 ? (const void*)ck_ab_kernel<true, 2, false>
+                          : (const void*)ck_ab_kernel<false, 2, false>);
 }
 const void* ck_kernel_b(int ppl) {
   return ppl == 1 ? (const void*)ck_combine_kernel<1> : (const void*)ck_combine_kernel<2>;
+}
+int ck_cus() {
+  static int cus[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) !=
+                       hipSuccess)
+    cus[dev] = 0;
+  return cus[dev];
+}
+// Phases A and B: the ready flags zeroed (a memset node under capture), then
+// ONE launch with the walks among its workgroups, or A and B as two launches
+// when the walks (one workgroup per utterance, at most one of the two
+// workgroup slots per CU the launch's registers allow) could hold half the
+// chip's slots while they wait (B > CUs), or LT_CHUNK_FUSE=0. The walks'
+// block position: a walk needs about K x 0.7 us and follows A's front at
+// half its own pace, so it starts when the chunks left take half its time:
+// the fraction 1 - 30 / B of A's workgroups (chunk waves take ~25 us per
+// round of 2048; LT_CHUNK_WALK_AT overrides, in percent).
+int ck_launch_ab(CkArgs& a, bool bf16, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(a.ready, 0, 4LL * a.B * a.K, st);
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  const bool fuse = a.B <= ck_cus() && ck_env("LT_CHUNK_FUSE", 1) != 0;
+  a.nc = fuse ? a.B : 0;
+  const long long items = 2LL * a.B * ((a.K + 1) / 2);
+  const long long nwa = (items + 3) / 4;
+  const int at = ck_env("LT_CHUNK_WALK_AT", std::max(0, 100 - 3000 / std::max(a.B, 1)));
+  a.wpos = (int)(nwa * std::min(std::max(at, 0), 100) / 100);
+  int rc = ck_launch(ck_kernel_ab(a.PPL, bf16, a.V == 32), (int)(a.nc + nwa), 0, st, a);
+  if (rc || fuse) return rc;
+  return ck_launch(ck_kernel_b(a.PPL), a.B, 0, st, a);
 }
 const void* ck_kernel_c(int ppl, bool bf16, bool full) {
   if (full)
@@ -1477,9 +1658,7 @@ int chunk_loss_grad(const lt_problem* pb, int local_norm, const void* W, const i
   a.dW = dW;
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
-  if ((rc = ck_launch(ck_kernel_a(a.PPL, bf16, a.V == 32), (int)(((long long)a.B * a.K + 3) / 4), 0, st, a)))
-    return rc;
-  if ((rc = ck_launch(ck_kernel_b(a.PPL), a.B, 0, st, a))) return rc;
+  if ((rc = ck_launch_ab(a, bf16, st))) return rc;
   if ((rc = ck_launch(ck_kernel_c(a.PPL, bf16, a.V == 32), a.B * a.K, ck_lds_c(a, bf16), st, a,
                       64 * kMargWaves)))
     return rc;
@@ -1529,9 +1708,7 @@ int lt_chunk_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   a.num_out = num;
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
-  if ((rc = ck_launch(ck_kernel_a(a.PPL, bf16, a.V == 32), (int)(((long long)a.B * a.K + 3) / 4), 0, st, a)))
-    return rc;
-  if ((rc = ck_launch(ck_kernel_b(a.PPL), a.B, 0, st, a))) return rc;
+  if ((rc = ck_launch_ab(a, bf16, st))) return rc;
   // utterances outside the fast path's range: the frame-serial kernels
   // (their workgroups return at once for every other utterance)
   return lt_impl::serial_loss(pb, local_norm, W, num_frames, labels, num_labels, a.uflag, loss,

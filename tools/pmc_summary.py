@@ -14,7 +14,7 @@ Corrections (MI355X_MICROARCH.md "HBM [CDNA4]"):
     kernels are 16 B/lane LDS-DMA reads, so FETCH_SIZE is doubled.
   * WRITE_SIZE (KiB) is exact for 16 B/lane streaming stores and dword
     float stores; it is taken as is.
-  * The chunked path's transfer kernel (ck_transfer_kernel) reads W with
+  * The chunked path's transfer kernel (ck_ab_kernel, with the walks) reads W with
     dword loads, a width the guide leaves uncalibrated; it reads every frame
     exactly once (B*T*FR*4 bytes), so its doubled FETCH_SIZE against that
     count is the calibration, printed as ``fetch_vs_w``.
@@ -42,7 +42,7 @@ def _kernel_key(name):
   if 'bwd_kernel' in name:
     args = name.split('bwd_kernel<', 1)[-1].split('>', 1)[0].split(',')
     return 'bwd_kernel_ck' if len(args) >= 6 and args[5].strip() == 'true' else 'bwd_kernel'
-  for k in ('ck_transfer_kernel', 'ck_combine_kernel', 'ck_marg_kernel',
+  for k in ('ck_ab_kernel', 'ck_combine_kernel', 'ck_marg_kernel',
             'fwd_kernel', 'marg_kernel', 'backtrace_kernel', 'num_scatter_kernel', 'pipe_kernel',
             'joint_weights_fb_kernel', 'joint_weights_kernel', 'joint_backward_kernel',
             'joint_exp_kernel', 'joint_reduce_kernel'):
