@@ -63,6 +63,10 @@ constexpr int kRowT = 36;       // row stride of the transposed core in a record
 constexpr int kChunkLds = 40 * 1024;  // phase C LDS per workgroup (four per CU)
 constexpr int kMargWaves = 4;   // phase C: waves per workgroup (recursions on 0-3)
 constexpr int kGrp = 7;         // frames per numerator group (band offsets 0..kGrp)
+#ifndef LT_AB_WAVES
+#define LT_AB_WAVES 3
+#endif
+constexpr int kAbWaves = LT_AB_WAVES;  // ck_ab_kernel: waves per SIMD its registers allow
 constexpr unsigned kSpinMax = 1u << 20;  // phase B's bound on polls without progress (~1 s)
 // record layout (floats): [0, 1152) X^T rows: rec[i * 36 + j] = X[i][j] =
 // P_scaled[j][i] (start core state j -> end core state i); [1152, 1184)
@@ -71,7 +75,7 @@ constexpr unsigned kSpinMax = 1u << 20;  // phase B's bound on polls without pro
 // P00 relative to csum); 1218 csum (sum of the frames' offsets c_t);
 // 1219 flag (range violation); 1220 live frames.
 constexpr int kRecEj = 1152, kRecRt = 1184, kRecRho = 1216, kRecPi = 1217, kRecCs = 1218,
-              kRecFlag = 1219, kRecN = 1220;
+              kRecFlag = 1219, kRecN = 1220, kRecXa = 1248;
 
 struct CkArgs {
   const unsigned char* W;  // [B,T,C,R] fp32 / bf16
@@ -145,15 +149,26 @@ LT_DEVINL float safe_max(float m) { return __builtin_isfinite(m) ? m : 0.f; }
 #ifdef LT_DIAG
 #define CK_STAMP(k)                                                                  \
   do {                                                                               \
-    if (a.stamps && !LT_ABL(a, 64) && threadIdx.x == 0)                               \
+    if (a.stamps && !LT_ABL(a, 64 | 256) && threadIdx.x == 0)                         \
       a.stamps[(long long)blockIdx.x * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
+// phase B: per utterance b (the walking workgroup's), two marks per wave
 #define CK_WSTAMP(k)                                                                 \
   do {                                                                               \
     if (a.stamps && LT_ABL(a, 64) && (threadIdx.x & 63) == 0)                         \
-      a.stamps[(long long)blockIdx.x * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
+      a.stamps[(long long)b * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime();     \
+  } while (0)
+// phase A (LT_CK_DBG bit 256): per chunk wave, after phase C's per-workgroup marks
+#define CK_ASTAMP(k)                                                                 \
+  do {                                                                               \
+    if (a.stamps && LT_ABL(a, 256) && (threadIdx.x & 63) == 0)                        \
+      a.stamps[(long long)a.B * a.K * 8 + (long long)id * 4 + (k)] =                  \
+          (long long)__builtin_amdgcn_s_memtime();                                   \
   } while (0)
 #else
+#define CK_ASTAMP(k) \
+  do {               \
+  } while (0)
 #define CK_WSTAMP(k) \
   do {               \
   } while (0)
@@ -278,27 +293,60 @@ struct FrameRegs {
   float gb[PPL], gl[PPL];  // numerator arc weights of the lane's positions
 };
 
-// Every lane issues every load (indices clamped into the frame, the unused
-// values replaced afterwards): no load sits under a branch, so the
-// compiler's vmcnt bookkeeping across the prefetch stays exact.
+// Per-lane byte offsets of load_frame's loads inside a frame, fixed over the
+// chunk: the frame is one buffer resource (scalar base, bounded), so a load
+// costs no address arithmetic. The lane's k-step rows sit at compile-time
+// immediates past vb (FULL) or at scalar offsets (srow).
+template <int PPL>
+struct FrameOffs {
+  int vb, vr0, vbl, vdg, vgb[PPL], vgl[PPL];
+  int srow[16];
+};
+LT_DEVINL constexpr int krow(int s) { return (s & 3) + 8 * (s >> 2); }
 template <bool BF16, int PPL>
-LT_DEVINL void load_frame(const CkArgs& a, const unsigned char* Wf, int lane, const int* boff,
-                          const int* loff, FrameRegs<BF16, PPL>& f) {
-  const int V = a.V, R = a.R, i = lane & 31, h = lane >> 5;
-  const int ic = min(i, V - 1);
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int kk = min(kstep(s, h), V - 1);
-    f.w[s] = ldg<BF16>(Wf, (kk + 1) * R + ic + 1);
-  }
-  f.wr0 = ldg<BF16>(Wf, ic + 1);
-  f.wbl = ldg<BF16>(Wf, min(lane, V) * R);
-  f.wdg = ldg<BF16>(Wf, (ic + 1) * R);
-  f.w00 = ldg<BF16>(Wf, 0);
+LT_DEVINL void frame_offsets(const CkArgs& a, int lane, const int* boff, const int* loff,
+                             FrameOffs<PPL>& o) {
+  const int R = a.R, i = lane & 31, h = lane >> 5, es = BF16 ? 2 : 4;
+  o.vb = ((4 * h + 1) * R + i + 1) * es;  // row kstep(s, h) + 1, column i + 1
+  o.vr0 = (i + 1) * es;
+  o.vbl = lane * R * es;
+  o.vdg = (i + 1) * R * es;
 #pragma unroll
   for (int r = 0; r < PPL; ++r) {
-    f.gb[r] = ldg<BF16>(Wf, max(boff[r], 0));
-    f.gl[r] = ldg<BF16>(Wf, max(loff[r], 0));
+    o.vgb[r] = max(boff[r], 0) * es;
+    o.vgl[r] = max(loff[r], 0) * es;
+  }
+#pragma unroll
+  for (int s = 0; s < 16; ++s) o.srow[s] = krow(s) * R * es;
+}
+template <bool BF16>
+LT_DEVINL float ldb(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (BF16)
+    return __uint_as_float((unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0) << 16);
+  else
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+// Every lane issues every load (rows and columns past V read neighbouring
+// bytes of the chunk or, past its end, the resource's zeros; mask_frame
+// replaces them): no load sits under a branch, so the compiler's vmcnt
+// bookkeeping across the prefetch stays exact.
+template <bool BF16, int PPL, bool FULL>
+LT_DEVINL void load_frame(const unsigned char* Wf, int bytes, const FrameOffs<PPL>& o,
+                          FrameRegs<BF16, PPL>& f) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Wf, (short)0, bytes, 0x00020000);
+  constexpr int es = BF16 ? 2 : 4;
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+    f.w[s] = FULL ? ldb<BF16>(r, o.vb + krow(s) * 33 * es, 0) : ldb<BF16>(r, o.vb, o.srow[s]);
+  f.wr0 = ldb<BF16>(r, o.vr0, 0);
+  f.wbl = ldb<BF16>(r, o.vbl, 0);
+  f.wdg = ldb<BF16>(r, o.vdg, 0);
+  f.w00 = ldb<BF16>(r, 0, 0);
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) {
+    f.gb[q] = ldb<BF16>(r, o.vgb[q], 0);
+    f.gl[q] = ldb<BF16>(r, o.vgl[q], 0);
   }
 }
 // the values load_frame read for nothing (FULL: V = 32, every core value live)
@@ -350,10 +398,12 @@ LT_DEVINL void st_wt4(__amdgpu_buffer_rsrc_t r, int idx, float x, float y, float
 template <bool BF16, int PPL, bool FULL>
 LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   __shared__ __attribute__((aligned(16))) float s_rt[4][32];
+  __shared__ __attribute__((aligned(16))) float s_dg[4][32];
   __shared__ int s_lab[4][128];
   __shared__ __attribute__((aligned(16))) float2 s_g[4][128 + kGrp + 1];
   const int lane = threadIdx.x & 63;
   const int id = b * a.K + k;
+  CK_ASTAMP(0);
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const int t0 = k * a.L;
@@ -363,6 +413,7 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   const int i = lane & 31, h = lane >> 5;
   const int nt = t1 - t0;
   float* rt = s_rt[wave];
+  float* sdg = s_dg[wave];  // the frame's core blank self loops E[p][0], p = 1..32
   int* lab = s_lab[wave];
   float2* sg = s_g[wave];  // the frame's numerator arc weights (log2) by position
   for (int j = lane; j < a.U; j += 64) lab[j] = a.labels[(long long)b * a.U + j];
@@ -380,6 +431,7 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   }
   const long long es = BF16 ? 2 : 4;
   const unsigned char* W0 = a.W + ((long long)b * a.T + t0) * a.FR * es;
+  CK_ASTAMP(1);
 
   v16f X;  // X = P^T, column j (lane & 31) = start state j+1; identity
 #pragma unroll
@@ -389,21 +441,19 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   float pi = 0.f;     // log P00 - csum
   float csum = 0.f;   // sum of c_t (integers)
   int bad = 0;
-  // the lane's diagonal k-step (the blank self loop of state i+1 joins the
-  // core product there): 1 at s with kstep(s, h) == i, else 0
-  float dsel[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) dsel[s] = (kstep(s, h) == i && (FULL || i < V)) ? 1.f : 0.f;
   // numerator group bands: nbd[r][d] = log2 weight of the paths from
   // position s = lane + 64 r at the group's first frame to s + d after its
   // last (the string lattice's frame steps, lattices.py:340-377, composed)
   float nbd[PPL][kGrp + 1];
   const __amdgpu_buffer_rsrc_t nbr = wt_rsrc(a.nb + (long long)id * a.nbs, 4 * a.nbs);
 
-  // frames in registers two ahead; the loads are unconditional (clamped to
+  // the next frame in registers; the loads are unconditional (clamped to
   // the chunk's last frame) so the compiler's vmcnt tracking stays exact
-  FrameRegs<BF16, PPL> fr[2];
+  FrameRegs<BF16, PPL> fr;
+  FrameOffs<PPL> fo;
+  frame_offsets<BF16, PPL>(a, lane, boff, loff, fo);
   auto frame_ptr = [&](int f) { return W0 + (long long)min(f, nt - 1) * a.FR * es; };
+  auto frame_bytes = [&](int f) { return (nt - min(f, nt - 1)) * a.FR * (int)es; };
   auto step = [&](FrameRegs<BF16, PPL>& F, int f, bool reload) {
     mask_frame<BF16, PPL, FULL>(V, lane, boff, loff, F);
     // numerator: band step over the group (positions past the string read -inf)
@@ -452,11 +502,14 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     const float c = cfin ? ceilf(mx) : 0.f;
     const float cl = c * kLog2e;
     if (lane == 0) a.cf[(long long)b * a.T + t0 + f] = c;
-    // E_t^T as the A operand: lane (i, h), k-step s -> E[k][i]; the core
-    // diagonal also carries the blank self loop (alignments.py:294-297).
+    // E_t^T as the A operand: lane (i, h), k-step s -> E[k][i]. The core
+    // diagonal's blank self loop (alignments.py:294-297) is added beside
+    // the product (Dg X after the MFMAs, rt Dg in the state-0 row), which
+    // keeps the lane's diagonal k-step out of the registers.
     // The range test rides on the exponentials: every live E >= e^-61
     // (max - min <= kRange + 1; a NaN or -inf weight fails it, +inf fails cfin)
-    const float dgv = lt_exp_off(F.wdg, cl);
+    const float dgv = (FULL || i < V) ? lt_exp_off(F.wdg, cl) : 0.f;
+    if (lane < 32) sdg[lane] = dgv;
     float A[16];
     bool lbad = (lane <= V) && !(F.wbl >= c - (kRange + 1.f));
 #pragma unroll
@@ -464,18 +517,18 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
       const bool live = FULL || (kstep(s, h) < V && i < V);
       const float e = lt_exp_off(F.w[s], cl);
       lbad = lbad || (live && !(e >= kEmin));
-      A[s] = live ? __builtin_fmaf(dsel[s], dgv, e) : 0.f;
+      A[s] = live ? e : 0.f;
     }
     const float e0r = lt_exp_off(F.wr0, cl);
     const float e0 = (FULL || i < V) ? e0r : 0.f;
     lbad = lbad || ((FULL || i < V) && !(e0r >= kEmin));
     if (!cfin || __builtin_amdgcn_ballot_w64(lbad)) bad = 1;
     const float w00 = F.w00;
-    if (reload) load_frame(a, frame_ptr(f + 2), lane, boff, loff, F);
+    if (reload) load_frame<BF16, PPL, FULL>(frame_ptr(f + 1), frame_bytes(f + 1), fo, F);
 
     // state-0 row: r' = p00 * e0 + r Ec (VALU, beside the MFMAs)
     {
-      float part = 0.f;
+      float part = h ? 0.f : dgv * rt[i];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 r4 = *(const float4*)(rt + 8 * g + 4 * h);
@@ -506,6 +559,15 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     v16f D = {};
 #pragma unroll
     for (int s = 0; s < 16; ++s) D = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], X[s], D, 0, 0, 0);
+    // + Dg X: row kstep(r, h) of X times that state's blank self loop
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 d4 = *(const float4*)(sdg + 8 * g + 4 * h);
+      D[4 * g + 0] = __builtin_fmaf(d4.x, X[4 * g + 0], D[4 * g + 0]);
+      D[4 * g + 1] = __builtin_fmaf(d4.y, X[4 * g + 1], D[4 * g + 1]);
+      D[4 * g + 2] = __builtin_fmaf(d4.z, X[4 * g + 2], D[4 * g + 2]);
+      D[4 * g + 3] = __builtin_fmaf(d4.w, X[4 * g + 3], D[4 * g + 3]);
+    }
     // one power-of-two scale per column (start state j): its end state 1
     // (row 0, register 0 of half 0), within e^61 of the column's others
     const float cm = half_lo(D[0]);
@@ -516,18 +578,17 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     for (int r = 0; r < 16; ++r) X[r] = ldexpf(D[r], -e);
     ej += e;
   };
-  load_frame(a, frame_ptr(0), lane, boff, loff, fr[0]);
-  load_frame(a, frame_ptr(1), lane, boff, loff, fr[1]);
-  const int nmain = nt & ~1;
-  for (int f0 = 0; f0 < nmain; f0 += 2) {
-    step(fr[0], f0, true);
-    step(fr[1], f0 + 1, true);
-  }
-  if (nt & 1) step(fr[0], nt - 1, false);
+  // one frame in registers ahead (a frame step outlasts a load; a second
+  // buffer would cost the third wave per SIMD)
+  load_frame<BF16, PPL, FULL>(frame_ptr(0), frame_bytes(0), fo, fr);
+  for (int f = 0; f < nt; ++f) step(fr, f, f + 1 < nt);
+  CK_ASTAMP(2);
 
   const __amdgpu_buffer_rsrc_t rr = wt_rsrc(a.rec + (long long)id * kRec, 4 * kRec);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) st_wt(rr, kstep(r, h) * kRowT + i, X[r]);
+  for (int r = 0; r < 16; ++r) {
+    st_wt(rr, kstep(r, h) * kRowT + i, X[r]);
+  }
   if (lane < 32) {
     st_wt(rr, kRecEj + lane, ej);
     st_wt(rr, kRecRt + lane, rt[lane]);
@@ -541,6 +602,7 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     st_wt(rr, kRecN, nt);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  CK_ASTAMP(3);
   if (lane == 0)
     __hip_atomic_store((gu32*)(a.ready + id), bad ? 2u : 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -661,7 +723,9 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
   // al'[u] = (+)_d al[u - d] + N[u - d][d]; beta (wave 3, the reverse of
   // alignments.py:320-329): be'[s] = (+)_d N[s][d] + be[s + d]. The
   // neighbours come from an LDS copy of the vector padded with -inf.
-  constexpr int D = 8;  // groups in registers ahead (4 loads each: vmcnt <= 63)
+  // groups in registers ahead (2 PPL loads each: vmcnt <= 63); PPL = 2 keeps
+  // the walk inside the fused launch's register budget
+  constexpr int D = PPL == 1 ? 8 : (kAbWaves > 3 ? 4 : 5);
   constexpr int NB = kGrp + 1;
   constexpr int TS = NB + 1;  // alpha's scatter table row stride (odd: no bank conflicts)
   const int NGc = a.NGc;
@@ -823,15 +887,17 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
         s1 = __builtin_fmaf(R.x[g + 1].w, a1.w, s1);
       }
       s0 = __builtin_fmaf(R.rt, bc[32], s0);
-      const float nq = M + R.cs + lt_log(s0 + s1);  // lane i < 32: alpha'[i+1]
-      const float n0 = first_lane(al) + R.pi + R.cs;
-      const float sh = from_prev(nq, -kInf);
-      al = lane == 0 ? n0 : (lane < C ? sh : -kInf);
-      if (lane < C) dst[(long long)(k + 1) * CP + lane] = al;
-      if (reload) {
+      const float cs = R.cs, pi = R.pi;
+      // the record's last use: its successor two chunks on loads from here
+      if (reload && !LT_ABL(a, 512)) {
         rd.ensure_fwd(k + 2, lane);
         load_rec_alpha(rec_ptr(k + 2), lane, V, R);
       }
+      const float nq = M + cs + lt_log(s0 + s1);  // lane i < 32: alpha'[i+1]
+      const float n0 = first_lane(al) + pi + cs;
+      const float sh = from_prev(nq, -kInf);
+      al = lane == 0 ? n0 : (lane < C ? sh : -kInf);
+      if (lane < C) dst[(long long)(k + 1) * CP + lane] = al;
       __builtin_amdgcn_wave_barrier();
     };
     if (Kl > 0) {
@@ -874,19 +940,22 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
         p0 = __builtin_fmaf(R.x[4 * g + 2], b4.z, p0);
         p1 = __builtin_fmaf(R.x[4 * g + 3], b4.w, p1);
       }
-      const float tot = half_sum(p0 + p1);
-      const float nj = Mc + R.cs + R.ej + lt_log(tot);  // lane j: beta'[j+1]
-      // state 0: the rt row and its own self loop
-      const float rsum = wsum_u(lane < 32 ? R.rt * bc[lane & 31] : 0.f);
-      const float rterm = Mc + R.cs + R.rho + lt_log(rsum);
-      const float nb0 = lse2(first_lane(be) + R.pi + R.cs, rterm);
-      const float sh = from_prev(nj, -kInf);
-      be = lane == 0 ? nb0 : (lane < C ? sh : -kInf);
-      if (lane < C) dst[(long long)k * CP + lane] = be;
-      if (reload) {
+      const float rp = lane < 32 ? R.rt * bc[lane & 31] : 0.f;
+      const float cs = R.cs, ej = R.ej, rho = R.rho, pi = R.pi;
+      // the record's last use: its successor two chunks on loads from here
+      if (reload && !LT_ABL(a, 512)) {
         rd.ensure_bwd(k - 2, lane);
         load_rec_beta(rec_ptr(k - 2), lane, R);
       }
+      const float tot = half_sum(p0 + p1);
+      const float nj = Mc + cs + ej + lt_log(tot);  // lane j: beta'[j+1]
+      // state 0: the rt row and its own self loop
+      const float rsum = wsum_u(rp);
+      const float rterm = Mc + cs + rho + lt_log(rsum);
+      const float nb0 = lse2(first_lane(be) + pi + cs, rterm);
+      const float sh = from_prev(nj, -kInf);
+      be = lane == 0 ? nb0 : (lane < C ? sh : -kInf);
+      if (lane < C) dst[(long long)k * CP + lane] = be;
       __builtin_amdgcn_wave_barrier();
     };
     if (Kl > 0) {
@@ -937,7 +1006,7 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
 // correctness: a walk that never sees its chunk times out to the
 // frame-serial kernels.
 template <bool BF16, int PPL, bool FULL>
-__global__ __launch_bounds__(256, 2) void ck_ab_kernel(const CkArgs a) {
+__global__ __launch_bounds__(256, kAbWaves) void ck_ab_kernel(const CkArgs a) {
   const int nc = a.nc;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int x = blockIdx.x;

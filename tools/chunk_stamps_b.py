@@ -22,7 +22,8 @@ st = torch.zeros([B * 8 * 8], dtype=torch.int64, device='cuda')
 for _ in range(3):
   _native.loss_grad(W, nf, lab, nl, V, 1, False)
 torch.cuda.synchronize()
-for extra, what in ((0, 'all waves'), (1 | 128, 'num beta alone'), (2, 'den alone')):
+for extra, what in ((0, 'all waves'), (1 | 128, 'num beta alone'), (2, 'den alone'),
+                    (2 | 512, 'den alone, no record loads')):
   st.zero_()
   os.environ['LT_CK_DBG'] = str(64 | extra)
   os.environ['LT_CK_STAMPS'] = hex(st.data_ptr())
