@@ -1420,6 +1420,14 @@ int chunk_loss_grad(const lt_problem* pb, int local_norm, const void* W, const i
                     const int32_t* labels, const int32_t* num_labels, float* loss, float* log_z,
                     float* num, void* dW, void* state, size_t state_bytes, void* scratch,
                     size_t scratch_bytes, void* stream);
+// lt_vit.hip: bigram MaxTropical forward (distance, best final state, backpointers)
+bool vit_bigram_eligible(const lt_problem* pb);
+int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, unsigned char* bp,
+                       int* qstar, float* dist, void* stream);
+int vit_backtrace_lds(const lt_problem* pb, int* seg);
+int vit_backtrace(const lt_problem* pb, const unsigned char* bp, const int* qstar,
+                  const int32_t* nfr, const float* grad, int64_t* labels, void* arcs,
+                  int32_t conv, void* stream);
 // lt_pipe.hip: pipelined bigram Log recursions (alpha, and beta when dirs == 2)
 bool pipe_eligible(const lt_problem* pb);
 int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32_t* nfr,

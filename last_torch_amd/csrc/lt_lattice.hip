@@ -1063,18 +1063,28 @@ int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
   const long long bpb = (long long)pb->batch * pb->max_frames * g.C;
   unsigned char* bp = (unsigned char*)workspace;
   int* qstar = (int*)((char*)workspace + ((bpb + 255) & ~255LL));
-  lt_problem p2 = *pb;
-  p2.max_labels = 0;
-  Plan pl;
-  if ((rc = plan(&p2, g, 0, F_DEN, &pl))) return rc;
-  bind_streams(pl.a, W, nullptr, nullptr);
-  pl.a.nfr = num_frames;
-  pl.a.dist = path_weight;
-  pl.a.bp = bp;
-  pl.a.qstar = qstar;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   hipStream_t st = (hipStream_t)stream;
-  if ((rc = launch_fwd(M_MAX, pl, bf16, pb->batch, st))) return rc;
+  if (lt_impl::vit_bigram_eligible(pb)) {
+    // bigram: one wave per utterance, the chain in registers (lt_vit.hip)
+    if ((rc = lt_impl::vit_bigram_forward(pb, W, num_frames, bp, qstar, path_weight, stream)))
+      return rc;
+  } else {
+    lt_problem p2 = *pb;
+    p2.max_labels = 0;
+    Plan pl;
+    if ((rc = plan(&p2, g, 0, F_DEN, &pl))) return rc;
+    bind_streams(pl.a, W, nullptr, nullptr);
+    pl.a.nfr = num_frames;
+    pl.a.dist = path_weight;
+    pl.a.bp = bp;
+    pl.a.qstar = qstar;
+    if ((rc = launch_fwd(M_MAX, pl, bf16, pb->batch, st))) return rc;
+  }
+  int seg = 0;
+  if (lt_impl::vit_bigram_eligible(pb) && lt_impl::vit_backtrace_lds(pb, &seg) > 0)
+    return lt_impl::vit_backtrace(pb, bp, qstar, num_frames, grad, labels, arcs, label_convention,
+                                  stream);
   BtArgs bt;
   bt.bp = bp; bt.qstar = qstar; bt.nfr = num_frames; bt.grad = grad;
   bt.labels = (long long*)labels; bt.arcs = arcs;

@@ -1,0 +1,342 @@
+// lt_vit.hip -- MaxTropical shortest-distance forward with backpointers for
+// the bigram lattice (FullNGram n = 1, V <= 32, FrameDependent): the
+// forward half of lt_viterbi (lattices.py:185-247 -> shortest_path through
+// _forward in MaxTropical, lattices.py:379-496), frame-serial per utterance,
+// bit-exact with the generic frame kernel (same terms, same order, same
+// first-maximum rule: semirings.py MaxTropical, term order of
+// contexts.py:226-229 with the blank self loop first).
+//
+// One wave per utterance, the whole chain in registers and LDS:
+//   lane (j, h): destination q = j + 1 (a core state), half h of its in-arcs:
+//   h = 0 the blank self loop (term 0) and sources p = 0..16 (terms 1..17),
+//   h = 1 sources p = 17..32 (terms 18..33); the halves meet through one
+//   permlane32 swap (the earlier half wins ties). The start state 0 has only
+//   its blank self loop. alpha sits in LDS (one write, five b128 reads per
+//   frame); the frame's weights stream into registers three frames ahead
+//   through one buffer resource per frame (no address arithmetic). The
+//   alpha chain takes the maximum by a max3 tree; the backpointer (the
+//   first term equal to it) is formed beside the chain.
+// Backpointers: one byte per (frame, state), the term index, as the generic
+// kernel writes them (backtrace_kernel reads both).
+#include "lt_kernels.h"
+
+namespace {
+
+struct VitArgs {
+  const unsigned char* W;  // [B,T,C,R] fp32 / bf16
+  const int* nfr;
+  unsigned char* bp;       // [B,T,C]
+  int* qstar;              // [B] best final state
+  float* dist;             // [B] the shortest distance (MaxTropical)
+  int B, T, V, C, R;
+  int dbg;                 // diagnostic builds (LT_DIAG) only: 1 = no weight reloads
+};
+
+constexpr int kHalf = 17;  // sources per half (p < 17 in h = 0)
+
+// alpha's LDS slots: half 0's sources at [0, 17), half 1's at [20, 36)
+// (16-byte aligned for the b128 reads)
+LT_DEVINL int aslot(int p) { return p < kHalf ? p : p + 3; }
+
+LT_DEVINL float max3_raw(float x, float y, float z) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+  return r;
+}
+
+// the frame's weights stream into registers kAhead frames ahead (19 loads a
+// frame: kAhead x 19 stays inside vmcnt's 63), through one buffer resource
+// per frame (no address arithmetic)
+constexpr int kAhead = 3;
+
+template <bool BF16>
+LT_DEVINL float vld(__amdgpu_buffer_rsrc_t r, int voff) {
+  if constexpr (BF16)
+    return __uint_as_float((unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, voff, 0, 0) << 16);
+  else
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+}
+
+struct VitFrame {
+  float w[kHalf];  // W[p][q] for the lane's sources
+  float self;      // W[q][0]
+  float w00;       // W[0][0]
+};
+
+template <bool BF16, bool FULL>
+LT_DEVINL void vit_load(const unsigned char* Wf, int bytes, int vb, int vself, int R,
+                        VitFrame& f) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Wf, (short)0, bytes, 0x00020000);
+  constexpr int es = BF16 ? 2 : 4;
+#pragma unroll
+  for (int m = 0; m < kHalf; ++m) f.w[m] = vld<BF16>(r, vb + m * (FULL ? 33 : R) * es);
+  f.self = vld<BF16>(r, vself);
+  f.w00 = vld<BF16>(r, 0);
+}
+
+template <bool BF16, bool FULL>
+__global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_al[2][40];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int j = lane & 31, h = lane >> 5;
+  const int V = FULL ? 32 : a.V, R = FULL ? 33 : a.R, C = V + 1;
+  constexpr int es = BF16 ? 2 : 4;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int q = j + 1;
+  const bool live = j < V;  // a core destination
+  // the lane's sources p = 17 h + m (p <= V)
+  const int p0 = kHalf * h;
+  const int vb = (p0 * R + min(q, V)) * es;
+  const int vself = min(q, V) * R * es;
+  const long long fbytes = (long long)C * R * es;
+  const unsigned char* W0 = a.W + (long long)b * a.T * fbytes;
+  // backpointer stores through a buffer resource too: a per-frame 64-bit
+  // address would make the compiler drain vmcnt when it recycles the pair
+  const __amdgpu_buffer_rsrc_t bpr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.bp + (long long)b * a.T * C), (short)0,
+                                        a.T * C, 0x00020000);
+  // alpha_0: the start state (MaxTropical one = 0), every other state zero
+  if (lane < 40) s_al[0][lane] = lane == 0 ? 0.f : -kInf;
+  float a0 = 0.f;  // alpha[0] (only its blank self loop reaches it)
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  VitFrame fr[kAhead];
+  auto fptr = [&](int t) { return W0 + (long long)min(t, max(nf - 1, 0)) * fbytes; };
+  auto fb = [&](int t) { return (int)((nf - min(t, max(nf - 1, 0))) * fbytes); };
+  if (nf > 0) {
+#pragma unroll
+    for (int d = 0; d < kAhead; ++d) vit_load<BF16, FULL>(fptr(d), fb(d), vb, vself, R, fr[d]);
+  }
+  auto step = [&](VitFrame& F, int t) {
+    if (t >= nf) return;  // the last round's spare steps
+    const float* acur = s_al[t & 1];
+    float* anxt = s_al[(t + 1) & 1];
+    // the sources' alpha: five b128 reads of the lane's half
+    float al[20];
+#pragma unroll
+    for (int g = 0; g < 5; ++g) {
+      const float4 v = *(const float4*)(acur + 20 * h + 4 * g);
+      al[4 * g + 0] = v.x; al[4 * g + 1] = v.y; al[4 * g + 2] = v.z; al[4 * g + 3] = v.w;
+    }
+    const float aq = acur[aslot(min(q, V))];
+    float x[kHalf];
+#pragma unroll
+    for (int m = 0; m < kHalf; ++m) {
+      const bool ok = FULL ? (m < kHalf - 1 || h == 0) : p0 + m <= V;  // FULL: only p = 33 is out
+      x[m] = ok ? al[m] + F.w[m] : -kInf;
+    }
+    const float xs = aq + F.self;
+    const float w00 = F.w00;
+    const int ib = h ? 18 : 1;  // term index of x[0]
+    if (!LT_ABL(a, 1)) vit_load<BF16, FULL>(fptr(t + kAhead), fb(t + kAhead), vb, vself, R, F);
+    // the value: a max3 tree over the lane's terms, the halves by one
+    // permlane32 swap (the alpha chain waits on nothing else)
+    float mx = max3_raw(h ? x[16] : xs, x[0], x[1]);
+    mx = max3_raw(mx, x[2], x[3]);
+    const float m1 = max3_raw(x[4], x[5], x[6]);
+    const float m2 = max3_raw(x[7], x[8], x[9]);
+    const float m3 = max3_raw(x[10], x[11], x[12]);
+    const float m4 = max3_raw(x[13], x[14], x[15]);
+    mx = max3_raw(mx, m1, m2);
+    mx = max3_raw(mx, m3, m4);
+    if (h == 0) mx = fmaxf(mx, x[16]);
+    auto pv = __builtin_amdgcn_permlane32_swap(__float_as_int(mx), __float_as_int(mx), false, false);
+    // permlane32_swap hands the upper lanes the lower half's value in [0]
+    // and the lower lanes the upper half's in [1]
+    const float r = fmaxf(mx, __int_as_float(h ? pv[0] : pv[1]));
+    if (h == 0 && live) anxt[aslot(q)] = r;
+    a0 += w00;
+    if (lane == 32) anxt[0] = a0;
+    // the backpointer: the first term equal to the maximum (group_reduce's
+    // first-maximum rule), the lower half first
+    int ri = 99;
+#pragma unroll
+    for (int m = 16; m >= 0; --m) ri = x[m] == r ? ib + m : ri;
+    if (h == 0) ri = xs == r ? 0 : ri;
+    auto pi = __builtin_amdgcn_permlane32_swap(ri, ri, false, false);
+    const int rlo = h ? pi[0] : ri, rhi = h ? ri : pi[1];
+    const int bpv = lane == 32 ? 0 : (rlo < 99 ? rlo : rhi);
+    if ((h == 0 && live) || lane == 32)
+      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bpv, bpr, lane == 32 ? 0 : q, t * C, 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  };
+  for (int t0 = 0; t0 < nf; t0 += kAhead) {
+#pragma unroll
+    for (int d = 0; d < kAhead; ++d) step(fr[d], t0 + d);
+  }
+  // the distance: (+)_q alpha_T[q] in MaxTropical, the first maximum
+  const float* af = s_al[nf & 1];
+  float r = lane < C ? af[aslot(lane)] : -kInf;
+  int ri = lane < C ? lane : 0x7fffffff;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const float pv = __shfl_xor(r, s);
+    const int pi = __shfl_xor(ri, s);
+    if (pv > r || (pv == r && pi < ri)) { r = pv; ri = pi; }
+  }
+  if (lane == 0) {
+    a.dist[b] = r;
+    a.qstar[b] = ri;
+  }
+}
+
+// Backtrace of the bigram backpointers in segments (one workgroup per
+// utterance, the utterance's backpointers staged in LDS): every segment of S
+// frames walks back from each of its C possible end states at once (the
+// segment's start state per end state), one thread composes the segments
+// from the best final state, then every segment emits its own frames'
+// labels. Serial depth S + T/S + S instead of T. The walk itself is the
+// generic backtrace's (lattices.py:229-247 through the one-hot arcs):
+// backpointer 0 = the blank self loop (label 0, state kept), k + 1 = the
+// arc from source k with label q.
+struct VbtArgs {
+  const unsigned char* bp;
+  const int* qstar;
+  const int* nfr;
+  const float* grad;
+  long long* labels;  // [B,T]
+  void* arcs;         // [B,T,C,R] or null
+  int B, T, C, R, conv, S;
+};
+
+template <bool BF16>
+LT_DEVINL void st_arc(void* arcs, long long e, float v) {
+  if constexpr (BF16) ((unsigned short*)arcs)[e] = (unsigned short)(__float_as_uint(v) >> 16);
+  else ((float*)arcs)[e] = v;
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void vit_backtrace_kernel(const VbtArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int C = a.C, R = a.R, S = a.S;
+  const long long FR = (long long)C * R;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  long long* lab = a.labels + (long long)b * a.T;
+  for (int t = nf + tid; t < a.T; t += 256) lab[t] = 0;  // padding frames
+  if (a.arcs) {
+    const long long n = (long long)a.T * FR;
+    for (long long e = tid; e < n; e += 256) st_arc<BF16>(a.arcs, (long long)b * a.T * FR + e, 0.f);
+  }
+  const int nseg = (nf + S - 1) / S;
+  unsigned char* rows = lds;                          // [nf][C]
+  unsigned char* start = lds + ((nf * C + 15) & ~15);  // [nseg][C]
+  int* endq = (int*)(start + ((nseg * C + 15) & ~15));  // [nseg]
+  const unsigned char* src = a.bp + (long long)b * a.T * C;
+  const int nb = nf * C;
+  for (int e = tid * 4; e < nb; e += 1024) {
+    if (e + 4 <= nb && ((((uintptr_t)(src + e)) & 3) == 0)) {
+      *(unsigned*)(rows + e) = *(const unsigned*)(src + e);
+    } else {
+      for (int k = e; k < nb && k < e + 4; ++k) rows[k] = src[k];
+    }
+  }
+  __syncthreads();
+  // each (segment, end state): the state before the segment's first frame
+  for (int x = tid; x < nseg * C; x += 256) {
+    const int sg = x / C;
+    int q = x - sg * C;
+    const int t1 = min(nf, (sg + 1) * S);
+    for (int t = t1 - 1; t >= sg * S; --t) {
+      const int i = rows[t * C + q];
+      q = i ? i - 1 : q;
+    }
+    start[x] = (unsigned char)q;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int q = nf > 0 ? a.qstar[b] : 0;
+    for (int sg = nseg - 1; sg >= 0; --sg) {
+      endq[sg] = q;
+      q = start[sg * C + q];
+    }
+  }
+  __syncthreads();
+  if (a.arcs) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // zero fill before the scatter
+  __syncthreads();
+  const float gb = a.grad ? a.grad[b] : 1.f;
+  for (int sg = tid; sg < nseg; sg += 256) {
+    int q = endq[sg];
+    const int t1 = min(nf, (sg + 1) * S);
+    for (int t = t1 - 1; t >= sg * S; --t) {
+      const int i = rows[t * C + q];
+      const int p = i ? i - 1 : q, y = i ? q : 0;
+      lab[t] = i ? (a.conv == LT_LABELS_REFERENCE ? (long long)(y - 1) : (long long)y) : 0LL;
+      if (a.arcs) st_arc<BF16>(a.arcs, ((long long)b * a.T + t) * FR + (long long)p * R + y, gb);
+      q = p;
+    }
+  }
+}
+
+}  // namespace
+
+namespace lt_impl {
+bool vit_bigram_eligible(const lt_problem* pb) {
+  return pb->context_size == 1 && pb->vocab_size >= 1 && pb->vocab_size <= 32 &&
+         getenv("LT_VIT_GENERIC") == nullptr;
+}
+
+// MaxTropical forward (distance, best final state, backpointers) of every
+// utterance; lt_viterbi's backtrace reads the backpointers.
+int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, unsigned char* bp,
+                       int* qstar, float* dist, void* stream) {
+  VitArgs a;
+  a.W = (const unsigned char*)W;
+  a.nfr = nfr;
+  a.bp = bp;
+  a.qstar = qstar;
+  a.dist = dist;
+  a.B = pb->batch;
+  a.T = pb->max_frames;
+  a.V = pb->vocab_size;
+  a.C = a.V + 1;
+  a.R = a.V + 1;
+  a.dbg = 0;
+#ifdef LT_DIAG
+  if (const char* d = getenv("LT_VIT_DBG")) a.dbg = atoi(d);
+#endif
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  const bool full = a.V == 32;
+  const void* k = full ? (bf16 ? (const void*)vit_bigram_kernel<true, true>
+                               : (const void*)vit_bigram_kernel<false, true>)
+                       : (bf16 ? (const void*)vit_bigram_kernel<true, false>
+                               : (const void*)vit_bigram_kernel<false, false>);
+  void* args[] = {(void*)&a};
+  hipError_t e = hipLaunchKernel(k, dim3(a.B), dim3(64), args, 0, (hipStream_t)stream);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
+  return LT_OK;
+}
+
+// LDS bytes of vit_backtrace for T frames (0: too long, use the generic one)
+int vit_backtrace_lds(const lt_problem* pb, int* seg) {
+  const int T = pb->max_frames, C = pb->vocab_size + 1;
+  const int S = std::max(16, (T + 255) / 256);
+  const int nseg = (T + S - 1) / S;
+  const long long bytes = ((T * (long long)C + 15) & ~15LL) + ((nseg * C + 15) & ~15) + 4LL * nseg;
+  *seg = S;
+  return bytes <= 144 * 1024 ? (int)bytes : 0;
+}
+
+int vit_backtrace(const lt_problem* pb, const unsigned char* bp, const int* qstar,
+                  const int32_t* nfr, const float* grad, int64_t* labels, void* arcs,
+                  int32_t conv, void* stream) {
+  VbtArgs a;
+  a.bp = bp; a.qstar = qstar; a.nfr = nfr; a.grad = grad;
+  a.labels = (long long*)labels; a.arcs = arcs;
+  a.B = pb->batch; a.T = pb->max_frames; a.C = pb->vocab_size + 1; a.R = a.C; a.conv = conv;
+  const int lds = vit_backtrace_lds(pb, &a.S);
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  const void* k = bf16 ? (const void*)vit_backtrace_kernel<true> : (const void*)vit_backtrace_kernel<false>;
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  void* args[] = {(void*)&a};
+  if (e == hipSuccess) e = hipLaunchKernel(k, dim3(a.B), dim3(256), args, lds, (hipStream_t)stream);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
+  return LT_OK;
+}
+}  // namespace lt_impl
