@@ -75,7 +75,7 @@ constexpr unsigned kSpinMax = 1u << 20;  // phase B's bound on polls without pro
 // P00 relative to csum); 1218 csum (sum of the frames' offsets c_t);
 // 1219 flag (range violation); 1220 live frames.
 constexpr int kRecEj = 1152, kRecRt = 1184, kRecRho = 1216, kRecPi = 1217, kRecCs = 1218,
-              kRecFlag = 1219, kRecN = 1220, kRecXa = 1248;
+              kRecFlag = 1219, kRecN = 1220;
 
 struct CkArgs {
   const unsigned char* W;  // [B,T,C,R] fp32 / bf16
