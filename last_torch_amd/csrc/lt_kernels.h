@@ -395,9 +395,13 @@ struct KArgs {
 // the compiler cannot see through: each role loop then loads only the
 // fields it uses (scalar loads at the use), instead of the whole KArgs being
 // hoisted to the kernel entry and kept live (SGPR spills) across all roles.
+// KOFF: the byte offset of this role's KArgs among the kernel's arguments
+// (fwdbwd_kernel's second KArgs sits at sizeof(KArgs)).
+template <int KOFF = 0>
 LT_DEVINL const KArgs& fresh_args() {
   typedef const __attribute__((address_space(4))) KArgs* KP;
-  KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+  KP p = (KP)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+              KOFF);
   asm volatile("" : "+s"(p));
   return *(const KArgs*)p;
 }
@@ -837,9 +841,8 @@ LT_DEVINL void num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, con
 }
 
 template <int MODE, bool BF16, bool WST, int LG, int P>
-__global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
+LT_DEVINL void fwd_body(const KArgs& a, const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const NGram& g = a.g;
@@ -1279,10 +1282,9 @@ LT_DEVINL void num_beta_loop(const KArgs& a, unsigned char* lds, float* nbb, con
 // are computed and written per frame (a.beta / a.beta_num); the arc
 // marginals come later from marg_kernel, so this kernel can run
 // concurrently with the forward (both depend only on W).
-template <bool BF16, bool WST, bool DST, int LG, int P, bool CK = false>
-__global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
+template <bool BF16, bool WST, bool DST, int LG, int P, bool CK = false, int KOFF = 0>
+LT_DEVINL void bwd_body(const KArgs& a, const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const NGram& g = a.g;
@@ -1360,15 +1362,15 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
     loader_loop(a, b, nf, true, lw, lane, ldsb, DST && do_num ? 1 : 0);
   } else if (role == 0) {
     if (!LT_ABL(a, 1) && (!CK || do_den))
-      den_bwd_loop<BF16, WST, DST, LG, P, CK>(fresh_args(), lds, bbuf, nbuf3, b, nf, tid, gb,
+      den_bwd_loop<BF16, WST, DST, LG, P, CK>(fresh_args<KOFF>(), lds, bbuf, nbuf3, b, nf, tid, gb,
                                               log_z, do_den, do_num);
     else idle_loop(nf);
   } else {
     if (do_num && !LT_ABL(a, 2)) {
       if constexpr (CK)
-        num_beta_loop<BF16, WST>(fresh_args(), lds, nbb, ctx, ylab, b, nf, al, aux_lanes);
+        num_beta_loop<BF16, WST>(fresh_args<KOFF>(), lds, nbb, ctx, ylab, b, nf, al, aux_lanes);
       else
-        num_bwd_loop<BF16, WST, DST>(fresh_args(), lds, nbb, nbuf3, ctx, ylab, b, nf, al,
+        num_bwd_loop<BF16, WST, DST>(fresh_args<KOFF>(), lds, nbb, nbuf3, ctx, ylab, b, nf, al,
                                      aux_lanes, gb, numv);
     } else {
       idle_loop(nf);
@@ -1383,6 +1385,25 @@ __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
     const int nthr = blockDim.x;
     for (long long e = tid; e < n; e += nthr) stw<BF16>(a.dW, base + e, 0.f);
   }
+}
+
+template <int MODE, bool BF16, bool WST, int LG, int P>
+__global__ __launch_bounds__(1024) void fwd_kernel(const KArgs a) {
+  fwd_body<MODE, BF16, WST, LG, P>(a, blockIdx.x);
+}
+template <bool BF16, bool WST, bool DST, int LG, int P, bool CK = false>
+__global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
+  bwd_body<BF16, WST, DST, LG, P, CK>(a, blockIdx.x);
+}
+// The checkpointing pair in one launch: workgroups [0, nb) run the Log
+// forward (alpha, alpha^n, loss) and [nb, 2 nb) the checkpointing backward
+// (beta, beta^n). Both depend only on W, so they run side by side, as
+// two launches on two streams would, without the library owning a stream.
+static_assert(sizeof(KArgs) % alignof(KArgs) == 0, "the second KArgs follows the first");
+template <bool BF16, bool WST, int LG, int P>
+__global__ __launch_bounds__(1024) void fwdbwd_kernel(const KArgs af, const KArgs ab, int nb) {
+  if ((int)blockIdx.x < nb) fwd_body<M_LOG, BF16, WST, LG, P>(af, blockIdx.x);
+  else bwd_body<BF16, WST, false, LG, P, true, (int)sizeof(KArgs)>(ab, blockIdx.x - nb);
 }
 
 }  // namespace
@@ -1404,7 +1425,8 @@ struct Plan {
   X(3, 5) X(2, 9) X(1, 4) X(1, 3) X(2, 5) X(3, 3) X(2, 3) X(M1, 4) X(M1, 8) X(M1, 16)
 #define LT_DECL(LG, P)                                                                   \
   int launch_fwd_##LG##_##P(int mode, const Plan& pl, bool bf16, int grid, hipStream_t st); \
-  int launch_bwd_##LG##_##P(const Plan& pl, bool bf16, int grid, hipStream_t st);
+  int launch_bwd_##LG##_##P(const Plan& pl, bool bf16, int grid, hipStream_t st);          \
+  int launch_fwdbwd_##LG##_##P(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStream_t st);
 LT_VARIANTS(LT_DECL)
 #undef LT_DECL
 int set_error(int code, const char* msg);

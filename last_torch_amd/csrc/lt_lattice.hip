@@ -899,8 +899,8 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   if (ck && lt_impl::pipe_eligible(pb))
     return lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
                                 num, alpha, alpha_num, beta, beta_num, arcs, 2, nullptr, stream);
-  // With checkpoints, the beta pass (independent of alpha) and then the
-  // alpha pass, both on the caller's stream (the library forks no stream:
+  // With checkpoints, the beta pass (independent of alpha) and the alpha
+  // pass, both on the caller's stream (the library forks no stream:
   // everything stays ordered on `stream` and capturable).
   Plan pf, pbk;
   if (ck) {
@@ -924,6 +924,24 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   pf.a.alpha = alpha;
   pf.a.alpha_num = alpha_num;
   pf.a.arcs = ck ? arcs : nullptr;
+#ifdef LT_DIAG
+  if (getenv("LT_PLAN_DEBUG")) {
+    fprintf(stderr, "fwd plan lg=%d P=%d wst=%d threads=%d lds=%d\n", pf.lg, pf.tmax, pf.wst,
+            pf.threads, pf.lds_bytes);
+    if (ck)
+      fprintf(stderr, "bwd plan lg=%d P=%d wst=%d threads=%d lds=%d\n", pbk.lg, pbk.tmax,
+              pbk.wst, pbk.threads, pbk.lds_bytes);
+  }
+#endif
+  // same geometry (the usual case): beta and alpha side by side in one
+  // launch; else beta, then alpha
+  if (ck && pf.lg == pbk.lg && pf.tmax == pbk.tmax && pf.wst == pbk.wst &&
+      pf.threads == pbk.threads && env_int("LT_PAIR", 1)) {
+#define LT_CASE(LG, P) \
+  if (pf.lg == LG && pf.tmax == P) return lt_impl::launch_fwdbwd_##LG##_##P(pf, pbk, bf16, pb->batch, st);
+    LT_VARIANTS(LT_CASE)
+#undef LT_CASE
+  }
   if (ck && (rc = launch_bwd(pbk, bf16, pb->batch, st))) return rc;
   return launch_fwd(M_LOG, pf, bf16, pb->batch, st);
 }

@@ -26,4 +26,8 @@ N=5 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/p
 step pmc write
 N=5 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
   python3 tools/chunk_prof.py > $OUT/pmc_write.log 2>&1 || { tail -20 $OUT/pmc_write.log; exit 1; }
+
+step configs
+timeout -k 10 300 python3 -u tools/configs_bench.py > $OUT/configs.jsonl 2> $OUT/configs.err || { tail -20 $OUT/configs.err; exit 1; }
+cat $OUT/configs.jsonl
 step done
