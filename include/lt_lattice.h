@@ -146,8 +146,9 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
  * to produce (lattices.py:131-183 with the backward of alignments.py:300-318;
  * D1/D3 in the reference). Utterances with num = -inf get dW = 0.
  * For the bigram (FullNGram n = 1, V <= 32, U <= 127) this is the chunked
- * two-level scan below (three launches, plus the frame-serial pair whose
- * workgroups exit at once unless an utterance is out of its range). Other
+ * two-level scan below (two launches after a flag memset, plus the
+ * frame-serial pair whose workgroups exit at once unless an utterance is out
+ * of its range or a hand-off wait timed out). Other
  * bigram shapes with 2B below the CU count run ONE fused launch (alpha and
  * beta recursions plus workgroups that turn every frame into marginals as
  * soon as both recursions have passed it; should a hand-off wait time out,
@@ -183,7 +184,11 @@ int lt_scale_grad(const lt_problem* pb, const float* grad, void* dW,
  * span more than 61 (max - min) run through the frame-serial kernels inside
  * the same calls (same results, slower). Sizes from
  * lt_chunk_workspace_bytes(); both buffers 16-byte aligned.
- * lt_loss_grad runs the same three launches for every shape they take. */
+ * Phase A (chunk transfers) and phase B (the boundary walks) share one
+ * launch while B <= CUs: per-chunk ready flags, write-through stores,
+ * agent-scope acquire on the walks' side; a walk that never sees its chunk
+ * times out and sends its utterance to the frame-serial kernels.
+ * lt_loss_grad runs the same launches for every shape they take. */
 int lt_chunk_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_t* state_bytes,
                              size_t* scratch_bytes);
 int lt_chunk_forward(const lt_problem* pb, int32_t local_norm, const void* W,

@@ -1143,7 +1143,7 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W) || misaligned(dW)) return fail(LT_EINVAL, "W/dW must be 16-byte aligned");
   if (lt_impl::chunk_eligible(pb) && pb->max_frames > 0) {
-    // bigram: the chunked two-level scan (lt_chunk.hip), three launches (plus
+    // bigram: the chunked two-level scan (lt_chunk.hip), two launches (plus
     // the frame-serial pair, whose workgroups exit at once unless an
     // utterance is out of the fast path's range)
     size_t st = 0, sc = 0;
