@@ -381,6 +381,8 @@ class RecognitionLattice(nn.Module, Generic[T]):
     gradients are the arc marginals (Log) or the best-path indicator
     (MaxTropical) -- per utterance, without the batch aliasing of D6.
     """
+    if semiring is semirings.LogLogExpectation and blank_mask is None and lexical_mask is None:
+      return self._forward_expectation(cache, frames, num_frames)
     for name, mask in (('blank_mask', blank_mask), ('lexical_mask', lexical_mask)):
       if mask is not None and len(mask) != self.alignment.num_states():
         raise ValueError(f'The length of {name} should be equal to '
@@ -427,6 +429,47 @@ class RecognitionLattice(nn.Module, Generic[T]):
     C = alpha.shape[-1]
     return (self._home(dist.reshape(batch_dims), frames),
             self._home(alpha.reshape(*batch_dims, frames.shape[-2], C), frames))
+
+  def _expectation(self, cache, frames, num_frames):
+    """(log Z, sum over arcs of m(arc) * w(arc)) per utterance, m the arc
+    marginals (the gradient of log Z: the den backward kernel on a ROCm
+    device, autograd through cpu.py on the CPU). FullNGram x FrameDependent."""
+    if self._table_path():
+      raise NotImplementedError('the expectation path covers FullNGram x FrameDependent lattices')
+    W, nf, batch_dims, B, V, n, _ = self._prepare(cache, frames, num_frames)
+    with torch.enable_grad():
+      Wd = W.detach().requires_grad_(True)
+      if Wd.device.type == 'cpu':
+        log_z, _ = cpu.den_forward(Wd, nf, self.context, self.alignment, semirings.Log)
+      else:
+        log_z, _ = _DenFn.apply(Wd, nf, V, n, _semiring_id(semirings.Log))
+      (m,) = torch.autograd.grad(log_z.sum(), Wd)
+    # arcs of zero weight (w = -inf) carry m = 0 and contribute nothing
+    mw = torch.where(m > 0, m * Wd.detach().float(), torch.zeros_like(m)).sum(dim=(-3, -2, -1))
+    return log_z.detach(), mw, batch_dims
+
+  def _forward_expectation(self, cache, frames, num_frames):
+    """_forward under semirings.LogLogExpectation (semirings.py:405-484).
+    The lattice's arc weights are single tensors, so every arc carries the
+    expectation pair weighted(w, -w): the value -w, the convention of the
+    reference's entropy test (tests/semirings_test.py:305-312). The shortest
+    distance is then (log Z, log Z + log E_p[-w_path]) by the forward-backward
+    identity (the x component sums Z m(arc) v(arc) over arcs). Returns
+    ((log_z, log_sum), None): there is no per-frame alpha of a pair."""
+    log_z, mw, batch_dims = self._expectation(cache, frames, num_frames)
+    log_sum = log_z + torch.log(-mw)
+    return ((self._home(log_z.reshape(batch_dims), frames),
+             self._home(log_sum.reshape(batch_dims), frames)), None)
+
+  def entropy(self, frames: torch.Tensor, num_frames: torch.Tensor,
+              cache: Optional[T] = None) -> torch.Tensor:
+    """Entropy (nats) of the alignment-path distribution p(path) = exp(w_path)
+    / Z of every utterance: H = log Z - E_p[w_path], the lattice entropy the
+    LogLogExpectation semiring computes (tests/semirings_test.py:305-312:
+    entropy = log_z + exp(log_sum - log_z)), here for weights of any sign.
+    Values only (no gradient)."""
+    log_z, mw, batch_dims = self._expectation(cache, frames, num_frames)
+    return self._home((log_z - mw).reshape(batch_dims), frames)
 
   def _forward_backward(self, cache: T, frames: torch.Tensor, num_frames: torch.Tensor):
     """log_z with gradients from the backward algorithm (lattices.py:498-642;

@@ -6,8 +6,11 @@ selects its HIP kernel by semiring identity (``Log``, ``MaxTropical``,
 ``Real``); the methods here are the per-element algebra used by the
 per-frame plugin methods (``FrameDependent.forward`` etc.). The tuple-valued
 semirings (``Expectation`` / ``LogLogExpectation``, ``Cartesian``) are host
-algebra only, as in the reference: the lattice's arc weights are single
-tensors, so ``RecognitionLattice`` rejects them.
+algebra, as in the reference, where the lattice's arc weights are single
+tensors. ``RecognitionLattice._forward`` takes ``LogLogExpectation`` with the
+pair weighted(w, -w) on every arc (the lattice entropy,
+``RecognitionLattice.entropy``) through the forward-backward marginals;
+``Cartesian`` and other ``Expectation`` instances it rejects.
 
 Differences from the reference, all bug fixes:
   * ``Log.plus`` / ``Log.sum`` have working, NaN-safe gradients (the

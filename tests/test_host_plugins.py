@@ -299,14 +299,17 @@ def test_cartesian():
   assert [v.item() for v in S.prod(c, axis=0)] == [2.0, 7.0]
 
 
-def test_tuple_semirings_rejected_by_lattice():
+def test_cartesian_rejected_by_lattice():
+  """Cartesian has no lattice path (the lattice's weights are single
+  tensors); LogLogExpectation has one (tests/test_entropy.py)."""
   ctx = lt.contexts.FullNGram(vocab_size=2, context_size=1)
   lat = lt.RecognitionLattice(context=ctx, alignment=lt.alignments.FrameDependent(),
                               weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
                               weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(
                                   torch.zeros([1, 3, 3])))
   with pytest.raises(NotImplementedError):
-    lat._forward(None, torch.zeros([1, 1, 1]), torch.ones([1]), lt.semirings.LogLogExpectation)
+    lat._forward(None, torch.zeros([1, 1, 1]), torch.ones([1]),
+                 lt.semirings.Cartesian(lt.semirings.Real, lt.semirings.MaxTropical))
 
 
 def test_joint_weight_fn_host_paths():
