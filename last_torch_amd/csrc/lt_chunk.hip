@@ -113,7 +113,7 @@ struct CkArgs {
   int b_ni, b_slots, b_off_ra, b_off_rb, b_off_ga, b_off_gb, b_gslots, b_gslot, b_off_buf;
   // phase C LDS carve
   int c_ni, c_off_ad, c_off_bd, c_off_an, c_off_bn, c_off_nw, c_off_fs, c_off_tab, c_off_cf,
-      c_off_buf, c_off_e, c_bytes;
+      c_off_buf, c_off_fl, c_off_e, c_bytes;
 };
 
 // lanes l and l ^ 32 combined (v_permlane32_swap: both halves get both)
@@ -1058,6 +1058,9 @@ LT_DEVINL void store_dw(void* dW, long long e, float v) {
 // per-frame scalars of phase C (log2): alpha's and beta's scales, the start
 // state's alpha and beta, W[0][0]
 constexpr int kFs = 8, kFsMa = 0, kFsA0 = 1, kFsMb = 2, kFsB0 = 3, kFsW00 = 4;
+// phase C's per-frame progress bits: den alpha / beta have passed the frame
+// (rows written, E_f read), numerator alpha / beta rows written
+constexpr int kFlA = 1, kFlB = 2, kFlNA = 4, kFlNB = 8, kFlAll = 15;
 
 template <bool BF16, int PPL, bool FULL>
 __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kernel(const CkArgs a) {
@@ -1137,6 +1140,18 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       if (tid + 64 * kMargWaves * i < nnw) nw[tid + 64 * kMargWaves * i] = g2[i];
   }
   if (tid < nt) fs[tid * kFs + kFsW00] = ldsw<BF16>(wch + tid * a.FB, 0) * kLog2e;
+  // per-frame progress bits for the marginal pass (kFl*), the frames in
+  // the order their inputs complete (middle first), a job counter
+  int* fl = (int*)(lds + a.c_off_fl);
+  int* ford = fl + a.L;
+  int* njob = ford + a.L;
+  if (tid < nt) {
+    fl[tid] = 0;
+    const int mid = (nt - 1) / 2;  // job j -> frames mid, mid+1, mid-1, mid+2, ...
+    const int k = (tid + 1) / 2;
+    ford[tid] = (tid & 1) ? mid + k : mid - k;
+  }
+  if (tid == 0) *njob = 0;
   __syncthreads();  // the gathers above read W; E overwrites it below
   // E in place, frame by frame: each thread's elements of a frame loaded
   // together (element-wise: no barrier between a thread's reads and stores)
@@ -1159,6 +1174,16 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   CK_STAMP(5);
   // every LDS load below is unconditional (clamped index, unused values
   // masked afterwards): a load under a branch would pay its full latency
+
+  // a recursion wave has passed frame f (its rows written, E_f read): one
+  // LDS atomic after its own LDS writes (in order within the wave)
+  auto mark = [&](int f, int bit) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_or(fl + f, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto mark_all = [&](int bit) {
+    for (int f = 0; f < nt; ++f) mark(f, bit);
+  };
 
   if (wave == 0 && !a.local && !LT_ABL(a, 4)) {
     // ---- den alpha in scaled linear space. Lane p in [1, V]: alpha[p] =
@@ -1220,6 +1245,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       const float sh = from_prev(ldexpf(sq, -ex), 0.f);
       al = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
+      mark(f, kFlA);
     }
   } else if (wave == 1 && !a.local && !LT_ABL(a, 4)) {
     // ---- den beta, the same scaled linear space; frame f gets beta_{f+1}.
@@ -1274,6 +1300,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       const float sh = from_prev(ldexpf(sj, -ex), 0.f);
       be = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
+      mark(f, kFlB);
     }
   } else if (wave == 2 && !LT_ABL(a, 8)) {
     // ---- num alpha (log2): al'[u] = al[u] + blank(u) (+) al[u-1] + arc(u)
@@ -1300,6 +1327,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
 #pragma unroll
       for (int r = 0; r < PPL; ++r) al[r] = nv[r];
       __builtin_amdgcn_wave_barrier();
+      mark(f, kFlNA);
     }
   } else if (wave == 3 && !LT_ABL(a, 8)) {
     // ---- num beta (log2); frame f gets beta_{f+1}
@@ -1327,9 +1355,11 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
 #pragma unroll
       for (int r = 0; r < PPL; ++r) be[r] = nv[r];
       __builtin_amdgcn_wave_barrier();
+      mark(f, kFlNB);
     }
+  } else {  // a recursion this chunk does not run (local / ablations): nothing to wait for
+    mark_all(wave == 0 ? kFlA : wave == 1 ? kFlB : wave == 2 ? kFlNA : kFlNB);
   }
-  __syncthreads();
   CK_STAMP(2);
 
   // ---- marginals, one wave per frame: den - num, each normalised by its
@@ -1350,7 +1380,22 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     bo[r] = boff[uc];
     lo[r] = max(loff[uc], 0);
   }
-  for (int f = LT_ABL(a, 16) ? nt : wave; f < nt; f += kMargWaves) {
+  // frames as jobs in the order their inputs complete (middle first): a
+  // wave done with its recursion takes the next job and waits for that
+  // frame's four bits, so the marginals overlap the longer recursions
+  for (;;) {
+    int jb = 0;
+    if (lane == 0) jb = __hip_atomic_fetch_add(njob, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    jb = __builtin_amdgcn_readfirstlane(jb);
+    if (jb >= nt || LT_ABL(a, 16)) break;
+    const int f = ford[jb];
+    for (;;) {
+      const int bits = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(fl + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if ((bits & kFlAll) == kFlAll) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     float* fb = eptr(f);  // E_f, then the frame's dW in place
     // numerator terms (log2)
     float sb[PPL], sl[PPL];
@@ -1540,6 +1585,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
     t->c_off_tab = off; off += al16(8LL * a->NPG + 4LL * a->U);
     t->c_off_cf = off; off += al16(4LL * L);
     t->c_off_buf = off; off += 4 * 64 * 4;
+    t->c_off_fl = off; off += al16(4LL * (2 * L + 1));
     t->c_off_e = off; off += bf16 ? al16(4LL * L * ((a->FR + 3) & ~3)) : 0;
     return off;
   };
