@@ -271,6 +271,28 @@ def chunk_len(B, T, U, V):
     L -= 1
 
 
+def loss_grad_design(B, T, U, V, n, C, device):
+  """(kernel names, description, design bytes per frame) of the design
+  lt_loss_grad dispatches to for this shape (lt_lattice.hip lt_loss_grad)."""
+  if _native.chunk_path(B, T, U, V, n, device):
+    L = chunk_len(B, T, U, V)
+    fuse_ab = B <= torch.cuda.get_device_properties(device).multi_processor_count
+    knames = ['ck_ab_kernel'] + ([] if fuse_ab else ['ck_combine_kernel']) + ['ck_marg_kernel']
+    design = (f'chunked two-level scan, L={L} frames per chunk (lt_chunk.hip: '
+              f"{' -> '.join(knames)})")
+    return knames, design, chunk_design_bytes(T, U, V, L)
+  ck_b = sum(algorithmic_bytes(T, U, V, C, checkpoints=True)[:2])
+  if _native.fused_path(B, T, U, V, n, device):
+    return ['pipe_kernel'], 'lt_loss_grad (fused pipe)', ck_b
+  if _native.prefer_checkpoints(B, device, (T, U, V, n, False)):
+    knames = ['pipe_kernel' if _native.pipe_path(B, T, U, V, n) else 'fwdbwd_kernel',
+              'marg_kernel']
+    return knames, ('checkpointing: alpha || beta recursions with checkpoints, then the '
+                    f"marginal pass ({' -> '.join(knames)})"), ck_b
+  return ['fwd_kernel', 'bwd_kernel'], 'recursion backward', sum(
+      algorithmic_bytes(T, U, V, C, checkpoints=False)[:2])
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
@@ -320,20 +342,9 @@ def main():
   value = cells_per_step * args.steps / wall
 
   fwd_b, bwd_b, survey_b = algorithmic_bytes(T, U, V, C, checkpoints=ckpt)
-  chunk = fused and _native.chunk_path(B, T, U, V, n)
   if fused:
     call_s = float(np.mean(fwd_ms)) * 1e-3
-    if chunk:
-      L = chunk_len(B, T, U, V)
-      fuse_ab = B <= torch.cuda.get_device_properties(device).multi_processor_count
-      knames = ['ck_ab_kernel'] + ([] if fuse_ab else ['ck_combine_kernel']) + ['ck_marg_kernel']
-      design = (f'chunked two-level scan, L={L} frames per chunk (lt_chunk.hip: '
-                f"{' -> '.join(knames)})")
-      design_b = chunk_design_bytes(T, U, V, L)
-    else:
-      knames = ['pipe_kernel'] if _native.fused_path(B, T, U, V, n, device) else ['lt_loss_grad']
-      design = 'lt_loss_grad (fused pipe)' if knames == ['pipe_kernel'] else 'lt_loss_grad'
-      design_b = fwd_b + bwd_b
+    knames, design, design_b = loss_grad_design(B, T, U, V, n, C, device)
     kernel = f"lt_loss_grad ({' + '.join(knames)})"
     kernels_ms = {'loss_grad': call_s * 1e3}
   else:
@@ -408,7 +419,8 @@ def main():
         'ms_per_call': call2,
         'hbm_frac_step': survey_b * 256 * T / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
         'frac_call': survey_b * 256 * T / (call2 * 1e-3) / 1e9 / HBM_PEAK_GBS,
-        'design': design if fused else ('checkpoints' if ckpt else 'recursion'),
+        'design': (loss_grad_design(256, T, U, V, n, C, device)[1] if fused else
+                   ('checkpoints' if ckpt else 'recursion')),
     }
     del W2
     torch.cuda.empty_cache()

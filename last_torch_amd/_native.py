@@ -271,22 +271,31 @@ def loss_backward(W, num_frames, labels, num_labels, log_z, num, alpha, alpha_nu
   return dW
 
 
-def chunk_path(batch, frames, labels, vocab_size, context_size):
+def chunk_path(batch, frames, labels, vocab_size, context_size, device=None):
   """Whether lt_loss_grad runs the chunked two-level scan (lt_chunk.hip) for
-  this shape; mirrors lt_impl::chunk_eligible. LT_CHUNK=0 turns it off."""
-  if os.environ.get('LT_CHUNK', '1') == '0':
+  this shape; mirrors lt_impl::chunk_preferred: an eligible shape and
+  5 * batch <= 3 * CUs (beyond that the frame-serial checkpointing design is
+  faster, tools/design_ab.py). LT_CHUNK=0 turns it off, LT_CHUNK=1 forces it
+  for any batch."""
+  env = os.environ.get('LT_CHUNK', '')
+  if env == '0':
     return False
   if context_size != 1 or not 1 <= vocab_size <= 32 or labels + 1 > 128 or frames < 1:
     return False
   C = vocab_size + 1
-  return batch * frames * C * C < 2 ** 31
+  if batch * frames * C * C >= 2 ** 31:
+    return False
+  if env == '1' or not torch.cuda.is_available():
+    return True
+  cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
+  return 5 * batch <= 3 * cus
 
 
 def fused_path(batch, frames, labels, vocab_size, context_size, device=None, bf16=False):
   """Whether lt_loss_grad runs as ONE fused pipe launch for this shape
   (mirrors lt_loss_grad: not the chunked path, checkpointing batch size, 2B
   below the CU count, pipe shape; LT_FUSED=0/1 forces the choice)."""
-  if chunk_path(batch, frames, labels, vocab_size, context_size):
+  if chunk_path(batch, frames, labels, vocab_size, context_size, device):
     return False
   cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
   env = os.environ.get('LT_FUSED', '')

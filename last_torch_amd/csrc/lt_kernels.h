@@ -1438,6 +1438,8 @@ int serial_loss(const lt_problem* pb, int local_norm, const void* W, const int32
                 void* dW, void* side, void* stream);
 // lt_chunk.hip: chunked two-level scan (bigram Log)
 bool chunk_eligible(const lt_problem* pb);
+// lt_loss_grad's choice: the chunked scan while it is the faster design
+bool chunk_preferred(const lt_problem* pb);
 int chunk_loss_grad(const lt_problem* pb, int local_norm, const void* W, const int32_t* num_frames,
                     const int32_t* labels, const int32_t* num_labels, float* loss, float* log_z,
                     float* num, void* dW, void* state, size_t state_bytes, void* scratch,

@@ -1120,7 +1120,7 @@ int lt_loss_grad_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_
   NGram g;
   int rc = check_problem(pb, &g);
   if (rc) return rc;
-  if (lt_impl::chunk_eligible(pb) && pb->max_frames > 0) {
+  if (lt_impl::chunk_preferred(pb) && pb->max_frames > 0) {
     size_t st = 0, sc = 0;
     if ((rc = lt_chunk_workspace_bytes(pb, local_norm, &st, &sc))) return rc;
     if (bytes) *bytes = ((st + 255) & ~(size_t)255) + sc;
@@ -1142,7 +1142,7 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
       (pb->max_labels > 0 && !labels))
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W) || misaligned(dW)) return fail(LT_EINVAL, "W/dW must be 16-byte aligned");
-  if (lt_impl::chunk_eligible(pb) && pb->max_frames > 0) {
+  if (lt_impl::chunk_preferred(pb) && pb->max_frames > 0) {
     // bigram: the chunked two-level scan (lt_chunk.hip), two launches (plus
     // the frame-serial pair, whose workgroups exit at once unless an
     // utterance is out of the fast path's range)

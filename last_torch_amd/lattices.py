@@ -88,7 +88,7 @@ class _LossFn(torch.autograd.Function):
     if not ctx.needs_input_grad[0]:
       return _native.loss_forward(W, nf, labels, nl, V, n, local, want_alpha=False)[0]
     B, T = W.shape[:2]
-    if _native.chunk_path(B, T, labels.shape[-1], V, n):
+    if _native.chunk_path(B, T, labels.shape[-1], V, n, W.device):
       loss, _, _, state = _native.chunk_forward(W, nf, labels, nl, V, n, local)
       ctx.mode = 'chunk'
       ctx.save_for_backward(W, nf, labels, nl, state)

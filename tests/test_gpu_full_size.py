@@ -4,7 +4,8 @@
   the bench step's launch (the chunked two-level scan, lt_chunk.hip) -- every
   utterance against the C oracle, plus size-independent properties
   (per-frame marginal sums, determinism, linearity in the incoming gradient).
-* north star: B=256 of the same shape (sampled utterances + properties).
+* north star: B=256 of the same shape (sampled utterances + properties), in
+  the design lt_loss_grad picks there and in the chunked scan forced.
 * cfg4: MaxTropical Viterbi at B=64, T=2000: labels and path weights
   bit-exact on every utterance.
 * cfg5: trigram (C = 1057) bf16 at B=32, T=1000, U=100: loss on a sample,
@@ -115,11 +116,17 @@ def test_cfg2_varlen_local_norm(cuda):
     assert (dW[pad] == 0).all()
 
 
-def test_north_star_b256(cuda):
+@pytest.mark.parametrize('force', ['', '1'])
+def test_north_star_b256(cuda, force, monkeypatch):
   """B=256 (the north-star shape): sampled utterances against the oracle and
-  the per-frame marginal sums of all of them."""
+  the per-frame marginal sums of all of them -- the design lt_loss_grad picks
+  there (the checkpointing pipe + marginal pass, what bench.py times) and the
+  chunked scan forced (LT_CHUNK=1)."""
   V, n = 32, 1
+  if force:
+    monkeypatch.setenv('LT_CHUNK', force)
   W, nf, lab, nl = _bench_inputs(256, 1000, 100, V, n, cuda, seed=99)
+  assert nat.chunk_path(256, 1000, 100, V, n) == bool(force)
   loss, lz, _, dW = nat.loss_grad(W, nf, lab, nl, V, n, False)
   s = _frame_sums(dW, nf)
   tol = 1e-5 + 2e-6 * lz.abs().double().clamp(min=1.0)[:, None]
