@@ -99,20 +99,25 @@ LT_DEVINL void store_unit(unsigned char* p, const float* v) {
     q.x = __float_as_uint(v[0]); q.y = __float_as_uint(v[1]);
     q.z = __float_as_uint(v[2]); q.w = __float_as_uint(v[3]);
   }
-  __builtin_nontemporal_store(q.x, (unsigned*)p);  // dW is written once
-  __builtin_nontemporal_store(q.y, (unsigned*)p + 1);
-  __builtin_nontemporal_store(q.z, (unsigned*)p + 2);
-  __builtin_nontemporal_store(q.w, (unsigned*)p + 3);
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  v4u qv = {q.x, q.y, q.z, q.w};
+  __builtin_nontemporal_store(qv, (v4u*)p);  // dW is written once: one 16-byte store
 }
 
 // One tile: F whole frames (small frames) or one slice of a frame.
 //   phase 0: the tile's W as 16-B units into registers; alpha/beta (+num)
-//            rows, the arc table and a zeroed numerator buffer into LDS
-//   phase 1: each numerator chain head sums its arc's marginals -> Sub[e]
-//            (one writer per element; its W element comes from L2, the tile
-//            was just streamed); den marginals in registers
-//   phase 2: dW = den - Sub, 16-B stores. Misaligned tiles / the tail go
-//            element by element.
+//            rows and the arc table into LDS (whole-frame tiles also zero a
+//            per-element numerator buffer)
+//   phase 1: den marginals in registers -> dW, 16-B stores from the tile's
+//            first 16-byte boundary (head and tail element by element).
+//            Whole-frame tiles (tpf == 1) subtract the numerator first: each
+//            chain head (one per lattice element the string uses) sums its
+//            arcs' marginals into the buffer (its W element from L2, the
+//            tile was just streamed).
+//   phase 2: frame slices (tpf > 1: trigram-size frames, where a buffer the
+//            size of the slice would cap the workgroups per CU): once the
+//            tile's own stores have completed, the chain heads rewrite their
+//            elements as den - num.
 template <bool BF16>
 LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   constexpr int VE = BF16 ? 8 : 4;  // elements per 16-byte unit
@@ -141,8 +146,15 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   const long long base = ((long long)b * a.T + t0) * FR + e_lo;  // tile is contiguous
   unsigned char* dWb = (unsigned char*)a.dW + base * ES;
   const unsigned char* Wb = a.W + base * ES;
-  const bool vec = ((base * ES) & 15) == 0;
-  const int nunits = vec ? E / VE : 0;
+  // 16-byte units from the first aligned element h0 of the tile (a trigram
+  // frame is 2 mod 16 bytes long, so most tiles start misaligned); the h0
+  // head elements and the tail go element by element
+  const int h0 = min(E, (int)(((16 - ((base * ES) & 15)) & 15) / ES));
+  const int nunits = (E - h0) / VE;
+  const int ntail = h0 + (E - h0 - nunits * VE);  // head + tail elements
+  auto tail_el = [&](int i) { return i < h0 ? i : i + nunits * VE; };
+  unsigned char* dWu = dWb + (long long)h0 * ES;   // unit u at dWu + 16 u
+  const unsigned char* Wu = Wb + (long long)h0 * ES;
   float gb = a.grad ? a.grad[b] : 1.f;
   const float lz = a.do_den ? a.log_z[b] : 0.f;
   const float nm = a.do_num ? a.num[b] : 0.f;
@@ -150,8 +162,8 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   const int Fl = max(0, min(Fh, nf - t0));  // live frames of the tile
   if (Fl == 0 || gb == 0.f) {                // padding (lattices.py:775-779) / unreachable
     const float z[VE] = {};
-    for (int u = tid; u < nunits; u += nthr) store_unit<BF16>(dWb + (long long)u * 16, z);
-    for (int e = nunits * VE + tid; e < E; e += nthr) stw<BF16>(a.dW, base + e, 0.f);
+    for (int u = tid; u < nunits; u += nthr) store_unit<BF16>(dWu + (long long)u * 16, z);
+    for (int i = tid; i < ntail; i += nthr) stw<BF16>(a.dW, base + tail_el(i), 0.f);
     return;
   }
   float* A = (float*)(lds + a.off_a);     // [F][C]
@@ -160,15 +172,16 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   float* BN = (float*)(lds + a.off_bn);   // [F][NP]
   int* aoff = (int*)(lds + a.off_arc);    // [NK] offsets, then [NK] links
   int* alink = aoff + NK;
-  float* Sub = (float*)(lds + a.off_sub); // [E] numerator marginals per element
   int* nbt = (int*)(lds + a.off_nb);      // [C] next_base (n >= 2)
+  float* Sub = (float*)(lds + a.off_sub); // tpf == 1: [E] numerator marginals per element
+  const bool dense = a.do_num && a.tpf == 1;
 
   // ---- phase 0
   uint4 wq[kMgUnits];
 #pragma unroll
   for (int r = 0; r < kMgUnits; ++r) {
     const int u = tid + r * 256;
-    if (u < nunits) wq[r] = *(const uint4*)(Wb + (long long)u * 16);
+    if (u < nunits) wq[r] = *(const uint4*)(Wu + (long long)u * 16);
   }
   const long long row0 = (long long)b * a.T + t0;
   // every row load in flight at once (a strided load -> LDS loop would wait
@@ -206,42 +219,42 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
       bool z;
       nbt[p] = next_base(g, p, &z);
     }
-  if (a.do_num) {
+  if (dense) {
     float4* S4 = (float4*)Sub;  // the region is padded to 16 bytes
     for (int e = tid; e < (E + 3) / 4; e += nthr) S4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
 
-  // ---- phase 1: numerator chains (deterministic: chain order = ascending k)
-  if (a.do_num) {
-    // chain i: head (el >= 0) of frame f, arc k; the heads' W elements (L2:
-    // the tile was just streamed) are gathered for NH rounds at once
-    auto head = [&](int i, int& f, int& k) {
-      f = (int)fdiv((unsigned)i, (unsigned)NK, a.mNK);
-      k = i - f * NK;
-      const int o = aoff[k];
-      if (!(alink[k] >> 30) || o < e_lo || o >= e_hi) return -1;
-      return f * Ew + o - e_lo;
-    };
-    auto chain = [&](int f, int k, float wv) {
-      float sacc = 0.f;
-      for (int kk = k; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
-        const int u = kk >> 1;
-        const float bn = BN[f * NP + ((kk & 1) ? u + 1 : u)];
-        sacc += lt_exp(AN[f * NP + u] + wv + bn - nm);
-      }
-      return gb * sacc;
-    };
-    constexpr int NH = 4;
-    const int nI = Fl * NK;
-    int hel[NH], hf[NH], hk[NH];
-    float hw[NH];
-#pragma unroll
-    for (int r = 0; r < NH; ++r) {
-      const int i = tid + r * 256;
-      hel[r] = i < nI ? head(i, hf[r], hk[r]) : -1;
-      if (hel[r] >= 0) hw[r] = ldw<BF16>(Wb, hel[r]);
+  // numerator chains (deterministic: chain order = ascending k): chain i's
+  // head (el >= 0) of frame f, arc k; the heads' W elements come from L2
+  // (the tile was just streamed), gathered for NH rounds at once
+  auto head = [&](int i, int& f, int& k) {
+    f = (int)fdiv((unsigned)i, (unsigned)NK, a.mNK);
+    k = i - f * NK;
+    const int o = aoff[k];
+    if (!(alink[k] >> 30) || o < e_lo || o >= e_hi) return -1;
+    return f * Ew + o - e_lo;
+  };
+  auto chain = [&](int f, int k, float wv) {
+    float sacc = 0.f;
+    for (int kk = k; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
+      const int u = kk >> 1;
+      const float bn = BN[f * NP + ((kk & 1) ? u + 1 : u)];
+      sacc += lt_exp(AN[f * NP + u] + wv + bn - nm);
     }
+    return gb * sacc;
+  };
+  constexpr int NH = 4;
+  const int nI = a.do_num ? Fl * NK : 0;
+  int hel[NH], hf[NH], hk[NH];
+  float hw[NH];
+#pragma unroll
+  for (int r = 0; r < NH; ++r) {
+    const int i = tid + r * 256;
+    hel[r] = i < nI ? head(i, hf[r], hk[r]) : -1;
+    if (hel[r] >= 0) hw[r] = ldw<BF16>(Wb, hel[r]);
+  }
+  if (dense) {  // whole frames: the chains' sums into Sub before the den pass
 #pragma unroll
     for (int r = 0; r < NH; ++r)
       if (hel[r] >= 0) Sub[hel[r]] = chain(hf[r], hk[r], hw[r]);
@@ -254,6 +267,13 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   // den marginals of the register units
   const bool den = a.do_den;
   const bool zero_next = g.n == 0, nb_table = g.n >= 2;
+  // den marginal of frame f's element el (within the frame) with weight w
+  auto den_el = [&](int f, int el, float w) {
+    const int p = (int)fdiv((unsigned)el, (unsigned)R, a.mR);
+    const int y = el - p * R;
+    const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
+    return gb * lt_exp(A[f * C + p] + w + Bt[f * C + q] - lz);
+  };
   float v[kMgUnits][VE];
 #pragma unroll
   for (int r = 0; r < kMgUnits; ++r) {
@@ -263,7 +283,7 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
     if (u < nunits && den) {
       float w[VE];
       unpack_unit<BF16>(wq[r], w);
-      const int e0 = u * VE;
+      const int e0 = h0 + u * VE;
       int f = a.tpf == 1 ? (int)fdiv((unsigned)e0, (unsigned)FR, a.mF) : 0;
       const int el0 = e_lo + e0 - f * Ew;
       int p = (int)fdiv((unsigned)el0, (unsigned)R, a.mR);
@@ -281,35 +301,47 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
       }
     }
   }
-  __syncthreads();
-
-  // ---- phase 2
+  if (dense) __syncthreads();
 #pragma unroll
   for (int r = 0; r < kMgUnits; ++r) {
     const int u = tid + r * 256;
     if (u < nunits) {
-      if (a.do_num) {
+      if (dense) {
 #pragma unroll
-        for (int c = 0; c < VE; ++c) v[r][c] -= Sub[u * VE + c];
+        for (int c = 0; c < VE; ++c) v[r][c] -= Sub[h0 + u * VE + c];
       }
-      store_unit<BF16>(dWb + (long long)u * 16, v[r]);
+      store_unit<BF16>(dWu + (long long)u * 16, v[r]);
     }
   }
-  // misaligned tile or tail: element by element
-  for (int e = nunits * VE + tid; e < E; e += nthr) {
+  // the head before the first 16-byte boundary and the tail: element by element
+  for (int i = tid; i < ntail; i += nthr) {
+    const int e = tail_el(i);
     const int f = a.tpf == 1 ? (int)fdiv((unsigned)e, (unsigned)FR, a.mF) : 0;
-    const int el = e_lo + e - f * Ew;
     float x = 0.f;
     if (f < Fl) {
-      if (den) {
-        const int p = (int)fdiv((unsigned)el, (unsigned)R, a.mR);
-        const int y = el - p * R;
-        const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
-        x = gb * lt_exp(A[f * C + p] + ldw<BF16>(Wb, e) + Bt[f * C + q] - lz);
-      }
-      if (a.do_num) x -= Sub[e];
+      if (den) x = den_el(f, e_lo + e - f * Ew, ldw<BF16>(Wb, e));
+      if (dense) x -= Sub[e];
     }
     stw<BF16>(a.dW, base + e, x);
+  }
+  if (!a.do_num || dense) return;
+
+  // ---- phase 2 (frame slices): the chain heads rewrite their elements as
+  // den - num once the tile's own stores have completed in every wave (same
+  // workgroup, same address, in order)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  auto rewrite = [&](int el, int f, int k, float wv) {
+    const float d = den ? den_el(f, el - f * Ew + e_lo, wv) : 0.f;
+    stw<BF16>(a.dW, base + el, d - chain(f, k, wv));
+  };
+#pragma unroll
+  for (int r = 0; r < NH; ++r)
+    if (hel[r] >= 0) rewrite(hel[r], hf[r], hk[r], hw[r]);
+  for (int i = tid + NH * 256; i < nI; i += nthr) {
+    int f, k;
+    const int el = head(i, f, k);
+    if (el >= 0) rewrite(el, f, k, ldw<BF16>(Wb, el));
   }
 }
 
@@ -647,7 +679,6 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
   const long long emax_cap = 256LL * units * (16 / es);
   m->B = pb->batch; m->T = pb->max_frames; m->U = pb->max_labels; m->FR = (int)FR; m->g = g;
   m->do_den = do_den; m->do_num = do_num;
-  long long emax;
   if (FR <= emax_cap) {
     m->tpf = 1;
     long long period = 1;  // frames per 16-byte-aligned run
@@ -658,7 +689,6 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
     m->F = F;
     m->TS = (int)FR;
     m->tiles = std::max(1, ceil_div(pb->max_frames, F));
-    emax = F * FR;
   } else {
     m->tpf = (int)((FR + emax_cap - 1) / emax_cap);
     long long ts = (FR + m->tpf - 1) / m->tpf;
@@ -667,7 +697,6 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
     m->tpf = (int)((FR + m->TS - 1) / m->TS);
     m->F = 1;
     m->tiles = std::max(1, pb->max_frames * m->tpf);
-    emax = m->TS;
   }
   m->mR = magic_of((unsigned)R);
   m->mF = magic_of((unsigned)FR);
@@ -680,7 +709,9 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
   m->off_an = off; off += do_num ? al16(4LL * m->F * NP) : 0;
   m->off_bn = off; off += do_num ? al16(4LL * m->F * NP) : 0;
   m->off_arc = off; off += do_num ? al16(8LL * NK) : 0;
-  m->off_sub = off; off += do_num ? al16(4 * emax) : 0;
+  // whole-frame tiles keep a dense numerator buffer (one float per element);
+  // frame slices (tpf > 1, large frames) rewrite the chain heads instead
+  m->off_sub = off; off += (do_num && m->tpf == 1) ? al16(4LL * m->F * FR) : 0;
   m->lds_bytes = std::max(off, 16);
   if (off > kLdsMax) return fail(LT_EUNSUPPORTED, "marginal tile exceeds LDS");
   *grid = (long long)pb->batch * m->tiles;

@@ -23,6 +23,8 @@ ws = torch.empty([_native.loss_grad_workspace_bytes(W, V, 1, U, False)], dtype=t
                  device='cuda')
 names = {0: 'all', 1: 'B: no den', 2: 'B: no num', 3: 'B: nothing', 4: 'C: no den rec',
          8: 'C: no num rec', 16: 'C: no marginals', 28: 'C: DMA + tables only', 31: 'A only (+B/C shells)'}
+if os.environ.get('DBGS'):
+  names = {int(x): f'dbg {x}' for x in os.environ['DBGS'].split(',')}
 for dbg, name in names.items():
   os.environ['LT_CK_DBG'] = str(dbg)
   for _ in range(3):

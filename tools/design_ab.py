@@ -13,7 +13,7 @@ from last_torch_amd import _native  # noqa: E402
 
 T, U, V = 1000, 100, 32
 N = int(os.environ.get('N', 20))
-designs = {'chunk': {}, 'serial': {'LT_CHUNK': '0'}}
+designs = {'chunk': {'LT_CHUNK': '1'}, 'serial': {'LT_CHUNK': '0'}}
 for B in [int(x) for x in os.environ.get('BS', '64,128,192,256').split(',')]:
   g = torch.Generator(device='cuda')
   g.manual_seed(0)
