@@ -20,6 +20,9 @@ cat $OUT/bench.json
 step trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 bench.py --steps 10 \
   --no-north-star --no-joint --cpu-utts 0 --cpu-ref-utts 0 > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 1; }
+step trace b256
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace256 -o run -- python3 bench.py --batch 256 \
+  --steps 10 --no-north-star --no-joint --cpu-utts 0 --cpu-ref-utts 0 > $OUT/trace256.log 2>&1 || { tail -20 $OUT/trace256.log; exit 1; }
 step pmc fetch
 N=5 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
   python3 tools/chunk_prof.py > $OUT/pmc_fetch.log 2>&1 || { tail -20 $OUT/pmc_fetch.log; exit 1; }
