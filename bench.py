@@ -149,9 +149,12 @@ def joint_step_leg(T, U, V, n, device, B=64, F=256, H=512, reps=5):
   nf = torch.full([B], T, device=device)
   labels = torch.randint(1, V + 1, [B, U], device=device)
   nl = torch.full([B], U, device=device)
-  out = {'batch': B, 'frames': T, 'labels': U, 'features': F, 'hidden': H}
-  for name, fused in (('producer', True), ('pytorch_hidden', False)):
+  out = {'batch': B, 'frames': T, 'labels': U, 'features': F, 'hidden': H,
+         'producer_precision': 'fp32-faithful split-bf16 products (JointWeightFn default)'}
+  for name, fused, prec in (('producer', True, 'fp32'), ('producer_bf16', True, 'bf16'),
+                            ('pytorch_hidden', False, 'fp32')):
     wfn.fused = fused
+    wfn.precision = prec
     for _ in range(3):
       lat(frames=frames, num_frames=nf, labels=labels, num_labels=nl).sum().backward()
     torch.cuda.synchronize()

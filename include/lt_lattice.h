@@ -301,6 +301,18 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
                      const float* ctx_proj, const float* frame_proj, const float* out_weight,
                      const float* out_bias, void* W, int32_t weight_dtype, void* workspace,
                      size_t workspace_bytes, void* stream);
+/* lt_joint_weights with the product precision chosen: LT_JOINT_BF16 (as
+ * lt_joint_weights) or LT_JOINT_SPLIT, the fp32-faithful mode for the
+ * reference's fp32 JointWeightFn: the tanh values and out_weight each split
+ * into bf16 hi + lo, hi*hi + hi*lo + lo*hi summed in fp32 (about 16 mantissa
+ * bits per product, as lt_joint_weights_backward); out_weight then takes
+ * twice the LDS (4 * out_dim * (hidden + 8) bytes <= 128 KB). */
+#define LT_JOINT_BF16 0
+#define LT_JOINT_SPLIT 1
+int lt_joint_weights_ex(int64_t rows, int32_t num_states, int32_t hidden, int32_t out_dim,
+                        const float* ctx_proj, const float* frame_proj, const float* out_weight,
+                        const float* out_bias, void* W, int32_t weight_dtype, int32_t precision,
+                        void* workspace, size_t workspace_bytes, void* stream);
 
 /* Adjoint of lt_joint_weights (JointWeightFn's parameter gradients; the
  * reference gets them from autograd through weight_fns.py:174-227): with

@@ -80,6 +80,8 @@ _SIG = {
                                          ctypes.POINTER(ctypes.c_size_t)],
     'lt_joint_weights': [ctypes.c_int64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P,
                          ctypes.c_size_t, _P],
+    'lt_joint_weights_ex': [ctypes.c_int64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _I32,
+                            _P, ctypes.c_size_t, _P],
     'lt_joint_weights_backward_workspace_bytes': [ctypes.c_int64, _I32, _I32, _I32,
                                                   ctypes.POINTER(ctypes.c_size_t)],
     'lt_joint_weights_backward': [ctypes.c_int64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P,
@@ -523,10 +525,17 @@ def table_viterbi(graph, W, num_frames, label_convention):
   return labels, weight
 
 
-def joint_weights(ctx_proj, frame_proj, out_weight, out_bias, dtype=torch.float32):
-  """lt_joint_weights: W [..., C, R] = out_bias + tanh(ctx_proj[c] + frame_proj[...]) @
-  out_weight^T on the matrix cores (bf16 products, fp32 sums); frame_proj
-  [..., H], ctx_proj [C, H], out_weight [R, H], out_bias [R] (fp32)."""
+JOINT_BF16, JOINT_SPLIT = 0, 1  # lt_joint_weights_ex precisions (include/lt_lattice.h)
+
+
+def joint_weights(ctx_proj, frame_proj, out_weight, out_bias, dtype=torch.float32,
+                  precision='fp32'):
+  """lt_joint_weights_ex: W [..., C, R] = out_bias + tanh(ctx_proj[c] + frame_proj[...]) @
+  out_weight^T on the matrix cores, fp32 sums; frame_proj [..., H], ctx_proj
+  [C, H], out_weight [R, H], out_bias [R] (fp32). precision 'fp32': split-bf16
+  products (LT_JOINT_SPLIT, fp32-faithful); 'bf16': one bf16 product."""
+  if precision not in ('fp32', 'bf16'):
+    raise ValueError(f"lt_joint_weights: precision must be 'fp32' or 'bf16', got {precision!r}")
   for name, t in (('ctx_proj', ctx_proj), ('frame_proj', frame_proj),
                   ('out_weight', out_weight), ('out_bias', out_bias)):
     if not t.is_cuda:
@@ -543,9 +552,10 @@ def joint_weights(ctx_proj, frame_proj, out_weight, out_bias, dtype=torch.float3
   _check(lib().lt_joint_weights_workspace_bytes(pf.shape[0], C, H, ctypes.byref(nbytes)),
          'lt_joint_weights_workspace_bytes')
   ws = torch.empty([(nbytes.value + 15) // 16 * 4], dtype=torch.float32, device=pf.device)
-  _check(lib().lt_joint_weights(pf.shape[0], C, H, R, _ptr(pc), _ptr(pf), _ptr(wo), _ptr(bo),
-                                _ptr(W), LT_DTYPE_BF16 if dtype == torch.bfloat16 else LT_DTYPE_F32,
-                                _ptr(ws), ws.numel() * 4, _stream()), 'lt_joint_weights')
+  _check(lib().lt_joint_weights_ex(pf.shape[0], C, H, R, _ptr(pc), _ptr(pf), _ptr(wo), _ptr(bo),
+                                   _ptr(W), LT_DTYPE_BF16 if dtype == torch.bfloat16 else LT_DTYPE_F32,
+                                   JOINT_SPLIT if precision == 'fp32' else JOINT_BF16,
+                                   _ptr(ws), ws.numel() * 4, _stream()), 'lt_joint_weights_ex')
   return W
 
 

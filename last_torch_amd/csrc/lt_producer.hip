@@ -22,8 +22,10 @@
 //                            (blocks that exceed LDS)
 //   joint_backward_kernel    d_wo, d_pf, d_pc (+ bias) per 32-frame block
 //   joint_reduce_kernel      fixed-order sum of the per-workgroup partials
-// Wo and the hidden values enter the forward products as bf16; the backward
-// uses split-bf16 products; all sums are fp32.
+// Wo and the hidden values enter the forward products as bf16
+// (LT_JOINT_BF16) or split-bf16 (LT_JOINT_SPLIT: hi + lo each, three
+// products, fp32-faithful); the backward uses split-bf16 products; all sums
+// are fp32.
 #include "lt_kernels.h"
 
 namespace {
@@ -72,6 +74,63 @@ LT_DEVINL f32x2 exp2x(f32x2 x) {  // e^{2x}
   return f32x2{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
 }
 
+LT_DEVINL void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+  u32x4 h, l;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const f32x2 x = {v[2 * p], v[2 * p + 1]};
+    const unsigned hp = pk_bf16(x);
+    const f32x2 xh = {__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
+    h[p] = hp;
+    l[p] = pk_bf16(x - xh);
+  }
+  hi = __builtin_bit_cast(bf16x8, h);
+  lo = __builtin_bit_cast(bf16x8, l);
+}
+
+LT_DEVINL f32x16 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+// One K step (16 hidden units) of a hidden tile against one or two Wo
+// column tiles. tp: the lane's 8 tanh values (fp32). SP (split-bf16, the
+// precision of lt_joint_weights_ex's LT_JOINT_SPLIT): tanh = hi + lo and
+// Wo = hi + lo in bf16, hi*hi + hi*lo + lo*hi on the matrix cores (about 16
+// mantissa bits, fp32 sums); else one bf16 product.
+template <bool SP, bool TWO>
+LT_DEVINL void joint_kstep(const f32x2 (&tp)[4], const unsigned short* w0, const unsigned short* w1,
+                           const unsigned short* w0l, const unsigned short* w1l, f32x16& acc0,
+                           f32x16& acc1) {
+  if constexpr (SP) {
+    const float v[8] = {tp[0].x, tp[0].y, tp[1].x, tp[1].y, tp[2].x, tp[2].y, tp[3].x, tp[3].y};
+    bf16x8 ah, al;
+    split8(v, ah, al);
+    acc0 = mfma3(ah, al, *(const bf16x8*)w0, *(const bf16x8*)w0l, acc0);
+    if (TWO) acc1 = mfma3(ah, al, *(const bf16x8*)w1, *(const bf16x8*)w1l, acc1);
+  } else {
+    const u32x4 t = {pk_bf16(tp[0]), pk_bf16(tp[1]), pk_bf16(tp[2]), pk_bf16(tp[3])};
+    const bf16x8 af = __builtin_bit_cast(bf16x8, t);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)w0, acc0, 0, 0, 0);
+    if (TWO) acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)w1, acc1, 0, 0, 0);
+  }
+}
+
+// Wo [R, H] fp32 -> LDS rows of HP bf16: hi, and for SP the residual lo
+// (wo - hi) in a second block of R * HP (WL elements after the first)
+template <bool SP>
+LT_DEVINL void stage_wo(const float* wo, unsigned short* w, int R, int H, int HP, int WL, int tid,
+                        int nthr) {
+  for (int i = tid; i < R * H; i += nthr) {
+    const int y = i / H, hh = i - y * H;
+    const float v = wo[i];
+    const unsigned short hi = f2bf(v);
+    w[y * HP + hh] = hi;
+    if (SP) w[WL + y * HP + hh] = f2bf(v - __uint_as_float((unsigned)hi << 16));
+  }
+}
+
 // e^{2x} of both projections, and the direct-path flag (rows * H and C * H
 // values, float4 per thread).
 __global__ __launch_bounds__(256) void joint_exp_kernel(const JArgs a, float* ec, float* ef,
@@ -94,15 +153,13 @@ __global__ __launch_bounds__(256) void joint_exp_kernel(const JArgs a, float* ec
 
 // One wave: a 32-row tile of the flattened (f, c) rows against one or two
 // 32-column tiles of y (TWO: R > 32), K = H in steps of 16.
-template <bool OBF16, bool TWO>
+template <bool OBF16, bool TWO, bool SP>
 __global__ __launch_bounds__(256) void joint_weights_kernel(const JArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned short wol[];  // [R][H + 8] bf16
+  extern __shared__ __attribute__((aligned(16))) unsigned short wol[];  // [R][H + 8] bf16 (x2: SP)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, R = a.R, C = a.C, HP = H + 8;  // padded rows: no LDS bank conflicts
-  for (int i = tid; i < R * H; i += blockDim.x) {
-    const int y = i / H, h = i - y * H;
-    wol[y * HP + h] = f2bf(a.wo[i]);
-  }
+  const int WL = R * HP;  // SP: the lo block's offset
+  stage_wo<SP>(a.wo, wol, R, H, HP, WL, tid, blockDim.x);
   __syncthreads();
   const bool split = *a.big == 0;
   const long long M = a.rows * C;
@@ -114,6 +171,8 @@ __global__ __launch_bounds__(256) void joint_weights_kernel(const JArgs a) {
   // columns past R read row R - 1 (valid) and are never stored
   const unsigned short* w0 = wol + (v0 ? y0 : R - 1) * HP + hk;
   const unsigned short* w1 = wol + (v1 ? y1 : R - 1) * HP + hk;
+  const unsigned short* w0l = w0 + WL;
+  const unsigned short* w1l = w1 + WL;
   for (long long tile = (long long)blockIdx.x * 4 + wave; tile < ntile;
        tile += (long long)gridDim.x * 4) {
     const long long m = tile * 32 + r;
@@ -128,14 +187,11 @@ __global__ __launch_bounds__(256) void joint_weights_kernel(const JArgs a) {
       for (int k0 = 0; k0 < H; k0 += 16) {
         const float4 c0 = *(const float4*)(pc + k0), c1 = *(const float4*)(pc + k0 + 4);
         const float4 f0 = *(const float4*)(pf + k0), f1 = *(const float4*)(pf + k0 + 4);
-        const u32x4 t = {pk_bf16(tanh_from_exp(f32x2{c0.x, c0.y} * f32x2{f0.x, f0.y})),
-                         pk_bf16(tanh_from_exp(f32x2{c0.z, c0.w} * f32x2{f0.z, f0.w})),
-                         pk_bf16(tanh_from_exp(f32x2{c1.x, c1.y} * f32x2{f1.x, f1.y})),
-                         pk_bf16(tanh_from_exp(f32x2{c1.z, c1.w} * f32x2{f1.z, f1.w}))};
-        const bf16x8 af = __builtin_bit_cast(bf16x8, t);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w0 + k0), acc0, 0, 0, 0);
-        if (TWO)
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w1 + k0), acc1, 0, 0, 0);
+        const f32x2 tp[4] = {tanh_from_exp(f32x2{c0.x, c0.y} * f32x2{f0.x, f0.y}),
+                             tanh_from_exp(f32x2{c0.z, c0.w} * f32x2{f0.z, f0.w}),
+                             tanh_from_exp(f32x2{c1.x, c1.y} * f32x2{f1.x, f1.y}),
+                             tanh_from_exp(f32x2{c1.z, c1.w} * f32x2{f1.z, f1.w})};
+        joint_kstep<SP, TWO>(tp, w0 + k0, w1 + k0, w0l + k0, w1l + k0, acc0, acc1);
       }
     } else {
       const float* pc = a.pc + (long long)c * H + hk;
@@ -144,14 +200,11 @@ __global__ __launch_bounds__(256) void joint_weights_kernel(const JArgs a) {
       for (int k0 = 0; k0 < H; k0 += 16) {
         const float4 c0 = *(const float4*)(pc + k0), c1 = *(const float4*)(pc + k0 + 4);
         const float4 f0 = *(const float4*)(pf + k0), f1 = *(const float4*)(pf + k0 + 4);
-        const u32x4 t = {pk_bf16(tanh_from_exp(exp2x(f32x2{c0.x + f0.x, c0.y + f0.y}))),
-                         pk_bf16(tanh_from_exp(exp2x(f32x2{c0.z + f0.z, c0.w + f0.w}))),
-                         pk_bf16(tanh_from_exp(exp2x(f32x2{c1.x + f1.x, c1.y + f1.y}))),
-                         pk_bf16(tanh_from_exp(exp2x(f32x2{c1.z + f1.z, c1.w + f1.w})))};
-        const bf16x8 af = __builtin_bit_cast(bf16x8, t);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w0 + k0), acc0, 0, 0, 0);
-        if (TWO)
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w1 + k0), acc1, 0, 0, 0);
+        const f32x2 tp[4] = {tanh_from_exp(exp2x(f32x2{c0.x + f0.x, c0.y + f0.y})),
+                             tanh_from_exp(exp2x(f32x2{c0.z + f0.z, c0.w + f0.w})),
+                             tanh_from_exp(exp2x(f32x2{c1.x + f1.x, c1.y + f1.y})),
+                             tanh_from_exp(exp2x(f32x2{c1.z + f1.z, c1.w + f1.w}))};
+        joint_kstep<SP, TWO>(tp, w0 + k0, w1 + k0, w0l + k0, w1l + k0, acc0, acc1);
       }
     }
     // C/D: column y = lane & 31 (+32), row (i & 3) + 8 (i >> 2) + 4 (lane >> 5)
@@ -165,27 +218,25 @@ __global__ __launch_bounds__(256) void joint_weights_kernel(const JArgs a) {
   }
 }
 
-template <bool OBF16>
+template <bool OBF16, bool SP>
 const void* pick(bool two) {
-  return two ? (const void*)joint_weights_kernel<OBF16, true>
-             : (const void*)joint_weights_kernel<OBF16, false>;
+  return two ? (const void*)joint_weights_kernel<OBF16, true, SP>
+             : (const void*)joint_weights_kernel<OBF16, false, SP>;
 }
 
 // Frame-block form (used when a block fits LDS): a workgroup stages 32
 // frames' e^{2 pf} (or pf on the direct path) in LDS once and its waves walk
 // the context states, so the per-tile operands come from LDS plus one
 // broadcast row of e^{2 pc}; the row-tile form above re-reads both per tile.
-template <bool OBF16, bool TWO>
+template <bool OBF16, bool TWO, bool SP>
 __global__ __launch_bounds__(1024) void joint_weights_fb_kernel(const JArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned short wfl[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int H = a.H, R = a.R, C = a.C, HP = H + 8, FS = H + 4;
-  float* fb = (float*)(wfl + ((R * HP + 7) & ~7));  // [32][H + 4] fp32
+  const int WL = (R * HP + 7) & ~7;                           // SP: the lo block's offset
+  float* fb = (float*)(wfl + (SP ? 2 : 1) * WL);  // [32][H + 4] fp32
   float* crow = fb + 32 * FS + wave * H;             // [waves][H] fp32
-  for (int i = tid; i < R * H; i += blockDim.x) {
-    const int y = i / H, hh = i - y * H;
-    wfl[y * HP + hh] = f2bf(a.wo[i]);
-  }
+  stage_wo<SP>(a.wo, wfl, R, H, HP, WL, tid, blockDim.x);
   const bool csplit = *a.big == 0;  // every |pc| <= kSplitMax (the pre-pass's flag)
   const int rows = (int)a.rows;  // < 2^31 / H (host check)
   const int nblk = (rows + 31) / 32;
@@ -195,6 +246,8 @@ __global__ __launch_bounds__(1024) void joint_weights_fb_kernel(const JArgs a) {
   const float b0 = v0 ? a.bias[y0] : 0.f, b1 = v1 ? a.bias[y1] : 0.f;
   const unsigned short* w0 = wfl + (v0 ? y0 : R - 1) * HP + hk;
   const unsigned short* w1 = wfl + (v1 ? y1 : R - 1) * HP + hk;
+  const unsigned short* w0l = w0 + WL;
+  const unsigned short* w1l = w1 + WL;
   const int h4 = H / 4;
   for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
     __syncthreads();  // Wo staged / previous block's reads done
@@ -249,28 +302,22 @@ __global__ __launch_bounds__(1024) void joint_weights_fb_kernel(const JArgs a) {
         for (int k0 = 0; k0 < H; k0 += 16) {
           const float4 c0 = *(const float4*)(cr + k0), c1 = *(const float4*)(cr + k0 + 4);
           const float4 f0 = *(const float4*)(fr + k0), f1 = *(const float4*)(fr + k0 + 4);
-          const u32x4 t = {pk_bf16(tanh_from_exp(f32x2{c0.x, c0.y} * f32x2{f0.x, f0.y})),
-                           pk_bf16(tanh_from_exp(f32x2{c0.z, c0.w} * f32x2{f0.z, f0.w})),
-                           pk_bf16(tanh_from_exp(f32x2{c1.x, c1.y} * f32x2{f1.x, f1.y})),
-                           pk_bf16(tanh_from_exp(f32x2{c1.z, c1.w} * f32x2{f1.z, f1.w}))};
-          const bf16x8 af = __builtin_bit_cast(bf16x8, t);
-          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w0 + k0), acc0, 0, 0, 0);
-          if (TWO)
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w1 + k0), acc1, 0, 0, 0);
+          const f32x2 tp[4] = {tanh_from_exp(f32x2{c0.x, c0.y} * f32x2{f0.x, f0.y}),
+                               tanh_from_exp(f32x2{c0.z, c0.w} * f32x2{f0.z, f0.w}),
+                               tanh_from_exp(f32x2{c1.x, c1.y} * f32x2{f1.x, f1.y}),
+                               tanh_from_exp(f32x2{c1.z, c1.w} * f32x2{f1.z, f1.w})};
+          joint_kstep<SP, TWO>(tp, w0 + k0, w1 + k0, w0l + k0, w1l + k0, acc0, acc1);
         }
       } else {
 #pragma unroll 2
         for (int k0 = 0; k0 < H; k0 += 16) {
           const float4 c0 = *(const float4*)(cr + k0), c1 = *(const float4*)(cr + k0 + 4);
           const float4 f0 = *(const float4*)(fr + k0), f1 = *(const float4*)(fr + k0 + 4);
-          const u32x4 t = {pk_bf16(tanh_from_exp(exp2x(f32x2{c0.x + f0.x, c0.y + f0.y}))),
-                           pk_bf16(tanh_from_exp(exp2x(f32x2{c0.z + f0.z, c0.w + f0.w}))),
-                           pk_bf16(tanh_from_exp(exp2x(f32x2{c1.x + f1.x, c1.y + f1.y}))),
-                           pk_bf16(tanh_from_exp(exp2x(f32x2{c1.z + f1.z, c1.w + f1.w})))};
-          const bf16x8 af = __builtin_bit_cast(bf16x8, t);
-          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w0 + k0), acc0, 0, 0, 0);
-          if (TWO)
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, *(const bf16x8*)(w1 + k0), acc1, 0, 0, 0);
+          const f32x2 tp[4] = {tanh_from_exp(exp2x(f32x2{c0.x + f0.x, c0.y + f0.y})),
+                               tanh_from_exp(exp2x(f32x2{c0.z + f0.z, c0.w + f0.w})),
+                               tanh_from_exp(exp2x(f32x2{c1.x + f1.x, c1.y + f1.y})),
+                               tanh_from_exp(exp2x(f32x2{c1.z + f1.z, c1.w + f1.w}))};
+          joint_kstep<SP, TWO>(tp, w0 + k0, w1 + k0, w0l + k0, w1l + k0, acc0, acc1);
         }
       }
       // C/D: column y = lane & 31 (+32), row = frame (i & 3) + 8 (i >> 2) + 4 half
@@ -286,14 +333,16 @@ __global__ __launch_bounds__(1024) void joint_weights_fb_kernel(const JArgs a) {
   }
 }
 
-template <bool OBF16>
+template <bool OBF16, bool SP>
 const void* pick_fb(bool two) {
-  return two ? (const void*)joint_weights_fb_kernel<OBF16, true>
-             : (const void*)joint_weights_fb_kernel<OBF16, false>;
+  return two ? (const void*)joint_weights_fb_kernel<OBF16, true, SP>
+             : (const void*)joint_weights_fb_kernel<OBF16, false, SP>;
 }
 
-long long fb_lds(int H, int R, int nw) {  // Wo bf16, the frame block, a context row per wave
-  return 2LL * (((long long)R * (H + 8) + 7) & ~7LL) + 4LL * 32 * (H + 4) + 4LL * nw * H;
+// Wo bf16 (hi, and lo for SP), the frame block, a context row per wave
+long long fb_lds(int H, int R, int nw, bool sp) {
+  return (sp ? 4LL : 2LL) * (((long long)R * (H + 8) + 7) & ~7LL) + 4LL * 32 * (H + 4) +
+         4LL * nw * H;
 }
 
 // waves per frame-block workgroup: the fewest in [4, 16] that give the
@@ -325,11 +374,23 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
                      const float* ctx_proj, const float* frame_proj, const float* out_weight,
                      const float* out_bias, void* W, int32_t weight_dtype, void* workspace,
                      size_t workspace_bytes, void* stream) {
+  return lt_joint_weights_ex(rows, num_states, hidden, out_dim, ctx_proj, frame_proj, out_weight,
+                             out_bias, W, weight_dtype, LT_JOINT_BF16, workspace, workspace_bytes,
+                             stream);
+}
+
+int lt_joint_weights_ex(int64_t rows, int32_t num_states, int32_t hidden, int32_t out_dim,
+                        const float* ctx_proj, const float* frame_proj, const float* out_weight,
+                        const float* out_bias, void* W, int32_t weight_dtype, int32_t precision,
+                        void* workspace, size_t workspace_bytes, void* stream) {
   if (rows < 0 || num_states < 1 || hidden < 1 || out_dim < 1)
     return lt_impl::set_error(LT_EINVAL, "lt_joint_weights: bad sizes");
+  if (precision != LT_JOINT_BF16 && precision != LT_JOINT_SPLIT)
+    return lt_impl::set_error(LT_EINVAL, "lt_joint_weights: precision must be LT_JOINT_BF16 or LT_JOINT_SPLIT");
+  const bool sp = precision == LT_JOINT_SPLIT;
   if (hidden % 16 || out_dim > 64)
     return lt_impl::set_error(LT_EUNSUPPORTED, "lt_joint_weights: needs hidden % 16 == 0, V+1 <= 64");
-  const long long lds = 2LL * out_dim * (hidden + 8);
+  const long long lds = (sp ? 4LL : 2LL) * out_dim * (hidden + 8);
   if (lds > 128 * 1024)
     return lt_impl::set_error(LT_EUNSUPPORTED, "lt_joint_weights: output projection exceeds LDS");
   if (rows == 0) return LT_OK;
@@ -354,7 +415,7 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
   hipError_t e = hipMemsetAsync(big, 0, sizeof(int), st);
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   const int fnw = fb_waves(num_states);
-  const long long lfb = fb_lds(hidden, out_dim, fnw);
+  const long long lfb = fb_lds(hidden, out_dim, fnw, sp);
   const bool use_fb = lfb <= 160 * 1024 && hidden <= 1024 && rows * (long long)hidden < (1LL << 31);
   {
     // the frame-block kernel forms e^{2 pf} itself: the pre-pass then covers pc only
@@ -370,7 +431,8 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
   void* args[] = {&a};
   if (use_fb) {
     // frame-block form: one workgroup of fnw waves per CU
-    const void* k = bf ? pick_fb<true>(two) : pick_fb<false>(two);
+    const void* k = sp ? (bf ? pick_fb<true, true>(two) : pick_fb<false, true>(two))
+                       : (bf ? pick_fb<true, false>(two) : pick_fb<false, false>(two));
     if (lfb > 64 * 1024) {
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfb);
       if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
@@ -383,7 +445,8 @@ int lt_joint_weights(int64_t rows, int32_t num_states, int32_t hidden, int32_t o
   const long long tiles = (rows * num_states + 31) / 32;
   const long long want = (tiles + 3) / 4;
   const int grid = (int)std::min<long long>(want, 4LL * cus);  // persistent: Wo loaded once per WG
-  const void* k = bf ? pick<true>(two) : pick<false>(two);
+  const void* k = sp ? (bf ? pick<true, true>(two) : pick<false, true>(two))
+                     : (bf ? pick<true, false>(two) : pick<false, false>(two));
   if (lds > 64 * 1024) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
@@ -424,31 +487,11 @@ struct JBArgs {
   int C, H, R;
 };
 
-LT_DEVINL void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
-  u32x4 h, l;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const f32x2 x = {v[2 * p], v[2 * p + 1]};
-    const unsigned hp = pk_bf16(x);
-    const f32x2 xh = {__uint_as_float(hp << 16), __uint_as_float(hp & 0xffff0000u)};
-    h[p] = hp;
-    l[p] = pk_bf16(x - xh);
-  }
-  hi = __builtin_bit_cast(bf16x8, h);
-  lo = __builtin_bit_cast(bf16x8, l);
-}
-
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 // 8 bf16: p[0..3] and p[8..11] (8-byte aligned)
 LT_DEVINL bf16x8 tpair(const unsigned short* p) {
   const bf16x4 a = *(const bf16x4*)p, b = *(const bf16x4*)(p + 8);
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
-LT_DEVINL f32x16 mfma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 acc) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
 
 template <int KB, bool TWO, int NW>  // KB = ceil(R / 16) K blocks of gw; TWO: R > 32; NW waves

@@ -92,13 +92,13 @@ class _JointWeightsFn(torch.autograd.Function):
   # forward / setup_context split: torch.func transforms (the per-frame
   # weight_vjp_fn of RecognitionLattice._backward) accept only this form
   @staticmethod
-  def forward(pc, pf, wo, bias, chunk):
+  def forward(pc, pf, wo, bias, chunk, precision):
     from last_torch_amd import _native
-    return _native.joint_weights(pc, pf, wo, bias)
+    return _native.joint_weights(pc, pf, wo, bias, precision=precision)
 
   @staticmethod
   def setup_context(ctx, inputs, output):
-    pc, pf, wo, _, chunk = inputs
+    pc, pf, wo, _, chunk, _ = inputs
     ctx.save_for_backward(pc, pf, wo)
     ctx.chunk = chunk
 
@@ -110,7 +110,7 @@ class _JointWeightsFn(torch.autograd.Function):
     R = wo.shape[0]
     if _native.joint_weights_backward_supported(C, H, R, pf.numel() // H):
       dpc, dpf, dwo, dbias = _native.joint_weights_backward(pc, pf, wo, gW)
-      return dpc, dpf, dwo, dbias, None
+      return dpc, dpf, dwo, dbias, None, None
     pf2 = pf.reshape(-1, H)
     g2 = gW.reshape(-1, C, R).float()
     dpc = torch.zeros_like(pc)
@@ -123,7 +123,7 @@ class _JointWeightsFn(torch.autograd.Function):
       dh = torch.matmul(g, wo) * (1.0 - hid * hid)
       dpc += dh.sum(0)
       dpf[s:s + ctx.chunk] = dh.sum(1)
-    return dpc, dpf.reshape(pf.shape), dwo, g2.sum((0, 1)), None
+    return dpc, dpf.reshape(pf.shape), dwo, g2.sum((0, 1)), None, None
 
 
 class JointWeightFn(WeightFn[torch.Tensor]):
@@ -131,15 +131,21 @@ class JointWeightFn(WeightFn[torch.Tensor]):
   shared-emb / shared-rnn weight function (weight_fns.py:174-227).
 
   ``fused`` (default): on a ROCm device, with all context states at once,
-  the logits come from the lt_joint_weights matrix-core kernel (bf16
-  products, fp32 sums; hidden_size a multiple of 16, vocab_size < 64)."""
+  the logits come from the lt_joint_weights matrix-core kernel (fp32 sums;
+  hidden_size a multiple of 16, vocab_size < 64). ``precision`` 'fp32'
+  (default, faithful to the reference's fp32 layers): split-bf16 products,
+  about 16 mantissa bits each, as the backward; 'bf16': one bf16 product
+  (faster, ~2^-8 relative per product)."""
 
   def __init__(self, vocab_size: int, hidden_size: int, device=None, fused: bool = True,
-               backward_chunk: int = 16384):
+               backward_chunk: int = 16384, precision: str = 'fp32'):
     super().__init__()
+    if precision not in ('fp32', 'bf16'):
+      raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
     self.vocab_size = vocab_size
     self.hidden_size = hidden_size
     self.fused = fused
+    self.precision = precision
     self.backward_chunk = backward_chunk
     self.context_projection = nn.LazyLinear(hidden_size, bias=False, device=device)
     self.frame_projection = nn.LazyLinear(hidden_size, bias=False, device=device)
@@ -163,7 +169,7 @@ class JointWeightFn(WeightFn[torch.Tensor]):
       pf = self.frame_projection(frame)
       wo = torch.cat([self.to_blank.weight, self.to_vocab.weight], 0)
       bias = torch.cat([self.to_blank.bias, self.to_vocab.bias], 0)
-      return _JointWeightsFn.apply(pc, pf, wo, bias, self.backward_chunk)
+      return _JointWeightsFn.apply(pc, pf, wo, bias, self.backward_chunk, self.precision)
     blank, lexical = self.forward(cache, frame)
     return torch.cat([blank[..., None], lexical], dim=-1)
 

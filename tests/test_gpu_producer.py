@@ -1,15 +1,21 @@
 """GPU tests of the joint weight function's matrix-core producer
-(lt_joint_weights, lt_producer.hip).
+(lt_joint_weights / lt_joint_weights_ex, lt_producer.hip; SURVEY.md 8(f)
+rank 1).
 
 Numerics reference: a plain PyTorch fp32 restatement of JointWeightFn
-(weight_fns.py:174-227): W = bias + tanh(pc[c] + pf[f]) @ wo^T. The kernel
-feeds the tanh values and wo to the matrix cores as bf16 (8 significant
-bits) and sums in fp32, so each logit may differ from fp32 by the bf16
-rounding of its products: |dW| <= 2^-7 * (|tanh| @ |wo|^T) + 1e-5 (written
-in `_tol`). Against a bf16-emulating reference (the same roundings, fp32
-sums) the difference is summation order plus the rare bf16 rounding flip
-of a tanh value: checked on the mean. The backward is fp32 (recomputed
-tanh): against torch autograd of the fp32 formula, 1e-4 relative.
+(weight_fns.py:174-227): W = bias + tanh(pc[c] + pf[f]) @ wo^T.
+* precision 'bf16' feeds the tanh values and wo to the matrix cores as bf16
+  (8 significant bits) and sums in fp32, so each logit may differ from fp32
+  by the bf16 rounding of its products: |dW| <= 2^-7 * (|tanh| @ |wo|^T) +
+  1e-5 (`_tol`). Against a bf16-emulating reference (the same roundings,
+  fp32 sums) the difference is summation order plus the rare bf16 rounding
+  flip of a tanh value: checked on the mean.
+* precision 'fp32' (the default, LT_JOINT_SPLIT) splits both into bf16
+  hi + lo and sums hi*hi + hi*lo + lo*hi: each product carries ~2^-17
+  relative error, so |dW| <= 2^-14 * (|tanh| @ |wo|^T) + 1e-5 (`_tol32`),
+  i.e. fp32 autograd parity at 1e-4 of the logits' scale.
+The backward is fp32 (recomputed tanh): against torch autograd of the fp32
+formula, 1e-4 relative.
 """
 import pytest
 import torch
@@ -36,6 +42,10 @@ def _tol(pc, pf, wo):
       *pf.shape[:-1], pc.shape[0], wo.shape[0]) + 1e-5
 
 
+def _tol32(pc, pf, wo):
+  return _tol(pc, pf, wo) * 2.0 ** -7 + 1e-5
+
+
 def _inputs(cuda, lead, C, H, R, scale=1.0, seed=0):
   g = torch.Generator(device=cuda)
   g.manual_seed(seed)
@@ -57,7 +67,7 @@ def _inputs(cuda, lead, C, H, R, scale=1.0, seed=0):
 ])
 def test_forward_vs_torch(cuda, lead, C, H, R):
   pc, pf, wo, bias = _inputs(cuda, lead, C, H, R)
-  W = nat.joint_weights(pc, pf, wo, bias)
+  W = nat.joint_weights(pc, pf, wo, bias, precision='bf16')
   torch.cuda.synchronize()
   ref, _ = _ref(pc, pf, wo, bias)
   assert W.shape == ref.shape
@@ -66,10 +76,33 @@ def test_forward_vs_torch(cuda, lead, C, H, R):
   assert float((W - emu).abs().mean()) < 1e-4 * max(1.0, float(emu.abs().mean()))
 
 
+@pytest.mark.parametrize('lead,C,H,R', [
+    ((4, 7), 33, 64, 33),     # bigram V=32 (two column tiles)
+    ((3, 5), 1, 16, 6),       # n = 0, V = 5
+    ((1, 1), 33, 16, 64),     # full two tiles
+    ((5, 13), 21, 512, 33),   # H = 512 (the bench hidden size), ragged rows
+    ((37,), 33, 32, 33),      # rows * C not a multiple of 32
+    ((2, 3), 5, 848, 33),     # frame block exceeds LDS: the row-tile kernel
+])
+@pytest.mark.parametrize('scale', [1.0, 30.0])  # split e^{2a} e^{2b} / direct e^{2(a+b)}
+def test_forward_fp32_faithful(cuda, lead, C, H, R, scale):
+  """precision 'fp32' (split-bf16 products): fp32 parity at 2^-14 of the
+  logits' product scale, ~128x tighter than the bf16 bound."""
+  pc, pf, wo, bias = _inputs(cuda, lead, C, H, R, scale=scale)
+  W = nat.joint_weights(pc, pf, wo, bias, precision='fp32')
+  torch.cuda.synchronize()
+  ref, _ = _ref(pc, pf, wo, bias)
+  assert W.shape == ref.shape
+  err = (W - ref).abs()
+  assert bool((err <= _tol32(pc, pf, wo)).all()), float((err / _tol32(pc, pf, wo)).max())
+  Wb = nat.joint_weights(pc, pf, wo, bias, precision='bf16')
+  assert float(err.mean()) * 16 < float((Wb - ref).abs().mean()) + 1e-7
+
+
 @pytest.mark.parametrize('scale', [8.0, 30.0])  # split path (|x| <= 40) / direct path
 def test_forward_bf16_output_and_saturation(cuda, scale):
   pc, pf, wo, bias = _inputs(cuda, (3, 11), 33, 64, 33, scale=scale)  # tanh saturates
-  W = nat.joint_weights(pc, pf, wo, bias, dtype=torch.bfloat16)
+  W = nat.joint_weights(pc, pf, wo, bias, dtype=torch.bfloat16, precision='bf16')
   ref, _ = _ref(pc, pf, wo, bias)
   assert W.dtype == torch.bfloat16
   assert bool(torch.isfinite(W.float()).all())
@@ -81,17 +114,17 @@ def test_split_and_direct_paths_agree(cuda):
   """One projection above 40 switches the whole call to the direct path; the
   other rows must come out as on the split path up to bf16 rounding of tanh."""
   pc, pf, wo, bias = _inputs(cuda, (2, 9), 33, 64, 33, scale=3.0)
-  W = nat.joint_weights(pc, pf, wo, bias)
+  W = nat.joint_weights(pc, pf, wo, bias, precision='bf16')
   pf2 = pf.clone()
   pf2[1, 8, 0] = 50.0
-  W2 = nat.joint_weights(pc, pf2, wo, bias)
+  W2 = nat.joint_weights(pc, pf2, wo, bias, precision='bf16')
   torch.cuda.synchronize()
   assert bool(((W[:1] - W2[:1]).abs() <= _tol(pc, pf[:1], wo)).all())
   ref, _ = _ref(pc, pf2, wo, bias)
   assert bool(((W2 - ref).abs() <= _tol(pc, pf2, wo)).all())
   pf3 = pf.clone()
   pf3[0, 0, 0] = float('nan')
-  W3 = nat.joint_weights(pc, pf3, wo, bias)
+  W3 = nat.joint_weights(pc, pf3, wo, bias, precision='bf16')
   torch.cuda.synchronize()
   assert bool(torch.isnan(W3[0, 0]).all()) and bool(torch.isfinite(W3[1]).all())
 
@@ -127,7 +160,7 @@ def test_backward_vs_torch(cuda, lead, C, H, R, path):
   leaves = [t.clone().requires_grad_(True) for t in (pc, pf, wo, bias)]
   if path == 'kernel':
     assert nat.joint_weights_backward_supported(C, H, R)
-    W = lt.weight_fns._JointWeightsFn.apply(*leaves, 37)
+    W = lt.weight_fns._JointWeightsFn.apply(*leaves, 37, 'fp32')
     (W * g).sum().backward()
   else:
     grads = _torch_backward(pc, pf, wo, g, chunk=37)
@@ -170,16 +203,19 @@ def test_backward_errors_and_empty(cuda):
     nat.joint_weights_backward(pc, pf, wo, torch.zeros([2, 3, 33, 33], device=cuda))
 
 
-def test_joint_weight_fn_in_lattice(cuda):
+@pytest.mark.parametrize('precision,rtol', [('fp32', 1e-4), ('bf16', 2e-2)])
+def test_joint_weight_fn_in_lattice(cuda, precision, rtol):
   """RecognitionLattice with SharedEmbCacher + JointWeightFn: the fused
-  producer and the PyTorch path give the same loss within the bf16 product
-  tolerance, and gradients reach every parameter."""
+  producer and the PyTorch fp32 path give the same loss (1e-4 relative with
+  the default fp32-faithful products, the bf16 product tolerance with
+  precision='bf16'), and gradients reach every parameter."""
   torch.manual_seed(0)
   V, n, H, B, T, U = 8, 1, 32, 3, 12, 4
   ctx = lt.contexts.FullNGram(vocab_size=V, context_size=n)
   cacher = lt.weight_fns.SharedEmbCacher(num_context_states=V + 1, embedding_size=16,
                                          device=cuda)
-  fused = lt.weight_fns.JointWeightFn(vocab_size=V, hidden_size=H, device=cuda)
+  fused = lt.weight_fns.JointWeightFn(vocab_size=V, hidden_size=H, device=cuda,
+                                      precision=precision)
   lat = lt.RecognitionLattice(context=ctx, alignment=lt.alignments.FrameDependent(),
                               weight_fn_cacher_factory=lambda _: cacher,
                               weight_fn_factory=lambda _: fused)
@@ -195,7 +231,8 @@ def test_joint_weight_fn_in_lattice(cuda):
     p.grad = None
   loss_ref = lat(frames=frames, num_frames=nf, labels=labels, num_labels=nl)
   loss_ref.sum().backward()
-  assert torch.allclose(loss, loss_ref, rtol=2e-2, atol=2e-2), (loss, loss_ref)
+  assert torch.allclose(loss, loss_ref, rtol=rtol, atol=rtol), (loss, loss_ref)
   for k, p in fused.named_parameters():
     assert torch.isfinite(grads[k]).all() and grads[k].abs().sum() > 0, k
-    assert torch.allclose(grads[k], p.grad, rtol=5e-2, atol=5e-2 * float(p.grad.abs().max())), k
+    gt = 10 * rtol if precision == 'fp32' else 5e-2
+    assert torch.allclose(grads[k], p.grad, rtol=gt, atol=gt * float(p.grad.abs().max())), k

@@ -41,8 +41,10 @@ def main():
       return loss
 
     out = {'B': B, 'T': T, 'U': U, 'V': V, 'C': V + 1, 'F': F, 'H': H}
-    for name, fused in (('producer', True), ('pytorch_hidden', False)):
+    for name, fused, prec in (('producer', True, 'fp32'), ('producer_bf16', True, 'bf16'),
+                              ('pytorch_hidden', False, 'fp32')):
       wfn.fused = fused
+      wfn.precision = prec
       for _ in range(3):  # lazy layers, allocator, clocks
         step()
       torch.cuda.synchronize()

@@ -40,7 +40,8 @@ def main():
     def torch_fwd():
       return torch.matmul(torch.tanh(pc[None, None] + pf[:, :, None, :]), wo.t()) + bias
 
-    kern = timeit(lambda: nat.joint_weights(pc, pf, wo, bias))
+    kern = timeit(lambda: nat.joint_weights(pc, pf, wo, bias, precision='fp32'))
+    kern_bf16 = timeit(lambda: nat.joint_weights(pc, pf, wo, bias, precision='bf16'))
     # some |ctx projection| > 40: every block takes the direct e^{2(a+b)} path
     pc_big = pc.clone()
     pc_big.view(-1)[0] = 100.0
@@ -51,7 +52,7 @@ def main():
     gW = torch.randn([B, T, C, R], device='cuda')
 
     def kern_fb():
-      W = weight_fns._JointWeightsFn.apply(*leaves, int(os.environ.get("CHUNK", 16384)))
+      W = weight_fns._JointWeightsFn.apply(*leaves, int(os.environ.get("CHUNK", 16384)), 'fp32')
       torch.autograd.backward(W, gW)
 
     def torch_fb():
@@ -64,7 +65,8 @@ def main():
     rfb = timeit(torch_fb, reps=3)
     flops = 2.0 * B * T * C * R * H
     print(json.dumps({'H': H, 'B': B, 'T': T, 'C': C, 'R': R,
-                      'producer_fwd_ms': kern, 'producer_fwd_direct_ms': kern_direct,
+                      'producer_fwd_ms': kern, 'producer_fwd_bf16_ms': kern_bf16,
+                      'producer_fwd_direct_ms': kern_direct,
                       'torch_fwd_ms': ref,
                       'producer_bwd_kernel_ms': kbwd, 'producer_fwd_bwd_ms': kfb, 'torch_fwd_bwd_ms': rfb,
                       'producer_fwd_TFLOPs': flops / (kern * 1e-3) / 1e12,
