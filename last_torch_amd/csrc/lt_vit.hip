@@ -12,8 +12,9 @@
 //   h = 1 sources p = 17..32 (terms 18..33); the halves meet through one
 //   permlane32 swap (the earlier half wins ties). The start state 0 has only
 //   its blank self loop. alpha sits in LDS (one write, five b128 reads per
-//   frame); the frame's weights stream into registers three frames ahead
-//   through one buffer resource per frame (no address arithmetic). The
+//   frame); the frames stream into an LDS ring three frames ahead by
+//   LDS-DMA (5 contiguous 1 KiB wave instructions a frame, counted vmcnt
+//   waits) and each lane reads its 19 weights from LDS beside alpha. The
 //   alpha chain takes the maximum by a max3 tree; the backpointer (the
 //   first term equal to it) is formed beside the chain.
 // Backpointers: one byte per (frame, state), the term index, as the generic
@@ -44,17 +45,15 @@ LT_DEVINL float max3_raw(float x, float y, float z) {
   return r;
 }
 
-// the frame's weights stream into registers kAhead frames ahead (19 loads a
-// frame: kAhead x 19 stays inside vmcnt's 63), through one buffer resource
-// per frame (no address arithmetic)
+// the frames stream through an LDS ring kAhead frames ahead (kSlots slots:
+// the frame in use and the kAhead in flight)
 constexpr int kAhead = 3;
+constexpr int kSlots = kAhead + 1;
 
 template <bool BF16>
-LT_DEVINL float vld(__amdgpu_buffer_rsrc_t r, int voff) {
-  if constexpr (BF16)
-    return __uint_as_float((unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, voff, 0, 0) << 16);
-  else
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+LT_DEVINL float vlds(const unsigned char* fr, int off) {
+  if constexpr (BF16) return __uint_as_float((unsigned)*(const unsigned short*)(fr + off) << 16);
+  else return *(const float*)(fr + off);
 }
 
 struct VitFrame {
@@ -64,20 +63,9 @@ struct VitFrame {
 };
 
 template <bool BF16, bool FULL>
-LT_DEVINL void vit_load(const unsigned char* Wf, int bytes, int vb, int vself, int R,
-                        VitFrame& f) {
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Wf, (short)0, bytes, 0x00020000);
-  constexpr int es = BF16 ? 2 : 4;
-#pragma unroll
-  for (int m = 0; m < kHalf; ++m) f.w[m] = vld<BF16>(r, vb + m * (FULL ? 33 : R) * es);
-  f.self = vld<BF16>(r, vself);
-  f.w00 = vld<BF16>(r, 0);
-}
-
-template <bool BF16, bool FULL>
 __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
   __shared__ __attribute__((aligned(16))) float s_al[2][40];
+  __shared__ __attribute__((aligned(16))) unsigned char s_ring[kSlots][5 * 1024];
   const int b = blockIdx.x, lane = threadIdx.x;
   const int j = lane & 31, h = lane >> 5;
   const int V = FULL ? 32 : a.V, R = FULL ? 33 : a.R, C = V + 1;
@@ -91,7 +79,6 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
   const int vb = (p0 * R + min(q, V)) * es;
   const int vself = min(q, V) * R * es;
   const long long fbytes = (long long)C * R * es;
-  const unsigned char* W0 = a.W + (long long)b * a.T * fbytes;
   // backpointer stores through a buffer resource too: a per-frame 64-bit
   // address would make the compiler drain vmcnt when it recycles the pair
   const __amdgpu_buffer_rsrc_t bpr =
@@ -102,17 +89,42 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
   float a0 = 0.f;  // alpha[0] (only its blank self loop reaches it)
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
-  VitFrame fr[kAhead];
-  auto fptr = [&](int t) { return W0 + (long long)min(t, max(nf - 1, 0)) * fbytes; };
-  auto fb = [&](int t) { return (int)((nf - min(t, max(nf - 1, 0))) * fbytes); };
+  // frames stream into an LDS ring by LDS-DMA kAhead frames ahead (ni
+  // contiguous 1 KiB wave instructions a frame instead of 19 column loads)
+  const int ni = (int)(((fbytes + 30) / 16 + 63) / 64);
+  const long long goff0 = (long long)b * a.T * fbytes;
+  auto fclamp = [&](int t) { return min(t, max(nf - 1, 0)); };
+  auto issue = [&](int t) {  // frame t (clamped) -> slot t % kSlots
+    const long long off = goff0 + (long long)fclamp(t) * fbytes;
+    const long long a0 = off & ~15LL;
+    const int n16 = (int)((off + fbytes - a0 + 15) >> 4);
+    const unsigned dst = lds_base_addr(&s_ring[t % kSlots][0]);
+    for (int i = 0; i < ni; ++i) {
+      int g = lane + 64 * i;
+      g = g < n16 ? g : n16 - 1;
+      glds16(a.W + a0 + 16LL * g, dst + 1024u * i);
+    }
+  };
+  // frame t's DMA has landed: ring issues and one backpointer store a step,
+  // in issue order (vmcnt counts both, in order)
+  auto wait_frame = [&](int t) { wait_vmcnt((kAhead - 1) * ni + min(t, kAhead)); };
   if (nf > 0) {
-#pragma unroll
-    for (int d = 0; d < kAhead; ++d) vit_load<BF16, FULL>(fptr(d), fb(d), vb, vself, R, fr[d]);
+    for (int d = 0; d < kAhead; ++d) issue(d);
   }
-  auto step = [&](VitFrame& F, int t) {
+  auto step = [&](int t) {
     if (t >= nf) return;  // the last round's spare steps
     const float* acur = s_al[t & 1];
     float* anxt = s_al[(t + 1) & 1];
+    wait_frame(t);
+    VitFrame F;
+    {
+      const unsigned char* fr =
+          &s_ring[t % kSlots][0] + ((goff0 + (long long)fclamp(t) * fbytes) & 15);
+#pragma unroll
+      for (int m = 0; m < kHalf; ++m) F.w[m] = vlds<BF16>(fr, vb + m * (FULL ? 33 : R) * es);
+      F.self = vlds<BF16>(fr, vself);
+      F.w00 = vlds<BF16>(fr, 0);
+    }
     // the sources' alpha: five b128 reads of the lane's half
     float al[20];
 #pragma unroll
@@ -130,7 +142,7 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
     const float xs = aq + F.self;
     const float w00 = F.w00;
     const int ib = h ? 18 : 1;  // term index of x[0]
-    if (!LT_ABL(a, 1)) vit_load<BF16, FULL>(fptr(t + kAhead), fb(t + kAhead), vb, vself, R, F);
+    if (!LT_ABL(a, 1)) issue(t + kAhead);
     // the value: a max3 tree over the lane's terms, the halves by one
     // permlane32 swap (the alpha chain waits on nothing else)
     float mx = max3_raw(h ? x[16] : xs, x[0], x[1]);
@@ -163,10 +175,7 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
   };
-  for (int t0 = 0; t0 < nf; t0 += kAhead) {
-#pragma unroll
-    for (int d = 0; d < kAhead; ++d) step(fr[d], t0 + d);
-  }
+  for (int t = 0; t < nf; ++t) step(t);
   // the distance: (+)_q alpha_T[q] in MaxTropical, the first maximum
   const float* af = s_al[nf & 1];
   float r = lane < C ? af[aslot(lane)] : -kInf;
