@@ -67,7 +67,11 @@ constexpr int kGrp = 7;         // frames per numerator group (band offsets 0..k
 #define LT_AB_WAVES 3
 #endif
 constexpr int kAbWaves = LT_AB_WAVES;  // ck_ab_kernel: waves per SIMD its registers allow
-constexpr unsigned kSpinMax = 1u << 20;  // phase B's bound on polls without progress (~1 s)
+constexpr unsigned kSpinMax = 1u << 20;
+constexpr int kWalkSlots = 3;                    // phase B: den walk record ring depth (LDS)
+constexpr int kRecNi = (4 * kRec + 1023) / 1024;  // LDS-DMA wave instructions per record
+constexpr int kWalkSlot = kRecNi * 1024;         // bytes per ring slot
+constexpr int kWalkLds = 2 * kWalkSlots * kWalkSlot;  // dynamic LDS of the walk launches  // phase B's bound on polls without progress (~1 s)
 // record layout (floats): [0, 1152) X^T rows: rec[i * 36 + j] = X[i][j] =
 // P_scaled[j][i] (start core state j -> end core state i); [1152, 1184)
 // per-start-state (column) power-of-two scales ej (int); [1184, 1216) the
@@ -617,6 +621,18 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
 // fast path's range (bad). A bounded spin: on timeout (a placement that never
 // schedules the producer) ok = 0, the range is taken as covered, and the
 // utterance goes to the frame-serial kernels.
+// A flag poll and the agent-scope acquire as inline asm, each ending in
+// its own vmcnt(0): the compiler sees no memory instruction of its own in a
+// walk's step loop, so it has no reason to drain the walk's in-flight
+// LDS-DMA record loads at every step (it did for the builtin forms).
+LT_DEVINL unsigned poll_flag(const unsigned* p) {
+  unsigned v;
+  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+LT_DEVINL void acquire_agent() {
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+}
 struct ChunkReady {
   const unsigned* f;
   int lo, hi, Kl, ok, bad;
@@ -636,13 +652,12 @@ struct ChunkReady {
     k = min(k, Kl - 1);
     for (unsigned spins = 0; k > hi; ++spins) {
       const int x = hi + 1 + lane;
-      const unsigned v = x < Kl ? __hip_atomic_load((const gu32*)(f + x), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const unsigned v = poll_flag(f + min(x, Kl - 1)) & (x < Kl ? ~0u : 0u);
       int c;
       take(v, lane, &c);
       if (c) {
         hi += c;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        acquire_agent();
       } else if (spins > kSpinMax) {
         timeout();
       } else {
@@ -654,13 +669,12 @@ struct ChunkReady {
     k = max(k, 0);
     for (unsigned spins = 0; k < lo; ++spins) {
       const int x = lo - 1 - lane;
-      const unsigned v = x >= 0 ? __hip_atomic_load((const gu32*)(f + x), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const unsigned v = poll_flag(f + max(x, 0)) & (x >= 0 ? ~0u : 0u);
       int c;
       take(v, lane, &c);
       if (c) {
         lo -= c;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        acquire_agent();
       } else if (spins > kSpinMax) {
         timeout();
       } else {
@@ -849,12 +863,31 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
   const int Kl = (nf + a.L - 1) / a.L;  // live chunks
   const int V = a.V, C = a.C, CP = a.CP;
   const int nl = a.nlab[b];
-  const float* rec0 = a.rec + (long long)b * a.K * kRec;
-
   if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
   CK_WSTAMP(2 * wave);
   ChunkReady rd(a.ready + (long long)b * a.K, Kl);
+
+  // den walks: the records stream through a ring of kWalkSlots LDS slots
+  // per wave by LDS-DMA (1 KiB contiguous per instruction), issued
+  // kWalkSlots steps ahead; each step reads its record from LDS. (Records
+  // gathered straight into registers -- a row per lane for alpha, a column
+  // for beta -- stalled each step about as long as the rest of the step.)
+  extern __shared__ __attribute__((aligned(16))) unsigned char ck_dyn[];
+  const unsigned ring_a = lds_base_addr(ck_dyn) + (unsigned)(wave * kWalkSlots * kWalkSlot);
+  const unsigned char* ring = ck_dyn + wave * kWalkSlots * kWalkSlot;
+  auto issue_rec = [&](int k, int n) {  // step n's record k (clamped to [0, Kl)) -> slot n mod kWalkSlots
+    const int kc = min(max(k, 0), Kl - 1);
+    dma_issue((const unsigned char*)a.rec, ((long long)b * a.K + kc) * (kRec * 4), kRec * 4,
+              ring_a + (unsigned)((n % kWalkSlots) * kWalkSlot), kRecNi, lane);
+  };
+  // step n's record has landed: the ring's issues and each step's one
+  // boundary-row store, in issue order (vmcnt counts both, in order; the
+  // flag polls drain it themselves)
+  auto wait_rec = [&](int n) {
+    wait_vmcnt(n < kWalkSlots ? kRecNi * (kWalkSlots - 1) + n : (kRecNi + 1) * kWalkSlots - kRecNi);
+  };
+  auto slot = [&](int n) { return (const float*)(ring + (n % kWalkSlots) * kWalkSlot); };
 
   if (wave == 0 && !a.local && !LT_ABL(a, 1)) {
     // ---- den alpha across chunks (lattices.py:379-496 in chunk steps)
@@ -862,9 +895,14 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
     float al = lane == 0 ? 0.f : -kInf;  // lane p: alpha[p]
     float* dst = a.abd + (long long)b * (a.K + 1) * CP;
     if (lane < C) dst[lane] = al;
-    RecAlpha rr[2];
-    auto rec_ptr = [&](int k) { return rec0 + (long long)min(k, Kl - 1) * kRec; };
-    auto step = [&](RecAlpha& R, int k, bool reload) {
+    if (Kl > 0) {
+      rd.ensure_fwd(kWalkSlots - 1, lane);
+      for (int n = 0; n < kWalkSlots; ++n) issue_rec(n, n);
+    }
+    for (int k = 0; k < Kl; ++k) {
+      wait_rec(k);
+      RecAlpha R;
+      load_rec_alpha(slot(k), lane, V, R);
       const float x = lane < C ? al + R.sc : -kInf;
       const float M = safe_max(wmax_u(x));
       const float av = lane < C ? lt_exp(x - M) : 0.f;
@@ -888,27 +926,16 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
       }
       s0 = __builtin_fmaf(R.rt, bc[32], s0);
       const float cs = R.cs, pi = R.pi;
-      // the record's last use: its successor two chunks on loads from here
-      if (reload && !LT_ABL(a, 512)) {
-        rd.ensure_fwd(k + 2, lane);
-        load_rec_alpha(rec_ptr(k + 2), lane, V, R);
-      }
+      // the slot's last read has returned: its next record goes in
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      rd.ensure_fwd(k + kWalkSlots, lane);
+      issue_rec(k + kWalkSlots, k + kWalkSlots);
       const float nq = M + cs + lt_log(s0 + s1);  // lane i < 32: alpha'[i+1]
       const float n0 = first_lane(al) + pi + cs;
       const float sh = from_prev(nq, -kInf);
       al = lane == 0 ? n0 : (lane < C ? sh : -kInf);
       if (lane < C) dst[(long long)(k + 1) * CP + lane] = al;
       __builtin_amdgcn_wave_barrier();
-    };
-    if (Kl > 0) {
-      rd.ensure_fwd(1, lane);
-      load_rec_alpha(rec_ptr(0), lane, V, rr[0]);
-      load_rec_alpha(rec_ptr(1), lane, V, rr[1]);
-      for (int k0 = 0; k0 < (Kl & ~1); k0 += 2) {
-        step(rr[0], k0, true);
-        step(rr[1], k0 + 1, true);
-      }
-      if (Kl & 1) step(rr[0], Kl - 1, false);
     }
     // log_z = (+)_q alpha_T[q] (lattices.py:496)
     const float x = lane < C ? al : -kInf;
@@ -922,9 +949,15 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
     float be = lane < C ? 0.f : -kInf;  // lane p: beta[p]
     float* dst = a.bbd + (long long)b * (a.K + 1) * CP;
     if (lane < C) dst[(long long)Kl * CP + lane] = be;
-    RecBeta rr[2];
-    auto rec_ptr = [&](int k) { return rec0 + (long long)max(k, 0) * kRec; };
-    auto step = [&](RecBeta& R, int k, bool reload) {
+    if (Kl > 0) {
+      rd.ensure_bwd(Kl - kWalkSlots, lane);
+      for (int n = 0; n < kWalkSlots; ++n) issue_rec(Kl - 1 - n, n);
+    }
+    for (int n = 0; n < Kl; ++n) {
+      const int k = Kl - 1 - n;
+      wait_rec(n);
+      RecBeta R;
+      load_rec_beta(slot(n), lane, R);
       const float xc = (lane >= 1 && lane < C) ? be : -kInf;  // core beta
       const float Mc = safe_max(wmax_u(xc));
       if (lane >= 1 && lane <= 32) bc[lane - 1] = lane < C ? lt_exp(xc - Mc) : 0.f;
@@ -942,11 +975,9 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
       }
       const float rp = lane < 32 ? R.rt * bc[lane & 31] : 0.f;
       const float cs = R.cs, ej = R.ej, rho = R.rho, pi = R.pi;
-      // the record's last use: its successor two chunks on loads from here
-      if (reload && !LT_ABL(a, 512)) {
-        rd.ensure_bwd(k - 2, lane);
-        load_rec_beta(rec_ptr(k - 2), lane, R);
-      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      rd.ensure_bwd(k - kWalkSlots, lane);
+      issue_rec(k - kWalkSlots, n + kWalkSlots);
       const float tot = half_sum(p0 + p1);
       const float nj = Mc + cs + ej + lt_log(tot);  // lane j: beta'[j+1]
       // state 0: the rt row and its own self loop
@@ -957,16 +988,6 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
       be = lane == 0 ? nb0 : (lane < C ? sh : -kInf);
       if (lane < C) dst[(long long)k * CP + lane] = be;
       __builtin_amdgcn_wave_barrier();
-    };
-    if (Kl > 0) {
-      rd.ensure_bwd(Kl - 2, lane);
-      load_rec_beta(rec_ptr(Kl - 1), lane, rr[0]);
-      load_rec_beta(rec_ptr(Kl - 2), lane, rr[1]);
-      for (int n0 = 0; n0 < (Kl & ~1); n0 += 2) {
-        step(rr[0], Kl - 1 - n0, true);
-        step(rr[1], Kl - 2 - n0, true);
-      }
-      if (Kl & 1) step(rr[0], 0, false);
     }
   } else if (wave == 2 && !LT_ABL(a, 2) && !LT_ABL(a, 128)) {
     num_walk<PPL, true>(a, b, lane, nf, Kl, nl, s_nv[0], &s_num, rd);
@@ -1709,9 +1730,10 @@ int ck_launch_ab(CkArgs& a, bool bf16, hipStream_t st) {
   const long long nwa = (items + 3) / 4;
   const int at = ck_env("LT_CHUNK_WALK_AT", std::max(0, 100 - 3000 / std::max(a.B, 1)));
   a.wpos = (int)(nwa * std::min(std::max(at, 0), 100) / 100);
-  int rc = ck_launch(ck_kernel_ab(a.PPL, bf16, a.V == 32), (int)(a.nc + nwa), 0, st, a);
+  int rc = ck_launch(ck_kernel_ab(a.PPL, bf16, a.V == 32), (int)(a.nc + nwa), fuse ? kWalkLds : 0,
+                     st, a);
   if (rc || fuse) return rc;
-  return ck_launch(ck_kernel_b(a.PPL), a.B, 0, st, a);
+  return ck_launch(ck_kernel_b(a.PPL), a.B, kWalkLds, st, a);
 }
 const void* ck_kernel_c(int ppl, bool bf16, bool full) {
   if (full)
