@@ -1717,10 +1717,11 @@ int ck_cus() {
 // when the walks (one workgroup per utterance, at most one of the two
 // workgroup slots per CU the launch's registers allow) could hold half the
 // chip's slots while they wait (B > CUs), or LT_CHUNK_FUSE=0. The walks'
-// block position: a walk needs about K x 0.7 us and follows A's front at
-// half its own pace, so it starts when the chunks left take half its time:
-// the fraction 1 - 30 / B of A's workgroups (chunk waves take ~25 us per
-// round of 2048; LT_CHUNK_WALK_AT overrides, in percent).
+// block position, the fraction 1 - 48 / B of A's workgroups: a walk follows
+// A's front and then needs about K x 0.55 us on its own, so small batches
+// start it early and larger ones keep its slots for A longer
+// (tools/walk_sweep.py: B = 64 best at 0-25 %, B = 128 at 50-65 %;
+// LT_CHUNK_WALK_AT overrides, in percent).
 int ck_launch_ab(CkArgs& a, bool bf16, hipStream_t st) {
   hipError_t e = hipMemsetAsync(a.ready, 0, 4LL * a.B * a.K, st);
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
@@ -1728,7 +1729,7 @@ int ck_launch_ab(CkArgs& a, bool bf16, hipStream_t st) {
   a.nc = fuse ? a.B : 0;
   const long long items = 2LL * a.B * ((a.K + 1) / 2);
   const long long nwa = (items + 3) / 4;
-  const int at = ck_env("LT_CHUNK_WALK_AT", std::max(0, 100 - 3000 / std::max(a.B, 1)));
+  const int at = ck_env("LT_CHUNK_WALK_AT", std::max(0, 100 - 4800 / std::max(a.B, 1)));
   a.wpos = (int)(nwa * std::min(std::max(at, 0), 100) / 100);
   int rc = ck_launch(ck_kernel_ab(a.PPL, bf16, a.V == 32), (int)(a.nc + nwa), fuse ? kWalkLds : 0,
                      st, a);
