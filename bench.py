@@ -87,7 +87,7 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, chec
   # stand-in weight-fn projection head (512 x 33 fp32) so the
   # step's one collective carries [loss sum || parameter grads]
   head = torch.nn.Parameter(torch.zeros([512, 33], device=W.device))
-  head.grad = torch.zeros_like(head)
+  bucket = sharding.GradBucket([head], device=W.device)  # head.grad is a view of the bucket
 
   def step(ev=None):
     if ev is not None:
@@ -106,7 +106,7 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, chec
     if ev is not None:
       ev[2].record()
     if dist_on:
-      sharding.all_reduce_step(loss, [head])
+      bucket.all_reduce_step(loss)
     return dW
 
   for _ in range(warmup):
@@ -323,10 +323,18 @@ def main():
   world = int(os.environ.get('WORLD_SIZE', '1'))
   rank = int(os.environ.get('RANK', '0'))
   local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-  dist_on = world > 1
+  # LT_BENCH_DIST=1: the N > 1 code path (RCCL init, barriers, the per-step
+  # all-reduce, max-over-ranks timing) even with one rank, to exercise it on
+  # a one-GPU box
+  dist_on = world > 1 or os.environ.get('LT_BENCH_DIST', '0') == '1'
   torch.cuda.set_device(local_rank)
   device = torch.device('cuda', local_rank)
   if dist_on:
+    # RCCL logging: its version banner (NCCL_DEBUG=VERSION) is printed to
+    # stdout, so the level is WARN and the log file stderr -- stdout carries
+    # only the one JSON line the driver parses
+    os.environ['NCCL_DEBUG'] = 'WARN'
+    os.environ['NCCL_DEBUG_FILE'] = '/dev/stderr'
     torch.distributed.init_process_group('nccl', device_id=device)
 
   B, T, U, V, n = args.batch, args.frames, args.labels, args.vocab, args.context

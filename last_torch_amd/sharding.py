@@ -68,3 +68,35 @@ def all_reduce_step(loss: torch.Tensor, params: Iterable[torch.nn.Parameter] = (
     g.copy_(flat[off:off + k].view_as(g).to(g.dtype))
     off += k
   return flat[0]
+
+
+class GradBucket:
+  """The step's collective with no packing: one flat fp32 buffer [loss sum ||
+  grads], the parameters' .grad set to views of it (as DDP's buckets do), so
+  a step is the loss sum written into slot 0 and ONE all-reduce -- no
+  concatenate before it and no copy back after it. Parameters must be fp32
+  and keep the bucket's views as their gradients (backward accumulates into
+  them in place)."""
+
+  def __init__(self, params: Iterable[torch.nn.Parameter], device=None):
+    self.params = list(params)
+    n = sum(p.numel() for p in self.params)
+    dev = device if device is not None else (self.params[0].device if self.params else 'cpu')
+    self.flat = torch.zeros([1 + n], dtype=torch.float32, device=dev)
+    off = 1
+    for p in self.params:
+      if p.dtype != torch.float32:
+        raise TypeError(f'GradBucket: parameters must be float32, got {p.dtype}')
+      k = p.numel()
+      p.grad = self.flat[off:off + k].view_as(p)
+      off += k
+
+  def all_reduce_step(self, loss: torch.Tensor, group: Optional[dist.ProcessGroup] = None
+                      ) -> torch.Tensor:
+    """all-reduce(SUM) of [loss.sum() || grads] in place; returns the global
+    loss sum (the identity without an initialised process group)."""
+    torch.sum(loss.detach().reshape(-1).to(torch.float32), dim=0, keepdim=True,
+              out=self.flat[:1])
+    if dist.is_available() and dist.is_initialized():
+      dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+    return self.flat[0]

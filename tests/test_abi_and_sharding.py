@@ -107,7 +107,14 @@ def _gloo_worker(rank, world, port, payload, out_q):
     p = torch.nn.Parameter(torch.zeros(5))
     p.grad = torch.full([5], float(rank + 1))
     total = sharding.all_reduce_step(torch.tensor(loss), [p])
-    out_q.put((rank, idx, loss, dW, float(total), p.grad.numpy().copy()))
+    # the same exchange through a persistent bucket (grads are views of it)
+    q = torch.nn.Parameter(torch.zeros(2, 3))
+    bucket = sharding.GradBucket([q])
+    q.grad.fill_(float(rank + 1))
+    total2 = bucket.all_reduce_step(torch.tensor(loss))
+    assert q.grad.data_ptr() == bucket.flat[1:].data_ptr()
+    out_q.put((rank, idx, loss, dW, float(total), p.grad.numpy().copy(), float(total2),
+               q.grad.numpy().copy()))
   finally:
     dist.destroy_process_group()
 
@@ -136,10 +143,12 @@ def test_gloo_world2_sharded_loss_matches_full_batch():
     assert p.exitcode == 0
   loss = np.zeros(B, np.float32)
   dW = np.zeros_like(full_dW)
-  for rank, idx, l, g, total, pgrad in res:
+  for rank, idx, l, g, total, pgrad, total2, qgrad in res:
     loss[idx] = l
     dW[idx] = g
     np.testing.assert_allclose(total, full_loss.sum(), rtol=1e-6)
     np.testing.assert_array_equal(pgrad, np.full(5, 3.0))  # 1 + 2
+    np.testing.assert_allclose(total2, full_loss.sum(), rtol=1e-6)
+    np.testing.assert_array_equal(qgrad, np.full((2, 3), 3.0))
   np.testing.assert_array_equal(loss, full_loss)
   np.testing.assert_array_equal(dW, full_dW)
