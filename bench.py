@@ -276,8 +276,9 @@ def chunk_len(B, T, U, V):
 
 def loss_grad_design(B, T, U, V, n, C, device):
   """(kernel names, description, design bytes per frame) of the design
-  lt_loss_grad dispatches to for this shape (lt_lattice.hip lt_loss_grad)."""
-  if _native.chunk_path(B, T, U, V, n, device):
+  lt_loss_grad dispatches to for this shape (lt_loss_grad_design)."""
+  d = _native.loss_grad_design(B, T, U, V, n)
+  if d == _native.DESIGN_CHUNK:
     L = chunk_len(B, T, U, V)
     fuse_ab = B <= torch.cuda.get_device_properties(device).multi_processor_count
     knames = ['ck_ab_kernel'] + ([] if fuse_ab else ['ck_combine_kernel']) + ['ck_marg_kernel']
@@ -285,9 +286,9 @@ def loss_grad_design(B, T, U, V, n, C, device):
               f"{' -> '.join(knames)})")
     return knames, design, chunk_design_bytes(T, U, V, L)
   ck_b = sum(algorithmic_bytes(T, U, V, C, checkpoints=True)[:2])
-  if _native.fused_path(B, T, U, V, n, device):
+  if d == _native.DESIGN_FUSED_PIPE:
     return ['pipe_kernel'], 'lt_loss_grad (fused pipe)', ck_b
-  if _native.prefer_checkpoints(B, device, (T, U, V, n, False)):
+  if d == _native.DESIGN_CHECKPOINTS:
     knames = ['pipe_kernel' if _native.pipe_path(B, T, U, V, n) else 'fwdbwd_kernel',
               'marg_kernel']
     return knames, ('checkpointing: alpha || beta recursions with checkpoints, then the '

@@ -283,6 +283,20 @@ int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* 
                      float* path_weight, void* workspace, size_t workspace_bytes,
                      void* stream);
 
+/* The design lt_loss_grad runs for *pb (the environment overrides LT_CHUNK,
+ * LT_CHECKPOINTS, LT_FUSED apply as in the call): LT_DESIGN_CHUNK the chunked
+ * two-level scan (bigram, 5 * batch <= 3 * CUs), LT_DESIGN_FUSED_PIPE one
+ * pipelined launch with the marginals beside the recursions,
+ * LT_DESIGN_CHECKPOINTS alpha || beta with checkpoints then one streaming
+ * marginal pass (the north-star B = 256), LT_DESIGN_RECURSION forward then a
+ * backward recursion that writes dW. For bindings that call the two-call
+ * entry points themselves and want lt_loss_grad's choice. */
+#define LT_DESIGN_CHUNK 0
+#define LT_DESIGN_FUSED_PIPE 1
+#define LT_DESIGN_CHECKPOINTS 2
+#define LT_DESIGN_RECURSION 3
+int lt_loss_grad_design(const lt_problem* pb, int32_t* design);
+
 /* Joint weight function on the matrix cores (replaces
  * the hidden-tensor path of JointWeightFn.forward, weight_fns.py:174-227):
  *   W[f, c, y] = out_bias[y] + sum_h out_weight[y, h] * tanh(ctx_proj[c, h] + frame_proj[f, h])

@@ -59,6 +59,7 @@ _SIG = {
     'lt_loss_backward_workspace_bytes': [ctypes.POINTER(Problem), _I32,
                                          ctypes.POINTER(ctypes.c_size_t)],
     'lt_loss_backward': [ctypes.POINTER(Problem), _I32] + [_P] * 14 + [ctypes.c_size_t, _P],
+    'lt_loss_grad_design': [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_int32)],
     'lt_loss_grad_workspace_bytes': [ctypes.POINTER(Problem), _I32,
                                      ctypes.POINTER(ctypes.c_size_t)],
     'lt_loss_grad': [ctypes.POINTER(Problem), _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
@@ -304,6 +305,22 @@ def fused_path(batch, frames, labels, vocab_size, context_size, device=None, bf1
   want = (env != '0') if env else 2 * batch < cus
   return (want and prefer_checkpoints(batch, device) and
           pipe_path(batch, frames, labels, vocab_size, context_size, bf16))
+
+
+DESIGN_CHUNK, DESIGN_FUSED_PIPE, DESIGN_CHECKPOINTS, DESIGN_RECURSION = 0, 1, 2, 3
+DESIGN_NAMES = {DESIGN_CHUNK: 'chunk', DESIGN_FUSED_PIPE: 'fused_pipe',
+                DESIGN_CHECKPOINTS: 'checkpoints', DESIGN_RECURSION: 'recursion'}
+
+
+def loss_grad_design(batch, frames, labels, vocab_size, context_size, bf16=False):
+  """lt_loss_grad_design: the design lt_loss_grad runs for this shape on the
+  current device (DESIGN_* above; the LT_CHUNK / LT_CHECKPOINTS / LT_FUSED
+  overrides apply)."""
+  pb = Problem(batch, frames, vocab_size, context_size, labels,
+               LT_DTYPE_BF16 if bf16 else LT_DTYPE_F32)
+  out = ctypes.c_int32(-1)
+  _check(lib().lt_loss_grad_design(ctypes.byref(pb), ctypes.byref(out)), 'lt_loss_grad_design')
+  return out.value
 
 
 def loss_grad_workspace_bytes(W, vocab_size, context_size, max_labels, local_norm):

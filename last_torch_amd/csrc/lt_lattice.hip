@@ -1147,11 +1147,33 @@ int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
   return hip_check(hipGetLastError(), "backtrace launch");
 }
 
+// The design lt_loss_grad runs for this problem (LT_DESIGN_*): the chunked
+// scan while it is faster, else the fused pipe launch, the checkpointing pair
+// or the recursion pair (the environment overrides apply, as in the call).
+static int loss_grad_design(const lt_problem* pb) {
+  if (lt_impl::chunk_preferred(pb) && pb->max_frames > 0) return LT_DESIGN_CHUNK;
+  const int cus = cu_count();
+  const bool ck_def = 2 * pb->batch <= cus || (lt_impl::pipe_eligible(pb) && 2 * pb->batch <= 3 * cus);
+  const bool ck = env_int("LT_CHECKPOINTS", ck_def ? 1 : 0) != 0;
+  const int fused = env_int("LT_FUSED", 2 * pb->batch < cus ? 1 : 0);
+  if (ck && fused && lt_impl::pipe_eligible(pb)) return LT_DESIGN_FUSED_PIPE;
+  return ck ? LT_DESIGN_CHECKPOINTS : LT_DESIGN_RECURSION;
+}
+
+int lt_loss_grad_design(const lt_problem* pb, int32_t* design) {
+  NGram g;
+  int rc = check_problem(pb, &g);
+  if (rc) return rc;
+  if (!design) return fail(LT_EINVAL, "null pointer");
+  *design = loss_grad_design(pb);
+  return LT_OK;
+}
+
 int lt_loss_grad_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_t* bytes) {
   NGram g;
   int rc = check_problem(pb, &g);
   if (rc) return rc;
-  if (lt_impl::chunk_preferred(pb) && pb->max_frames > 0) {
+  if (loss_grad_design(pb) == LT_DESIGN_CHUNK) {
     size_t st = 0, sc = 0;
     if ((rc = lt_chunk_workspace_bytes(pb, local_norm, &st, &sc))) return rc;
     if (bytes) *bytes = ((st + 255) & ~(size_t)255) + sc;
@@ -1173,7 +1195,8 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
       (pb->max_labels > 0 && !labels))
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W) || misaligned(dW)) return fail(LT_EINVAL, "W/dW must be 16-byte aligned");
-  if (lt_impl::chunk_preferred(pb) && pb->max_frames > 0) {
+  const int design = loss_grad_design(pb);
+  if (design == LT_DESIGN_CHUNK) {
     // bigram: the chunked two-level scan (lt_chunk.hip), two launches (plus
     // the frame-serial pair, whose workgroups exit at once unless an
     // utterance is out of the fast path's range)
@@ -1199,15 +1222,12 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
     return lt_loss_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z, num,
                            alpha, an, nullptr, nullptr, nullptr, stream);
   }
-  const int cus = cu_count();
   // checkpointing (alpha || beta, then the marginal pass) while 2B recursion
   // workgroups find CUs; with the pipelined bigram recursions up to 1.5 CUs
-  // utterances (measured crossover ~1.75: tools/b256_check.py)
-  const bool ck_def = 2 * pb->batch <= cus || (lt_impl::pipe_eligible(pb) && 2 * pb->batch <= 3 * cus);
-  const bool ck = env_int("LT_CHECKPOINTS", ck_def ? 1 : 0) != 0;
-  // fused: the recursions and the marginal pass in one launch (lt_pipe.hip)
-  const int fused = env_int("LT_FUSED", 2 * pb->batch < cus ? 1 : 0);
-  if (ck && fused && lt_impl::pipe_eligible(pb)) {
+  // utterances (measured crossover ~1.75: tools/b256_check.py); fused: the
+  // recursions and the marginal pass in one launch (lt_pipe.hip)
+  const bool ck = design == LT_DESIGN_CHECKPOINTS || design == LT_DESIGN_FUSED_PIPE;
+  if (design == LT_DESIGN_FUSED_PIPE) {
     int* ctl = (int*)(ws + w.ctl);
     if ((rc = lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss,
                                    log_z, num, alpha, an, beta, bn, arcs, 2, nullptr, stream, dW,

@@ -195,3 +195,17 @@ def test_cfg5_trigram_bf16(cuda):
   Wc, nfc, labc, nlc = _np(W[idx], nf[idx], lab[idx], nl[idx])
   _, rlz, _, rdW = orc.loss_grad(Wc, nfc, labc, nlc, V, n)
   assert_grad_close(dW[idx].float().cpu().numpy(), rdW, rlz, bf16=True)
+
+
+@pytest.mark.parametrize('B', [8, 64, 120, 160, 192, 256, 512])
+def test_design_query_matches_python_mirrors(cuda, B):
+  """lt_loss_grad_design (the C dispatch) and the Python mirrors the autograd
+  path and bench.py use agree at the bench shape for every batch size."""
+  T, U, V, n = 1000, 100, 32, 1
+  d = nat.loss_grad_design(B, T, U, V, n)
+  assert (d == nat.DESIGN_CHUNK) == nat.chunk_path(B, T, U, V, n)
+  assert (d == nat.DESIGN_FUSED_PIPE) == nat.fused_path(B, T, U, V, n)
+  if B == 64:
+    assert d == nat.DESIGN_CHUNK
+  if B == 256:
+    assert d == nat.DESIGN_CHECKPOINTS
