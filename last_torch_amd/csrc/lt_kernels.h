@@ -786,14 +786,31 @@ LT_DEVINL void den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int
       LT_STAMP(a, tid == 0, 0, i, 2);
     }
   } else {
+    const int R = g.V + 1;
+    const bool fstep = g.n >= 1 && ngrp % g.V == 0;
+    const int fda = fstep ? ngrp / g.V : 0;
     for (int i = 0; i < nf; ++i) {
       lds_barrier();
       const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
       const float* acur = abuf + (i & 1) * C;
       float* anxt = abuf + ((i + 1) & 1) * C;
+      // a lane's slice advances by a constant from one pass to the next once
+      // its destination is a full-order state and ngrp is a multiple of V
+      // (the source base moves by ngrp / V, the label stays): no per-pass
+      // index math (trigram: 5.5 passes a frame)
+      int ao[P], wo[P], n2 = 0, qprev = -1;
       for (int qq = a.den_q0 + grp; qq < C; qq += ngrp) {
-        int ao[P], wo[P];
-        const int n2 = fwd_slice<P>(g, qq, j, a.Pr, ao, wo);
+        if (fstep && qprev >= g.An) {
+#pragma unroll
+          for (int m = 0; m < P; ++m) {
+            const bool blank = m == 0 && j == 0;
+            ao[m] += m < n2 ? (blank ? ngrp : fda) : 0;
+            wo[m] += m < n2 ? (blank ? ngrp * R : fda * R) : 0;
+          }
+        } else {
+          n2 = fwd_slice<P>(g, qq, j, a.Pr, ao, wo);
+        }
+        qprev = qq;
         group(qq, ao, wo, n2, wrow, acur, anxt);
       }
       start_state(wrow, acur, anxt);
@@ -1113,12 +1130,28 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
         if (has) group(grp, woff, boff, nv, wrow, arow, bcur, bnxt, ncur, dWf, crow, false);
       });
   } else {
+    // a lane's slice advances by a constant from one pass to the next once
+    // its source is a full-order state and ngrp is a multiple of V^(n-1)
+    // (next(p, y) - y is then unchanged): W moves by ngrp rows, the blank's
+    // beta index by ngrp, the lexical ones not at all
+    const int R = g.V + 1;
+    const bool bstep = g.n == 1 || (g.n >= 2 && ngrp % g.Vn1 == 0);
     for (int i = 0; i < nf; ++i)
       step(i, [&](const unsigned char* wrow, const float* arow, const float* bcur, float* bnxt,
                   const float* ncur, void* dWf, float* crow) {
+        int wo[P], bo[P], n2 = 0, pprev = -1;
         for (int p = grp; p < C; p += ngrp) {
-          int wo[P], bo[P];
-          const int n2 = bwd_slice<P>(g, p, j, a.Pr, wo, bo);
+          if (bstep && pprev >= g.An) {
+#pragma unroll
+            for (int m = 0; m < P; ++m) {
+              const bool blank = m == 0 && j == 0;
+              wo[m] += m < n2 ? ngrp * R : 0;
+              bo[m] += (m < n2 && blank) ? ngrp : 0;
+            }
+          } else {
+            n2 = bwd_slice<P>(g, p, j, a.Pr, wo, bo);
+          }
+          pprev = p;
           group(p, wo, bo, n2, wrow, arow, bcur, bnxt, ncur, dWf, crow, false);
         }
       });
