@@ -16,7 +16,8 @@
 //   LDS-DMA (5 contiguous 1 KiB wave instructions a frame, counted vmcnt
 //   waits) and each lane reads its 19 weights from LDS beside alpha. The
 //   alpha chain takes the maximum by a max3 tree; the backpointer (the
-//   first term equal to it) is formed beside the chain.
+//   first term equal to it) is formed one step later, from the kept terms,
+//   while the next frame's LDS reads are in flight.
 // Backpointers: one byte per (frame, state), the term index, as the generic
 // kernel writes them (backtrace_kernel reads both).
 #include "lt_kernels.h"
@@ -107,10 +108,30 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
   };
   // frame t's DMA has landed: ring issues and one backpointer store a step,
   // in issue order (vmcnt counts both, in order)
-  auto wait_frame = [&](int t) { wait_vmcnt((kAhead - 1) * ni + min(t, kAhead)); };
+  // (frame t - 1's store goes out in step t, before that step's ring issue)
+  auto wait_frame = [&](int t) { wait_vmcnt((kAhead - 1) * ni + min(max(t - 1, 0), kAhead - 1)); };
   if (nf > 0) {
     for (int d = 0; d < kAhead; ++d) issue(d);
   }
+  const int ib = h ? 18 : 1;  // term index of x[0]
+  // the previous frame's terms and value: its backpointer is formed in the
+  // next step while that step's LDS reads are in flight (off the chain)
+  float xq[kHalf], xsq = 0.f, rq = 0.f;
+#pragma unroll
+  for (int m = 0; m < kHalf; ++m) xq[m] = 0.f;
+  auto emit_bp = [&](int tb) {
+    // the first term equal to the maximum (group_reduce's first-maximum
+    // rule), the lower half first
+    int ri = 99;
+#pragma unroll
+    for (int m = 16; m >= 0; --m) ri = xq[m] == rq ? ib + m : ri;
+    if (h == 0) ri = xsq == rq ? 0 : ri;
+    auto pi = __builtin_amdgcn_permlane32_swap(ri, ri, false, false);
+    const int rlo = h ? pi[0] : ri, rhi = h ? ri : pi[1];
+    const int bpv = lane == 32 ? 0 : (rlo < 99 ? rlo : rhi);
+    if ((h == 0 && live) || lane == 32)
+      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bpv, bpr, lane == 32 ? 0 : q, tb * C, 0);
+  };
   auto step = [&](int t) {
     if (t >= nf) return;  // the last round's spare steps
     const float* acur = s_al[t & 1];
@@ -133,6 +154,7 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
       al[4 * g + 0] = v.x; al[4 * g + 1] = v.y; al[4 * g + 2] = v.z; al[4 * g + 3] = v.w;
     }
     const float aq = acur[aslot(min(q, V))];
+    if (t > 0) emit_bp(t - 1);
     float x[kHalf];
 #pragma unroll
     for (int m = 0; m < kHalf; ++m) {
@@ -141,7 +163,6 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
     }
     const float xs = aq + F.self;
     const float w00 = F.w00;
-    const int ib = h ? 18 : 1;  // term index of x[0]
     if (!LT_ABL(a, 1)) issue(t + kAhead);
     // the value: a max3 tree over the lane's terms, the halves by one
     // permlane32 swap (the alpha chain waits on nothing else)
@@ -161,21 +182,15 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
     if (h == 0 && live) anxt[aslot(q)] = r;
     a0 += w00;
     if (lane == 32) anxt[0] = a0;
-    // the backpointer: the first term equal to the maximum (group_reduce's
-    // first-maximum rule), the lower half first
-    int ri = 99;
 #pragma unroll
-    for (int m = 16; m >= 0; --m) ri = x[m] == r ? ib + m : ri;
-    if (h == 0) ri = xs == r ? 0 : ri;
-    auto pi = __builtin_amdgcn_permlane32_swap(ri, ri, false, false);
-    const int rlo = h ? pi[0] : ri, rhi = h ? ri : pi[1];
-    const int bpv = lane == 32 ? 0 : (rlo < 99 ? rlo : rhi);
-    if ((h == 0 && live) || lane == 32)
-      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bpv, bpr, lane == 32 ? 0 : q, t * C, 0);
+    for (int m = 0; m < kHalf; ++m) xq[m] = x[m];
+    xsq = xs;
+    rq = r;
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
   };
   for (int t = 0; t < nf; ++t) step(t);
+  if (nf > 0) emit_bp(nf - 1);
   // the distance: (+)_q alpha_T[q] in MaxTropical, the first maximum
   const float* af = s_al[nf & 1];
   float r = lane < C ? af[aslot(lane)] : -kInf;
