@@ -163,7 +163,6 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
     }
     const float xs = aq + F.self;
     const float w00 = F.w00;
-    if (!LT_ABL(a, 1)) issue(t + kAhead);
     // the value: a max3 tree over the lane's terms, the halves by one
     // permlane32 swap (the alpha chain waits on nothing else)
     float mx = max3_raw(h ? x[16] : xs, x[0], x[1]);
@@ -182,6 +181,7 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
     if (h == 0 && live) anxt[aslot(q)] = r;
     a0 += w00;
     if (lane == 32) anxt[0] = a0;
+    if (!LT_ABL(a, 1)) issue(t + kAhead);
 #pragma unroll
     for (int m = 0; m < kHalf; ++m) xq[m] = x[m];
     xsq = xs;
