@@ -252,11 +252,26 @@ __global__ __launch_bounds__(256) void vit_backtrace_kernel(const VbtArgs a) {
   int* endq = (int*)(start + ((nseg * C + 15) & ~15));  // [nseg]
   const unsigned char* src = a.bp + (long long)b * a.T * C;
   const int nb = nf * C;
-  for (int e = tid * 4; e < nb; e += 1024) {
-    if (e + 4 <= nb && ((((uintptr_t)(src + e)) & 3) == 0)) {
-      *(unsigned*)(rows + e) = *(const unsigned*)(src + e);
-    } else {
-      for (int k = e; k < nb && k < e + 4; ++k) rows[k] = src[k];
+  if ((((uintptr_t)src) & 15) == 0) {
+    // 16-byte loads, four in flight per thread before their LDS stores
+    const int n16 = nb >> 4;
+    for (int e = tid; e < n16; e += 1024) {
+      uint4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (e + 256 * k < n16) v[k] = ((const uint4*)src)[e + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (e + 256 * k < n16) ((uint4*)rows)[e + 256 * k] = v[k];
+    }
+    for (int e = (n16 << 4) + tid; e < nb; e += 256) rows[e] = src[e];
+  } else {
+    for (int e = tid * 4; e < nb; e += 1024) {
+      if (e + 4 <= nb && ((((uintptr_t)(src + e)) & 3) == 0)) {
+        *(unsigned*)(rows + e) = *(const unsigned*)(src + e);
+      } else {
+        for (int k = e; k < nb && k < e + 4; ++k) rows[k] = src[k];
+      }
     }
   }
   __syncthreads();
