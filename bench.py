@@ -76,7 +76,8 @@ def make_inputs(B, T, U, V, C, device, seed, dtype=torch.float32):
 
 def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, checkpoints=True,
               fused=False):
-  """Returns (wall seconds over `steps`, fwd ms list, bwd ms list); fused:
+  """Returns (wall seconds over `steps`, fwd ms list, bwd ms list, all-reduces
+  issued); fused:
   lt_loss_grad in one C-ABI call (fwd list; bwd list empty), else
   lt_loss_forward (fwd list) + lt_loss_backward (bwd list)."""
   grad = torch.ones([W.shape[0]], dtype=torch.float32, device=W.device)
@@ -127,7 +128,48 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, chec
   wall = time.perf_counter() - t0
   fwd_ms = [e[0].elapsed_time(e[1]) for e in evs] if events else []
   bwd_ms = [e[1].elapsed_time(e[2]) for e in evs] if (events and not fused) else []
-  return wall, fwd_ms, bwd_ms
+  return wall, fwd_ms, bwd_ms, bucket.calls
+
+
+def weights_leg(B, T, U, V, n, C, device, reps=10):
+  """The bench step on a trained model's kind of arc weights:
+  log_softmax(sigma * randn) rows (weight_fns.py:120-136) for sigma 5 and
+  10, and randn with one masked (-inf) arc per utterance
+  (lattices.py:450-453): ms per lt_loss_grad call and the utterances that
+  left the chunked fast path (its fallback flag words)."""
+  out = {}
+  g = torch.Generator(device=device)
+  lab = torch.randint(1, V + 1, [B, U], generator=g.manual_seed(5), device=device,
+                      dtype=torch.int32)
+  nf = torch.full([B], T, dtype=torch.int32, device=device)
+  nl = torch.full([B], U, dtype=torch.int32, device=device)
+  for name in ('randn', 'logsoftmax_s5', 'logsoftmax_s10', 'neginf_arc'):
+    W = torch.randn([B, T, C, V + 1], generator=g.manual_seed(6), device=device)
+    if name.startswith('logsoftmax'):
+      W = torch.log_softmax(float(name.split('_s')[1]) * W, dim=-1)
+    elif name == 'neginf_arc':
+      ar = torch.arange(B, device=device)
+      W[ar, torch.randint(0, T, [B], generator=g, device=device),
+        torch.randint(0, C, [B], generator=g, device=device),
+        torch.randint(0, V + 1, [B], generator=g, device=device)] = -float('inf')
+    ws = torch.empty([_native.loss_grad_workspace_bytes(W, V, n, U, False)], dtype=torch.uint8,
+                     device=device)
+    for _ in range(2):
+      _native.loss_grad(W, nf, lab, nl, V, n, False, workspace=ws)
+    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+    e0.record()
+    for _ in range(reps):
+      _native.loss_grad(W, nf, lab, nl, V, n, False, workspace=ws)
+    e1.record()
+    torch.cuda.synchronize()
+    rec = {'ms_per_call': e0.elapsed_time(e1) / reps}
+    if _native.loss_grad_design(B, T, U, V, n) == _native.DESIGN_CHUNK:
+      rec['fallback_utterances'] = _native.chunk_fallback_count(ws, B)
+    out[name] = rec
+    del W, ws
+  out['slowdown_logsoftmax_s10_vs_randn'] = (out['logsoftmax_s10']['ms_per_call'] /
+                                             out['randn']['ms_per_call'])
+  return out
 
 
 def joint_step_leg(T, U, V, n, device, B=64, F=256, H=512, reps=5):
@@ -297,6 +339,99 @@ def loss_grad_design(B, T, U, V, n, C, device):
       algorithmic_bytes(T, U, V, C, checkpoints=False)[:2])
 
 
+def launch_ranks(argv, n):
+  """`--gpus N > 1` without a torch.distributed environment: start N ranks
+  with torch.distributed.run as a CHILD process (one process per GPU, RCCL
+  rendezvous on 127.0.0.1) and exit with its status. The parent never
+  touches the GPU (no HIP call before or after), so nothing is exec'ed over
+  an initialised device."""
+  import socket
+  import subprocess
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+         '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + argv
+  return subprocess.call(cmd)
+
+
+def global_batch(B_global, T, U, V, seed, varlen):
+  """The step's global batch, the same on every rank: num_frames (T, or
+  U[T/2, T] with --varlen), labels and num_labels, host tensors. Each rank
+  keeps the LPT shard sharding.shard_utterances gives it."""
+  g = torch.Generator().manual_seed(seed)
+  if varlen:
+    nf = torch.randint(T // 2, T + 1, [B_global], generator=g, dtype=torch.int32)
+  else:
+    nf = torch.full([B_global], T, dtype=torch.int32)
+  labels = torch.randint(1, V + 1, [B_global, U], generator=g, dtype=torch.int32)
+  nl = torch.full([B_global], U, dtype=torch.int32)
+  return nf, labels, nl
+
+
+def shard_weights(idx, T, C, V, device, seed):
+  """Arc weights of the utterances `idx` of the global batch: utterance i
+  from its own seeded stream (seed + i), so a rank materialises only its
+  shard and every rank agrees on every utterance."""
+  W = torch.empty([len(idx), T, C, V + 1], dtype=torch.float32, device=device)
+  g = torch.Generator(device=device)
+  for j, i in enumerate(idx):
+    g.manual_seed(seed + int(i))
+    W[j] = torch.randn([T, C, V + 1], generator=g, device=device)
+  return W
+
+
+def cpu_dist_step(args, world, rank):
+  """--device cpu: the N > 1 control flow on host tensors with gloo (the
+  CPU test of the launcher): each rank's LPT shard through the product's
+  CPU path (RecognitionLattice on CPU tensors -> cpu.py), the loss into
+  the GradBucket, one all-reduce per step; prints the same JSON line."""
+  import last_torch_amd as lt
+  B, T, U, V, n = args.batch, args.frames, args.labels, args.vocab, args.context
+  C = lt.contexts.FullNGram(vocab_size=V, context_size=n).num_states()
+  nf, lab, nl = global_batch(B * world, T, U, V, 1234, args.varlen)
+  idx = sharding.local_shard(nf, rank, world)
+  head = torch.nn.Parameter(torch.zeros([C, V + 1]))
+  bucket = sharding.GradBucket([head])
+  ctx = lt.contexts.FullNGram(vocab_size=V, context_size=n)
+  W = shard_weights(idx, T, C, V, 'cpu', 1234)
+  wfn = lt.weight_fns.TableWeightFn(W)
+  lat = lt.RecognitionLattice(context=ctx, alignment=lt.alignments.FrameDependent(),
+                              weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+                              weight_fn_factory=lambda _: wfn)
+  frames = torch.arange(T, dtype=torch.float32)[None, :, None].expand(len(idx), T, 1)
+
+  def step():
+    bucket.zero_grad()
+    wfn.table = W + head  # a stand-in trainable head on the arc weights
+    loss = lat(frames, nf[idx], lab[idx], nl[idx])
+    loss.sum().backward()
+    return bucket.all_reduce_step(loss)
+
+  for _ in range(args.warmup):
+    step()
+  torch.distributed.barrier()
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    total = step()
+  torch.distributed.barrier()
+  wall = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+  torch.distributed.all_reduce(wall, op=torch.distributed.ReduceOp.MAX)
+  cells = int(nf.sum()) * U * C
+  if rank == 0:
+    print(json.dumps({
+        'metric': METRIC, 'value': cells * args.steps / float(wall), 'unit': 'cells/s',
+        'n_gpus': 0, 'ranks': world, 'rccl_world_size': None,
+        'gloo_world_size': torch.distributed.get_world_size(), 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': float(wall) / args.steps * 1e3,
+        'higher_is_better': True, 'scaling': 'weak', 'device': 'cpu',
+        'collectives_per_step': bucket.calls / (args.steps + args.warmup),
+        'global_loss_sum': float(total), 'shard_sizes': [len(s) for s in
+                                                         sharding.shard_utterances(nf, world)],
+        'head_grad_sum': float(head.grad.sum()),
+    }), flush=True)
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
@@ -307,6 +442,10 @@ def main():
   ap.add_argument('--labels', type=int, default=100)
   ap.add_argument('--vocab', type=int, default=32)
   ap.add_argument('--context', type=int, default=1)
+  ap.add_argument('--varlen', action='store_true',
+                  help='num_frames ~ U[T/2, T] over the global batch (LPT-sharded)')
+  ap.add_argument('--device', choices=['cuda', 'cpu'], default='cuda',
+                  help='cpu: the N > 1 control flow on host tensors with gloo (tests)')
   ap.add_argument('--cpu-utts', type=int, default=int(os.environ.get('LT_BENCH_CPU_UTTS', 128)),
                   help='utterances of the C-oracle baseline (0: skip)')
   ap.add_argument('--cpu-ref-utts', type=int,
@@ -314,6 +453,8 @@ def main():
                   help='utterances of the PyTorch-CPU cpu_ref baseline (0: skip)')
   ap.add_argument('--no-north-star', action='store_true')
   ap.add_argument('--no-joint', action='store_true')
+  ap.add_argument('--no-weights', action='store_true',
+                  help='skip the realistic-weights leg (log_softmax / masked arcs)')
   ap.add_argument('--design', choices=['auto', 'checkpoints', 'recursion'], default='auto',
                   help='auto: lt_loss_grad (the chunked scan for the bigram); checkpoints / '
                        'recursion: the two-call lt_loss_forward + lt_loss_backward designs')
@@ -321,15 +462,27 @@ def main():
                   help='PMC summary (tools/pmc_summary.py) the traffic figure is read from')
   args = ap.parse_args()
 
+  if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+    sys.exit(launch_ranks(sys.argv[1:], args.gpus))
   world = int(os.environ.get('WORLD_SIZE', '1'))
   rank = int(os.environ.get('RANK', '0'))
   local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+  if world != args.gpus:
+    raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
+  if args.device == 'cpu':
+    torch.distributed.init_process_group('gloo')
+    try:
+      cpu_dist_step(args, world, rank)
+    finally:
+      torch.distributed.destroy_process_group()
+    return
   # LT_BENCH_DIST=1: the N > 1 code path (RCCL init, barriers, the per-step
   # all-reduce, max-over-ranks timing) even with one rank, to exercise it on
   # a one-GPU box
   dist_on = world > 1 or os.environ.get('LT_BENCH_DIST', '0') == '1'
   torch.cuda.set_device(local_rank)
   device = torch.device('cuda', local_rank)
+  rccl_world = None
   if dist_on:
     # RCCL logging: its version banner (NCCL_DEBUG=VERSION) is printed to
     # stdout, so the level is WARN and the log file stderr -- stdout carries
@@ -337,26 +490,38 @@ def main():
     os.environ['NCCL_DEBUG'] = 'WARN'
     os.environ['NCCL_DEBUG_FILE'] = '/dev/stderr'
     torch.distributed.init_process_group('nccl', device_id=device)
+    # the rank count RCCL itself sees: an all-reduce of ones
+    ones = torch.ones([1], device=device)
+    torch.distributed.all_reduce(ones)
+    rccl_world = int(ones.item())
+    if rccl_world != args.gpus or torch.distributed.get_world_size() != args.gpus:
+      raise SystemExit(f'bench.py: RCCL sees {rccl_world} ranks, --gpus {args.gpus}')
 
   B, T, U, V, n = args.batch, args.frames, args.labels, args.vocab, args.context
   C = _native.num_context_states(V, n)
-  W, nf, labels, nl = make_inputs(B, T, U, V, C, device, seed=1234 + rank)
+  # the global batch of B * N utterances, LPT-sharded; each rank
+  # materialises its shard's arc weights only
+  nf_g, lab_g, nl_g = global_batch(B * world, T, U, V, 1234, args.varlen)
+  idx = sharding.local_shard(nf_g, rank, world)
+  W = shard_weights(idx, T, C, V, device, 1234)
+  nf, labels, nl = (x[idx].to(device) for x in (nf_g, lab_g, nl_g))
   fused = args.design == 'auto'
   ckpt = args.design == 'checkpoints'
-  wall, fwd_ms, bwd_ms = run_steps(W, nf, labels, nl, V, n, args.steps, args.warmup, dist_on,
-                                   checkpoints=ckpt, fused=fused)
+  wall, fwd_ms, bwd_ms, calls = run_steps(W, nf, labels, nl, V, n, args.steps, args.warmup,
+                                          dist_on, checkpoints=ckpt, fused=fused)
 
   t = torch.tensor([wall], dtype=torch.float64, device=device)
   if dist_on:
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
   wall = float(t.item())
-  cells_per_step = world * B * T * U * C
+  # the units all ranks processed: every utterance's live frames
+  cells_per_step = int(nf_g.sum()) * U * C
   value = cells_per_step * args.steps / wall
 
   fwd_b, bwd_b, survey_b = algorithmic_bytes(T, U, V, C, checkpoints=ckpt)
   if fused:
     call_s = float(np.mean(fwd_ms)) * 1e-3
-    knames, design, design_b = loss_grad_design(B, T, U, V, n, C, device)
+    knames, design, design_b = loss_grad_design(len(idx), T, U, V, n, C, device)
     kernel = f"lt_loss_grad ({' + '.join(knames)})"
     kernels_ms = {'loss_grad': call_s * 1e3}
   else:
@@ -371,8 +536,9 @@ def main():
   # roofline: SURVEY 8(d)'s design-independent bytes per frame for every
   # design (the design's own bytes are reported beside it), over the C-ABI
   # call's own duration (HIP events on the stream the kernels run on)
-  achieved = survey_b * B * T / call_s / 1e9
-  traffic = read_traffic(args.pmc, knames, B, T)
+  frames_local = int(nf.sum())
+  achieved = survey_b * frames_local / call_s / 1e9
+  traffic = read_traffic(args.pmc, knames, len(idx), T)
 
   result = None
   if rank == 0:
@@ -381,6 +547,7 @@ def main():
         'value': value,
         'unit': 'cells/s',
         'n_gpus': world,
+        'rccl_world_size': rccl_world,
         'steps': args.steps,
         'warmup': args.warmup,
         'ms_per_step': wall / args.steps * 1e3,
@@ -388,15 +555,18 @@ def main():
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'f32',
-        'data': 'synthetic (randn arc weights, uniform labels, full-length utterances)',
+        'data': ('synthetic (randn arc weights, uniform labels, '
+                 f"{'U[T/2,T] lengths' if args.varlen else 'full-length utterances'}, "
+                 'global batch LPT-sharded over the ranks)'),
         'config': {
             'workload': (f'Log-semiring forward-backward (loss + dW), B={B}/GPU, T={T}, '
                          f'U={U}, V={V}, FullNGram n={n} (C={C}), fp32 (BASELINE configs[1]; '
                          f'configs[2] at 8 GPUs)'),
             'batch_per_gpu': B, 'global_batch': B * world, 'frames': T, 'labels': U,
             'vocab': V, 'context_size': n, 'context_states': C,
-            'parallelism': f'utterance-sharded x{world}, RCCL all-reduce of summed loss',
+            'parallelism': f'utterance-sharded x{world} (LPT), one RCCL all-reduce per step',
         },
+        'collectives_per_step': (calls / (args.steps + args.warmup)) if dist_on else 0,
         'design': design,
         'kernels_ms': kernels_ms,
         'roofline': {
@@ -409,10 +579,10 @@ def main():
             'traffic': traffic,
             'survey_bytes_per_frame': survey_b,
             'design_bytes_per_frame': design_b,
-            'traffic_bytes_per_frame': traffic / (B * T) if traffic else None,
+            'traffic_bytes_per_frame': traffic / frames_local if traffic else None,
         },
     }
-    result['step_gbs'] = survey_b * B * T * world / (wall / args.steps) / 1e9
+    result['step_gbs'] = survey_b * int(nf_g.sum()) / (wall / args.steps) / 1e9
     result['hbm_frac_step'] = result['step_gbs'] / HBM_PEAK_GBS
 
   # north-star shape (B=256 on one GPU), measured in the same run at N=1
@@ -421,8 +591,8 @@ def main():
     torch.cuda.empty_cache()
     W2, nf2, lab2, nl2 = make_inputs(256, T, U, V, C, device, seed=99)
     steps2 = max(5, args.steps // 2)
-    wall2, f2, b2 = run_steps(W2, nf2, lab2, nl2, V, n, steps2, 2, False, checkpoints=ckpt,
-                              fused=fused)
+    wall2, f2, b2, _ = run_steps(W2, nf2, lab2, nl2, V, n, steps2, 2, False, checkpoints=ckpt,
+                                 fused=fused)
     ms2 = wall2 / steps2 * 1e3
     call2 = float(np.mean(f2)) + (float(np.mean(b2)) if b2 else 0.0)
     result['north_star_b256'] = {
@@ -436,6 +606,8 @@ def main():
     }
     del W2
     torch.cuda.empty_cache()
+    if not args.no_weights and fused:
+      result['realistic_weights'] = weights_leg(B, T, U, V, n, C, device)
     if not args.no_joint:
       result['joint_weight_fn_step'] = joint_step_leg(T, U, V, n, device)
 

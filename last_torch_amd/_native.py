@@ -414,6 +414,13 @@ def grad_workspace_errors(workspace, W, vocab_size, context_size, max_labels, lo
   return int(workspace[off + 8:off + 12].view(torch.int32).item())
 
 
+def chunk_fallback_count(workspace, batch):
+  """Utterances the last chunked lt_loss_grad call on `workspace` sent to the
+  frame-serial kernels (the state's per-utterance fallback words, at its
+  start); diagnostic use, synchronises."""
+  return int(workspace[:4 * batch].view(torch.int32).ne(0).sum().item())
+
+
 def scale_grad(dW, grad, vocab_size, context_size):
   """lt_scale_grad: dW[b] *= grad[b] in place (no work where grad[b] == 1)."""
   pb = _problem(dW, vocab_size, context_size)

@@ -6,7 +6,8 @@ weights once through the ``WeightFn`` plugin as a contiguous
 [B, T, C, V+1] tensor and hands it to the HIP kernels in
 ``liblt_lattice.so`` through ``_native`` (C ABI: include/lt_lattice.h):
 
-  forward         -> lt_loss_forward / lt_loss_backward   (one launch each)
+  forward         -> lt_loss_grad (loss + dW, the design per shape);
+                     lt_scale_grad in the backward; lt_loss_forward without grad
   _forward        -> lt_den_forward (Log, MaxTropical, Real);
                      autograd: lt_den_backward (Log) / lt_viterbi arcs (Max)
   _forward_backward -> lt_den_forward + lt_den_backward
@@ -73,42 +74,35 @@ def _kernel_weights(W: torch.Tensor) -> torch.Tensor:
 class _LossFn(torch.autograd.Function):
   """loss = log_z - num (or -num), lattices.py:131-183, on the HIP kernels.
 
-  The forward keeps only what the backward needs: for the bigram (V <= 32)
-  the chunked scan's boundary state (lt_chunk_forward; ~12 MB at B=64,
-  T=1000 against dW's 279 MB), for other n-grams the forward alphas
-  (lt_loss_forward). dW is formed in the backward, already scaled by the
-  incoming gradient (lt_chunk_backward / lt_loss_backward): a forward that is
-  never differentiated costs no dW, and the graph can be backpropagated more
-  than once (retain_graph). Without a gradient only the loss is computed."""
+  With a gradient wanted, the forward is ONE lt_loss_grad call -- the loss
+  and d(sum loss)/dW together, in whichever design lt_loss_grad_design picks
+  for the shape (the chunked scan at the bench's B=64, the checkpointing
+  pipe + marginal pass at B=256, the trigram's checkpointing pair): exactly
+  what bench.py times, with the chunked path's per-frame certificate deciding
+  which utterances the frame-serial kernels redo. The backward scales that
+  dW by the incoming per-utterance gradient in place (lt_scale_grad: no work
+  where it is 1); a second backward (retain_graph) recomputes it. Without a
+  gradient only the loss is computed (lt_loss_forward)."""
 
   @staticmethod
   def forward(ctx, W, nf, labels, nl, V, n, local):
     ctx.cfg = (V, n, local)
-    ctx.mode = None
     if not ctx.needs_input_grad[0]:
       return _native.loss_forward(W, nf, labels, nl, V, n, local, want_alpha=False)[0]
-    B, T = W.shape[:2]
-    if _native.chunk_path(B, T, labels.shape[-1], V, n, W.device):
-      loss, _, _, state = _native.chunk_forward(W, nf, labels, nl, V, n, local)
-      ctx.mode = 'chunk'
-      ctx.save_for_backward(W, nf, labels, nl, state)
-    else:
-      loss, lz, num, alpha, an = _native.loss_forward(W, nf, labels, nl, V, n, local,
-                                                      want_alpha=True)
-      ctx.mode = 'alpha'
-      ctx.save_for_backward(W, nf, labels, nl, lz, num, alpha, an)
+    loss, _, _, dW = _native.loss_grad(W, nf, labels, nl, V, n, local)
+    ctx.dW = dW
+    ctx.save_for_backward(W, nf, labels, nl)
     return loss
 
   @staticmethod
   def backward(ctx, g):
     V, n, local = ctx.cfg
-    g = g.float().contiguous()
-    if ctx.mode == 'chunk':
-      W, nf, labels, nl, state = ctx.saved_tensors
-      dW = _native.chunk_backward(W, nf, labels, nl, V, n, local, state, grad=g)
-    else:
-      W, nf, labels, nl, lz, num, alpha, an = ctx.saved_tensors
-      dW = _native.loss_backward(W, nf, labels, nl, lz, num, alpha, an, g, V, n, local)
+    dW = ctx.dW
+    ctx.dW = None
+    if dW is None:  # a second backward through the same graph
+      W, nf, labels, nl = ctx.saved_tensors
+      dW = _native.loss_grad(W, nf, labels, nl, V, n, local)[3]
+    _native.scale_grad(dW, g.float().contiguous(), V, n)
     return dW, None, None, None, None, None, None
 
 

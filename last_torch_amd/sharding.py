@@ -47,25 +47,28 @@ def all_reduce_step(loss: torch.Tensor, params: Iterable[torch.nn.Parameter] = (
 
   Parameter gradients are summed in place (callers that want the mean
   divide by the global utterance count). Returns the global loss sum.
-  Without an initialised process group this is the identity.
-  """
+  Without an initialised process group this is the identity. A parameter
+  without a gradient on this rank (unused, or an empty shard) contributes
+  zeros to the bucket, so every rank all-reduces the same layout, and its
+  .grad stays None here: an optimizer does not treat it as trained, and the
+  other ranks' sum for it is not applied on this rank. Where a parameter
+  can be unused on some ranks only, GradBucket (every parameter always has
+  its gradient view) keeps the ranks' updates identical."""
   total = loss.detach().sum().reshape(1).to(torch.float32)
   if not (dist.is_available() and dist.is_initialized()):
     return total[0]
-  # every rank lays out the bucket from the full ordered parameter list: a
-  # parameter without a gradient on this rank (unused, or an empty shard)
-  # contributes zeros, so all ranks all-reduce buckets of the same layout
-  grads = []
+  params = list(params)
+  parts = [total]
   for p in params:
-    if p.grad is None:
-      p.grad = torch.zeros_like(p)
-    grads.append(p.grad)
-  flat = torch.cat([total] + [g.reshape(-1).to(torch.float32) for g in grads])
+    parts.append(torch.zeros([p.numel()], dtype=torch.float32, device=total.device)
+                 if p.grad is None else p.grad.reshape(-1).to(torch.float32))
+  flat = torch.cat(parts)
   dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
   off = 1
-  for g in grads:
-    k = g.numel()
-    g.copy_(flat[off:off + k].view_as(g).to(g.dtype))
+  for p in params:
+    k = p.numel()
+    if p.grad is not None:
+      p.grad.copy_(flat[off:off + k].view_as(p.grad).to(p.grad.dtype))
     off += k
   return flat[0]
 
@@ -74,29 +77,56 @@ class GradBucket:
   """The step's collective with no packing: one flat fp32 buffer [loss sum ||
   grads], the parameters' .grad set to views of it (as DDP's buckets do), so
   a step is the loss sum written into slot 0 and ONE all-reduce -- no
-  concatenate before it and no copy back after it. Parameters must be fp32
-  and keep the bucket's views as their gradients (backward accumulates into
-  them in place)."""
+  concatenate before it and no copy back after it. Parameters must be fp32.
+  Backward accumulates into the views in place; ``zero_grad()`` (instead of
+  the optimizer's, whose default set_to_none would detach .grad from the
+  bucket) clears them for the next step, and ``all_reduce_step`` re-binds any
+  .grad that was replaced or dropped (copying a replaced gradient's values
+  into the bucket first), so the reduced buffer is always the one the
+  optimizer steps on."""
 
   def __init__(self, params: Iterable[torch.nn.Parameter], device=None):
     self.params = list(params)
     n = sum(p.numel() for p in self.params)
     dev = device if device is not None else (self.params[0].device if self.params else 'cpu')
     self.flat = torch.zeros([1 + n], dtype=torch.float32, device=dev)
+    self.views = []
+    self.calls = 0  # all-reduces issued (one per step)
     off = 1
     for p in self.params:
       if p.dtype != torch.float32:
         raise TypeError(f'GradBucket: parameters must be float32, got {p.dtype}')
       k = p.numel()
-      p.grad = self.flat[off:off + k].view_as(p)
+      v = self.flat[off:off + k].view_as(p)
+      self.views.append(v)
+      p.grad = v
       off += k
+
+  def zero_grad(self) -> None:
+    """Zeros every gradient (and the loss slot) in place, keeping the views."""
+    self.flat.zero_()
+    self._bind()
+
+  def _bind(self) -> None:
+    for p, v in zip(self.params, self.views):
+      g = p.grad
+      if g is None:
+        v.zero_()
+      elif g.data_ptr() != v.data_ptr():
+        # optimizer.zero_grad(set_to_none) then backward made a fresh tensor
+        v.copy_(g)
+      else:
+        continue
+      p.grad = v
 
   def all_reduce_step(self, loss: torch.Tensor, group: Optional[dist.ProcessGroup] = None
                       ) -> torch.Tensor:
     """all-reduce(SUM) of [loss.sum() || grads] in place; returns the global
     loss sum (the identity without an initialised process group)."""
+    self._bind()
     torch.sum(loss.detach().reshape(-1).to(torch.float32), dim=0, keepdim=True,
               out=self.flat[:1])
     if dist.is_available() and dist.is_initialized():
       dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+      self.calls += 1
     return self.flat[0]

@@ -62,6 +62,49 @@ def assert_values_close(got, ref, rtol=1e-5, atol=1e-5):
   np.testing.assert_allclose(got[fin], ref[fin], rtol=rtol, atol=atol)
 
 
+def marginal_scale(ref, den, log_z, num, bf16=False):
+  """Per-element tolerance of a loss gradient dW = g (den - num) against a
+  float64 reference: 1e-8 + (1e-4 + 4 * 2^-24 * max(1, |log_z_b|, |num_b|))
+  * (den + num), den / num the arc's denominator / numerator marginals
+  (alignments.py:300-318: exp(alpha + w + beta - log_z)). Each marginal is an
+  exponential of an fp32 log-space sum of terms of magnitude ~|log_z| (or
+  |num|), so its rounding is relative to the marginal itself, not absolute:
+  an arc whose marginals are 1e-6 is checked to ~1e-9. `den` None: a locally
+  normalised loss (no denominator; num = -ref). bf16 dW adds its own
+  rounding, 2^-8 (den + num)."""
+  ref = np.asarray(ref, np.float64)
+  if den is None:
+    den = np.zeros_like(ref)
+    nm = -ref
+  else:
+    den = np.asarray(den, np.float64)
+    nm = den - ref
+  nm = np.maximum(nm, 0.0)
+  mag = np.maximum(1.0, np.abs(np.where(np.isfinite(log_z), log_z, 0.0)))
+  if num is not None:
+    mag = np.maximum(mag, np.abs(np.where(np.isfinite(num), num, 0.0)))
+  rel = 1e-4 + 4 * 2.0 ** -24 * mag.astype(np.float64) + (2.0 ** -8 if bf16 else 0.0)
+  return 1e-8 + rel.reshape([-1] + [1] * (ref.ndim - 1)) * (den + nm)
+
+
+def grad_error_ratio(got, ref, den, log_z, num, bf16=False):
+  """|got - ref| / marginal_scale: <= 1 everywhere passes."""
+  got = np.asarray(got, np.float64)
+  ref = np.asarray(ref, np.float64)
+  return np.abs(got - ref) / marginal_scale(ref, den, log_z, num, bf16)
+
+
+def assert_grad_marginal_close(got, ref, den, log_z, num, bf16=False):
+  """Every dW element within marginal_scale (relative to its own marginals),
+  plus the absolute check of assert_grad_close as a secondary bound."""
+  r = grad_error_ratio(got, ref, den, log_z, num, bf16)
+  bad = ~(r <= 1.0)
+  assert not bad.any(), (f'{int(bad.sum())} of {bad.size} dW elements beyond the marginal bound; '
+                         f'worst ratio {float(np.nanmax(r)):.3g} at '
+                         f'{np.argwhere(bad)[0].tolist()}')
+  assert_grad_close(got, ref, log_z, bf16=bf16, num=num)
+
+
 def assert_grad_close(got, ref, log_z, bf16=False, num=None):
   """Arc-marginal gradients: per utterance b,
   |got - ref| <= 1e-5 + 1e-6 * max(1, |log_z_b|, |num_b|) (+ 8e-3 relative

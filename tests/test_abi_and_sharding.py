@@ -95,32 +95,54 @@ def test_lpt_shards_are_balanced_and_disjoint():
 
 
 def _gloo_worker(rank, world, port, payload, out_q):
+  """One rank: its LPT shard through the product's CPU path
+  (RecognitionLattice on host tensors -> cpu.py) with the arc weights as a
+  trainable table, loss.sum().backward() into a GradBucket, then the step's
+  one all-reduce; a second step after bucket.zero_grad()."""
   os.environ['MASTER_ADDR'] = '127.0.0.1'
   os.environ['MASTER_PORT'] = str(port)
   dist.init_process_group('gloo', rank=rank, world_size=world)
   try:
-    from oracle import oracle as orc  # test infrastructure: the per-shard compute
+    import last_torch_amd as lt
     W, nf, lab, nl, V, n = payload
     idx = sharding.local_shard(torch.tensor(nf), rank, world)
-    loss, _, _, dW = orc.loss_grad(W[idx], nf[idx], lab[idx], nl[idx], V, n)
-    # a stand-in weight-fn parameter whose grad is exercised by the bucket
+    table = torch.nn.Parameter(torch.tensor(W[idx]))
+    head = torch.nn.Parameter(torch.zeros(W.shape[-2:]))  # shared by every rank
+    bucket = sharding.GradBucket([head])
+    wfn = lt.weight_fns.TableWeightFn(table.detach())  # a plain tensor attribute
+    lat = lt.RecognitionLattice(context=lt.contexts.FullNGram(vocab_size=V, context_size=n),
+                                alignment=lt.alignments.FrameDependent(),
+                                weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+                                weight_fn_factory=lambda _: wfn)
+    T = W.shape[1]
+    frames = torch.arange(T, dtype=torch.float32)[None, :, None].expand(len(idx), T, 1)
+    totals, head_grads = [], []
+    for _ in range(2):
+      bucket.zero_grad()
+      table.grad = None
+      wfn.table = table + head
+      loss = lat(frames, torch.tensor(nf[idx]), torch.tensor(lab[idx]), torch.tensor(nl[idx]))
+      loss.sum().backward()
+      assert head.grad.data_ptr() == bucket.flat[1:].data_ptr()
+      totals.append(float(bucket.all_reduce_step(loss)))
+      head_grads.append(head.grad.numpy().copy())
+    # the functional form: a parameter unused on this rank keeps grad None
     p = torch.nn.Parameter(torch.zeros(5))
+    unused = torch.nn.Parameter(torch.zeros(3))
     p.grad = torch.full([5], float(rank + 1))
-    total = sharding.all_reduce_step(torch.tensor(loss), [p])
-    # the same exchange through a persistent bucket (grads are views of it)
-    q = torch.nn.Parameter(torch.zeros(2, 3))
-    bucket = sharding.GradBucket([q])
-    q.grad.fill_(float(rank + 1))
-    total2 = bucket.all_reduce_step(torch.tensor(loss))
-    assert q.grad.data_ptr() == bucket.flat[1:].data_ptr()
-    out_q.put((rank, idx, loss, dW, float(total), p.grad.numpy().copy(), float(total2),
-               q.grad.numpy().copy()))
+    total3 = float(sharding.all_reduce_step(loss, [p, unused]))
+    out_q.put((rank, idx, loss.detach().numpy(), table.grad.numpy().copy(), totals, head_grads,
+               p.grad.numpy().copy(), unused.grad is None, total3, bucket.calls))
   finally:
     dist.destroy_process_group()
 
 
 def test_gloo_world2_sharded_loss_matches_full_batch():
-  from oracle import oracle as orc
+  """world_size-2 gloo: each rank's shard through the product's CPU path;
+  per-shard losses and dW reassemble to the oracle's full batch, and the one
+  all-reduce per step gives the global loss sum and the summed head
+  gradient on both ranks, on two consecutive steps (zero_grad between)."""
+  from oracle import oracle as orc  # the checker
   rng = np.random.default_rng(3)
   B, T, U, V, n = 6, 9, 3, 3, 1
   C = orc.num_states(V, n)
@@ -143,12 +165,53 @@ def test_gloo_world2_sharded_loss_matches_full_batch():
     assert p.exitcode == 0
   loss = np.zeros(B, np.float32)
   dW = np.zeros_like(full_dW)
-  for rank, idx, l, g, total, pgrad, total2, qgrad in res:
+  for rank, idx, l, g, totals, head_grads, pgrad, unused_none, total3, calls in res:
     loss[idx] = l
     dW[idx] = g
-    np.testing.assert_allclose(total, full_loss.sum(), rtol=1e-6)
+    for total in totals + [total3]:
+      np.testing.assert_allclose(total, full_loss.sum(), rtol=1e-5)
+    # the head's gradient is the sum of every utterance's dW, on both steps
+    for hg in head_grads:
+      np.testing.assert_allclose(hg, full_dW.sum(axis=(0, 1)), atol=1e-5)
     np.testing.assert_array_equal(pgrad, np.full(5, 3.0))  # 1 + 2
-    np.testing.assert_allclose(total2, full_loss.sum(), rtol=1e-6)
-    np.testing.assert_array_equal(qgrad, np.full((2, 3), 3.0))
-  np.testing.assert_array_equal(loss, full_loss)
-  np.testing.assert_array_equal(dW, full_dW)
+    assert unused_none
+    assert calls == 2  # one all-reduce per step
+  np.testing.assert_allclose(loss, full_loss, rtol=1e-5, atol=1e-5)
+  np.testing.assert_allclose(dW, full_dW, atol=1e-5)
+
+
+def test_bench_launcher_n2_cpu():
+  """bench.py --gpus 2 without a torch.distributed environment starts its
+  own two ranks (torch.distributed.run as a child), every rank sees world
+  size 2, the global batch is LPT-sharded, one all-reduce per step, one
+  JSON line whose global loss sum is the oracle's."""
+  import json
+  import subprocess
+  import sys
+  from oracle import oracle as orc
+  import bench
+  env = dict(os.environ)
+  env.pop('WORLD_SIZE', None)
+  B, T, U, V = 3, 8, 3, 3
+  out = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2',
+                        '--device', 'cpu', '--batch', str(B), '--frames', str(T), '--labels',
+                        str(U), '--vocab', str(V), '--steps', '2', '--warmup', '1',
+                        '--varlen'], capture_output=True, text=True, timeout=240, env=env,
+                       cwd='/tmp')
+  assert out.returncode == 0, out.stderr[-2000:]
+  line = [x for x in out.stdout.splitlines() if x.startswith('{')]
+  assert len(line) == 1, out.stdout
+  r = json.loads(line[0])
+  assert r['ranks'] == 2 and r['gloo_world_size'] == 2
+  assert r['collectives_per_step'] == 1.0
+  assert r['shard_sizes'] == [3, 3]
+  nf, lab, nl = bench.global_batch(2 * B, T, U, V, 1234, True)
+  W = bench.shard_weights(range(2 * B), T, V + 1, V, 'cpu', 1234).numpy()
+  ref, _, _, _ = orc.loss_grad(W, nf.numpy(), lab.numpy(), nl.numpy(), V, 1, want_grad=False)
+  np.testing.assert_allclose(r['global_loss_sum'], ref.sum(), rtol=1e-5)
+  # a mismatched world is refused
+  env2 = dict(env, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0')
+  bad = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2',
+                        '--device', 'cpu'], capture_output=True, text=True, timeout=120, env=env2,
+                       cwd='/tmp')
+  assert bad.returncode != 0 and 'WORLD_SIZE=1' in bad.stderr

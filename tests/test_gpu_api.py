@@ -1,8 +1,8 @@
 """The RecognitionLattice API surface on the HIP kernels (the CPU twin is
 tests/test_lattice_api.py): the ``_backward`` callback, gradients through
-``_forward``, and the autograd contract of ``forward`` (dW formed in the
-backward from the chunked scan's state, scaled by the incoming gradient;
-a second backward with retain_graph)."""
+``_forward``, and the autograd contract of ``forward`` (dW from the
+forward's lt_loss_grad, scaled by the incoming gradient; a second backward
+with retain_graph)."""
 import numpy as np
 import pytest
 import torch
@@ -32,9 +32,9 @@ def test_forward_gradients_gpu(cuda, case):
 
 @pytest.mark.parametrize('V,n', [(32, 1), (3, 2)])
 def test_loss_autograd_contract(cuda, V, n):
-  """forward keeps no dW: the backward forms it with the incoming gradient
-  (bigram: lt_chunk_backward; trigram: lt_loss_backward from the forward
-  alphas); a second backward (retain_graph) gives the same gradient."""
+  """forward is one lt_loss_grad call (loss and dW together, the design the
+  shape picks); the backward scales dW by the incoming gradient; a second
+  backward (retain_graph) recomputes it and gives the same gradient."""
   from oracle import oracle as orc  # test infrastructure only
   rng = np.random.default_rng(3)
   B, T, U = 5, 40, 6

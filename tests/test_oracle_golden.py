@@ -126,3 +126,36 @@ def test_marginals_sum_to_one_per_frame():
   s = dW.reshape(B, T, -1).sum(-1)
   expect = (np.arange(T)[None, :] < nf[:, None]).astype(np.float64)
   np.testing.assert_allclose(s, expect, atol=1e-5)
+
+
+def test_marginal_bound_negative_control():
+  """The per-element dW bound (golden_cases.marginal_scale) at the bench
+  shape: the oracle's own float32 dW of one B=1, T=1000, U=100 bigram
+  utterance passes it; the same dW with every element below 4e-3 in
+  magnitude zeroed (what round 2's absolute slack of ~1e-6 |log_z| let
+  through) fails it, and so does a single low-probability arc off by 1e-6."""
+  from golden_cases import assert_grad_marginal_close, grad_error_ratio, marginal_scale
+  rng = np.random.default_rng(40)
+  T, U, V, n = 1000, 100, 32, 1
+  W = rng.standard_normal((1, T, V + 1, V + 1)).astype(np.float32)
+  nf = np.array([T], np.int32)
+  lab = rng.integers(1, V + 1, (1, U)).astype(np.int32)
+  nl = np.array([U], np.int32)
+  _, lz, num, dW = orc.loss_grad(W, nf, lab, nl, V, n)
+  _, den = orc.den_grad(W, nf, V, n)
+  assert abs(float(lz[0])) > 1000  # the regime where the absolute slack was ~4e-3
+  assert_grad_marginal_close(dW, dW, den, lz, num)
+  zeroed = np.where(np.abs(dW) < 4e-3, 0.0, dW).astype(np.float32)
+  assert (zeroed != dW).mean() > 0.5
+  with pytest.raises(AssertionError):
+    assert_grad_marginal_close(zeroed, dW, den, lz, num)
+  # one arc of tiny marginal perturbed by 1e-6
+  scale = marginal_scale(dW, den, lz, num)
+  i = np.unravel_index(np.argmin(scale), scale.shape)
+  bumped = dW.copy()
+  bumped[i] += 1e-6
+  assert grad_error_ratio(bumped, dW, den, lz, num).max() > 1
+  with pytest.raises(AssertionError):
+    assert_grad_marginal_close(bumped, dW, den, lz, num)
+  # the frame sums of the round-2 style absolute bound would not see it
+  assert 1e-6 < 1e-5 + 1e-6 * abs(float(lz[0]))
