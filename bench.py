@@ -305,12 +305,12 @@ def chunk_len(B, T, U, V):
   NPG = (U + 2) & ~1
   CP = (V + 4) & ~3
   al16 = lambda x: (x + 15) & ~15
-  budget = int(os.environ.get('LT_CHUNK_LDS', 40 * 1024))
-  L = max(1, min(32, int(os.environ.get('LT_CHUNK_LEN', 32))))
+  budget = 40 * 1024
+  L = 32
   while True:
     n16 = (L * FB + 30) // 16
     b = ((n16 + 63) // 64) * 1024 + 2 * al16(4 * L * CP) + 2 * al16(4 * L * NPG) + \
-        al16(8 * L * NPG) + al16(32 * L) + al16(8 * NPG + 4 * U) + al16(4 * L) + 1024 + al16(4 * (2 * L + 1))
+        al16(8 * L * NPG) + al16(32 * L) + al16(8 * NPG + 4 * U) + al16(4 * L) + 1024 + al16(4 * (2 * L + 2))
     if L <= 4 or b <= budget:
       return L
     L -= 1

@@ -283,8 +283,8 @@ int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* 
                      float* path_weight, void* workspace, size_t workspace_bytes,
                      void* stream);
 
-/* The design lt_loss_grad runs for *pb (the environment overrides LT_CHUNK,
- * LT_CHECKPOINTS, LT_FUSED apply as in the call): LT_DESIGN_CHUNK the chunked
+/* The design lt_loss_grad runs for *pb (a function of the shape and the
+ * device's CU count only; the library reads no environment): LT_DESIGN_CHUNK the chunked
  * two-level scan (bigram, 5 * batch <= 3 * CUs), LT_DESIGN_FUSED_PIPE one
  * pipelined launch with the marginals beside the recursions,
  * LT_DESIGN_CHECKPOINTS alpha || beta with checkpoints then one streaming
@@ -295,7 +295,20 @@ int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* 
 #define LT_DESIGN_FUSED_PIPE 1
 #define LT_DESIGN_CHECKPOINTS 2
 #define LT_DESIGN_RECURSION 3
+#define LT_DESIGN_AUTO (-1)
 int lt_loss_grad_design(const lt_problem* pb, int32_t* design);
+/* lt_loss_grad with the design given explicitly (LT_DESIGN_AUTO: the call's
+ * own choice, as lt_loss_grad): for callers that time or test one design at
+ * a shape where lt_loss_grad would pick another. LT_EUNSUPPORTED when the
+ * shape cannot take it (LT_DESIGN_CHUNK and LT_DESIGN_FUSED_PIPE are bigram
+ * designs). Replaces the LT_CHUNK / LT_CHECKPOINTS / LT_FUSED environment
+ * overrides of round 2. */
+int lt_loss_grad_workspace_bytes_ex(const lt_problem* pb, int32_t local_norm, int32_t design,
+                                    size_t* bytes);
+int lt_loss_grad_ex(const lt_problem* pb, int32_t local_norm, int32_t design, const void* W,
+                    const int32_t* num_frames, const int32_t* labels,
+                    const int32_t* num_labels, float* loss, float* log_z, float* num,
+                    void* dW, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Joint weight function on the matrix cores (replaces
  * the hidden-tensor path of JointWeightFn.forward, weight_fns.py:174-227):

@@ -63,6 +63,9 @@ _SIG = {
     'lt_loss_grad_workspace_bytes': [ctypes.POINTER(Problem), _I32,
                                      ctypes.POINTER(ctypes.c_size_t)],
     'lt_loss_grad': [ctypes.POINTER(Problem), _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
+    'lt_loss_grad_workspace_bytes_ex': [ctypes.POINTER(Problem), _I32, _I32,
+                                        ctypes.POINTER(ctypes.c_size_t)],
+    'lt_loss_grad_ex': [ctypes.POINTER(Problem), _I32, _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
     'lt_scale_grad': [ctypes.POINTER(Problem), _P, _P, _P],
     'lt_chunk_workspace_bytes': [ctypes.POINTER(Problem), _I32, ctypes.POINTER(ctypes.c_size_t),
                                  ctypes.POINTER(ctypes.c_size_t)],
@@ -200,10 +203,7 @@ def prefer_checkpoints(batch, device=None, shape=None):
   bigram recursions (`shape` = (frames, labels, vocab_size, context_size,
   bf16)), up to 1.5 CUs of utterances; beyond that the single-workgroup
   recursion backward (marginals fused into the beta recursion) is faster.
-  Mirrors lt_loss_grad. LT_CHECKPOINTS=0/1 forces the choice."""
-  env = os.environ.get('LT_CHECKPOINTS')
-  if env in ('0', '1'):
-    return env == '1'
+  Mirrors lt_loss_grad_design."""
   cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
   if 2 * batch <= cus:
     return True
@@ -213,9 +213,7 @@ def prefer_checkpoints(batch, device=None, shape=None):
 def pipe_path(batch, frames, labels, vocab_size, context_size, bf16=False):
   """Whether lt_loss_forward with checkpoints runs the pipelined bigram
   recursions (lt_pipe.hip, kernel ``pipe_kernel``) for this shape; mirrors
-  lt_impl::pipe_eligible. LT_NO_PIPE=1 turns them off."""
-  if os.environ.get('LT_NO_PIPE', '0') not in ('', '0'):
-    return False
+  lt_impl::pipe_eligible."""
   if context_size != 1 or not 1 <= vocab_size <= 32 or labels + 1 > 256:
     return False
   C = vocab_size + 1
@@ -278,17 +276,13 @@ def chunk_path(batch, frames, labels, vocab_size, context_size, device=None):
   """Whether lt_loss_grad runs the chunked two-level scan (lt_chunk.hip) for
   this shape; mirrors lt_impl::chunk_preferred: an eligible shape and
   5 * batch <= 3 * CUs (beyond that the frame-serial checkpointing design is
-  faster, tools/design_ab.py). LT_CHUNK=0 turns it off, LT_CHUNK=1 forces it
-  for any batch."""
-  env = os.environ.get('LT_CHUNK', '')
-  if env == '0':
-    return False
+  faster, tools/design_ab.py)."""
   if context_size != 1 or not 1 <= vocab_size <= 32 or labels + 1 > 128 or frames < 1:
     return False
   C = vocab_size + 1
   if batch * frames * C * C >= 2 ** 31:
     return False
-  if env == '1' or not torch.cuda.is_available():
+  if not torch.cuda.is_available():
     return True
   cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
   return 5 * batch <= 3 * cus
@@ -296,26 +290,23 @@ def chunk_path(batch, frames, labels, vocab_size, context_size, device=None):
 
 def fused_path(batch, frames, labels, vocab_size, context_size, device=None, bf16=False):
   """Whether lt_loss_grad runs as ONE fused pipe launch for this shape
-  (mirrors lt_loss_grad: not the chunked path, checkpointing batch size, 2B
-  below the CU count, pipe shape; LT_FUSED=0/1 forces the choice)."""
+  (mirrors lt_loss_grad_design: not the chunked path, checkpointing batch
+  size, 2B below the CU count, pipe shape)."""
   if chunk_path(batch, frames, labels, vocab_size, context_size, device):
     return False
   cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
-  env = os.environ.get('LT_FUSED', '')
-  want = (env != '0') if env else 2 * batch < cus
-  return (want and prefer_checkpoints(batch, device) and
+  return (2 * batch < cus and prefer_checkpoints(batch, device) and
           pipe_path(batch, frames, labels, vocab_size, context_size, bf16))
 
 
-DESIGN_CHUNK, DESIGN_FUSED_PIPE, DESIGN_CHECKPOINTS, DESIGN_RECURSION = 0, 1, 2, 3
+DESIGN_AUTO, DESIGN_CHUNK, DESIGN_FUSED_PIPE, DESIGN_CHECKPOINTS, DESIGN_RECURSION = -1, 0, 1, 2, 3
 DESIGN_NAMES = {DESIGN_CHUNK: 'chunk', DESIGN_FUSED_PIPE: 'fused_pipe',
                 DESIGN_CHECKPOINTS: 'checkpoints', DESIGN_RECURSION: 'recursion'}
 
 
 def loss_grad_design(batch, frames, labels, vocab_size, context_size, bf16=False):
   """lt_loss_grad_design: the design lt_loss_grad runs for this shape on the
-  current device (DESIGN_* above; the LT_CHUNK / LT_CHECKPOINTS / LT_FUSED
-  overrides apply)."""
+  current device (DESIGN_* above)."""
   pb = Problem(batch, frames, vocab_size, context_size, labels,
                LT_DTYPE_BF16 if bf16 else LT_DTYPE_F32)
   out = ctypes.c_int32(-1)
@@ -323,35 +314,34 @@ def loss_grad_design(batch, frames, labels, vocab_size, context_size, bf16=False
   return out.value
 
 
-def loss_grad_workspace_bytes(W, vocab_size, context_size, max_labels, local_norm):
+def loss_grad_workspace_bytes(W, vocab_size, context_size, max_labels, local_norm,
+                              design=DESIGN_AUTO):
   pb = _problem(W, vocab_size, context_size, max_labels)
   out = ctypes.c_size_t(0)
-  _check(lib().lt_loss_grad_workspace_bytes(ctypes.byref(pb), int(bool(local_norm)),
-                                            ctypes.byref(out)), 'lt_loss_grad_workspace_bytes')
+  _check(lib().lt_loss_grad_workspace_bytes_ex(ctypes.byref(pb), int(bool(local_norm)),
+                                               int(design), ctypes.byref(out)),
+         'lt_loss_grad_workspace_bytes_ex')
   return out.value
 
 
 def loss_grad(W, num_frames, labels, num_labels, vocab_size, context_size, local_norm,
-              workspace=None):
-  """lt_loss_grad: (loss, log_z, num, dW) with dW = d(sum loss)/dW in one call
-  (for the bigram a single launch: recursions and marginals overlapped).
-  ``workspace`` (uint8 device tensor of lt_loss_grad_workspace_bytes) is
+              workspace=None, design=DESIGN_AUTO):
+  """lt_loss_grad(_ex): (loss, log_z, num, dW) with dW = d(sum loss)/dW in one
+  call, in `design` (DESIGN_AUTO: the call's own choice for the shape).
+  ``workspace`` (uint8 device tensor of loss_grad_workspace_bytes) is
   allocated when not given."""
   U = labels.shape[-1]
   pb = _problem(W, vocab_size, context_size, U)
   B = W.shape[0]
-  ws_bytes = ctypes.c_size_t(0)
-  _check(lib().lt_loss_grad_workspace_bytes(ctypes.byref(pb), int(bool(local_norm)),
-                                            ctypes.byref(ws_bytes)),
-         'lt_loss_grad_workspace_bytes')
-  if workspace is None or workspace.numel() < ws_bytes.value:
-    workspace = torch.empty([max(ws_bytes.value, 1)], dtype=torch.uint8, device=W.device)
+  nbytes = loss_grad_workspace_bytes(W, vocab_size, context_size, U, local_norm, design)
+  if workspace is None or workspace.numel() < nbytes:
+    workspace = torch.empty([max(nbytes, 1)], dtype=torch.uint8, device=W.device)
   loss, log_z, num = _f32([B], W), _f32([B], W), _f32([B], W)
   dW = torch.empty_like(W)
-  _check(lib().lt_loss_grad(ctypes.byref(pb), int(bool(local_norm)), _ptr(W), _ptr(num_frames),
-                            _ptr(labels), _ptr(num_labels), _ptr(loss), _ptr(log_z), _ptr(num),
-                            _ptr(dW), _ptr(workspace), workspace.numel(), _stream()),
-         'lt_loss_grad')
+  _check(lib().lt_loss_grad_ex(ctypes.byref(pb), int(bool(local_norm)), int(design), _ptr(W),
+                               _ptr(num_frames), _ptr(labels), _ptr(num_labels), _ptr(loss),
+                               _ptr(log_z), _ptr(num), _ptr(dW), _ptr(workspace),
+                               workspace.numel(), _stream()), 'lt_loss_grad_ex')
   return loss, log_z, num, dW
 
 

@@ -55,14 +55,15 @@ namespace {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
 
-constexpr float kRange = 60.f;  // max - min of a frame's weights on the fast path
-constexpr float kEmin = 0x1p-88f;  // < e^-(kRange + 1): the exponential form of the range test
-constexpr float kLn2 = 0.6931471805599453f;
+// the strict range (lt_chunk_forward's fast path): every weight of a frame
+// within e^61 of its max, as E = exp(W - c) >= kEmin
+constexpr float kEmin = 0x1p-88f;
 constexpr int kRec = 1248;      // floats per chunk record (whole 128-byte lines)
 constexpr int kRowT = 36;       // row stride of the transposed core in a record
 constexpr int kChunkLds = 40 * 1024;  // phase C LDS per workgroup (four per CU)
 constexpr int kMargWaves = 4;   // phase C: waves per workgroup (recursions on 0-3)
 constexpr int kGrp = 7;         // frames per numerator group (band offsets 0..kGrp)
+constexpr float kCert = 64.f;   // phase C's per-frame certificate: log2(max alpha max beta e^c / Z)
 #ifndef LT_AB_WAVES
 #define LT_AB_WAVES 3
 #endif
@@ -108,6 +109,8 @@ struct CkArgs {
   int nc, wpos;            // ck_ab_kernel: nc walking workgroups (B fused, 0 not) from block wpos
   int nbs;                 // floats per chunk of numerator bands (whole 128-byte lines)
   int local;               // LocallyNormalizedWeightFn: no denominator
+  int strict;              // 1 (lt_chunk_forward): a chunk outside the strict range (flag 3)
+                           // leaves the fast path in B; 0: phase C's certificate decides
   int dbg;                 // diagnostic builds (LT_DIAG) only: role ablations
   long long* stamps;       // diagnostic builds only: per-workgroup s_memtime marks
   long long FB;            // bytes per frame
@@ -125,10 +128,10 @@ LT_DEVINL float half_sum(float v) {
   auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
   return __int_as_float(p[0]) + __int_as_float(p[1]);
 }
-// lane l & 31's value in both halves
-LT_DEVINL float half_lo(float v) {
+// lane l ^ 32's value
+LT_DEVINL float half_other(float v) {
   auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
-  return (threadIdx.x & 32) ? __int_as_float(p[0]) : v;
+  return (threadIdx.x & 32) ? __int_as_float(p[0]) : __int_as_float(p[1]);
 }
 // lane l gets v of lane l-1 (lane 0: fill)
 LT_DEVINL float from_prev(float v, float fill) {
@@ -143,12 +146,6 @@ LT_DEVINL float rot_next(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xF, 0xF, false));
 }
 
-// Log-semiring plus of two terms, semirings.py:248-255 (non-finite max -> 0)
-LT_DEVINL float lse2(float a, float b) {
-  float c = fmaxf(a, b);
-  c = __builtin_isfinite(c) ? c : 0.f;
-  return c + lt_log(lt_exp(a - c) + lt_exp(b - c));
-}
 LT_DEVINL float safe_max(float m) { return __builtin_isfinite(m) ? m : 0.f; }
 #ifdef LT_DIAG
 #define CK_STAMP(k)                                                                  \
@@ -397,8 +394,10 @@ LT_DEVINL void st_wt4(__amdgpu_buffer_rsrc_t r, int idx, float x, float y, float
 // Chunk k of utterance b: the transfer record, the numerator bands and the
 // frame offsets, then the hand-off to phase B: record and bands stored
 // write-through (sc1), the wave's s_waitcnt vmcnt(0), then one relaxed
-// agent-scope flag store (1, or 2 for a chunk outside the range); phase B
-// polls it and acquires (ChunkReady).
+// agent-scope flag store (1: inside the strict range; 3: a masked (-inf) or
+// far-below-max weight, which only the relaxed path takes, under phase C's
+// per-frame certificate; 2: a NaN / +inf weight or an all -inf frame, always
+// the frame-serial kernels); phase B polls it and acquires (ChunkReady).
 template <bool BF16, int PPL, bool FULL>
 LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   __shared__ __attribute__((aligned(16))) float s_rt[4][32];
@@ -442,9 +441,9 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   for (int r = 0; r < 16; ++r) X[r] = (kstep(r, h) == i && i < V) ? 1.f : 0.f;
   int ej = 0;         // column power-of-two scale (lane's column)
   int rho = -100000;  // rt scale (log2)
-  float pi = 0.f;     // log P00 - csum
-  float csum = 0.f;   // sum of c_t (integers)
-  int bad = 0;
+  float pi = 0.f;     // log2 P00 - csum
+  float csum = 0.f;   // sum of the frames' offsets c_t (integers, log2 units)
+  int bad = 0;        // 2: a NaN / +inf weight or an all -inf frame; 3: outside the strict range
   // numerator group bands: nbd[r][d] = log2 weight of the paths from
   // position s = lane + 64 r at the group's first frame to s + d after its
   // last (the string lattice's frame steps, lattices.py:340-377, composed)
@@ -497,40 +496,48 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
       }
       __builtin_amdgcn_wave_barrier();
     }
-    // the frame's offset c = ceil(max W) (masked values are -inf)
+    // the frame's offset c = ceil(max W log2 e), an integer in log2 units
+    // (masked values are -inf), so every sum of offsets is exact
     float mx = max3_raw(F.wr0, F.wbl, F.w[15]);
 #pragma unroll
     for (int s = 0; s < 15; s += 3) mx = max3_raw(mx, max3_raw(F.w[s], F.w[s + 1], F.w[s + 2]), mx);
     mx = wmax_u(mx);
     const bool cfin = __builtin_isfinite(mx);
-    const float c = cfin ? ceilf(mx) : 0.f;
-    const float cl = c * kLog2e;
-    if (lane == 0) a.cf[(long long)b * a.T + t0 + f] = c;
+    const float cl = cfin ? ceilf(mx * kLog2e) : 0.f;
+    if (lane == 0) a.cf[(long long)b * a.T + t0 + f] = cl;
     // E_t^T as the A operand: lane (i, h), k-step s -> E[k][i]. The core
     // diagonal's blank self loop (alignments.py:294-297) is added beside
     // the product (Dg X after the MFMAs, rt Dg in the state-0 row), which
     // keeps the lane's diagonal k-step out of the registers.
-    // The range test rides on the exponentials: every live E >= e^-61
-    // (max - min <= kRange + 1; a NaN or -inf weight fails it, +inf fails cfin)
+    // Flags ride on the exponentials: a NaN weight gives a NaN E (fails
+    // e >= 0); a weight below e^-61 of the frame's max, or -inf, gives
+    // E < kEmin (outside the strict range, kept as an exact zero or a
+    // small value: the relaxed path's per-frame certificate covers it).
     const float dgv = (FULL || i < V) ? lt_exp_off(F.wdg, cl) : 0.f;
     if (lane < 32) sdg[lane] = dgv;
     float A[16];
-    bool lbad = (lane <= V) && !(F.wbl >= c - (kRange + 1.f));
+    const float ebl = lt_exp_off(F.wbl, cl);
+    bool lnan = (lane <= V) && !(ebl >= 0.f);
+    bool lwide = (lane <= V) && !(ebl >= kEmin);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const bool live = FULL || (kstep(s, h) < V && i < V);
       const float e = lt_exp_off(F.w[s], cl);
-      lbad = lbad || (live && !(e >= kEmin));
+      lnan = lnan || (live && !(e >= 0.f));
+      lwide = lwide || (live && !(e >= kEmin));
       A[s] = live ? e : 0.f;
     }
     const float e0r = lt_exp_off(F.wr0, cl);
     const float e0 = (FULL || i < V) ? e0r : 0.f;
-    lbad = lbad || ((FULL || i < V) && !(e0r >= kEmin));
-    if (!cfin || __builtin_amdgcn_ballot_w64(lbad)) bad = 1;
+    lnan = lnan || ((FULL || i < V) && !(e0r >= 0.f));
+    lwide = lwide || ((FULL || i < V) && !(e0r >= kEmin));
+    if (!cfin || __builtin_amdgcn_ballot_w64(lnan)) bad = 2;
+    else if (bad == 0 && __builtin_amdgcn_ballot_w64(lwide)) bad = 3;
     const float w00 = F.w00;
     if (reload) load_frame<BF16, PPL, FULL>(frame_ptr(f + 1), frame_bytes(f + 1), fo, F);
 
-    // state-0 row: r' = p00 * e0 + r Ec (VALU, beside the MFMAs)
+    // state-0 row: r' = p00 * e0 + r Ec (VALU, beside the MFMAs), scaled by
+    // a power of two so that its largest entry sits in [1/2, 1)
     {
       float part = h ? 0.f : dgv * rt[i];
 #pragma unroll
@@ -542,22 +549,18 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
         part = __builtin_fmaf(A[4 * g + 3], r4.w, part);
       }
       const float y = half_sum(part);
-      const float lam = pi * kLog2e;
-      const int B0 = max(rho, (int)floorf(lam));
+      const float lam = pi;  // log2 P00 - csum
+      const int B0 = __builtin_isfinite(lam) ? max(rho, (int)floorf(lam)) : rho;
       float nr = ldexpf(y, max(rho - B0, -200)) + e0 * __builtin_amdgcn_exp2f(lam - (float)B0);
       nr = (FULL || i < V) ? nr : 0.f;
-      // scale by state 1's entry (> 0: state 0 reaches every core state in
-      // one frame; the others stay within e^61 of it)
-      const float m = first_lane(nr);
       int e;
-      frexpf(m, &e);
-      e = m > 0.f ? e : 0;
+      frexpf(wmax_u(lane < 32 ? nr : 0.f), &e);  // 0 (nothing reached): e = 0
       nr = ldexpf(nr, -e);
       rho = B0 + e;
       if (lane < 32) rt[lane] = nr;
     }
-    pi += w00 - c;
-    csum += c;
+    pi += __builtin_fmaf(w00, kLog2e, -cl);
+    csum += cl;
 
     // core: X <- E^T X on the matrix cores (exact f32 FMA chains)
     v16f D = {};
@@ -572,9 +575,12 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
       D[4 * g + 2] = __builtin_fmaf(d4.z, X[4 * g + 2], D[4 * g + 2]);
       D[4 * g + 3] = __builtin_fmaf(d4.w, X[4 * g + 3], D[4 * g + 3]);
     }
-    // one power-of-two scale per column (start state j): its end state 1
-    // (row 0, register 0 of half 0), within e^61 of the column's others
-    const float cm = half_lo(D[0]);
+    // one power-of-two scale per column (start state j): its largest entry
+    // in [1/2, 1) (a column with nothing reached keeps its scale)
+    float cm = fmaxf(max3_raw(D[0], D[1], D[2]), max3_raw(D[3], D[4], D[5]));
+#pragma unroll
+    for (int r = 6; r < 16; r += 2) cm = max3_raw(cm, D[r], D[r + 1]);
+    cm = fmaxf(cm, half_other(cm));
     int e;
     frexpf(cm, &e);
     e = cm > 0.f ? e : 0;
@@ -608,7 +614,7 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   CK_ASTAMP(3);
   if (lane == 0)
-    __hip_atomic_store((gu32*)(a.ready + id), bad ? 2u : 1u, __ATOMIC_RELAXED,
+    __hip_atomic_store((gu32*)(a.ready + id), bad ? (unsigned)bad : 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -635,13 +641,14 @@ LT_DEVINL void acquire_agent() {
 }
 struct ChunkReady {
   const unsigned* f;
-  int lo, hi, Kl, ok, bad;
-  LT_DEVINL ChunkReady(const unsigned* flags, int kl) : f(flags), lo(kl), hi(-1), Kl(kl), ok(1), bad(0) {}
+  int lo, hi, Kl, ok, bad, strict;
+  LT_DEVINL ChunkReady(const unsigned* flags, int kl, int st)
+      : f(flags), lo(kl), hi(-1), Kl(kl), ok(1), bad(0), strict(st) {}
   LT_DEVINL void take(unsigned v, int lane, int* c) {
     const unsigned long long m = __builtin_amdgcn_ballot_w64(v != 0);
     *c = m == ~0ull ? 64 : __builtin_ctzll(~m);
     const unsigned long long live = *c == 64 ? ~0ull : ((1ull << *c) - 1);
-    if (__builtin_amdgcn_ballot_w64(v == 2u) & live) bad = 1;
+    if (__builtin_amdgcn_ballot_w64(v == 2u || (strict && v == 3u)) & live) bad = 1;
   }
   LT_DEVINL void timeout() {
     ok = 0;
@@ -690,8 +697,8 @@ struct ChunkReady {
 // ---------------------------------------------------------------------------
 struct RecAlpha {  // what lane i (< 32) needs of one record for the alpha step
   float4 x[8];     // X[i][0..31]
-  float rt, sc;    // rt[i]; the source-row scale of lane p (rho or ej[p-1], x ln2)
-  float pi, cs;
+  float rt, sc;    // rt[i]; the source-row scale of lane p (rho or ej[p-1], log2)
+  float pi, cs;    // log2 P00 - csum; csum (log2, an integer)
 };
 LT_DEVINL void load_rec_alpha(const float* rc, int lane, int V, RecAlpha& r) {
   // unconditional loads (lanes >= 32 re-read row lane & 31): exact vmcnt
@@ -700,13 +707,13 @@ LT_DEVINL void load_rec_alpha(const float* rc, int lane, int V, RecAlpha& r) {
   r.rt = rc[kRecRt + (lane & 31)];
   const int si = lane == 0 ? kRecRho : kRecEj + min(lane, 32) - 1;
   const int sc = ((const int*)rc)[si];
-  r.sc = lane <= V ? (float)sc * 0.6931471805599453f : 0.f;
+  r.sc = lane <= V ? (float)sc : 0.f;
   r.pi = rc[kRecPi];
   r.cs = rc[kRecCs];
 }
 struct RecBeta {   // lane (j, h): the rows of half h of column j
   float x[16];
-  float rt, ej;    // rt[lane & 31], ej[j] x ln2
+  float rt, ej;    // rt[lane & 31], ej[j] (log2)
   float rho, pi, cs;
 };
 LT_DEVINL void load_rec_beta(const float* rc, int lane, RecBeta& r) {
@@ -716,8 +723,8 @@ LT_DEVINL void load_rec_beta(const float* rc, int lane, RecBeta& r) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) r.x[4 * g + q] = rc[(8 * g + 4 * h + q) * kRowT + j];
   r.rt = rc[kRecRt + j];
-  r.ej = (float)((const int*)rc)[kRecEj + j] * 0.6931471805599453f;
-  r.rho = (float)((const int*)rc)[kRecRho] * 0.6931471805599453f;
+  r.ej = (float)((const int*)rc)[kRecEj + j];
+  r.rho = (float)((const int*)rc)[kRecRho];
   r.pi = rc[kRecPi];
   r.cs = rc[kRecCs];
 }
@@ -727,7 +734,9 @@ LT_DEVINL void load_rec_beta(const float* rc, int lane, RecBeta& r) {
 // al'[u] = (+)_d al[u - d] + N[u - d][d], scattered by destination through
 // an LDS table; !FWD, beta (the reverse of alignments.py:320-329):
 // be'[s] = (+)_d N[s][d] + be[s + d] from an LDS copy padded with -inf.
-// Boundary values at every chunk start -> nabd / nbbd (natural log).
+// Boundary values at every chunk start -> nabd / nbbd (log2, each vector
+// relative to the walk's integer offset at that boundary: phase C normalises
+// every frame by its own total, so only differences within a vector matter).
 template <int PPL, bool FWD>
 LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl, float* lds,
                         float* s_num, ChunkReady& rd) {
@@ -756,13 +765,14 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
     sv[64 * PPL + lane] = -kInf;
   }
   float v[PPL];
+  float off = 0.f;  // the vector's integer offset (log2): the walk holds v - off
 #pragma unroll
   for (int r = 0; r < PPL; ++r) v[r] = (lane + 64 * r == (FWD ? 0 : nl)) ? 0.f : -kInf;
   float* dst = (FWD ? a.nabd : a.nbbd) + (long long)b * (a.K + 1) * NPG;
   if (!FWD) {
 #pragma unroll
     for (int r = 0; r < PPL; ++r)
-      if (lane + 64 * r < NPG) dst[(long long)Kl * NPG + lane + 64 * r] = v[r] * kLn2;
+      if (lane + 64 * r < NPG) dst[(long long)Kl * NPG + lane + 64 * r] = v[r];
   }
   // band rows N[s][0 .. kGrp] of group q for the lane's source positions
   float4 gq[D][PPL][2];
@@ -783,7 +793,7 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
     if (FWD && q % NGc == 0) {  // a chunk starts here
 #pragma unroll
       for (int r = 0; r < PPL; ++r)
-        if (lane + 64 * r < NPG) dst[(long long)(q / NGc) * NPG + lane + 64 * r] = v[r] * kLn2;
+        if (lane + 64 * r < NPG) dst[(long long)(q / NGc) * NPG + lane + 64 * r] = v[r];
     }
     float n[PPL][NB];
 #pragma unroll
@@ -809,6 +819,7 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
       for (int d = 0; d < NB; ++d)
         x[r][d] = FWD ? tab[(lane + 64 * r) * TS + d] : n[r][d] + sv[lane + 64 * r + d];
     bload(qn, g);
+    float vm = -kInf;
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       float m = x[r][0];
@@ -819,11 +830,22 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
 #pragma unroll
       for (int d = 0; d < NB; ++d) sum += __builtin_amdgcn_exp2f(x[r][d] - ms);
       v[r] = lane + 64 * r < NPG ? ms + __builtin_amdgcn_logf(sum) : -kInf;
+      vm = fmaxf(vm, v[r]);
+    }
+    // the vector relative to an integer offset near its max: the values a
+    // marginal is made of stay small, so their rounding stays 2^-24 of
+    // small numbers however long the utterance (the offset is exact)
+    {
+      const float mv = wmax_u(vm);
+      const float fl = __builtin_isfinite(mv) ? floorf(mv) : 0.f;
+#pragma unroll
+      for (int r = 0; r < PPL; ++r) v[r] -= fl;
+      off += fl;
     }
     if (!FWD && q % NGc == 0) {  // beta at the chunk's first frame
 #pragma unroll
       for (int r = 0; r < PPL; ++r)
-        if (lane + 64 * r < NPG) dst[(long long)(q / NGc) * NPG + lane + 64 * r] = v[r] * kLn2;
+        if (lane + 64 * r < NPG) dst[(long long)(q / NGc) * NPG + lane + 64 * r] = v[r];
     }
     __builtin_amdgcn_wave_barrier();
   };
@@ -843,9 +865,11 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
     float nv = -kInf;
 #pragma unroll
     for (int r = 0; r < PPL; ++r)
-      if (lane + 64 * r == nl) nv = v[r] * kLn2;
+      if (lane + 64 * r == nl) nv = v[r];
     nv = wmax_u(nv);
-    if (lane == 0) *s_num = (nl >= 0 && nl <= a.U) ? nv : -kInf;
+    if (lane == 0)
+      *s_num = (nl >= 0 && nl <= a.U) ? (float)(((double)off + (double)nv) * 0.6931471805599453)
+                                       : -kInf;
   }
 }
 
@@ -866,7 +890,7 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
   if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
   CK_WSTAMP(2 * wave);
-  ChunkReady rd(a.ready + (long long)b * a.K, Kl);
+  ChunkReady rd(a.ready + (long long)b * a.K, Kl, a.strict);
 
   // den walks: the records stream through a ring of kWalkSlots LDS slots
   // per wave by LDS-DMA (1 KiB contiguous per instruction), issued
@@ -890,9 +914,14 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
   auto slot = [&](int n) { return (const float*)(ring + (n % kWalkSlots) * kWalkSlot); };
 
   if (wave == 0 && !a.local && !LT_ABL(a, 1)) {
-    // ---- den alpha across chunks (lattices.py:379-496 in chunk steps)
+    // ---- den alpha across chunks (lattices.py:379-496 in chunk steps), log2
+    // units: lane p holds alpha[p] - O with O an integer offset near the
+    // vector's max. The records' scales (ej, rho) and offsets (csum) are
+    // integers, so O is exact and every stored value stays small: its
+    // rounding is 2^-24 of a small number however long the utterance.
     float* bc = s_bc[0];  // bc[j] = a_{j+1} (core source j), bc[32] = a_0
-    float al = lane == 0 ? 0.f : -kInf;  // lane p: alpha[p]
+    float al = lane == 0 ? 0.f : -kInf;  // lane p: alpha[p] - O
+    float O = 0.f;
     float* dst = a.abd + (long long)b * (a.K + 1) * CP;
     if (lane < C) dst[lane] = al;
     if (Kl > 0) {
@@ -905,7 +934,7 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
       load_rec_alpha(slot(k), lane, V, R);
       const float x = lane < C ? al + R.sc : -kInf;
       const float M = safe_max(wmax_u(x));
-      const float av = lane < C ? lt_exp(x - M) : 0.f;
+      const float av = lane < C ? __builtin_amdgcn_exp2f(x - M) : 0.f;
       if (lane >= 1 && lane <= 32) bc[lane - 1] = av;
       if (lane == 0) bc[32] = av;
       __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -930,23 +959,28 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
       __builtin_amdgcn_s_waitcnt(0xc07f);
       rd.ensure_fwd(k + kWalkSlots, lane);
       issue_rec(k + kWalkSlots, k + kWalkSlots);
-      const float nq = M + cs + lt_log(s0 + s1);  // lane i < 32: alpha'[i+1]
-      const float n0 = first_lane(al) + pi + cs;
+      const float fl = floorf(M);
+      const float nq = (M - fl) + __builtin_amdgcn_logf(s0 + s1);  // lane i < 32: alpha'[i+1] - O'
+      const float n0 = first_lane(al) + pi - fl;
+      O += cs + fl;
       const float sh = from_prev(nq, -kInf);
       al = lane == 0 ? n0 : (lane < C ? sh : -kInf);
       if (lane < C) dst[(long long)(k + 1) * CP + lane] = al;
       __builtin_amdgcn_wave_barrier();
     }
-    // log_z = (+)_q alpha_T[q] (lattices.py:496)
+    // log_z = (+)_q alpha_T[q] (lattices.py:496), back to natural log once
     const float x = lane < C ? al : -kInf;
     const float M = safe_max(wmax_u(x));
-    const float s = wsum_u(lane < C ? lt_exp(x - M) : 0.f);
-    if (lane == 0) s_lz = M + lt_log(s);
+    const float s = wsum_u(lane < C ? __builtin_amdgcn_exp2f(x - M) : 0.f);
+    if (lane == 0)
+      s_lz = (float)(((double)O + (double)(M + __builtin_amdgcn_logf(s))) * 0.6931471805599453);
   } else if (wave == 1 && !a.local && !LT_ABL(a, 1)) {
-    // ---- den beta across chunks: beta_T = one for every state (lattices.py:788-790)
+    // ---- den beta across chunks: beta_T = one for every state
+    // (lattices.py:788-790); log2, relative to an integer offset as alpha
+    // (the offset itself is not needed: nothing reads beta's absolute value)
     float* bc = s_bc[1];
     const int h = lane >> 5;
-    float be = lane < C ? 0.f : -kInf;  // lane p: beta[p]
+    float be = lane < C ? 0.f : -kInf;  // lane p: beta[p] - O
     float* dst = a.bbd + (long long)b * (a.K + 1) * CP;
     if (lane < C) dst[(long long)Kl * CP + lane] = be;
     if (Kl > 0) {
@@ -960,7 +994,7 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
       load_rec_beta(slot(n), lane, R);
       const float xc = (lane >= 1 && lane < C) ? be : -kInf;  // core beta
       const float Mc = safe_max(wmax_u(xc));
-      if (lane >= 1 && lane <= 32) bc[lane - 1] = lane < C ? lt_exp(xc - Mc) : 0.f;
+      if (lane >= 1 && lane <= 32) bc[lane - 1] = lane < C ? __builtin_amdgcn_exp2f(xc - Mc) : 0.f;
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       // lane (j, h): sum over end states i of half h of X[i][j] b_i
@@ -974,16 +1008,17 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
         p1 = __builtin_fmaf(R.x[4 * g + 3], b4.w, p1);
       }
       const float rp = lane < 32 ? R.rt * bc[lane & 31] : 0.f;
-      const float cs = R.cs, ej = R.ej, rho = R.rho, pi = R.pi;
+      const float ej = R.ej, rho = R.rho, pi = R.pi;
       __builtin_amdgcn_s_waitcnt(0xc07f);
       rd.ensure_bwd(k - kWalkSlots, lane);
       issue_rec(k - kWalkSlots, n + kWalkSlots);
+      const float fl = floorf(Mc);
       const float tot = half_sum(p0 + p1);
-      const float nj = Mc + cs + ej + lt_log(tot);  // lane j: beta'[j+1]
+      const float nj = (Mc - fl) + ej + __builtin_amdgcn_logf(tot);  // lane j: beta'[j+1] - O'
       // state 0: the rt row and its own self loop
       const float rsum = wsum_u(rp);
-      const float rterm = Mc + cs + rho + lt_log(rsum);
-      const float nb0 = lse2(first_lane(be) + pi + cs, rterm);
+      const float rterm = (Mc - fl) + rho + __builtin_amdgcn_logf(rsum);
+      const float nb0 = lse2_b2(first_lane(be) + pi - fl, rterm);
       const float sh = from_prev(nj, -kInf);
       be = lane == 0 ? nb0 : (lane < C ? sh : -kInf);
       if (lane < C) dst[(long long)k * CP + lane] = be;
@@ -1101,7 +1136,14 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   const int FRP = (FR + 3) & ~3;
   float g = a.grad ? a.grad[b] : 1.f;
   const float lz = a.log_z[b], nm = a.num[b];
-  if (!__builtin_isfinite(nm) || (!a.local && !__builtin_isfinite(lz))) g = 0.f;
+  // a NaN, or a denominator with no finite path (the relaxed path admits
+  // masked arcs): the frame-serial kernels own the utterance (the
+  // reference's semantics for such lattices)
+  if ((!a.local && !__builtin_isfinite(lz)) || __builtin_isnan(nm)) {
+    if (tid == 0) a.uflag[b] = 1;
+    return;
+  }
+  if (!__builtin_isfinite(nm)) g = 0.f;  // unreachable string: loss +inf, dW = 0
   const long long e0 = ((long long)b * a.T + t0) * FR;
   if (t1 <= t0 || g == 0.f) {  // padding chunk / unreachable string: dW = 0
     const long long n = (long long)(tend - t0) * FR;
@@ -1166,13 +1208,17 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   int* fl = (int*)(lds + a.c_off_fl);
   int* ford = fl + a.L;
   int* njob = ford + a.L;
+  int* cert_fail = njob + 1;  // a frame outside the certificate (any wave)
   if (tid < nt) {
     fl[tid] = 0;
     const int mid = (nt - 1) / 2;  // job j -> frames mid, mid+1, mid-1, mid+2, ...
     const int k = (tid + 1) / 2;
     ford[tid] = (tid & 1) ? mid + k : mid - k;
   }
-  if (tid == 0) *njob = 0;
+  if (tid == 0) {
+    *njob = 0;
+    *cert_fail = 0;
+  }
   __syncthreads();  // the gathers above read W; E overwrites it below
   // E in place, frame by frame: each thread's elements of a frame loaded
   // together (element-wise: no barrier between a thread's reads and stores)
@@ -1180,7 +1226,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   for (int f = 0; f < nt; ++f) {
     const unsigned char* fr = wch + f * a.FB;
     float* ef = eptr(f);
-    const float cl = cfl[f] * kLog2e;
+    const float cl = cfl[f];  // log2 units (phase A's integer offset)
     float v[kEi];
 #pragma unroll
     for (int i = 0; i < kEi; ++i) v[i] = ldsw<BF16>(fr, min(tid + 64 * kMargWaves * i, FR - 1));
@@ -1207,40 +1253,43 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   };
 
   if (wave == 0 && !a.local && !LT_ABL(a, 4)) {
-    // ---- den alpha in scaled linear space. Lane p in [1, V]: alpha[p] =
-    // al 2^S, renormalised every frame by a power of two so that state 1
-    // sits in [1/2, 1) (readfirstlane + frexp: no reduction on the chain).
-    // Every E is in [e^-61, 1] and the frame range bound keeps every core
-    // value within ~2^89 of state 1. The start state (only its blank loop
-    // in-arc) is a log2 scalar a0 beside the chain. Lane (q, h): destination
-    // q+1, sources p in [16h, 16h+16) (+ p = 32 in h = 1), the blank self
-    // loop in h = 0; halves combined by permlane. Per frame, off the chain:
-    // xa = alpha_f / its max (all states), Ma = log2 of that max.
+    // ---- den alpha in scaled linear space. Lane p in [1, V]: alpha_f[p] =
+    // al 2^S (log2 units relative to the walk's offset); each frame the
+    // vector is taken over its own max, xa = alpha_f / 2^Ma with Ma = S + the
+    // exponent of the largest core value (or the start state's a0, a log2
+    // scalar beside the chain: its only in-arc is its blank loop), and the
+    // step runs on xa: alpha_{f+1}[q] = 2^(Ma + c) sum_p xa[p] E[p][q]. So
+    // every product and sum is relative to the vector's max, whatever the
+    // frame's range (masked -inf weights are exact zeros): a value lost to
+    // underflow is below 2^-126 of that max, which the marginal pass's
+    // per-frame certificate bounds. Lane (q, h): destination q+1, sources p
+    // in [16h, 16h+16) (+ p = 32 in h = 1), the blank self loop in h = 0;
+    // halves combined by permlane.
     const int q = lane & 31, h = lane >> 5;
     const int qe = min(q, V - 1) + 1;
     const bool core = lane >= 1 && lane <= V;
-    const float x0 = lane < C ? a.abd[((long long)b * (a.K + 1) + k) * CP + lane] * kLog2e : -kInf;
+    const float x0 = lane < C ? a.abd[((long long)b * (a.K + 1) + k) * CP + lane] : -kInf;
     float a0 = first_lane(x0);
     float S = wmax_u(core ? x0 : -kInf);  // -inf: no core state reached yet
     float al = (core && S != -kInf) ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     for (int f = 0; f < nt; ++f) {
       const float* ef = eptr(f);
-      const float cl = cfl[f] * kLog2e;
+      const float cl = cfl[f];
       const float w00 = fs[f * kFs + kFsW00];
       float e[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) e[m] = ef[min(16 * h + m, C - 1) * R + qe];
       const float e32 = ef[min(32, C - 1) * R + qe];
       const float eb = ef[qe * R];
-      const float M = fmaxf(a0, S);  // a0 is finite on the fast path
-      const float u = __builtin_amdgcn_exp2f(S - M), t = __builtin_amdgcn_exp2f(a0 - M);
-      if (lane < 36) buf[lane] = lane == 0 ? t : al * u;  // buf[p > V] = 0
-      // alpha_f for the marginals
       const float mc = wmax_u(core ? al : 0.f);
-      const float Ma = mc > 0.f ? fmaxf(a0, S + __builtin_amdgcn_logf(mc)) : a0;
-      if (lane < C)
-        xa[f * CP + lane] = lane == 0 ? __builtin_amdgcn_exp2f(a0 - Ma)
-                                      : al * __builtin_amdgcn_exp2f(S - Ma);
+      int ex;
+      (void)frexpf(mc, &ex);
+      const float Ma = safe_max(mc > 0.f ? fmaxf(a0, S + (float)ex) : a0);
+      // xa = alpha_f over 2^Ma (the marginals' row) and the step's operand
+      // row buf (36 floats, 0 past V)
+      const float xv = lane == 0 ? __builtin_amdgcn_exp2f(a0 - Ma) : al * __builtin_amdgcn_exp2f(S - Ma);
+      if (lane < 36) buf[lane] = xv;
+      if (lane < C) xa[f * CP + lane] = xv;
       if (lane == 0) {
         fs[f * kFs + kFsMa] = Ma;
         fs[f * kFs + kFsA0] = a0;
@@ -1258,44 +1307,46 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       }
       // h = 1: source 32 (buf[32] = 0 unless C > 32); h = 0: the blank loop of qe
       s0 = __builtin_fmaf(h ? buf[32] : buf[qe], h ? e32 : eb, s0);
-      const float sq = half_sum(s0 + s1);  // lane q: alpha'[q+1] / (2^M e^c)
-      int ex;
-      (void)frexpf(first_lane(sq), &ex);  // state 1: > 0 on the fast path
-      S = M + cl + (float)ex;
+      const float sq = half_sum(s0 + s1);  // lane q: alpha'[q+1] / 2^(Ma + c)
+      S = Ma + cl;
       a0 += w00;
-      const float sh = from_prev(ldexpf(sq, -ex), 0.f);
+      const float sh = from_prev(sq, 0.f);
       al = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
       mark(f, kFlA);
     }
   } else if (wave == 1 && !a.local && !LT_ABL(a, 4)) {
     // ---- den beta, the same scaled linear space; frame f gets beta_{f+1}.
-    // Lane (j, h): core source j+1 over labels y in [16h+1, 16h+16], the
-    // blank in h = 0; every lane also one term of the start state's sum
-    // (log2 scalar b0: no core state depends on it). Off the chain: xb =
-    // core beta / its max, Mb = log2 of that max.
+    // Each frame the core vector over its own max: xb = beta_{f+1} / 2^Mb;
+    // the step runs on xb. Lane (j, h): core source j+1 over labels y in
+    // [16h+1, 16h+16], the blank in h = 0; every lane also one term of the
+    // start state's sum (log2 scalar b0: no core state depends on it).
     const int j = lane & 31, h = lane >> 5;
     const int pe = min(j, V - 1) + 1;
     const bool core = lane >= 1 && lane <= V;
-    const float x0 = lane < C ? a.bbd[((long long)b * (a.K + 1) + k + 1) * CP + lane] * kLog2e : -kInf;
+    const float x0 = lane < C ? a.bbd[((long long)b * (a.K + 1) + k + 1) * CP + lane] : -kInf;
     float b0 = first_lane(x0);
     float S = safe_max(wmax_u(core ? x0 : -kInf));
     float be = core ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     for (int f = nt - 1; f >= 0; --f) {
       const float* ef = eptr(f);
-      const float cl = cfl[f] * kLog2e;
+      const float cl = cfl[f];
       const float w00 = fs[f * kFs + kFsW00];
       float e[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) e[m] = ef[pe * R + min(16 * h + m + 1, V)];
       const float eb = ef[pe * R];
       const float e0y = ef[min(j, V - 1) + 1];  // E[0][j+1]
-      // buf[y-1] = beta[y] (scaled) for core y; 0 past V
-      if (lane >= 1 && lane <= 32) buf[lane - 1] = be;
-      const float mc = wmax_u(be);  // > 0: every core beta is
-      if (lane < C) xb[f * CP + lane] = be * __builtin_amdgcn_rcpf(mc);
+      const float mc = wmax_u(be);
+      int ex;
+      (void)frexpf(mc, &ex);
+      const float Mb = mc > 0.f ? S + (float)ex : S;
+      const float xv = be * __builtin_amdgcn_exp2f(S - Mb);  // <= 1
+      // buf[y-1] = xb[y] for core y; 0 past V
+      if (lane >= 1 && lane <= 32) buf[lane - 1] = xv;
+      if (lane < C) xb[f * CP + lane] = xv;
       if (lane == 0) {
-        fs[f * kFs + kFsMb] = S + __builtin_amdgcn_logf(mc);
+        fs[f * kFs + kFsMb] = Mb;
         fs[f * kFs + kFsB0] = b0;
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -1311,14 +1362,12 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       }
       const float bj = buf[j];
       s0 = __builtin_fmaf(h ? 0.f : bj, eb, s0);
-      const float sj = half_sum(s0 + s1);  // lane j: beta'[j+1] / (2^S e^c)
+      const float sj = half_sum(s0 + s1);  // lane j: beta_f[j+1] / 2^(Mb + c)
       // start state: (+)_y E[0][y] beta[y], then its own blank loop
       const float r0 = wsum_u(lane < 32 ? bj * e0y : 0.f);
-      b0 = lse2_b2(b0 + w00, S + cl + __builtin_amdgcn_logf(r0));
-      int ex;
-      (void)frexpf(first_lane(sj), &ex);
-      S = S + cl + (float)ex;
-      const float sh = from_prev(ldexpf(sj, -ex), 0.f);
+      b0 = lse2_b2(b0 + w00, Mb + cl + __builtin_amdgcn_logf(r0));
+      S = Mb + cl;
+      const float sh = from_prev(sj, 0.f);
       be = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
       mark(f, kFlB);
@@ -1330,7 +1379,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       const int u = lane + 64 * r, uc = min(u, NPG - 1);
-      const float v = src[uc] * kLog2e;
+      const float v = src[uc];  // log2, relative to the walk's offset
       al[r] = u < NPG ? v : -kInf;
     }
     for (int f = 0; f < nt; ++f) {
@@ -1357,7 +1406,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       const int u = lane + 64 * r, uc = min(u, NPG - 1);
-      const float v = src[uc] * kLog2e;
+      const float v = src[uc];
       be[r] = u < NPG ? v : -kInf;
     }
     for (int f = nt - 1; f >= 0; --f) {
@@ -1470,9 +1519,18 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       }
       sum = wsum_u(sum);
       const float* fsf = fs + f * kFs;
-      const float base = fsf[kFsMa] + fsf[kFsMb] + cfl[f] * kLog2e;
+      const float base = fsf[kFsMa] + fsf[kFsMb] + cfl[f];
       const float v00 = fsf[kFsA0] + fsf[kFsW00] + fsf[kFsB0];
       const float zl = lse2_b2(base + __builtin_amdgcn_logf(sum), v00);
+      // the per-frame certificate of the scaled linear spaces (phases A, B
+      // and C): every value lost to underflow anywhere -- an E below 2^-126,
+      // a product or sum below 2^-126 of its vector's (or column's) max --
+      // carries at most 2^(base - 126 + 15) of this frame's total 2^zl (base
+      // = log2 of alpha_f's max x beta_{f+1}'s max x e^c, 2^15 the count of
+      // such terms). base - zl <= kCert keeps that below 2^-47 of the
+      // marginals' scale; a frame outside it (or a NaN / inf anywhere) sends
+      // the utterance to the frame-serial kernels.
+      if (!(base - zl <= kCert) && lane == 0) *cert_fail = 1;
       const float mult = g * __builtin_amdgcn_exp2f(base - zl);
       const float m00 = g * __builtin_amdgcn_exp2f(v00 - zl);
       __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -1508,6 +1566,10 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   // the chunk's dW sits in LDS in place of its W: one streaming pass of
   // 16-byte stores (scalar stores only at the unaligned head and tail)
   __syncthreads();
+  if (*cert_fail) {  // the frame-serial kernels redo this utterance after the launch
+    if (tid == 0) a.uflag[b] = 1;
+    return;
+  }
   CK_STAMP(3);
   {
     const long long es = BF16 ? 2 : 4;
@@ -1544,10 +1606,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
 // ---------------------------------------------------------------------------
 namespace {
 
-int ck_env(const char* name, int dflt) {
-  const char* s = getenv(name);
-  return (s && *s) ? atoi(s) : dflt;
-}
+int ck_env(const char* name, int dflt) { return lt_impl::tune_int(name, dflt); }
 long long up256(long long x) { return (x + 255) & ~255LL; }
 int al16(long long x) { return (int)((x + 15) & ~15LL); }
 
@@ -1570,7 +1629,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   a->local = local_norm ? 1 : 0;
 #ifdef LT_DIAG
   a->dbg = ck_env("LT_CK_DBG", 0);
-  if (const char* sp = getenv("LT_CK_STAMPS")) a->stamps = (long long*)strtoull(sp, nullptr, 0);
+  if (const char* sp = lt_impl::tune_str("LT_CK_STAMPS")) a->stamps = (long long*)strtoull(sp, nullptr, 0);
 #endif
   a->FB = (long long)a->FR * es;
   // A: per wave a ring of frame slots, the state-0 row and the gather tables
@@ -1606,7 +1665,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
     t->c_off_tab = off; off += al16(8LL * a->NPG + 4LL * a->U);
     t->c_off_cf = off; off += al16(4LL * L);
     t->c_off_buf = off; off += 4 * 64 * 4;
-    t->c_off_fl = off; off += al16(4LL * (2 * L + 1));
+    t->c_off_fl = off; off += al16(4LL * (2 * L + 2));
     t->c_off_e = off; off += bf16 ? al16(4LL * L * ((a->FR + 3) & ~3)) : 0;
     return off;
   };
@@ -1856,6 +1915,9 @@ int lt_chunk_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   a.loss = loss;
   a.lz_out = log_z;
   a.num_out = num;
+  // the loss alone has no phase C to certify it: chunks outside the strict
+  // range (every weight finite, within e^61 of its frame's max) leave here
+  a.strict = 1;
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   if ((rc = ck_launch_ab(a, bf16, st))) return rc;

@@ -51,6 +51,32 @@
 
 #include <algorithm>
 #include <string>
+#include <cstdlib>
+
+// Tuning and dispatch overrides from the environment (LT_CHUNK_LEN,
+// LT_PIPE_SLOTS, ...): read only by diagnostic builds (make diag, LT_DIAG).
+// The product library ignores the environment: its designs and launch
+// shapes are fixed per problem, and a caller picks a design explicitly
+// through lt_loss_grad_ex.
+namespace lt_impl {
+inline int tune_int(const char* name, int dflt) {
+#ifdef LT_DIAG
+  const char* s = getenv(name);
+  return (s && *s) ? atoi(s) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
+inline const char* tune_str(const char* name) {
+#ifdef LT_DIAG
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+}  // namespace lt_impl
 
 #include "../../include/lt_lattice.h"
 

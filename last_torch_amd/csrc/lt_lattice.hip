@@ -468,10 +468,7 @@ int hip_check(hipError_t e, const char* what) {
 constexpr int kLdsMax = 160 * 1024;
 constexpr int kMaxWaves = 16;
 
-int env_int(const char* name, int dflt) {
-  const char* s = getenv(name);
-  return (s && *s) ? atoi(s) : dflt;
-}
+int env_int(const char* name, int dflt) { return lt_impl::tune_int(name, dflt); }
 
 int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
@@ -493,7 +490,7 @@ int plan(const lt_problem* pb, const NGram& g, int kind, int flags, Plan* pl,
 #endif
 #ifdef LT_STAMPS
   {
-    const char* sp = getenv("LT_STAMPS_PTR");
+    const char* sp = lt_impl::tune_str("LT_STAMPS_PTR");
     a.stamps = sp ? (long long*)strtoull(sp, nullptr, 0) : nullptr;
   }
 #endif
@@ -956,7 +953,7 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   pf.a.alpha_num = alpha_num;
   pf.a.arcs = ck ? arcs : nullptr;
 #ifdef LT_DIAG
-  if (getenv("LT_PLAN_DEBUG")) {
+  if (lt_impl::tune_str("LT_PLAN_DEBUG")) {
     fprintf(stderr, "fwd plan lg=%d P=%d wst=%d threads=%d lds=%d\n", pf.lg, pf.tmax, pf.wst,
             pf.threads, pf.lds_bytes);
     if (ck)
@@ -1169,11 +1166,31 @@ int lt_loss_grad_design(const lt_problem* pb, int32_t* design) {
   return LT_OK;
 }
 
-int lt_loss_grad_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_t* bytes) {
+// An explicit design for *pb: LT_DESIGN_AUTO resolves to lt_loss_grad's own
+// choice; a design the shape cannot take is EUNSUPPORTED.
+static int resolve_design(const lt_problem* pb, int32_t design, int* out) {
+  if (design == LT_DESIGN_AUTO) {
+    *out = loss_grad_design(pb);
+    return LT_OK;
+  }
+  if (design == LT_DESIGN_CHUNK && !(lt_impl::chunk_eligible(pb) && pb->max_frames > 0))
+    return fail(LT_EUNSUPPORTED, "design chunk: FullNGram n = 1, vocab_size <= 32, labels < 128");
+  if (design == LT_DESIGN_FUSED_PIPE && !lt_impl::pipe_eligible(pb))
+    return fail(LT_EUNSUPPORTED, "design fused pipe: bigram shapes only");
+  if (design < LT_DESIGN_CHUNK || design > LT_DESIGN_RECURSION)
+    return fail(LT_EINVAL, "unknown design");
+  *out = design;
+  return LT_OK;
+}
+
+int lt_loss_grad_workspace_bytes_ex(const lt_problem* pb, int32_t local_norm, int32_t design,
+                                    size_t* bytes) {
   NGram g;
   int rc = check_problem(pb, &g);
   if (rc) return rc;
-  if (loss_grad_design(pb) == LT_DESIGN_CHUNK) {
+  int d = 0;
+  if ((rc = resolve_design(pb, design, &d))) return rc;
+  if (d == LT_DESIGN_CHUNK) {
     size_t st = 0, sc = 0;
     if ((rc = lt_chunk_workspace_bytes(pb, local_norm, &st, &sc))) return rc;
     if (bytes) *bytes = ((st + 255) & ~(size_t)255) + sc;
@@ -1183,23 +1200,28 @@ int lt_loss_grad_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_
   return LT_OK;
 }
 
-int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
-                 const int32_t* num_frames, const int32_t* labels, const int32_t* num_labels,
-                 float* loss, float* log_z, float* num, void* dW, void* workspace,
-                 size_t workspace_bytes, void* stream) {
+int lt_loss_grad_workspace_bytes(const lt_problem* pb, int32_t local_norm, size_t* bytes) {
+  return lt_loss_grad_workspace_bytes_ex(pb, local_norm, LT_DESIGN_AUTO, bytes);
+}
+
+int lt_loss_grad_ex(const lt_problem* pb, int32_t local_norm, int32_t design_in, const void* W,
+                    const int32_t* num_frames, const int32_t* labels, const int32_t* num_labels,
+                    float* loss, float* log_z, float* num, void* dW, void* workspace,
+                    size_t workspace_bytes, void* stream) {
   NGram g;
   int rc = check_problem(pb, &g);
   if (rc) return rc;
+  int design = 0;
+  if ((rc = resolve_design(pb, design_in, &design))) return rc;
   if (pb->batch == 0) return LT_OK;
   if (LT_NEED(W) || !num_frames || !num_labels || !loss || !log_z || !num || LT_NEED(dW) ||
       (pb->max_labels > 0 && !labels))
     return fail(LT_EINVAL, "null pointer");
   if (misaligned(W) || misaligned(dW)) return fail(LT_EINVAL, "W/dW must be 16-byte aligned");
-  const int design = loss_grad_design(pb);
   if (design == LT_DESIGN_CHUNK) {
     // bigram: the chunked two-level scan (lt_chunk.hip), two launches (plus
     // the frame-serial pair, whose workgroups exit at once unless an
-    // utterance is out of the fast path's range)
+    // utterance leaves the fast path)
     size_t st = 0, sc = 0;
     if ((rc = lt_chunk_workspace_bytes(pb, local_norm, &st, &sc))) return rc;
     const size_t st_al = (st + 255) & ~(size_t)255;
@@ -1250,6 +1272,14 @@ int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
   return lt_loss_backward(pb, local_norm, W, num_frames, labels, num_labels, log_z, num, alpha,
                           an, nullptr, nullptr, nullptr, nullptr, dW, ws + w.side,
                           workspace_bytes - w.side, stream);
+}
+
+int lt_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
+                 const int32_t* num_frames, const int32_t* labels, const int32_t* num_labels,
+                 float* loss, float* log_z, float* num, void* dW, void* workspace,
+                 size_t workspace_bytes, void* stream) {
+  return lt_loss_grad_ex(pb, local_norm, LT_DESIGN_AUTO, W, num_frames, labels, num_labels, loss,
+                         log_z, num, dW, workspace, workspace_bytes, stream);
 }
 
 int lt_scale_grad(const lt_problem* pb, const float* grad, void* dW, void* stream) {

@@ -1201,10 +1201,7 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers), 4) void pipe_kernel(con
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
-int pipe_env(const char* name, int dflt) {
-  const char* s = getenv(name);
-  return (s && *s) ? atoi(s) : dflt;
-}
+int pipe_env(const char* name, int dflt) { return lt_impl::tune_int(name, dflt); }
 
 template <int J, bool BF16, int PN>
 int launch_pipe_t(const PArgs& a, int grid, int threads, int lds, hipStream_t st) {
@@ -1292,7 +1289,7 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
 #endif
 #ifdef LT_STAMPS
   {
-    const char* sp = getenv("LT_STAMPS_PTR");
+    const char* sp = lt_impl::tune_str("LT_STAMPS_PTR");
     a.stamps = sp ? (long long*)strtoull(sp, nullptr, 0) : nullptr;
     a.stamp_block = pipe_env("LT_STAMP_BLOCK", 0);
   }
@@ -1369,7 +1366,7 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
     lds = std::max(lds, a.moff_wave + nw * a.mwave_bytes);
     lds = std::max(lds, pipe_env("LT_FUSED_LDS", 0));  // e.g. > 80 KB: one workgroup per CU
 #ifdef LT_DIAG
-    if (const char* tp = getenv("LT_FUSED_TRACE")) a.trace = (long long*)strtoull(tp, nullptr, 0);
+    if (const char* tp = lt_impl::tune_str("LT_FUSED_TRACE")) a.trace = (long long*)strtoull(tp, nullptr, 0);
 #endif
     if (lds > 160 * 1024) return set_error(LT_EUNSUPPORTED, "pipe: fused LDS");
     // marginal workgroups fill the second workgroup slot of the CUs the

@@ -985,7 +985,7 @@ TArgs t_args(const lt_graph* g, const lt_table_problem* pb, const void* W, const
 // threads per utterance workgroup: the denominator reductions take 8 lanes
 // per state, so 512 threads cover up to 64 states in one pass
 int tab_threads(const TArgs& a) {
-  const char* e = getenv("LT_TAB_THREADS");
+  const char* e = lt_impl::tune_str("LT_TAB_THREADS");
   const int t = (e && *e) ? atoi(e) : (a.C > 32 ? 512 : 256);
   return t >= 512 ? 512 : 256;
 }
@@ -1264,7 +1264,7 @@ int lt_table_viterbi(const lt_graph* g, const lt_table_problem* pb, const void* 
   const int arcs_lds = arcs_bytes <= budget / 2 ? 1 : 0;
   const long long room = budget - (arcs_lds ? arcs_bytes : 0);
   const int chunk = (int)std::min<long long>(std::max(1, a.T), room / per_frame);
-  if (chunk >= 1 && !getenv("LT_TAB_BT_SERIAL")) {
+  if (chunk >= 1 && !lt_impl::tune_str("LT_TAB_BT_SERIAL")) {
     const int lds = (int)((arcs_lds ? arcs_bytes : 0) + chunk * per_frame + 16);
     hipLaunchKernelGGL(tab_backtrace_lds_kernel, dim3(a.B), dim3(256), lds, st, a, chunk, arcs_lds);
   } else {

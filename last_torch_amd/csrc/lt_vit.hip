@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void vit_backtrace_kernel(const VbtArgs a) {
 namespace lt_impl {
 bool vit_bigram_eligible(const lt_problem* pb) {
   return pb->context_size == 1 && pb->vocab_size >= 1 && pb->vocab_size <= 32 &&
-         getenv("LT_VIT_GENERIC") == nullptr;
+         lt_impl::tune_str("LT_VIT_GENERIC") == nullptr;
 }
 
 // MaxTropical forward (distance, best final state, backpointers) of every
@@ -336,7 +336,7 @@ int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, 
   a.R = a.V + 1;
   a.dbg = 0;
 #ifdef LT_DIAG
-  if (const char* d = getenv("LT_VIT_DBG")) a.dbg = atoi(d);
+  if (const char* d = lt_impl::tune_str("LT_VIT_DBG")) a.dbg = atoi(d);
 #endif
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const bool full = a.V == 32;

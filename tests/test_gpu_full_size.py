@@ -71,10 +71,11 @@ def _frame_sum_tol(lz, num=None, bf16=False):
   return (2 * rel + 1e-8 * 34881)[:, None]
 
 
-def _check_loss_grad(W, nf, lab, nl, V, n, local=False, idx=None, bf16=False):
+def _check_loss_grad(W, nf, lab, nl, V, n, local=False, idx=None, bf16=False,
+                     design=nat.DESIGN_AUTO):
   """lt_loss_grad on the batch, the utterances `idx` (all: None) against the
   oracle: loss, log_z, num and every dW element relative to its marginals."""
-  loss, lz, num, dW = nat.loss_grad(W, nf, lab, nl, V, n, local)
+  loss, lz, num, dW = nat.loss_grad(W, nf, lab, nl, V, n, local, design=design)
   torch.cuda.synchronize()
   sel = slice(None) if idx is None else idx
   Wc, nfc, labc, nlc = _np(W[sel], nf[sel], lab[sel], nl[sel])
@@ -172,18 +173,16 @@ def test_cfg2_realistic_weights(cuda, kind):
   _check_loss_grad(W, nf, lab, nl, V, n, local=True)
 
 
-@pytest.mark.parametrize('force', ['', '1'])
-def test_north_star_b256(cuda, force, monkeypatch):
+@pytest.mark.parametrize('design', ['auto', 'chunk'])
+def test_north_star_b256(cuda, design):
   """B=256 (the north-star shape): sampled utterances against the oracle and
   the per-frame marginal sums of all of them -- the design lt_loss_grad picks
-  there (the checkpointing pipe + marginal pass, what bench.py times) and the
-  chunked scan forced (LT_CHUNK=1)."""
+  there (what bench.py times) and the chunked scan (lt_loss_grad_ex)."""
   V, n = 32, 1
-  if force:
-    monkeypatch.setenv('LT_CHUNK', force)
+  d = nat.DESIGN_AUTO if design == 'auto' else nat.DESIGN_CHUNK
   W, nf, lab, nl = _bench_inputs(256, 1000, 100, V, n, cuda, seed=99)
-  assert nat.chunk_path(256, 1000, 100, V, n) == bool(force)
-  loss, lz, num, dW = _check_loss_grad(W, nf, lab, nl, V, n, idx=[0, 1, 63, 64, 128, 200, 254, 255])
+  loss, lz, num, dW = _check_loss_grad(W, nf, lab, nl, V, n, idx=[0, 1, 63, 64, 128, 200, 254, 255],
+                                       design=d)
   s = _frame_sums(dW)
   assert (s.abs() <= _frame_sum_tol(lz, num)).all()
 

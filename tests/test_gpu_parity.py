@@ -266,39 +266,47 @@ def test_random_vs_oracle(cuda, B, T, U, V, n, dt):
   np.testing.assert_array_equal(a.cpu().numpy(), ra)
 
 
-def _poisoned_ws(W, V, n, U, local):
+def _poisoned_ws(W, V, n, U, local, design=nat.DESIGN_AUTO):
   # NaN bytes: a stale hand-off read of a checkpoint row would show in dW
-  nb = nat.loss_grad_workspace_bytes(W, V, n, U, local)
+  nb = nat.loss_grad_workspace_bytes(W, V, n, U, local, design)
   return torch.full([max(nb, 1)], 0xFF, dtype=torch.uint8, device=W.device)
 
 
-# lt_loss_grad's designs: the chunked two-level scan (bigram default), the
-# fused pipe launch and the two-call path
-LOSS_GRAD_PATHS = {'chunk': {'LT_CHUNK': '1'}, 'fused': {'LT_CHUNK': '0', 'LT_FUSED': '1'},
-                   'two-call': {'LT_CHUNK': '0', 'LT_FUSED': '0'}}
+# lt_loss_grad's designs (lt_loss_grad_ex): the chunked two-level scan
+# (bigram default), the fused pipe launch, the checkpointing pair and the
+# recursion pair
+LOSS_GRAD_PATHS = {'chunk': nat.DESIGN_CHUNK, 'fused': nat.DESIGN_FUSED_PIPE,
+                   'two-call': nat.DESIGN_CHECKPOINTS, 'recursion': nat.DESIGN_RECURSION}
+
+
+def _design_or_skip(path, B, T, U, V, n, device, bf16=False):
+  d = LOSS_GRAD_PATHS[path]
+  if d == nat.DESIGN_CHUNK and not (n == 1 and 1 <= V <= 32 and U + 1 <= 128 and T >= 1):
+    pytest.skip('shape outside the chunked design (bigram, V <= 32, U < 128)')
+  if d == nat.DESIGN_FUSED_PIPE and not nat.pipe_path(B, T, U, V, n, bf16):
+    pytest.skip('shape outside the fused pipe design (bigram)')
+  return d
 
 
 @pytest.mark.parametrize('case', LATTICE_CASES)
 @pytest.mark.parametrize('local', [False, True])
 @pytest.mark.parametrize('path', list(LOSS_GRAD_PATHS))
-def test_golden_loss_grad(cuda, case, local, path, monkeypatch):
+def test_golden_loss_grad(cuda, case, local, path):
   """lt_loss_grad against the reference's fixtures, on each design."""
-  for k, v in LOSS_GRAD_PATHS[path].items():
-    monkeypatch.setenv(k, v)
-  fused = '1' if path == 'fused' else '0'
   c = load(case)
   W, nf, lab, nl = _dev(c, cuda, 'W_local' if local else 'W')
   U = lab.shape[-1]
-  ws = _poisoned_ws(W, c['V'], c['n'], U, local)
-  loss, lz, _, dW = nat.loss_grad(W, nf, lab, nl, c['V'], c['n'], local, workspace=ws)
+  d = _design_or_skip(path, W.shape[0], W.shape[1], U, c['V'], c['n'], cuda,
+                      W.dtype == torch.bfloat16)
+  ws = _poisoned_ws(W, c['V'], c['n'], U, local, d)
+  loss, lz, _, dW = nat.loss_grad(W, nf, lab, nl, c['V'], c['n'], local, workspace=ws, design=d)
   torch.cuda.synchronize()
   assert_loss_close(loss.cpu().numpy(), c['loss_local' if local else 'loss'])
   if not local:
     assert_loss_close(lz.cpu().numpy(), c['den_Log'])
   ref = c['loss_local_grad' if local else 'loss_grad']
   assert_grad_close(dW.float().cpu().numpy(), ref, c['den_Log'], c['bf16'])
-  if fused == '1' and nat.fused_path(W.shape[0], W.shape[1], U, c['V'], c['n'], cuda,
-                                     W.dtype == torch.bfloat16):
+  if d == nat.DESIGN_FUSED_PIPE:
     assert nat.grad_workspace_errors(ws, W, c['V'], c['n'], U, local) == 0
 
 
@@ -317,9 +325,7 @@ FUSED_RANDOM = [
 
 @pytest.mark.parametrize('B,T,U,V,dt', FUSED_RANDOM)
 @pytest.mark.parametrize('path', ['chunk', 'fused'])
-def test_random_loss_grad_vs_oracle(cuda, B, T, U, V, dt, path, monkeypatch):
-  for k, v in LOSS_GRAD_PATHS[path].items():
-    monkeypatch.setenv(k, v)
+def test_random_loss_grad_vs_oracle(cuda, B, T, U, V, dt, path):
   orc = _orc()
   n = 1
   W, nf, lab, nl = _random_problem(B, T, U, V, n, seed=B * 100 + T + U + V)
@@ -328,20 +334,17 @@ def test_random_loss_grad_vs_oracle(cuda, B, T, U, V, dt, path, monkeypatch):
     W = torch.tensor(W).bfloat16().float().numpy()
   Wd = torch.tensor(W).to(torch.bfloat16 if bf16 else torch.float32).to(cuda)
   nfd, labd, nld = (torch.tensor(x).to(cuda) for x in (nf, lab, nl))
-  if path == 'chunk' and not nat.chunk_path(B, T, U, V, n):
-    pytest.skip('shape outside the chunked path (U + 1 > 128)')
-  if path == 'fused':
-    assert nat.fused_path(B, T, U, V, n, cuda, bf16)
+  d = _design_or_skip(path, B, T, U, V, n, cuda, bf16)
   for local in (False, True):
-    ws = _poisoned_ws(Wd, V, n, U, local)
-    loss, lz, _, dW = nat.loss_grad(Wd, nfd, labd, nld, V, n, local, workspace=ws)
+    ws = _poisoned_ws(Wd, V, n, U, local, d)
+    loss, lz, _, dW = nat.loss_grad(Wd, nfd, labd, nld, V, n, local, workspace=ws, design=d)
     rl, rlz, _, rdW = orc.loss_grad(W, nf, lab, nl, V, n, local_norm=local)
     assert_loss_close(loss.cpu().numpy(), rl)
     assert_grad_close(dW.float().cpu().numpy(), rdW, rlz, bf16)
     if path == 'fused':
       assert nat.grad_workspace_errors(ws, Wd, V, n, U, local) == 0
     # deterministic: a second call gives the same bits
-    loss2, _, _, dW2 = nat.loss_grad(Wd, nfd, labd, nld, V, n, local)
+    loss2, _, _, dW2 = nat.loss_grad(Wd, nfd, labd, nld, V, n, local, design=d)
     assert torch.equal(loss, loss2) and torch.equal(dW, dW2)
 
 
