@@ -15,36 +15,41 @@ import torch
 from last_torch_amd import semirings
 
 
-_IN_ARCS = {}
-
-
 def _in_arcs(table: torch.Tensor, device) -> torch.Tensor:
   """[C, D] flat arc indices p * V + (y - 1) into each destination state,
   ascending, padded with C * V (one past the last arc) where the in-degree
   is below the maximum D."""
-  key = (table.shape, table.cpu().numpy().tobytes(), str(device))
-  idx = _IN_ARCS.get(key)
-  if idx is None:
-    C, V = table.shape
-    dst = table.reshape(-1).long().cpu()
-    order = torch.argsort(dst * (C * V) + torch.arange(C * V), stable=True)
-    counts = torch.bincount(dst, minlength=C)
-    D = max(int(counts.max()), 1)
-    idx = torch.full((C, D), C * V, dtype=torch.int64)
-    start = torch.cumsum(counts, 0) - counts
-    for q in range(C):
-      idx[q, :counts[q]] = order[start[q]:start[q] + counts[q]]
-    idx = idx.to(device)
-    _IN_ARCS[key] = idx
-  return idx
+  C, V = table.shape
+  dst = table.reshape(-1).long().cpu()
+  order = torch.argsort(dst * (C * V) + torch.arange(C * V), stable=True)
+  counts = torch.bincount(dst, minlength=C)
+  D = max(int(counts.max()), 1)
+  idx = torch.full((C, D), C * V, dtype=torch.int64)
+  start = torch.cumsum(counts, 0) - counts
+  for q in range(C):
+    idx[q, :counts[q]] = order[start[q]:start[q] + counts[q]]
+  return idx.to(device)
 
 
-def _reduce_by_table(weights: torch.Tensor, table: torch.Tensor, semiring) -> torch.Tensor:
+def _cached(ctx, key, make):
+  """A per-instance cache (the dataclasses are frozen): the in-arc index and
+  the next-state table are built once per context and device, not on every
+  per-frame forward_reduce call."""
+  cache = ctx.__dict__.get('_cache')
+  if cache is None:
+    cache = {}
+    object.__setattr__(ctx, '_cache', cache)
+  if key not in cache:
+    cache[key] = make()
+  return cache[key]
+
+
+def _reduce_by_table(weights: torch.Tensor, ctx, table_fn, semiring) -> torch.Tensor:
   """result[..., q] = (+)_{p -y-> q} weights[..., p, y-1]: one gather of
   every state's in-arcs (ascending, so the semiring's own tie rules see the
   arcs in the order a per-state loop would) and one semiring sum."""
-  C, V = table.shape
-  idx = _in_arcs(table, weights.device)
+  C, V = ctx.shape()
+  idx = _cached(ctx, ('in_arcs', str(weights.device)), lambda: _in_arcs(table_fn(), weights.device))
   flat = weights.reshape(*weights.shape[:-2], C * V)
   pad = semiring.zeros((*flat.shape[:-1], 1), flat.dtype, flat.device)
   return semiring.sum(torch.cat([flat, pad], dim=-1)[..., idx], dim=-1)
@@ -135,7 +140,8 @@ class FullNGram(ContextDependency):
 
   def _arc_index(self, device):
     # destination of arc (p, y) flattened as p*V + (y-1)
-    return self.next_state_table().reshape(-1).to(device)
+    return _cached(self, ('dst', str(device)),
+                   lambda: self.next_state_table().reshape(-1).to(device))
 
   def forward_reduce(self, weights, semiring):
     if tuple(weights.shape[-2:]) != self.shape():
@@ -143,7 +149,7 @@ class FullNGram(ContextDependency):
                        f' {tuple(weights.shape[-2:])}')
     # every destination has the same in-degree except the start (none) and
     # the ascending states (one)
-    return _reduce_by_table(weights, self.next_state_table(), semiring)
+    return _reduce_by_table(weights, self, self.next_state_table, semiring)
 
   def backward_broadcast(self, weights):
     C, V = self.shape()
@@ -196,7 +202,7 @@ class NextStateTable(ContextDependency):
     C, V = self.shape()
     if tuple(weights.shape[-2:]) != (C, V):
       raise ValueError(f'weights.shape[-2:] should be {(C, V)} but got {tuple(weights.shape[-2:])}')
-    return _reduce_by_table(weights, self.next_state_table, semiring)
+    return _reduce_by_table(weights, self, lambda: self.next_state_table, semiring)
 
   def backward_broadcast(self, weights):
     """contexts.py:315-320: [..., C] -> [..., C, V] = weights[next_state]."""

@@ -1,4 +1,4 @@
-"""PyTorch CPU restatement of the lattice algorithms, for CPU tensors.
+"""PyTorch CPU path of the lattice algorithms, for CPU tensors.
 
 ``RecognitionLattice`` runs here when its arc weights live on the CPU and on
 the HIP kernels (liblt_lattice.so) when they live on a ROCm device: the
@@ -6,17 +6,27 @@ device of the tensors picks the implementation, as in the reference, and
 there is no fallback from one to the other (a ROCm tensor never runs here;
 a missing HIP library raises).
 
-The formulation is the reference's own: a loop over frames vectorised over
-the batch and the states, built from the plugin classes' per-frame methods
-(``alignment.forward`` / ``string_forward``, ``context.forward_reduce``), with
-gradients by torch autograd through the semirings' sound derivatives
-(semirings.py). FrameDependent alignments (the north-star path).
+One formulation covers both alignment lattices and any context dependency.
+A frame of FrameDependent (K = 0) or FrameLabelDependent(K) is
+
+    alpha' = (+)_{i=0..max(K,1)} term_i,   term_0 = alpha (x) blank,
+    K = 0:   term_1 = L(alpha)
+    K >= 1:  term_i = L^i(alpha) (x) blank
+
+with L the lexical step (the context's forward_reduce: a semiring sum over
+each state's in-arcs) or, on the label string, one position shift
+(alignments.py:286-297, 320-329, 363-377, 421-432; alignment-state-invariant
+weights, lattices.py:444-447). The loop runs over frames vectorised over the
+batch and the states; gradients are torch autograd through the semirings'
+sound derivatives (semirings.py). The terms are summed in the order above, so
+MaxTropical's first-argmax rule prefers the blank, then fewer expansions.
 
   den_forward   lattices.py:379-496   shortest distance + alpha_0..T-1
   num_forward   lattices.py:250-377   string (numerator) distance
   loss          lattices.py:131-183   log_z - num (or -num, locally normalised)
   viterbi       lattices.py:185-247   max-tropical distance, labels from its
-                                      derivative w.r.t. a lexical mask
+                                      derivative w.r.t. one zero lexical mask
+                                      per expansion
 """
 import torch
 
@@ -25,22 +35,39 @@ from last_torch_amd import contexts
 from last_torch_amd import semirings
 
 
-def _check_alignment(alignment):
-  if not isinstance(alignment, alignments.FrameDependent):
-    raise NotImplementedError('the CPU lattice path implements FrameDependent alignments; '
-                              f'got {type(alignment).__name__} (run it on a ROCm device)')
+def expansions(alignment) -> int:
+  """K: 0 for FrameDependent, max_expansions for FrameLabelDependent."""
+  if isinstance(alignment, alignments.FrameLabelDependent):
+    return int(alignment.max_expansions)
+  if isinstance(alignment, alignments.FrameDependent):
+    return 0
+  raise NotImplementedError('the CPU lattice path implements FrameDependent and '
+                            f'FrameLabelDependent alignments; got {type(alignment).__name__}')
 
 
 def _live(nf: torch.Tensor, t: int) -> torch.Tensor:
   return (t < nf)[:, None]
 
 
+def _frame(alpha, step, blank, K, semiring):
+  """One frame: (+) of the terms in the module docstring; `step(x, i)` is
+  the i-th lexical step (0-based) applied to x."""
+  terms = [semiring.times(alpha, blank)]
+  last = alpha
+  for i in range(max(K, 1)):
+    last = step(last, i)
+    terms.append(semiring.times(last, blank) if K else last)
+  return semiring.sum(torch.stack(terms), dim=0)
+
+
 def den_forward(W: torch.Tensor, nf: torch.Tensor, context: contexts.ContextDependency,
-                alignment, semiring) -> tuple[torch.Tensor, torch.Tensor]:
+                alignment, semiring, lex_masks=None) -> tuple[torch.Tensor, torch.Tensor]:
   """(dist [B], alpha_0..T-1 [B, T, C]) over W [B, T, C, V+1]: alpha_0 = one
   at the start state; frames t >= num_frames[b] leave alpha unchanged; dist =
-  (+) of the final alphas (every state is final, lattices.py:496)."""
-  _check_alignment(alignment)
+  (+) of the final alphas (every state is final, lattices.py:496).
+  lex_masks: per expansion a tensor added to the lexical weights of that
+  expansion (viterbi's derivative probes)."""
+  K = expansions(alignment)
   B, T, C, _ = W.shape
   one = semiring.ones([], W.dtype)
   zero = semiring.zeros([], W.dtype)
@@ -48,7 +75,13 @@ def den_forward(W: torch.Tensor, nf: torch.Tensor, context: contexts.ContextDepe
   alphas = []
   for t in range(T):
     alphas.append(alpha)
-    nxt = alignment.forward(alpha, [W[:, t, :, 0]], [W[:, t, :, 1:]], context, semiring)
+    blank, lex = W[:, t, :, 0], W[:, t, :, 1:]
+
+    def step(x, i, lex=lex, t=t):
+      li = lex if lex_masks is None else lex + lex_masks[i][:, t]
+      return context.forward_reduce(semiring.times(x[..., None], li), semiring)
+
+    nxt = _frame(alpha, step, blank, K, semiring)
     alpha = torch.where(_live(nf, t), nxt, alpha)
   alpha_all = torch.stack(alphas, dim=1) if alphas else W.new_zeros([B, 0, C])
   return semiring.sum(alpha, dim=-1), alpha_all
@@ -75,8 +108,9 @@ def string_weights(W: torch.Tensor, labels: torch.Tensor, context: contexts.Cont
 def num_forward(W: torch.Tensor, nf: torch.Tensor, labels: torch.Tensor, nl: torch.Tensor,
                 context: contexts.ContextDependency, alignment, semiring) -> torch.Tensor:
   """Shortest distance of the lattice intersected with the label string
-  (lattices.py:250-377): alpha over string positions 0..U, read at nl."""
-  _check_alignment(alignment)
+  (lattices.py:250-377): alpha over string positions 0..U, read at nl. The
+  lexical step on the string moves every position one place up."""
+  K = expansions(alignment)
   B, T = W.shape[:2]
   U = labels.shape[-1]
   blank, lex = string_weights(W, labels, context)
@@ -85,7 +119,11 @@ def num_forward(W: torch.Tensor, nf: torch.Tensor, labels: torch.Tensor, nl: tor
   alpha = torch.where(torch.arange(U + 1) == 0, one, semiring.zeros([], W.dtype)).expand(B, U + 1)
   for t in range(T):
     lex_t = torch.cat([lex[:, t], zero], dim=-1)   # no arc out of position U
-    nxt = alignment.string_forward(alpha, [blank[:, t]], [lex_t], semiring)
+
+    def step(x, i, lex_t=lex_t):
+      return torch.cat([zero, semiring.times(x, lex_t)[:, :-1]], dim=-1)
+
+    nxt = _frame(alpha, step, blank[:, t], K, semiring)
     alpha = torch.where(_live(nf, t), nxt, alpha)
   ok = (nl >= 0) & (nl <= U)
   num = torch.gather(alpha, 1, nl.clamp(0, U).long()[:, None])[:, 0]
@@ -108,22 +146,31 @@ def loss(W: torch.Tensor, nf: torch.Tensor, labels: torch.Tensor, nl: torch.Tens
 
 def viterbi(W: torch.Tensor, nf: torch.Tensor, context: contexts.ContextDependency, alignment,
             label_convention: str) -> tuple[torch.Tensor, torch.Tensor]:
-  """Best path by differentiating the max-tropical distance w.r.t. a zero
-  lexical mask (lattices.py:185-247): per frame the one-hot mask derivative
-  names the lexical label taken, all-zero means blank. 'reference' emits
-  label y as y - 1, 'true' emits y. Every utterance is decoded
-  on its own (its distance depends on its own mask only)."""
-  _check_alignment(alignment)
+  """Best path by differentiating the max-tropical distance w.r.t. zero
+  lexical masks, one per expansion of a frame (lattices.py:185-247 has one,
+  FrameDependent's only expansion): the one-hot derivative of mask i at
+  frame t names the label of the frame's (i+1)-th lexical arc, all-zero
+  means none. Returns labels [B, T * A] (A = 1 for FrameDependent, K + 1
+  for FrameLabelDependent: slot i of a frame the (i+1)-th lexical label,
+  else 0; the last slot is always 0) and the path weights. 'reference'
+  emits label y as y - 1, 'true' emits y. Every utterance is
+  decoded on its own (its distance depends on its own masks only)."""
+  K = expansions(alignment)
   B, T, C, R = W.shape
+  n_masks = max(K, 1)
   with torch.enable_grad():
-    mask = torch.zeros([B, T, 1, R - 1], dtype=W.dtype, requires_grad=True)
-    Wm = torch.cat([W.detach()[..., :1], W.detach()[..., 1:] + mask], dim=-1)
-    dist, _ = den_forward(Wm, nf, context, alignment, semirings.MaxTropical)
-    (g,) = torch.autograd.grad(dist.sum(), mask, allow_unused=True)
-  if g is None:
-    g = torch.zeros_like(mask)
-  g = g[:, :, 0, :]
-  blank = torch.all(g == 0, dim=-1)
-  idx = torch.argmax(g, dim=-1)
-  lexical = idx if label_convention == 'reference' else idx + 1
-  return torch.where(blank, torch.zeros_like(idx), lexical), dist.detach()
+    masks = [torch.zeros([B, T, 1, R - 1], dtype=W.dtype, requires_grad=True)
+             for _ in range(n_masks)]
+    dist, _ = den_forward(W.detach(), nf, context, alignment, semirings.MaxTropical,
+                          lex_masks=masks)
+    grads = torch.autograd.grad(dist.sum(), masks, allow_unused=True)
+  slots = []
+  for g in grads:
+    g = torch.zeros([B, T, R - 1], dtype=W.dtype) if g is None else g[:, :, 0, :]
+    blank = torch.all(g == 0, dim=-1)
+    idx = torch.argmax(g, dim=-1)
+    lexical = idx if label_convention == 'reference' else idx + 1
+    slots.append(torch.where(blank, torch.zeros_like(idx), lexical))
+  if K:
+    slots.append(torch.zeros_like(slots[0]))
+  return torch.stack(slots, dim=-1).reshape(B, T * len(slots)), dist.detach()

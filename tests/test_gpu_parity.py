@@ -17,7 +17,7 @@ import torch
 
 import last_torch_amd as lt
 from last_torch_amd import _native as nat
-from golden_cases import (LATTICE_CASES, assert_grad_close, assert_loss_close, assert_values_close,
+from golden_cases import (assert_grad_marginal_close, LATTICE_CASES, assert_grad_close, assert_loss_close, assert_values_close,
                           load)
 
 pytestmark = pytest.mark.gpu
@@ -93,7 +93,8 @@ def test_golden_loss_and_grad(cuda, case, local, ckpt):
   if not local:
     assert_loss_close(lz.cpu().numpy(), c['den_Log'])
   ref = c['loss_local_grad' if local else 'loss_grad']
-  assert_grad_close(dW.float().cpu().numpy(), ref, c['den_Log'], c['bf16'])
+  assert_grad_marginal_close(dW.float().cpu().numpy(), ref, None if local else c['den_grad'],
+                             c['den_Log'], c['num_Log'], c['bf16'])
 
 
 @pytest.mark.parametrize('case', LATTICE_CASES)
@@ -305,7 +306,8 @@ def test_golden_loss_grad(cuda, case, local, path):
   if not local:
     assert_loss_close(lz.cpu().numpy(), c['den_Log'])
   ref = c['loss_local_grad' if local else 'loss_grad']
-  assert_grad_close(dW.float().cpu().numpy(), ref, c['den_Log'], c['bf16'])
+  assert_grad_marginal_close(dW.float().cpu().numpy(), ref, None if local else c['den_grad'],
+                             c['den_Log'], c['num_Log'], c['bf16'])
   if d == nat.DESIGN_FUSED_PIPE:
     assert nat.grad_workspace_errors(ws, W, c['V'], c['n'], U, local) == 0
 
@@ -338,9 +340,10 @@ def test_random_loss_grad_vs_oracle(cuda, B, T, U, V, dt, path):
   for local in (False, True):
     ws = _poisoned_ws(Wd, V, n, U, local, d)
     loss, lz, _, dW = nat.loss_grad(Wd, nfd, labd, nld, V, n, local, workspace=ws, design=d)
-    rl, rlz, _, rdW = orc.loss_grad(W, nf, lab, nl, V, n, local_norm=local)
+    rl, rlz, rnum, rdW = orc.loss_grad(W, nf, lab, nl, V, n, local_norm=local)
+    den = None if local else orc.den_grad(W, nf, V, n)[1]
     assert_loss_close(loss.cpu().numpy(), rl)
-    assert_grad_close(dW.float().cpu().numpy(), rdW, rlz, bf16)
+    assert_grad_marginal_close(dW.float().cpu().numpy(), rdW, den, rlz, rnum, bf16)
     if path == 'fused':
       assert nat.grad_workspace_errors(ws, Wd, V, n, U, local) == 0
     # deterministic: a second call gives the same bits

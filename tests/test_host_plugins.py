@@ -157,8 +157,22 @@ def test_lattice_device_dispatch():
       alignment=lt.alignments.FrameLabelDependent(max_expansions=2),
       weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
       weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(table))
+  # FrameLabelDependent runs on the CPU path too (round 3)
+  loss = fsa(frames, torch.tensor([3, 2]), torch.ones([2, 2]), torch.tensor([1, 1]))
+  assert loss.device.type == 'cpu' and torch.isfinite(loss).all()
+  labels, nal, _ = fsa.shortest_path(frames, torch.tensor([3, 2]))
+  assert labels.shape == (2, 9) and nal.tolist() == [9, 6]
+
+  class NotAnAlignment:
+    def num_states(self):
+      return 1
+
+  odd = lt.RecognitionLattice(
+      context=lt.contexts.FullNGram(vocab_size=2, context_size=1), alignment=NotAnAlignment(),
+      weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+      weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(table))
   with pytest.raises(NotImplementedError, match='FrameDependent'):
-    fsa(frames, torch.tensor([3, 2]), torch.ones([2, 2]), torch.tensor([1, 1]))
+    odd(frames, torch.tensor([3, 2]), torch.ones([2, 2]), torch.tensor([1, 1]))
 
 
 # ---------------------------------------------------------------------------
