@@ -744,12 +744,62 @@ LT_DEVINL void advance(Cursor& c, const KArgs& a) {
   c.goff += c.step;
 }
 
+// Log numerator offsets: the recursion holds the string vector relative to
+// an integer offset O near its max (exact), so its roundings stay 2^-24 of
+// small numbers however long the utterance; history rows and num are O +
+// value, rounded once. The offset every lane subtracts at step k is the
+// floor of the max of the vector step k-1 read, taken by the first aux wave
+// into an LDS ping-pong slot (misc + kNumSub) between two barriers.
+constexpr int kNumSub = 8;
+LT_DEVINL float num_sub_take(const KArgs& a, unsigned char* lds, const float* vec, int NP, int al,
+                             int k) {
+  float* sub = (float*)(lds + a.off_misc) + kNumSub;
+  const float sp = sub[(k + 1) & 1];  // written at step k - 1
+  if (al < 64) {                      // the first aux wave: this step's input max
+    float m = -kInf;
+    for (int u = al; u < NP; u += 64) m = fmaxf(m, vec[u]);
+    m = gmax<6>(m, 6);
+    if (al == 0) sub[k & 1] = floorf(__builtin_isfinite(m) ? m : 0.f);
+  }
+  return sp;
+}
+LT_DEVINL void num_sub_init(const KArgs& a, unsigned char* lds, int al) {
+  if (al == 0) {
+    float* sub = (float*)(lds + a.off_misc) + kNumSub;
+    sub[0] = 0.f;
+    sub[1] = 0.f;
+  }
+}
+
+// The denominator's Log vector the same way: its offset slots at misc +
+// kDenSub, the max taken by the first den wave over the C states.
+constexpr int kDenSub = 12;
+LT_DEVINL float den_sub_take(const KArgs& a, unsigned char* lds, const float* vec, int C, int tid,
+                             int k) {
+  float* sub = (float*)(lds + a.off_misc) + kDenSub;
+  const float sp = sub[(k + 1) & 1];
+  if (tid < 64) {
+    float m = -kInf;
+    for (int q = tid; q < C; q += 64) m = fmaxf(m, vec[q]);
+    m = gmax<6>(m, 6);
+    if (tid == 0) sub[k & 1] = floorf(__builtin_isfinite(m) ? m : 0.f);
+  }
+  return sp;
+}
+LT_DEVINL void den_sub_init(const KArgs& a, unsigned char* lds, int tid) {
+  if (tid == 0) {
+    float* sub = (float*)(lds + a.off_misc) + kDenSub;
+    sub[0] = 0.f;
+    sub[1] = 0.f;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Forward kernel: denominator and/or numerator, Log / MaxTropical / Real.
 // ---------------------------------------------------------------------------
 template <int MODE, bool BF16, bool WST, int LG, int P>
-LT_DEVINL void den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int b, int nf,
-                            int tid) {
+LT_DEVINL float den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int b, int nf,
+                             int tid) {
   const NGram& g = a.g;
   const int C = g.C;
   const int lgL = LG >= 0 ? LG : a.lgL;
@@ -768,6 +818,9 @@ LT_DEVINL void den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int
                           (long long)b * a.T, false);
   float* hist = a.alpha ? a.alpha + (long long)b * a.T * C : nullptr;
   unsigned char* bpp = a.bp ? a.bp + (long long)b * a.T * C : nullptr;
+  // Log: alpha relative to an integer offset O near its max (den_sub_take),
+  // history rows O + value; MaxTropical / Real: exact values, no offset
+  float O = 0.f, sp = 0.f;
   // one destination group: terms -> semiring sum -> alpha_{t+1}[q]
   auto group = [&](int qq, const int* ao, const int* wo, int n2, const unsigned char* wrow,
                    const float* acur, float* anxt) {
@@ -783,18 +836,22 @@ LT_DEVINL void den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int
     int bi = 0;
     const float r = group_reduce<MODE, LG, P>(x, lgL, j * a.Pr, &bi);
     if (j == 0) {
-      anxt[qq] = r;
-      if (hist) hist[qq] = aself;
+      anxt[qq] = MODE == M_LOG ? r - sp : r;
+      if (hist) hist[qq] = MODE == M_LOG ? O + aself : aself;
       if (MODE == M_MAX && bpp) bpp[qq] = (unsigned char)bi;
     }
   };
   auto start_state = [&](const unsigned char* wrow, const float* acur, float* anxt) {
     if (a.extra0 && tid == 0) {  // blank self loop only
       const float av = acur[0];
-      anxt[0] = s_times<MODE>(av, ldw<BF16>(wrow, 0));
-      if (hist) hist[0] = av;
+      const float r = s_times<MODE>(av, ldw<BF16>(wrow, 0));
+      anxt[0] = MODE == M_LOG ? r - sp : r;
+      if (hist) hist[0] = MODE == M_LOG ? O + av : av;
       if (MODE == M_MAX && bpp) bpp[0] = 0;
     }
+  };
+  auto take = [&](int i, const float* acur) {
+    if constexpr (MODE == M_LOG) sp = den_sub_take(a, lds, acur, C, tid, i);
   };
   if (fast) {
     for (int i = 0; i < nf; ++i) {
@@ -804,8 +861,10 @@ LT_DEVINL void den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int
       const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
       const float* acur = abuf + (i & 1) * C;
       float* anxt = abuf + ((i + 1) & 1) * C;
+      take(i, acur);
       if (has) group(q, aoff, woff, nv, wrow, acur, anxt);
       start_state(wrow, acur, anxt);
+      O += sp;
       advance(cw, a);
       if (hist) hist += C;
       if (bpp) bpp += C;
@@ -820,6 +879,7 @@ LT_DEVINL void den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int
       const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
       const float* acur = abuf + (i & 1) * C;
       float* anxt = abuf + ((i + 1) & 1) * C;
+      take(i, acur);
       // a lane's slice advances by a constant from one pass to the next once
       // its destination is a full-order state and ngrp is a multiple of V
       // (the source base moves by ngrp / V, the label stays): no per-pass
@@ -840,16 +900,18 @@ LT_DEVINL void den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, int
         group(qq, ao, wo, n2, wrow, acur, anxt);
       }
       start_state(wrow, acur, anxt);
+      O += sp;
       advance(cw, a);
       if (hist) hist += C;
       if (bpp) bpp += C;
     }
   }
+  return O;
 }
 
 template <int MODE, bool BF16, bool WST>
-LT_DEVINL void num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, const int* ctx,
-                            const int* ylab, int b, int nf, int al, int aux_lanes) {
+LT_DEVINL float num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, const int* ctx,
+                             const int* ylab, int b, int nf, int al, int aux_lanes) {
   const int NP = a.U + 1;
   int ob = 0, olm = 0;
   if (al < NP) {
@@ -860,6 +922,7 @@ LT_DEVINL void num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, con
   Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)a.FR * (BF16 ? 2 : 4),
                           (long long)b * a.T, false);
   float* hist = a.alpha_num ? a.alpha_num + (long long)b * a.T * NP : nullptr;
+  float O = 0.f;  // Log: the vector's integer offset (MaxTropical / Real: 0, exact values)
   for (int i = 0; i < nf; ++i) {
     LT_STAMP(a, al == 0, 1, i, 0);
     lds_barrier();
@@ -867,6 +930,7 @@ LT_DEVINL void num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, con
     const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
     const float* ncur = nbuf + (i & 1) * NP;
     float* nnxt = nbuf + ((i + 1) & 1) * NP;
+    const float sp = MODE == M_LOG ? num_sub_take(a, lds, ncur, NP, al, i) : 0.f;
     for (int u = al; u < NP; u += aux_lanes) {
       int o0 = ob, o2 = olm;
       if (u != al) { o0 = ctx[u]; o2 = ctx[u - 1] + ylab[u - 1]; }
@@ -874,13 +938,15 @@ LT_DEVINL void num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, con
       const float xb = s_times<MODE>(cu, ldw<BF16>(wrow, o0));
       float xl = s_zero<MODE>();
       if (u >= 1) xl = s_times<MODE>(ncur[u - 1], ldw<BF16>(wrow, o2));
-      if (hist) hist[u] = cu;
-      nnxt[u] = s_plus<MODE>(xb, xl);
+      if (hist) hist[u] = MODE == M_LOG ? O + cu : cu;
+      nnxt[u] = MODE == M_LOG ? s_plus<MODE>(xb, xl) - sp : s_plus<MODE>(xb, xl);
     }
+    O += sp;
     advance(cw, a);
     if (hist) hist += NP;
     LT_STAMP(a, al == 0, 1, i, 2);
   }
+  return O;
 }
 
 template <int MODE, bool BF16, bool WST, int LG, int P>
@@ -915,24 +981,28 @@ LT_DEVINL void fwd_body(const KArgs& a, const int b) {
   } else if (role == 0) {
     if (do_den)
       for (int q = tid; q < C; q += den_lanes) abuf[q] = (q == 0) ? s_one<MODE>() : s_zero<MODE>();
+    den_sub_init(a, lds, tid);
   } else if (do_num) {
     for (int u = al; u < NP; u += aux_lanes) nbuf[u] = (u == 0) ? s_one<MODE>() : s_zero<MODE>();
     load_labels(a, b, ylab, al, aux_lanes);
+    num_sub_init(a, lds, al);
   }
   lds_barrier();
   if (role == 1 && do_num && al == 0) walk_states(a, ctx, ylab);
   lds_barrier();
+  float noff = 0.f;  // the numerator vector's final offset (Log)
+  float doff = 0.f;  // the denominator vector's final offset (Log)
 
   // ---- frame loop (alignment scan, lattices.py:856-892), one loop per role
   if (role == 2) {
     loader_loop(a, b, nf, false, lw, lane, ldsb);
   } else if (role == 0) {
     if (do_den && !LT_ABL(a, 1))
-      den_fwd_loop<MODE, BF16, WST, LG, P>(a, lds, abuf, b, nf, tid);
+      doff = den_fwd_loop<MODE, BF16, WST, LG, P>(a, lds, abuf, b, nf, tid);
     else idle_loop(nf);
   } else {
     if (do_num && !LT_ABL(a, 2))
-      num_fwd_loop<MODE, BF16, WST>(a, lds, nbuf, ctx, ylab, b, nf, al, aux_lanes);
+      noff = num_fwd_loop<MODE, BF16, WST>(a, lds, nbuf, ctx, ylab, b, nf, al, aux_lanes);
     else idle_loop(nf);
   }
   lds_barrier();
@@ -952,7 +1022,7 @@ LT_DEVINL void fwd_body(const KArgs& a, const int b) {
         float s = 0.f;
         for (int q = lane; q < C; q += 64) s += lt_exp(af[q] - c);
         s = gsum<6>(s, 6);
-        r = c + lt_log(s);
+        r = doff + (c + lt_log(s));
       } else if constexpr (MODE == M_MAX) {
         r = -kInf;
         for (int q = lane; q < C; q += 64)
@@ -972,21 +1042,24 @@ LT_DEVINL void fwd_body(const KArgs& a, const int b) {
     if (a.alpha) {  // padding frames carry alpha (lattices.py:460-461)
       const long long n = (long long)(a.T - nf) * C;
       float* dst = a.alpha + ((long long)b * a.T + nf) * C;
-      for (long long e = tid; e < n; e += den_lanes) dst[e] = af[e % C];
+      for (long long e = tid; e < n; e += den_lanes)
+        dst[e] = MODE == M_LOG ? doff + af[e % C] : af[e % C];
     }
   } else if (role == 1 && do_num) {
     const float* nfin = nbuf + fin * NP;
     if (al == 0) {
       const int nl = a.nlab[b];
       // lattices.py:375-377: (+) over positions equal to num_labels
-      const float r = (nl >= 0 && nl <= a.U) ? nfin[nl] : s_zero<MODE>();
+      const float r = (nl >= 0 && nl <= a.U) ? (MODE == M_LOG ? noff + nfin[nl] : nfin[nl])
+                                             : s_zero<MODE>();
       misc[1] = r;
       if (a.num) a.num[b] = r;
     }
     if (a.alpha_num) {
       const long long n = (long long)(a.T - nf) * NP;
       float* dst = a.alpha_num + ((long long)b * a.T + nf) * NP;
-      for (long long e = al; e < n; e += aux_lanes) dst[e] = nfin[e % NP];
+      for (long long e = al; e < n; e += aux_lanes)
+        dst[e] = MODE == M_LOG ? noff + nfin[e % NP] : nfin[e % NP];
     }
   }
   if (a.flags & F_LOSS) {
@@ -1044,6 +1117,10 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
   // CK: beta_t (computed at step i for frame t = nf-1-i) is frame t-1's
   // checkpoint row; the row of frame nf-1 (beta_nf = 0) is the prologue's.
   float* brow = (CK && a.beta) ? a.beta + (t_last - 1) * C : nullptr;
+  // beta relative to an integer offset Ob near its max (den_sub_take): the
+  // recursion's roundings stay small; rows are Ob + value, and a marginal's
+  // exponent takes the large terms as (alpha - log_z) + Ob first
+  float Ob = 0.f, dsub = 0.f;
   // one source group: beta_t[p] (alignments.py:315-316) and, unless CK, the
   // marginals of its out-arcs (alignments.py:311-314) -> dW
   auto group = [&](int p, const int* wo, const int* bo, int n2, const unsigned char* wrow,
@@ -1089,13 +1166,13 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
           s = gsum<LG>(ls, lgL);
         }
         if (j == 0 || (xwv && tid == L - 1)) {
-          const float bval = c + lt_log(s);
+          const float bval = (c + lt_log(s)) - dsub;
           bnxt[pl] = bval;
-          if (CK && crow) crow[pl] = bval;
+          if (CK && crow) crow[pl] = (Ob + dsub) + bval;
         }
         if constexpr (CK) return;
         // marginal exp(alpha + w + beta' - log_z) = e * exp(c + alpha - log_z)
-        const float sp = (gb == 0.f) ? 0.f : lt_exp(c + ap - log_z) * gb;
+        const float sp = (gb == 0.f) ? 0.f : lt_exp(((ap - log_z) + Ob) + c) * gb;
 #pragma unroll
         for (int m = 0; m < P; ++m) v[m] = x[m] * sp - nm[m];
       } else {
@@ -1135,7 +1212,9 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
                    : (BF16 ? (void*)((unsigned short*)a.dW + gframe)
                            : (void*)((float*)a.dW + gframe));
     float* crow = (brow && i < nf - 1) ? brow : nullptr;
+    dsub = den_sub_take(a, lds, bcur, C, tid, i);
     work(wrow, arow, bcur, bnxt, ncur, dWf, crow);
+    Ob += dsub;
     advance(cw, a);
     if (!CK) advance(ca, a);
     gframe -= FR;
@@ -1193,8 +1272,11 @@ template <bool BF16, bool DST>
 LT_DEVINL void num_bwd_frame(const KArgs& a, const unsigned char* wrow, const float* anrow,
                              const float* ncur, float* nnxt, float* mdst, float* side,
                              const int* ctx, const int* ylab, int al, int num_lanes, int ob,
-                             int ol, float gb, float numv) {
+                             int ol, float gb, float numv, float Ob, float sp) {
   const int NP = a.U + 1;
+  // beta^n in ncur is relative to the integer offset Ob (num_sub_take):
+  // the marginal's exponent alpha^n + w + beta^n - num takes it with alpha^n
+  // - num, the two large terms first
   for (int u = al; u < NP; u += num_lanes) {
     int o0 = ob, o1 = ol;
     if (u != al) { o0 = ctx[u]; o1 = u < a.U ? o0 + ylab[u] : 0; }
@@ -1204,7 +1286,7 @@ LT_DEVINL void num_bwd_frame(const KArgs& a, const unsigned char* wrow, const fl
     const float wl = ldw<BF16>(wrow, o1);
     const float bu = ncur[u];
     const float bu1 = ncur[lex ? u + 1 : u];
-    const float an = anrow[u] - numv;
+    const float an = (anrow[u] - numv) + Ob;
     const float xb = wb + bu;
     const float xl = lex ? wl + bu1 : -kInf;
     // log_plus (semirings.py:248-255) sharing its exponentials with the
@@ -1212,7 +1294,7 @@ LT_DEVINL void num_bwd_frame(const KArgs& a, const unsigned char* wrow, const fl
     float c = fmaxf(xb, xl);
     if (!__builtin_isfinite(c)) c = 0.f;
     const float eb = lt_exp(xb - c), el = lt_exp(xl - c);
-    nnxt[u] = c + lt_log(eb + el);
+    nnxt[u] = (c + lt_log(eb + el)) - sp;
     float mb = 0.f, ml = 0.f;
     if (gb != 0.f) {
       const float sc = lt_exp(an + c) * gb;
@@ -1253,11 +1335,15 @@ LT_DEVINL void num_bwd_loop(const KArgs& a, unsigned char* lds, float* nbb, floa
   const int lead = DST ? 1 : 0;  // frames ahead of the den lanes
   int nb = 0;                    // beta^n buffer parity
   int k3 = 0;                    // marginal buffer of the frame being computed
+  float Ob = 0.f;  // beta^n's integer offset
+  int k = 0;       // num_bwd_frame calls (the offset slots' parity)
   if (DST && nf > 0) {           // prologue frame nf-1 (after the caller's barrier)
     const unsigned char* wrow = WST ? ringw + cw.soff + cw.mis : a.W + cw.goff;
     const float* anrow = (const float*)(ringn + cn.soff + cn.mis);
+    const float sp = num_sub_take(a, lds, nbb, NP, al, k++);
     num_bwd_frame<BF16, DST>(a, wrow, anrow, nbb, nbb + NP, nbuf3, nullptr, ctx, ylab, al,
-                             num_lanes, ob, ol, gb, numv);
+                             num_lanes, ob, ol, gb, numv, Ob, sp);
+    Ob += sp;
     advance(cw, a);
     advance(cn, a);
     nb = 1;
@@ -1281,8 +1367,10 @@ LT_DEVINL void num_bwd_loop(const KArgs& a, unsigned char* lds, float* nbb, floa
       }
       const unsigned char* wrow = WST ? ringw + cw.soff + cw.mis : a.W + cw.goff;
       const float* anrow = (const float*)(ringn + cn.soff + cn.mis);
+      const float sp = num_sub_take(a, lds, nbb + nb * NP, NP, al, k++);
       num_bwd_frame<BF16, DST>(a, wrow, anrow, nbb + nb * NP, nbb + (nb ^ 1) * NP, mdst, side,
-                               ctx, ylab, al, num_lanes, ob, ol, gb, numv);
+                               ctx, ylab, al, num_lanes, ob, ol, gb, numv, Ob, sp);
+      Ob += sp;
       advance(cw, a);
       advance(cn, a);
       if (side) side -= NP * 2;
@@ -1310,6 +1398,7 @@ LT_DEVINL void num_beta_loop(const KArgs& a, unsigned char* lds, float* nbb, con
   Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)a.FR * es, t_last, true);
   float* row = a.beta_num ? a.beta_num + (t_last - 1) * NP : nullptr;
   int nb = 0;
+  float Ob = 0.f;  // the vector's integer offset (num_sub_take); rows are Ob + value
   for (int i = 0; i < nf; ++i) {
     LT_STAMP(a, al == 0, 1, i, 0);
     lds_barrier();
@@ -1318,6 +1407,8 @@ LT_DEVINL void num_beta_loop(const KArgs& a, unsigned char* lds, float* nbb, con
     const float* ncur = nbb + nb * NP;
     float* nnxt = nbb + (nb ^ 1) * NP;
     float* crow = (row && i < nf - 1) ? row : nullptr;
+    const float sp = num_sub_take(a, lds, ncur, NP, al, i);
+    Ob += sp;
     for (int u = al; u < NP; u += num_lanes) {
       int o0 = ob, o1 = ol;
       if (u != al) { o0 = ctx[u]; o1 = u < a.U ? o0 + ylab[u] : 0; }
@@ -1326,9 +1417,9 @@ LT_DEVINL void num_beta_loop(const KArgs& a, unsigned char* lds, float* nbb, con
       const float wl = ldw<BF16>(wrow, o1);
       const float bu = ncur[u];
       const float bu1 = ncur[lex ? u + 1 : u];
-      const float v = log_plus(wb + bu, lex ? wl + bu1 : -kInf);
+      const float v = log_plus(wb + bu, lex ? wl + bu1 : -kInf) - sp;
       nnxt[u] = v;
-      if (crow) crow[u] = v;
+      if (crow) crow[u] = Ob + v;
     }
     advance(cw, a);
     if (row) row -= NP;
@@ -1388,6 +1479,7 @@ LT_DEVINL void bwd_body(const KArgs& a, const int b) {
         if (crow) crow[p] = 0.f;
       }
     }
+    den_sub_init(a, lds, tid);
   } else {
     if (do_num) {
       float* crow = (CK && a.beta_num && nf > 0)
@@ -1398,6 +1490,7 @@ LT_DEVINL void bwd_body(const KArgs& a, const int b) {
         if (crow) crow[u] = v;
       }
       load_labels(a, b, ylab, al, aux_lanes);
+      num_sub_init(a, lds, al);
     }
     if (DST && do_num)
       for (int e = al; e < 3 * FR; e += aux_lanes) nbuf3[e] = 0.f;

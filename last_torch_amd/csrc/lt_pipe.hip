@@ -576,6 +576,10 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     if (!REV) v[s] = (u == 0) ? 0.f : -kInf;
     else v[s] = (u == nl) ? 0.f : -kInf;
   }
+  // the vector is kept relative to an integer offset near its max (exact),
+  // so the recursion's roundings are 2^-24 of small numbers however long the
+  // utterance; history rows and num are offset + value, rounded once
+  float off = 0.f;
   float* hist = REV ? a.beta_num : a.alpha_num;
   int* pub = a.fused ? a.prog + (REV ? 3 : 1) * a.B + b : nullptr;
   int tag_next = nf > 0 ? ctl[CTL_TAG] : 0;
@@ -599,7 +603,7 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
       float* hr = hist + (row0 + t) * NP;
 #pragma unroll
       for (int s = 0; s < PN; ++s)
-        if (PN * lane + s < NP) st_sc1(hr + PN * lane + s, v[s]);
+        if (PN * lane + s < NP) st_sc1(hr + PN * lane + s, off + v[s]);
     }
     float nv[PN];
     if (LT_ABL(a, 16)) {  // timing ablation: no numerator arithmetic
@@ -625,8 +629,15 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
         nv[s] = u < NP ? log_plus2(wb[s] + v[s], xl) : -kInf;
       }
     }
+    {
+      float vm = nv[0];
 #pragma unroll
-    for (int s = 0; s < PN; ++s) v[s] = nv[s];
+      for (int s = 1; s < PN; ++s) vm = fmaxf(vm, nv[s]);
+      const float fl = floorf(safe(wave_max(vm)));
+#pragma unroll
+      for (int s = 0; s < PN; ++s) v[s] = nv[s] - fl;
+      off += fl;
+    }
     asm volatile("" ::: "memory");  // LDS is in order per wave: no wait
     if (lane == 0) *(ctl + CTL_NUM) = i + 1;
     if (pub && ((i + 1) % kPubEvery) == 0) {
@@ -648,7 +659,7 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
         float* hr = a.alpha_num + (row0 + t) * NP;
 #pragma unroll
         for (int s = 0; s < PN; ++s)
-          if (PN * lane + s < NP) hr[PN * lane + s] = v[s];
+          if (PN * lane + s < NP) hr[PN * lane + s] = off + v[s];
       }
     }
     // lattices.py:375-377
@@ -656,8 +667,8 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     for (int s = 0; s < PN; ++s) {
       const int u = PN * lane + s;
       if (u < NP && u == nl) {
-        ((lds_float*)(as3(lds) + a.off_ctl))[CTL_FIN1] = v[s];
-        if (a.num) a.num[b] = v[s];
+        ((lds_float*)(as3(lds) + a.off_ctl))[CTL_FIN1] = off + v[s];
+        if (a.num) a.num[b] = off + v[s];
       }
     }
     if (lane == 0 && !(nl >= 0 && nl <= U)) {
