@@ -1172,7 +1172,9 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
         }
         if constexpr (CK) return;
         // marginal exp(alpha + w + beta' - log_z) = e * exp(c + alpha - log_z)
-        const float sp = (gb == 0.f) ? 0.f : lt_exp(((ap - log_z) + Ob) + c) * gb;
+        // (no finite out-term: no marginal, whatever alpha - log_z is)
+        const float sp = (gb == 0.f || !__builtin_isfinite(mx))
+                             ? 0.f : lt_exp(((ap - log_z) + Ob) + c) * gb;
 #pragma unroll
         for (int m = 0; m < P; ++m) v[m] = x[m] * sp - nm[m];
       } else {
@@ -1292,11 +1294,14 @@ LT_DEVINL void num_bwd_frame(const KArgs& a, const unsigned char* wrow, const fl
     // log_plus (semirings.py:248-255) sharing its exponentials with the
     // marginals exp(an + x) = exp(x - c) * exp(an + c)
     float c = fmaxf(xb, xl);
-    if (!__builtin_isfinite(c)) c = 0.f;
+    // no path through (t, u) on either arc: no marginal (alpha^n alone may
+    // be far above num, and exp of it times a zero term is NaN)
+    const bool live = __builtin_isfinite(c);
+    if (!live) c = 0.f;
     const float eb = lt_exp(xb - c), el = lt_exp(xl - c);
     nnxt[u] = (c + lt_log(eb + el)) - sp;
     float mb = 0.f, ml = 0.f;
-    if (gb != 0.f) {
+    if (gb != 0.f && live) {
       const float sc = lt_exp(an + c) * gb;
       mb = eb * sc;
       ml = el * sc;

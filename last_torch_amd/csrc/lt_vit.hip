@@ -106,12 +106,10 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
       glds16(a.W + a0 + 16LL * g, dst + 1024u * i);
     }
   };
-  // frame f's DMA has landed. In vmcnt's issue order a step s issues the
-  // previous frame's backpointer store (s >= 1) and then the ring issue of
-  // frame s + kAhead; frame f = t + 1 is awaited in step t, before that
-  // step's own store and issue, so the younger operations are step t-1's
-  // store and issue (frame t + 2), or the ring issue alone in step 1.
-  auto wait_next = [&](int t) { wait_vmcnt(ni + (t >= 2 ? 1 : 0)); };
+  // frame t's DMA has landed: ring issues and one backpointer store a step,
+  // in issue order (vmcnt counts both, in order)
+  // (frame t - 1's store goes out in step t, before that step's ring issue)
+  auto wait_frame = [&](int t) { wait_vmcnt((kAhead - 1) * ni + min(max(t - 1, 0), kAhead - 1)); };
   if (nf > 0) {
     for (int d = 0; d < kAhead; ++d) issue(d);
   }
@@ -134,26 +132,20 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
     if ((h == 0 && live) || lane == 32)
       __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bpv, bpr, lane == 32 ? 0 : q, tb * C, 0);
   };
-  // the frame's weights, read from its ring slot into registers one step
-  // ahead: in step t they are issued right after alpha_t's reads, so the
-  // LDS queue (in order per wave) returns alpha first and the chain waits
-  // for nothing else; alpha never waits on a weight read
-  auto load_weights = [&](int t, VitFrame& F) {
-    const unsigned char* fr =
-        &s_ring[t % kSlots][0] + ((goff0 + (long long)fclamp(t) * fbytes) & 15);
-#pragma unroll
-    for (int m = 0; m < kHalf; ++m) F.w[m] = vlds<BF16>(fr, vb + m * (FULL ? 33 : R) * es);
-    F.self = vlds<BF16>(fr, vself);
-    F.w00 = vlds<BF16>(fr, 0);
-  };
-  VitFrame F;
-  if (nf > 0) {
-    wait_vmcnt(2 * ni);  // frame 0 (frames 1 and 2 may still be in flight)
-    load_weights(0, F);
-  }
-  for (int t = 0; t < nf; ++t) {
+  auto step = [&](int t) {
+    if (t >= nf) return;  // the last round's spare steps
     const float* acur = s_al[t & 1];
     float* anxt = s_al[(t + 1) & 1];
+    wait_frame(t);
+    VitFrame F;
+    {
+      const unsigned char* fr =
+          &s_ring[t % kSlots][0] + ((goff0 + (long long)fclamp(t) * fbytes) & 15);
+#pragma unroll
+      for (int m = 0; m < kHalf; ++m) F.w[m] = vlds<BF16>(fr, vb + m * (FULL ? 33 : R) * es);
+      F.self = vlds<BF16>(fr, vself);
+      F.w00 = vlds<BF16>(fr, 0);
+    }
     // the sources' alpha: five b128 reads of the lane's half
     float al[20];
 #pragma unroll
@@ -162,12 +154,6 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
       al[4 * g + 0] = v.x; al[4 * g + 1] = v.y; al[4 * g + 2] = v.z; al[4 * g + 3] = v.w;
     }
     const float aq = acur[aslot(min(q, V))];
-    asm volatile("" ::: "memory");  // the weight prefetch stays behind alpha's reads
-    VitFrame Fn;
-    if (t + 1 < nf) {
-      wait_next(t);
-      load_weights(t + 1, Fn);
-    }
     if (t > 0) emit_bp(t - 1);
     float x[kHalf];
 #pragma unroll
@@ -192,7 +178,6 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
     // permlane32_swap hands the upper lanes the lower half's value in [0]
     // and the lower lanes the upper half's in [1]
     const float r = fmaxf(mx, __int_as_float(h ? pv[0] : pv[1]));
-    // LDS is in order per wave: the next step's reads see these writes
     if (h == 0 && live) anxt[aslot(q)] = r;
     a0 += w00;
     if (lane == 32) anxt[0] = a0;
@@ -201,11 +186,11 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
     for (int m = 0; m < kHalf; ++m) xq[m] = x[m];
     xsq = xs;
     rq = r;
-    if (t + 1 < nf) F = Fn;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-  }
+  };
+  for (int t = 0; t < nf; ++t) step(t);
   if (nf > 0) emit_bp(nf - 1);
-  __builtin_amdgcn_s_waitcnt(0xc07f);
   // the distance: (+)_q alpha_T[q] in MaxTropical, the first maximum
   const float* af = s_al[nf & 1];
   float r = lane < C ? af[aslot(lane)] : -kInf;
