@@ -310,7 +310,7 @@ def chunk_len(B, T, U, V):
   while True:
     n16 = (L * FB + 30) // 16
     b = ((n16 + 63) // 64) * 1024 + 2 * al16(4 * L * CP) + 2 * al16(4 * L * NPG) + \
-        al16(8 * L * NPG) + al16(32 * L) + al16(8 * NPG + 4 * U) + al16(4 * L) + 1024 + al16(4 * (2 * L + 2))
+        al16(8 * L * NPG) + al16(32 * L) + al16(8 * NPG + 4 * U) + al16(4 * L) + 1024 + al16(4 * (2 * L + 3))
     if L <= 4 or b <= budget:
       return L
     L -= 1

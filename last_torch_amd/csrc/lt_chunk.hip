@@ -69,7 +69,10 @@ constexpr float kCert = 64.f;   // phase C's per-frame certificate: log2(max alp
 #endif
 constexpr int kAbWaves = LT_AB_WAVES;  // ck_ab_kernel: waves per SIMD its registers allow
 constexpr unsigned kSpinMax = 1u << 20;
-constexpr int kWalkSlots = 3;                    // phase B: den walk record ring depth (LDS)
+#ifndef LT_WALK_SLOTS
+#define LT_WALK_SLOTS 3
+#endif
+constexpr int kWalkSlots = LT_WALK_SLOTS;        // phase B: den walk record ring depth (LDS)
 constexpr int kRecNi = (4 * kRec + 1023) / 1024;  // LDS-DMA wave instructions per record
 constexpr int kWalkSlot = kRecNi * 1024;         // bytes per ring slot
 constexpr int kWalkLds = 2 * kWalkSlots * kWalkSlot;  // dynamic LDS of the walk launches  // phase B's bound on polls without progress (~1 s)
@@ -97,6 +100,8 @@ struct CkArgs {
   float* nbbd;             // [B,K+1,NPG] num beta at chunk starts
   float* cf;               // [B,T] frame offsets c_t = ceil(max W_t) (phase A's)
   unsigned* ready;         // [B,K] chunk k's record and bands published (scratch, zeroed per call)
+  unsigned* prog;          // [B,4] phase 2's boundaries done per walk (zeroed with ready)
+  float* mid;              // [B,2] phase 1's den alpha and num alpha offsets at the middle
   float* loss;
   float* log_z;            // state copies (read by C)
   float* num;
@@ -108,6 +113,8 @@ struct CkArgs {
   int NGc;                 // numerator groups per chunk, ceil(L / kGrp)
   int nc, wpos;            // ck_ab_kernel: nc walking workgroups (B fused, 0 not) from block wpos
   int nbs;                 // floats per chunk of numerator bands (whole 128-byte lines)
+  int half;                // 1: the walks stop at the middle (phase 1), phase C's launch finishes them
+  int cont;                // phase C's launch: blocks [0, B) finish the walks (phase 2)
   int local;               // LocallyNormalizedWeightFn: no denominator
   int strict;              // 1 (lt_chunk_forward): a chunk outside the strict range (flag 3)
                            // leaves the fast path in B; 0: phase C's certificate decides
@@ -729,6 +736,55 @@ LT_DEVINL void load_rec_beta(const float* rc, int lane, RecBeta& r) {
   r.cs = rc[kRecCs];
 }
 
+// The walks in two halves (lt_loss_grad): phase 1 runs beside phase A as far
+// as the middle chunk boundary Kh = Kl / 2 -- alpha over chunks [0, Kh),
+// beta over [Kh, Kl), the chunks phase A publishes first (outside-in) -- and
+// phase 2 finishes them in phase C's launch, from the boundary rows and
+// offsets phase 1 left, while C's workgroups take the chunks middle-out as
+// their boundaries land. So the launch of A no longer waits for the second
+// half of every walk (a walk is K steps of ~0.6 us, as long as A itself), and
+// that half overlaps C. Phase 0: the whole walk in one go (lt_chunk_forward).
+// Phase 2 publishes its boundary rows write-through (relaxed agent-scope
+// stores) and, every kProgStep boundaries and at its end, after its own
+// s_waitcnt vmcnt(0), the count of boundaries done to a progress word
+// (CkArgs::prog) that phase C's workgroups poll before their boundary loads.
+constexpr int kProgStep = 4;
+enum { kWalkFull = 0, kWalkFirst = 1, kWalkRest = 2 };
+LT_DEVINL void bd_store(float* p, float v, bool wt) {
+  if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+LT_DEVINL void prog_publish(const CkArgs& a, int b, int w, int n, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0)
+    __hip_atomic_store((gu32*)(a.prog + 4LL * b + w), (unsigned)n, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The walks' LDS, carved from the launch's dynamic LDS (no static LDS, so
+// phase C's launch can hold them at its own four workgroups per CU): the den
+// record rings, the numerator alpha's scatter table and beta's padded copy,
+// the den step operand rows, three scalars.
+constexpr int kWalkNvA = (128 + kGrp + 1) * (kGrp + 2);
+constexpr int kWalkNvB = 128 + kGrp + 1;
+constexpr int kWalkLdsBytes = kWalkLds + 4 * (kWalkNvA + kWalkNvB) + 4 * 128 + 16;
+struct WalkLds {
+  unsigned char* ring;
+  float *nva, *nvb, *bc, *lz, *num;
+  int* bad;
+};
+LT_DEVINL WalkLds walk_lds(unsigned char* base) {
+  WalkLds w;
+  w.ring = base;
+  w.nva = (float*)(base + kWalkLds);
+  w.nvb = w.nva + kWalkNvA;
+  w.bc = w.nvb + kWalkNvB;
+  w.lz = w.bc + 128;
+  w.num = w.lz + 1;
+  w.bad = (int*)(w.num + 1);
+  return w;
+}
+
 // Phase B's numerator over the groups of kGrp frames (phase A's bands),
 // base-2 log space. FWD, alpha (lattices.py:340-377 composed per group):
 // al'[u] = (+)_d al[u - d] + N[u - d][d], scattered by destination through
@@ -737,23 +793,21 @@ LT_DEVINL void load_rec_beta(const float* rc, int lane, RecBeta& r) {
 // Boundary values at every chunk start -> nabd / nbbd (log2, each vector
 // relative to the walk's integer offset at that boundary: phase C normalises
 // every frame by its own total, so only differences within a vector matter).
-template <int PPL, bool FWD>
+// D groups of bands in registers ahead.
+template <int PPL, bool FWD, int D>
 LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl, float* lds,
-                        float* s_num, ChunkReady& rd) {
+                        float* s_num, ChunkReady& rd, int ph) {
   const int NPG = a.NPG;
-  // ---- numerator over the groups of kGrp frames (phase A's bands), base-2
-  // log space. alpha (wave 2, lattices.py:340-377 composed per group):
-  // al'[u] = (+)_d al[u - d] + N[u - d][d]; beta (wave 3, the reverse of
-  // alignments.py:320-329): be'[s] = (+)_d N[s][d] + be[s + d]. The
-  // neighbours come from an LDS copy of the vector padded with -inf.
-  // groups in registers ahead (2 PPL loads each: vmcnt <= 63); PPL = 2 keeps
-  // the walk inside the fused launch's register budget
-  constexpr int D = PPL == 1 ? 8 : (kAbWaves > 3 ? 4 : 5);
   constexpr int NB = kGrp + 1;
   constexpr int TS = NB + 1;  // alpha's scatter table row stride (odd: no bank conflicts)
   const int NGc = a.NGc;
   const int ntl = nf - (Kl - 1) * a.L;  // live frames of the last chunk
   const int Q = Kl > 0 ? (Kl - 1) * NGc + (ntl + kGrp - 1) / kGrp : 0;
+  const int Kh = Kl / 2, qh = Kh * NGc;  // the middle chunk boundary's group
+  // this phase's groups [q0, q1): alpha walks them up, beta down
+  const int q0 = ph == kWalkRest ? (FWD ? qh : 0) : (FWD ? 0 : (ph == kWalkFirst ? qh : 0));
+  const int q1 = ph == kWalkRest ? (FWD ? Q : qh) : (FWD ? (ph == kWalkFirst ? qh : Q) : Q);
+  const bool wt = ph == kWalkRest;
   const float* nb0 = a.nb + (long long)b * a.K * a.nbs;
   // alpha: tab[u][d] = al[u - d] + N[u - d][d] (rows u < d stay -inf);
   // beta: sv[s] = be[s] with sv[64 PPL, +NB) = -inf
@@ -766,14 +820,31 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
   }
   float v[PPL];
   float off = 0.f;  // the vector's integer offset (log2): the walk holds v - off
-#pragma unroll
-  for (int r = 0; r < PPL; ++r) v[r] = (lane + 64 * r == (FWD ? 0 : nl)) ? 0.f : -kInf;
   float* dst = (FWD ? a.nabd : a.nbbd) + (long long)b * (a.K + 1) * NPG;
-  if (!FWD) {
+  if (ph == kWalkRest) {  // phase 1's vector at the middle boundary, and alpha's offset
 #pragma unroll
-    for (int r = 0; r < PPL; ++r)
-      if (lane + 64 * r < NPG) dst[(long long)Kl * NPG + lane + 64 * r] = v[r];
+    for (int r = 0; r < PPL; ++r) {
+      const int u = lane + 64 * r;
+      const float x = dst[(long long)Kh * NPG + min(u, NPG - 1)];
+      v[r] = u < NPG ? x : -kInf;
+    }
+    if (FWD) off = a.mid[2LL * b + 1];
+  } else {
+#pragma unroll
+    for (int r = 0; r < PPL; ++r) v[r] = (lane + 64 * r == (FWD ? 0 : nl)) ? 0.f : -kInf;
+    if (!FWD) {
+#pragma unroll
+      for (int r = 0; r < PPL; ++r)
+        if (lane + 64 * r < NPG) dst[(long long)Kl * NPG + lane + 64 * r] = v[r];
+    }
   }
+  int pub = 0;  // phase 2: boundaries published (progress word)
+  auto publish = [&](int done, bool last) {
+    if (wt && (last || done - pub >= kProgStep)) {
+      prog_publish(a, b, FWD ? 2 : 3, done, lane);
+      pub = done;
+    }
+  };
   // band rows N[s][0 .. kGrp] of group q for the lane's source positions
   float4 gq[D][PPL][2];
   auto bload = [&](int q, float4 (*g)[2]) {
@@ -793,7 +864,8 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
     if (FWD && q % NGc == 0) {  // a chunk starts here
 #pragma unroll
       for (int r = 0; r < PPL; ++r)
-        if (lane + 64 * r < NPG) dst[(long long)(q / NGc) * NPG + lane + 64 * r] = v[r];
+        if (lane + 64 * r < NPG) bd_store(dst + (long long)(q / NGc) * NPG + lane + 64 * r, v[r], wt);
+      publish(q / NGc - Kh, false);
     }
     float n[PPL][NB];
 #pragma unroll
@@ -845,22 +917,33 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
     if (!FWD && q % NGc == 0) {  // beta at the chunk's first frame
 #pragma unroll
       for (int r = 0; r < PPL; ++r)
-        if (lane + 64 * r < NPG) dst[(long long)(q / NGc) * NPG + lane + 64 * r] = v[r];
+        if (lane + 64 * r < NPG) bd_store(dst + (long long)(q / NGc) * NPG + lane + 64 * r, v[r], wt);
+      publish(Kh - q / NGc, false);
     }
     __builtin_amdgcn_wave_barrier();
   };
-  // alpha walks q = 0 .. Q-1, beta q = Q-1 .. 0
-  auto qof = [&](int n) { return FWD ? n : Q - 1 - n; };
+  const int cnt = q1 - q0;
+  auto qof = [&](int n) { return FWD ? q0 + n : q1 - 1 - n; };
 #pragma unroll
   for (int d = 0; d < D; ++d) bload(qof(d), gq[d]);
-  const int nmain = Q - Q % D;
+  const int nmain = cnt - cnt % D;
   for (int n0 = 0; n0 < nmain; n0 += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) step(gq[d], qof(n0 + d), qof(n0 + d + D));
   }
 #pragma unroll
   for (int d = 0; d < D; ++d)
-    if (nmain + d < Q) step(gq[d], qof(nmain + d), qof(nmain + d));
+    if (nmain + d < cnt) step(gq[d], qof(nmain + d), qof(nmain + d));
+  if (ph == kWalkFirst) {
+    if (FWD) {  // alpha at the middle boundary (phase 2's start) and its offset
+#pragma unroll
+      for (int r = 0; r < PPL; ++r)
+        if (lane + 64 * r < NPG) dst[(long long)Kh * NPG + lane + 64 * r] = v[r];
+      if (lane == 0) a.mid[2LL * b + 1] = off;
+    }
+    return;
+  }
+  publish(FWD ? (Kl - 1) - Kh : Kh, true);
   if constexpr (FWD) {
     float nv = -kInf;
 #pragma unroll
@@ -874,32 +957,36 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
 }
 
 // Utterance b's walks, one per wave, each following phase A's progress
-// through the ready flags (ChunkReady) when A runs in the same launch.
-template <int PPL>
-LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
-  __shared__ __attribute__((aligned(16))) float s_bc[2][64];
-  __shared__ int s_bad;
-  __shared__ float s_lz, s_num;
-  __shared__ float s_nv[2][(128 + kGrp + 1) * (kGrp + 2)];
+// through the ready flags (ChunkReady) when A runs in the same launch; `ph`
+// as above; `dyn` the launch's dynamic LDS (walk_lds).
+template <int PPL, int D>
+LT_DEVINL void combine_role(const CkArgs& a, int b, int wave, unsigned char* dyn, int ph) {
+  const WalkLds wl = walk_lds(dyn);
   const int lane = threadIdx.x & 63;
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const int Kl = (nf + a.L - 1) / a.L;  // live chunks
+  const int Kh = Kl / 2;                // the middle boundary (phases 1 and 2)
   const int V = a.V, C = a.C, CP = a.CP;
   const int nl = a.nlab[b];
-  if (threadIdx.x == 0) s_bad = 0;
+  if (ph == kWalkRest && a.uflag[b]) return;  // phase 1 sent it to the frame-serial kernels
+  if (threadIdx.x == 0) *wl.bad = 0;
   __syncthreads();
   CK_WSTAMP(2 * wave);
   ChunkReady rd(a.ready + (long long)b * a.K, Kl, a.strict);
+  if (ph == kWalkRest) {  // every chunk published (phase A's launch is over)
+    rd.lo = 0;
+    rd.hi = Kl - 1;
+  }
+  const bool wt = ph == kWalkRest;
 
   // den walks: the records stream through a ring of kWalkSlots LDS slots
   // per wave by LDS-DMA (1 KiB contiguous per instruction), issued
   // kWalkSlots steps ahead; each step reads its record from LDS. (Records
   // gathered straight into registers -- a row per lane for alpha, a column
   // for beta -- stalled each step about as long as the rest of the step.)
-  extern __shared__ __attribute__((aligned(16))) unsigned char ck_dyn[];
-  const unsigned ring_a = lds_base_addr(ck_dyn) + (unsigned)(wave * kWalkSlots * kWalkSlot);
-  const unsigned char* ring = ck_dyn + wave * kWalkSlots * kWalkSlot;
+  const unsigned ring_a = lds_base_addr(wl.ring) + (unsigned)(wave * kWalkSlots * kWalkSlot);
+  const unsigned char* ring = wl.ring + wave * kWalkSlots * kWalkSlot;
   auto issue_rec = [&](int k, int n) {  // step n's record k (clamped to [0, Kl)) -> slot n mod kWalkSlots
     const int kc = min(max(k, 0), Kl - 1);
     dma_issue((const unsigned char*)a.rec, ((long long)b * a.K + kc) * (kRec * 4), kRec * 4,
@@ -907,7 +994,7 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
   };
   // step n's record has landed: the ring's issues and each step's one
   // boundary-row store, in issue order (vmcnt counts both, in order; the
-  // flag polls drain it themselves)
+  // flag polls and progress words drain it themselves)
   auto wait_rec = [&](int n) {
     wait_vmcnt(n < kWalkSlots ? kRecNi * (kWalkSlots - 1) + n : (kRecNi + 1) * kWalkSlots - kRecNi);
   };
@@ -919,19 +1006,29 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
     // vector's max. The records' scales (ej, rho) and offsets (csum) are
     // integers, so O is exact and every stored value stays small: its
     // rounding is 2^-24 of a small number however long the utterance.
-    float* bc = s_bc[0];  // bc[j] = a_{j+1} (core source j), bc[32] = a_0
-    float al = lane == 0 ? 0.f : -kInf;  // lane p: alpha[p] - O
-    float O = 0.f;
+    float* bc = wl.bc;  // bc[j] = a_{j+1} (core source j), bc[32] = a_0
     float* dst = a.abd + (long long)b * (a.K + 1) * CP;
-    if (lane < C) dst[lane] = al;
-    if (Kl > 0) {
-      rd.ensure_fwd(kWalkSlots - 1, lane);
-      for (int n = 0; n < kWalkSlots; ++n) issue_rec(n, n);
+    const int k0 = ph == kWalkRest ? Kh : 0, k1 = ph == kWalkFirst ? Kh : Kl;
+    float al, O;
+    if (ph == kWalkRest) {  // phase 1's vector at the middle boundary and its offset
+      const float x = dst[(long long)Kh * CP + min(lane, C - 1)];
+      al = lane < C ? x : -kInf;
+      O = a.mid[2LL * b];
+    } else {
+      al = lane == 0 ? 0.f : -kInf;  // lane p: alpha[p] - O
+      O = 0.f;
+      if (lane < C) dst[lane] = al;
     }
-    for (int k = 0; k < Kl; ++k) {
-      wait_rec(k);
+    int pub = 0;
+    if (k1 > k0) {
+      rd.ensure_fwd(k0 + kWalkSlots - 1, lane);
+      for (int n = 0; n < kWalkSlots; ++n) issue_rec(k0 + n, n);
+    }
+    for (int k = k0; k < k1; ++k) {
+      const int n = k - k0;
+      wait_rec(n);
       RecAlpha R;
-      load_rec_alpha(slot(k), lane, V, R);
+      load_rec_alpha(slot(n), lane, V, R);
       const float x = lane < C ? al + R.sc : -kInf;
       const float M = safe_max(wmax_u(x));
       const float av = lane < C ? __builtin_amdgcn_exp2f(x - M) : 0.f;
@@ -958,37 +1055,54 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
       // the slot's last read has returned: its next record goes in
       __builtin_amdgcn_s_waitcnt(0xc07f);
       rd.ensure_fwd(k + kWalkSlots, lane);
-      issue_rec(k + kWalkSlots, k + kWalkSlots);
+      issue_rec(k + kWalkSlots, n + kWalkSlots);
       const float fl = floorf(M);
       const float nq = (M - fl) + __builtin_amdgcn_logf(s0 + s1);  // lane i < 32: alpha'[i+1] - O'
       const float n0 = first_lane(al) + pi - fl;
       O += cs + fl;
       const float sh = from_prev(nq, -kInf);
       al = lane == 0 ? n0 : (lane < C ? sh : -kInf);
-      if (lane < C) dst[(long long)(k + 1) * CP + lane] = al;
+      if (lane < C) bd_store(dst + (long long)(k + 1) * CP + lane, al, wt);
+      if (wt && k + 1 - Kh - pub >= kProgStep && k + 1 < k1) {
+        prog_publish(a, b, 0, k + 1 - Kh, lane);
+        pub = k + 1 - Kh;
+      }
       __builtin_amdgcn_wave_barrier();
     }
-    // log_z = (+)_q alpha_T[q] (lattices.py:496), back to natural log once
-    const float x = lane < C ? al : -kInf;
-    const float M = safe_max(wmax_u(x));
-    const float s = wsum_u(lane < C ? __builtin_amdgcn_exp2f(x - M) : 0.f);
-    if (lane == 0)
-      s_lz = (float)(((double)O + (double)(M + __builtin_amdgcn_logf(s))) * 0.6931471805599453);
+    if (ph == kWalkFirst) {
+      if (lane == 0) a.mid[2LL * b] = O;
+    } else {
+      if (wt) prog_publish(a, b, 0, k1 - Kh, lane);
+      // log_z = (+)_q alpha_T[q] (lattices.py:496), back to natural log once
+      const float x = lane < C ? al : -kInf;
+      const float M = safe_max(wmax_u(x));
+      const float s = wsum_u(lane < C ? __builtin_amdgcn_exp2f(x - M) : 0.f);
+      if (lane == 0)
+        *wl.lz = (float)(((double)O + (double)(M + __builtin_amdgcn_logf(s))) * 0.6931471805599453);
+    }
   } else if (wave == 1 && !a.local && !LT_ABL(a, 1)) {
     // ---- den beta across chunks: beta_T = one for every state
     // (lattices.py:788-790); log2, relative to an integer offset as alpha
     // (the offset itself is not needed: nothing reads beta's absolute value)
-    float* bc = s_bc[1];
+    float* bc = wl.bc + 64;
     const int h = lane >> 5;
-    float be = lane < C ? 0.f : -kInf;  // lane p: beta[p] - O
     float* dst = a.bbd + (long long)b * (a.K + 1) * CP;
-    if (lane < C) dst[(long long)Kl * CP + lane] = be;
-    if (Kl > 0) {
-      rd.ensure_bwd(Kl - kWalkSlots, lane);
-      for (int n = 0; n < kWalkSlots; ++n) issue_rec(Kl - 1 - n, n);
+    const int k0 = ph == kWalkFirst ? Kh : 0, k1 = ph == kWalkRest ? Kh : Kl;  // chunks, walked down
+    float be;  // lane p: beta[p] - O
+    if (ph == kWalkRest) {
+      const float x = dst[(long long)Kh * CP + min(lane, C - 1)];
+      be = lane < C ? x : -kInf;
+    } else {
+      be = lane < C ? 0.f : -kInf;
+      if (lane < C) dst[(long long)Kl * CP + lane] = be;
     }
-    for (int n = 0; n < Kl; ++n) {
-      const int k = Kl - 1 - n;
+    int pub = 0;
+    if (k1 > k0) {
+      rd.ensure_bwd(k1 - kWalkSlots, lane);
+      for (int n = 0; n < kWalkSlots; ++n) issue_rec(k1 - 1 - n, n);
+    }
+    for (int n = 0; n < k1 - k0; ++n) {
+      const int k = k1 - 1 - n;
       wait_rec(n);
       RecBeta R;
       load_rec_beta(slot(n), lane, R);
@@ -1021,28 +1135,44 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
       const float nb0 = lse2_b2(first_lane(be) + pi - fl, rterm);
       const float sh = from_prev(nj, -kInf);
       be = lane == 0 ? nb0 : (lane < C ? sh : -kInf);
-      if (lane < C) dst[(long long)k * CP + lane] = be;
+      if (lane < C) bd_store(dst + (long long)k * CP + lane, be, wt);
+      if (wt && Kh - k - pub >= kProgStep && k > k0) {
+        prog_publish(a, b, 1, Kh - k, lane);
+        pub = Kh - k;
+      }
       __builtin_amdgcn_wave_barrier();
     }
+    if (wt) prog_publish(a, b, 1, Kh - k0, lane);
   } else if (wave == 2 && !LT_ABL(a, 2) && !LT_ABL(a, 128)) {
-    num_walk<PPL, true>(a, b, lane, nf, Kl, nl, s_nv[0], &s_num, rd);
+    num_walk<PPL, true, D>(a, b, lane, nf, Kl, nl, wl.nva, wl.num, rd, ph);
   } else if (wave == 3 && !LT_ABL(a, 2)) {
-    num_walk<PPL, false>(a, b, lane, nf, Kl, nl, s_nv[1], nullptr, rd);
+    num_walk<PPL, false, D>(a, b, lane, nf, Kl, nl, wl.nvb, nullptr, rd, ph);
   }
   // any chunk out of the fast path's range (a weight not finite, or a frame
   // spanning more than kRange; every walk has seen every chunk's flag) or a
   // hand-off timeout: the frame-serial kernels take the utterance
-  if (lane == 0 && (rd.bad || !rd.ok)) s_bad = 1;
+  if (lane == 0 && (rd.bad || !rd.ok)) *wl.bad = 1;
   CK_WSTAMP(2 * wave + 1);
   __syncthreads();
-  if (s_bad) {
+  if (ph == kWalkFirst) {  // phase 2 (phase C's launch) finishes the walks
+    if (threadIdx.x == 0) a.uflag[b] = *wl.bad ? 1 : 0;
+    return;
+  }
+  if (*wl.bad) {
     if (threadIdx.x == 0) a.uflag[b] = 1;
     return;
   }
   if (threadIdx.x == 0) {
-    a.uflag[b] = 0;
-    const float lz = a.local ? 0.f : s_lz;
-    const float nm = s_num;
+    const float lz = a.local ? 0.f : *wl.lz;
+    const float nm = *wl.num;
+    // phase 2: phase C's workgroups took the chunks before log_z and num
+    // existed; a denominator with no finite path, a NaN or an unreachable
+    // string (the reference's semantics, dW = 0) goes to the frame-serial
+    // kernels after the launch, which rewrite the utterance
+    if (ph == kWalkRest && ((!a.local && !__builtin_isfinite(lz)) || !__builtin_isfinite(nm)))
+      a.uflag[b] = 1;
+    else if (ph == kWalkFull)
+      a.uflag[b] = 0;
     a.log_z[b] = lz;
     a.num[b] = nm;
     if (a.lz_out) a.lz_out[b] = lz;
@@ -1050,6 +1180,14 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave) {
     a.loss[b] = a.local ? -nm : lz - nm;  // lattices.py:178-183
   }
 }
+
+// numerator band groups in registers ahead: the walk launches' (2 PPL loads
+// each: vmcnt <= 63; PPL = 2 keeps the walk inside the fused launch's
+// register budget) and phase C's (its four workgroups per CU)
+template <int PPL>
+constexpr int kWalkD = PPL == 1 ? 8 : (kAbWaves > 3 ? 4 : 5);
+template <int PPL>
+constexpr int kWalkDc = PPL == 1 ? 4 : 3;
 
 // A and B in one launch: the nc = B workgroups at block indices [wpos, wpos
 // + nc) walk one utterance each (nc = 0: ck_combine_kernel walks after the
@@ -1067,7 +1205,8 @@ __global__ __launch_bounds__(256, kAbWaves) void ck_ab_kernel(const CkArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int x = blockIdx.x;
   if (x >= a.wpos && x < a.wpos + nc) {
-    combine_role<PPL>(a, x - a.wpos, wave);
+    extern __shared__ __attribute__((aligned(16))) unsigned char ck_dyn[];
+    combine_role<PPL, kWalkD<PPL>>(a, x - a.wpos, wave, ck_dyn, a.half ? kWalkFirst : kWalkFull);
     return;
   }
   if (x >= a.wpos) x -= nc;
@@ -1085,7 +1224,9 @@ __global__ __launch_bounds__(256, kAbWaves) void ck_ab_kernel(const CkArgs a) {
 
 template <int PPL>
 __global__ __launch_bounds__(256) void ck_combine_kernel(const CkArgs a) {
-  combine_role<PPL>(a, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  extern __shared__ __attribute__((aligned(16))) unsigned char ck_dyn[];
+  combine_role<PPL, kWalkD<PPL>>(a, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                                 ck_dyn, a.half ? kWalkFirst : kWalkFull);
 }
 
 // Phase C's gather tables: per position, in LDS (labels staged by the whole
@@ -1121,12 +1262,21 @@ constexpr int kFlA = 1, kFlB = 2, kFlNA = 4, kFlNB = 8, kFlAll = 15;
 template <bool BF16, int PPL, bool FULL>
 __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kernel(const CkArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int b = blockIdx.x / a.K, k = blockIdx.x - (blockIdx.x / a.K) * a.K;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a.cont && (int)blockIdx.x < a.B) {  // phase 2 of utterance blockIdx.x's walks
+    combine_role<PPL, kWalkDc<PPL>>(a, blockIdx.x, wave, lds, kWalkRest);
+    return;
+  }
+  // level j of utterance b: chunks middle-out (Kh, Kh - 1, Kh + 1, Kh - 2,
+  // ...: the order phase 2's boundaries land in), then the padding chunks
+  const int c = a.cont ? (int)blockIdx.x - a.B : (int)blockIdx.x;
+  const int j = c / a.B, b = c - j * a.B;
   if (a.uflag[b]) return;  // the frame-serial kernels own this utterance
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int Kl = (nf + a.L - 1) / a.L, Kh = Kl / 2;
+  const int k = j < 2 * Kh ? ((j & 1) ? Kh - 1 - (j >> 1) : Kh + (j >> 1)) : j;
   const int t0 = k * a.L;
   const int tend = min(t0 + a.L, a.T);
   const int t1 = max(t0, min(t0 + a.L, nf));
@@ -1135,15 +1285,17 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   const int NPG = a.NPG, NP = a.NP;
   const int FRP = (FR + 3) & ~3;
   float g = a.grad ? a.grad[b] : 1.f;
-  const float lz = a.log_z[b], nm = a.num[b];
-  // a NaN, or a denominator with no finite path (the relaxed path admits
-  // masked arcs): the frame-serial kernels own the utterance (the
-  // reference's semantics for such lattices)
-  if ((!a.local && !__builtin_isfinite(lz)) || __builtin_isnan(nm)) {
-    if (tid == 0) a.uflag[b] = 1;
-    return;
+  if (!a.cont) {  // (phase 2 checks log_z and num itself, once they exist)
+    const float lz = a.log_z[b], nm = a.num[b];
+    // a NaN, or a denominator with no finite path (the relaxed path admits
+    // masked arcs): the frame-serial kernels own the utterance (the
+    // reference's semantics for such lattices)
+    if ((!a.local && !__builtin_isfinite(lz)) || __builtin_isnan(nm)) {
+      if (tid == 0) a.uflag[b] = 1;
+      return;
+    }
+    if (!__builtin_isfinite(nm)) g = 0.f;  // unreachable string: loss +inf, dW = 0
   }
-  if (!__builtin_isfinite(nm)) g = 0.f;  // unreachable string: loss +inf, dW = 0
   const long long e0 = ((long long)b * a.T + t0) * FR;
   if (t1 <= t0 || g == 0.f) {  // padding chunk / unreachable string: dW = 0
     const long long n = (long long)(tend - t0) * FR;
@@ -1168,14 +1320,53 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   float* buf = (float*)(lds + a.c_off_buf) + 64 * wave;
   float* cfl = (float*)(lds + a.c_off_cf);
   if (tid < nt) cfl[tid] = a.cf[(long long)b * a.T + t0 + tid];
+  int* fl = (int*)(lds + a.c_off_fl);
+  // phase 2's boundaries this chunk needs (alpha at k, beta at k + 1): one
+  // lane polls the walks' progress words, then the agent-scope acquire
+  // before any wave's loads of them (after the barriers below)
+  if (a.cont && tid == 0) {
+    const int need_a = k - Kh, need_b = Kh - (k + 1);
+    const unsigned* pg = a.prog + 4LL * b;
+    int ok = 1;
+    for (unsigned spins = 0;; ++spins) {
+      bool done = true;
+      if (need_a > 0)
+        done = (a.local || (int)poll_flag(pg + 0) >= need_a) && (int)poll_flag(pg + 2) >= need_a;
+      if (done && need_b > 0)
+        done = (a.local || (int)poll_flag(pg + 1) >= need_b) && (int)poll_flag(pg + 3) >= need_b;
+      if (done) break;
+      if (spins > kSpinMax) {  // phase 2 never ran (a placement that starves it)
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    acquire_agent();
+    fl[2 * a.L + 2] = ok;
+  }
   gather_tables(a, b, labs, boff, loff, tid, blockDim.x);
   wait_vmcnt(0);
   __syncthreads();
+  if (a.cont && !fl[2 * a.L + 2]) {
+    if (tid == 0) a.uflag[b] = 1;
+    return;
+  }
   CK_STAMP(1);
-  // E_f = exp(W_f - c_f) (c_f = ceil(max W_f), so E <= 1): in place over
-  // the f32 image, in a region of its own for bf16
+  // E_f = exp(W_f - c_f) (c_f = phase A's integer offset, log2 units, so
+  // E <= 1) is formed by the den recursions as they first read the frame,
+  // from the staged W, and stored to E_f's home (in place over the f32
+  // image, a float region of its own for bf16): alpha owns frames [0, hs),
+  // beta [hs, nt), the ones each reaches first, and each reads the other's
+  // frames as E once that frame's bit is set. No pass and barrier of its
+  // own, one exponential per element. The marginals read E_f and leave the
+  // frame's dW in its place.
+  const int hs = (nt + 1) / 2;
+  auto wrow = [&](int f) -> const unsigned char* { return wch + f * a.FB; };
   auto eptr = [&](int f) -> float* {
     return BF16 ? (float*)(lds + a.c_off_e) + f * FRP : (float*)(wch + f * a.FB);
+  };
+  auto ew = [](float w, float cl) -> float {
+    return __builtin_amdgcn_exp2f(__builtin_fmaf(w, kLog2e, -cl));
   };
   // the numerator's arc weights leave W first (exact, log2); every read of
   // this pass issues before the barrier, every E store after it
@@ -1205,7 +1396,6 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   if (tid < nt) fs[tid * kFs + kFsW00] = ldsw<BF16>(wch + tid * a.FB, 0) * kLog2e;
   // per-frame progress bits for the marginal pass (kFl*), the frames in
   // the order their inputs complete (middle first), a job counter
-  int* fl = (int*)(lds + a.c_off_fl);
   int* ford = fl + a.L;
   int* njob = ford + a.L;
   int* cert_fail = njob + 1;  // a frame outside the certificate (any wave)
@@ -1219,25 +1409,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     *njob = 0;
     *cert_fail = 0;
   }
-  __syncthreads();  // the gathers above read W; E overwrites it below
-  // E in place, frame by frame: each thread's elements of a frame loaded
-  // together (element-wise: no barrier between a thread's reads and stores)
-  constexpr int kEi = 5;  // ceil(33 * 33 / 256)
-  for (int f = 0; f < nt; ++f) {
-    const unsigned char* fr = wch + f * a.FB;
-    float* ef = eptr(f);
-    const float cl = cfl[f];  // log2 units (phase A's integer offset)
-    float v[kEi];
-#pragma unroll
-    for (int i = 0; i < kEi; ++i) v[i] = ldsw<BF16>(fr, min(tid + 64 * kMargWaves * i, FR - 1));
-#pragma unroll
-    for (int i = 0; i < kEi; ++i)
-      if (tid + 64 * kMargWaves * i < FR) ef[tid + 64 * kMargWaves * i] =
-          __builtin_amdgcn_exp2f(__builtin_fmaf(v[i], kLog2e, -cl));
-    for (int e = tid + 64 * kMargWaves * kEi; e < FR; e += 64 * kMargWaves)  // V > 32 never
-      ef[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(ldsw<BF16>(fr, e), kLog2e, -cl));
-  }
-  __syncthreads();
+  __syncthreads();  // nw, fs, fl and the job order for every wave
   CK_STAMP(5);
   // every LDS load below is unconditional (clamped index, unused values
   // masked afterwards): a load under a branch would pay its full latency
@@ -1250,6 +1422,15 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   };
   auto mark_all = [&](int bit) {
     for (int f = 0; f < nt; ++f) mark(f, bit);
+  };
+  auto wait_bits = [&](int f, int want) {
+    for (;;) {
+      const int bits = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(fl + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if ((bits & want) == want) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
 
   if (wave == 0 && !a.local && !LT_ABL(a, 4)) {
@@ -1273,14 +1454,32 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     float S = wmax_u(core ? x0 : -kInf);  // -inf: no core state reached yet
     float al = (core && S != -kInf) ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     for (int f = 0; f < nt; ++f) {
-      const float* ef = eptr(f);
+      const unsigned char* fr = wrow(f);
+      float* ef = eptr(f);
       const float cl = cfl[f];
       const float w00 = fs[f * kFs + kFsW00];
-      float e[16];
+      float e[16], e32, eb;
+      if (f < hs) {  // alpha's frame: E from W, stored to its home
 #pragma unroll
-      for (int m = 0; m < 16; ++m) e[m] = ef[min(16 * h + m, C - 1) * R + qe];
-      const float e32 = ef[min(32, C - 1) * R + qe];
-      const float eb = ef[qe * R];
+        for (int m = 0; m < 16; ++m) e[m] = ldsw<BF16>(fr, min(16 * h + m, C - 1) * R + qe);
+        e32 = ldsw<BF16>(fr, min(32, C - 1) * R + qe);
+        eb = ldsw<BF16>(fr, qe * R);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) e[m] = ew(e[m], cl);
+        e32 = ew(e32, cl);
+        eb = ew(eb, cl);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) ef[min(16 * h + m, C - 1) * R + qe] = e[m];
+        ef[min(32, C - 1) * R + qe] = e32;
+        ef[qe * R] = eb;
+        if (lane == 0) ef[0] = 0.f;  // (0, 0) is taken in log2 (xb[0] = 0)
+      } else {       // beta's: E once beta has passed it
+        wait_bits(f, kFlB);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) e[m] = ef[min(16 * h + m, C - 1) * R + qe];
+        e32 = ef[min(32, C - 1) * R + qe];
+        eb = ef[qe * R];
+      }
       const float mc = wmax_u(core ? al : 0.f);
       int ex;
       (void)frexpf(mc, &ex);
@@ -1329,14 +1528,32 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     float S = safe_max(wmax_u(core ? x0 : -kInf));
     float be = core ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     for (int f = nt - 1; f >= 0; --f) {
-      const float* ef = eptr(f);
+      const unsigned char* fr = wrow(f);
+      float* ef = eptr(f);
       const float cl = cfl[f];
       const float w00 = fs[f * kFs + kFsW00];
-      float e[16];
+      float e[16], eb, e0y;  // e0y = E[0][j+1]
+      if (f >= hs) {  // beta's frame: E from W, stored to its home
 #pragma unroll
-      for (int m = 0; m < 16; ++m) e[m] = ef[pe * R + min(16 * h + m + 1, V)];
-      const float eb = ef[pe * R];
-      const float e0y = ef[min(j, V - 1) + 1];  // E[0][j+1]
+        for (int m = 0; m < 16; ++m) e[m] = ldsw<BF16>(fr, pe * R + min(16 * h + m + 1, V));
+        eb = ldsw<BF16>(fr, pe * R);
+        e0y = ldsw<BF16>(fr, min(j, V - 1) + 1);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) e[m] = ew(e[m], cl);
+        eb = ew(eb, cl);
+        e0y = ew(e0y, cl);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) ef[pe * R + min(16 * h + m + 1, V)] = e[m];
+        ef[pe * R] = eb;
+        ef[min(j, V - 1) + 1] = e0y;
+        if (lane == 0) ef[0] = 0.f;
+      } else {        // alpha's: E once alpha has passed it
+        wait_bits(f, kFlA);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) e[m] = ef[pe * R + min(16 * h + m + 1, V)];
+        eb = ef[pe * R];
+        e0y = ef[min(j, V - 1) + 1];
+      }
       const float mc = wmax_u(be);
       int ex;
       (void)frexpf(mc, &ex);
@@ -1612,7 +1829,7 @@ int al16(long long x) { return (int)((x + 15) & ~15LL); }
 
 struct CkLayout {
   // state (kept from lt_chunk_forward to lt_chunk_backward)
-  size_t uflag, lz, num, abd, bbd, nabd, nbbd, cf, state;
+  size_t uflag, lz, num, abd, bbd, nabd, nbbd, cf, mid, state;
   // scratch: forward = records + numerator bands; backward = the fallback's checkpoints
   size_t ready, rec, nb, f_alpha, f_an, f_loss, f_lz, f_num, f_side, scratch;
 };
@@ -1665,7 +1882,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
     t->c_off_tab = off; off += al16(8LL * a->NPG + 4LL * a->U);
     t->c_off_cf = off; off += al16(4LL * L);
     t->c_off_buf = off; off += 4 * 64 * 4;
-    t->c_off_fl = off; off += al16(4LL * (2 * L + 2));
+    t->c_off_fl = off; off += al16(4LL * (2 * L + 3));
     t->c_off_e = off; off += bf16 ? al16(4LL * L * ((a->FR + 3) & ~3)) : 0;
     return off;
   };
@@ -1690,9 +1907,10 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   w->nabd = o; o += up256(4 * B * (K + 1) * a->NPG);
   w->nbbd = o; o += up256(4 * B * (K + 1) * a->NPG);
   w->cf = o; o += up256(4 * B * T);
+  w->mid = o; o += up256(8 * B);
   w->state = o;
   size_t s = 0;
-  w->ready = s; s += up256(4LL * B * K);
+  w->ready = s; s += up256(4LL * B * K + 16LL * B);  // ready flags, then the progress words
   w->rec = s; s += up256(4LL * B * K * kRec);
   a->nbs = (a->NGc * (kGrp + 1) * a->NPG + 31) & ~31;
   w->nb = s; s += up256(4LL * B * K * a->nbs);
@@ -1719,9 +1937,11 @@ void ck_bind(CkArgs* a, const CkLayout& w, void* state, void* scratch) {
   a->nabd = (float*)(st + w.nabd);
   a->nbbd = (float*)(st + w.nbbd);
   a->cf = (float*)(st + w.cf);
+  a->mid = (float*)(st + w.mid);
   a->rec = sc ? (float*)(sc + w.rec) : nullptr;
   a->nb = sc ? (float*)(sc + w.nb) : nullptr;
   a->ready = sc ? (unsigned*)(sc + w.ready) : nullptr;
+  a->prog = sc ? (unsigned*)(sc + w.ready) + (long long)a->B * a->K : nullptr;
 }
 
 int ck_launch(const void* k, int grid, int lds, hipStream_t st, const CkArgs& a,
@@ -1782,7 +2002,7 @@ int ck_cus() {
 // (tools/walk_sweep.py: B = 64 best at 0-25 %, B = 128 at 50-65 %;
 // LT_CHUNK_WALK_AT overrides, in percent).
 int ck_launch_ab(CkArgs& a, bool bf16, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(a.ready, 0, 4LL * a.B * a.K, st);
+  hipError_t e = hipMemsetAsync(a.ready, 0, 4LL * a.B * a.K + 16LL * a.B, st);
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   const bool fuse = a.B <= ck_cus() && ck_env("LT_CHUNK_FUSE", 1) != 0;
   a.nc = fuse ? a.B : 0;
@@ -1790,10 +2010,10 @@ int ck_launch_ab(CkArgs& a, bool bf16, hipStream_t st) {
   const long long nwa = (items + 3) / 4;
   const int at = ck_env("LT_CHUNK_WALK_AT", std::max(0, 100 - 4800 / std::max(a.B, 1)));
   a.wpos = (int)(nwa * std::min(std::max(at, 0), 100) / 100);
-  int rc = ck_launch(ck_kernel_ab(a.PPL, bf16, a.V == 32), (int)(a.nc + nwa), fuse ? kWalkLds : 0,
-                     st, a);
+  int rc = ck_launch(ck_kernel_ab(a.PPL, bf16, a.V == 32), (int)(a.nc + nwa),
+                     fuse ? kWalkLdsBytes : 0, st, a);
   if (rc || fuse) return rc;
-  return ck_launch(ck_kernel_b(a.PPL), a.B, kWalkLds, st, a);
+  return ck_launch(ck_kernel_b(a.PPL), a.B, kWalkLdsBytes, st, a);
 }
 const void* ck_kernel_c(int ppl, bool bf16, bool full) {
   if (full)
@@ -1867,9 +2087,12 @@ int chunk_loss_grad(const lt_problem* pb, int local_norm, const void* W, const i
   a.dW = dW;
   hipStream_t st = (hipStream_t)stream;
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  // the walks' second halves run in phase C's launch (blocks [0, B))
+  a.half = 1;
   if ((rc = ck_launch_ab(a, bf16, st))) return rc;
-  if ((rc = ck_launch(ck_kernel_c(a.PPL, bf16, a.V == 32), a.B * a.K, ck_lds_c(a, bf16), st, a,
-                      64 * kMargWaves)))
+  a.cont = 1;
+  if ((rc = ck_launch(ck_kernel_c(a.PPL, bf16, a.V == 32), a.B + a.B * a.K,
+                      std::max(ck_lds_c(a, bf16), kWalkLdsBytes), st, a, 64 * kMargWaves)))
     return rc;
   char* sc = (char*)scratch;
   return serial_loss(pb, local_norm, W, num_frames, labels, num_labels, a.uflag, loss, log_z, num,

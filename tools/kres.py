@@ -8,10 +8,11 @@ import subprocess
 import sys
 
 src = sys.argv[1]
+extra = [x for x in sys.argv[3:]]
 flt = sys.argv[2] if len(sys.argv) > 2 else ''
 out = subprocess.run(['/opt/rocm/bin/hipcc', '-O3', '-std=c++17', '-fPIC', '--offload-arch=gfx950',
                       '-c', src, '-o', '/tmp/kres.o', '-Rpass-analysis=kernel-resource-usage',
-                      '--offload-device-only'], capture_output=True, text=True).stderr
+                      '--offload-device-only'] + extra, capture_output=True, text=True).stderr
 cur = None
 rows = {}
 for line in out.splitlines():
