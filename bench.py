@@ -172,6 +172,35 @@ def weights_leg(B, T, U, V, n, C, device, reps=10):
   return out
 
 
+def cold_w_leg(B, T, U, V, n, C, device, nbuf=3, reps=12):
+  """lt_loss_grad with `nbuf` W buffers used in rotation:
+  3 x 279 MB at B=64 cannot sit in the 256 MiB Infinity Cache, so each call
+  reads its W from HBM. Reported beside the same call on one W (hot)."""
+  lab = torch.randint(1, V + 1, [B, U], generator=torch.Generator(device=device).manual_seed(7),
+                      device=device, dtype=torch.int32)
+  nf = torch.full([B], T, dtype=torch.int32, device=device)
+  nl = torch.full([B], U, dtype=torch.int32, device=device)
+  Ws = [make_inputs(B, T, U, V, C, device, seed=300 + i)[0] for i in range(nbuf)]
+  ws = torch.empty([_native.loss_grad_workspace_bytes(Ws[0], V, n, U, False)], dtype=torch.uint8,
+                   device=device)
+  out = {'buffers': nbuf, 'w_bytes_each': Ws[0].numel() * 4}
+  for name, order in (('hot', [0] * reps), ('cold', [i % nbuf for i in range(reps)])):
+    for i in range(nbuf):
+      _native.loss_grad(Ws[i], nf, lab, nl, V, n, False, workspace=ws)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(True), torch.cuda.Event(True)) for _ in order]
+    for (e0, e1), i in zip(evs, order):
+      e0.record()
+      _native.loss_grad(Ws[i], nf, lab, nl, V, n, False, workspace=ws)
+      e1.record()
+    torch.cuda.synchronize()
+    out[f'{name}_ms_per_call'] = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+  out['cold_over_hot'] = out['cold_ms_per_call'] / out['hot_ms_per_call']
+  del Ws, ws
+  torch.cuda.empty_cache()
+  return out
+
+
 def joint_step_leg(T, U, V, n, device, B=64, F=256, H=512, reps=5):
   """a whole training step of RecognitionLattice driven
   by SharedEmbCacher + JointWeightFn (weight_fns.py:174-242) at the bench
@@ -608,6 +637,7 @@ def main():
     torch.cuda.empty_cache()
     if not args.no_weights and fused:
       result['realistic_weights'] = weights_leg(B, T, U, V, n, C, device)
+      result['cold_w'] = cold_w_leg(B, T, U, V, n, C, device)
     if not args.no_joint:
       result['joint_weight_fn_step'] = joint_step_leg(T, U, V, n, device)
 
