@@ -16,7 +16,15 @@ p_of = $(word 2,$(subst _, ,$(1)))
 LIB := last_torch_amd/liblt_lattice.so
 DEPS := $(CSRC)/lt_kernels.h include/lt_lattice.h
 
-all: $(LIB) oracle
+CPULIB := last_torch_amd/liblt_lattice_cpu.so
+CXX ?= g++
+CPUFLAGS ?= -O3 -std=c++17 -fPIC -march=x86-64-v3 -Wall -pthread
+
+all: $(LIB) $(CPULIB) oracle
+
+# the host twin (include/lt_lattice_cpu.h): g++ only, no HIP
+$(CPULIB): $(CSRC)/lt_cpu.cpp include/lt_lattice_cpu.h include/lt_lattice.h
+	$(CXX) $(CPUFLAGS) -shared -o $@ $<
 
 $(OBJ)/lt_inst_%.o: $(CSRC)/lt_inst.hip $(DEPS)
 	@mkdir -p $(OBJ)
@@ -53,7 +61,7 @@ oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf $(OBJ) $(LIB)
+	rm -rf $(OBJ) $(LIB) $(CPULIB)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

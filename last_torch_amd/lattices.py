@@ -18,7 +18,9 @@ weights once through the ``WeightFn`` plugin as a contiguous
 The device of the arc weights picks the implementation, as in the
 reference: ROCm tensors run the HIP kernels (FrameDependent and
 FrameLabelDependent alignments, FullNGram or any next-state table), CPU
-tensors the PyTorch restatement in ``cpu.py`` (FrameDependent). There is no
+tensors the C++ host twin (``liblt_lattice_cpu.so``, include/lt_lattice_cpu.h:
+``forward`` and ``shortest_path`` of FullNGram x FrameDependent) or the
+PyTorch restatement in ``cpu.py`` (every other method and lattice). There is no
 fallback between the two: a ROCm tensor never runs on the CPU, and a missing
 HIP library raises. Arbitrary batch dims are flattened (the reference's
 ``_string_forward`` supports only one, D13).
@@ -30,6 +32,7 @@ import torch
 import torch.nn as nn
 
 from last_torch_amd import _native
+from last_torch_amd import _native_cpu
 from last_torch_amd import alignments
 from last_torch_amd import cpu
 from last_torch_amd import contexts
@@ -104,6 +107,32 @@ class _LossFn(torch.autograd.Function):
       dW = _native.loss_grad(W, nf, labels, nl, V, n, local)[3]
     _native.scale_grad(dW, g.float().contiguous(), V, n)
     return dW, None, None, None, None, None, None
+
+
+class _CpuLossFn(torch.autograd.Function):
+  """The same loss on host tensors through the C++ twin (lt_cpu_loss_grad,
+  include/lt_lattice_cpu.h): FullNGram x FrameDependent, loss and
+  d(sum loss)/dW in one call on the host thread pool; the backward scales
+  it by the incoming gradient."""
+
+  @staticmethod
+  def forward(ctx, W, nf, labels, nl, V, n, local):
+    want = ctx.needs_input_grad[0]
+    loss, _, _, dW = _native_cpu.loss_grad(W, nf, labels, nl, V, n, local, with_grad=want)
+    ctx.dW = dW
+    if want:
+      ctx.save_for_backward(W, nf, labels, nl)
+    ctx.cfg = (V, n, local)
+    return loss
+
+  @staticmethod
+  def backward(ctx, g):
+    dW = ctx.dW
+    ctx.dW = None
+    if dW is None:  # a second backward through the same graph
+      W, nf, labels, nl = ctx.saved_tensors
+      dW = _native_cpu.loss_grad(W, nf, labels, nl, *ctx.cfg)[3]
+    return (dW * g.to(dW.dtype)[:, None, None, None], None, None, None, None, None, None)
 
 
 class _TableLossFn(torch.autograd.Function):
@@ -306,7 +335,10 @@ class RecognitionLattice(nn.Module, Generic[T]):
     nl = _lengths(num_labels, B, W.device)
     local = isinstance(self.weight_fn, weight_fns.LocallyNormalizedWeightFn)
     if W.device.type == 'cpu':
-      loss = cpu.loss(W, nf, lab, nl.long(), self.context, self.alignment, local)
+      if not self._table_path() and _native_cpu.available():
+        loss = _CpuLossFn.apply(W, nf, lab.contiguous(), nl, V, n, local)
+      else:
+        loss = cpu.loss(W, nf, lab, nl.long(), self.context, self.alignment, local)
     elif self._table_path():
       loss = _TableLossFn.apply(W, nf, lab.contiguous(), nl, self._graph(W.device), local)
     else:
@@ -326,7 +358,9 @@ class RecognitionLattice(nn.Module, Generic[T]):
     conv = {'reference': _native.LABELS_REFERENCE, 'true': _native.LABELS_TRUE}[label_convention]
     W, nf, batch_dims, B, V, n, _ = self._prepare(cache, frames, num_frames)
     with torch.no_grad():
-      if W.device.type == 'cpu':
+      if W.device.type == 'cpu' and not self._table_path() and _native_cpu.available():
+        labels, weights, _ = _native_cpu.viterbi(W.detach(), nf, V, n, conv)
+      elif W.device.type == 'cpu':
         labels, weights = cpu.viterbi(W, nf, self.context, self.alignment, label_convention)
       elif self._table_path():
         # A labels per frame: slot i = the (i+1)-th lexical label of the frame
