@@ -18,7 +18,7 @@ DEPS := $(CSRC)/lt_kernels.h include/lt_lattice.h
 
 CPULIB := last_torch_amd/liblt_lattice_cpu.so
 CXX ?= g++
-CPUFLAGS ?= -O3 -std=c++17 -fPIC -march=x86-64-v3 -Wall -pthread
+CPUFLAGS ?= -O3 -std=c++17 -fPIC -march=x86-64-v3 -fno-math-errno -fopenmp-simd -Wall -pthread
 
 all: $(LIB) $(CPULIB) oracle
 
@@ -46,6 +46,10 @@ $(OBJ)/lt_chunk.o: $(CSRC)/lt_chunk.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+$(OBJ)/lt_tri.o: $(CSRC)/lt_tri.hip $(DEPS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
 $(OBJ)/lt_vit.o: $(CSRC)/lt_vit.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -54,7 +58,7 @@ $(OBJ)/lt_producer.o: $(CSRC)/lt_producer.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_vit.o $(INST_OBJS)
+$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_vit.o $(OBJ)/lt_tri.o $(INST_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
 oracle:
@@ -78,7 +82,7 @@ $(STAMP_OBJ)/lt_lattice.o: $(CSRC)/lt_lattice.hip $(DEPS)
 $(STAMP_OBJ)/lt_pipe.o: $(CSRC)/lt_pipe.hip $(DEPS)
 	@mkdir -p $(STAMP_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -c -o $@ $<
-stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_vit.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
+stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_vit.o $(OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(STAMP_OBJ)/liblt_lattice_stamps.so $^
 .PHONY: stamps
 
@@ -91,6 +95,6 @@ $(DIAG_OBJ)/lt_inst_%.o: $(CSRC)/lt_inst.hip $(DEPS)
 $(DIAG_OBJ)/%.o: $(CSRC)/%.hip $(DEPS)
 	@mkdir -p $(DIAG_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_DIAG -c -o $@ $<
-diag: $(DIAG_OBJ)/lt_lattice.o $(DIAG_OBJ)/lt_pipe.o $(DIAG_OBJ)/lt_chunk.o $(DIAG_OBJ)/lt_table.o $(DIAG_OBJ)/lt_producer.o $(DIAG_OBJ)/lt_vit.o $(foreach v,$(VARIANTS),$(DIAG_OBJ)/lt_inst_$(v).o)
+diag: $(DIAG_OBJ)/lt_lattice.o $(DIAG_OBJ)/lt_pipe.o $(DIAG_OBJ)/lt_chunk.o $(DIAG_OBJ)/lt_table.o $(DIAG_OBJ)/lt_producer.o $(DIAG_OBJ)/lt_vit.o $(DIAG_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(DIAG_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(DIAG_OBJ)/liblt_lattice_diag.so $^
 .PHONY: diag

@@ -271,6 +271,35 @@ def cpu_ref(T, U, V, n, sample_utts):
   }
 
 
+def cpu_twin(T, U, V, n, C, sample_utts):
+  """The C++ host twin of the library (liblt_lattice_cpu.so,
+  include/lt_lattice_cpu.h: the same lattice, loss + dW, fp32, utterances
+  over a host thread pool) on the same workload shape, timed on this box's
+  host cores (at most 16 threads: the GPU box's CPU share)."""
+  from last_torch_amd import _native_cpu
+  threads = max(1, min(16, len(os.sched_getaffinity(0))))
+  _native_cpu.set_num_threads(threads)
+  g = torch.Generator().manual_seed(0)
+  W = torch.randn([sample_utts, T, C, V + 1], generator=g)
+  nf = torch.full([sample_utts], T, dtype=torch.int32)
+  lab = torch.randint(1, V + 1, (sample_utts, U), generator=g, dtype=torch.int32)
+  nl = torch.full([sample_utts], U, dtype=torch.int32)
+  _native_cpu.loss_grad(W[:threads], nf[:threads], lab[:threads], nl[:threads], V, n)  # warm
+  t0 = time.perf_counter()
+  _native_cpu.loss_grad(W, nf, lab, nl, V, n)
+  dt = time.perf_counter() - t0
+  return {
+      'value': sample_utts * T * U * C / dt,
+      'unit': 'cells/s',
+      'cores': threads,
+      'kind': 'port',
+      'affinity_cores': len(os.sched_getaffinity(0)),
+      'sample': (f'C++ host twin (last_torch_amd/liblt_lattice_cpu.so, lt_cpu_loss_grad: loss + '
+                 f'dW, fp32) on {sample_utts} utterances of T={T} U={U} V={V} n={n}: '
+                 f'{dt:.2f} s on {threads} threads'),
+  }
+
+
 def cpu_baseline(T, U, V, n, C, sample_utts):
   """The C oracle (single-threaded restatement of the reference) on a
   bounded sample of the same workload: loss + dW for `sample_utts`
@@ -477,6 +506,9 @@ def main():
                   help='cpu: the N > 1 control flow on host tensors with gloo (tests)')
   ap.add_argument('--cpu-utts', type=int, default=int(os.environ.get('LT_BENCH_CPU_UTTS', 128)),
                   help='utterances of the C-oracle baseline (0: skip)')
+  ap.add_argument('--cpu-twin-utts', type=int,
+                  default=int(os.environ.get('LT_BENCH_CPU_TWIN_UTTS', 64)),
+                  help='utterances of the C++ host twin baseline (cpu_baseline; 0: skip)')
   ap.add_argument('--cpu-ref-utts', type=int,
                   default=int(os.environ.get('LT_BENCH_CPU_REF_UTTS', 8)),
                   help='utterances of the PyTorch-CPU cpu_ref baseline (0: skip)')
@@ -642,8 +674,10 @@ def main():
       result['joint_weight_fn_step'] = joint_step_leg(T, U, V, n, device)
 
   if rank == 0 and not dist_on:
+    if args.cpu_twin_utts > 0:
+      result['cpu_baseline'] = cpu_twin(T, U, V, n, C, args.cpu_twin_utts)
     if args.cpu_ref_utts > 0:
-      result['cpu_baseline'] = cpu_ref(T, U, V, n, args.cpu_ref_utts)
+      result['cpu_baseline_torch'] = cpu_ref(T, U, V, n, args.cpu_ref_utts)
     if args.cpu_utts > 0:
       result['cpu_baseline_oracle'] = cpu_baseline(T, U, V, n, C, args.cpu_utts)
   if rank == 0:

@@ -82,23 +82,49 @@ inline int next_base(const Topo& g, int p) {
   return ((p - g.An) % g.Vn1) * g.V + g.An - 1;
 }
 
-// arc weights of one frame, fp32 or bf16 (weight_fns.py:69-75 layout)
-struct Frame {
-  const float* f = nullptr;
-  const uint16_t* h = nullptr;
-  float operator[](long long e) const {
-    if (f) return f[e];
-    uint32_t u = (uint32_t)h[e] << 16;
-    float v;
-    std::memcpy(&v, &u, 4);
-    return v;
+// Arc weights of frame `row` as fp32 (weight_fns.py:69-75 layout): fp32 W
+// is read in place, bf16 W widened once per frame into a per-thread buffer,
+// so the frame loops below are plain float loops the compiler vectorises.
+const float* frame_at(const void* W, bool bf16, long long row, long long FR) {
+  if (!bf16) return (const float*)W + row * FR;
+  thread_local std::vector<float> buf;
+  if ((long long)buf.size() < FR) buf.resize(FR);
+  const uint16_t* h = (const uint16_t*)W + row * FR;
+  for (long long e = 0; e < FR; ++e) {
+    const uint32_t u = (uint32_t)h[e] << 16;
+    std::memcpy(&buf[e], &u, 4);
   }
-};
-Frame frame_at(const void* W, bool bf16, long long row, long long FR) {
-  Frame fr;
-  if (bf16) fr.h = (const uint16_t*)W + row * FR;
-  else fr.f = (const float*)W + row * FR;
-  return fr;
+  return buf.data();
+}
+
+// exp(x) in fp32 without a libm call, so loops over it vectorise:
+// x = n ln2 + r (Cody-Waite, |r| <= ln2 / 2), e^r by its degree-6 Taylor
+// polynomial (relative error < 2e-7 on that range), 2^n into the exponent.
+// exp(-inf) = 0 and anything below -103.3 flushes to 0; +inf and anything
+// above 88.7 give +inf; NaN propagates.
+inline float exp_f(float x) {
+  const float t = std::min(std::max(x, -104.f), 89.f);
+  // round to nearest by the 1.5 * 2^23 shift; n in [-151, 129]
+  const float nf = (t * 1.44269504088896341f + 12582912.f) - 12582912.f;
+  const float r = std::fma(nf, -0.693145751953125f, std::fma(nf, -1.428606765330187e-06f, t));
+  float p = 1.f / 720.f;
+  p = std::fma(p, r, 1.f / 120.f);
+  p = std::fma(p, r, 1.f / 24.f);
+  p = std::fma(p, r, 1.f / 6.f);
+  p = std::fma(p, r, 0.5f);
+  p = std::fma(p, r, 1.f);
+  p = std::fma(p, r, 1.f);
+  // 2^n in two halves so n down to -150 stays representable through denormals
+  const int n = (int)nf;
+  const int n1 = n >> 1, n2 = n - n1;
+  float s1, s2;
+  const int32_t b1 = (n1 + 127) << 23, b2 = (n2 + 127) << 23;
+  std::memcpy(&s1, &b1, 4);
+  std::memcpy(&s2, &b2, 4);
+  float v = p * s1 * s2;
+  v = x < -103.3f ? 0.f : v;
+  v = x > 88.72f ? INFINITY : v;
+  return x != x ? x : v;
 }
 
 inline uint16_t to_bf16(float f) {  // round to nearest even, NaN kept
@@ -152,7 +178,7 @@ struct FwdScratch {
 };
 
 template <int SR>
-void den_step(const Topo& g, const Frame& w, const float* a, float* na, int16_t* bp,
+void den_step(const Topo& g, const float* w, const float* a, float* na, int16_t* bp,
               FwdScratch& sc) {
   const int V = g.V, R = g.R;
   float* m = sc.m.data();
@@ -172,7 +198,7 @@ void den_step(const Topo& g, const Frame& w, const float* a, float* na, int16_t*
       na[q] = bt + lex;
     } else {  // logaddexp (semirings.py:248-255)
       const float c = safe(std::max(bt, lex));
-      na[q] = c + std::log(std::exp(bt - c) + std::exp(lex - c));
+      na[q] = c + std::log(exp_f(bt - c) + exp_f(lex - c));
     }
   };
   if (g.n == 0) {  // one state, V lexical self loops (labels 1..V)
@@ -192,7 +218,7 @@ void den_step(const Topo& g, const Frame& w, const float* a, float* na, int16_t*
       for (int k = 0; k < V; ++k) mx = std::max(mx, a0 + w[1 + k]);
       const float c = safe(mx);
       float acc = 0.f;
-      for (int k = 0; k < V; ++k) acc += std::exp(a0 + w[1 + k] - c);
+      for (int k = 0; k < V; ++k) acc += exp_f(a0 + w[1 + k] - c);
       r = c + std::log(acc);
     }
     finish(0, blank(0), r, best);
@@ -238,6 +264,7 @@ void den_step(const Topo& g, const Frame& w, const float* a, float* na, int16_t*
           if (x > m[y]) { m[y] = x; bi[y] = k; }
         }
       } else {
+#pragma omp simd
         for (int y = 0; y < V; ++y) m[y] = std::max(m[y], ap + w[e0 + y]);
       }
     }
@@ -251,7 +278,8 @@ void den_step(const Topo& g, const Frame& w, const float* a, float* na, int16_t*
       const int p = pb + k * g.Vn1;
       const float ap = a[p];
       const long long e0 = (long long)p * R + 1;
-      for (int y = 0; y < V; ++y) s[y] += std::exp(ap + w[e0 + y] - m[y]);
+#pragma omp simd
+      for (int y = 0; y < V; ++y) s[y] += exp_f(ap + w[e0 + y] - m[y]);
     }
     for (int y = 0; y < V; ++y) finish(q0 + y, blank(q0 + y), m[y] + std::log(s[y]), 0);
   }
@@ -303,7 +331,7 @@ void string_arcs(const Topo& g, int U, const int32_t* lab, StringArcs* s) {
 }
 
 template <int SR>
-void num_step(const Topo& g, const Frame& w, const StringArcs& sa, const float* a, float* na,
+void num_step(const Topo& g, const float* w, const StringArcs& sa, const float* a, float* na,
               int NP) {
   const int R = g.R;
   for (int u = 0; u < NP; ++u) {
@@ -318,7 +346,7 @@ void num_step(const Topo& g, const Frame& w, const StringArcs& sa, const float* 
     else if (SR == LT_SEMIRING_MAX) na[u] = bt >= lx ? bt : lx;
     else {
       const float c = safe(std::max(bt, lx));
-      na[u] = c + std::log(std::exp(bt - c) + std::exp(lx - c));
+      na[u] = c + std::log(exp_f(bt - c) + exp_f(lx - c));
     }
   }
 }
@@ -365,7 +393,7 @@ double den_forward_utt(const Problem& P, const void* W, int b, int nf, float* hi
     if (off) off[t] = O;
     if (alpha_abs)
       for (int q = 0; q < C; ++q) alpha_abs[(long long)t * C + q] = O + a[q];
-    const Frame w = frame_at(W, P.bf16, (long long)b * P.T + t, P.FR);
+    const float* w = frame_at(W, P.bf16, (long long)b * P.T + t, P.FR);
     den_step<SR>(g, w, a.data(), na.data(), bp ? bp + (long long)t * C : nullptr, sc);
     a.swap(na);
     if (SR == LT_SEMIRING_LOG) O += renorm(a.data(), C);
@@ -397,7 +425,7 @@ double num_forward_utt(const Problem& P, const void* W, int b, int nf, const Str
     if (off) off[t] = O;
     if (alpha_abs)
       for (int u = 0; u < NP; ++u) alpha_abs[(long long)t * NP + u] = O + a[u];
-    const Frame w = frame_at(W, P.bf16, (long long)b * P.T + t, P.FR);
+    const float* w = frame_at(W, P.bf16, (long long)b * P.T + t, P.FR);
     num_step<SR>(P.g, w, sa, a.data(), na.data(), NP);
     a.swap(na);
     if (SR == LT_SEMIRING_LOG) O += renorm(a.data(), NP);
@@ -422,28 +450,36 @@ void den_backward_utt(const Problem& P, const void* W, int b, int nf, const floa
   const int C = g.C, R = g.R, V = g.V;
   std::fill(bcur.begin(), bcur.end(), 0.f);  // every state is final (lattices.py:788-790)
   float Ob = 0.f;
-  std::vector<float> x(R);
+  std::vector<float> x(R), bz(V);
   for (int t = nf - 1; t >= 0; --t) {
-    const Frame w = frame_at(W, P.bf16, (long long)b * P.T + t, P.FR);
+    const float* w = frame_at(W, P.bf16, (long long)b * P.T + t, P.FR);
     const double kt = (aoff ? (double)aoff[t] : 0.0) + Ob - log_z;
     const float* at = ah + (long long)t * C;
     for (int p = 0; p < C; ++p) {
       const long long e0 = (long long)p * R;
       const int nb = next_base(g, p);
-      x[0] = w[e0] + bcur[p];
-      float mx = x[0];
-      for (int y = 1; y <= V; ++y) {
-        x[y] = w[e0 + y] + bcur[nb < 0 ? 0 : nb + y];
-        mx = std::max(mx, x[y]);
-      }
+      // beta over next(p, 1..V): contiguous (n = 0: every label loops to 0)
+      if (nb < 0) std::fill(bz.begin(), bz.end(), bcur[0]);
+      const float* bl = nb < 0 ? bz.data() : bcur.data() + nb + 1;
+      float* xp = x.data();
+      const float* wp = w + e0;
+      xp[0] = wp[0] + bcur[p];
+#pragma omp simd
+      for (int y = 1; y <= V; ++y) xp[y] = wp[y] + bl[y - 1];
+      float mx = kNegInf;
+#pragma omp simd reduction(max : mx)
+      for (int y = 0; y <= V; ++y) mx = std::max(mx, xp[y]);
       const bool live = std::isfinite(mx);
       const float c = live ? mx : 0.f;
       float s = 0.f;
-      for (int y = 0; y <= V; ++y) { x[y] = std::exp(x[y] - c); s += x[y]; }
+#pragma omp simd reduction(+ : s)
+      for (int y = 0; y <= V; ++y) { xp[y] = exp_f(xp[y] - c); s += xp[y]; }
       bnxt[p] = c + std::log(s);
       // no finite out-term: no marginal, whatever alpha is
       const float sp = (gb == 0.f || !live) ? 0.f : (float)std::exp((double)at[p] + c + kt) * gb;
-      for (int y = 0; y <= V; ++y) dfr[e0 + y] = x[y] * sp;
+      float* dp = dfr.data() + e0;
+#pragma omp simd
+      for (int y = 0; y <= V; ++y) dp[y] = xp[y] * sp;
     }
     emit(t, dfr.data());
     bcur.swap(bnxt);
@@ -600,7 +636,7 @@ int lt_cpu_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
     for (int u = 0; u < NP; ++u) nb[u] = u == nl ? 0.f : kNegInf;
     float Obn = 0.f;
     auto num_frame = [&](int t, float* d) {
-      const Frame w = frame_at(W, P.bf16, (long long)b * P.T + t, P.FR);
+      const float* w = frame_at(W, P.bf16, (long long)b * P.T + t, P.FR);
       const double kt = (double)noff[t] + Obn - nv;
       const float* at = nh.data() + (long long)t * NP;
       for (int u = 0; u < NP; ++u) {
@@ -612,7 +648,7 @@ int lt_cpu_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
         const float mx = std::max(xb, xl);
         const bool live = std::isfinite(mx);
         const float c = live ? mx : 0.f;
-        const float ebv = std::exp(xb - c), elv = std::exp(xl - c);
+        const float ebv = exp_f(xb - c), elv = exp_f(xl - c);
         nbn[u] = c + std::log(ebv + elv);
         if (gb != 0.f && live) {
           const float sp = (float)std::exp((double)at[u] + c + kt) * gb;
