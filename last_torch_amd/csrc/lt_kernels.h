@@ -909,6 +909,132 @@ LT_DEVINL float den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, in
   return O;
 }
 
+// ---------------------------------------------------------------------------
+// Trigram den recursions (FullNGram n = 2, V <= 32, Log; lt_tri.hip).
+// The full-order destinations come in V blocks of V (contexts.py:226-229):
+// block j holds the states (j+1, y), y = 1..V, whose V+1 sources are
+// p_k = 1 + j + k V (the order-1 state j+1, then the order-2 states
+// (x, j+1)), and their lexical arcs are the label runs W[p_k, 1..V]. A den
+// lane owns the two destinations y and y+16 of one block and reduces all
+// 2 x (V+2) of their terms in registers: no lane groups, no cross-lane sums,
+// one pass per frame. alpha[p_k] is one address per block (four blocks a
+// wave: four banks), the W reads are 16 consecutive labels per block.
+// The backward lane owns two source rows p and p + 576 and walks its V
+// labels from a lane-dependent start, so that 32 consecutive sources read 32
+// different banks both in W (rows 66 B apart) and in beta (next(p, y) =
+// nb(p) + y, one block of V per source, blocks V floats apart).
+// Log vectors stay relative to an integer offset: the max of the vector a
+// step writes goes through an LDS slot (ds_max on an order-preserving int
+// image, three slots in rotation) to the next step, which subtracts its
+// floor (the same rounding scheme as den_sub_take, without a serial pass).
+// ---------------------------------------------------------------------------
+constexpr int kTriDenWaves = 9;
+LT_DEVINL int tri_enc(float f) {  // order-preserving int image of a float
+  const int i = __float_as_int(f);
+  return i ^ ((i >> 31) & 0x7fffffff);
+}
+LT_DEVINL float tri_dec(int i) { return __int_as_float(i ^ ((i >> 31) & 0x7fffffff)); }
+
+// the wave's max into the step's slot (lane 0, LDS atomic)
+LT_DEVINL void tri_publish_max(int* slot, float v) {
+  v = gmax<6>(v, 6);  // butterfly: every lane holds the wave's max
+  if ((threadIdx.x & 63) == 0) atomicMax(slot, tri_enc(v));
+}
+
+// VT: V as a compile-time constant (32: every address an immediate offset
+// from one lane base, no per-term address registers), 0 = runtime V
+template <bool BF16, bool WST, int VT>
+LT_DEVINL float den_fwd_tri(const KArgs& a, unsigned char* lds, float* abuf, int b, int nf,
+                            int tid) {
+  const NGram& g = a.g;
+  const int V = VT > 0 ? VT : g.V, R = V + 1;
+  const int C = VT > 0 ? 1 + VT + VT * VT : g.C;
+  int* slot = (int*)(lds + a.off_misc) + 2;
+  const int blk = tid >> 4, yl = tid & 15;
+  const int y0 = yl + 1, y1 = yl + 17;
+  const bool pairs = tid < 16 * V && y0 <= V;
+  const bool v1 = y1 <= V;
+  const int pb = 1 + blk;  // Apn = 1, An = V + 1 for n = 2
+  const int qa = V + 1 + blk * V + y0 - 1, qb = qa + 16;
+  const int lo = tid - 16 * V;  // low-order destination (start state, order-1 states)
+  const bool low = lo >= 0 && lo <= V;
+  if (tid == 0) {
+    slot[0] = tri_enc(0.f);  // max of alpha_0
+    slot[1] = tri_enc(-kInf);
+    slot[2] = tri_enc(-kInf);
+  }
+  const unsigned char* ring = lds + a.off_ring + a.st_off[0];
+  Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)a.FR * (BF16 ? 2 : 4),
+                          (long long)b * a.T, false);
+  float* hist = a.alpha ? a.alpha + (long long)b * a.T * C : nullptr;
+  float O = 0.f;
+  for (int i = 0; i < nf; ++i) {
+    lds_barrier();
+    const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
+    const float* acur = abuf + (i & 1) * C;
+    float* anxt = abuf + ((i + 1) & 1) * C;
+    const int s3 = i % 3;
+    const float mprev = tri_dec(slot[s3]);
+    const float sp = __builtin_isfinite(mprev) ? floorf(mprev) : 0.f;
+    if (tid == 0) slot[s3 == 0 ? 2 : s3 - 1] = tri_enc(-kInf);  // slot of step i + 2
+    float lmax = -kInf;
+    if (pairs) {
+      // the lane's two destinations one after the other (33 terms in
+      // registers at a time: no spills at four waves per SIMD)
+#pragma unroll 1
+      for (int d = 0; d < 2; ++d) {
+        const int q = d ? qb : qa, y = d ? y1 : y0;
+        if (d && !v1) break;
+        float x[33];
+        const float aq = acur[q];
+        if (hist) hist[q] = O + aq;
+        const float tq = aq + ldw<BF16>(wrow, q * R);  // blank self loop
+        float m = tq;
+#pragma unroll
+        for (int k = 0; k < 33; ++k) {
+          if (k <= V) {
+            const int p = pb + k * V;
+            x[k] = acur[p] + ldw<BF16>(wrow, p * R + y);
+          } else {
+            x[k] = -kInf;
+          }
+          m = fmaxf(m, x[k]);
+        }
+        // one logsumexp over blank + lexical terms with the safe max
+        // (semirings.py:248-255, 279-286)
+        const float c = __builtin_isfinite(m) ? m : 0.f;
+        const float l = c * kLog2e;
+        float s = lt_exp_off(tq, l);
+#pragma unroll
+        for (int k = 0; k < 33; ++k) s += lt_exp_off(x[k], l);
+        const float r = (c + lt_log(s)) - sp;
+        anxt[q] = r;
+        lmax = fmaxf(lmax, r);
+      }
+    } else if (low) {
+      const int q = lo;
+      const float aq = acur[q];
+      if (hist) hist[q] = O + aq;
+      const float tb = aq + ldw<BF16>(wrow, q * R);  // blank self loop
+      float r;
+      if (q == 0) {
+        r = tb;  // the start state has no lexical in-arc (contexts.py:216-217)
+      } else {
+        const float tl = acur[0] + ldw<BF16>(wrow, q);  // from state 0, label q
+        r = log_plus(tb, tl);
+      }
+      r -= sp;
+      anxt[q] = r;
+      lmax = r;
+    }
+    tri_publish_max(slot + (s3 == 2 ? 0 : s3 + 1), lmax);
+    O += sp;
+    advance(cw, a);
+    if (hist) hist += C;
+  }
+  return O;
+}
+
 template <int MODE, bool BF16, bool WST>
 LT_DEVINL float num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, const int* ctx,
                              const int* ylab, int b, int nf, int al, int aux_lanes) {
@@ -949,7 +1075,8 @@ LT_DEVINL float num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, co
   return O;
 }
 
-template <int MODE, bool BF16, bool WST, int LG, int P>
+// DEN > 0: the den role runs den_fwd_tri (trigram, lt_tri.hip; DEN = 32: V = 32, 1: any V)
+template <int MODE, bool BF16, bool WST, int LG, int P, int DEN = 0>
 LT_DEVINL void fwd_body(const KArgs& a, const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -997,9 +1124,12 @@ LT_DEVINL void fwd_body(const KArgs& a, const int b) {
   if (role == 2) {
     loader_loop(a, b, nf, false, lw, lane, ldsb);
   } else if (role == 0) {
-    if (do_den && !LT_ABL(a, 1))
-      doff = den_fwd_loop<MODE, BF16, WST, LG, P>(a, lds, abuf, b, nf, tid);
-    else idle_loop(nf);
+    if (do_den && !LT_ABL(a, 1)) {
+      if constexpr (DEN > 0) doff = den_fwd_tri<BF16, WST, DEN == 1 ? 0 : DEN>(a, lds, abuf, b, nf, tid);
+      else doff = den_fwd_loop<MODE, BF16, WST, LG, P>(a, lds, abuf, b, nf, tid);
+    } else {
+      idle_loop(nf);
+    }
   } else {
     if (do_num && !LT_ABL(a, 2))
       noff = num_fwd_loop<MODE, BF16, WST>(a, lds, nbuf, ctx, ylab, b, nf, al, aux_lanes);
@@ -1265,6 +1395,85 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
   }
 }
 
+// Trigram checkpointing backward den recursion (see den_fwd_tri): beta_t[p]
+// = (+)_y W[p, y] + beta_{t+1}[next(p, y)] (alignments.py:315-316,
+// contexts.py:232-256) for the sources p = tid and tid + 576 of this lane;
+// beta_t is frame t-1's checkpoint row (the CK convention of den_bwd_loop).
+template <bool BF16, bool WST, int VT>
+LT_DEVINL void den_bwd_tri(const KArgs& a, unsigned char* lds, float* bbuf, int b, int nf,
+                           int tid) {
+  const NGram& g = a.g;
+  const int V = VT > 0 ? VT : g.V, R = V + 1;
+  const int C = VT > 0 ? 1 + VT + VT * VT : g.C;
+  int* slot = (int*)(lds + a.off_misc) + 2;
+  const int nthr = kTriDenWaves * 64;
+  const bool h0 = tid < C, h1 = tid + nthr < C;
+  const int p0 = h0 ? tid : 0, p1 = h1 ? tid + nthr : 0;
+  bool z;
+  const int nb0 = next_base(g, p0, &z), nb1 = next_base(g, p1, &z);
+  const int ys = VT > 0 ? (tid & (VT - 1)) : (tid & 63) % V;  // the lane's first label - 1
+  if (tid == 0) {
+    slot[0] = tri_enc(0.f);  // max of beta_T = 0
+    slot[1] = tri_enc(-kInf);
+    slot[2] = tri_enc(-kInf);
+  }
+  const unsigned char* ring = lds + a.off_ring + a.st_off[0];
+  const long long t_last = (long long)b * a.T + (nf - 1);
+  Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)a.FR * (BF16 ? 2 : 4),
+                          t_last, true);
+  float* brow = a.beta ? a.beta + (t_last - 1) * C : nullptr;
+  float Ob = 0.f;
+  for (int i = 0; i < nf; ++i) {
+    lds_barrier();
+    const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
+    const float* bcur = bbuf + (i & 1) * C;
+    float* bnxt = bbuf + ((i + 1) & 1) * C;
+    const int s3 = i % 3;
+    const float mprev = tri_dec(slot[s3]);
+    const float sp = __builtin_isfinite(mprev) ? floorf(mprev) : 0.f;
+    if (tid == 0) slot[s3 == 0 ? 2 : s3 - 1] = tri_enc(-kInf);
+    float* crow = (brow && i < nf - 1) ? brow : nullptr;
+    float lmax = -kInf;
+#pragma unroll 1
+    for (int d = 0; d < 2; ++d) {
+      if (!(d ? h1 : h0)) break;
+      const int p = d ? p1 : p0, nb = d ? nb1 : nb0;
+      float x[32];
+      const float tp = ldw<BF16>(wrow, p * R) + bcur[p];  // blank self loop
+      float m = tp;
+      int y = ys + 1;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        if (k < V) {
+          if constexpr (VT == 32) {
+            const int yk = ((ys + k) & 31) + 1;
+            x[k] = ldw<BF16>(wrow, p * R + yk) + bcur[nb + yk];
+          } else {
+            x[k] = ldw<BF16>(wrow, p * R + y) + bcur[nb + y];
+            y = y == V ? 1 : y + 1;
+          }
+        } else {
+          x[k] = -kInf;
+        }
+        m = fmaxf(m, x[k]);
+      }
+      const float c = __builtin_isfinite(m) ? m : 0.f;
+      const float l = c * kLog2e;
+      float s = lt_exp_off(tp, l);
+#pragma unroll
+      for (int k = 0; k < 32; ++k) s += lt_exp_off(x[k], l);
+      const float r = (c + lt_log(s)) - sp;
+      bnxt[p] = r;
+      if (crow) crow[p] = (Ob + sp) + r;
+      lmax = fmaxf(lmax, r);
+    }
+    tri_publish_max(slot + (s3 == 2 ? 0 : s3 + 1), lmax);
+    Ob += sp;
+    advance(cw, a);
+    if (brow) brow -= C;
+  }
+}
+
 // Numerator beta + marginals for one frame (the reverse of
 // alignments.py:320-329): beta^n_t[u] from beta^n_{t+1}; marginals
 // exp(alpha^n_t[u] + w + beta^n_{t+1} - num) * g accumulated (LDS atomics:
@@ -1437,7 +1646,8 @@ LT_DEVINL void num_beta_loop(const KArgs& a, unsigned char* lds, float* nbb, con
 // are computed and written per frame (a.beta / a.beta_num); the arc
 // marginals come later from marg_kernel, so this kernel can run
 // concurrently with the forward (both depend only on W).
-template <bool BF16, bool WST, bool DST, int LG, int P, bool CK = false, int KOFF = 0>
+// DEN > 0: the den role runs den_bwd_tri (trigram checkpointing backward, as fwd_body)
+template <bool BF16, bool WST, bool DST, int LG, int P, bool CK = false, int KOFF = 0, int DEN = 0>
 LT_DEVINL void bwd_body(const KArgs& a, const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1518,10 +1728,15 @@ LT_DEVINL void bwd_body(const KArgs& a, const int b) {
   if (role == 2) {
     loader_loop(a, b, nf, true, lw, lane, ldsb, DST && do_num ? 1 : 0);
   } else if (role == 0) {
-    if (!LT_ABL(a, 1) && (!CK || do_den))
-      den_bwd_loop<BF16, WST, DST, LG, P, CK>(fresh_args<KOFF>(), lds, bbuf, nbuf3, b, nf, tid, gb,
-                                              log_z, do_den, do_num);
-    else idle_loop(nf);
+    if (!LT_ABL(a, 1) && (!CK || do_den)) {
+      if constexpr (DEN > 0)
+        den_bwd_tri<BF16, WST, DEN == 1 ? 0 : DEN>(fresh_args<KOFF>(), lds, bbuf, b, nf, tid);
+      else
+        den_bwd_loop<BF16, WST, DST, LG, P, CK>(fresh_args<KOFF>(), lds, bbuf, nbuf3, b, nf, tid,
+                                                gb, log_z, do_den, do_num);
+    } else {
+      idle_loop(nf);
+    }
   } else {
     if (do_num && !LT_ABL(a, 2)) {
       if constexpr (CK)
@@ -1587,6 +1802,8 @@ struct Plan {
 LT_VARIANTS(LT_DECL)
 #undef LT_DECL
 int set_error(int code, const char* msg);
+// lt_tri.hip: the trigram checkpointing pair (den_fwd_tri / den_bwd_tri roles)
+int launch_tri_fwdbwd(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStream_t st);
 // lt_lattice.hip: frame-serial loss (+ dW) for the utterances with only[b] != 0
 size_t serial_side_bytes(const lt_problem* pb, int local_norm);
 int serial_loss(const lt_problem* pb, int local_norm, const void* W, const int32_t* num_frames,

@@ -961,6 +961,17 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
               pbk.wst, pbk.threads, pbk.lds_bytes);
   }
 #endif
+  // trigram with W staged in LDS: the den roles of lt_tri.hip (one lane per
+  // state pair, every term in registers) in the same side-by-side launch
+  if (ck && !local_norm && g.n == 2 && g.V >= 2 && g.V <= 32 && pf.wst && pbk.wst &&
+      pf.a.aux_waves == pbk.a.aux_waves && pf.a.load_waves == pbk.a.load_waves &&
+      env_int("LT_NO_TRI", 0) == 0) {
+    for (Plan* pl : {&pf, &pbk}) {
+      pl->a.den_waves = kTriDenWaves;
+      pl->threads = 64 * (kTriDenWaves + pl->a.aux_waves + pl->a.load_waves);
+    }
+    return lt_impl::launch_tri_fwdbwd(pf, pbk, bf16, pb->batch, st);
+  }
   // same geometry (the usual case): beta and alpha side by side in one
   // launch; else beta, then alpha
   if (ck && pf.lg == pbk.lg && pf.tmax == pbk.tmax && pf.wst == pbk.wst &&
