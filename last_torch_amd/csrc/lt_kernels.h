@@ -929,6 +929,10 @@ LT_DEVINL float den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, in
 // floor (the same rounding scheme as den_sub_take, without a serial pass).
 // ---------------------------------------------------------------------------
 constexpr int kTriDenWaves = 9;
+#ifndef LT_TRI_LOAD
+#define LT_TRI_LOAD 4
+#endif
+constexpr int kTriLoadWaves = LT_TRI_LOAD;  // loader waves of the trigram launch
 LT_DEVINL int tri_enc(float f) {  // order-preserving int image of a float
   const int i = __float_as_int(f);
   return i ^ ((i >> 31) & 0x7fffffff);

@@ -964,11 +964,21 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   // trigram with W staged in LDS: the den roles of lt_tri.hip (one lane per
   // state pair, every term in registers) in the same side-by-side launch
   if (ck && !local_norm && g.n == 2 && g.V >= 2 && g.V <= 32 && pf.wst && pbk.wst &&
-      pf.a.aux_waves == pbk.a.aux_waves && pf.a.load_waves == pbk.a.load_waves &&
+      pf.a.aux_waves == pbk.a.aux_waves && pf.a.slot_bytes == pbk.a.slot_bytes &&
       env_int("LT_NO_TRI", 0) == 0) {
     for (Plan* pl : {&pf, &pbk}) {
-      pl->a.den_waves = kTriDenWaves;
-      pl->threads = 64 * (kTriDenWaves + pl->a.aux_waves + pl->a.load_waves);
+      // four loader waves: a frame is 69 LDS-DMA wave instructions (bf16),
+      // whose issue cost alone is a microsecond on two waves
+      KArgs& ka = pl->a;
+      ka.den_waves = kTriDenWaves;
+      const int instr = ka.st_ninstr[0] + ka.st_ninstr[1] + ka.st_ninstr[2];
+      ka.load_waves = std::min(kTriLoadWaves, std::max(1, instr));
+      // loader_loop: wave 0 issues gw0 instructions a frame, the others gw1
+      // (instr % load_waves <= 1 keeps that exact)
+      while (ka.load_waves > 2 && instr % ka.load_waves > 1) --ka.load_waves;
+      ka.gw0 = (instr + ka.load_waves - 1) / ka.load_waves;
+      ka.gw1 = instr / ka.load_waves;
+      pl->threads = 64 * (kTriDenWaves + ka.aux_waves + ka.load_waves);
     }
     return lt_impl::launch_tri_fwdbwd(pf, pbk, bf16, pb->batch, st);
   }

@@ -207,157 +207,6 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
   }
 }
 
-// The same forward (V = 32) on NW waves per utterance: the single-wave
-// kernel above is issue-bound (one wave issues every instruction of the
-// frame step: ~88 VALU, 54 SALU, 24 LDS a frame, PMC 70 % active), so the
-// work of a step is split over NW waves on NW SIMDs of one CU:
-//   lane i of the workgroup: destination q = i / LPD + 1 (LPD = 2 NW lanes
-//   per core state), terms [r TPL, (r+1) TPL) of its 34 (term 0 the blank
-//   self loop, term k+1 source p = k: the generic kernel's order); the lane
-//   max by a max3 tree, the destination's by DPP row exchanges; the
-//   backpointer (first term equal to the maximum: lowest lane, then lowest
-//   term) is formed one step later, off the alpha chain.
-// alpha of the 33 states sits in LDS (double-buffered); each wave streams its
-// share of the frame's LDS-DMA instructions kAhead frames ahead and waits
-// for its own share; one s_barrier per frame publishes both alpha and the
-// frame. The start state's alpha (blank self loop only) is kept by every lane.
-#ifndef LT_VIT_NW
-#define LT_VIT_NW 2
-#endif
-constexpr int kVitWaves = LT_VIT_NW;  // waves per utterance at V = 32 (1: vit_bigram_kernel)
-
-template <int NW>
-struct VitNw {
-  static constexpr int LPD = 2 * NW;             // lanes per destination
-  static constexpr int TPL = (34 + LPD - 1) / LPD;  // terms per lane
-  static constexpr int LG = NW == 2 ? 2 : 3;     // log2 LPD
-};
-
-// max / first-index reductions over the LPD lanes of a destination (DPP
-// inside a row: quad_perm exchanges, then the row half mirror for 8 lanes)
-template <int LG>
-LT_DEVINL float grp_max_dpp(float v) {
-  v = fmaxf(v, dppf<0xB1>(v));  // quad_perm [1,0,3,2]
-  v = fmaxf(v, dppf<0x4E>(v));  // quad_perm [2,3,0,1]
-  if constexpr (LG > 2) v = fmaxf(v, dppf<0x141>(v));  // row_half_mirror
-  return v;
-}
-template <int LG>
-LT_DEVINL int grp_min_dpp(int v) {
-  v = min(v, dppi<0xB1>(v));
-  v = min(v, dppi<0x4E>(v));
-  if constexpr (LG > 2) v = min(v, dppi<0x141>(v));
-  return v;
-}
-
-template <bool BF16, int NW>
-__global__ __launch_bounds__(64 * NW) void vit_bigram_nw_kernel(const VitArgs a) {
-  using P = VitNw<NW>;
-  constexpr int LPD = P::LPD, TPL = P::TPL;
-  constexpr int C = 33, R = 33;
-  constexpr int es = BF16 ? 2 : 4;
-  constexpr long long fbytes = (long long)C * R * es;
-  constexpr int ni = (int)(((fbytes + 30) / 16 + 63) / 64);  // DMA instructions a frame
-  __shared__ __attribute__((aligned(16))) float s_al[2][36];
-  __shared__ __attribute__((aligned(16))) unsigned char s_ring[kSlots][ni * 1024];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-  const int w = tid >> 6;
-  const int j = tid / LPD, r = tid % LPD;
-  const int q = j + 1;
-  const int o0 = r * TPL;  // the lane's first term
-  int nf = a.nfr[b];
-  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
-  // this wave's DMA instructions of a frame: i = w, w + NW, ...
-  constexpr int cnt_max = (ni + NW - 1) / NW;
-  const int cnt = (ni - w + NW - 1) / NW;
-  const __amdgpu_buffer_rsrc_t bpr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.bp + (long long)b * a.T * C), (short)0,
-                                        a.T * C, 0x00020000);
-  if (tid < 36) s_al[0][tid] = tid == 0 ? 0.f : -kInf;
-  float a0 = 0.f;
-  const long long goff0 = (long long)b * a.T * fbytes;
-  auto fclamp = [&](int t) { return min(t, max(nf - 1, 0)); };
-  auto issue = [&](int t) {
-    const long long off = goff0 + (long long)fclamp(t) * fbytes;
-    const long long g0 = off & ~15LL;
-    const int n16 = (int)((off + fbytes - g0 + 15) >> 4);
-    const unsigned dst = lds_base_addr(&s_ring[t % kSlots][0]);
-#pragma unroll
-    for (int k = 0; k < cnt_max; ++k) {
-      const int i = w + NW * k;
-      if (i < ni) {
-        int g = lane + 64 * i;
-        g = g < n16 ? g : n16 - 1;
-        glds16(a.W + g0 + 16LL * g, dst + 1024u * i);
-      }
-    }
-  };
-  if (nf > 0)
-    for (int d = 0; d < kAhead; ++d) issue(d);
-  // the previous frame's terms and destination value (backpointer one step late)
-  float xq[TPL], rq = 0.f;
-#pragma unroll
-  for (int m = 0; m < TPL; ++m) xq[m] = -kInf;
-  auto emit_bp = [&](int tb) {
-    int ri = 99;
-#pragma unroll
-    for (int m = TPL - 1; m >= 0; --m) ri = xq[m] == rq ? o0 + m : ri;
-    ri = grp_min_dpp<P::LG>(ri);
-    // one store instruction a wave (the vmcnt count above relies on it): the
-    // destinations' first lanes, and lane 1 for the start state (always 0)
-    if (r == 0 || tid == 1)
-      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(tid == 1 ? 0 : ri), bpr,
-                                           tid == 1 ? 0 : q, tb * C, 0);
-  };
-  for (int t = 0; t < nf; ++t) {
-    // frame t landed (this wave's share; the barrier joins the others'), alpha_t written
-    wait_vmcnt((kAhead - 1) * cnt + min(max(t - 1, 0), kAhead - 1));
-    lds_barrier();
-    const float* acur = s_al[t & 1];
-    float* anxt = s_al[(t + 1) & 1];
-    const unsigned char* fr = &s_ring[t % kSlots][0] + ((goff0 + (long long)fclamp(t) * fbytes) & 15);
-    float x[TPL];
-#pragma unroll
-    for (int m = 0; m < TPL; ++m) {
-      const int o = o0 + m;
-      if (o == 0) x[m] = acur[q] + vlds<BF16>(fr, q * R * es);       // blank self loop
-      else if (o <= C) x[m] = acur[o - 1] + vlds<BF16>(fr, ((o - 1) * R + q) * es);
-      else x[m] = -kInf;
-    }
-    const float w00 = vlds<BF16>(fr, 0);
-    if (t > 0) emit_bp(t - 1);
-    float mx = x[0];
-#pragma unroll
-    for (int m = 1; m + 1 < TPL; m += 2) mx = max3_raw(mx, x[m], x[m + 1]);
-    if constexpr ((TPL & 1) == 0) mx = fmaxf(mx, x[TPL - 1]);
-    const float rv = grp_max_dpp<P::LG>(mx);
-    if (r == 0) anxt[q] = rv;
-    a0 += w00;
-    if (tid == 0) anxt[0] = a0;
-    issue(t + kAhead);
-#pragma unroll
-    for (int m = 0; m < TPL; ++m) xq[m] = x[m];
-    rq = rv;
-  }
-  if (nf > 0) emit_bp(nf - 1);
-  lds_barrier();
-  if (w == 0) {
-    const float* af = s_al[nf & 1];
-    float v = lane < C ? af[lane] : -kInf;
-    int vi = lane < C ? lane : 0x7fffffff;
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-      const float pv = __shfl_xor(v, s);
-      const int pi = __shfl_xor(vi, s);
-      if (pv > v || (pv == v && pi < vi)) { v = pv; vi = pi; }
-    }
-    if (lane == 0) {
-      a.dist[b] = v;
-      a.qstar[b] = vi;
-    }
-  }
-}
-
 // Backtrace of the bigram backpointers in segments (one workgroup per
 // utterance, the utterance's backpointers staged in LDS): every segment of S
 // frames walks back from each of its C possible end states at once (the
@@ -491,16 +340,12 @@ int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, 
 #endif
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const bool full = a.V == 32;
-  // V = 32: the step split over kVitWaves waves (vit_bigram_nw_kernel)
-  const void* k = full ? (kVitWaves == 1 ? (bf16 ? (const void*)vit_bigram_kernel<true, true>
-                                                 : (const void*)vit_bigram_kernel<false, true>)
-                                         : (bf16 ? (const void*)vit_bigram_nw_kernel<true, kVitWaves>
-                                                 : (const void*)vit_bigram_nw_kernel<false, kVitWaves>))
+  const void* k = full ? (bf16 ? (const void*)vit_bigram_kernel<true, true>
+                               : (const void*)vit_bigram_kernel<false, true>)
                        : (bf16 ? (const void*)vit_bigram_kernel<true, false>
                                : (const void*)vit_bigram_kernel<false, false>);
-  const int threads = full ? 64 * kVitWaves : 64;
   void* args[] = {(void*)&a};
-  hipError_t e = hipLaunchKernel(k, dim3(a.B), dim3(threads), args, 0, (hipStream_t)stream);
+  hipError_t e = hipLaunchKernel(k, dim3(a.B), dim3(64), args, 0, (hipStream_t)stream);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;

@@ -18,6 +18,7 @@ for r in 1 2; do
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/kt5 -o run -- python tools/cfg5_time.py > $out/kt5.log 2>&1 || exit $?
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/kt4 -o run -- python tools/vit_time.py > $out/kt4.log 2>&1 || exit $?
+bash tools/r3_b256_prof.sh ${1:-r3m}_b256 || exit $?
 i=0
 for pmc in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
            "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"; do
