@@ -289,14 +289,14 @@ def chunk_path(batch, frames, labels, vocab_size, context_size, device=None):
 
 
 def fused_path(batch, frames, labels, vocab_size, context_size, device=None, bf16=False):
-  """Whether lt_loss_grad runs as ONE fused pipe launch for this shape
-  (mirrors lt_loss_grad_design: not the chunked path, checkpointing batch
-  size, 2B below the CU count, pipe shape)."""
+  """Whether lt_loss_grad runs as ONE fused pipe launch for this shape: the
+  bigram past the chunked scan's range while the launch's recursion grid is
+  co-resident (an occupancy query: lt_loss_grad_design answers it)."""
   if chunk_path(batch, frames, labels, vocab_size, context_size, device):
     return False
-  cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
-  return (2 * batch < cus and prefer_checkpoints(batch, device) and
-          pipe_path(batch, frames, labels, vocab_size, context_size, bf16))
+  if not pipe_path(batch, frames, labels, vocab_size, context_size, bf16):
+    return False
+  return loss_grad_design(batch, frames, labels, vocab_size, context_size, bf16) == DESIGN_FUSED_PIPE
 
 
 DESIGN_AUTO, DESIGN_CHUNK, DESIGN_FUSED_PIPE, DESIGN_CHECKPOINTS, DESIGN_RECURSION = -1, 0, 1, 2, 3
@@ -389,19 +389,16 @@ def chunk_backward(W, num_frames, labels, num_labels, vocab_size, context_size, 
 
 
 def grad_workspace_errors(workspace, W, vocab_size, context_size, max_labels, local_norm):
-  """The hand-off error word of a fused lt_loss_grad workspace (0 = no
-  timed-out wait); test / diagnostic use, synchronises."""
-  pb = _problem(W, vocab_size, context_size, max_labels)
+  """The hand-off error word of a fused-pipe lt_loss_grad workspace (0 = no
+  timed-out wait): after the granule rows (alpha, beta [B,T,C]; alpha^n,
+  beta^n [B,T,U+1]; 8 bytes each) and the band flags [2][B] of
+  pipe_mid_workspace_bytes; test / diagnostic use, synchronises."""
+  del local_norm
   C = num_context_states(vocab_size, context_size)
   B, T = W.shape[:2]
   NP = max_labels + 1
-  up = lambda x: (x + 255) & ~255
-  off = 0
-  if not local_norm:
-    off += 2 * up(4 * B * T * C)
-  off += 2 * up(4 * B * T * NP) + up(4 * B * 4 * NP)
-  del pb
-  return int(workspace[off + 8:off + 12].view(torch.int32).item())
+  off = 8 * (2 * B * T * C + 2 * B * T * NP + 2 * B)
+  return int(workspace[off:off + 4].view(torch.int32).item())
 
 
 def chunk_fallback_count(workspace, batch):

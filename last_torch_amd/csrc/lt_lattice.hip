@@ -288,15 +288,39 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
       const int el0 = e_lo + e0 - f * Ew;
       int p = (int)fdiv((unsigned)el0, (unsigned)R, a.mR);
       int y = el0 - p * R;
+      if (R >= VE) {
+        // a unit spans at most two source rows (p0 and the next, possibly
+        // in the next frame of the tile): their alpha and next-state bases
+        // are read once, every element is branch-free
+        const int p1r = p + 1;
+        const bool fw = p1r == C;
+        const int p1 = fw ? 0 : p1r, f1 = fw ? f + 1 : f;
+        const float a0v = A[f * C + p], a1v = f1 < Fl ? A[f1 * C + p1] : 0.f;
+        const int nb0 = zero_next ? 0 : (nb_table ? nbt[p] : 0);
+        const int nb1 = zero_next ? 0 : (nb_table ? nbt[p1] : 0);
+        const float lzc = lz;
 #pragma unroll
-      for (int c = 0; c < VE; ++c) {
-        if (f < Fl) {
-          const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
-          v[r][c] = gb * lt_exp(A[f * C + p] + w[c] + Bt[f * C + q] - lz);
+        for (int c = 0; c < VE; ++c) {
+          const int yc = y + c;
+          const bool w2 = yc >= R;
+          const int yy = w2 ? yc - R : yc;
+          const int pp = w2 ? p1 : p, ff = w2 ? f1 : f;
+          const int q = yy == 0 ? pp : (w2 ? nb1 : nb0) + yy;
+          const float av = w2 ? a1v : a0v;
+          const float x = gb * lt_exp(av + w[c] + Bt[ff * C + q] - lzc);
+          v[r][c] = ff < Fl ? x : 0.f;
         }
-        if (++y == R) {
-          y = 0;
-          if (++p == C) { p = 0; ++f; }
+      } else {
+#pragma unroll
+        for (int c = 0; c < VE; ++c) {
+          if (f < Fl) {
+            const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
+            v[r][c] = gb * lt_exp(A[f * C + p] + w[c] + Bt[f * C + q] - lz);
+          }
+          if (++y == R) {
+            y = 0;
+            if (++p == C) { p = 0; ++f; }
+          }
         }
       }
     }
@@ -1170,6 +1194,10 @@ int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
 // or the recursion pair (the environment overrides apply, as in the call).
 static int loss_grad_design(const lt_problem* pb) {
   if (lt_impl::chunk_preferred(pb) && pb->max_frames > 0) return LT_DESIGN_CHUNK;
+  // bigram past the chunked scan's range: the pipelined recursions with the
+  // marginals in their own workgroups (mid mode), while the grid fits
+  if (lt_impl::pipe_eligible(pb) && env_int("LT_MID", 1) && lt_impl::pipe_mid_fits(pb))
+    return LT_DESIGN_FUSED_PIPE;
   const int cus = cu_count();
   const bool ck_def = 2 * pb->batch <= cus || (lt_impl::pipe_eligible(pb) && 2 * pb->batch <= 3 * cus);
   const bool ck = env_int("LT_CHECKPOINTS", ck_def ? 1 : 0) != 0;
@@ -1217,6 +1245,10 @@ int lt_loss_grad_workspace_bytes_ex(const lt_problem* pb, int32_t local_norm, in
     if (bytes) *bytes = ((st + 255) & ~(size_t)255) + sc;
     return LT_OK;
   }
+  if (d == LT_DESIGN_FUSED_PIPE) {
+    if (bytes) *bytes = lt_impl::pipe_mid_workspace_bytes(pb);
+    return LT_OK;
+  }
   if (bytes) *bytes = grad_ws(pb, local_norm).total;
   return LT_OK;
 }
@@ -1251,6 +1283,24 @@ int lt_loss_grad_ex(const lt_problem* pb, int32_t local_norm, int32_t design_in,
     char* scratch = state + st_al;
     return lt_impl::chunk_loss_grad(pb, local_norm, W, num_frames, labels, num_labels, loss,
                                     log_z, num, dW, state, st, scratch, sc, stream);
+  }
+  if (design == LT_DESIGN_FUSED_PIPE && pb->max_frames > 0) {
+    // bigram, large batches: one launch of the pipelined alpha || beta
+    // recursions whose marginal waves turn the far half of each utterance's
+    // frames into dW while the frames are in the ring (lt_pipe.hip, mid mode)
+    const size_t need = lt_impl::pipe_mid_workspace_bytes(pb);
+    if (!workspace || workspace_bytes < need) return fail(LT_EINVAL, "workspace too small");
+    if ((rc = lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
+                                   num, nullptr, nullptr, nullptr, nullptr, nullptr, 2, nullptr,
+                                   stream, dW, nullptr, 1, workspace)))
+      return rc;
+    const long long BT = (long long)pb->batch * pb->max_frames;
+    const int* err = (const int*)((char*)workspace +
+                                  8 * (2 * BT * g.C + 2 * BT * (pb->max_labels + 1) +
+                                       2LL * pb->batch));
+    hipLaunchKernelGGL(handoff_check_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, err,
+                       loss, pb->batch);
+    return hip_check(hipGetLastError(), "hand-off check launch");
   }
   const GradWs w = grad_ws(pb, local_norm);
   if (!workspace || workspace_bytes < w.total) return fail(LT_EINVAL, "workspace too small");

@@ -43,6 +43,8 @@
 // drains instead of hanging.
 #include "lt_kernels.h"
 
+#include <atomic>
+
 namespace {
 
 constexpr int kPipeMaxSlots = 32;
@@ -90,7 +92,24 @@ struct PArgs {
   int mC4, mNP4, mFR4;     // padded row lengths (floats) in a wave's region
   long long* trace;  // LT_FUSED_TRACE (diagnostics): [dirs*B][2] recursion start/end,
                      // then [ntiles][4] tile grab/ready/done/role (s_memrealtime)
+  // ---- in-workgroup marginals (lt_loss_grad at large batches, mid mode):
+  // each recursion workgroup turns its second half of the frames into dW
+  // from the W still in its ring (alpha: frames [nf/2, nf), beta: [0, nf/2))
+  int mid;           // 0: off; 1: NM marginal waves per workgroup
+  int NM;            // marginal waves (waves 2 + NH ...)
+  int off_hring, off_nring, off_mw, mw_bytes;  // LDS: own den / num rows per slot, wave regions
+  // the rows the other direction needs (steps i < s0 of each workgroup), as
+  // 8-byte {value, tag} granules written by one sc1 store each: a consumer
+  // polls its granules until the tags match (MI355X_MICROARCH.md, granule
+  // hand-off R2: no progress counter, no publication lag)
+  unsigned long long* gden[2];  // [B,T,C]  alpha rows (fwd), beta rows (bwd)
+  unsigned long long* gnum[2];  // [B,T,NP] alpha^n rows, beta^n rows
+  unsigned epoch;               // per call: tag = epoch * T + t
+  unsigned long long* mflag;    // [2][B] band zeroed: (epoch, ~epoch), alpha side then beta side
 };
+constexpr int kMidBand = 32;    // frames next to the middle zeroed before the granules flow
+// floats per slot of the den (hring) and numerator (nring) row rings
+constexpr int kHS = 64;
 
 #ifdef LT_STAMPS
 #define PSTAMP(a, w, i, k)                                                         \
@@ -106,7 +125,9 @@ struct PArgs {
 #endif
 
 // control block (ints) at off_ctl
-enum { CTL_TAG = 0, CTL_DEN = kPipeMaxSlots, CTL_NUM, CTL_ABORT, CTL_FIN0, CTL_FIN1, CTL_N };
+constexpr int kPipeMidWaves = 2;  // marginal waves per workgroup in mid mode
+enum { CTL_TAG = 0, CTL_DEN = kPipeMaxSlots, CTL_NUM, CTL_ABORT, CTL_FIN0, CTL_FIN1, CTL_MRG,
+       CTL_N = CTL_MRG + kPipeMidWaves };
 
 typedef __attribute__((address_space(3))) volatile int lds_vint;
 typedef __attribute__((address_space(3))) float lds_float;
@@ -159,6 +180,17 @@ LT_DEVINL void st_sc1(int* p, int v) {
 }
 LT_DEVINL int ld_sc1(const int* p) {
   return __hip_atomic_load((g_int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+LT_DEVINL void st_gran(unsigned long long* p, float v, unsigned tag) {
+  const unsigned long long g = (unsigned long long)__float_as_uint(v) | ((unsigned long long)tag << 32);
+  __hip_atomic_store((g_u64*)p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// true when the granule carries `tag`; its value in *v
+LT_DEVINL bool ld_gran(const unsigned long long* p, unsigned tag, float* v) {
+  const unsigned long long g = __hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *v = __uint_as_float((unsigned)g);
+  return (unsigned)(g >> 32) == tag;
 }
 #ifdef LT_STAMPS
 #define LT_PUB_WAIT(n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
@@ -329,6 +361,8 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
   float* hrow = (REV ? a.beta : a.alpha);
   const long long hstep = REV ? -(long long)C : (long long)C;
   int* pub = a.fused ? a.prog + (REV ? 2 : 0) * a.B + b : nullptr;
+  lds_float* hring = (lds_float*)(as3(lds) + a.off_hring);  // mid mode
+  const int mid_s0 = REV ? nf - nf / 2 : nf / 2;
   if (hrow) hrow += ((long long)b * a.T + (REV ? nf - 1 : 0)) * C + hist_idx;
 
   // the current step's operands (software-pipelined: step i+1's are loaded
@@ -403,6 +437,15 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     // history value of row t: the pre-update vector (lattices.py:462)
     const float hlo = pub0 ? ((REV && !mode) ? lt_log(g0) : u0) : (mode ? uo : lt_log(g));
     const float hval = base_hi + (base_lo + hlo);
+    if (a.mid) {
+      hring[slot * kHS + hist_idx] = hval;  // the slot's marginal waves read it
+      // the other direction turns this frame into marginals: its granule
+      if (i < mid_s0) {
+        const int t = REV ? nf - 1 - i : i;
+        st_gran(a.gden[REV] + ((long long)b * a.T + t) * C + hist_idx, hval,
+                a.epoch * (unsigned)a.T + (unsigned)t);
+      }
+    }
     float shift, gn, g0n;
     if (!bad) {
       // fast path: publish g' = S 2^-e (exact scaling), base += c + e ln2
@@ -582,6 +625,7 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
   float off = 0.f;
   float* hist = REV ? a.beta_num : a.alpha_num;
   int* pub = a.fused ? a.prog + (REV ? 3 : 1) * a.B + b : nullptr;
+  lds_float* nring = (lds_float*)(as3(lds) + a.off_nring);  // mid mode
   int tag_next = nf > 0 ? ctl[CTL_TAG] : 0;
   const long long row0 = (long long)b * a.T;
   int slot = 0;
@@ -598,6 +642,17 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     for (int s = 0; s < PN; ++s) {
       wb[s] = Wr[ob[s]];
       wl[s] = Wr[ol[s]];
+    }
+    if (a.mid) {
+      const bool gr = i < (REV ? nf - nf / 2 : nf / 2);
+      unsigned long long* gp = a.gnum[REV] + (row0 + t) * NP;
+      const unsigned tag = a.epoch * (unsigned)a.T + (unsigned)t;
+#pragma unroll
+      for (int s = 0; s < PN; ++s)
+        if (PN * lane + s < NP) {
+          nring[slot * NP + PN * lane + s] = off + v[s];
+          if (gr) st_gran(gp + PN * lane + s, off + v[s], tag);
+        }
     }
     if (hist && !LT_ABL(a, 8)) {
       float* hr = hist + (row0 + t) * NP;
@@ -737,6 +792,8 @@ LT_DEVINL void helper_pipe(const PArgs& a, unsigned char* lds, int b, int nf, in
     asm volatile("" ::: "memory");
   };
   int seen_den = 0, seen_num = 0;
+  // mid mode: the first step whose frame this workgroup turns into marginals
+  const int s0 = REV ? nf - nf / 2 : nf / 2;
   int slot = hw;  // slot of step i (advanced by NH per processed step; NH <= K)
   auto process = [&](const float* w, int i) -> bool {
     // the slot's previous frame (step i-K) must be consumed
@@ -751,6 +808,10 @@ LT_DEVINL void helper_pipe(const PArgs& a, unsigned char* lds, int b, int nf, in
         if (!wait_ge(ctl + CTL_NUM, need, ctl + CTL_ABORT, a.err)) return false;
         seen_num = ctl[CTL_NUM];
       }
+      // mid mode: the marginal wave of the slot's previous step (need - 1)
+      if (a.mid && need - 1 >= s0 &&
+          !wait_ge(ctl + CTL_MRG + (need - 1 - s0) % a.NM, need, ctl + CTL_ABORT, a.err))
+        return false;
     }
     PSTAMP(a, 2 + hw, i, 1);
     float mx = -kInf;
@@ -1060,6 +1121,209 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
   }
 }
 
+// ---- in-workgroup marginals (mid mode) --------------------------------------
+// Marginal wave m of a recursion workgroup turns the frames of its steps
+// i = s0 + m, s0 + m + NM, ... (the workgroup's far half: alpha frames
+// [nf/2, nf), beta frames [0, nf/2)) into dW while the frame is still in the
+// ring: the workgroup's own den / numerator rows of the step from LDS (hring,
+// nring: the pre-update vectors the den and numerator waves leave there with
+// the step), the other direction's rows of the frame from its granules (that
+// direction passed the frame in its own first half). Every frame is
+// normalised by its own total, as marg_role does (alignments.py:311-317; the
+// string arcs of lattices.py:314-338 summed per lattice arc in LDS, one
+// wave's adds in program and lane order: deterministic).
+template <bool BF16, int NL, int PN, bool EXACT, bool REV>
+LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m, int lane) {
+  lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
+  const lds_int* ctx = (const lds_int*)(as3(lds) + a.off_ctx);
+  const lds_int* ylab = (const lds_int*)(as3(lds) + a.off_ylab);
+  const lds_float* hring = (const lds_float*)(as3(lds) + a.off_hring);
+  const lds_float* nring = (const lds_float*)(as3(lds) + a.off_nring);
+  const int C = a.C, R = a.R, FR = a.FR, NP = a.U + 1, NK = 2 * NP, U = a.U, T = a.T;
+  const bool do_den = a.flags & F_DEN;
+  constexpr int es = BF16 ? 2 : 4;
+  constexpr int NKL = 2 * PN;
+  lds_float* A = (lds_float*)(as3(lds) + a.off_mw + m * a.mw_bytes);  // [64]
+  lds_float* Bt = A + 64;         // [64]
+  lds_float* AN = Bt + 64;        // [64 PN]
+  lds_float* BN = AN + 64 * PN;   // [64 PN]
+  lds_float* Sub = BN + 64 * PN;  // [64 NL]
+  // elements e = lane + 64k: source p, destination q (n = 1: the blank stays
+  // in p, label y goes to state y; contexts.py:190-205); past the frame A[63]
+  int pq[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int e = lane + 64 * k;
+    const int p = e / R, y = e - (e / R) * R;
+    pq[k] = e < FR ? (p | ((y == 0 ? p : y) << 16)) : (63 | (63 << 16));
+  }
+  auto partial = [&](int k) { return EXACT ? k == NL - 1 : 64 * (k + 1) > FR; };
+  // numerator arc slots kk = lane + 64 s: the arc's element (-1: none) and
+  // its positions u and u or u+1 (lattices.py:314-338)
+  int on[NKL], uab[NKL];
+#pragma unroll
+  for (int s2 = 0; s2 < NKL; ++s2) {
+    const int kk = lane + 64 * s2;
+    const int u = min(kk >> 1, NP - 1);
+    uab[s2] = u | (min((kk & 1) ? u + 1 : u, NP - 1) << 16);
+    int o = -1;
+    if (kk < NK) {
+      const int uu = kk >> 1;
+      o = (kk & 1) == 0 ? ctx[uu] : (uu < U ? ctx[uu] + ylab[uu] : -1);
+    }
+    on[s2] = o;
+  }
+  const unsigned nbytes = (unsigned)__builtin_amdgcn_readfirstlane((int)a.w_bytes);
+  const __amdgpu_buffer_rsrc_t dr =
+      __builtin_amdgcn_make_buffer_rsrc(a.dW, (short)0, (int)nbytes, 0x00020000);
+  constexpr unsigned kOff = 0xFFFFFFF0u;
+  const int s0 = REV ? nf - nf / 2 : nf / 2;
+  const long long ub = (long long)b * T;
+  const unsigned long long* god = a.gden[REV ? 0 : 1];  // the other direction's rows
+  const unsigned long long* gon = a.gnum[REV ? 0 : 1];
+  auto store_frame = [&](int t, const float* x) {
+    const unsigned vb = (unsigned)__builtin_amdgcn_readfirstlane((int)((ub + t) * (long long)FR * es)) +
+                        (unsigned)(lane * es);
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      int vo = (int)(vb + (unsigned)(64 * k * es));
+      if (partial(k) && lane + 64 * k >= FR) vo = (int)kOff;
+      if constexpr (BF16)
+        __builtin_amdgcn_raw_buffer_store_b16(f2bf(x[k]), dr, vo, 0, 0);
+      else
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x[k]), dr, vo, 0, 0);
+    }
+  };
+  for (int i = s0 + m; i < nf; i += a.NM) {
+    const int t = REV ? nf - 1 - i : i;
+    const int slot = i % a.K;
+    // the own recursions are past step i: their rows of the step are in the rings
+    if (do_den && !wait_ge(ctl + CTL_DEN, i + 1, ctl + CTL_ABORT, a.err)) break;
+    if (!wait_ge(ctl + CTL_NUM, i + 1, ctl + CTL_ABORT, a.err)) break;
+    // the other direction's rows of frame t: poll the granules until every
+    // lane's tag matches (bounded; an abort drains the workgroup)
+    const unsigned tag = a.epoch * (unsigned)T + (unsigned)t;
+    float od = do_den ? 0.f : -kInf, onv[PN];
+    {
+      int n = 0;
+      bool ok = true;
+      for (;;) {
+        bool got = true;
+        if (do_den && lane < C) got = ld_gran(god + (ub + t) * C + lane, tag, &od);
+#pragma unroll
+        for (int s2 = 0; s2 < PN; ++s2) {
+          const int u = lane + 64 * s2;
+          onv[s2] = -kInf;
+          if (u < NP) got = ld_gran(gon + (ub + t) * NP + u, tag, &onv[s2]) && got;
+        }
+        if (__builtin_amdgcn_ballot_w64(!got) == 0) break;
+        if (*(ctl + CTL_ABORT)) { ok = false; break; }
+        __builtin_amdgcn_s_sleep(2);
+        if (++n > (1 << 22)) {
+          *(ctl + CTL_ABORT) = 1;
+          if (a.err) atomicOr(a.err, 2);
+          ok = false;
+          break;
+        }
+      }
+      if (!ok) break;
+    }
+    // frame t's rows into this wave's region (A[lanes >= C] = -inf serves the
+    // elements past the frame)
+    const lds_float* hr = hring + slot * kHS;
+    const lds_float* nr = nring + slot * NP;
+    const float own = (do_den && lane < C) ? hr[lane] : -kInf;
+    if constexpr (!REV) {  // own alpha_t, alpha^n_t; the beta side's beta_{t+1}, beta^n_{t+1}
+      A[lane] = (do_den && lane < C) ? own : -kInf;
+      Bt[lane] = (do_den && lane < C) ? od : 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < PN; ++s2) {
+        const int u = lane + 64 * s2;
+        AN[u] = u < NP ? nr[u] : -kInf;
+        BN[u] = onv[s2];
+      }
+    } else {  // own beta_{t+1}, beta^n_{t+1}; the alpha side's alpha_t, alpha^n_t
+      A[lane] = (do_den && lane < C) ? od : -kInf;
+      Bt[lane] = (do_den && lane < C) ? own : 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < PN; ++s2) {
+        const int u = lane + 64 * s2;
+        AN[u] = onv[s2];
+        BN[u] = u < NP ? nr[u] : -kInf;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NL; ++k) Sub[lane + 64 * k] = 0.f;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    // the frame's raw weights (fp32) staged in the slot by the helpers
+    const lds_float* Wr = (const lds_float*)as3(lds + a.off_ring + slot * a.slot_bytes);
+    float x[NL];
+    float m1 = -kInf;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      float w = Wr[lane + 64 * k];
+      if (partial(k) && lane + 64 * k >= FR) w = -kInf;  // the next frame's weight
+      x[k] = A[pq[k] & 0xffff] + w + Bt[pq[k] >> 16];
+      m1 = fmaxf(m1, x[k]);
+    }
+    const float md = safe(wave_max(m1));
+    float sd = 0.f;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      x[k] = lt_exp(x[k] - md);
+      sd += x[k];
+    }
+    sd = wave_sum(sd);
+    const float rd = (do_den && sd > 0.f && sd < kInf) ? __builtin_amdgcn_rcpf(sd) : 0.f;
+    float xn[NKL];
+    float mn = -kInf;
+#pragma unroll
+    for (int s2 = 0; s2 < NKL; ++s2) {
+      const float w = on[s2] >= 0 ? Wr[on[s2]] : -kInf;
+      xn[s2] = AN[uab[s2] & 0xffff] + w + BN[uab[s2] >> 16];
+      mn = fmaxf(mn, xn[s2]);
+    }
+    const float mns = safe(wave_max(mn));
+    float sn = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < NKL; ++s2) {
+      xn[s2] = lt_exp(xn[s2] - mns);
+      sn += xn[s2];
+    }
+    sn = wave_sum(sn);
+    const float rn = (sn > 0.f && sn < kInf) ? __builtin_amdgcn_rcpf(sn) : 0.f;
+    // a frame with a zero total (log_z = -inf, or an unreachable string) gets
+    // dW = 0, as lt_loss_backward does
+    const bool zero = (do_den && rd == 0.f) || rn == 0.f;
+    if (!zero) {
+#pragma unroll
+      for (int s2 = 0; s2 < NKL; ++s2)
+        if (on[s2] >= 0)
+          __hip_atomic_fetch_add(Sub + on[s2], xn[s2] * rn, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < NL; ++k) x[k] = x[k] * rd - Sub[lane + 64 * k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NL; ++k) x[k] = 0.f;
+    }
+    // the slot's LDS reads are issued (LDS is in order per wave): step done
+    asm volatile("" ::: "memory");
+    if (lane == 0) *(ctl + CTL_MRG + m) = i + 1;
+    store_frame(t, x);
+  }
+  // padding frames (lattices.py:775-779): zero marginals, from the alpha side
+  if (!REV && m == 0) {
+    float z[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) z[k] = 0.f;
+    for (int t = nf; t < T; ++t) store_frame(t, z);
+  }
+}
+
 // arc table of utterance b (lattices.py:314-338 arcs of the string; chains
 // link the string arcs that share a lattice arc) with sc1 stores, for the
 // marginal roles (fused mode)
@@ -1088,7 +1352,7 @@ LT_DEVINL void write_arcs_sc1(const PArgs& a, int b, const int* ctx, const int* 
 }
 
 template <int J, bool BF16, int PN, int D>
-__global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers), 4) void pipe_kernel(const PArgs a) {
+__global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void pipe_kernel(const PArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   int blk = (int)blockIdx.x;
   if (a.fused) {
@@ -1166,6 +1430,31 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers), 4) void pipe_kernel(con
   }
   if (!do_den && tid == 0) ctl[CTL_DEN] = 0x3fffffff;
   __syncthreads();
+  if (a.mid) {
+    // zero the granules this workgroup writes last -- the band of frames next
+    // to the middle, which the other direction polls first -- then raise the
+    // flag (epoch, ~epoch) behind every wave's stores: a poll of a granule not
+    // yet written then sees a zero tag, never a stale or arbitrary one (the
+    // frames further out are written before the band; mid_marg reaches them
+    // only after a band frame of the same direction)
+    const int h = nf / 2;
+    const int f0 = rev ? h : max(0, h - kMidBand), f1 = rev ? min(nf, h + kMidBand) : h;
+    const int NPr = a.U + 1;
+    // sc1 (write-through) stores: visible to a reader on any XCD
+    if (do_den)
+      for (int k = tid; k < (f1 - f0) * a.C; k += nthr)
+        __hip_atomic_store((g_u64*)(a.gden[rev] + ((long long)b * a.T + f0) * a.C + k), 0ULL,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = tid; k < (f1 - f0) * NPr; k += nthr)
+      __hip_atomic_store((g_u64*)(a.gnum[rev] + ((long long)b * a.T + f0) * NPr + k), 0ULL,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store((g_u64*)(a.mflag + (rev ? 1 : 0) * a.B + b),
+                         (unsigned long long)a.epoch | ((unsigned long long)~a.epoch << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (a.fused && !rev) {
     // published with the first steps: every storing wave's stores complete
     // before the barrier, the publications come after it
@@ -1190,6 +1479,36 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers), 4) void pipe_kernel(con
     if (a.fused && !LT_ABL(a, 8192)) __builtin_amdgcn_s_setprio(1);
     if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, wave - 2, lane);
     else helper_pipe<BF16, NL, false>(a, lds, b, nf, wave - 2, lane);
+  } else if (a.mid && wave - 2 - a.NH < a.NM) {
+    constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
+    const int m = wave - 2 - a.NH;
+    // the other direction's band granules are zeroed (its flag carries this call's epoch)
+    const unsigned long long want =
+        (unsigned long long)a.epoch | ((unsigned long long)~a.epoch << 32);
+    const unsigned long long* fl = a.mflag + (rev ? 0 : 1) * a.B + b;
+    int n = 0;
+    lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
+    bool ok = true;
+    while (__hip_atomic_load((const g_u64*)fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+      if (*(ctl + CTL_ABORT)) { ok = false; break; }
+      __builtin_amdgcn_s_sleep(4);
+      if (++n > (1 << 22)) {
+        *(ctl + CTL_ABORT) = 1;
+        if (a.err) atomicOr(a.err, 2);
+        ok = false;
+        break;
+      }
+    }
+    if (ok) {
+      const bool exact = (a.FR + 63) / 64 == NL;
+      if (rev) {
+        if (exact) mid_marg<BF16, NL, PN, true, true>(a, lds, b, nf, m, lane);
+        else mid_marg<BF16, NL, PN, false, true>(a, lds, b, nf, m, lane);
+      } else {
+        if (exact) mid_marg<BF16, NL, PN, true, false>(a, lds, b, nf, m, lane);
+        else mid_marg<BF16, NL, PN, false, false>(a, lds, b, nf, m, lane);
+      }
+    }
   }
   __syncthreads();
   if (a.trace && tid == 0) a.trace[2 * blk + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1224,6 +1543,17 @@ int launch_pipe_t(const PArgs& a, int grid, int threads, int lds, hipStream_t st
     int occ = -1;
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, threads, lds);
     fprintf(stderr, "[lt pipe] occupancy %d blocks/CU (threads %d, lds %d)\n", occ, threads, lds);
+  }
+  if (a.mid) {
+    // every recursion workgroup must be resident at once: the marginal waves
+    // of one direction wait on the other direction's first half
+    int occ = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, threads, lds) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        (long long)occ * cus < grid)
+      return lt_impl::set_error(LT_EUNSUPPORTED, "pipe mid: the grid is not co-resident");
+    if (a.W == nullptr) return LT_OK;  // a fit query only
   }
   hipLaunchKernelGGL((pipe_kernel<J, BF16, PN, D>), dim3(grid), dim3(threads), lds, st, a);
   e = hipGetLastError();
@@ -1263,12 +1593,34 @@ bool pipe_eligible(const lt_problem* pb) {
   return bytes < 0xFFFFFFF0LL && rows < 0xFFFFFFF0LL;
 }
 
+// mid mode workspace: the granule rows (alpha, beta [B,T,C]; alpha^n, beta^n
+// [B,T,U+1]; 8 bytes each), the band flags [2][B] and the error word
+size_t pipe_mid_workspace_bytes(const lt_problem* pb) {
+  const long long BT = (long long)pb->batch * pb->max_frames;
+  const long long C = pb->vocab_size + 1, NP = pb->max_labels + 1;
+  return (size_t)(8 * (2 * BT * C + 2 * BT * NP + 2LL * pb->batch) + 16);
+}
+
+static std::atomic<unsigned> g_mid_epoch{0};
+
+bool pipe_mid_fits(const lt_problem* pb) {
+  if (!pipe_eligible(pb) || pb->batch == 0 || pb->max_frames == 0) return false;
+  lt_problem q = *pb;
+  // the occupancy query of the launch itself (no W: nothing is launched)
+  return launch_pipe(&q, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, nullptr, nullptr, nullptr, nullptr, 2, nullptr, nullptr, nullptr,
+                     nullptr, 1, nullptr) == LT_OK;
+}
+
 int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32_t* nfr,
                 const int32_t* labels, const int32_t* nlab, float* loss, float* log_z,
                 float* num, float* alpha, float* alpha_num, float* beta, float* beta_num,
-                int32_t* arcs, int dirs, int* err, void* stream, void* dW, int* fctl) {
+                int32_t* arcs, int dirs, int* err, void* stream, void* dW, int* fctl, int mid,
+                void* mws) {
   if (!pipe_eligible(pb)) return set_error(LT_EUNSUPPORTED, "pipe: shape not eligible");
-  const bool fused = dW != nullptr;
+  if (mid && (dirs != 2 || (!dW && W) || (!mws && W)))
+    return set_error(LT_EINVAL, "pipe mid: both directions, dW and the workspace");
+  const bool fused = dW != nullptr && !mid;
   if (fused && (dirs != 2 || !fctl)) return set_error(LT_EINVAL, "pipe: fused needs both directions");
   PArgs a;
   memset(&a, 0, sizeof(a));
@@ -1315,7 +1667,6 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   a.off_u = off; off += al16((a.rowE + 4) * 4);
   a.off_ctx = off; off += al16(NP * 4);
   a.off_ylab = off; off += al16(NP * 4);
-  a.off_ring = off;
   int so = 0;
   const int NLc = a.J == 17 ? 18 : (a.J == 5 ? 5 : (a.J == 2 ? 2 : 1));
   if (NLc * 64 < FR) return set_error(LT_EUNSUPPORTED, "pipe: helper load plan");
@@ -1329,13 +1680,30 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   int grid = dirs * pb->batch;
   int cap = (grid > 256 || fused) ? 80 * 1024 : 160 * 1024;
   cap = pipe_env("LT_PIPE_LDS", cap);
-  int K = (cap - off) / so;
+  // mid mode: the marginal waves' regions, and per ring slot the den and
+  // numerator rows of its step
+  int per_slot = so;
+  if (mid) {
+    a.mid = 1;
+    a.NM = kPipeMidWaves;
+    a.mw_bytes = 4 * (128 + 128 * PN + 64 * NLc);
+    a.off_mw = off;
+    off += al16((long long)a.NM * a.mw_bytes);
+    per_slot = so + 4 * (kHS + ((NP + 3) & ~3));
+  }
+  a.off_ring = off;
+  int K = (cap - off) / per_slot;
   K = std::min(K, std::min(kPipeMaxSlots, pipe_env("LT_PIPE_SLOTS", 16)));
   if (K < 2) return set_error(LT_EUNSUPPORTED, "pipe: ring does not fit in LDS");
   a.K = K;
   a.NH = std::min(a.NH, K);
   int lds = off + K * so;
-  const int threads = 64 * (2 + a.NH);
+  if (mid) {
+    a.off_hring = lds;
+    a.off_nring = a.off_hring + K * kHS * 4;
+    lds = a.off_nring + K * ((NP + 3) & ~3) * 4;
+  }
+  const int threads = 64 * (2 + a.NH + (mid ? a.NM : 0));
   if (grid == 0) return LT_OK;
   hipStream_t st = (hipStream_t)stream;
   if (fused) {
@@ -1387,6 +1755,32 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
     const hipError_t e =
         hipMemsetAsync(fctl, 0, sizeof(int) * (4 + 4LL * pb->batch), st);
     if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
+  }
+  if (mid) {
+    // rows only for the other direction (granules), no checkpoints, no arcs
+    a.alpha = a.beta = a.alpha_num = a.beta_num = nullptr;
+    a.arcs = nullptr;
+    a.dW = dW;
+    const long long BT = (long long)pb->batch * pb->max_frames;
+    unsigned long long* g = (unsigned long long*)mws;
+    a.gden[0] = g; g += W ? BT * C : 0;
+    a.gden[1] = g; g += W ? BT * C : 0;
+    a.gnum[0] = g; g += W ? BT * NP : 0;
+    a.gnum[1] = g; g += W ? BT * NP : 0;
+    a.mflag = g; g += W ? 2LL * pb->batch : 0;
+    a.err = W ? (int*)g : nullptr;
+    // tags epoch * T + t stay nonzero and unique until the epoch wraps
+    unsigned ep = ++g_mid_epoch;
+    const unsigned lim = 0xFFFFFFFEu / (unsigned)(pb->max_frames + 1);
+    if (ep == 0 || ep >= lim) {
+      g_mid_epoch = 1;
+      ep = 1;
+    }
+    a.epoch = ep;
+    if (W) {
+      const hipError_t e = hipMemsetAsync(a.err, 0, sizeof(int), st);
+      if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
+    }
   }
   if (pipe_env("LT_VERBOSE", 0))
     fprintf(stderr, "[lt pipe] V=%d H=%d J=%d JP=%d PN=%d NH=%d K=%d slot=%d lds=%d grid=%d\n",
