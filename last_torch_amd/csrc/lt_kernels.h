@@ -1836,7 +1836,7 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
                 const int32_t* labels, const int32_t* nlab, float* loss, float* log_z,
                 float* num, float* alpha, float* alpha_num, float* beta, float* beta_num,
                 int32_t* arcs, int dirs, int* err, void* stream, void* dW = nullptr,
-                int* fctl = nullptr, int mid = 0, void* mws = nullptr);
+                int mid = 0, void* mws = nullptr);
 // mid mode (lt_loss_grad at large batches): workspace bytes; whether the
 // grid fits co-resident (launch_pipe with W == nullptr answers the same)
 size_t pipe_mid_workspace_bytes(const lt_problem* pb);

@@ -777,10 +777,10 @@ int cu_count() {
   return cus;
 }
 
-// lt_loss_grad workspace: checkpoints, arc table, hand-off counters and the
-// recursion backward's side buffer, each 256-byte aligned
+// lt_loss_grad workspace: checkpoints, arc table and the recursion
+// backward's side buffer, each 256-byte aligned
 struct GradWs {
-  size_t alpha, beta, an, bn, arcs, ctl, side, total;
+  size_t alpha, beta, an, bn, arcs, side, total;
 };
 GradWs grad_ws(const lt_problem* pb, int local_norm) {
   GradWs w;
@@ -794,7 +794,6 @@ GradWs grad_ws(const lt_problem* pb, int local_norm) {
   w.an = o; o += up(4 * B * T * NP);
   w.bn = o; o += up(4 * B * T * NP);
   w.arcs = o; o += up(4 * B * 4 * NP);
-  w.ctl = o; o += up(4 * (4 + 4 * B));
   w.side = o; o += up((long long)side_bytes(pb));
   w.total = o;
   return w;
@@ -1194,15 +1193,14 @@ int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
 // or the recursion pair (the environment overrides apply, as in the call).
 static int loss_grad_design(const lt_problem* pb) {
   if (lt_impl::chunk_preferred(pb) && pb->max_frames > 0) return LT_DESIGN_CHUNK;
-  // bigram past the chunked scan's range: the pipelined recursions with the
-  // marginals in their own workgroups (mid mode), while the grid fits
-  if (lt_impl::pipe_eligible(pb) && env_int("LT_MID", 1) && lt_impl::pipe_mid_fits(pb))
+  // the one-launch fused pipe (mid mode) measured level with the checkpointing
+  // pair at B = 192 / 256 (profiles/r03_mid_modes.txt), so it is not the
+  // default; lt_loss_grad_ex runs it on request
+  if (lt_impl::pipe_eligible(pb) && env_int("LT_MID", 0) && lt_impl::pipe_mid_fits(pb))
     return LT_DESIGN_FUSED_PIPE;
   const int cus = cu_count();
   const bool ck_def = 2 * pb->batch <= cus || (lt_impl::pipe_eligible(pb) && 2 * pb->batch <= 3 * cus);
   const bool ck = env_int("LT_CHECKPOINTS", ck_def ? 1 : 0) != 0;
-  const int fused = env_int("LT_FUSED", 2 * pb->batch < cus ? 1 : 0);
-  if (ck && fused && lt_impl::pipe_eligible(pb)) return LT_DESIGN_FUSED_PIPE;
   return ck ? LT_DESIGN_CHECKPOINTS : LT_DESIGN_RECURSION;
 }
 
@@ -1224,8 +1222,8 @@ static int resolve_design(const lt_problem* pb, int32_t design, int* out) {
   }
   if (design == LT_DESIGN_CHUNK && !(lt_impl::chunk_eligible(pb) && pb->max_frames > 0))
     return fail(LT_EUNSUPPORTED, "design chunk: FullNGram n = 1, vocab_size <= 32, labels < 128");
-  if (design == LT_DESIGN_FUSED_PIPE && !lt_impl::pipe_eligible(pb))
-    return fail(LT_EUNSUPPORTED, "design fused pipe: bigram shapes only");
+  if (design == LT_DESIGN_FUSED_PIPE && !(lt_impl::pipe_eligible(pb) && pb->max_labels + 1 <= 128))
+    return fail(LT_EUNSUPPORTED, "design fused pipe: bigram shapes, labels < 128");
   if (design < LT_DESIGN_CHUNK || design > LT_DESIGN_RECURSION)
     return fail(LT_EINVAL, "unknown design");
   *out = design;
@@ -1292,7 +1290,7 @@ int lt_loss_grad_ex(const lt_problem* pb, int32_t local_norm, int32_t design_in,
     if (!workspace || workspace_bytes < need) return fail(LT_EINVAL, "workspace too small");
     if ((rc = lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
                                    num, nullptr, nullptr, nullptr, nullptr, nullptr, 2, nullptr,
-                                   stream, dW, nullptr, 1, workspace)))
+                                   stream, dW, 1, workspace)))
       return rc;
     const long long BT = (long long)pb->batch * pb->max_frames;
     const int* err = (const int*)((char*)workspace +
@@ -1317,20 +1315,8 @@ int lt_loss_grad_ex(const lt_problem* pb, int32_t local_norm, int32_t design_in,
   }
   // checkpointing (alpha || beta, then the marginal pass) while 2B recursion
   // workgroups find CUs; with the pipelined bigram recursions up to 1.5 CUs
-  // utterances (measured crossover ~1.75: tools/b256_check.py); fused: the
-  // recursions and the marginal pass in one launch (lt_pipe.hip)
-  const bool ck = design == LT_DESIGN_CHECKPOINTS || design == LT_DESIGN_FUSED_PIPE;
-  if (design == LT_DESIGN_FUSED_PIPE) {
-    int* ctl = (int*)(ws + w.ctl);
-    if ((rc = lt_impl::launch_pipe(pb, local_norm, W, num_frames, labels, num_labels, loss,
-                                   log_z, num, alpha, an, beta, bn, arcs, 2, nullptr, stream, dW,
-                                   ctl)))
-      return rc;
-    hipLaunchKernelGGL(handoff_check_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
-                       (const int*)(ctl + 2), loss, pb->batch);
-    return hip_check(hipGetLastError(), "hand-off check launch");
-  }
-  if (ck) {
+  // utterances (measured crossover ~1.75: tools/b256_check.py)
+  if (design == LT_DESIGN_CHECKPOINTS || design == LT_DESIGN_FUSED_PIPE) {
     if ((rc = lt_loss_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
                               num, alpha, an, beta, bn, arcs, stream)))
       return rc;

@@ -49,7 +49,7 @@ namespace {
 
 constexpr int kPipeMaxSlots = 32;
 // 6 waves (den, num, 4 helpers); __launch_bounds__(384, 4) keeps them at
-// <= 128 VGPRs so that two workgroups share a CU in the fused launch
+// <= 128 VGPRs so that two workgroups share a CU at large batches
 constexpr int kPipeMaxHelpers = 4;
 
 struct PArgs {
@@ -80,18 +80,7 @@ struct PArgs {
   int stamp_block;
   int dbg;           // timing ablations (LT_PIPE_DBG): 1 no raw-W stores, 2 no E stores,
                      // 4 no den history, 8 no num history
-  // ---- fused loss + gradient (lt_loss_grad): marginal workgroups in the
-  // same launch consume frames as soon as both recursions have passed them
-  int fused;         // 0: recursions only; 1: + marginal roles (grid > dirs * B)
-  int* prog;         // [4][B] published steps: alpha den, alpha num, beta den, beta num
-  int* qctr;         // [0] role ticket, [1] marginal tile queue
-  void* dW;          // [B,T,C,V+1], W's dtype
-  const char* wsbase;  // workspace holding alpha, beta, alpha_num, beta_num, arcs (< 4 GB)
-  int FW, FT, NB, ntiles;  // frames per marginal wave / tile, tiles per utterance, tiles
-  int moff_ctl, moff_arc, moff_wave, mwave_bytes;  // marginal-role LDS layout
-  int mC4, mNP4, mFR4;     // padded row lengths (floats) in a wave's region
-  long long* trace;  // LT_FUSED_TRACE (diagnostics): [dirs*B][2] recursion start/end,
-                     // then [ntiles][4] tile grab/ready/done/role (s_memrealtime)
+  void* dW;          // [B,T,C,V+1], W's dtype (mid mode)
   // ---- in-workgroup marginals (lt_loss_grad at large batches, mid mode):
   // each recursion workgroup turns its second half of the frames into dW
   // from the W still in its ring (alpha: frames [nf/2, nf), beta: [0, nf/2))
@@ -125,7 +114,10 @@ constexpr int kHS = 64;
 #endif
 
 // control block (ints) at off_ctl
-constexpr int kPipeMidWaves = 2;  // marginal waves per workgroup in mid mode
+#ifndef LT_PIPE_MID
+#define LT_PIPE_MID 2
+#endif
+constexpr int kPipeMidWaves = LT_PIPE_MID;  // marginal waves per workgroup in mid mode
 enum { CTL_TAG = 0, CTL_DEN = kPipeMaxSlots, CTL_NUM, CTL_ABORT, CTL_FIN0, CTL_FIN1, CTL_MRG,
        CTL_N = CTL_MRG + kPipeMidWaves };
 
@@ -161,42 +153,19 @@ LT_DEVINL void lds_release_store(lds_vint* p, int v) {
   *p = v;
 }
 
-// ---- cross-workgroup hand-off (fused mode) --------------------------------
-// The recursions' history rows are written with sc1 (write-through) stores and
-// published per direction and wave through an sc1 flag store of the number of
-// completed steps; consumers poll with sc1 loads and read the rows with sc1
-// loads only (MI355X_MICROARCH.md, hand-off table row 1). A step's row is
-// published once the wave's vmcnt shows it complete: vmcnt decrements in
-// issue order, so `s_waitcnt vmcnt(n)` leaves only the n youngest stores
-// outstanding. Publications run every kPubEvery steps, kPubLag steps behind.
+// ---- cross-workgroup stores --------------------------------------------------
+// History rows go out with sc1 (write-through) stores; the mid mode's rows for
+// the other direction are 8-byte {value, tag} granules (one sc1 store each).
 typedef __attribute__((address_space(1))) float g_float;
 typedef __attribute__((address_space(1))) int g_int;
-constexpr int kPubEvery = 16, kPubLag = 8;
 LT_DEVINL void st_sc1(float* p, float v) {
   __hip_atomic_store((g_float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-LT_DEVINL void st_sc1(int* p, int v) {
-  __hip_atomic_store((g_int*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-LT_DEVINL int ld_sc1(const int* p) {
-  return __hip_atomic_load((g_int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 typedef __attribute__((address_space(1))) unsigned long long g_u64;
 LT_DEVINL void st_gran(unsigned long long* p, float v, unsigned tag) {
   const unsigned long long g = (unsigned long long)__float_as_uint(v) | ((unsigned long long)tag << 32);
   __hip_atomic_store((g_u64*)p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// true when the granule carries `tag`; its value in *v
-LT_DEVINL bool ld_gran(const unsigned long long* p, unsigned tag, float* v) {
-  const unsigned long long g = __hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  *v = __uint_as_float((unsigned)g);
-  return (unsigned)(g >> 32) == tag;
-}
-#ifdef LT_STAMPS
-#define LT_PUB_WAIT(n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-#else
-#define LT_PUB_WAIT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
-#endif
 
 // ---- cross-lane helpers (full exec) -------------------------------------
 template <int CTRL>
@@ -360,7 +329,6 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
   ubuf[pub_pos] = pub0 ? u0 : uo;
   float* hrow = (REV ? a.beta : a.alpha);
   const long long hstep = REV ? -(long long)C : (long long)C;
-  int* pub = a.fused ? a.prog + (REV ? 2 : 0) * a.B + b : nullptr;
   lds_float* hring = (lds_float*)(as3(lds) + a.off_hring);  // mid mode
   const int mid_s0 = REV ? nf - nf / 2 : nf / 2;
   if (hrow) hrow += ((long long)b * a.T + (REV ? nf - 1 : 0)) * C + hist_idx;
@@ -527,11 +495,6 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
       st_sc1(hrow, hval);
       hrow += hstep;
     }
-    if (pub && ((i + 1) % kPubEvery) == 0) {
-      // one store per step: the kPubLag youngest are steps i-7..i
-      LT_PUB_WAIT(8);
-      if (lane == 0) st_sc1(pub, i + 1 - kPubLag);
-    }
     if (!bad) {
       // next normaliser: exponent of this frame's max S
       float mx = act ? S : 0.f;
@@ -553,10 +516,6 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     if (lane == 0) *(ctl + CTL_DEN) = i + 1;
     PSTAMP(a, 0, i, 2);
     slot = nslot;
-  }
-  if (pub) {  // every step (also after an abort: consumers must not wait forever)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) st_sc1(pub, nf);
   }
   // final vector: padding rows (fwd, lattices.py:460-461) and log_z
   if (!REV) {
@@ -624,7 +583,6 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
   // utterance; history rows and num are offset + value, rounded once
   float off = 0.f;
   float* hist = REV ? a.beta_num : a.alpha_num;
-  int* pub = a.fused ? a.prog + (REV ? 3 : 1) * a.B + b : nullptr;
   lds_float* nring = (lds_float*)(as3(lds) + a.off_nring);  // mid mode
   int tag_next = nf > 0 ? ctl[CTL_TAG] : 0;
   const long long row0 = (long long)b * a.T;
@@ -695,18 +653,7 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     }
     asm volatile("" ::: "memory");  // LDS is in order per wave: no wait
     if (lane == 0) *(ctl + CTL_NUM) = i + 1;
-    if (pub && ((i + 1) % kPubEvery) == 0) {
-      // PN stores per step: the kPubLag * PN youngest are steps i-7..i
-      if constexpr (PN == 1) LT_PUB_WAIT(8);
-      else if constexpr (PN == 2) LT_PUB_WAIT(16);
-      else LT_PUB_WAIT(32);
-      if (lane == 0) st_sc1(pub, i + 1 - kPubLag);
-    }
     PSTAMP(a, 1, i, 2);
-  }
-  if (pub) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) st_sc1(pub, nf);
   }
   if (!REV) {
     if (a.alpha_num) {
@@ -852,275 +799,6 @@ LT_DEVINL void helper_pipe(const PArgs& a, unsigned char* lds, int b, int nf, in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ---- marginal role (fused mode) ----------------------------------------------
-// dW[b,t,p,y] = den - num marginals of frame t (alignments.py:311-317 for the
-// denominator, the string arcs of lattices.py:314-338 for the numerator), for
-// the gradient of sum_b loss_b. Tiles of FT frames are taken from a queue in
-// the order the two recursions make them ready (middle of the utterance
-// first); each wave of the workgroup then runs FW frames on its own.
-//
-// Normalisers: each frame is normalised by its own total,
-//   log_z = logsumexp_{p,y} alpha_t[p] + W_t[p,y] + beta_{t+1}[next(p,y)]
-// (the forward-backward identity holds at every live frame), and likewise the
-// numerator, so no frame waits for the end of the alpha pass. A frame whose
-// total is zero (log_z = -inf, or an unreachable string: num = -inf at every
-// frame) gets dW = 0, as lt_loss_backward does for those utterances.
-LT_DEVINL int mid_out(int k, int nb) {
-  const int mid = nb >> 1;
-  return (k & 1) ? mid - ((k + 1) >> 1) : mid + (k >> 1);
-}
-
-// EXACT: the frame fills exactly NL slots of 64 (ceil(FR / 64) == NL), so
-// only the last slot is partial; otherwise every slot is checked.
-template <bool BF16, int NL, int PN, bool EXACT>
-LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
-  const int tid = threadIdx.x, lane = tid & 63, nthr = blockDim.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int C = a.C, R = a.R, FR = a.FR, NP = a.U + 1, NK = 2 * NP, T = a.T, B = a.B;
-  const bool do_den = a.flags & F_DEN;
-  const int es = BF16 ? 2 : 4;
-  constexpr int PNW = PN;      // numerator row values per lane (NP <= 64 PN)
-  constexpr int NKL = 2 * PN;  // numerator arc slots per lane (NK <= 128 PN)
-  constexpr int D = NL * 64;   // dummy element: Wl[D] = -inf
-  lds_vint* sh = (lds_vint*)(as3(lds) + a.moff_ctl);
-  lds_int* aoff = (lds_int*)(as3(lds) + a.moff_arc);  // [NKL*64] arc element (or D)
-  // this wave's region (padded so that every lane's accesses are in range)
-  lds_float* A = (lds_float*)(as3(lds) + a.moff_wave + wave * a.mwave_bytes);
-  lds_float* Bt = A + 64;
-  lds_float* AN = Bt + 64;
-  lds_float* BN = AN + a.mNP4;
-  lds_float* Wl = BN + a.mNP4;
-  lds_float* Sub = Wl + a.mFR4;
-  if (lane == 0) Wl[D] = -kInf;
-  // this lane's elements e = lane + 64k: source p, destination q (n = 1:
-  // blank stays in p, label y goes to state y; contexts.py:190-205)
-  int pq[NL];  // p | q << 16
-#pragma unroll
-  for (int k = 0; k < NL; ++k) {
-    const int e = lane + 64 * k;
-    const int p = e / R, y = e - (e / R) * R;
-    pq[k] = e < FR ? (p | ((y == 0 ? p : y) << 16)) : (63 | (63 << 16));  // A[63] = -inf
-  }
-  // slot k may hold lanes past the frame (partial)
-  auto partial = [&](int k) { return EXACT ? k == NL - 1 : 64 * (k + 1) > FR; };
-  // numerator arc slots kk = lane + 64s: positions u and u or u+1 (clamped;
-  // invalid slots point at the dummy element, whose -inf term vanishes)
-  int uab[NKL];  // u | (u or u+1) << 16
-#pragma unroll
-  for (int s2 = 0; s2 < NKL; ++s2) {
-    const int kk = lane + 64 * s2;
-    const int u = min(kk >> 1, NP - 1);
-    uab[s2] = u | (min((kk & 1) ? u + 1 : u, NP - 1) << 16);
-  }
-  // buffer descriptors: out-of-range offsets (kOff) read 0 / drop the store,
-  // so the per-element accesses need no branches. The handed-off rows and the
-  // arc table (all in one workspace, < 4 GB) are read with sc1 loads (cache
-  // policy 16): plain buffer loads, not atomics, so nothing orders them
-  // behind this wave's stores.
-  const unsigned nbytes = (unsigned)__builtin_amdgcn_readfirstlane((int)a.w_bytes);
-  const __amdgpu_buffer_rsrc_t wr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.W, (short)0, (int)nbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t dr =
-      __builtin_amdgcn_make_buffer_rsrc(a.dW, (short)0, (int)nbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.wsbase, (short)0, (int)0xFFFFFFF0u, 0x00020000);
-  const unsigned o_al = (unsigned)((const char*)a.alpha - a.wsbase);
-  const unsigned o_be = (unsigned)((const char*)a.beta - a.wsbase);
-  const unsigned o_an = (unsigned)((const char*)a.alpha_num - a.wsbase);
-  const unsigned o_bn = (unsigned)((const char*)a.beta_num - a.wsbase);
-  const unsigned o_ar = (unsigned)((const char*)a.arcs - a.wsbase);
-  constexpr unsigned kOff = 0xFFFFFFF0u;
-  constexpr int kSc1 = 16;
-  for (;;) {
-    if (tid == 0) *sh = atomicAdd(a.qctr + 1, 1);
-    __syncthreads();
-    const int j = *sh;
-    if (j >= a.ntiles) break;
-    long long* tr = a.trace ? a.trace + 2LL * a.dirs * B + 4LL * j : nullptr;
-    if (tr && tid == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
-    const int kb = j / B, b = j - kb * B;
-    const int t0 = mid_out(kb, a.NB) * a.FT, t1 = min(T, t0 + a.FT);
-    int nf = a.nfr[b];
-    nf = nf < 0 ? 0 : (nf > T ? T : nf);
-    const int tl = min(t1, nf);  // live frames of the tile: [t0, tl)
-    if (t0 < tl) {
-      if (tid == 0) {
-        // alpha rows [0, tl) and beta rows [t0, nf) published
-        const int* pg = a.prog;
-        int n = 0;
-        bool ok = true;
-        for (int r = do_den ? 0 : 1; r < 4 && ok; r += do_den ? 1 : 2) {
-          const int need = (r < 2) ? tl : nf - t0;
-          while (ld_sc1(pg + r * B + b) < need) {
-            __builtin_amdgcn_s_sleep(8);
-            if (++n > (1 << 22)) {
-              if (a.err) atomicOr(a.err, 2);
-              ok = false;
-              break;
-            }
-          }
-        }
-      }
-      __syncthreads();
-      if (tr && tid == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
-      for (int k = tid; k < NKL * 64; k += nthr) {
-        const int ro = (int)(k < NK ? o_ar + (unsigned)(((long long)b * 2 * NK + k) * 4) : kOff);
-        const int o = (int)__builtin_amdgcn_raw_buffer_load_b32(xr, ro, 0, kSc1);
-        aoff[k] = (k < NK && o >= 0) ? o : D;
-      }
-      __syncthreads();
-    }
-    // ---- this wave's frames (the next one in flight)
-    const int tw0 = t0 + wave * a.FW, tw1 = min(t1, tw0 + a.FW);
-    const int twl = min(tw1, tl);  // this wave's live frames end
-    const long long ub = (long long)b * T;
-    struct Buf {
-      float w[NL], ra, rb, ran[PNW], rbn[PNW];
-    };
-    Buf X;
-    auto fetch = [&](Buf& f, int t) {
-      if (t >= twl) return;
-      const unsigned vb = (unsigned)__builtin_amdgcn_readfirstlane(
-          (int)((ub + t) * (long long)FR * es)) + (unsigned)(lane * es);
-      // lanes past the frame read the next frame (or 0 past the tensor): unused
-#pragma unroll
-      for (int k = 0; k < NL; ++k) {
-        const int vo = (int)(vb + (unsigned)(64 * k * es));
-        if constexpr (BF16)
-          f.w[k] = __uint_as_float(
-              ((unsigned)__builtin_amdgcn_raw_buffer_load_b16(wr, vo, 0, 0)) << 16);
-        else
-          f.w[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wr, vo, 0, 0));
-      }
-      const unsigned rc = (unsigned)__builtin_amdgcn_readfirstlane((int)((ub + t) * C * 4));
-      const unsigned rn = (unsigned)__builtin_amdgcn_readfirstlane((int)((ub + t) * NP * 4));
-      if (LT_ABL(a, 1024)) return;
-      if (do_den) {
-        const unsigned ro = lane < C ? rc + lane * 4 : kOff;
-        f.ra = __uint_as_float(
-            __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(lane < C ? o_al + ro : kOff), 0, kSc1));
-        f.rb = __uint_as_float(
-            __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(lane < C ? o_be + ro : kOff), 0, kSc1));
-      }
-#pragma unroll
-      for (int s = 0; s < PNW; ++s) {
-        const int u = lane + 64 * s;
-        const unsigned ro = rn + u * 4;
-        f.ran[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-            xr, (int)(u < NP ? o_an + ro : kOff), 0, kSc1));
-        f.rbn[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-            xr, (int)(u < NP ? o_bn + ro : kOff), 0, kSc1));
-      }
-    };
-    auto process = [&](Buf& f, int t) {
-      if (t >= tw1) return;
-      const unsigned vb = (unsigned)__builtin_amdgcn_readfirstlane(
-          (int)((ub + t) * (long long)FR * es)) + (unsigned)(lane * es);
-      float x[NL];  // denominator terms, then the frame's dW values
-#pragma unroll
-      for (int k = 0; k < NL; ++k) x[k] = 0.f;
-      bool zero = t >= tl;
-      if (!zero) {
-        // frame t's operands into this wave's (padded) LDS region
-        // A[63] = -inf serves the lanes past the frame (and every lane when
-        // there is no denominator)
-        A[lane] = (do_den && lane < C) ? f.ra : -kInf;
-        Bt[lane] = do_den ? f.rb : 0.f;
-#pragma unroll
-        for (int s = 0; s < PNW; ++s) {
-          AN[lane + 64 * s] = f.ran[s];
-          BN[lane + 64 * s] = f.rbn[s];
-        }
-#pragma unroll
-        for (int k = 0; k < NL; ++k) {
-            Wl[lane + 64 * k] = f.w[k];
-          Sub[lane + 64 * k] = 0.f;
-        }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        // denominator terms and the frame total
-        float m = -kInf;
-#pragma unroll
-        for (int k = 0; k < NL; ++k) {
-            // past the frame: the next frame's weight (may be +inf) -> -inf
-          if (partial(k) && lane + 64 * k >= FR) f.w[k] = -kInf;
-          x[k] = A[pq[k] & 0xffff] + f.w[k] + Bt[pq[k] >> 16];
-          m = fmaxf(m, x[k]);
-        }
-        fetch(f, t + 1);  // the next frame's loads overlap this one
-        const float md = safe(wave_max(m));
-        float sd = 0.f;
-#pragma unroll
-        for (int k = 0; k < NL; ++k) {
-            x[k] = lt_exp(x[k] - md);
-          sd += x[k];
-        }
-        sd = wave_sum(sd);
-        const float rd = (do_den && sd > 0.f && sd < kInf) ? __builtin_amdgcn_rcpf(sd) : 0.f;
-        // numerator arc terms and their total
-        float xn[NKL];
-        int on[NKL];
-        float mn = -kInf;
-#pragma unroll
-        for (int s = 0; s < NKL; ++s) {
-          on[s] = aoff[lane + 64 * s];
-          xn[s] = AN[uab[s] & 0xffff] + Wl[on[s]] + BN[uab[s] >> 16];
-          mn = fmaxf(mn, xn[s]);
-        }
-        const float mns = safe(wave_max(mn));
-        float sn = 0.f;
-#pragma unroll
-        for (int s = 0; s < NKL; ++s) {
-          xn[s] = lt_exp(xn[s] - mns);
-          sn += xn[s];
-        }
-        sn = wave_sum(sn);
-        const float rn = (sn > 0.f && sn < kInf) ? __builtin_amdgcn_rcpf(sn) : 0.f;
-        zero = (do_den && rd == 0.f) || rn == 0.f;
-        if (LT_ABL(a, 256)) zero = false;
-        if (!zero) {
-          // string arcs sharing a lattice arc meet in LDS float adds; one
-          // wave's adds apply in program and lane order (deterministic)
-#pragma unroll
-          for (int s = 0; s < NKL; ++s)
-            __hip_atomic_fetch_add(Sub + on[s], xn[s] * rn, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-          __builtin_amdgcn_wave_barrier();
-          asm volatile("" ::: "memory");
-#pragma unroll
-          for (int k = 0; k < NL; ++k) {
-                x[k] = x[k] * rd - Sub[lane + 64 * k];
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-      }
-      if (zero) {
-#pragma unroll
-        for (int k = 0; k < NL; ++k) x[k] = 0.f;
-      }
-      // full slots store as is; the partial last slot only from lanes in the frame
-#pragma unroll
-      for (int k = 0; k < NL; ++k) {
-        int vo = (int)(vb + (unsigned)(64 * k * es));
-        if (partial(k) && lane + 64 * k >= FR) vo = (int)kOff;
-        if (LT_ABL(a, 4096)) vo = (int)kOff;
-        if constexpr (BF16)
-          __builtin_amdgcn_raw_buffer_store_b16(f2bf(x[k]), dr, vo, 0, 0);
-        else
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x[k]), dr, vo, 0, 0);
-      }
-    };
-    fetch(X, tw0);
-    for (int t = tw0; t < tw1; ++t) process(X, t);
-    __syncthreads();
-    if (tr && tid == 0) {
-      tr[2] = __builtin_amdgcn_s_memrealtime();
-      tr[3] = (long long)blockIdx.x;
-    }
-  }
-}
-
 // ---- in-workgroup marginals (mid mode) --------------------------------------
 // Marginal wave m of a recursion workgroup turns the frames of its steps
 // i = s0 + m, s0 + m + NM, ... (the workgroup's far half: alpha frames
@@ -1128,10 +806,17 @@ LT_DEVINL void marg_role(const PArgs& a, unsigned char* lds) {
 // ring: the workgroup's own den / numerator rows of the step from LDS (hring,
 // nring: the pre-update vectors the den and numerator waves leave there with
 // the step), the other direction's rows of the frame from its granules (that
-// direction passed the frame in its own first half). Every frame is
-// normalised by its own total, as marg_role does (alignments.py:311-317; the
-// string arcs of lattices.py:314-338 summed per lattice arc in LDS, one
-// wave's adds in program and lane order: deterministic).
+// direction passed the frame in its own first half).
+//
+// dW[b,t,p,y] = den - num marginals of frame t (alignments.py:311-317 for the
+// denominator; the string arcs of lattices.py:314-338 for the numerator,
+// summed per lattice arc in LDS, one wave's adds in program and lane order:
+// deterministic). Each frame is normalised by its own total,
+//   log_z = logsumexp_{p,y} alpha_t[p] + W_t[p,y] + beta_{t+1}[next(p,y)]
+// (the forward-backward identity holds at every live frame), and likewise the
+// numerator, so no frame waits for the end of the other pass. A frame whose
+// total is zero (log_z = -inf, or an unreachable string) gets dW = 0, as
+// lt_loss_backward does for those utterances.
 template <bool BF16, int NL, int PN, bool EXACT, bool REV>
 LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m, int lane) {
   lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
@@ -1148,15 +833,35 @@ LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m
   lds_float* AN = Bt + 64;        // [64 PN]
   lds_float* BN = AN + 64 * PN;   // [64 PN]
   lds_float* Sub = BN + 64 * PN;  // [64 NL]
+  lds_float* AL = Sub + 64 * NL;  // [64] exp(alpha - max alpha)
+  lds_float* BL = AL + 64;        // [64] exp(beta - max beta)
   // elements e = lane + 64k: source p, destination q (n = 1: the blank stays
   // in p, label y goes to state y; contexts.py:190-205); past the frame A[63]
-  int pq[NL];
+  // packed per element: the byte offset of its E = exp(W - c) in the slot
+  // (helper_pipe's consumer layout) in bits 0-15, p in 16-23, q in 24-31; the
+  // den marginal of a frame is then a product of three linear factors, no
+  // exp per element
+  int pk[NL];
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     const int e = lane + 64 * k;
-    const int p = e / R, y = e - (e / R) * R;
-    pq[k] = e < FR ? (p | ((y == 0 ? p : y) << 16)) : (63 | (63 << 16));
+    int o = a.soff_c + 8, p = 63, q = 63;
+    if (e < FR) {
+      p = e / R;
+      const int y = e - p * R;
+      q = y == 0 ? p : y;
+      if (y == 0) {
+        o = a.soff_eb + 4 * p;
+      } else {
+        const int row = REV ? p : y - 1;
+        const int kk = REV ? y - 1 : p;
+        o = a.soff_e + 4 * (row * a.rowE + (kk / a.J) * a.JP + (kk % a.J));
+      }
+    }
+    pk[k] = o | (p << 16) | (q << 24);
   }
+  auto pof = [&](int k) { return (pk[k] >> 16) & 0xff; };
+  auto qof = [&](int k) { return (int)((unsigned)pk[k] >> 24); };
   auto partial = [&](int k) { return EXACT ? k == NL - 1 : 64 * (k + 1) > FR; };
   // numerator arc slots kk = lane + 64 s: the arc's element (-1: none) and
   // its positions u and u or u+1 (lattices.py:314-338)
@@ -1194,31 +899,49 @@ LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x[k]), dr, vo, 0, 0);
     }
   };
+  // the other direction's granules of a step, prefetched one assigned step
+  // ahead so their latency hides under the current frame's work
+  unsigned long long gd = 0, gn[PN];
+#pragma unroll
+  for (int s2 = 0; s2 < PN; ++s2) gn[s2] = 0;
+  auto fetch = [&](int i) {
+    const int t = REV ? nf - 1 - i : i;
+    if (do_den && lane < C)
+      gd = __hip_atomic_load((const g_u64*)(god + (ub + t) * C + lane), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int s2 = 0; s2 < PN; ++s2) {
+      const int u = lane + 64 * s2;
+      if (u < NP)
+        gn[s2] = __hip_atomic_load((const g_u64*)(gon + (ub + t) * NP + u), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  auto tags_ok = [&](unsigned tag) {
+    bool got = !(do_den && lane < C) || (unsigned)(gd >> 32) == tag;
+#pragma unroll
+    for (int s2 = 0; s2 < PN; ++s2)
+      got = got && (lane + 64 * s2 >= NP || (unsigned)(gn[s2] >> 32) == tag);
+    return got;
+  };
+  if (s0 + m < nf) fetch(s0 + m);
   for (int i = s0 + m; i < nf; i += a.NM) {
     const int t = REV ? nf - 1 - i : i;
     const int slot = i % a.K;
     // the own recursions are past step i: their rows of the step are in the rings
     if (do_den && !wait_ge(ctl + CTL_DEN, i + 1, ctl + CTL_ABORT, a.err)) break;
     if (!wait_ge(ctl + CTL_NUM, i + 1, ctl + CTL_ABORT, a.err)) break;
-    // the other direction's rows of frame t: poll the granules until every
-    // lane's tag matches (bounded; an abort drains the workgroup)
+    // the other direction's rows of frame t: the prefetched granules, else
+    // poll until every lane's tag matches (bounded; an abort drains)
     const unsigned tag = a.epoch * (unsigned)T + (unsigned)t;
-    float od = do_den ? 0.f : -kInf, onv[PN];
-    {
+    if (__builtin_amdgcn_ballot_w64(!tags_ok(tag)) != 0) {
       int n = 0;
       bool ok = true;
       for (;;) {
-        bool got = true;
-        if (do_den && lane < C) got = ld_gran(god + (ub + t) * C + lane, tag, &od);
-#pragma unroll
-        for (int s2 = 0; s2 < PN; ++s2) {
-          const int u = lane + 64 * s2;
-          onv[s2] = -kInf;
-          if (u < NP) got = ld_gran(gon + (ub + t) * NP + u, tag, &onv[s2]) && got;
-        }
-        if (__builtin_amdgcn_ballot_w64(!got) == 0) break;
-        if (*(ctl + CTL_ABORT)) { ok = false; break; }
         __builtin_amdgcn_s_sleep(2);
+        fetch(i);
+        if (__builtin_amdgcn_ballot_w64(!tags_ok(tag)) == 0) break;
+        if (*(ctl + CTL_ABORT)) { ok = false; break; }
         if (++n > (1 << 22)) {
           *(ctl + CTL_ABORT) = 1;
           if (a.err) atomicOr(a.err, 2);
@@ -1228,6 +951,12 @@ LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m
       }
       if (!ok) break;
     }
+    const float od = do_den ? __uint_as_float((unsigned)gd) : -kInf;
+    float onv[PN];
+#pragma unroll
+    for (int s2 = 0; s2 < PN; ++s2)
+      onv[s2] = lane + 64 * s2 < NP ? __uint_as_float((unsigned)gn[s2]) : -kInf;
+    if (i + a.NM < nf) fetch(i + a.NM);
     // frame t's rows into this wave's region (A[lanes >= C] = -inf serves the
     // elements past the frame)
     const lds_float* hr = hring + slot * kHS;
@@ -1252,29 +981,53 @@ LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m
         BN[u] = u < NP ? nr[u] : -kInf;
       }
     }
+    // linear factors of the two den rows, each over its own max
+    const float va = (do_den && lane < C) ? (REV ? od : own) : -kInf;
+    const float vb = (do_den && lane < C) ? (REV ? own : od) : -kInf;
+    const float ma = safe(wave_max(va)), mb = safe(wave_max(vb));
+    AL[lane] = lane < C ? lt_exp(va - ma) : 0.f;
+    BL[lane] = lane < C ? lt_exp(vb - mb) : 0.f;
 #pragma unroll
     for (int k = 0; k < NL; ++k) Sub[lane + 64 * k] = 0.f;
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
+    const unsigned char* sb = lds + a.off_ring + slot * a.slot_bytes;
     // the frame's raw weights (fp32) staged in the slot by the helpers
-    const lds_float* Wr = (const lds_float*)as3(lds + a.off_ring + slot * a.slot_bytes);
+    const lds_float* Wr = (const lds_float*)as3((unsigned char*)sb);
     float x[NL];
-    float m1 = -kInf;
-#pragma unroll
-    for (int k = 0; k < NL; ++k) {
-      float w = Wr[lane + 64 * k];
-      if (partial(k) && lane + 64 * k >= FR) w = -kInf;  // the next frame's weight
-      x[k] = A[pq[k] & 0xffff] + w + Bt[pq[k] >> 16];
-      m1 = fmaxf(m1, x[k]);
-    }
-    const float md = safe(wave_max(m1));
+    // den marginals exp(alpha + w + beta) / frame total as the products
+    // exp(alpha - ma) exp(w - c) exp(beta - mb) over their sum: every product
+    // is <= 1 and a dropped (underflowed) one is below 2^-126; with the sum at
+    // or above 2^-64 that is below fp32 rounding of any marginal that matters.
+    // Below it (or on a non-finite sum) the frame runs the exact log-space
+    // sum with the safe max (semirings.py:279-286).
     float sd = 0.f;
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
-      x[k] = lt_exp(x[k] - md);
+      const float ev = *(const lds_float*)as3((unsigned char*)sb + (pk[k] & 0xffff));
+      const float pr = AL[pof(k)] * ev * BL[qof(k)];
+      x[k] = (partial(k) && lane + 64 * k >= FR) ? 0.f : pr;
       sd += x[k];
     }
     sd = wave_sum(sd);
+    if (do_den && !(sd >= 0x1p-64f && sd < kInf)) {
+      float m1 = -kInf;
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        float w = Wr[lane + 64 * k];
+        if (partial(k) && lane + 64 * k >= FR) w = -kInf;  // the next frame's weight
+        x[k] = A[pof(k)] + w + Bt[qof(k)];
+        m1 = fmaxf(m1, x[k]);
+      }
+      const float md = safe(wave_max(m1));
+      sd = 0.f;
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        x[k] = lt_exp(x[k] - md);
+        sd += x[k];
+      }
+      sd = wave_sum(sd);
+    }
     const float rd = (do_den && sd > 0.f && sd < kInf) ? __builtin_amdgcn_rcpf(sd) : 0.f;
     float xn[NKL];
     float mn = -kInf;
@@ -1324,69 +1077,13 @@ LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m
   }
 }
 
-// arc table of utterance b (lattices.py:314-338 arcs of the string; chains
-// link the string arcs that share a lattice arc) with sc1 stores, for the
-// marginal roles (fused mode)
-LT_DEVINL void write_arcs_sc1(const PArgs& a, int b, const int* ctx, const int* ylab, int tid,
-                              int nthr) {
-  const int NP = a.U + 1, NK = 2 * NP;
-  int* off = a.arcs + (long long)b * 2 * NK;
-  int* link = off + NK;
-  auto arc = [&](int k) {
-    const int u = k >> 1;
-    return (k & 1) == 0 ? ctx[u] : (u < a.U ? ctx[u] + ylab[u] : -1);
-  };
-  for (int k = tid; k < NK; k += nthr) {
-    const int o = arc(k);
-    int head = o >= 0 ? 1 : 0, nxt = -1;
-    if (o >= 0) {
-      for (int k2 = 0; k2 < NK; ++k2) {
-        if (arc(k2) != o) continue;
-        if (k2 < k) head = 0;
-        else if (k2 > k && nxt < 0) nxt = k2;
-      }
-    }
-    st_sc1(off + k, o);
-    st_sc1(link + k, (head << 30) | (nxt + 1));
-  }
-}
-
 template <int J, bool BF16, int PN, int D>
 __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void pipe_kernel(const PArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  int blk = (int)blockIdx.x;
-  if (a.fused) {
-    // roles by arrival: the first dirs*B workgroups to start run the
-    // recursions, so every recursion is resident before any marginal
-    // workgroup waits on it (no dependence on the dispatch order)
-    if (threadIdx.x == 0) *(lds_vint*)as3(lds) = atomicAdd(a.qctr, 1);
-    __syncthreads();
-    blk = *(lds_vint*)as3(lds);
-    __syncthreads();
-    if (a.trace && threadIdx.x == 0) {
-      // [grid][2] after the tile records: start time, (XCC, SE/SH/CU) ids
-      long long* tw = a.trace + 2LL * a.dirs * a.B + 4LL * a.ntiles + 2LL * blockIdx.x;
-      tw[0] = __builtin_amdgcn_s_memrealtime();
-      unsigned hw, xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      tw[1] = ((long long)xcc << 32) | hw | ((long long)blk << 40);
-    }
-    if (blk >= a.dirs * a.B) {
-      constexpr int NLm = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
-      if ((a.FR + 63) / 64 == NLm) marg_role<BF16, NLm, PN, true>(a, lds);
-      else marg_role<BF16, NLm, PN, false>(a, lds);
-      return;
-    }
-  }
+  const int blk = (int)blockIdx.x;
   const bool rev = a.dirs == 2 && blk >= a.B;
   const int b = rev ? blk - a.B : blk;
   const int tid = threadIdx.x, lane = tid & 63;
-  if (a.fused && LT_ABL(a, 128)) {  // timing ablation: marginal roles alone
-    if (threadIdx.x < 2) st_sc1(a.prog + ((rev ? 2 : 0) + threadIdx.x) * a.B + b, a.T);
-    return;
-  }
-  if (a.trace && threadIdx.x == 0) a.trace[2 * blk] = __builtin_amdgcn_s_memrealtime();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nthr = blockDim.x;
   const bool do_den = a.flags & F_DEN;
@@ -1455,13 +1152,6 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void
                          (unsigned long long)a.epoch | ((unsigned long long)~a.epoch << 32),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (a.fused && !rev) {
-    // published with the first steps: every storing wave's stores complete
-    // before the barrier, the publications come after it
-    write_arcs_sc1(a, b, ctx, ylab, tid, nthr);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
 
   if (wave == 0) {
     __builtin_amdgcn_s_setprio(3);
@@ -1475,50 +1165,49 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void
     else num_pipe<PN, false>(a, lds, b, nf, lane);
   } else if (wave - 2 < a.NH) {
     constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
-    // above the marginal roles (priority 0) that share the CU in fused mode
-    if (a.fused && !LT_ABL(a, 8192)) __builtin_amdgcn_s_setprio(1);
     if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, wave - 2, lane);
     else helper_pipe<BF16, NL, false>(a, lds, b, nf, wave - 2, lane);
   } else if (a.mid && wave - 2 - a.NH < a.NM) {
-    constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
-    const int m = wave - 2 - a.NH;
-    // the other direction's band granules are zeroed (its flag carries this call's epoch)
-    const unsigned long long want =
-        (unsigned long long)a.epoch | ((unsigned long long)~a.epoch << 32);
-    const unsigned long long* fl = a.mflag + (rev ? 0 : 1) * a.B + b;
-    int n = 0;
-    lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
-    bool ok = true;
-    while (__hip_atomic_load((const g_u64*)fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
-      if (*(ctl + CTL_ABORT)) { ok = false; break; }
-      __builtin_amdgcn_s_sleep(4);
-      if (++n > (1 << 22)) {
-        *(ctl + CTL_ABORT) = 1;
-        if (a.err) atomicOr(a.err, 2);
-        ok = false;
-        break;
+    if constexpr (PN <= 2) {  // mid mode: U < 128 (pipe_mid_fits)
+      constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
+      const int m = wave - 2 - a.NH;
+      // the other direction's band granules are zeroed (its flag carries this call's epoch)
+      const unsigned long long want =
+          (unsigned long long)a.epoch | ((unsigned long long)~a.epoch << 32);
+      const unsigned long long* fl = a.mflag + (rev ? 0 : 1) * a.B + b;
+      int n = 0;
+      lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
+      bool ok = true;
+      while (__hip_atomic_load((const g_u64*)fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+        if (*(ctl + CTL_ABORT)) { ok = false; break; }
+        __builtin_amdgcn_s_sleep(4);
+        if (++n > (1 << 22)) {
+          *(ctl + CTL_ABORT) = 1;
+          if (a.err) atomicOr(a.err, 2);
+          ok = false;
+          break;
+        }
       }
-    }
-    if (ok) {
-      const bool exact = (a.FR + 63) / 64 == NL;
-      if (rev) {
-        if (exact) mid_marg<BF16, NL, PN, true, true>(a, lds, b, nf, m, lane);
-        else mid_marg<BF16, NL, PN, false, true>(a, lds, b, nf, m, lane);
-      } else {
-        if (exact) mid_marg<BF16, NL, PN, true, false>(a, lds, b, nf, m, lane);
-        else mid_marg<BF16, NL, PN, false, false>(a, lds, b, nf, m, lane);
+      if (ok) {
+        const bool exact = (a.FR + 63) / 64 == NL;
+        if (rev) {
+          if (exact) mid_marg<BF16, NL, PN, true, true>(a, lds, b, nf, m, lane);
+          else mid_marg<BF16, NL, PN, false, true>(a, lds, b, nf, m, lane);
+        } else {
+          if (exact) mid_marg<BF16, NL, PN, true, false>(a, lds, b, nf, m, lane);
+          else mid_marg<BF16, NL, PN, false, false>(a, lds, b, nf, m, lane);
+        }
       }
     }
   }
   __syncthreads();
-  if (a.trace && tid == 0) a.trace[2 * blk + 1] = __builtin_amdgcn_s_memrealtime();
   if (!rev) {
     if (tid == 0 && a.loss) {
       const lds_float* fin = (const lds_float*)(as3(lds) + a.off_ctl);
       const float num = fin[CTL_FIN1];
       a.loss[b] = (a.flags & F_LOCAL) ? -num : fin[CTL_FIN0] - num;
     }
-    if (a.arcs && !a.fused) {
+    if (a.arcs) {
       KArgs ka;
       ka.arcs = a.arcs;
       ka.U = a.U;
@@ -1541,7 +1230,7 @@ int launch_pipe_t(const PArgs& a, int grid, int threads, int lds, hipStream_t st
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   if (pipe_env("LT_VERBOSE", 0)) {
     int occ = -1;
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, threads, lds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, threads, lds);
     fprintf(stderr, "[lt pipe] occupancy %d blocks/CU (threads %d, lds %d)\n", occ, threads, lds);
   }
   if (a.mid) {
@@ -1604,24 +1293,24 @@ size_t pipe_mid_workspace_bytes(const lt_problem* pb) {
 static std::atomic<unsigned> g_mid_epoch{0};
 
 bool pipe_mid_fits(const lt_problem* pb) {
-  if (!pipe_eligible(pb) || pb->batch == 0 || pb->max_frames == 0) return false;
+  // (U < 128: the marginal waves' registers stay below the spill point)
+  if (!pipe_eligible(pb) || pb->batch == 0 || pb->max_frames == 0 || pb->max_labels + 1 > 128)
+    return false;
   lt_problem q = *pb;
   // the occupancy query of the launch itself (no W: nothing is launched)
   return launch_pipe(&q, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, nullptr, nullptr, nullptr, 2, nullptr, nullptr, nullptr,
-                     nullptr, 1, nullptr) == LT_OK;
+                     nullptr, nullptr, nullptr, nullptr, nullptr, 2, nullptr, nullptr, nullptr, 1,
+                     nullptr) == LT_OK;
 }
 
 int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32_t* nfr,
                 const int32_t* labels, const int32_t* nlab, float* loss, float* log_z,
                 float* num, float* alpha, float* alpha_num, float* beta, float* beta_num,
-                int32_t* arcs, int dirs, int* err, void* stream, void* dW, int* fctl, int mid,
+                int32_t* arcs, int dirs, int* err, void* stream, void* dW, int mid,
                 void* mws) {
   if (!pipe_eligible(pb)) return set_error(LT_EUNSUPPORTED, "pipe: shape not eligible");
   if (mid && (dirs != 2 || (!dW && W) || (!mws && W)))
     return set_error(LT_EINVAL, "pipe mid: both directions, dW and the workspace");
-  const bool fused = dW != nullptr && !mid;
-  if (fused && (dirs != 2 || !fctl)) return set_error(LT_EINVAL, "pipe: fused needs both directions");
   PArgs a;
   memset(&a, 0, sizeof(a));
   const int V = pb->vocab_size, C = V + 1, R = V + 1, FR = C * R, U = pb->max_labels;
@@ -1660,6 +1349,7 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   a.w_bytes = (unsigned)((long long)pb->batch * pb->max_frames * FR * es);
   const int PN = U + 1 <= 64 ? 1 : (U + 1 <= 128 ? 2 : 4);
   const int NP = U + 1;
+  if (mid && PN > 2) return set_error(LT_EUNSUPPORTED, "pipe mid: labels < 128");
   auto al16 = [](long long x) { return (int)((x + 15) & ~15LL); };
   int off = 0;
   a.off_ctl = off; off += al16(CTL_N * 4);
@@ -1676,9 +1366,8 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   a.soff_c = so; so += 16;
   a.slot_bytes = so;
   // LDS budget: two workgroups per CU when the grid exceeds the CU count
-  // (fused: always -- marginal workgroups share the CUs)
-  int grid = dirs * pb->batch;
-  int cap = (grid > 256 || fused) ? 80 * 1024 : 160 * 1024;
+  const int grid = dirs * pb->batch;
+  int cap = grid > 256 ? 80 * 1024 : 160 * 1024;
   cap = pipe_env("LT_PIPE_LDS", cap);
   // mid mode: the marginal waves' regions, and per ring slot the den and
   // numerator rows of its step
@@ -1686,7 +1375,7 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   if (mid) {
     a.mid = 1;
     a.NM = kPipeMidWaves;
-    a.mw_bytes = 4 * (128 + 128 * PN + 64 * NLc);
+    a.mw_bytes = 4 * (256 + 128 * PN + 64 * NLc);
     a.off_mw = off;
     off += al16((long long)a.NM * a.mw_bytes);
     per_slot = so + 4 * (kHS + ((NP + 3) & ~3));
@@ -1706,56 +1395,6 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   const int threads = 64 * (2 + a.NH + (mid ? a.NM : 0));
   if (grid == 0) return LT_OK;
   hipStream_t st = (hipStream_t)stream;
-  if (fused) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    a.fused = 1;
-    a.dW = dW;
-    a.qctr = fctl;
-    a.err = fctl + 2;
-    a.prog = fctl + 4;
-    const int nw = threads / 64;
-    a.FW = std::max(1, pipe_env("LT_FUSED_FW", 4));
-    a.FT = a.FW * nw;
-    a.NB = (a.T + a.FT - 1) / a.FT;
-    a.ntiles = a.NB * a.B;
-    const int NK = 2 * NP;
-    a.mC4 = 64;
-    a.moff_ctl = 0;
-    a.moff_arc = 16;
-    const int NLm = a.J == 17 ? 18 : (a.J == 5 ? 5 : (a.J == 2 ? 2 : 1));
-    a.mNP4 = 64 * PN;
-    a.mFR4 = 64 * NLm + 4;
-    a.moff_wave = al16(16 + 4LL * 128 * PN);
-    a.mwave_bytes = 4 * (128 + 2 * a.mNP4 + 2 * a.mFR4);
-    // the recursions' rows and the arc table are read through one descriptor
-    const char* lo = (const char*)alpha_num;
-    const char* hi = (const char*)alpha_num;
-    for (const void* p : {(const void*)alpha, (const void*)beta, (const void*)beta_num,
-                          (const void*)arcs})
-      if (p) {
-        lo = std::min(lo, (const char*)p);
-        hi = std::max(hi, (const char*)p);
-      }
-    const long long span = (hi - lo) + (long long)pb->batch * pb->max_frames * 4 *
-                                           std::max(C, NP) + 4LL * pb->batch * 2 * NK;
-    if (span >= 0xFFFFFFF0LL) return set_error(LT_EUNSUPPORTED, "pipe: fused workspace span");
-    a.wsbase = lo;
-    lds = std::max(lds, a.moff_wave + nw * a.mwave_bytes);
-    lds = std::max(lds, pipe_env("LT_FUSED_LDS", 0));  // e.g. > 80 KB: one workgroup per CU
-#ifdef LT_DIAG
-    if (const char* tp = lt_impl::tune_str("LT_FUSED_TRACE")) a.trace = (long long*)strtoull(tp, nullptr, 0);
-#endif
-    if (lds > 160 * 1024) return set_error(LT_EUNSUPPORTED, "pipe: fused LDS");
-    // marginal workgroups fill the second workgroup slot of the CUs the
-    // recursions leave; with no slot left they start as recursions retire
-    const int marg = std::max(1, pipe_env("LT_FUSED_MARG", grid < 2 * cus ? 2 * cus - grid : cus));
-    grid += marg;
-    const hipError_t e =
-        hipMemsetAsync(fctl, 0, sizeof(int) * (4 + 4LL * pb->batch), st);
-    if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
-  }
   if (mid) {
     // rows only for the other direction (granules), no checkpoints, no arcs
     a.alpha = a.beta = a.alpha_num = a.beta_num = nullptr;

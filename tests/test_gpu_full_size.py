@@ -252,6 +252,6 @@ def test_design_query_matches_python_mirrors(cuda, B):
   assert (d == nat.DESIGN_FUSED_PIPE) == nat.fused_path(B, T, U, V, n)
   if B == 64:
     assert d == nat.DESIGN_CHUNK
-  if B == 256:  # two recursion workgroups per CU: co-resident on 256 CUs
-    assert d == nat.DESIGN_FUSED_PIPE
+  if B == 256:  # the checkpointing pair (the fused pipe measured level with it)
+    assert d == nat.DESIGN_CHECKPOINTS
 
