@@ -55,8 +55,8 @@ struct MgArgs {
   int B, T, U, FR, do_den, do_num;
   NGram g;
   int F;         // frames per tile (whole-frame tiles), 1 for slice tiles
-  int tpf;       // tiles per frame (1 = whole-frame tiles)
-  int TS;        // elements per slice tile (tpf > 1)
+  int tpf;       // slices per frame (1 = whole-frame tiles)
+  int TS;        // elements per slice (tpf > 1)
   int tiles;     // tiles per utterance
   unsigned mR, mF, mNK;  // magic multipliers for / (V+1), / FR, / NK
   int off_a, off_b, off_an, off_bn, off_arc, off_sub, off_nb, lds_bytes;
@@ -118,7 +118,9 @@ LT_DEVINL void store_unit(unsigned char* p, const float* v) {
 //            size of the slice would cap the workgroups per CU): once the
 //            tile's own stores have completed, the chain heads rewrite their
 //            elements as den - num.
-template <bool BF16>
+// SLICED: frames cut in tpf > 1 slices, one per workgroup (compiled apart, so the whole-frame
+// tiles keep their own register budget)
+template <bool BF16, bool SLICED>
 LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   constexpr int VE = BF16 ? 8 : 4;  // elements per 16-byte unit
   constexpr int ES = BF16 ? 2 : 4;
@@ -129,41 +131,47 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   const int C = g.C, R = g.V + 1, NP = a.U + 1, NK = 2 * NP, FR = a.FR;
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
-  int t0, Fh, e_lo, e_hi;
-  if (a.tpf == 1) {
-    t0 = tile * a.F;
-    Fh = min(a.F, a.T - t0);
-    e_lo = 0;
-    e_hi = FR;
-  } else {
-    t0 = tile / a.tpf;
-    Fh = 1;
-    e_lo = (tile % a.tpf) * a.TS;
-    e_hi = min(FR, e_lo + a.TS);
-  }
-  const int Ew = e_hi - e_lo;
-  const int E = Fh * Ew;
-  const long long base = ((long long)b * a.T + t0) * FR + e_lo;  // tile is contiguous
-  unsigned char* dWb = (unsigned char*)a.dW + base * ES;
-  const unsigned char* Wb = a.W + base * ES;
-  // 16-byte units from the first aligned element h0 of the tile (a trigram
-  // frame is 2 mod 16 bytes long, so most tiles start misaligned); the h0
-  // head elements and the tail go element by element
-  const int h0 = min(E, (int)(((16 - ((base * ES) & 15)) & 15) / ES));
-  const int nunits = (E - h0) / VE;
-  const int ntail = h0 + (E - h0 - nunits * VE);  // head + tail elements
-  auto tail_el = [&](int i) { return i < h0 ? i : i + nunits * VE; };
-  unsigned char* dWu = dWb + (long long)h0 * ES;   // unit u at dWu + 16 u
-  const unsigned char* Wu = Wb + (long long)h0 * ES;
+  // whole-frame tiles: F frames; frame slices: slice tile % tpf of frame
+  // tile / tpf (one workgroup per slice: a workgroup taking a frame's slices
+  // in turn over one load of its rows measured 1.66 ms against 1.40 ms at
+  // cfg5, fewer workgroups in flight)
+  const int t0 = !SLICED ? tile * a.F : tile / a.tpf;
+  const int s0 = !SLICED ? 0 : tile % a.tpf;
+  const int Fh = !SLICED ? min(a.F, a.T - t0) : 1;
   float gb = a.grad ? a.grad[b] : 1.f;
   const float lz = a.do_den ? a.log_z[b] : 0.f;
   const float nm = a.do_num ? a.num[b] : 0.f;
   if ((a.do_num && !__builtin_isfinite(nm)) || (a.do_den && !__builtin_isfinite(lz))) gb = 0.f;
   const int Fl = max(0, min(Fh, nf - t0));  // live frames of the tile
-  if (Fl == 0 || gb == 0.f) {                // padding (lattices.py:775-779) / unreachable
+  // slice sl: elements [e_lo, e_hi) of each of the tile's frames, contiguous
+  // in HBM; 16-byte units from its first aligned element h0 (a trigram frame
+  // is 2 mod 16 bytes long, so most slices start misaligned); the h0 head
+  // elements and the tail go element by element
+  struct Slice {
+    int e_lo, Ew, E, h0, nunits, ntail;
+    long long base;
+  };
+  auto slice = [&](int sl) {
+    Slice x;
+    x.e_lo = !SLICED ? 0 : sl * a.TS;
+    const int e_hi = !SLICED ? FR : min(FR, x.e_lo + a.TS);
+    x.Ew = e_hi - x.e_lo;
+    x.E = Fh * x.Ew;
+    x.base = ((long long)b * a.T + t0) * FR + x.e_lo;
+    x.h0 = min(x.E, (int)(((16 - ((x.base * ES) & 15)) & 15) / ES));
+    x.nunits = (x.E - x.h0) / VE;
+    x.ntail = x.h0 + (x.E - x.h0 - x.nunits * VE);
+    return x;
+  };
+  if (Fl == 0 || gb == 0.f) {  // padding (lattices.py:775-779) / unreachable
     const float z[VE] = {};
-    for (int u = tid; u < nunits; u += nthr) store_unit<BF16>(dWu + (long long)u * 16, z);
-    for (int i = tid; i < ntail; i += nthr) stw<BF16>(a.dW, base + tail_el(i), 0.f);
+    {
+      const Slice x = slice(s0);
+      unsigned char* dWu = (unsigned char*)a.dW + (x.base + x.h0) * ES;
+      for (int u = tid; u < x.nunits; u += nthr) store_unit<BF16>(dWu + (long long)u * 16, z);
+      for (int i = tid; i < x.ntail; i += nthr)
+        stw<BF16>(a.dW, x.base + (i < x.h0 ? i : i + x.nunits * VE), 0.f);
+    }
     return;
   }
   float* A = (float*)(lds + a.off_a);     // [F][C]
@@ -174,15 +182,22 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   int* alink = aoff + NK;
   int* nbt = (int*)(lds + a.off_nb);      // [C] next_base (n >= 2)
   float* Sub = (float*)(lds + a.off_sub); // tpf == 1: [E] numerator marginals per element
-  const bool dense = a.do_num && a.tpf == 1;
+  const bool dense = a.do_num && !SLICED;
 
-  // ---- phase 0
+  // ---- phase 0: the first slice's W as 16-B units into registers; alpha /
+  // beta (+num) rows and the arc table into LDS, once for every slice
+  // (whole-frame tiles also zero a per-element numerator buffer)
   uint4 wq[kMgUnits];
+  auto load_units = [&](const Slice& x) {
+    const unsigned char* Wu = a.W + (x.base + x.h0) * ES;
 #pragma unroll
-  for (int r = 0; r < kMgUnits; ++r) {
-    const int u = tid + r * 256;
-    if (u < nunits) wq[r] = *(const uint4*)(Wu + (long long)u * 16);
-  }
+    for (int r = 0; r < kMgUnits; ++r) {
+      const int u = tid + r * 256;
+      if (u < x.nunits) wq[r] = *(const uint4*)(Wu + (long long)u * 16);
+    }
+  };
+  const Slice x = slice(s0);
+  load_units(x);
   const long long row0 = (long long)b * a.T + t0;
   // every row load in flight at once (a strided load -> LDS loop would wait
   // one memory latency per trip)
@@ -221,19 +236,21 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
     }
   if (dense) {
     float4* S4 = (float4*)Sub;  // the region is padded to 16 bytes
-    for (int e = tid; e < (E + 3) / 4; e += nthr) S4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e = tid; e < (x.E + 3) / 4; e += nthr) S4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
 
+  const bool den = a.do_den;
+  const bool zero_next = g.n == 0, nb_table = g.n >= 2;
   // numerator chains (deterministic: chain order = ascending k): chain i's
-  // head (el >= 0) of frame f, arc k; the heads' W elements come from L2
-  // (the tile was just streamed), gathered for NH rounds at once
-  auto head = [&](int i, int& f, int& k) {
+  // head of frame f, arc k (its element within the slice, or -1 when the
+  // lattice element lies outside it)
+  auto head = [&](const Slice& x, int i, int& f, int& k) {
     f = (int)fdiv((unsigned)i, (unsigned)NK, a.mNK);
     k = i - f * NK;
     const int o = aoff[k];
-    if (!(alink[k] >> 30) || o < e_lo || o >= e_hi) return -1;
-    return f * Ew + o - e_lo;
+    if (!(alink[k] >> 30) || o < x.e_lo || o >= x.e_lo + x.Ew) return -1;
+    return f * x.Ew + o - x.e_lo;
   };
   auto chain = [&](int f, int k, float wv) {
     float sacc = 0.f;
@@ -244,29 +261,6 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
     }
     return gb * sacc;
   };
-  constexpr int NH = 4;
-  const int nI = a.do_num ? Fl * NK : 0;
-  int hel[NH], hf[NH], hk[NH];
-  float hw[NH];
-#pragma unroll
-  for (int r = 0; r < NH; ++r) {
-    const int i = tid + r * 256;
-    hel[r] = i < nI ? head(i, hf[r], hk[r]) : -1;
-    if (hel[r] >= 0) hw[r] = ldw<BF16>(Wb, hel[r]);
-  }
-  if (dense) {  // whole frames: the chains' sums into Sub before the den pass
-#pragma unroll
-    for (int r = 0; r < NH; ++r)
-      if (hel[r] >= 0) Sub[hel[r]] = chain(hf[r], hk[r], hw[r]);
-    for (int i = tid + NH * 256; i < nI; i += nthr) {
-      int f, k;
-      const int el = head(i, f, k);
-      if (el >= 0) Sub[el] = chain(f, k, ldw<BF16>(Wb, el));
-    }
-  }
-  // den marginals of the register units
-  const bool den = a.do_den;
-  const bool zero_next = g.n == 0, nb_table = g.n >= 2;
   // den marginal of frame f's element el (within the frame) with weight w
   auto den_el = [&](int f, int el, float w) {
     const int p = (int)fdiv((unsigned)el, (unsigned)R, a.mR);
@@ -274,105 +268,132 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
     const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
     return gb * lt_exp(A[f * C + p] + w + Bt[f * C + q] - lz);
   };
-  float v[kMgUnits][VE];
+  constexpr int NH = 4;
+  const int nI = a.do_num ? Fl * NK : 0;
+  {
+    const unsigned char* Wb = a.W + x.base * ES;
+    unsigned char* dWu = (unsigned char*)a.dW + (x.base + x.h0) * ES;  // unit u at dWu + 16 u
+    auto tail_el = [&](int i) { return i < x.h0 ? i : i + x.nunits * VE; };
+    // the chain heads' W elements come from L2 (the slice was just
+    // streamed), gathered for NH rounds at once
+    int hel[NH], hf[NH], hk[NH];
+    float hw[NH];
 #pragma unroll
-  for (int r = 0; r < kMgUnits; ++r) {
-    const int u = tid + r * 256;
+    for (int r = 0; r < NH; ++r) {
+      const int i = tid + r * 256;
+      hel[r] = i < nI ? head(x, i, hf[r], hk[r]) : -1;
+      if (hel[r] >= 0) hw[r] = ldw<BF16>(Wb, hel[r]);
+    }
+    if (dense) {  // whole frames: the chains' sums into Sub before the den pass
 #pragma unroll
-    for (int c = 0; c < VE; ++c) v[r][c] = 0.f;
-    if (u < nunits && den) {
-      float w[VE];
-      unpack_unit<BF16>(wq[r], w);
-      const int e0 = h0 + u * VE;
-      int f = a.tpf == 1 ? (int)fdiv((unsigned)e0, (unsigned)FR, a.mF) : 0;
-      const int el0 = e_lo + e0 - f * Ew;
-      int p = (int)fdiv((unsigned)el0, (unsigned)R, a.mR);
-      int y = el0 - p * R;
-      if (R >= VE) {
-        // a unit spans at most two source rows (p0 and the next, possibly
-        // in the next frame of the tile): their alpha and next-state bases
-        // are read once, every element is branch-free
-        const int p1r = p + 1;
-        const bool fw = p1r == C;
-        const int p1 = fw ? 0 : p1r, f1 = fw ? f + 1 : f;
-        const float a0v = A[f * C + p], a1v = f1 < Fl ? A[f1 * C + p1] : 0.f;
-        const int nb0 = zero_next ? 0 : (nb_table ? nbt[p] : 0);
-        const int nb1 = zero_next ? 0 : (nb_table ? nbt[p1] : 0);
-        const float lzc = lz;
+      for (int r = 0; r < NH; ++r)
+        if (hel[r] >= 0) Sub[hel[r]] = chain(hf[r], hk[r], hw[r]);
+      for (int i = tid + NH * 256; i < nI; i += nthr) {
+        int f, k;
+        const int el = head(x, i, f, k);
+        if (el >= 0) Sub[el] = chain(f, k, ldw<BF16>(Wb, el));
+      }
+    }
+    // den marginals of the register units
+    float v[kMgUnits][VE];
 #pragma unroll
-        for (int c = 0; c < VE; ++c) {
-          const int yc = y + c;
-          const bool w2 = yc >= R;
-          const int yy = w2 ? yc - R : yc;
-          const int pp = w2 ? p1 : p, ff = w2 ? f1 : f;
-          const int q = yy == 0 ? pp : (w2 ? nb1 : nb0) + yy;
-          const float av = w2 ? a1v : a0v;
-          const float x = gb * lt_exp(av + w[c] + Bt[ff * C + q] - lzc);
-          v[r][c] = ff < Fl ? x : 0.f;
-        }
-      } else {
+    for (int r = 0; r < kMgUnits; ++r) {
+      const int u = tid + r * 256;
 #pragma unroll
-        for (int c = 0; c < VE; ++c) {
-          if (f < Fl) {
-            const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
-            v[r][c] = gb * lt_exp(A[f * C + p] + w[c] + Bt[f * C + q] - lz);
+      for (int c = 0; c < VE; ++c) v[r][c] = 0.f;
+      if (u < x.nunits && den) {
+        float w[VE];
+        unpack_unit<BF16>(wq[r], w);
+        const int e0 = x.h0 + u * VE;
+        int f = !SLICED ? (int)fdiv((unsigned)e0, (unsigned)FR, a.mF) : 0;
+        const int el0 = x.e_lo + e0 - f * x.Ew;
+        int p = (int)fdiv((unsigned)el0, (unsigned)R, a.mR);
+        int y = el0 - p * R;
+        if (R >= VE) {
+          // a unit spans at most two source rows (p0 and the next, possibly
+          // in the next frame of the tile): their alpha and next-state bases
+          // are read once, every element is branch-free
+          const int p1r = p + 1;
+          const bool fw = p1r == C;
+          const int p1 = fw ? 0 : p1r, f1 = fw ? f + 1 : f;
+          const float a0v = A[f * C + p], a1v = f1 < Fl ? A[f1 * C + p1] : 0.f;
+          const int nb0 = nb_table ? nbt[p] : 0;
+          const int nb1 = nb_table ? nbt[p1] : 0;
+#pragma unroll
+          for (int c = 0; c < VE; ++c) {
+            const int yc = y + c;
+            const bool w2 = yc >= R;
+            const int yy = w2 ? yc - R : yc;
+            const int pp = w2 ? p1 : p, ff = w2 ? f1 : f;
+            const int q = yy == 0 ? pp : (zero_next ? 0 : (w2 ? nb1 : nb0) + yy);
+            const float av = w2 ? a1v : a0v;
+            const float xv = gb * lt_exp(av + w[c] + Bt[ff * C + q] - lz);
+            v[r][c] = ff < Fl ? xv : 0.f;
           }
-          if (++y == R) {
-            y = 0;
-            if (++p == C) { p = 0; ++f; }
+        } else {
+#pragma unroll
+          for (int c = 0; c < VE; ++c) {
+            if (f < Fl) {
+              const int q = y == 0 ? p : (zero_next ? 0 : (nb_table ? nbt[p] : 0) + y);
+              v[r][c] = gb * lt_exp(A[f * C + p] + w[c] + Bt[f * C + q] - lz);
+            }
+            if (++y == R) {
+              y = 0;
+              if (++p == C) { p = 0; ++f; }
+            }
           }
         }
       }
     }
-  }
-  if (dense) __syncthreads();
+    if (dense) __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kMgUnits; ++r) {
-    const int u = tid + r * 256;
-    if (u < nunits) {
-      if (dense) {
+    for (int r = 0; r < kMgUnits; ++r) {
+      const int u = tid + r * 256;
+      if (u < x.nunits) {
+        if (dense) {
 #pragma unroll
-        for (int c = 0; c < VE; ++c) v[r][c] -= Sub[h0 + u * VE + c];
+          for (int c = 0; c < VE; ++c) v[r][c] -= Sub[x.h0 + u * VE + c];
+        }
+        store_unit<BF16>(dWu + (long long)u * 16, v[r]);
       }
-      store_unit<BF16>(dWu + (long long)u * 16, v[r]);
     }
-  }
-  // the head before the first 16-byte boundary and the tail: element by element
-  for (int i = tid; i < ntail; i += nthr) {
-    const int e = tail_el(i);
-    const int f = a.tpf == 1 ? (int)fdiv((unsigned)e, (unsigned)FR, a.mF) : 0;
-    float x = 0.f;
-    if (f < Fl) {
-      if (den) x = den_el(f, e_lo + e - f * Ew, ldw<BF16>(Wb, e));
-      if (dense) x -= Sub[e];
+    // the head before the first 16-byte boundary and the tail: element by element
+    for (int i = tid; i < x.ntail; i += nthr) {
+      const int e = tail_el(i);
+      const int f = !SLICED ? (int)fdiv((unsigned)e, (unsigned)FR, a.mF) : 0;
+      float xv = 0.f;
+      if (f < Fl) {
+        if (den) xv = den_el(f, x.e_lo + e - f * x.Ew, ldw<BF16>(Wb, e));
+        if (dense) xv -= Sub[e];
+      }
+      stw<BF16>(a.dW, x.base + e, xv);
     }
-    stw<BF16>(a.dW, base + e, x);
-  }
-  if (!a.do_num || dense) return;
+    if (!a.do_num || dense) return;
 
-  // ---- phase 2 (frame slices): the chain heads rewrite their elements as
-  // den - num once the tile's own stores have completed in every wave (same
-  // workgroup, same address, in order)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  auto rewrite = [&](int el, int f, int k, float wv) {
-    const float d = den ? den_el(f, el - f * Ew + e_lo, wv) : 0.f;
-    stw<BF16>(a.dW, base + el, d - chain(f, k, wv));
-  };
+    // ---- phase 2 (frame slices): the chain heads rewrite their elements as
+    // den - num once the slice's own stores have completed in every wave
+    // (same workgroup, same address, in order)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    auto rewrite = [&](int el, int f, int k, float wv) {
+      const float d = den ? den_el(f, el - f * x.Ew + x.e_lo, wv) : 0.f;
+      stw<BF16>(a.dW, x.base + el, d - chain(f, k, wv));
+    };
 #pragma unroll
-  for (int r = 0; r < NH; ++r)
-    if (hel[r] >= 0) rewrite(hel[r], hf[r], hk[r], hw[r]);
-  for (int i = tid + NH * 256; i < nI; i += nthr) {
-    int f, k;
-    const int el = head(i, f, k);
-    if (el >= 0) rewrite(el, f, k, ldw<BF16>(Wb, el));
+    for (int r = 0; r < NH; ++r)
+      if (hel[r] >= 0) rewrite(hel[r], hf[r], hk[r], hw[r]);
+    for (int i = tid + NH * 256; i < nI; i += nthr) {
+      int f, k;
+      const int el = head(x, i, f, k);
+      if (el >= 0) rewrite(el, f, k, ldw<BF16>(Wb, el));
+    }
   }
 }
 
-template <bool BF16>
+template <bool BF16, bool SLICED>
 __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  marg_tile<BF16>(a, (int)blockIdx.x, lds);
+  marg_tile<BF16, SLICED>(a, (int)blockIdx.x, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -772,8 +793,9 @@ __global__ __launch_bounds__(256) void handoff_check_kernel(const int* err, floa
 
 int cu_count() {
   int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
   return cus;
 }
 
@@ -1074,8 +1096,11 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
     m.arcs = arcs; m.log_z = log_z; m.num = num; m.grad = grad; m.dW = dW;
     if (grid == 0) return LT_OK;
     hipStream_t st = (hipStream_t)stream;
-    const void* k = pb->weight_dtype == LT_DTYPE_BF16 ? (const void*)marg_kernel<true>
-                                                       : (const void*)marg_kernel<false>;
+    const bool bf = pb->weight_dtype == LT_DTYPE_BF16, sliced = m.tpf > 1;
+    const void* k = bf ? (sliced ? (const void*)marg_kernel<true, true>
+                                 : (const void*)marg_kernel<true, false>)
+                       : (sliced ? (const void*)marg_kernel<false, true>
+                                 : (const void*)marg_kernel<false, false>);
     if (m.lds_bytes > 64 * 1024 &&
         (rc = hip_check(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             m.lds_bytes), "marginal LDS")))

@@ -207,6 +207,178 @@ __global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
   }
 }
 
+// Two-wave variant (vit_split_kernel, the default): the alpha chain and the
+// backpointers on two waves of one workgroup (two SIMDs). Wave 0 runs the
+// chain alone -- weights, alpha, the max3 tree, the LDS-DMA ring -- and
+// publishes alpha_{t+1} with an LDS progress word; wave 1 follows, re-forms
+// frame t's terms from the same alpha_t and weights (the same additions, so
+// the same floats), takes the first term equal to alpha_{t+1}[q] and stores
+// the backpointer byte. The ring (kSSlots frames) and the alpha rows
+// (kSAl) give the backpointer wave kSSlots - kSAhead - 1 frames of slack;
+// the chain waits on its progress word only when it would overwrite a frame
+// or row that wave has not passed.
+constexpr int kSAhead = 3;
+constexpr int kSSlots = 8;
+constexpr int kSAl = 8;
+
+template <bool BF16, bool FULL>
+__global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_al[kSAl][40];
+  __shared__ __attribute__((aligned(16))) unsigned char s_ring[kSSlots][5 * 1024];
+  __shared__ int s_prog[2];  // [0] chain: alpha rows published; [1] backpointer frames done
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, h = lane >> 5;
+  const int V = FULL ? 32 : a.V, R = FULL ? 33 : a.R, C = V + 1;
+  constexpr int es = BF16 ? 2 : 4;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int q = j + 1;
+  const bool live = j < V;
+  const int p0 = kHalf * h;
+  const int vb = (p0 * R + min(q, V)) * es;
+  const int vself = min(q, V) * R * es;
+  const long long fbytes = (long long)C * R * es;
+  const long long goff0 = (long long)b * a.T * fbytes;
+  auto fclamp = [&](int t) { return min(t, max(nf - 1, 0)); };
+  // alpha_0: the start state (MaxTropical one = 0), every other state zero
+  if (tid < 40) s_al[0][tid] = tid == 0 ? 0.f : -kInf;
+  if (tid < 2) s_prog[tid] = 0;
+  __syncthreads();
+  auto frame = [&](int t) {
+    return &s_ring[t % kSSlots][0] + ((goff0 + (long long)fclamp(t) * fbytes) & 15);
+  };
+  // frame t's terms x (the lane's sources) and xs (the blank self loop)
+  auto terms = [&](int t, float* x, float& xs, float& w00) {
+    const unsigned char* fr = frame(t);
+    float w[kHalf];
+#pragma unroll
+    for (int m = 0; m < kHalf; ++m) w[m] = vlds<BF16>(fr, vb + m * (FULL ? 33 : R) * es);
+    const float self = vlds<BF16>(fr, vself);
+    w00 = vlds<BF16>(fr, 0);
+    const float* acur = s_al[t % kSAl];
+    float al[20];
+#pragma unroll
+    for (int g = 0; g < 5; ++g) {
+      const float4 v = *(const float4*)(acur + 20 * h + 4 * g);
+      al[4 * g + 0] = v.x; al[4 * g + 1] = v.y; al[4 * g + 2] = v.z; al[4 * g + 3] = v.w;
+    }
+    const float aq = acur[aslot(min(q, V))];
+#pragma unroll
+    for (int m = 0; m < kHalf; ++m) {
+      const bool ok = FULL ? (m < kHalf - 1 || h == 0) : p0 + m <= V;
+      x[m] = ok ? al[m] + w[m] : -kInf;
+    }
+    xs = aq + self;
+  };
+  auto wait_prog = [&](int k, int want) {
+    for (int n = 0; n < (1 << 26); ++n) {
+      const int v = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&s_prog[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (v >= want) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  auto publish = [&](int k, int v) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's LDS accesses done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(&s_prog[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  if (wave == 0) {
+    // ---- the chain
+    const int ni = (int)(((fbytes + 30) / 16 + 63) / 64);
+    auto issue = [&](int t) {  // frame t (clamped) -> slot t % kSSlots
+      const long long off = goff0 + (long long)fclamp(t) * fbytes;
+      const long long a0 = off & ~15LL;
+      const int n16 = (int)((off + fbytes - a0 + 15) >> 4);
+      const unsigned dst = lds_base_addr(&s_ring[t % kSSlots][0]);
+      for (int i = 0; i < ni; ++i) {
+        int g = lane + 64 * i;
+        g = g < n16 ? g : n16 - 1;
+        glds16(a.W + a0 + 16LL * g, dst + 1024u * i);
+      }
+    };
+    // every step issues one frame (clamped past the end), so the ring's
+    // vmcnt counts stay uniform to the last frame (prefetching frame t + 1's
+    // weights into registers a step early measured slower: 0.869 against
+    // 0.846 ms at cfg4)
+    if (nf > 0)
+      for (int d = 0; d < kSAhead; ++d) issue(d);
+    float a0 = 0.f;
+    int bseen = 0;  // the backpointer wave's progress as last read
+    for (int t = 0; t < nf; ++t) {
+      wait_vmcnt((kSAhead - 1) * ni);  // frame t landed (the only VMEM ops are the ring's)
+      float x[kHalf], xs, w00;
+      terms(t, x, xs, w00);
+      float mx = max3_raw(h ? x[16] : xs, x[0], x[1]);
+      mx = max3_raw(mx, x[2], x[3]);
+      const float m1 = max3_raw(x[4], x[5], x[6]);
+      const float m2 = max3_raw(x[7], x[8], x[9]);
+      const float m3 = max3_raw(x[10], x[11], x[12]);
+      const float m4 = max3_raw(x[13], x[14], x[15]);
+      mx = max3_raw(mx, m1, m2);
+      mx = max3_raw(mx, m3, m4);
+      if (h == 0) mx = fmaxf(mx, x[16]);
+      auto pv = __builtin_amdgcn_permlane32_swap(__float_as_int(mx), __float_as_int(mx), false, false);
+      const float r = fmaxf(mx, __int_as_float(h ? pv[0] : pv[1]));
+      float* anxt = s_al[(t + 1) % kSAl];
+      if (h == 0 && live) anxt[aslot(q)] = r;
+      a0 += w00;
+      if (lane == 32) anxt[0] = a0;
+      publish(0, t + 1);
+      // the slot of frame t + kSAhead held frame t + kSAhead - kSSlots, and
+      // the next step overwrites the alpha row alpha_{t + 2 - kSAl}: the
+      // backpointer wave must be past both (every step, the last ones too)
+      const int want = max(t + kSAhead - kSSlots + 1, t + 3 - kSAl);
+      if (bseen < want) {  // re-read only when the last value seen is short
+        wait_prog(1, want);
+        bseen = __builtin_amdgcn_readfirstlane(s_prog[1]);
+      }
+      issue(t + kSAhead);
+    }
+    wait_vmcnt(0);
+    // the distance: (+)_q alpha_T[q] in MaxTropical, the first maximum
+    const float* af = s_al[nf % kSAl];
+    float r = lane < C ? af[aslot(lane)] : -kInf;
+    int ri = lane < C ? lane : 0x7fffffff;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const float pv = __shfl_xor(r, s);
+      const int pi = __shfl_xor(ri, s);
+      if (pv > r || (pv == r && pi < ri)) { r = pv; ri = pi; }
+    }
+    if (lane == 0) {
+      a.dist[b] = r;
+      a.qstar[b] = ri;
+    }
+  } else {
+    // ---- the backpointers: the first term equal to alpha_{t+1}[q]
+    // (group_reduce's first-maximum rule), the lower half first
+    const __amdgpu_buffer_rsrc_t bpr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.bp + (long long)b * a.T * C), (short)0,
+                                          a.T * C, 0x00020000);
+    const int ib = h ? 18 : 1;  // term index of x[0]
+    for (int t = 0; t < nf; ++t) {
+      wait_prog(0, t + 1);
+      float x[kHalf], xs, w00;
+      terms(t, x, xs, w00);
+      const float rq = s_al[(t + 1) % kSAl][aslot(min(q, V))];
+      int ri = 99;
+#pragma unroll
+      for (int m = 16; m >= 0; --m) ri = x[m] == rq ? ib + m : ri;
+      if (h == 0) ri = xs == rq ? 0 : ri;
+      auto pi = __builtin_amdgcn_permlane32_swap(ri, ri, false, false);
+      const int rlo = h ? pi[0] : ri, rhi = h ? ri : pi[1];
+      const int bpv = lane == 32 ? 0 : (rlo < 99 ? rlo : rhi);
+      if ((h == 0 && live) || lane == 32)
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bpv, bpr, lane == 32 ? 0 : q, t * C, 0);
+      publish(1, t + 1);
+      (void)w00;
+    }
+  }
+}
+
 // Backtrace of the bigram backpointers in segments (one workgroup per
 // utterance, the utterance's backpointers staged in LDS): every segment of S
 // frames walks back from each of its C possible end states at once (the
@@ -340,12 +512,21 @@ int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, 
 #endif
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const bool full = a.V == 32;
-  const void* k = full ? (bf16 ? (const void*)vit_bigram_kernel<true, true>
-                               : (const void*)vit_bigram_kernel<false, true>)
-                       : (bf16 ? (const void*)vit_bigram_kernel<true, false>
-                               : (const void*)vit_bigram_kernel<false, false>);
+#ifndef LT_VIT_SPLIT
+#define LT_VIT_SPLIT 1
+#endif
+  const void* k = LT_VIT_SPLIT
+      ? (full ? (bf16 ? (const void*)vit_split_kernel<true, true>
+                      : (const void*)vit_split_kernel<false, true>)
+              : (bf16 ? (const void*)vit_split_kernel<true, false>
+                      : (const void*)vit_split_kernel<false, false>))
+      : (full ? (bf16 ? (const void*)vit_bigram_kernel<true, true>
+                      : (const void*)vit_bigram_kernel<false, true>)
+              : (bf16 ? (const void*)vit_bigram_kernel<true, false>
+                      : (const void*)vit_bigram_kernel<false, false>));
   void* args[] = {(void*)&a};
-  hipError_t e = hipLaunchKernel(k, dim3(a.B), dim3(64), args, 0, (hipStream_t)stream);
+  hipError_t e = hipLaunchKernel(k, dim3(a.B), dim3(LT_VIT_SPLIT ? 128 : 64), args, 0,
+                                 (hipStream_t)stream);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;
