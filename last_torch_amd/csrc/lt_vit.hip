@@ -6,7 +6,8 @@
 // first-maximum rule: semirings.py MaxTropical, term order of
 // contexts.py:226-229 with the blank self loop first).
 //
-// One wave per utterance, the whole chain in registers and LDS:
+// One workgroup of two waves per utterance, the whole chain in registers and
+// LDS (vit_split_kernel):
 //   lane (j, h): destination q = j + 1 (a core state), half h of its in-arcs:
 //   h = 0 the blank self loop (term 0) and sources p = 0..16 (terms 1..17),
 //   h = 1 sources p = 17..32 (terms 18..33); the halves meet through one
@@ -15,9 +16,8 @@
 //   frame); the frames stream into an LDS ring three frames ahead by
 //   LDS-DMA (5 contiguous 1 KiB wave instructions a frame, counted vmcnt
 //   waits) and each lane reads its 19 weights from LDS beside alpha. The
-//   alpha chain takes the maximum by a max3 tree; the backpointer (the
-//   first term equal to it) is formed one step later, from the kept terms,
-//   while the next frame's LDS reads are in flight.
+//   alpha chain takes the maximum by a max3 tree on wave 0; wave 1 forms the
+//   backpointers (the first term equal to the maximum) behind it.
 // Backpointers: one byte per (frame, state), the term index, as the generic
 // kernel writes them (backtrace_kernel reads both).
 #include "lt_kernels.h"
@@ -46,169 +46,15 @@ LT_DEVINL float max3_raw(float x, float y, float z) {
   return r;
 }
 
-// the frames stream through an LDS ring kAhead frames ahead (kSlots slots:
-// the frame in use and the kAhead in flight)
-constexpr int kAhead = 3;
-constexpr int kSlots = kAhead + 1;
-
+// one weight of an LDS-staged frame (bf16 widened)
 template <bool BF16>
 LT_DEVINL float vlds(const unsigned char* fr, int off) {
   if constexpr (BF16) return __uint_as_float((unsigned)*(const unsigned short*)(fr + off) << 16);
   else return *(const float*)(fr + off);
 }
 
-struct VitFrame {
-  float w[kHalf];  // W[p][q] for the lane's sources
-  float self;      // W[q][0]
-  float w00;       // W[0][0]
-};
-
-template <bool BF16, bool FULL>
-__global__ __launch_bounds__(64) void vit_bigram_kernel(const VitArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_al[2][40];
-  __shared__ __attribute__((aligned(16))) unsigned char s_ring[kSlots][5 * 1024];
-  const int b = blockIdx.x, lane = threadIdx.x;
-  const int j = lane & 31, h = lane >> 5;
-  const int V = FULL ? 32 : a.V, R = FULL ? 33 : a.R, C = V + 1;
-  constexpr int es = BF16 ? 2 : 4;
-  int nf = a.nfr[b];
-  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
-  const int q = j + 1;
-  const bool live = j < V;  // a core destination
-  // the lane's sources p = 17 h + m (p <= V)
-  const int p0 = kHalf * h;
-  const int vb = (p0 * R + min(q, V)) * es;
-  const int vself = min(q, V) * R * es;
-  const long long fbytes = (long long)C * R * es;
-  // backpointer stores through a buffer resource too: a per-frame 64-bit
-  // address would make the compiler drain vmcnt when it recycles the pair
-  const __amdgpu_buffer_rsrc_t bpr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.bp + (long long)b * a.T * C), (short)0,
-                                        a.T * C, 0x00020000);
-  // alpha_0: the start state (MaxTropical one = 0), every other state zero
-  if (lane < 40) s_al[0][lane] = lane == 0 ? 0.f : -kInf;
-  float a0 = 0.f;  // alpha[0] (only its blank self loop reaches it)
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  // frames stream into an LDS ring by LDS-DMA kAhead frames ahead (ni
-  // contiguous 1 KiB wave instructions a frame instead of 19 column loads)
-  const int ni = (int)(((fbytes + 30) / 16 + 63) / 64);
-  const long long goff0 = (long long)b * a.T * fbytes;
-  auto fclamp = [&](int t) { return min(t, max(nf - 1, 0)); };
-  auto issue = [&](int t) {  // frame t (clamped) -> slot t % kSlots
-    const long long off = goff0 + (long long)fclamp(t) * fbytes;
-    const long long a0 = off & ~15LL;
-    const int n16 = (int)((off + fbytes - a0 + 15) >> 4);
-    const unsigned dst = lds_base_addr(&s_ring[t % kSlots][0]);
-    for (int i = 0; i < ni; ++i) {
-      int g = lane + 64 * i;
-      g = g < n16 ? g : n16 - 1;
-      glds16(a.W + a0 + 16LL * g, dst + 1024u * i);
-    }
-  };
-  // frame t's DMA has landed: ring issues and one backpointer store a step,
-  // in issue order (vmcnt counts both, in order)
-  // (frame t - 1's store goes out in step t, before that step's ring issue)
-  auto wait_frame = [&](int t) { wait_vmcnt((kAhead - 1) * ni + min(max(t - 1, 0), kAhead - 1)); };
-  if (nf > 0) {
-    for (int d = 0; d < kAhead; ++d) issue(d);
-  }
-  const int ib = h ? 18 : 1;  // term index of x[0]
-  // the previous frame's terms and value: its backpointer is formed in the
-  // next step while that step's LDS reads are in flight (off the chain)
-  float xq[kHalf], xsq = 0.f, rq = 0.f;
-#pragma unroll
-  for (int m = 0; m < kHalf; ++m) xq[m] = 0.f;
-  auto emit_bp = [&](int tb) {
-    // the first term equal to the maximum (group_reduce's first-maximum
-    // rule), the lower half first
-    int ri = 99;
-#pragma unroll
-    for (int m = 16; m >= 0; --m) ri = xq[m] == rq ? ib + m : ri;
-    if (h == 0) ri = xsq == rq ? 0 : ri;
-    auto pi = __builtin_amdgcn_permlane32_swap(ri, ri, false, false);
-    const int rlo = h ? pi[0] : ri, rhi = h ? ri : pi[1];
-    const int bpv = lane == 32 ? 0 : (rlo < 99 ? rlo : rhi);
-    if ((h == 0 && live) || lane == 32)
-      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bpv, bpr, lane == 32 ? 0 : q, tb * C, 0);
-  };
-  auto step = [&](int t) {
-    if (t >= nf) return;  // the last round's spare steps
-    const float* acur = s_al[t & 1];
-    float* anxt = s_al[(t + 1) & 1];
-    wait_frame(t);
-    VitFrame F;
-    {
-      const unsigned char* fr =
-          &s_ring[t % kSlots][0] + ((goff0 + (long long)fclamp(t) * fbytes) & 15);
-#pragma unroll
-      for (int m = 0; m < kHalf; ++m) F.w[m] = vlds<BF16>(fr, vb + m * (FULL ? 33 : R) * es);
-      F.self = vlds<BF16>(fr, vself);
-      F.w00 = vlds<BF16>(fr, 0);
-    }
-    // the sources' alpha: five b128 reads of the lane's half
-    float al[20];
-#pragma unroll
-    for (int g = 0; g < 5; ++g) {
-      const float4 v = *(const float4*)(acur + 20 * h + 4 * g);
-      al[4 * g + 0] = v.x; al[4 * g + 1] = v.y; al[4 * g + 2] = v.z; al[4 * g + 3] = v.w;
-    }
-    const float aq = acur[aslot(min(q, V))];
-    if (t > 0) emit_bp(t - 1);
-    float x[kHalf];
-#pragma unroll
-    for (int m = 0; m < kHalf; ++m) {
-      const bool ok = FULL ? (m < kHalf - 1 || h == 0) : p0 + m <= V;  // FULL: only p = 33 is out
-      x[m] = ok ? al[m] + F.w[m] : -kInf;
-    }
-    const float xs = aq + F.self;
-    const float w00 = F.w00;
-    // the value: a max3 tree over the lane's terms, the halves by one
-    // permlane32 swap (the alpha chain waits on nothing else)
-    float mx = max3_raw(h ? x[16] : xs, x[0], x[1]);
-    mx = max3_raw(mx, x[2], x[3]);
-    const float m1 = max3_raw(x[4], x[5], x[6]);
-    const float m2 = max3_raw(x[7], x[8], x[9]);
-    const float m3 = max3_raw(x[10], x[11], x[12]);
-    const float m4 = max3_raw(x[13], x[14], x[15]);
-    mx = max3_raw(mx, m1, m2);
-    mx = max3_raw(mx, m3, m4);
-    if (h == 0) mx = fmaxf(mx, x[16]);
-    auto pv = __builtin_amdgcn_permlane32_swap(__float_as_int(mx), __float_as_int(mx), false, false);
-    // permlane32_swap hands the upper lanes the lower half's value in [0]
-    // and the lower lanes the upper half's in [1]
-    const float r = fmaxf(mx, __int_as_float(h ? pv[0] : pv[1]));
-    if (h == 0 && live) anxt[aslot(q)] = r;
-    a0 += w00;
-    if (lane == 32) anxt[0] = a0;
-    if (!LT_ABL(a, 1)) issue(t + kAhead);
-#pragma unroll
-    for (int m = 0; m < kHalf; ++m) xq[m] = x[m];
-    xsq = xs;
-    rq = r;
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-  };
-  for (int t = 0; t < nf; ++t) step(t);
-  if (nf > 0) emit_bp(nf - 1);
-  // the distance: (+)_q alpha_T[q] in MaxTropical, the first maximum
-  const float* af = s_al[nf & 1];
-  float r = lane < C ? af[aslot(lane)] : -kInf;
-  int ri = lane < C ? lane : 0x7fffffff;
-#pragma unroll
-  for (int s = 1; s < 64; s <<= 1) {
-    const float pv = __shfl_xor(r, s);
-    const int pi = __shfl_xor(ri, s);
-    if (pv > r || (pv == r && pi < ri)) { r = pv; ri = pi; }
-  }
-  if (lane == 0) {
-    a.dist[b] = r;
-    a.qstar[b] = ri;
-  }
-}
-
-// Two-wave variant (vit_split_kernel, the default): the alpha chain and the
-// backpointers on two waves of one workgroup (two SIMDs). Wave 0 runs the
+// The alpha chain and the backpointers on two waves of one workgroup (two
+// SIMDs; cfg4 0.848 ms against 0.882 ms with both on one wave, round 3). Wave 0 runs the
 // chain alone -- weights, alpha, the max3 tree, the LDS-DMA ring -- and
 // publishes alpha_{t+1} with an LDS progress word; wave 1 follows, re-forms
 // frame t's terms from the same alpha_t and weights (the same additions, so
@@ -512,21 +358,12 @@ int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, 
 #endif
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const bool full = a.V == 32;
-#ifndef LT_VIT_SPLIT
-#define LT_VIT_SPLIT 1
-#endif
-  const void* k = LT_VIT_SPLIT
-      ? (full ? (bf16 ? (const void*)vit_split_kernel<true, true>
-                      : (const void*)vit_split_kernel<false, true>)
-              : (bf16 ? (const void*)vit_split_kernel<true, false>
-                      : (const void*)vit_split_kernel<false, false>))
-      : (full ? (bf16 ? (const void*)vit_bigram_kernel<true, true>
-                      : (const void*)vit_bigram_kernel<false, true>)
-              : (bf16 ? (const void*)vit_bigram_kernel<true, false>
-                      : (const void*)vit_bigram_kernel<false, false>));
+  const void* k = full ? (bf16 ? (const void*)vit_split_kernel<true, true>
+                               : (const void*)vit_split_kernel<false, true>)
+                       : (bf16 ? (const void*)vit_split_kernel<true, false>
+                               : (const void*)vit_split_kernel<false, false>);
   void* args[] = {(void*)&a};
-  hipError_t e = hipLaunchKernel(k, dim3(a.B), dim3(LT_VIT_SPLIT ? 128 : 64), args, 0,
-                                 (hipStream_t)stream);
+  hipError_t e = hipLaunchKernel(k, dim3(a.B), dim3(128), args, 0, (hipStream_t)stream);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;
