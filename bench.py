@@ -271,7 +271,7 @@ def cpu_ref(T, U, V, n, sample_utts):
   }
 
 
-def cpu_twin(T, U, V, n, C, sample_utts):
+def cpu_twin(T, U, V, n, C, sample_utts, min_seconds=10.0):
   """The C++ host twin of the library (liblt_lattice_cpu.so,
   include/lt_lattice_cpu.h: the same lattice, loss + dW, fp32, utterances
   over a host thread pool) on the same workload shape, timed on this box's
@@ -285,18 +285,22 @@ def cpu_twin(T, U, V, n, C, sample_utts):
   lab = torch.randint(1, V + 1, (sample_utts, U), generator=g, dtype=torch.int32)
   nl = torch.full([sample_utts], U, dtype=torch.int32)
   _native_cpu.loss_grad(W[:threads], nf[:threads], lab[:threads], nl[:threads], V, n)  # warm
+  # passes over the sample until about 10 s of host work (16 threads x 10 s)
+  passes, dt = 0, 0.0
   t0 = time.perf_counter()
-  _native_cpu.loss_grad(W, nf, lab, nl, V, n)
-  dt = time.perf_counter() - t0
+  while passes < 1 or (dt < min_seconds and passes < 1000):
+    _native_cpu.loss_grad(W, nf, lab, nl, V, n)
+    passes += 1
+    dt = time.perf_counter() - t0
   return {
-      'value': sample_utts * T * U * C / dt,
+      'value': passes * sample_utts * T * U * C / dt,
       'unit': 'cells/s',
       'cores': threads,
       'kind': 'port',
       'affinity_cores': len(os.sched_getaffinity(0)),
       'sample': (f'C++ host twin (last_torch_amd/liblt_lattice_cpu.so, lt_cpu_loss_grad: loss + '
-                 f'dW, fp32) on {sample_utts} utterances of T={T} U={U} V={V} n={n}: '
-                 f'{dt:.2f} s on {threads} threads'),
+                 f'dW, fp32) on {sample_utts} utterances of T={T} U={U} V={V} n={n}, '
+                 f'{passes} passes: {dt:.2f} s on {threads} threads'),
   }
 
 
