@@ -31,7 +31,8 @@ struct VitArgs {
   int* qstar;              // [B] best final state
   float* dist;             // [B] the shortest distance (MaxTropical)
   int B, T, V, C, R;
-  int dbg;                 // diagnostic builds (LT_DIAG) only: 1 = no weight reloads
+  int dbg;                 // diagnostic builds (LT_DIAG) only
+  long long* stamps;       // diagnostic builds: [kVitStampSteps][4] s_memtime of block 0's chain
 };
 
 constexpr int kHalf = 17;  // sources per half (p < 17 in h = 0)
@@ -65,6 +66,7 @@ LT_DEVINL float vlds(const unsigned char* fr, int off) {
 // or row that wave has not passed.
 constexpr int kSAhead = 3;
 constexpr int kSSlots = 8;
+[[maybe_unused]] constexpr int kVitStampSteps = 128;  // diagnostic stamps (LT_DIAG)
 constexpr int kSAl = 8;
 
 template <bool BF16, bool FULL>
@@ -72,6 +74,14 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
   __shared__ __attribute__((aligned(16))) float s_al[kSAl][40];
   __shared__ __attribute__((aligned(16))) unsigned char s_ring[kSSlots][5 * 1024];
   __shared__ int s_prog[2];  // [0] chain: alpha rows published; [1] backpointer frames done
+#ifdef LT_DIAG
+  __shared__ long long s_st[kVitStampSteps][4];
+  const bool stamp = a.stamps != nullptr && blockIdx.x == 0;
+#define VSTAMP(t, k) \
+  do { if (stamp && (t) < kVitStampSteps && lane == 0) s_st[t][k] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define VSTAMP(t, k) do {} while (0)
+#endif
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, h = lane >> 5;
@@ -131,32 +141,43 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(&s_prog[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
+  const int ni = (int)(((fbytes + 30) / 16 + 63) / 64);
+  auto issue = [&](int t) {  // frame t (clamped) -> slot t % kSSlots
+    const long long off = goff0 + (long long)fclamp(t) * fbytes;
+    const long long a0 = off & ~15LL;
+    const int n16 = (int)((off + fbytes - a0 + 15) >> 4);
+    const unsigned dst = lds_base_addr(&s_ring[t % kSSlots][0]);
+    for (int i = 0; i < ni; ++i) {
+      int g = lane + 64 * i;
+      g = g < n16 ? g : n16 - 1;
+      glds16(a.W + a0 + 16LL * g, dst + 1024u * i);
+    }
+  };
   if (wave == 0) {
     // ---- the chain
-    const int ni = (int)(((fbytes + 30) / 16 + 63) / 64);
-    auto issue = [&](int t) {  // frame t (clamped) -> slot t % kSSlots
-      const long long off = goff0 + (long long)fclamp(t) * fbytes;
-      const long long a0 = off & ~15LL;
-      const int n16 = (int)((off + fbytes - a0 + 15) >> 4);
-      const unsigned dst = lds_base_addr(&s_ring[t % kSSlots][0]);
-      for (int i = 0; i < ni; ++i) {
-        int g = lane + 64 * i;
-        g = g < n16 ? g : n16 - 1;
-        glds16(a.W + a0 + 16LL * g, dst + 1024u * i);
-      }
-    };
     // every step issues one frame (clamped past the end), so the ring's
-    // vmcnt counts stay uniform to the last frame (prefetching frame t + 1's
-    // weights into registers a step early measured slower: 0.869 against
-    // 0.846 ms at cfg4)
+    // vmcnt counts stay uniform to the last frame. Chain stamps
+    // (tools/vit_stamps.py): of a ~1,200-tick step, the frame wait and LDS
+    // reads take ~290, the terms / max tree / alpha write / publish ~440, the
+    // ring issue ~330. Measured slower: prefetching frame t + 1's weights
+    // into registers a step early (0.869 against 0.846 ms at cfg4), and the
+    // ring's DMA issued by the backpointer wave instead (1.07-1.11 ms: that
+    // wave then paces the chain)
     if (nf > 0)
       for (int d = 0; d < kSAhead; ++d) issue(d);
     float a0 = 0.f;
     int bseen = 0;  // the backpointer wave's progress as last read
     for (int t = 0; t < nf; ++t) {
+      VSTAMP(t, 0);
       wait_vmcnt((kSAhead - 1) * ni);  // frame t landed (the only VMEM ops are the ring's)
       float x[kHalf], xs, w00;
       terms(t, x, xs, w00);
+#ifdef LT_DIAG
+      if (stamp) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        VSTAMP(t, 1);
+      }
+#endif
       float mx = max3_raw(h ? x[16] : xs, x[0], x[1]);
       mx = max3_raw(mx, x[2], x[3]);
       const float m1 = max3_raw(x[4], x[5], x[6]);
@@ -173,6 +194,7 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
       a0 += w00;
       if (lane == 32) anxt[0] = a0;
       publish(0, t + 1);
+      VSTAMP(t, 2);
       // the slot of frame t + kSAhead held frame t + kSAhead - kSSlots, and
       // the next step overwrites the alpha row alpha_{t + 2 - kSAl}: the
       // backpointer wave must be past both (every step, the last ones too)
@@ -182,8 +204,15 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
         bseen = __builtin_amdgcn_readfirstlane(s_prog[1]);
       }
       issue(t + kSAhead);
+      VSTAMP(t, 3);
     }
     wait_vmcnt(0);
+#ifdef LT_DIAG
+    if (stamp) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int i = lane; i < kVitStampSteps * 4; i += 64) a.stamps[i] = (&s_st[0][0])[i];
+    }
+#endif
     // the distance: (+)_q alpha_T[q] in MaxTropical, the first maximum
     const float* af = s_al[nf % kSAl];
     float r = lane < C ? af[aslot(lane)] : -kInf;
@@ -353,8 +382,10 @@ int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, 
   a.C = a.V + 1;
   a.R = a.V + 1;
   a.dbg = 0;
+  a.stamps = nullptr;
 #ifdef LT_DIAG
   if (const char* d = lt_impl::tune_str("LT_VIT_DBG")) a.dbg = atoi(d);
+  if (const char* sp = lt_impl::tune_str("LT_VIT_STAMPS")) a.stamps = (long long*)strtoull(sp, nullptr, 0);
 #endif
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const bool full = a.V == 32;
