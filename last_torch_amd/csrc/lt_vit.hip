@@ -162,7 +162,8 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
     // ring issue ~330. Measured slower: prefetching frame t + 1's weights
     // into registers a step early (0.869 against 0.846 ms at cfg4), and the
     // ring's DMA issued by the backpointer wave instead (1.07-1.11 ms: that
-    // wave then paces the chain)
+    // wave then paces the chain); a third, loader wave issuing it (0.848 ms,
+    // no change: the chain's own latency, ~1,100 ticks a step, is the floor)
     if (nf > 0)
       for (int d = 0; d < kSAhead; ++d) issue(d);
     float a0 = 0.f;
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
       a.dist[b] = r;
       a.qstar[b] = ri;
     }
-  } else {
+  } else if (wave == 1) {
     // ---- the backpointers: the first term equal to alpha_{t+1}[q]
     // (group_reduce's first-maximum rule), the lower half first
     const __amdgpu_buffer_rsrc_t bpr =
