@@ -173,13 +173,14 @@ def test_cfg2_realistic_weights(cuda, kind):
   _check_loss_grad(W, nf, lab, nl, V, n, local=True)
 
 
-@pytest.mark.parametrize('design', ['auto', 'chunk'])
+@pytest.mark.parametrize('design', ['auto', 'chunk', 'fused'])
 def test_north_star_b256(cuda, design):
   """B=256 (the north-star shape): sampled utterances against the oracle and
   the per-frame marginal sums of all of them -- the design lt_loss_grad picks
-  there (what bench.py times) and the chunked scan (lt_loss_grad_ex)."""
+  there (what bench.py times), the chunked scan and the one-launch fused pipe
+  (lt_loss_grad_ex; its 2B recursion workgroups co-resident on 256 CUs)."""
   V, n = 32, 1
-  d = nat.DESIGN_AUTO if design == 'auto' else nat.DESIGN_CHUNK
+  d = {'auto': nat.DESIGN_AUTO, 'chunk': nat.DESIGN_CHUNK, 'fused': nat.DESIGN_FUSED_PIPE}[design]
   W, nf, lab, nl = _bench_inputs(256, 1000, 100, V, n, cuda, seed=99)
   loss, lz, num, dW = _check_loss_grad(W, nf, lab, nl, V, n, idx=[0, 1, 63, 64, 128, 200, 254, 255],
                                        design=d)
