@@ -14,7 +14,7 @@ from last_torch_amd import _native  # noqa: E402
 T, U, V = 1000, 100, 32
 N = int(os.environ.get('N', 20))
 designs = {'chunk': {'LT_CHUNK': '1'}, 'serial': {'LT_CHUNK': '0'},
-           'fused': {'LT_CHUNK': '0', 'LT_FUSED': '1'}}
+           'fused': {'LT_CHUNK': '0', 'LT_MID': '1'}}
 for B in [int(x) for x in os.environ.get('BS', '64,128,192,256').split(',')]:
   g = torch.Generator(device='cuda')
   g.manual_seed(0)
@@ -26,7 +26,7 @@ for B in [int(x) for x in os.environ.get('BS', '64,128,192,256').split(',')]:
   losses = {}
   for rnd in range(3):
     for name, env in designs.items():
-      for k in ('LT_CHUNK', 'LT_FUSED'):
+      for k in ('LT_CHUNK', 'LT_MID'):
         os.environ.pop(k, None)
       os.environ.update(env)
       ws = torch.empty([_native.loss_grad_workspace_bytes(W, V, 1, U, False)], dtype=torch.uint8,
@@ -43,7 +43,7 @@ for B in [int(x) for x in os.environ.get('BS', '64,128,192,256').split(',')]:
       losses[name] = out[0].double().cpu()
       del ws
   os.environ.pop('LT_CHUNK', None)
-  os.environ.pop('LT_FUSED', None)
+  os.environ.pop('LT_MID', None)
   dl = (losses['chunk'] - losses['serial']).abs().max().item()
   gb = 15756.0 * B * T / 1e9
   line = ' '.join(f'{k} {min(v):.3f} ms ({100 * gb / min(v) / 8:.1f} %)' for k, v in res.items())
