@@ -71,7 +71,9 @@ constexpr int kSAl = 8;
 
 template <bool BF16, bool FULL>
 __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_al[kSAl][40];
+  // alpha rows: [0, 17) and [20, 36) the two halves' sources (b128 reads),
+  // [40, 72) spare slots for the chain's branch-free store
+  __shared__ __attribute__((aligned(16))) float s_al[kSAl][72];
   __shared__ __attribute__((aligned(16))) unsigned char s_ring[kSSlots][5 * 1024];
   __shared__ int s_prog[2];  // [0] chain: alpha rows published; [1] backpointer frames done
 #ifdef LT_DIAG
@@ -190,10 +192,12 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
       if (h == 0) mx = fmaxf(mx, x[16]);
       auto pv = __builtin_amdgcn_permlane32_swap(__float_as_int(mx), __float_as_int(mx), false, false);
       const float r = fmaxf(mx, __int_as_float(h ? pv[0] : pv[1]));
+      // one store for every lane, no exec branch: the destination's value
+      // (lower half), alpha[0] (lane 32), else a spare slot of the row
       float* anxt = s_al[(t + 1) % kSAl];
-      if (h == 0 && live) anxt[aslot(q)] = r;
       a0 += w00;
-      if (lane == 32) anxt[0] = a0;
+      const int wslot = h == 0 ? (live ? aslot(q) : 40 + j) : (lane == 32 ? 0 : 40 + j);
+      anxt[wslot] = lane == 32 ? a0 : r;
       publish(0, t + 1);
       VSTAMP(t, 2);
       // the slot of frame t + kSAhead held frame t + kSAhead - kSSlots, and

@@ -8,6 +8,6 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
   -p no:cacheprovider -k "cfg4 or viterbi or shortest or vit or max_tropical or golden" > $out/gpu.log 2>&1 || exit $?
 for r in 1 2; do
   TAG=product timeout -k 10 200 python -u tools/vit_time.py >> $out/vit.txt 2>&1 || exit $?
-  TAG=variant LT_LIB_PATH=build/var/vitold.so timeout -k 10 200 python -u tools/vit_time.py >> $out/vit.txt 2>&1 || exit $?
+  TAG=variant LT_LIB_PATH=build/var/vitprev.so timeout -k 10 200 python -u tools/vit_time.py >> $out/vit.txt 2>&1 || exit $?
 done
 timeout -k 10 200 python -u tools/vit_stamps.py > $out/stamps.txt 2>&1 || exit $?
