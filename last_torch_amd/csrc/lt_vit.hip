@@ -47,6 +47,40 @@ LT_DEVINL float max3_raw(float x, float y, float z) {
   return r;
 }
 
+// 4 (2) consecutive 1 KiB LDS-DMA wave-instructions from one lane address:
+// the instruction's immediate offset steps the global and the LDS address
+// alike (M0 = the LDS base, set once)
+LT_DEVINL void glds16x4(const void* gsrc, unsigned lds_addr) {
+  unsigned keep;
+  lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "global_load_lds_dwordx4 %1, off offset:1024\n\t"
+      "global_load_lds_dwordx4 %1, off offset:2048\n\t"
+      "global_load_lds_dwordx4 %1, off offset:3072\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+LT_DEVINL void glds16x2(const void* gsrc, unsigned lds_addr) {
+  unsigned keep;
+  lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "global_load_lds_dwordx4 %1, off offset:1024\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
 // one weight of an LDS-staged frame (bf16 widened)
 template <bool BF16>
 LT_DEVINL float vlds(const unsigned char* fr, int off) {
@@ -144,12 +178,22 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
     if (lane == 0) __hip_atomic_store(&s_prog[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   const int ni = (int)(((fbytes + 30) / 16 + 63) / 64);
+  // wave-instructions that never leave the frame: 4 (fp32 V = 32), 2 (bf16)
+  const int kf = (int)min((long long)min(ni, 4), fbytes / 16 / 64);
   auto issue = [&](int t) {  // frame t (clamped) -> slot t % kSSlots
     const long long off = goff0 + (long long)fclamp(t) * fbytes;
     const long long a0 = off & ~15LL;
     const int n16 = (int)((off + fbytes - a0 + 15) >> 4);
     const unsigned dst = lds_base_addr(&s_ring[t % kSSlots][0]);
-    for (int i = 0; i < ni; ++i) {
+    // the first kf wave-instructions never leave the frame (or W): one lane
+    // address, the instruction's 1 KiB step as its immediate offset (global
+    // and LDS alike); the rest clamp each lane to the frame's last 16 bytes
+    // (inline asm, as glds16: the compiler sees no LDS write to order its
+    // LDS reads behind, so the ring's counted vmcnt waits stay partial)
+    const unsigned char* gb = a.W + a0 + 16 * lane;
+    if (kf == 4) glds16x4(gb, dst);
+    else if (kf == 2) glds16x2(gb, dst);
+    for (int i = (kf == 4 || kf == 2) ? kf : 0; i < ni; ++i) {
       int g = lane + 64 * i;
       g = g < n16 ? g : n16 - 1;
       glds16(a.W + a0 + 16LL * g, dst + 1024u * i);
