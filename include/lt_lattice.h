@@ -301,8 +301,9 @@ int lt_loss_grad_design(const lt_problem* pb, int32_t* design);
  * own choice, as lt_loss_grad): for callers that time or test one design at
  * a shape where lt_loss_grad would pick another. LT_EUNSUPPORTED when the
  * shape cannot take it (LT_DESIGN_CHUNK and LT_DESIGN_FUSED_PIPE are bigram
- * designs). Replaces the LT_CHUNK / LT_CHECKPOINTS / LT_FUSED environment
- * overrides of round 2. */
+ * designs; LT_DESIGN_FUSED_PIPE, the one-launch pipe with the marginals in
+ * the recursion workgroups, also needs U < 128 and its 2B workgroups
+ * co-resident). Replaces the environment overrides of round 2. */
 int lt_loss_grad_workspace_bytes_ex(const lt_problem* pb, int32_t local_norm, int32_t design,
                                     size_t* bytes);
 int lt_loss_grad_ex(const lt_problem* pb, int32_t local_norm, int32_t design, const void* W,
