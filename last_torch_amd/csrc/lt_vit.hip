@@ -88,8 +88,9 @@ LT_DEVINL float vlds(const unsigned char* fr, int off) {
   else return *(const float*)(fr + off);
 }
 
-// The alpha chain and the backpointers on two waves of one workgroup (two
-// SIMDs; cfg4 0.848 ms against 0.882 ms with both on one wave, round 3). Wave 0 runs the
+// The alpha chain and the backpointers on separate waves of one workgroup
+// (cfg4: 0.882 ms with both on one wave, 0.831 ms with one backpointer wave,
+// 0.742 ms with kBpWaves = 2 dealing the frames round robin, round 3). Wave 0 runs the
 // chain alone -- weights, alpha, the max3 tree, the LDS-DMA ring -- and
 // publishes alpha_{t+1} with an LDS progress word; wave 1 follows, re-forms
 // frame t's terms from the same alpha_t and weights (the same additions, so
@@ -100,16 +101,21 @@ LT_DEVINL float vlds(const unsigned char* fr, int off) {
 // or row that wave has not passed.
 constexpr int kSAhead = 3;
 constexpr int kSSlots = 8;
+#ifndef LT_VIT_BPW
+#define LT_VIT_BPW 2
+#endif
+constexpr int kBpWaves = LT_VIT_BPW;  // backpointer waves (frames dealt round robin)
 [[maybe_unused]] constexpr int kVitStampSteps = 128;  // diagnostic stamps (LT_DIAG)
 constexpr int kSAl = 8;
 
 template <bool BF16, bool FULL>
-__global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
+__global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const VitArgs a) {
   // alpha rows: [0, 17) and [20, 36) the two halves' sources (b128 reads),
   // [40, 72) spare slots for the chain's branch-free store
   __shared__ __attribute__((aligned(16))) float s_al[kSAl][72];
   __shared__ __attribute__((aligned(16))) unsigned char s_ring[kSSlots][5 * 1024];
-  __shared__ int s_prog[2];  // [0] chain: alpha rows published; [1] backpointer frames done
+  __shared__ int s_prog[1 + kBpWaves];  // [0] chain: alpha rows published; [1 + k] backpointer
+                                       // wave k: 1 + its last frame done
 #ifdef LT_DIAG
   __shared__ long long s_st[kVitStampSteps][4];
   const bool stamp = a.stamps != nullptr && blockIdx.x == 0;
@@ -135,7 +141,7 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
   auto fclamp = [&](int t) { return min(t, max(nf - 1, 0)); };
   // alpha_0: the start state (MaxTropical one = 0), every other state zero
   if (tid < 40) s_al[0][tid] = tid == 0 ? 0.f : -kInf;
-  if (tid < 2) s_prog[tid] = 0;
+  if (tid < 1 + kBpWaves) s_prog[tid] = 0;
   __syncthreads();
   auto frame = [&](int t) {
     return &s_ring[t % kSSlots][0] + ((goff0 + (long long)fclamp(t) * fbytes) & 15);
@@ -249,8 +255,13 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
       // backpointer wave must be past both (every step, the last ones too)
       const int want = max(t + kSAhead - kSSlots + 1, t + 3 - kSAl);
       if (bseen < want) {  // re-read only when the last value seen is short
-        wait_prog(1, want);
-        bseen = __builtin_amdgcn_readfirstlane(s_prog[1]);
+        // every backpointer wave past `want` - 1: all frames below `want` done
+        int m = 0x7fffffff;
+        for (int k = 1; k <= kBpWaves; ++k) {
+          wait_prog(k, want);
+          m = min(m, __builtin_amdgcn_readfirstlane(s_prog[k]));
+        }
+        bseen = m;
       }
       issue(t + kSAhead);
       VSTAMP(t, 3);
@@ -276,14 +287,15 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
       a.dist[b] = r;
       a.qstar[b] = ri;
     }
-  } else if (wave == 1) {
-    // ---- the backpointers: the first term equal to alpha_{t+1}[q]
+  } else {
+    // ---- the backpointers (wave 1 + k takes frames k, k + kBpWaves, ...):
+    // the first term equal to alpha_{t+1}[q]
     // (group_reduce's first-maximum rule), the lower half first
     const __amdgpu_buffer_rsrc_t bpr =
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.bp + (long long)b * a.T * C), (short)0,
                                           a.T * C, 0x00020000);
     const int ib = h ? 18 : 1;  // term index of x[0]
-    for (int t = 0; t < nf; ++t) {
+    for (int t = wave - 1; t < nf; t += kBpWaves) {
       wait_prog(0, t + 1);
       float x[kHalf], xs, w00;
       terms(t, x, xs, w00);
@@ -297,7 +309,7 @@ __global__ __launch_bounds__(128) void vit_split_kernel(const VitArgs a) {
       const int bpv = lane == 32 ? 0 : (rlo < 99 ? rlo : rhi);
       if ((h == 0 && live) || lane == 32)
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bpv, bpr, lane == 32 ? 0 : q, t * C, 0);
-      publish(1, t + 1);
+      publish(wave, t + 1);
       (void)w00;
     }
   }
@@ -443,7 +455,8 @@ int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, 
                        : (bf16 ? (const void*)vit_split_kernel<true, false>
                                : (const void*)vit_split_kernel<false, false>);
   void* args[] = {(void*)&a};
-  hipError_t e = hipLaunchKernel(k, dim3(a.B), dim3(128), args, 0, (hipStream_t)stream);
+  hipError_t e =
+      hipLaunchKernel(k, dim3(a.B), dim3(64 * (1 + kBpWaves)), args, 0, (hipStream_t)stream);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;
