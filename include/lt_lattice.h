@@ -41,6 +41,7 @@ extern "C" {
 #define LT_EINVAL (-1)       /* bad argument / shape */
 #define LT_EUNSUPPORTED (-2) /* configuration outside what the kernels do */
 #define LT_EHIP (-3)         /* HIP runtime error (launch, attribute) */
+#define LT_ENOMEM (-4)       /* host memory exhausted (the host twin's workers) */
 
 #define LT_DTYPE_F32 0
 #define LT_DTYPE_BF16 1
@@ -269,6 +270,28 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
                        const void* W, const int32_t* num_frames, const int32_t* labels,
                        const int32_t* num_labels, float* loss, float* log_z, float* num,
                        void* dW, void* workspace, size_t workspace_bytes, void* stream);
+
+/* The gradient of lt_table_forward's distance (RecognitionLattice._forward
+ * under autograd, lattices.py:379-496 with semirings.py:184-401; the
+ * marginals of _backward / _forward_backward, lattices.py:498-799 with
+ * FrameDependent.backward alignments.py:300-318 and
+ * FrameLabelDependent.backward :379-419):
+ *   LT_SEMIRING_LOG   dW = grad_b * d log_z / dW (the arc marginals); dist =
+ *                     log_z and alpha = the [B,T,C] history of lt_table_forward
+ *   LT_SEMIRING_REAL  dW = grad_b * d dist / dW = grad_b * alpha * beta'
+ *                     (dist, alpha from lt_table_forward in Real)
+ *   LT_SEMIRING_MAX   dW = grad_b on every arc of the best path (the first
+ *                     maximum, as lt_table_viterbi), 0 elsewhere; dist and
+ *                     alpha are not read (may be NULL)
+ * grad [B] nullable (1). Padding frames and utterances of non-finite distance
+ * get dW = 0. workspace: lt_table_den_backward_workspace_bytes() (0 bytes for
+ * fp32 W in Log / Real). */
+int lt_table_den_backward_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
+                                          int32_t semiring, size_t* bytes);
+int lt_table_den_backward(const lt_graph* g, const lt_table_problem* pb, int32_t semiring,
+                          const void* W, const int32_t* num_frames, const float* dist,
+                          const float* alpha, const float* grad, void* dW, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 /* RecognitionLattice.shortest_path (lattices.py:185-247), per utterance (no
  * D6 aliasing): labels [B, T*A] int64 with A = 1 (FrameDependent) or K+1

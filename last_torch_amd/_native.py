@@ -78,6 +78,8 @@ _SIG = {
     'lt_table_num_forward': [_G, _TP, _I32, _P, _P, _P, _P, _P, _P],
     'lt_table_loss_grad_workspace_bytes': [_G, _TP, ctypes.POINTER(ctypes.c_size_t)],
     'lt_table_loss_grad': [_G, _TP, _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
+    'lt_table_den_backward_workspace_bytes': [_G, _TP, _I32, ctypes.POINTER(ctypes.c_size_t)],
+    'lt_table_den_backward': [_G, _TP, _I32] + [_P] * 7 + [ctypes.c_size_t, _P],
     'lt_table_viterbi_workspace_bytes': [_G, _TP, ctypes.POINTER(ctypes.c_size_t)],
     'lt_table_viterbi': [_G, _TP, _P, _P, _I32, _P, _P, _P, ctypes.c_size_t, _P],
     'lt_joint_weights_workspace_bytes': [ctypes.c_int64, _I32, _I32,
@@ -517,6 +519,31 @@ def table_loss_grad(graph, W, num_frames, labels, num_labels, local_norm, want_g
                                   nbytes.value if want_grad else 0, _stream()),
          'lt_table_loss_grad')
   return loss, log_z, num, dW
+
+
+def table_den_backward(graph, W, num_frames, semiring, dist=None, alpha=None, grad=None):
+  """lt_table_den_backward: dW [B,T,C,V+1] (W's dtype) = grad_b * the gradient
+  of the semiring's distance (Log: the arc marginals, from lt_table_forward's
+  log_z and alpha; Real: alpha * beta'; MaxTropical: the best path's arcs)."""
+  pb = _tproblem(graph, W)
+  B = W.shape[0]
+  nbytes = ctypes.c_size_t(0)
+  _check(lib().lt_table_den_backward_workspace_bytes(ctypes.byref(graph.g), ctypes.byref(pb),
+                                                     semiring, ctypes.byref(nbytes)),
+         'lt_table_den_backward_workspace_bytes')
+  ws = torch.empty([max(nbytes.value, 1)], dtype=torch.uint8, device=W.device)
+  dW = torch.empty_like(W)
+  if dist is not None:
+    dist = dist.to(torch.float32).contiguous()
+  if alpha is not None:
+    alpha = alpha.to(torch.float32).contiguous()
+  if grad is not None:
+    grad = grad.to(device=W.device, dtype=torch.float32).reshape(B).contiguous()
+  _check(lib().lt_table_den_backward(ctypes.byref(graph.g), ctypes.byref(pb), semiring, _ptr(W),
+                                     _ptr(num_frames), _ptr(dist), _ptr(alpha), _ptr(grad),
+                                     _ptr(dW), _ptr(ws), nbytes.value, _stream()),
+         'lt_table_den_backward')
+  return dW
 
 
 def table_viterbi(graph, W, num_frames, label_convention):

@@ -51,8 +51,29 @@ def lib():
   return _lib
 
 
+def _cpu_supported():
+  """The twin is built for x86-64-v3 (AVX2, FMA; Makefile CPUFLAGS): on a
+  host without them it would die of SIGILL, so it is not offered there."""
+  try:
+    with open('/proc/cpuinfo') as f:
+      for line in f:
+        if line.startswith('flags'):
+          flags = set(line.split(':', 1)[1].split())
+          return {'avx2', 'fma', 'bmi2'} <= flags
+  except OSError:
+    pass
+  return False
+
+
+_SUPPORTED = None
+
+
 def available():
-  return os.path.exists(LIB_PATH)
+  """The library exists and this host can run its code."""
+  global _SUPPORTED
+  if _SUPPORTED is None:
+    _SUPPORTED = _cpu_supported()
+  return _SUPPORTED and os.path.exists(LIB_PATH)
 
 
 def _check(rc):

@@ -20,8 +20,11 @@
 //     double first and exponentiate a small float.
 #include "../../include/lt_lattice_cpu.h"
 
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
+#include <new>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -150,20 +153,54 @@ void zero_rows(void* dW, bool bf16, long long off, long long n) {
 // semirings.py:248-255 / 279-286: c = max, a non-finite c is replaced by 0
 inline float safe(float c) { return std::isfinite(c) ? c : 0.f; }
 
-// Runs fn(b, worker) for every utterance b on the thread pool.
+// The default pool size: the CPUs this process may run on (its affinity
+// mask, which cgroup cpusets also narrow), not the machine's count.
+int default_threads() {
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) {
+    const int n = CPU_COUNT(&set);
+    if (n > 0) return n;
+  }
+  return (int)std::max(1u, std::thread::hardware_concurrency());
+}
+
+// Runs fn(b, worker) for every utterance b on the thread pool. An exception
+// inside a worker (a per-utterance buffer that cannot be allocated) or a
+// thread that cannot be started ends the call with an LT_* code instead of
+// std::terminate: the other workers stop taking utterances, and the caller
+// returns the code.
 template <typename F>
-void for_utterances(int B, F&& fn) {
+int for_utterances(int B, F&& fn) {
   int nt = g_threads.load();
-  if (nt <= 0) nt = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (nt <= 0) nt = default_threads();
   nt = std::max(1, std::min(nt, B));
   std::atomic<int> next{0};
+  std::atomic<int> err{LT_OK};
   auto work = [&](int w) {
-    for (int b = next++; b < B; b = next++) fn(b, w);
+    try {
+      for (int b = next++; b < B && err.load(std::memory_order_relaxed) == LT_OK; b = next++)
+        fn(b, w);
+    } catch (const std::bad_alloc&) {
+      int ok = LT_OK;
+      err.compare_exchange_strong(ok, LT_ENOMEM);
+    } catch (...) {
+      int ok = LT_OK;
+      err.compare_exchange_strong(ok, LT_EINVAL);
+    }
   };
   std::vector<std::thread> pool;
-  for (int w = 1; w < nt; ++w) pool.emplace_back(work, w);
+  try {
+    pool.reserve(nt);
+    for (int w = 1; w < nt; ++w) pool.emplace_back(work, w);
+  } catch (...) {
+    // fewer workers than asked: the ones started and this thread finish the batch
+  }
   work(0);
   for (auto& th : pool) th.join();
+  const int rc = err.load();
+  if (rc == LT_ENOMEM) return fail(rc, "host memory exhausted in a worker");
+  if (rc != LT_OK) return fail(rc, "exception in a worker");
+  return LT_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -500,7 +537,7 @@ int lt_cpu_set_num_threads(int32_t n) {
 
 int lt_cpu_num_threads(void) {
   const int nt = g_threads.load();
-  return nt > 0 ? nt : (int)std::max(1u, std::thread::hardware_concurrency());
+  return nt > 0 ? nt : default_threads();
 }
 
 const char* lt_cpu_last_error(void) { return g_err.c_str(); }
@@ -515,7 +552,7 @@ int lt_cpu_den_forward(const lt_problem* pb, int32_t semiring, const void* W,
   if (P.B == 0) return LT_OK;
   if (check_ptrs(W, P.T) || !num_frames || !dist) return fail(LT_EINVAL, "null pointer");
   const int C = P.g.C;
-  for_utterances(P.B, [&](int b, int) {
+  rc = for_utterances(P.B, [&](int b, int) {
     std::vector<float> a(C), na(C);
     FwdScratch sc(P.g.V);
     const int nf = clamp_frames(num_frames, b, P.T);
@@ -529,7 +566,7 @@ int lt_cpu_den_forward(const lt_problem* pb, int32_t semiring, const void* W,
       r = den_forward_utt<LT_SEMIRING_REAL>(P, W, b, nf, nullptr, nullptr, ab, nullptr, a, na, sc);
     dist[b] = (float)r;
   });
-  return LT_OK;
+  return rc;
 }
 
 int lt_cpu_num_forward(const lt_problem* pb, int32_t semiring, const void* W,
@@ -544,7 +581,7 @@ int lt_cpu_num_forward(const lt_problem* pb, int32_t semiring, const void* W,
   if (check_ptrs(W, P.T) || !num_frames || !num_labels || !num || (!labels && P.U > 0))
     return fail(LT_EINVAL, "null pointer");
   const int NP = P.U + 1;
-  for_utterances(P.B, [&](int b, int) {
+  rc = for_utterances(P.B, [&](int b, int) {
     std::vector<float> a(NP), na(NP);
     StringArcs sa;
     string_arcs(P.g, P.U, labels ? labels + (long long)b * P.U : nullptr, &sa);
@@ -559,7 +596,7 @@ int lt_cpu_num_forward(const lt_problem* pb, int32_t semiring, const void* W,
       r = num_forward_utt<LT_SEMIRING_REAL>(P, W, b, nf, sa, num_labels[b], nullptr, nullptr, ab, a, na);
     num[b] = (float)r;
   });
-  return LT_OK;
+  return rc;
 }
 
 int lt_cpu_den_backward(const lt_problem* pb, const void* W, const int32_t* num_frames,
@@ -571,7 +608,7 @@ int lt_cpu_den_backward(const lt_problem* pb, const void* W, const int32_t* num_
   if (check_ptrs(W, P.T) || !num_frames || !log_z || (!alpha && P.T > 0) || (!dW && P.T > 0))
     return fail(LT_EINVAL, "null pointer");
   const int C = P.g.C;
-  for_utterances(P.B, [&](int b, int) {
+  rc = for_utterances(P.B, [&](int b, int) {
     std::vector<float> bc(C), bn(C), dfr(P.FR);
     const int nf = clamp_frames(num_frames, b, P.T);
     float gb = grad ? grad[b] : 1.f;
@@ -583,7 +620,7 @@ int lt_cpu_den_backward(const lt_problem* pb, const void* W, const int32_t* num_
                      });
     zero_rows(dW, P.bf16, base + (long long)nf * P.FR, (long long)(P.T - nf) * P.FR);
   });
-  return LT_OK;
+  return rc;
 }
 
 int lt_cpu_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
@@ -599,7 +636,7 @@ int lt_cpu_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
   const Topo& g = P.g;
   const int C = g.C, R = g.R, NP = P.U + 1;
   const bool den = !local_norm;
-  for_utterances(P.B, [&](int b, int) {
+  rc = for_utterances(P.B, [&](int b, int) {
     const int nf = clamp_frames(num_frames, b, P.T);
     const int nl = num_labels[b];
     StringArcs sa;
@@ -673,7 +710,7 @@ int lt_cpu_loss_grad(const lt_problem* pb, int32_t local_norm, const void* W,
       }
     }
   });
-  return LT_OK;
+  return rc;
 }
 
 int lt_cpu_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
@@ -689,7 +726,7 @@ int lt_cpu_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frame
     return fail(LT_EINVAL, "null pointer");
   const Topo& g = P.g;
   const int C = g.C, R = g.R, V = g.V;
-  for_utterances(P.B, [&](int b, int) {
+  rc = for_utterances(P.B, [&](int b, int) {
     const int nf = clamp_frames(num_frames, b, P.T);
     std::vector<float> a(C), na(C);
     std::vector<int16_t> bp((size_t)std::max(nf, 1) * C);
@@ -729,7 +766,7 @@ int lt_cpu_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frame
       }
     }
   });
-  return LT_OK;
+  return rc;
 }
 
 }  // extern "C"

@@ -145,6 +145,66 @@ LT_DEVINL float lt_exp(float x) { return __builtin_amdgcn_exp2f(x * kLog2e); }
 LT_DEVINL float lt_exp_off(float x, float cl) { return __builtin_amdgcn_exp2f(__builtin_fmaf(x, kLog2e, -cl)); }
 // Arguments are sums of exp() with the max term == 1 (>= 1) or exactly 0.
 LT_DEVINL float lt_log(float x) { return __builtin_amdgcn_logf(x) * 0.6931471805599453f; }
+// log(x) for log-space recursions that take one log per frame for T frames:
+// v_log_f32's error (about an ulp of log2 x, and biased) adds up over the
+// frames (measured: ~1e-3 after 1,000 FrameLabelDependent(2) frames). Here
+// x = 2^e m with m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(z), z = (m - 1) /
+// (m + 1), |z| <= 0.1716, by five terms of its series (truncation < 1e-9);
+// the result's only sizeable error is its final rounding (unbiased). Zero,
+// negative, infinite and NaN arguments go through v_log_f32 (-inf, NaN, inf).
+LT_DEVINL float lt_log_acc(float x) {
+  if (!(x > 0.f) || x == __builtin_inff()) return lt_log(x);
+  int e = __builtin_amdgcn_frexp_expf(x);
+  float m = __builtin_amdgcn_frexp_mantf(x);  // [0.5, 1)
+  if (m < 0.70710678f) {
+    m *= 2.f;
+    --e;
+  }
+  const float z = __builtin_amdgcn_rcpf(m + 1.f) * (m - 1.f);
+  const float z2 = z * z;
+  float p = 1.f / 9.f;
+  p = __builtin_fmaf(p, z2, 1.f / 7.f);
+  p = __builtin_fmaf(p, z2, 1.f / 5.f);
+  p = __builtin_fmaf(p, z2, 1.f / 3.f);
+  p = __builtin_fmaf(p, z2, 1.f);
+  const float lm = 2.f * z * p;
+  const float ef = (float)e;
+  return __builtin_fmaf(ef, 0.693145751953125f, __builtin_fmaf(ef, 1.428606765330187e-06f, lm));
+}
+
+// Log-space values as an exact integer part plus a small fraction, (i, f):
+// the value is i + f with i integer-valued (or -inf: the semiring zero) and
+// f in [0, 1) after each step. The string (numerator) recursions need it:
+// their positions span hundreds of nats within one frame (the positions
+// ahead of the alignment's diagonal), so a value kept relative to one
+// offset per frame is rounded at its own magnitude -- 2^-24 * 80 at 80 nats
+// below the frame's max, every frame -- while (i, f) rounds only the
+// fraction. lae_split: (ia, fa) (+) (ib, fb) = log(e^(ia+fa) + e^(ib+fb))
+// (semirings.py:248-255), the result's integer part taken from the term
+// with the larger integer part (exact), its fraction f1 + log(1 + e^d) with
+// d = (i2 - i1) + (f2 - f1) (d <= ~|f| range; its rounding reaches the result
+// only through e^d).
+LT_DEVINL void lae_split(float ia, float fa, float ib, float fb, float& io, float& fo) {
+  constexpr float ninf = -__builtin_inff();
+  ia = fa == ninf ? ninf : ia;  // a masked arc (w = -inf) is the zero term
+  ib = fb == ninf ? ninf : ib;
+  const bool ab = ia >= ib;
+  const float i1 = ab ? ia : ib, f1 = ab ? fa : fb;
+  const float i2 = ab ? ib : ia, f2 = ab ? fb : fa;
+  const float d = (i2 - i1) + (f2 - f1);  // i2 = -inf: -inf (exp 0); both -inf: NaN (masked)
+  const float r = f1 + lt_log_acc(1.f + __builtin_amdgcn_exp2f(d * kLog2e));
+  const float fl = floorf(r);
+  const bool zero = i1 == ninf;
+  const bool fin = __builtin_isfinite(r);  // +inf / NaN weights propagate as the value
+  io = zero ? i1 : (fin ? i1 + fl : r);
+  fo = (zero || !fin) ? 0.f : r - fl;
+}
+// (i, f) of a plain log value x (finite or -inf)
+LT_DEVINL void split_of(float x, float& i, float& f) {
+  const bool fin = __builtin_isfinite(x);
+  i = fin ? floorf(x) : x;
+  f = fin ? x - floorf(x) : 0.f;
+}
 
 template <int CTRL>
 LT_DEVINL float dppf(float v) {

@@ -543,15 +543,6 @@ LT_DEVINL void den_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
   }
 }
 
-// _LogAddExp.forward (semirings.py:248-255) with one exp: the max term's
-// exp(a - c) is exactly 1, so c + log(1 + exp(min - c)) is the same value;
-// a non-finite max is returned as is (= the reference's safe-max result).
-LT_DEVINL float log_plus2(float a, float b) {
-  const float m = fmaxf(a, b), n = fminf(a, b);
-  const float r = m + lt_log(1.f + lt_exp(n - m));
-  return __builtin_isfinite(m) ? r : m;
-}
-
 // ---- numerator wave --------------------------------------------------------
 // Positions u = PN*lane + s. fwd: a'[u] = a[u] W[c_u,0] (+) a[u-1] W[c_{u-1},y_u]
 // (alignments.py:320-329, lattices.py:314-338); bwd is its transpose.
@@ -563,7 +554,7 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
   const lds_int* ylab = (const lds_int*)(as3(lds) + a.off_ylab);
   const int NP = a.U + 1, U = a.U;
   int ob[PN], ol[PN];
-  float v[PN];
+  float v[PN], o[PN];
   const int nl = a.nlab[b];
 #pragma unroll
   for (int s = 0; s < PN; ++s) {
@@ -575,13 +566,16 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
       if (!REV) ol[s] = u >= 1 ? ctx[u - 1] + ylab[u - 1] : 0;
       else ol[s] = u < U ? ctx[u] + ylab[u] : 0;
     }
-    if (!REV) v[s] = (u == 0) ? 0.f : -kInf;
-    else v[s] = (u == nl) ? 0.f : -kInf;
+    v[s] = 0.f;
+    if (!REV) o[s] = (u == 0) ? 0.f : -kInf;
+    else o[s] = (u == nl) ? 0.f : -kInf;
   }
-  // the vector is kept relative to an integer offset near its max (exact),
-  // so the recursion's roundings are 2^-24 of small numbers however long the
-  // utterance; history rows and num are offset + value, rounded once
-  float off = 0.f;
+  // every position is an exact integer part o plus a fraction v in [0, 1)
+  // (lae_split, lt_kernels.h): the positions span hundreds of nats within a
+  // frame, and a value kept relative to one offset per frame was rounded at
+  // its own magnitude every frame (round 3: up to 26 units of 2^-24 |num|
+  // after 1,000 frames, tools/ck_precision.py). History rows and num are
+  // o + v, rounded once.
   float* hist = REV ? a.beta_num : a.alpha_num;
   lds_float* nring = (lds_float*)(as3(lds) + a.off_nring);  // mid mode
   int tag_next = nf > 0 ? ctl[CTL_TAG] : 0;
@@ -608,48 +602,50 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
 #pragma unroll
       for (int s = 0; s < PN; ++s)
         if (PN * lane + s < NP) {
-          nring[slot * NP + PN * lane + s] = off + v[s];
-          if (gr) st_gran(gp + PN * lane + s, off + v[s], tag);
+          nring[slot * NP + PN * lane + s] = o[s] + v[s];
+          if (gr) st_gran(gp + PN * lane + s, o[s] + v[s], tag);
         }
     }
     if (hist && !LT_ABL(a, 8)) {
       float* hr = hist + (row0 + t) * NP;
 #pragma unroll
       for (int s = 0; s < PN; ++s)
-        if (PN * lane + s < NP) st_sc1(hr + PN * lane + s, off + v[s]);
+        if (PN * lane + s < NP) st_sc1(hr + PN * lane + s, o[s] + v[s]);
     }
-    float nv[PN];
     if (LT_ABL(a, 16)) {  // timing ablation: no numerator arithmetic
 #pragma unroll
-      for (int s = 0; s < PN; ++s) nv[s] = v[s] + wb[s] + wl[s];
+      for (int s = 0; s < PN; ++s) v[s] = v[s] + wb[s] + wl[s];
     } else
     if constexpr (!REV) {
-      const float prev = from_prev_lane(v[PN - 1], -kInf);
+      const float pv = from_prev_lane(v[PN - 1], 0.f), po = from_prev_lane(o[PN - 1], -kInf);
+      float no[PN], nv[PN];
 #pragma unroll
       for (int s = 0; s < PN; ++s) {
         const int u = PN * lane + s;
-        const float left = s == 0 ? prev : v[s - 1];
-        const float xl = u >= 1 ? left + wl[s] : -kInf;
-        nv[s] = u < NP ? log_plus2(v[s] + wb[s], xl) : -kInf;
+        const float lo = s == 0 ? po : o[s - 1], lv = s == 0 ? pv : v[s - 1];
+        lae_split(o[s], v[s] + wb[s], u >= 1 ? lo : -kInf, lv + wl[s], no[s], nv[s]);
+        if (u >= NP) no[s] = -kInf;
+      }
+#pragma unroll
+      for (int s = 0; s < PN; ++s) {
+        o[s] = no[s];
+        v[s] = nv[s];
       }
     } else {
-      const float next = from_next_lane(v[0], -kInf);
+      const float nxv = from_next_lane(v[0], 0.f), nxo = from_next_lane(o[0], -kInf);
+      float no[PN], nv[PN];
 #pragma unroll
       for (int s = 0; s < PN; ++s) {
         const int u = PN * lane + s;
-        const float right = s == PN - 1 ? next : v[s + 1];
-        const float xl = u < U ? wl[s] + right : -kInf;
-        nv[s] = u < NP ? log_plus2(wb[s] + v[s], xl) : -kInf;
+        const float ro = s == PN - 1 ? nxo : o[s + 1], rv = s == PN - 1 ? nxv : v[s + 1];
+        lae_split(o[s], wb[s] + v[s], u < U ? ro : -kInf, wl[s] + rv, no[s], nv[s]);
+        if (u >= NP) no[s] = -kInf;
       }
-    }
-    {
-      float vm = nv[0];
 #pragma unroll
-      for (int s = 1; s < PN; ++s) vm = fmaxf(vm, nv[s]);
-      const float fl = floorf(safe(wave_max(vm)));
-#pragma unroll
-      for (int s = 0; s < PN; ++s) v[s] = nv[s] - fl;
-      off += fl;
+      for (int s = 0; s < PN; ++s) {
+        o[s] = no[s];
+        v[s] = nv[s];
+      }
     }
     asm volatile("" ::: "memory");  // LDS is in order per wave: no wait
     if (lane == 0) *(ctl + CTL_NUM) = i + 1;
@@ -661,7 +657,7 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
         float* hr = a.alpha_num + (row0 + t) * NP;
 #pragma unroll
         for (int s = 0; s < PN; ++s)
-          if (PN * lane + s < NP) hr[PN * lane + s] = off + v[s];
+          if (PN * lane + s < NP) hr[PN * lane + s] = o[s] + v[s];
       }
     }
     // lattices.py:375-377
@@ -669,8 +665,8 @@ LT_DEVINL void num_pipe(const PArgs& a, unsigned char* lds, int b, int nf, int l
     for (int s = 0; s < PN; ++s) {
       const int u = PN * lane + s;
       if (u < NP && u == nl) {
-        ((lds_float*)(as3(lds) + a.off_ctl))[CTL_FIN1] = off + v[s];
-        if (a.num) a.num[b] = off + v[s];
+        ((lds_float*)(as3(lds) + a.off_ctl))[CTL_FIN1] = o[s] + v[s];
+        if (a.num) a.num[b] = o[s] + v[s];
       }
     }
     if (lane == 0 && !(nl >= 0 && nl <= U)) {

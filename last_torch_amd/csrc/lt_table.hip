@@ -47,6 +47,7 @@ struct TArgs {
   long long* vlabels;   // Viterbi: [B, T*A]
   int B, T, U, C, V, R, K, conv, local;
   int acc;  // tab_bwd_den_kernel: FrameLabelDependent dW sums in LDS
+  const float* gin;  // den backward: per-utterance gradient factor [B] (nullable)
   // numerator backward run beside the denominator's (lt_table_loss_grad):
   // the chain heads' marginal sums go to nsub [B,T,2S] and their elements to
   // ntab [B,2S] (-1: none), subtracted from dW afterwards (tab_apply_kernel)
@@ -84,7 +85,7 @@ LT_DEVINL float t_safe(float x) { return __builtin_isfinite(x) ? x : 0.f; }
 LT_DEVINL float t_lae(float a, float b) {
   const float m = fmaxf(a, b);
   const float c = t_safe(m);
-  return c + lt_log(lt_exp(a - c) + lt_exp(b - c));
+  return c + lt_log_acc(lt_exp(a - c) + lt_exp(b - c));
 }
 // running logsumexp (m, s): the result is m + log(s) with the safe max
 struct Lse {
@@ -98,7 +99,7 @@ struct Lse {
       s += lt_exp(x - m);
     }
   }
-  LT_DEVINL float get() const { return s > 0.f ? m + lt_log(s) : -kInf; }
+  LT_DEVINL float get() const { return s > 0.f ? m + lt_log_acc(s) : -kInf; }
 };
 
 template <int SR>
@@ -109,6 +110,30 @@ template <int SR>
 LT_DEVINL float t_times(float a, float b) { return SR == M_REAL ? a * b : a + b; }
 
 constexpr int kTabMaxThreads = 512;
+
+// Maximum over the workgroup (every thread passes its value, every thread
+// gets the result); two barriers.
+LT_DEVINL float t_block_max(float v) {
+  __shared__ float red[kTabMaxThreads / 64];
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float m = red[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+  __syncthreads();
+  return m;
+}
+
+// Log vectors are kept relative to an integer offset near their maximum
+// (exact in fp32), so a recursion over T frames rounds small numbers, not
+// values of magnitude |log_z| (the tuned kernels' scheme): the
+// offset after a frame whose new vector is v. Every thread returns it.
+LT_DEVINL float t_renorm_shift(const float* v, int S) {
+  float m = -kInf;
+  for (int q = threadIdx.x; q < S; q += blockDim.x) m = fmaxf(m, v[q]);
+  m = t_block_max(m);
+  return __builtin_isfinite(m) ? floorf(m) : 0.f;
+}
 
 // Graph accessors: the context lattice (states p, in-arcs from the CSR) and
 // the string acceptor (positions u, one in-arc from u-1; lattices.py:314-338).
@@ -381,11 +406,101 @@ struct FrameStage {
   }
 };
 
+// ---- string forward in Log (lattices.py:250-377, alignments.py:320-329 and
+// :420-432 for FrameLabelDependent): every position as an exact integer part
+// plus a fraction (lae_split, lt_kernels.h) -- the positions span hundreds
+// of nats within a frame, so one offset per frame would round each value at
+// its own magnitude every frame (measured: up to 16 units of 2^-24 |num|
+// after 1,000 FrameLabelDependent(2) frames). History rows and num are i + f.
+template <bool BF16>
+LT_DEVINL void tab_str_fwd_log(const TArgs& a, const int b, float* sm) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int U = a.U, S = U + 1, K = a.K;
+  float* ia = sm;  // alpha: integer parts, fractions
+  float* fa = ia + S;
+  float* il = fa + S;  // the lexical chain L^i alpha
+  float* fl = il + S;
+  float* ic = fl + S;  // the frame's sum (FrameLabelDependent) / the new alpha
+  float* fc = ic + S;
+  int* ctx = (int*)(fc + S);
+  int* yn = ctx + S;
+  float* wl = (float*)(yn + S);  // [2S]: blank of u, then the arc leaving u
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  for (int u = tid; u < S; u += nthr) {
+    ia[u] = u == 0 ? 0.f : -kInf;
+    fa[u] = 0.f;
+  }
+  if (tid == 0) t_walk(a, b, ctx, yn);
+  __syncthreads();
+  const long long fbytes = (long long)a.C * a.R * (BF16 ? 2 : 4);
+  const unsigned char* wb = a.W + (long long)b * a.T * fbytes;
+  auto ldc = [&](const unsigned char* w) {
+    return [=](int e) { return ldw<BF16>(w, ctx[e >> 1] + ((e & 1) ? yn[e >> 1] : 0)); };
+  };
+  RegStage<2> cs;
+  cs.fetch(nf > 0 ? 2 * S : 0, ldc(wb));
+  for (int t = 0; t < a.T; ++t) {
+    if (a.alpha)
+      for (int u = tid; u < S; u += nthr) a.alpha[((long long)b * a.T + t) * S + u] = ia[u] + fa[u];
+    if (t >= nf) continue;  // padding frames carry alpha (lattices.py:460-461)
+    const unsigned char* wf = wb + t * fbytes;
+    cs.store(wl, 2 * S, ldc(wf));
+    cs.fetch(t + 1 < nf ? 2 * S : 0, ldc(wf + fbytes));
+    __syncthreads();
+    if (K == 0) {
+      for (int u = tid; u < S; u += nthr)
+        lae_split(ia[u], fa[u] + wl[2 * u], u >= 1 ? ia[u - 1] : -kInf,
+                  u >= 1 ? fa[u - 1] + wl[2 * u - 1] : 0.f, ic[u], fc[u]);
+    } else {
+      // terminated[0] = alpha (x) blank; the chain starts at alpha
+      for (int u = tid; u < S; u += nthr) {
+        ic[u] = ia[u];
+        fc[u] = fa[u] + wl[2 * u];
+        il[u] = ia[u];
+        fl[u] = fa[u];
+      }
+      __syncthreads();
+      for (int i = 1; i <= K; ++i) {
+        // last = shift_down(last (x) lexical): position u takes u - 1's
+        // value times the arc leaving u - 1 (ia / fa hold it for one sweep)
+        for (int u = tid; u < S; u += nthr) {
+          ia[u] = u >= 1 ? il[u - 1] : -kInf;
+          fa[u] = u >= 1 ? fl[u - 1] + wl[2 * u - 1] : 0.f;
+        }
+        __syncthreads();
+        for (int u = tid; u < S; u += nthr) {
+          il[u] = ia[u];
+          fl[u] = fa[u];
+          lae_split(ic[u], fc[u], ia[u], fa[u] + wl[2 * u], ic[u], fc[u]);
+        }
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+    for (int u = tid; u < S; u += nthr) {
+      ia[u] = ic[u];
+      fa[u] = fc[u];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int nl = a.nlab[b];
+    const float r = (nl >= 0 && nl <= a.U) ? ia[nl] + fa[nl] : -kInf;
+    a.dist[b] = r;  // lattices.py:375-377
+    if (a.loss) a.loss[b] = a.local ? -r : a.den_in[b] - r;  // lattices.py:131-183
+  }
+}
+
 // ---- forward: den (NUM = false) or string (NUM = true) shortest distance ----
 // STAGE: the frame's weights are copied to LDS once (coalesced) and the
 // in-arc gathers read LDS; otherwise they read W from global memory.
 template <bool BF16, int SR, bool NUM, bool VIT, bool STAGE>
 LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
+  if constexpr (NUM && SR == M_LOG) {
+    tab_str_fwd_log<BF16>(a, b, sm);
+    return;
+  }
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int S = NUM ? a.U + 1 : a.C, K = a.K, R = a.R;
   int* gsm = (int*)sm;  // graph copy (STAGE): C+1 + 2*C*V ints
@@ -422,9 +537,21 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
   };
   RegStage<2> cs;
   if (NUM) cs.fetch(nf > 0 ? 2 * S : 0, ldc(wb));
+  constexpr bool kOff = SR == M_LOG;  // Log: va relative to the integer offset O
+  float O = 0.f;
+  // the vector after a frame: Log renormalised to a new integer offset
+  auto settle = [&](const float* src) {
+    if constexpr (kOff) {
+      const float sp = t_renorm_shift(src, S);
+      for (int q = tid; q < S; q += nthr) va[q] = src[q] - sp;
+      O += sp;
+    } else {
+      for (int q = tid; q < S; q += nthr) va[q] = src[q];
+    }
+  };
   for (int t = 0; t < a.T; ++t) {
     if (a.alpha)
-      for (int q = tid; q < S; q += nthr) a.alpha[((long long)b * a.T + t) * S + q] = va[q];
+      for (int q = tid; q < S; q += nthr) a.alpha[((long long)b * a.T + t) * S + q] = O + va[q];
     if (t >= nf) continue;  // padding frames carry alpha (lattices.py:460-461)
     const unsigned char* wf = wb + t * fbytes;
     if (STAGE) {
@@ -462,7 +589,7 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
         vn[q] = o;
       }
       __syncthreads();
-      for (int q = tid; q < S; q += nthr) va[q] = vn[q];
+      settle(vn);
       __syncthreads();
       continue;
     }
@@ -504,13 +631,13 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
       }
       __syncthreads();
     }
-    for (int q = tid; q < S; q += nthr) va[q] = acc[q];
+    settle(acc);
     __syncthreads();
   }
   if (tid == 0) {
     if (NUM) {
       const int nl = a.nlab[b];
-      const float r = (nl >= 0 && nl <= a.U) ? va[nl] : t_zero<SR>();
+      const float r = (nl >= 0 && nl <= a.U) ? O + va[nl] : t_zero<SR>();
       a.dist[b] = r;  // lattices.py:375-377
       if (a.loss) a.loss[b] = a.local ? -r : a.den_in[b] - r;  // lattices.py:131-183
     } else {
@@ -520,7 +647,7 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
       if constexpr (SR == M_LOG) {
         Lse l;
         for (int q = 0; q < S; ++q) l.add(va[q]);
-        r = l.get();
+        r = O + l.get();
       } else if constexpr (SR == M_MAX) {
         r = va[0];
         for (int q = 1; q < S; ++q)
@@ -631,12 +758,41 @@ __global__ void tab_backtrace_kernel(const TArgs a) {
   }
 }
 
-// ---- backward (Log): denominator marginals -> dW (written for every frame) --
+// ---- backward: denominator arc gradients -> dW (written for every frame) ---
 // FrameDependent.backward (alignments.py:300-318) / FrameLabelDependent.backward
 // (:379-419) in reverse frame order; the K+1 blank and K lexical marginals of
 // a frame add up on the shared weights. Utterances whose loss is not finite,
 // and padding frames, get dW = 0. do_den = 0 (local normalisation): zeros.
-template <bool BF16, bool STAGE>
+// SR = M_LOG: d log_z / dW, the arc marginals exp(alpha + w + beta - log_z);
+// SR = M_REAL: d dist / dW = alpha * beta' (the Real semiring's (+, x),
+// semirings.py:143-173, differentiated as plain arithmetic). a.gin (nullable):
+// a per-utterance factor on every element (the incoming gradient).
+template <int SR>
+LT_DEVINL float t_plus(float a, float b) {
+  if constexpr (SR == M_LOG) return t_lae(a, b);
+  else return a + b;
+}
+// (+) over the G lanes of a group of per-lane partial sums
+template <int SR, int G>
+struct OutSum {
+  Lse l;
+  float r = 0.f;
+  LT_DEVINL void add(float x) {
+    if constexpr (SR == M_LOG) l.add(x);
+    else r += x;
+  }
+  LT_DEVINL float merge() {
+    if constexpr (SR == M_LOG) {
+      lse_merge<G>(l);
+      return l.get();
+    } else {
+      for (int o = 1; o < G; o <<= 1) r += __shfl_xor(r, o, 64);
+      return r;
+    }
+  }
+};
+
+template <bool BF16, bool STAGE, int SR>
 LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int C = a.C, V = a.V, R = a.R, K = a.K;
@@ -653,11 +809,27 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
   float* dacc = wl + (long long)C * R;      // a.acc: the frame's lexical dW sums [C*(V+1)]
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
-  const float lz = a.local ? 0.f : a.den_in[b];
+  const float lz = (a.local || SR == M_REAL) ? 0.f : a.den_in[b];
   const float nm = a.num_in[b];
-  const bool live = !a.local && __builtin_isfinite(nm) && __builtin_isfinite(lz);
+  const float gb = a.gin ? a.gin[b] : 1.f;
+  const bool live = !a.local && __builtin_isfinite(nm) && __builtin_isfinite(lz) && gb != 0.f;
   const long long FR = (long long)C * R;
-  for (int q = tid; q < C; q += nthr) beta[q] = 0.f;  // every state final (Log.ones)
+  // Log: beta relative to the integer offset Ob (t_renorm_shift); an arc's
+  // marginal exp(alpha + w + beta' - log_z) takes the large terms first,
+  // ((alpha - log_z) + Ob) + (w + beta'_rel)
+  float Ob = 0.f;
+  // the gradient of one arc: Log from (alpha - log_z + Ob) and w + beta'_rel;
+  // Real alpha * beta' (the weight not included)
+  auto mg = [&](float al_or_lo, float x) {
+    if constexpr (SR == M_LOG) return lt_exp(al_or_lo + x) * gb;
+    else return al_or_lo * x * gb;
+  };
+  // the alpha-side factor of mg: Log (alpha - log_z) + Ob, Real alpha
+  auto af = [&](float alv) {
+    if constexpr (SR == M_LOG) return (alv - lz) + Ob;
+    else return alv;
+  };
+  for (int q = tid; q < C; q += nthr) beta[q] = t_one<SR>();  // every state final
   __syncthreads();
   using DG = typename std::conditional<STAGE, DenGraphP, DenGraph>::type;
   DG dg{g_off, g_arc, V, R};
@@ -689,7 +861,7 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
       for (int q0 = 0; q0 < C; q0 += nthr / G) {
         const int q = q0 + tid / G;
         const bool valid = q < C;
-        const float r = t_reduce_g<M_LOG, G>(dg, q, valid, la + (long long)(i - 1) * C, wr, nullptr);
+        const float r = t_reduce_g<SR, G>(dg, q, valid, la + (long long)(i - 1) * C, wr, nullptr);
         if (valid && !(tid & (G - 1))) la[(long long)i * C + q] = r;
       }
       __syncthreads();
@@ -699,24 +871,27 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
     for (int p0 = 0; p0 < C; p0 += nthr / G) {
       const int p = p0 + tid / G;
       const bool valid = p < C;
-      const float bb = valid ? wr(p * R) + beta[p] : 0.f;
-      Lse s;
+      const float bb = valid ? t_times<SR>(wr(p * R), beta[p]) : 0.f;
+      OutSum<SR, G> s;
       if (K == 0 && valid) {
+        const float a0 = af(la[p]);
 #pragma unroll 4
         for (int y = 1 + jg; y <= V; y += G) {
-          const float lb = wr(p * R + y) + beta[g_tab[p * V + y - 1]];
-          stw<false>(a.dW, fo + p * R + y, lt_exp(la[p] + lb - lz));
+          const float bq = beta[g_tab[p * V + y - 1]];
+          const float lb = t_times<SR>(wr(p * R + y), bq);
+          stw<false>(a.dW, fo + p * R + y, mg(a0, SR == M_LOG ? lb : bq));
           s.add(lb);
         }
       }
-      lse_merge<G>(s);
+      const float sv = s.merge();
       if (!valid || jg) continue;
       if (K == 0) {
-        stw<false>(a.dW, fo + p * R, lt_exp(la[p] + bb - lz));
-        nbA[p] = t_lae(bb, s.get());
+        stw<false>(a.dW, fo + p * R, mg(af(la[p]), SR == M_LOG ? bb : beta[p]));
+        nbA[p] = t_plus<SR>(bb, sv);
       } else {
         float mb = 0.f;
-        for (int i = 0; i <= K; ++i) mb += lt_exp(la[(long long)i * C + p] + bb - lz);
+        for (int i = 0; i <= K; ++i)
+          mb += mg(af(la[(long long)i * C + p]), SR == M_LOG ? bb : beta[p]);
         stw<false>(a.dW, fo + p * R, mb);
         nbA[p] = bb;  // blank[K] + beta
       }
@@ -728,13 +903,14 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
       for (int p0 = 0; p0 < C; p0 += nthr / G) {
         const int p = p0 + tid / G;
         const bool valid = p < C;
-        Lse s;
+        OutSum<SR, G> s;
         if (valid) {
-          const float lj = la[(long long)j * C + p] - lz;
+          const float lj = af(la[(long long)j * C + p]);
 #pragma unroll 4
           for (int y = 1 + jg; y <= V; y += G) {
-            const float lb = wr(p * R + y) + cur[g_tab[p * V + y - 1]];
-            const float m = lt_exp(lb + lj);
+            const float cq = cur[g_tab[p * V + y - 1]];
+            const float lb = t_times<SR>(wr(p * R + y), cq);
+            const float m = mg(lj, SR == M_LOG ? lb : cq);
             const long long e = fo + p * R + y;
             // the same lane owns (p, y) for every j: accumulate in place
             // (in LDS when it fits; dW is written once, at j = 0)
@@ -748,16 +924,63 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
             s.add(lb);
           }
         }
-        lse_merge<G>(s);
-        if (valid && !jg) nxt[p] = t_lae(wr(p * R) + beta[p], s.get());
+        const float sv = s.merge();
+        if (valid && !jg) nxt[p] = t_plus<SR>(t_times<SR>(wr(p * R), beta[p]), sv);
       }
       __syncthreads();
       float* tmp = cur;
       cur = nxt;
       nxt = tmp;
     }
-    for (int p = tid; p < C; p += nthr) beta[p] = cur[p];
+    if constexpr (SR == M_LOG) {
+      const float sp = t_renorm_shift(cur, C);
+      for (int p = tid; p < C; p += nthr) beta[p] = cur[p] - sp;
+      Ob += sp;
+    } else {
+      for (int p = tid; p < C; p += nthr) beta[p] = cur[p];
+    }
     __syncthreads();
+  }
+}
+
+template <bool BF16, bool STAGE, int SR>
+__global__ __launch_bounds__(kTabMaxThreads) void tab_bwd_den_kernel(const TArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  tab_bwd_den_body<BF16, STAGE, SR>(a, (int)blockIdx.x, sm);
+}
+
+// MaxTropical: the gradient of the shortest distance is the best path's
+// indicator (semirings.py:354-401: the first maximum wins), times the
+// incoming gradient. One thread per utterance walks the Viterbi backpointers
+// (tab_fwd_kernel's VIT mode) as tab_backtrace_kernel does and adds g to
+// every arc the path takes -- the blank of the frame's end state and its
+// lexical arcs (alignment-state-invariant weights: an element taken twice in
+// one frame gets 2g). dW (fp32) is zeroed beforehand.
+__global__ void tab_onehot_kernel(const TArgs a) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.B) return;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const int K = a.K, KK = K > 0 ? K : 1;
+  const long long FR = (long long)a.C * a.R;
+  const float gb = a.gin ? a.gin[b] : 1.f;
+  int q = a.qstar[b];
+  for (int t = nf - 1; t >= 0; --t) {
+    float* dw = a.dW + ((long long)b * a.T + t) * FR;
+    const int* bpt = a.bp + (((long long)b * a.T + t) * KK) * a.C;
+    if (K > 0) dw[(long long)q * a.R] += gb;  // the end state's blank
+    const int i = K > 0 ? a.win[((long long)b * a.T + t) * a.C + q] : 1;
+    for (int j = i; j >= 1; --j) {
+      const int pos = bpt[(long long)(j - 1) * a.C + q];
+      if (pos < 0) {  // FrameDependent: the blank self loop won
+        dw[(long long)q * a.R] += gb;
+        break;
+      }
+      const int id = a.in_arc[pos];
+      const int p = id / a.V, y = id - p * a.V + 1;
+      dw[(long long)p * a.R + y] += gb;
+      q = p;
+    }
   }
 }
 
@@ -765,22 +988,21 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
 // The same recursion on the string acceptor; string arcs that share a lattice
 // arc are summed by their chain head in ascending order (one writer per
 // element and frame: deterministic).
-template <bool BF16, bool STAGE>
-__global__ __launch_bounds__(kTabMaxThreads) void tab_bwd_den_kernel(const TArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  tab_bwd_den_body<BF16, STAGE>(a, (int)blockIdx.x, sm);
-}
-
 template <bool BF16>
 LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int U = a.U, S = U + 1, K = a.K, NK = 2 * S;
-  float* beta = sm;
-  float* nbA = beta + S;
-  float* nbB = nbA + S;
-  float* mb = nbB + S;
+  // beta and the backward chain in the (i, f) representation of
+  // tab_str_fwd_log: integer parts and fractions
+  float* bi = sm;
+  float* bf = bi + S;
+  float* ai = bf + S;  // nbA
+  float* af = ai + S;
+  float* ci = af + S;  // nbB
+  float* cf = ci + S;
+  float* mb = cf + S;
   float* ml = mb + S;
-  float* la = ml + S;  // [K+1][S]
+  float* la = ml + S;  // [K+1][S]: alpha history row and its lexical chain (absolute)
   int* ctx = (int*)(la + (long long)(K + 1) * S);
   int* yn = ctx + S;
   int* link = yn + S;  // [NK]: head << 30 | (next entry + 1)
@@ -798,7 +1020,10 @@ LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
   }
   const int nl = a.nlab[b];
   if (tid == 0) t_walk(a, b, ctx, yn);
-  for (int u = tid; u < S; u += nthr) beta[u] = u == nl ? 0.f : -kInf;
+  for (int u = tid; u < S; u += nthr) {
+    bi[u] = u == nl ? 0.f : -kInf;
+    bf[u] = 0.f;
+  }
   __syncthreads();
   auto elem = [&](int k) {  // W element of string entry k = 2u + kind, or -1
     const int u = k >> 1;
@@ -842,6 +1067,9 @@ LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
     cs.fetch(2 * S, ldc(nf - 1));
     ds.fetch(NK, ldd(nf - 1));
   }
+  // a string arc's marginal exp(alpha + w + beta' - num), beta' = (i, f):
+  // the large terms first, ((alpha - num) + i) + (f + w)
+  auto marg = [&](float alv, float i, float f) { return lt_exp(((alv - nm) + i) + f); };
   for (int t = nf - 1; t >= 0; --t) {
     const long long fo = ((long long)b * a.T + t) * FR;
     hs.store(la, S, ldh(t));
@@ -858,33 +1086,38 @@ LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
       __syncthreads();
     }
     for (int u = tid; u < S; u += nthr) {
-      const float bb = wc[2 * u] + beta[u];
+      const float bbf = wc[2 * u] + bf[u];  // blank + beta: (bi[u], bbf)
       if (K == 0) {
-        const float lb = u < U ? wc[2 * u + 1] + beta[u + 1] : -kInf;
-        mb[u] = lt_exp(la[u] + bb - nm);
-        ml[u] = lt_exp(la[u] + lb - nm);
-        nbA[u] = t_lae(bb, lb);
+        const bool lex = u < U;
+        const float li = lex ? bi[u + 1] : -kInf, lf = lex ? wc[2 * u + 1] + bf[u + 1] : 0.f;
+        mb[u] = marg(la[u], bi[u], bbf);
+        ml[u] = lex ? marg(la[u], li, lf) : 0.f;
+        lae_split(bi[u], bbf, li, lf, ai[u], af[u]);
       } else {
-        float s = 0.f;
-        for (int i = 0; i <= K; ++i) s += lt_exp(la[(long long)i * S + u] + bb - nm);
-        mb[u] = s;
+        float sacc = 0.f;
+        for (int i = 0; i <= K; ++i) sacc += marg(la[(long long)i * S + u], bi[u], bbf);
+        mb[u] = sacc;
         ml[u] = 0.f;
-        nbA[u] = bb;
+        ai[u] = bi[u];  // next_beta = blank[K] + beta
+        af[u] = bbf;
       }
     }
     __syncthreads();
-    float* cur = nbA;
-    float* nxt = nbB;
+    float *pi = ai, *pf = af, *qi = ci, *qf = cf;
     for (int j = K - 1; j >= 0; --j) {
       for (int u = tid; u < S; u += nthr) {
-        const float lb = u < U ? wc[2 * u + 1] + cur[u + 1] : -kInf;
-        ml[u] += lt_exp(lb + la[(long long)j * S + u] - nm);
-        nxt[u] = t_lae(wc[2 * u] + beta[u], lb);
+        const bool lex = u < U;
+        const float li = lex ? pi[u + 1] : -kInf, lf = lex ? wc[2 * u + 1] + pf[u + 1] : 0.f;
+        if (lex) ml[u] += marg(la[(long long)j * S + u], li, lf);
+        lae_split(bi[u], wc[2 * u] + bf[u], li, lf, qi[u], qf[u]);
       }
       __syncthreads();
-      float* tmp = cur;
-      cur = nxt;
-      nxt = tmp;
+      float* t1 = pi;
+      pi = qi;
+      qi = t1;
+      t1 = pf;
+      pf = qf;
+      qf = t1;
     }
     for (int k = tid; k < NK; k += nthr) {
       const int lk = link[k];
@@ -896,7 +1129,10 @@ LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
       else stw<false>(a.dW, fo + elem(k), dh[k] - s);
     }
     __syncthreads();
-    for (int u = tid; u < S; u += nthr) beta[u] = cur[u];
+    for (int u = tid; u < S; u += nthr) {
+      bi[u] = pi[u];
+      bf[u] = pf[u];
+    }
     __syncthreads();
   }
 }
@@ -913,7 +1149,7 @@ template <bool BF16, bool STAGE>
 __global__ __launch_bounds__(kTabMaxThreads) void tab_bwd2_kernel(const TArgs ad, const TArgs an) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int blk = (int)blockIdx.x;
-  if (blk < ad.B) tab_bwd_den_body<BF16, STAGE>(ad, blk, sm);
+  if (blk < ad.B) tab_bwd_den_body<BF16, STAGE, M_LOG>(ad, blk, sm);
   else tab_bwd_num_body<BF16>(an, blk - ad.B, sm);
 }
 
@@ -1038,7 +1274,8 @@ int launch_t_fwd(int sr, bool num, bool vit, const TArgs& a0, hipStream_t st) {
   TArgs a = a0;
   const int S = num ? a.U + 1 : a.C;
   const long long FR = (long long)a.C * a.R;
-  const int lds = fwd_lds(S) + (num ? 8 * S : 0);  // + the string's compact weights
+  // + the string's compact weights and the Log string's (i, f) arrays
+  const int lds = fwd_lds(S) + (num ? 16 * S : 0);
   // STAGE: graph and frame in LDS (when both fit; the string forward reads
   // two weights per position and stages nothing)
   const long long staged = (long long)lds + graph_lds(a) + 4 * FR;
@@ -1158,7 +1395,7 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   an.dist = num;
   an.alpha = hn;
   if (!local_norm) {
-    const int ln = fwd_lds(S) + 8 * S;
+    const int ln = fwd_lds(S) + 16 * S;
     const int ld = fwd_lds(C);
     const long long staged = (long long)ld + graph_lds(a) + 4 * FR;
     if (staged <= kStageBudget) {
@@ -1196,7 +1433,7 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   ad.ntab = nullptr;
   an.hist = hn;
   const int lds_d = 4 * (3 * C + (K + 1) * C);
-  const int lds_n = 4 * (5 * S + (K + 1) * S) + 4 * (2 * S + 2 * S) + 4 * (2 * S + 2 * S);
+  const int lds_n = 4 * (8 * S + (K + 1) * S) + 4 * (2 * S + 2 * S) + 4 * (2 * S + 2 * S);
   if (lds_d + graph_lds(a) + 4 * FR <= kStageBudget) {
     // + the lexical dW sums of FrameLabelDependent(K > 0) when they fit too
     ad.acc = K > 0 && lds_d + graph_lds(a) + 8 * FR <= kStageBudget;
@@ -1221,6 +1458,108 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   if (blocks > 0)
     hipLaunchKernelGGL(tab_to_bf16_kernel, dim3(blocks), dim3(256), 0, st, dwf,
                        (unsigned short*)dW, n);
+  return t_hip(hipGetLastError(), "bf16 conversion launch");
+}
+
+// lt_table_den_backward's workspace: an fp32 gradient for bf16 W, and for
+// MaxTropical the Viterbi backpointers, winning expansion counts, best final
+// states and distances
+struct DenBwdLayout {
+  size_t dwf, bp, win, qstar, dist, total;
+};
+static DenBwdLayout den_bwd_layout(const lt_graph* g, const lt_table_problem* pb, int semiring) {
+  auto up = [](long long x) { return (size_t)((x + 255) & ~255LL); };
+  const long long BT = (long long)pb->batch * pb->max_frames;
+  const int KK = g->expansions > 0 ? g->expansions : 1;
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  DenBwdLayout l;
+  l.dwf = 0;
+  l.bp = (bf16 || semiring == M_MAX) ? up(4 * BT * g->num_states * (g->vocab_size + 1)) : 0;
+  l.win = l.bp;
+  l.qstar = l.bp;
+  l.dist = l.bp;
+  l.total = l.bp;
+  if (semiring == M_MAX) {
+    l.win = l.bp + up(4 * BT * KK * g->num_states);
+    l.qstar = l.win + up(BT * g->num_states);
+    l.dist = l.qstar + up(4LL * pb->batch);
+    l.total = l.dist + up(4LL * pb->batch);
+  }
+  return l;
+}
+
+int lt_table_den_backward_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
+                                          int32_t semiring, size_t* bytes) {
+  if (int rc = t_check(g, pb)) return rc;
+  if (semiring < 0 || semiring > 2) return t_fail(LT_EINVAL, "bad semiring");
+  if (bytes) *bytes = den_bwd_layout(g, pb, semiring).total;
+  return LT_OK;
+}
+
+int lt_table_den_backward(const lt_graph* g, const lt_table_problem* pb, int32_t semiring,
+                          const void* W, const int32_t* num_frames, const float* dist,
+                          const float* alpha, const float* grad, void* dW, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  if (int rc = t_check(g, pb)) return rc;
+  if (semiring < 0 || semiring > 2) return t_fail(LT_EINVAL, "bad semiring");
+  if (pb->batch == 0) return LT_OK;
+  const bool maxt = semiring == M_MAX;
+  if ((!W && pb->max_frames > 0) || !num_frames || (!dW && pb->max_frames > 0) ||
+      (!maxt && (!dist || (!alpha && pb->max_frames > 0))))
+    return t_fail(LT_EINVAL, "null pointer");
+  const DenBwdLayout l = den_bwd_layout(g, pb, semiring);
+  if (l.total && (!workspace || workspace_bytes < l.total))
+    return t_fail(LT_EINVAL, "workspace too small");
+  if (pb->max_frames == 0) return LT_OK;
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  hipStream_t st = (hipStream_t)stream;
+  float* dwf = bf16 ? (float*)((char*)workspace + l.dwf) : (float*)dW;
+  TArgs a = t_args(g, pb, W, num_frames);
+  a.gin = grad;
+  a.dW = dwf;
+  const int C = a.C, K = a.K;
+  const long long FR = (long long)C * a.R;
+  const long long n = (long long)a.B * a.T * FR;
+  int rc;
+  if (maxt) {
+    // the best path (tab_fwd_kernel VIT), then its arcs
+    a.bp = (int*)((char*)workspace + l.bp);
+    a.win = (unsigned char*)workspace + l.win;
+    a.qstar = (int*)((char*)workspace + l.qstar);
+    a.dist = (float*)((char*)workspace + l.dist);
+    if ((rc = t_fwd(M_MAX, false, true, a, bf16, st))) return rc;
+    if ((rc = t_hip(hipMemsetAsync(dwf, 0, sizeof(float) * n, st), "memset"))) return rc;
+    const int threads = 64;
+    hipLaunchKernelGGL(tab_onehot_kernel, dim3((a.B + threads - 1) / threads), dim3(threads), 0,
+                       st, a);
+    if ((rc = t_hip(hipGetLastError(), "one-hot launch"))) return rc;
+  } else {
+    a.hist = alpha;
+    a.den_in = dist;
+    a.num_in = dist;  // the den-only backward: live while the distance is finite
+    const int lds_d = 4 * (3 * C + (K + 1) * C);
+    if (lds_d + graph_lds(a) + 4 * FR <= kStageBudget) {
+      a.acc = K > 0 && lds_d + graph_lds(a) + 8 * FR <= kStageBudget;
+      const int lds = (int)(lds_d + graph_lds(a) + (a.acc ? 8 : 4) * FR);
+      if (semiring == M_LOG)
+        rc = bf16 ? t_launch(tab_bwd_den_kernel<true, true, M_LOG>, a.B, lds, st, a)
+                  : t_launch(tab_bwd_den_kernel<false, true, M_LOG>, a.B, lds, st, a);
+      else
+        rc = bf16 ? t_launch(tab_bwd_den_kernel<true, true, M_REAL>, a.B, lds, st, a)
+                  : t_launch(tab_bwd_den_kernel<false, true, M_REAL>, a.B, lds, st, a);
+    } else {
+      if (semiring == M_LOG)
+        rc = bf16 ? t_launch(tab_bwd_den_kernel<true, false, M_LOG>, a.B, lds_d, st, a)
+                  : t_launch(tab_bwd_den_kernel<false, false, M_LOG>, a.B, lds_d, st, a);
+      else
+        rc = bf16 ? t_launch(tab_bwd_den_kernel<true, false, M_REAL>, a.B, lds_d, st, a)
+                  : t_launch(tab_bwd_den_kernel<false, false, M_REAL>, a.B, lds_d, st, a);
+    }
+    if (rc) return rc;
+  }
+  if (!bf16) return LT_OK;
+  const int blocks = (int)std::min<long long>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(tab_to_bf16_kernel, dim3(blocks), dim3(256), 0, st, dwf, (unsigned short*)dW, n);
   return t_hip(hipGetLastError(), "bf16 conversion launch");
 }
 

@@ -9,7 +9,8 @@ weights once through the ``WeightFn`` plugin as a contiguous
   forward         -> lt_loss_grad (loss + dW, the design per shape);
                      lt_scale_grad in the backward; lt_loss_forward without grad
   _forward        -> lt_den_forward (Log, MaxTropical, Real);
-                     autograd: lt_den_backward (Log) / lt_viterbi arcs (Max)
+                     autograd: lt_den_backward (Log) / lt_viterbi arcs (Max) /
+                     lt_table_den_backward (Real)
   _forward_backward -> lt_den_forward + lt_den_backward
   _backward       -> lt_den_backward marginals, streamed to the callback
   _string_forward -> lt_num_forward
@@ -127,6 +128,18 @@ class _CpuLossFn(torch.autograd.Function):
 
   @staticmethod
   def backward(ctx, g):
+    if torch.is_grad_enabled():
+      # create_graph (higher-order gradients): the twin's dW is a constant,
+      # so the differentiable backward goes through cpu.py's autograd
+      W, nf, labels, nl = ctx.saved_tensors
+      V, n, local = ctx.cfg
+      loss = cpu.loss(W, nf.long(), labels, nl.long(),
+                      contexts.FullNGram(vocab_size=V, context_size=n),
+                      alignments.FrameDependent(), local)
+      fin = torch.isfinite(loss)
+      (dW,) = torch.autograd.grad(loss, W, torch.where(fin, g, torch.zeros_like(g)),
+                                  create_graph=True)
+      return dW, None, None, None, None, None, None
     dW = ctx.dW
     ctx.dW = None
     if dW is None:  # a second backward through the same graph
@@ -162,10 +175,11 @@ class _DenFn(torch.autograd.Function):
   best-path indicator (MaxTropical)."""
 
   @staticmethod
-  def forward(ctx, W, nf, V, n, sid):
+  def forward(ctx, W, nf, V, n, sid, graph=None):
     dist, alpha = _native.den_forward(W, nf, V, n, sid, want_alpha=True)
     ctx.save_for_backward(W, nf, dist, alpha)
     ctx.cfg = (V, n, sid)
+    ctx.graph = graph
     ctx.mark_non_differentiable(alpha)
     return dist, alpha
 
@@ -180,8 +194,56 @@ class _DenFn(torch.autograd.Function):
     elif sid == _native.SEMIRING_MAX:
       _, _, dW = _native.viterbi(W, nf, V, n, _native.LABELS_TRUE, grad=g, want_arcs=True)
     else:
-      raise NotImplementedError('gradients of the Real-semiring distance are not supported')
-    return dW, None, None, None, None
+      # Real (semirings.py:143-173, plain-arithmetic autograd in the
+      # reference): d dist / dW = alpha * beta' from the general table
+      # kernels on FullNGram.next_state_table() (the same state numbering)
+      if ctx.graph is None:
+        raise NotImplementedError('Real-semiring gradients need the lattice graph')
+      dW = _native.table_den_backward(ctx.graph, W, nf, sid, dist, alpha, g)
+    return dW, None, None, None, None, None
+
+
+class _TableDenFn(torch.autograd.Function):
+  """_forward's distance on the general table kernels (any next-state table,
+  FrameDependent or FrameLabelDependent); gradient lt_table_den_backward: the
+  arc marginals (Log), alpha * beta' (Real), the best path's arcs
+  (MaxTropical)."""
+
+  @staticmethod
+  def forward(ctx, W, nf, graph, sid):
+    dist, alpha = _native.table_forward(graph, W, nf, sid, want_alpha=True)
+    ctx.save_for_backward(W, nf, dist, alpha)
+    ctx.graph, ctx.sid = graph, sid
+    ctx.mark_non_differentiable(alpha)
+    return dist, alpha
+
+  @staticmethod
+  def backward(ctx, g, g_alpha):
+    del g_alpha
+    W, nf, dist, alpha = ctx.saved_tensors
+    dW = _native.table_den_backward(ctx.graph, W, nf, ctx.sid, dist, alpha, g.float())
+    return dW, None, None, None
+
+
+class _TableNumFn(torch.autograd.Function):
+  """_string_forward on the general table kernels; Log gradient = the string
+  marginals (lt_table_loss_grad with local normalisation gives -d num / dW)."""
+
+  @staticmethod
+  def forward(ctx, W, nf, labels, nl, graph, sid):
+    num = _native.table_num_forward(graph, W, nf, labels, nl, sid)
+    ctx.save_for_backward(W, nf, labels, nl)
+    ctx.graph, ctx.sid = graph, sid
+    return num
+
+  @staticmethod
+  def backward(ctx, g):
+    if ctx.sid != _native.SEMIRING_LOG:
+      raise NotImplementedError('string-distance gradients are supported for Log only')
+    W, nf, labels, nl = ctx.saved_tensors
+    _, _, _, dW = _native.table_loss_grad(ctx.graph, W, nf, labels, nl, True)
+    # an unreachable string has num = -inf and dW = 0 already
+    return dW * (-g).to(dW.dtype)[:, None, None, None], None, None, None, None, None
 
 
 class _NumFn(torch.autograd.Function):
@@ -392,9 +454,8 @@ class RecognitionLattice(nn.Module, Generic[T]):
     nl = _lengths(num_labels, B, W.device)
     if W.device.type == 'cpu':
       num = cpu.num_forward(W, nf, lab, nl.long(), self.context, self.alignment, semiring)
-    elif self._table_path():  # values only: gradients come through forward()
-      num = _native.table_num_forward(self._graph(W.device), W.detach(), nf, lab.contiguous(),
-                                      nl, sid)
+    elif self._table_path():
+      num = _TableNumFn.apply(W, nf, lab.contiguous(), nl, self._graph(W.device), sid)
     else:
       num = _NumFn.apply(W, nf, lab.contiguous(), nl, V, n, sid)
     return self._home(num.reshape(batch_dims), frames)
@@ -450,10 +511,11 @@ class RecognitionLattice(nn.Module, Generic[T]):
       return (dist.reshape(batch_dims),
               alpha.reshape(*batch_dims, frames.shape[-2], C))
     Wk = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
-    if table:  # values only: gradients come through forward() / shortest_path()
-      dist, alpha = _native.table_forward(self._graph(Wk.device), Wk.detach(), nf, sid)
+    if table:
+      dist, alpha = _TableDenFn.apply(Wk, nf, self._graph(Wk.device), sid)
     else:
-      dist, alpha = _DenFn.apply(Wk, nf, V, n, sid)
+      graph = self._graph(Wk.device) if sid == _native.SEMIRING_REAL else None
+      dist, alpha = _DenFn.apply(Wk, nf, V, n, sid, graph)
     C = alpha.shape[-1]
     return (self._home(dist.reshape(batch_dims), frames),
             self._home(alpha.reshape(*batch_dims, frames.shape[-2], C), frames))
@@ -462,13 +524,13 @@ class RecognitionLattice(nn.Module, Generic[T]):
     """(log Z, sum over arcs of m(arc) * w(arc)) per utterance, m the arc
     marginals (the gradient of log Z: the den backward kernel on a ROCm
     device, autograd through cpu.py on the CPU). FullNGram x FrameDependent."""
-    if self._table_path():
-      raise NotImplementedError('the expectation path covers FullNGram x FrameDependent lattices')
     W, nf, batch_dims, B, V, n, _ = self._prepare(cache, frames, num_frames)
     with torch.enable_grad():
       Wd = W.detach().requires_grad_(True)
       if Wd.device.type == 'cpu':
         log_z, _ = cpu.den_forward(Wd, nf, self.context, self.alignment, semirings.Log)
+      elif self._table_path():
+        log_z, _ = _TableDenFn.apply(Wd, nf, self._graph(Wd.device), _native.SEMIRING_LOG)
       else:
         log_z, _ = _DenFn.apply(Wd, nf, V, n, _semiring_id(semirings.Log))
       (m,) = torch.autograd.grad(log_z.sum(), Wd)
@@ -547,12 +609,18 @@ class RecognitionLattice(nn.Module, Generic[T]):
         (marg,) = torch.autograd.grad(dist.sum(), Wd)
       marg = marg.reshape(*batch_dims, *marg.shape[1:])
     else:
-      V, n = self._ngram()
       with torch.no_grad():
         Wk = _kernel_weights(W.to(dev).reshape(B, *W.shape[-3:]))
         lz = log_z.detach().reshape(B).to(dev, torch.float32).contiguous()
         al = alpha_0_to_T_minus_1.detach().reshape(B, Wk.shape[1], -1).to(dev, torch.float32)
-        marg = _native.den_backward(Wk, nf, lz, al.contiguous(), None, V, n).float()
+        if self._table_path():
+          # any next-state table, FrameDependent or FrameLabelDependent
+          # (self.alignment.backward, lattices.py:764)
+          marg = _native.table_den_backward(self._graph(dev), Wk, nf, _native.SEMIRING_LOG, lz,
+                                            al.contiguous()).float()
+        else:
+          V, n = self._ngram()
+          marg = _native.den_backward(Wk, nf, lz, al.contiguous(), None, V, n).float()
         marg = self._home(marg.reshape(*batch_dims, *marg.shape[1:]), frames)
     tdim = len(batch_dims)
     carry, outs = init_callback_carry, []

@@ -118,39 +118,45 @@ class _LogSumExpFn(torch.autograd.Function):
   """logsumexp along ``dim`` with the reference's safe max.
 
   Gradient: softmax weights; 0 for -inf operands, NaN where an operand is
-  +inf (an overflow upstream should not be silenced).
+  +inf (an overflow upstream should not be silenced). The backward
+  recomputes the weights from the saved operand with differentiable ops,
+  so higher-order gradients (create_graph) work.
   """
 
   @staticmethod
   def forward(ctx, a, dim):
     c = _safe_shift(torch.amax(a, dim=dim, keepdim=True))
-    e = torch.exp(a - c)
-    z = torch.sum(e, dim=dim, keepdim=True)
-    ctx.save_for_backward(e, z)
+    z = torch.sum(torch.exp(a - c), dim=dim, keepdim=True)
+    ctx.save_for_backward(a)
     ctx.dim = dim
     return torch.squeeze(c + torch.log(z), dim)
 
   @staticmethod
   def backward(ctx, g):
-    e, z = ctx.saved_tensors
+    (a,) = ctx.saved_tensors
+    c = _safe_shift(torch.amax(a.detach(), dim=ctx.dim, keepdim=True))
+    e = torch.exp(a - c)
+    z = torch.sum(e, dim=ctx.dim, keepdim=True)
     z = torch.where(z != 0, z, torch.ones_like(z))
     return torch.unsqueeze(g, ctx.dim) * e / z, None
 
 
 class _LogAddExpFn(torch.autograd.Function):
-  """Binary logaddexp with the same safety rules (semirings.py:244-272)."""
+  """Binary logaddexp with the same safety rules (semirings.py:244-272);
+  differentiable backward as _LogSumExpFn."""
 
   @staticmethod
   def forward(ctx, a, b):
     c = _safe_shift(torch.maximum(a, b))
-    ea, eb = torch.exp(a - c), torch.exp(b - c)
-    z = ea + eb
-    ctx.save_for_backward(ea, eb, z)
-    return c + torch.log(z)
+    ctx.save_for_backward(a, b)
+    return c + torch.log(torch.exp(a - c) + torch.exp(b - c))
 
   @staticmethod
   def backward(ctx, g):
-    ea, eb, z = ctx.saved_tensors
+    a, b = ctx.saved_tensors
+    c = _safe_shift(torch.maximum(a.detach(), b.detach()))
+    ea, eb = torch.exp(a - c), torch.exp(b - c)
+    z = ea + eb
     s = g / torch.where(z != 0, z, torch.ones_like(z))
     return s * ea, s * eb
 

@@ -42,18 +42,22 @@ def local_shard(num_frames, rank: int, world_size: int) -> np.ndarray:
 
 
 def all_reduce_step(loss: torch.Tensor, params: Iterable[torch.nn.Parameter] = (),
-                    group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+                    group: Optional[dist.ProcessGroup] = None,
+                    skip_unused: bool = False) -> torch.Tensor:
   """The step's single collective: all-reduce(SUM) of [loss.sum() || grads].
 
   Parameter gradients are summed in place (callers that want the mean
   divide by the global utterance count). Returns the global loss sum.
-  Without an initialised process group this is the identity. A parameter
-  without a gradient on this rank (unused, or an empty shard) contributes
-  zeros to the bucket, so every rank all-reduces the same layout, and its
-  .grad stays None here: an optimizer does not treat it as trained, and the
-  other ranks' sum for it is not applied on this rank. Where a parameter
-  can be unused on some ranks only, GradBucket (every parameter always has
-  its gradient view) keeps the ranks' updates identical."""
+  Without an initialised process group this is the identity.
+
+  A parameter without a gradient on this rank (unused here, or an empty
+  shard) contributes zeros, so every rank all-reduces the same layout, and
+  by default receives the summed gradient as a fresh .grad: every rank ends
+  the step with the same gradients, so the replicas' optimizer updates stay
+  identical. ``skip_unused=True`` leaves such a .grad None on this rank
+  (the other ranks' sum is then not applied here, and the replicas may
+  drift apart; only for callers that re-synchronise parameters
+  themselves)."""
   total = loss.detach().sum().reshape(1).to(torch.float32)
   if not (dist.is_available() and dist.is_initialized()):
     return total[0]
@@ -67,8 +71,11 @@ def all_reduce_step(loss: torch.Tensor, params: Iterable[torch.nn.Parameter] = (
   off = 1
   for p in params:
     k = p.numel()
+    red = flat[off:off + k].view(p.shape)
     if p.grad is not None:
-      p.grad.copy_(flat[off:off + k].view_as(p.grad).to(p.grad.dtype))
+      p.grad.copy_(red.to(p.grad.dtype))
+    elif not skip_unused:
+      p.grad = red.to(p.dtype).clone()
     off += k
   return flat[0]
 

@@ -53,7 +53,9 @@ def lib():
     l.tab_loss_grad.argtypes = ([_c_int] * 6 + [_I, _F, _I, _I, _I, _c_int, ctypes.c_void_p,
                                                  _F, _F, _F, ctypes.c_void_p])
     l.tab_viterbi.argtypes = [_c_int] * 5 + [_I, _F, _I, _c_int, _L, _F]
-    for f in ('tab_den_forward', 'tab_num_forward', 'tab_loss_grad', 'tab_viterbi'):
+    l.tab_den_grad.argtypes = [_c_int] * 5 + [_I, _F, _I, _F, _F]
+    for f in ('tab_den_forward', 'tab_num_forward', 'tab_loss_grad', 'tab_viterbi',
+              'tab_den_grad'):
       getattr(l, f).restype = None
     _lib = l
   return _lib
@@ -194,6 +196,16 @@ def tab_loss_grad(table, W, num_frames, labels, num_labels, K, local_norm=False,
   lib().tab_loss_grad(B, T, U, C, V, K, table, W, _i32(num_frames), labels, _i32(num_labels),
                       int(bool(local_norm)), _ptr(g), loss, lz, num, _ptr(dW))
   return loss, lz, num, dW
+
+
+def tab_den_grad(table, W, num_frames, K):
+  """(log_z [B], d log_z / dW [B,T,C,V+1]): the denominator's arc marginals
+  for any next-state table and alignment K."""
+  table, W, B, T, C, V = _tab(table, W)
+  lz = np.zeros([B], np.float32)
+  dW = np.zeros_like(W)
+  lib().tab_den_grad(B, T, C, V, K, table, W, _i32(num_frames), lz, dW)
+  return lz, dW
 
 
 def tab_viterbi(table, W, num_frames, K, convention=1):

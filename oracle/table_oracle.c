@@ -427,6 +427,31 @@ void tab_loss_grad(int B, int T, int U, int C, int V, int K, const int* table, c
   graph_free(&gd);
 }
 
+/* d log_z / dW alone (the denominator's arc marginals; the gradient of
+ * _forward's Log distance, lattices.py:379-496, and the marginals _backward
+ * streams, lattices.py:686-799): backward_d over the context graph, as in
+ * tab_loss_grad without the string. Utterances whose log_z is not finite
+ * get zeros. */
+void tab_den_grad(int B, int T, int C, int V, int K, const int* table, const float* W,
+                  const int* nf, float* log_z, float* dW) {
+  graph_t gd;
+  context_graph(C, V, table, &gd);
+  const long long FR = (long long)C * (V + 1);
+  double* hd = (double*)malloc(sizeof(double) * (size_t)(T + 1) * C);
+  double* acc = (double*)malloc(sizeof(double) * (size_t)(T > 0 ? T : 1) * FR);
+  for (int b = 0; b < B; ++b) {
+    const int nfb = nf[b] < 0 ? 0 : (nf[b] > T ? T : nf[b]);
+    const float* Wb = W + (long long)b * T * FR;
+    const double lz = forward_d(&gd, K, TAB_LOG, T, FR, Wb, nfb, 0, hd, NULL, -1);
+    memset(acc, 0, sizeof(double) * (size_t)T * FR);
+    if (isfinite(lz)) backward_d(&gd, K, FR, Wb, nfb, hd, lz, -1, 1.0, acc);
+    for (long long e = 0; e < (long long)T * FR; ++e) dW[(long long)b * T * FR + e] = (float)acc[e];
+    if (log_z) log_z[b] = (float)lz;
+  }
+  free(hd); free(acc);
+  graph_free(&gd);
+}
+
 /* RecognitionLattice.shortest_path per utterance (no D6 aliasing):
  * labels [B, T*A] (A = 1 for FrameDependent, K+1 for FrameLabelDependent):
  * slot i of frame t holds the label of the (i+1)-th lexical arc taken in

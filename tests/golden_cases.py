@@ -87,22 +87,49 @@ def marginal_scale(ref, den, log_z, num, bf16=False):
   return 1e-8 + rel.reshape([-1] + [1] * (ref.ndim - 1)) * (den + nm)
 
 
-def grad_error_ratio(got, ref, den, log_z, num, bf16=False):
-  """|got - ref| / marginal_scale: <= 1 everywhere passes."""
+def grad_error_ratio(got, ref, den, log_z, num, bf16=False, weights=None):
+  """|got - ref| / marginal_scale: <= 1 everywhere passes. `weights` [B]:
+  got is the gradient of sum_b weights_b * loss_b, so ref and the bound are
+  both scaled by weights_b (a zero weight demands an exact zero)."""
   got = np.asarray(got, np.float64)
   ref = np.asarray(ref, np.float64)
-  return np.abs(got - ref) / marginal_scale(ref, den, log_z, num, bf16)
+  scale = marginal_scale(ref, den, log_z, num, bf16)
+  if weights is not None:
+    w = np.asarray(weights, np.float64).reshape([-1] + [1] * (ref.ndim - 1))
+    ref = ref * w
+    scale = scale * np.abs(w) + np.where(w == 0, 0.0, 1e-12)
+    with np.errstate(divide='ignore', invalid='ignore'):
+      r = np.abs(got - ref) / scale
+    return np.where((w == 0) & (got == 0), 0.0, np.where(w == 0, np.inf, r))
+  return np.abs(got - ref) / scale
 
 
-def assert_grad_marginal_close(got, ref, den, log_z, num, bf16=False):
+def assert_grad_marginal_close(got, ref, den, log_z, num, bf16=False, weights=None):
   """Every dW element within marginal_scale (relative to its own marginals),
-  plus the absolute check of assert_grad_close as a secondary bound."""
-  r = grad_error_ratio(got, ref, den, log_z, num, bf16)
+  plus the absolute check of assert_grad_close as a secondary bound. `den`
+  the arc's denominator marginals (the oracle's den_grad; None for a locally
+  normalised loss); for a denominator-only gradient (d log_z / dW) pass
+  ref = den and num = None. `weights`: see grad_error_ratio."""
+  r = grad_error_ratio(got, ref, den, log_z, num, bf16, weights)
   bad = ~(r <= 1.0)
   assert not bad.any(), (f'{int(bad.sum())} of {bad.size} dW elements beyond the marginal bound; '
                          f'worst ratio {float(np.nanmax(r)):.3g} at '
                          f'{np.argwhere(bad)[0].tolist()}')
-  assert_grad_close(got, ref, log_z, bf16=bf16, num=num)
+  if weights is None:
+    assert_grad_close(got, ref, log_z, bf16=bf16, num=num)
+  else:
+    w = np.asarray(weights, np.float64)
+    assert_grad_close(got, np.asarray(ref, np.float64) * w.reshape([-1] + [1] * (np.ndim(ref) - 1)),
+                      np.asarray(log_z, np.float64) * np.maximum(np.abs(w), 1e-30), bf16=bf16,
+                      num=None if num is None else np.asarray(num, np.float64) * np.abs(w))
+
+
+def table_den_marginals(orc, table, W, nf, lab, nl, K):
+  """Denominator arc marginals d log_z / dW of a table lattice from the
+  pinned table oracle (tab_den_grad; the string arguments are not used).
+  Test infrastructure."""
+  del lab, nl
+  return orc.tab_den_grad(table, W, nf, K)[1].astype(np.float64)
 
 
 def assert_grad_close(got, ref, log_z, bf16=False, num=None):

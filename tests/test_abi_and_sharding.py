@@ -37,7 +37,7 @@ def _header_define(name):
 
 def test_library_exports_every_declared_symbol():
   declared = _declared_functions()
-  assert len(declared) == 32, declared
+  assert len(declared) == 34, declared
   lib = _native.lib()
   for name in declared:
     assert hasattr(lib, name), f'{name} declared in lt_lattice.h but not exported'
@@ -126,13 +126,23 @@ def _gloo_worker(rank, world, port, payload, out_q):
       assert head.grad.data_ptr() == bucket.flat[1:].data_ptr()
       totals.append(float(bucket.all_reduce_step(loss)))
       head_grads.append(head.grad.numpy().copy())
-    # the functional form: a parameter unused on this rank keeps grad None
+    # the functional form: a parameter used on rank 1 only gets the same
+    # reduced .grad on both ranks (identical replica updates); with
+    # skip_unused its .grad stays None on the rank that did not use it
     p = torch.nn.Parameter(torch.zeros(5))
-    unused = torch.nn.Parameter(torch.zeros(3))
+    partial = torch.nn.Parameter(torch.zeros(3))
     p.grad = torch.full([5], float(rank + 1))
-    total3 = float(sharding.all_reduce_step(loss, [p, unused]))
+    if rank == 1:
+      partial.grad = torch.tensor([1.0, 2.0, 3.0])
+    total3 = float(sharding.all_reduce_step(loss, [p, partial]))
+    skipped = torch.nn.Parameter(torch.zeros(2))
+    if rank == 1:
+      skipped.grad = torch.ones(2)
+    sharding.all_reduce_step(loss, [skipped], skip_unused=True)
+    skip_ok = (skipped.grad is None) if rank == 0 else bool((skipped.grad == 1).all())
     out_q.put((rank, idx, loss.detach().numpy(), table.grad.numpy().copy(), totals, head_grads,
-               p.grad.numpy().copy(), unused.grad is None, total3, bucket.calls))
+               p.grad.numpy().copy(), partial.grad.numpy().copy(), skip_ok, total3,
+               bucket.calls))
   finally:
     dist.destroy_process_group()
 
@@ -165,7 +175,7 @@ def test_gloo_world2_sharded_loss_matches_full_batch():
     assert p.exitcode == 0
   loss = np.zeros(B, np.float32)
   dW = np.zeros_like(full_dW)
-  for rank, idx, l, g, totals, head_grads, pgrad, unused_none, total3, calls in res:
+  for rank, idx, l, g, totals, head_grads, pgrad, partial_grad, skip_ok, total3, calls in res:
     loss[idx] = l
     dW[idx] = g
     for total in totals + [total3]:
@@ -174,7 +184,8 @@ def test_gloo_world2_sharded_loss_matches_full_batch():
     for hg in head_grads:
       np.testing.assert_allclose(hg, full_dW.sum(axis=(0, 1)), atol=1e-5)
     np.testing.assert_array_equal(pgrad, np.full(5, 3.0))  # 1 + 2
-    assert unused_none
+    np.testing.assert_array_equal(partial_grad, [1.0, 2.0, 3.0])  # same on both ranks
+    assert skip_ok
     assert calls == 2  # one all-reduce per step
   np.testing.assert_allclose(loss, full_loss, rtol=1e-5, atol=1e-5)
   np.testing.assert_allclose(dW, full_dW, atol=1e-5)

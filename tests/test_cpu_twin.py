@@ -188,3 +188,43 @@ def test_errors():
     cpu.den_forward(W, torch.tensor([2]), 0, 1, LOG)
   with pytest.raises(Exception, match='semiring'):
     cpu.den_forward(W, torch.tensor([2]), 2, 1, 7)
+
+
+def test_twin_double_backward_matches_cpu_autograd():
+  """create_graph through RecognitionLattice.forward on host tensors: the
+  twin's constant dW cannot carry a second derivative, so its backward goes
+  through cpu.py's autograd; the gradient of |dL/dW|^2 matches cpu.py's own
+  double backward."""
+  import last_torch_amd as lt
+  from last_torch_amd import cpu as cpu_path
+  rng = np.random.default_rng(8)
+  B, T, U, V, n = 3, 7, 3, 3, 1
+  W = rng.standard_normal((B, T, V + 1, V + 1)).astype(np.float32)
+  nf = torch.tensor([7, 5, 3])
+  lab = torch.tensor(rng.integers(1, V + 1, (B, U)))
+  nl = torch.tensor([3, 2, 1])
+  table = torch.tensor(W, requires_grad=True)
+  lat = lt.RecognitionLattice(
+      context=lt.contexts.FullNGram(vocab_size=V, context_size=n),
+      alignment=lt.alignments.FrameDependent(),
+      weight_fn_cacher_factory=lambda _: lt.weight_fns.NullCacher(),
+      weight_fn_factory=lambda _: lt.weight_fns.TableWeightFn(table))
+  frames = torch.arange(T, dtype=torch.float32)[None, :, None].expand(B, T, 1)
+  loss = lat(frames, nf, lab, nl)
+  (g,) = torch.autograd.grad(loss.sum(), table, create_graph=True)
+  (h,) = torch.autograd.grad((g * g).sum(), table)
+  Wr = torch.tensor(W, requires_grad=True)
+  ref = cpu_path.loss(Wr, nf, lab, nl, lt.contexts.FullNGram(vocab_size=V, context_size=n),
+                      lt.alignments.FrameDependent(), False)
+  (gr,) = torch.autograd.grad(ref.sum(), Wr, create_graph=True)
+  (hr,) = torch.autograd.grad((gr * gr).sum(), Wr)
+  np.testing.assert_allclose(g.detach().numpy(), gr.detach().numpy(), atol=1e-5)
+  np.testing.assert_allclose(h.numpy(), hr.numpy(), atol=1e-4)
+  assert h.abs().sum() > 0
+
+
+def test_worker_count_follows_affinity():
+  """The default pool is the process's affinity mask, not the machine."""
+  import os
+  cpu.set_num_threads(0)
+  assert cpu.num_threads() == len(os.sched_getaffinity(0))

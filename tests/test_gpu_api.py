@@ -9,7 +9,7 @@ import torch
 
 import last_torch_amd as lt
 from last_torch_amd import _native as nat
-from golden_cases import assert_grad_close, assert_loss_close, load
+from golden_cases import assert_grad_marginal_close, assert_loss_close, load
 from test_lattice_api import (CASES, check_backward_callback, check_backward_vjp,
                               check_forward_gradients)
 
@@ -56,8 +56,8 @@ def test_loss_autograd_contract(cuda, V, n):
   w = torch.linspace(-1.0, 2.0, B, device=cuda)
   (w * loss).sum().backward(retain_graph=True)
   g1 = table.grad.clone()
-  assert_grad_close(g1.cpu().numpy(), rdW * w.cpu().numpy()[:, None, None, None],
-                    rlz * np.abs(w.cpu().numpy()).max(), num=rnum)
+  den = orc.den_grad(W, nf, V, n)[1]
+  assert_grad_marginal_close(g1.cpu().numpy(), rdW, den, rlz, rnum, weights=w.cpu().numpy())
   table.grad = None
   (w * loss).sum().backward()
   assert torch.equal(table.grad, g1)

@@ -7,7 +7,9 @@ Oracles: the reference's own FrameLabelDependent fixtures
 FullNGram.next_state_table()), and the pinned table oracle
 (oracle/table_oracle.c) for random DFAs. Tolerances as test_gpu_parity.py:
 Log values 1e-4 * max(1, |ref|); MaxTropical values and Viterbi labels
-bit-exact; gradients per golden_cases.assert_grad_close.
+bit-exact; dW element by element within golden_cases.marginal_scale
+(relative to the arc's own den + num marginals; the den marginals from the
+fixture's den_grad or, for random tables, golden_cases.table_den_marginals).
 """
 import numpy as np
 import pytest
@@ -15,8 +17,8 @@ import torch
 
 import last_torch_amd as lt
 from last_torch_amd import _native as nat
-from golden_cases import (FLD_CASES, LATTICE_CASES, assert_grad_close, assert_loss_close,
-                          assert_values_close, load, load_fld)
+from golden_cases import (FLD_CASES, LATTICE_CASES, assert_grad_marginal_close, assert_loss_close,
+                          assert_values_close, load, load_fld, table_den_marginals)
 
 pytestmark = pytest.mark.gpu
 
@@ -57,7 +59,8 @@ def _check_case(c, K, cuda, bf16=False):
       assert_values_close(d, c['den_Real'], **_real_tol(c['den_Real']))
   loss, lz, _, dW = nat.table_loss_grad(g, W, nf, lab, nl, False)
   assert_loss_close(loss.cpu().numpy(), c['loss'])
-  assert_grad_close(dW.float().cpu().numpy(), c['loss_grad'], c['den_Log'], bf16)
+  assert_grad_marginal_close(dW.float().cpu().numpy(), c['loss_grad'], c['den_grad'], c['den_Log'],
+                             c['num_Log'], bf16)
   for conv in (0, 1):
     labels, w = nat.table_viterbi(g, W, nf, conv)
     rl, rw = orc.tab_viterbi(table, c['W'], c['num_frames'], K, conv)
@@ -121,11 +124,13 @@ def test_random_dfa_vs_oracle(cuda, C, V, K, B, T, U, dt):
     else:
       assert_loss_close(d.cpu().numpy(), rd)
       assert_loss_close(num.cpu().numpy(), rn)
+  den = table_den_marginals(orc, table, W, nf, lab, nl, K)
   for local in (False, True):
     loss, lz, _, dW = nat.table_loss_grad(g, Wd, nfd, labd, nld, local)
-    rl, rlz, _, rdW = orc.tab_loss_grad(table, W, nf, lab, nl, K, local_norm=local)
+    rl, rlz, rnum, rdW = orc.tab_loss_grad(table, W, nf, lab, nl, K, local_norm=local)
     assert_loss_close(loss.cpu().numpy(), rl)
-    assert_grad_close(dW.float().cpu().numpy(), rdW, rlz, bf16)
+    assert_grad_marginal_close(dW.float().cpu().numpy(), rdW, None if local else den, rlz, rnum,
+                               bf16)
   labels, w = nat.table_viterbi(g, Wd, nfd, 0)
   rlab, rw = orc.tab_viterbi(table, W, nf, K, 0)
   np.testing.assert_array_equal(w.cpu().numpy(), rw)
@@ -161,11 +166,12 @@ def test_frame_label_dependent_api(cuda):
   fin = torch.isfinite(loss.detach())
   loss.masked_fill(~fin, 0).sum().backward()
   tab = orc.full_ngram_table(V, n)
-  rl, rlz, _, rdW = orc.tab_loss_grad(tab, W, num_frames.numpy().astype(np.int32),
-                                      labels.numpy().astype(np.int32),
-                                      num_labels.numpy().astype(np.int32), K)
+  args = (num_frames.numpy().astype(np.int32), labels.numpy().astype(np.int32),
+          num_labels.numpy().astype(np.int32), K)
+  rl, rlz, rnum, rdW = orc.tab_loss_grad(tab, W, *args)
   assert_loss_close(loss.detach().cpu().numpy(), rl)
-  assert_grad_close(table.grad.cpu().numpy(), rdW, rlz)
+  assert_grad_marginal_close(table.grad.cpu().numpy(), rdW, table_den_marginals(orc, tab, W, *args),
+                             rlz, rnum, weights=fin.float().cpu().numpy())
   al, nal, pw = lat.shortest_path(frames, num_frames)
   np.testing.assert_array_equal(nal.numpy(), 3 * num_frames.numpy())
   is_padding = torch.arange(18) >= nal[:, None]
@@ -177,7 +183,7 @@ def test_frame_label_dependent_api(cuda):
   assert ((al >= 0) & (al <= V)).all()
   assert torch.isfinite(pw).all()
   d, _ = lat._forward(None, frames, num_frames, lt.semirings.MaxTropical)
-  np.testing.assert_array_equal(pw.cpu().numpy(), d.cpu().numpy())
+  np.testing.assert_array_equal(pw.cpu().numpy(), d.detach().cpu().numpy())
 
 
 def test_next_state_table_api(cuda):
@@ -201,16 +207,45 @@ def test_next_state_table_api(cuda):
     loss = lat(frames, torch.tensor(nf), torch.tensor(lab), torch.tensor(nl))
     fin = torch.isfinite(loss.detach())
     loss.masked_fill(~fin, 0).sum().backward()
-    rl, rlz, _, rdW = orc.tab_loss_grad(tab, W, nf, lab, nl, K)
+    rl, rlz, rnum, rdW = orc.tab_loss_grad(tab, W, nf, lab, nl, K)
     assert_loss_close(loss.detach().cpu().numpy(), rl)
-    assert_grad_close(table.grad.cpu().numpy(), rdW, rlz)
+    assert_grad_marginal_close(table.grad.cpu().numpy(), rdW,
+                               table_den_marginals(orc, tab, W, nf, lab, nl, K), rlz, rnum,
+                               weights=fin.float().cpu().numpy())
     d, _ = lat._forward(None, frames, torch.tensor(nf), lt.semirings.Log)
-    assert_loss_close(d.cpu().numpy(), orc.tab_den_forward(tab, W, nf, K, orc.LOG))
+    assert_loss_close(d.detach().cpu().numpy(), orc.tab_den_forward(tab, W, nf, K, orc.LOG))
     s = lat._string_forward(None, frames, torch.tensor(nf), torch.tensor(lab), torch.tensor(nl),
                             lt.semirings.MaxTropical)
-    np.testing.assert_array_equal(s.cpu().numpy(),
+    np.testing.assert_array_equal(s.detach().cpu().numpy(),
                                   orc.tab_num_forward(tab, W, nf, lab, nl, K, orc.MAX))
     al, nal, pw = lat.shortest_path(frames, torch.tensor(nf), label_convention='true')
     rlab, rw = orc.tab_viterbi(tab, W, nf, K, 0)
     np.testing.assert_array_equal(al.cpu().numpy(), rlab)
     np.testing.assert_array_equal(pw.cpu().numpy(), rw)
+
+
+def test_fld_k2_bigram_full_length(cuda):
+  """FrameLabelDependent(K=2) bigram at B=8, T=1000, U=100, V=32 (the
+  general table kernels at the BASELINE frame count): loss, log_z and every
+  dW element against the table oracle under the per-element marginal bound,
+  the string-only gradient (local normalisation) too."""
+  orc = _orc()
+  V, n, K, B, T, U = 32, 1, 2, 8, 1000, 100
+  rng = np.random.default_rng(1000)
+  tab = orc.full_ngram_table(V, n)
+  W = rng.standard_normal((B, T, V + 1, V + 1)).astype(np.float32)
+  nf = rng.integers(T // 2, T + 1, B).astype(np.int32)
+  nf[0] = T
+  lab = rng.integers(1, V + 1, (B, U)).astype(np.int32)
+  nl = rng.integers(U // 2, U + 1, B).astype(np.int32)
+  g = nat.TableGraph(tab, K, cuda)
+  Wd = torch.tensor(W, device=cuda)
+  nfd, labd, nld = (torch.tensor(x, device=cuda) for x in (nf, lab, nl))
+  den = table_den_marginals(orc, tab, W, nf, lab, nl, K)
+  for local in (False, True):
+    loss, lz, _, dW = nat.table_loss_grad(g, Wd, nfd, labd, nld, local)
+    rl, rlz, rnum, rdW = orc.tab_loss_grad(tab, W, nf, lab, nl, K, local_norm=local)
+    assert_loss_close(loss.cpu().numpy(), rl)
+    if not local:
+      assert_loss_close(lz.cpu().numpy(), rlz)
+    assert_grad_marginal_close(dW.cpu().numpy(), rdW, None if local else den, rlz, rnum)

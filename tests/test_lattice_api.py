@@ -14,7 +14,7 @@ import pytest
 import torch
 
 import last_torch_amd as lt
-from golden_cases import LATTICE_CASES, assert_grad_close, assert_loss_close, load
+from golden_cases import LATTICE_CASES, assert_grad_marginal_close, assert_loss_close, load
 
 CASES = [c for c in LATTICE_CASES if c in ('kat', 'bigram_v3', 'trigram_v2', 'cfg1', 'peaked',
                                             'unigram_v3')]
@@ -49,7 +49,8 @@ def check_backward_callback(c, device):
   assert carry == T and len(seen) == T
   seen.reverse()  # visited T-1 .. 0
   marg = np.stack([np.concatenate([b[..., None], l], axis=-1) for b, l in seen], axis=1)
-  assert_grad_close(marg, c['den_grad'], c['den_Log'])
+  # every element relative to its own marginal (den-only: ref = den, no num)
+  assert_grad_marginal_close(marg, c['den_grad'], c['den_grad'], c['den_Log'], None)
   # outputs stacked in time order along the frame axis
   np.testing.assert_allclose(outs.cpu().numpy(), marg[..., 0].sum(-1), rtol=1e-6, atol=1e-6)
 
@@ -88,7 +89,8 @@ def check_forward_gradients(c, device):
   dist, _ = _table_lattice(c, table)._forward(None, _frames(B, T, device), nf, lt.semirings.Log)
   assert_loss_close(dist.detach().cpu().numpy(), c['den_Log'])
   dist.sum().backward()
-  assert_grad_close(table.grad.cpu().numpy(), c['den_grad'], c['den_Log'])
+  assert_grad_marginal_close(table.grad.cpu().numpy(), c['den_grad'], c['den_grad'], c['den_Log'],
+                             None)
   # MaxTropical: one arc per live frame, its label the Viterbi label
   table = torch.tensor(c['W'], device=device, requires_grad=True)
   dist, _ = _table_lattice(c, table)._forward(None, _frames(B, T, device), nf,

@@ -14,7 +14,8 @@ import numpy as np
 import pytest
 
 from golden_cases import (FLD_CASES, LATTICE_CASES, SEMIRINGS, assert_grad_close,
-                          assert_loss_close, assert_values_close, load, load_fld)
+                          assert_grad_marginal_close, assert_loss_close, assert_values_close, load,
+                          load_fld)
 from oracle import oracle as orc
 
 SID = {'Log': orc.LOG, 'MaxTropical': orc.MAX, 'Real': orc.REAL}
@@ -67,6 +68,28 @@ def test_fld_loss_and_grad(case):
   assert_loss_close(loss, c['loss'])
   assert_loss_close(lz, c['den_Log'])
   assert_grad_close(dW, c['loss_grad'], c['den_Log'])
+
+
+@pytest.mark.parametrize('case', FLD_CASES)
+def test_fld_den_grad(case):
+  """tab_den_grad (d log_z / dW alone) against the reference's den_grad
+  (its FrameLabelDependent.backward composed in reverse frame order), every
+  element within its marginal bound."""
+  c = load_fld(case)
+  tab = orc.full_ngram_table(c['V'], c['n'])
+  lz, d = orc.tab_den_grad(tab, c['W'], c['num_frames'], c['K'])
+  assert_loss_close(lz, c['den_Log'])
+  assert_grad_marginal_close(d, c['den_grad'], c['den_grad'], c['den_Log'], None)
+
+
+@pytest.mark.parametrize('case', LATTICE_CASES)
+def test_full_ngram_den_grad_through_table(case):
+  c = load(case)
+  tab = orc.full_ngram_table(c['V'], c['n'])
+  W = c['W'].astype(np.float32)
+  lz, d = orc.tab_den_grad(tab, W, c['num_frames'], 0)
+  assert_loss_close(lz, c['den_Log'])
+  assert_grad_marginal_close(d, c['den_grad'], c['den_grad'], c['den_Log'], None)
 
 
 @pytest.mark.parametrize('case', FLD_CASES)
