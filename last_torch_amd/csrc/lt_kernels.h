@@ -180,15 +180,16 @@ LT_DEVINL float lt_log_acc(float x) {
 // offset per frame is rounded at its own magnitude -- 2^-24 * 80 at 80 nats
 // below the frame's max, every frame -- while (i, f) rounds only the
 // fraction. lae_split: (ia, fa) (+) (ib, fb) = log(e^(ia+fa) + e^(ib+fb))
-// (semirings.py:248-255), the result's integer part taken from the term
-// with the larger integer part (exact), its fraction f1 + log(1 + e^d) with
-// d = (i2 - i1) + (f2 - f1) (d <= ~|f| range; its rounding reaches the result
-// only through e^d).
+// (semirings.py:248-255), the result's integer part taken from the larger
+// term (exact), its fraction f1 + log(1 + e^d) with d = (i2 - i1) + (f2 - f1)
+// <= 0 (d's rounding reaches the result only through e^d).
 LT_DEVINL void lae_split(float ia, float fa, float ib, float fb, float& io, float& fo) {
   constexpr float ninf = -__builtin_inff();
   ia = fa == ninf ? ninf : ia;  // a masked arc (w = -inf) is the zero term
   ib = fb == ninf ? ninf : ib;
-  const bool ab = ia >= ib;
+  // the larger term by its whole value (the integer parts' difference is
+  // exact; both zero: NaN, false -> b, masked below)
+  const bool ab = (ia - ib) + (fa - fb) >= 0.f;
   const float i1 = ab ? ia : ib, f1 = ab ? fa : fb;
   const float i2 = ab ? ib : ia, f2 = ab ? fb : fa;
   const float d = (i2 - i1) + (f2 - f1);  // i2 = -inf: -inf (exp 0); both -inf: NaN (masked)

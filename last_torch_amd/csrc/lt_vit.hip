@@ -92,21 +92,29 @@ LT_DEVINL float vlds(const unsigned char* fr, int off) {
 // (cfg4: 0.882 ms with both on one wave, 0.831 ms with one backpointer wave,
 // 0.742 ms with kBpWaves = 2 dealing the frames round robin, round 3). Wave 0 runs the
 // chain alone -- weights, alpha, the max3 tree, the LDS-DMA ring -- and
-// publishes alpha_{t+1} with an LDS progress word; wave 1 follows, re-forms
-// frame t's terms from the same alpha_t and weights (the same additions, so
-// the same floats), takes the first term equal to alpha_{t+1}[q] and stores
-// the backpointer byte. The ring (kSSlots frames) and the alpha rows
-// (kSAl) give the backpointer wave kSSlots - kSAhead - 1 frames of slack;
-// the chain waits on its progress word only when it would overwrite a frame
-// or row that wave has not passed.
-constexpr int kSAhead = 3;
-constexpr int kSSlots = 8;
+// publishes alpha rows through an LDS progress word; the backpointer waves
+// follow, re-form frame t's terms from the same alpha_t and weights (the
+// same additions, so the same floats), take the first term equal to
+// alpha_{t+1}[q] and store the backpointer byte.
+// Round 4: the chain step keeps only alpha's LDS round trip on its critical
+// path -- frame t+1's weights are read into registers during step t (the
+// ring runs kSAhead = 8 frames ahead, so the frame has long landed), the
+// progress word is published every kPub frames (its lgkmcnt wait no longer
+// stalls every step), and the backpointer waves' slack (kSSlots - kSAhead -
+// 1 = 15 frames of ring, kSAl = 16 alpha rows) is checked against their
+// progress as last read, re-read only when it runs short.
+constexpr int kSAhead = 8;
+constexpr int kSSlots = 24;
+constexpr int kSAl = 16;
+constexpr int kPub = 4;
 #ifndef LT_VIT_BPW
 #define LT_VIT_BPW 2
 #endif
 constexpr int kBpWaves = LT_VIT_BPW;  // backpointer waves (frames dealt round robin)
+static_assert(kBpWaves >= 1 && kBpWaves <= 8, "backpointer waves");
+static_assert(kSSlots - kSAhead - 1 >= 2 * kPub, "the ring must leave the backpointer waves slack");
 [[maybe_unused]] constexpr int kVitStampSteps = 128;  // diagnostic stamps (LT_DIAG)
-constexpr int kSAl = 8;
+constexpr int kWaitSpins = 1 << 24;                   // progress waits time out (the result is NaN)
 
 template <bool BF16, bool FULL>
 __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const VitArgs a) {
@@ -116,6 +124,7 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
   __shared__ __attribute__((aligned(16))) unsigned char s_ring[kSSlots][5 * 1024];
   __shared__ int s_prog[1 + kBpWaves];  // [0] chain: alpha rows published; [1 + k] backpointer
                                        // wave k: 1 + its last frame done
+  __shared__ int s_err;                 // a progress wait timed out
 #ifdef LT_DIAG
   __shared__ long long s_st[kVitStampSteps][4];
   const bool stamp = a.stamps != nullptr && blockIdx.x == 0;
@@ -142,18 +151,22 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
   // alpha_0: the start state (MaxTropical one = 0), every other state zero
   if (tid < 40) s_al[0][tid] = tid == 0 ? 0.f : -kInf;
   if (tid < 1 + kBpWaves) s_prog[tid] = 0;
+  if (tid == 0) s_err = 0;
   __syncthreads();
   auto frame = [&](int t) {
     return &s_ring[t % kSSlots][0] + ((goff0 + (long long)fclamp(t) * fbytes) & 15);
   };
-  // frame t's terms x (the lane's sources) and xs (the blank self loop)
-  auto terms = [&](int t, float* x, float& xs, float& w00) {
+  // frame t's weights of the lane: its sources' arcs, the blank self loop,
+  // and w[0][0] (the start state's self loop)
+  auto weights = [&](int t, float* w, float& self, float& w00) {
     const unsigned char* fr = frame(t);
-    float w[kHalf];
 #pragma unroll
     for (int m = 0; m < kHalf; ++m) w[m] = vlds<BF16>(fr, vb + m * (FULL ? 33 : R) * es);
-    const float self = vlds<BF16>(fr, vself);
+    self = vlds<BF16>(fr, vself);
     w00 = vlds<BF16>(fr, 0);
+  };
+  // frame t's terms x (the lane's sources) and xs (the blank self loop)
+  auto terms_w = [&](int t, const float* w, float self, float* x, float& xs) {
     const float* acur = s_al[t % kSAl];
     float al[20];
 #pragma unroll
@@ -170,12 +183,14 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
     xs = aq + self;
   };
   auto wait_prog = [&](int k, int want) {
-    for (int n = 0; n < (1 << 26); ++n) {
+    int n = 0;
+    for (; n < kWaitSpins; ++n) {
       const int v = __builtin_amdgcn_readfirstlane(
           __hip_atomic_load(&s_prog[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
       if (v >= want) break;
       __builtin_amdgcn_s_sleep(1);
     }
+    if (n == kWaitSpins && lane == 0) s_err = 1;  // the distance becomes NaN (no silent result)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
   auto publish = [&](int k, int v) {
@@ -206,25 +221,21 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
     }
   };
   if (wave == 0) {
-    // ---- the chain
-    // every step issues one frame (clamped past the end), so the ring's
-    // vmcnt counts stay uniform to the last frame. Chain stamps
-    // (tools/vit_stamps.py): of a ~1,200-tick step, the frame wait and LDS
-    // reads take ~290, the terms / max tree / alpha write / publish ~440, the
-    // ring issue ~330. Measured slower: prefetching frame t + 1's weights
-    // into registers a step early (0.869 against 0.846 ms at cfg4), and the
-    // ring's DMA issued by the backpointer wave instead (1.07-1.11 ms: that
-    // wave then paces the chain); a third, loader wave issuing it (0.848 ms,
-    // no change: the chain's own latency, ~1,100 ticks a step, is the floor)
+    // ---- the chain: every step issues one frame (clamped past the end), so
+    // the ring's vmcnt counts stay uniform to the last frame
     if (nf > 0)
       for (int d = 0; d < kSAhead; ++d) issue(d);
     float a0 = 0.f;
-    int bseen = 0;  // the backpointer wave's progress as last read
+    int bseen = 0;  // min over the backpointer waves of their progress as last read
+    float w[kHalf], self = 0.f, w00 = 0.f;
+    if (nf > 0) {
+      wait_vmcnt((kSAhead - 1) * ni);  // frame 0 landed (the only VMEM ops are the ring's)
+      weights(0, w, self, w00);
+    }
     for (int t = 0; t < nf; ++t) {
       VSTAMP(t, 0);
-      wait_vmcnt((kSAhead - 1) * ni);  // frame t landed (the only VMEM ops are the ring's)
-      float x[kHalf], xs, w00;
-      terms(t, x, xs, w00);
+      float x[kHalf], xs;
+      terms_w(t, w, self, x, xs);
 #ifdef LT_DIAG
       if (stamp) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -248,17 +259,25 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
       a0 += w00;
       const int wslot = h == 0 ? (live ? aslot(q) : 40 + j) : (lane == 32 ? 0 : 40 + j);
       anxt[wslot] = lane == 32 ? a0 : r;
-      publish(0, t + 1);
+      if ((t + 1) % kPub == 0 || t + 1 == nf) publish(0, t + 1);
       VSTAMP(t, 2);
+      // frame t + 1's weights, behind alpha's store (LDS keeps a wave's order)
+      if (t + 1 < nf) {
+        wait_vmcnt((kSAhead - 2) * ni);  // frame t + 1 landed
+        weights(t + 1, w, self, w00);
+      }
       // the slot of frame t + kSAhead held frame t + kSAhead - kSSlots, and
-      // the next step overwrites the alpha row alpha_{t + 2 - kSAl}: the
-      // backpointer wave must be past both (every step, the last ones too)
+      // step t + 1 overwrites the alpha row alpha_{t + 2 - kSAl}: every
+      // backpointer wave must be past both (all frames below `want` done)
       const int want = max(t + kSAhead - kSSlots + 1, t + 3 - kSAl);
-      if (bseen < want) {  // re-read only when the last value seen is short
-        // every backpointer wave past `want` - 1: all frames below `want` done
+      if (bseen < want) {
         int m = 0x7fffffff;
         for (int k = 1; k <= kBpWaves; ++k) {
-          wait_prog(k, want);
+          // wave k's frames are k - 1, k - 1 + kBpWaves, ...: its progress
+          // must pass the last of them below `want` (and below nf)
+          const int lim = min(want, nf) - 1 - (k - 1);
+          const int need = lim < 0 ? 0 : (k - 1) + (lim / kBpWaves) * kBpWaves + 1;
+          if (need > 0) wait_prog(k, need);
           m = min(m, __builtin_amdgcn_readfirstlane(s_prog[k]));
         }
         bseen = m;
@@ -274,13 +293,14 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
     }
 #endif
     // the distance: (+)_q alpha_T[q] in MaxTropical, the first maximum
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const float* af = s_al[nf % kSAl];
     float r = lane < C ? af[aslot(lane)] : -kInf;
     int ri = lane < C ? lane : 0x7fffffff;
 #pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-      const float pv = __shfl_xor(r, s);
-      const int pi = __shfl_xor(ri, s);
+    for (int sft = 1; sft < 64; sft <<= 1) {
+      const float pv = __shfl_xor(r, sft);
+      const int pi = __shfl_xor(ri, sft);
       if (pv > r || (pv == r && pi < ri)) { r = pv; ri = pi; }
     }
     if (lane == 0) {
@@ -295,10 +315,15 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.bp + (long long)b * a.T * C), (short)0,
                                           a.T * C, 0x00020000);
     const int ib = h ? 18 : 1;  // term index of x[0]
+    int seen = 0;  // the chain's progress as last read
     for (int t = wave - 1; t < nf; t += kBpWaves) {
-      wait_prog(0, t + 1);
-      float x[kHalf], xs, w00;
-      terms(t, x, xs, w00);
+      if (seen < t + 1) {
+        wait_prog(0, t + 1);
+        seen = __builtin_amdgcn_readfirstlane(s_prog[0]);
+      }
+      float w[kHalf], self, w00, x[kHalf], xs;
+      weights(t, w, self, w00);
+      terms_w(t, w, self, x, xs);
       const float rq = s_al[(t + 1) % kSAl][aslot(min(q, V))];
       int ri = 99;
 #pragma unroll
@@ -313,6 +338,8 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
       (void)w00;
     }
   }
+  __syncthreads();
+  if (tid == 0 && s_err) a.dist[b] = __builtin_nanf("");  // a timed-out wait: no silent result
 }
 
 // Backtrace of the bigram backpointers in segments (one workgroup per

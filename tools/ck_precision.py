@@ -144,18 +144,18 @@ def main():
     gl = dWl[b].cpu().numpy()[:f].astype(np.float64)
     anl = outl[4][b].cpu().numpy()[:f].astype(np.float64)
     bnl = outl[5][1][b].cpu().numpy()[:f].astype(np.float64)
-    fin = np.isfinite(ran)
+    ran_f, rbn_f = ran[:f], rbn[:f]
     print(f'  local: num err {abs(float(outl[2][b]) - rnum) / unl:.2f} un; alpha_num max '
-          f'{np.abs(np.where(fin, anl - ran, 0)).max() / unl:.2f} un, beta_num max '
-          f'{np.abs(np.where(np.isfinite(rbn), bnl - rbn, 0)).max() / unl:.2f} un')
+          f'{np.abs(np.where(np.isfinite(ran_f), anl - ran_f, 0)).max() / unl:.2f} un, beta_num max '
+          f'{np.abs(np.where(np.isfinite(rbn_f), bnl - rbn_f, 0)).max() / unl:.2f} un')
     rl = np.abs(gl + nm) / (1e-8 + (1e-4 + 4 * unl) * nm)
     il = np.unravel_index(np.argmax(rl), rl.shape)
     print(f'  local dW / bound: max {rl.max():.3f} at {list(il)} (num {nm[il]:.3e}); '
           f'> 1: {(rl > 1).sum()}')
     # string exponent errors at live string arcs (alpha_num + beta_num from
     # the stored rows, exact arithmetic)
-    live = (ran + rbn - rnum) > -20
-    e = np.abs((anl + bnl - float(outl[2][b])) - (ran + rbn - rnum))[live]
+    live = (ran_f + rbn_f - rnum) > -20
+    e = np.abs((anl + bnl - float(outl[2][b])) - (ran_f + rbn_f - rnum))[live]
     print(f'  local string posterior exponent err: max {e.max() / unl:.2f} un mean {e.mean() / unl:.2f} un')
 
 
