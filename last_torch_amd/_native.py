@@ -605,7 +605,8 @@ def joint_weights_backward_supported(C, H, R, rows=0):
   waves = 8 if n % 8 == 0 else 4 if n % 4 == 0 else 2 if n % 2 == 0 else 1
   KB = (R + 15) // 16
   RB = 64 if R > 32 else 32
-  bufb = 4 * 32 * (16 * KB + 4) + 4 * 32 * (16 * KB + 8) + 4 * RB * 36
+  # the bf16 hi/lo tiles only for 8-wave workgroups (lt_producer.hip bwd_lds)
+  bufb = 4 * 32 * (16 * KB + 4) + (4 * 32 * (16 * KB + 8) + 4 * RB * 36 if waves == 8 else 0)
   return 2 * bufb + 4 * C * 32 * waves <= 160 * 1024
 
 

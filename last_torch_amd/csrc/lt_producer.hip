@@ -502,12 +502,14 @@ __global__ __launch_bounds__(64 * NW) void joint_backward_kernel(const JBArgs a)
   constexpr int RB = TWO ? 64 : 32;  // rows of the transposed bf16 tile: [r][m]
   constexpr int TS = 32 + 4;        // its row stride
   constexpr int GN = 32 * KB * 16;  // g tile elements staged per tile
-  // per buffer (bytes): fp32 [32][GS] | hi, lo [32][GB] | hi, lo [RB][TS]
-  constexpr int BUFB = 4 * 32 * GS + 2 * 2 * 32 * GB + 2 * 2 * RB * TS;
   constexpr int nthr = 64 * NW, HW = 32 * NW;
   // 8 waves share each staged g value: split it once at staging (PRE);
   // smaller workgroups split in each wave instead (fewer staging stores)
   constexpr bool PRE = NW == 8;
+  // per buffer (bytes): fp32 [32][GS] | (PRE) hi, lo [32][GB] | hi, lo [RB][TS]
+  // -- small workgroups allocate the fp32 tile only, so more of them fit a
+  // CU (round 4: at H = 32, one wave per workgroup, 3 -> 9 workgroups a CU)
+  constexpr int BUFB = 4 * 32 * GS + (PRE ? 2 * 2 * 32 * GB + 2 * 2 * RB * TS : 0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, R = a.R, C = a.C;
   // this workgroup's hidden columns: [h0, h0 + HW)
@@ -702,21 +704,27 @@ int bwd_waves(int H) {
   return n % 8 == 0 ? 8 : n % 4 == 0 ? 4 : n % 2 == 0 ? 2 : 1;
 }
 
-int bwd_grid(long long rows, int C, int H) {
+long long bwd_lds(int C, int H, int R) {  // keep in sync with BUFB
+  const int KB = (R + 15) / 16, RB = R > 32 ? 64 : 32;
+  const bool pre = bwd_waves(H) == 8;
+  const long long bufb =
+      4LL * 32 * (KB * 16 + 4) + (pre ? 4LL * 32 * (KB * 16 + 8) + 4LL * RB * 36 : 0);
+  return 2 * bufb + 4LL * C * 32 * bwd_waves(H);
+}
+
+int bwd_grid(long long rows, int C, int H, int R) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const long long tiles = (rows + 31) / 32;  // blocks of 32 frames
   const int gy = std::max(1, H / (32 * bwd_waves(H)));
-  // one resident workgroup per CU over the whole (x, y) grid
-  const long long gx = std::max<long long>(1, (cus * (bwd_waves(H) < 8 ? 2 : 1)) / gy);
+  // as many resident workgroups per CU as LDS and waves allow (at most 8
+  // waves' worth of workgroups: 1-wave workgroups are latency-bound alone)
+  const long long lds = std::max<long long>(1, bwd_lds(C, H, R));
+  const long long per_cu = std::max<long long>(
+      1, std::min<long long>(160 * 1024 / lds, std::max(1, 8 / bwd_waves(H))));
+  const long long gx = std::max<long long>(1, cus * per_cu / gy);
   return (int)std::max<long long>(1, std::min<long long>(tiles, gx));
-}
-
-long long bwd_lds(int C, int H, int R) {  // keep in sync with BUFB
-  const int KB = (R + 15) / 16, RB = R > 32 ? 64 : 32;
-  const long long bufb = 4LL * 32 * (KB * 16 + 4) + 4LL * 32 * (KB * 16 + 8) + 4LL * RB * 36;
-  return 2 * bufb + 4LL * C * 32 * bwd_waves(H);
 }
 
 long long bwd_stride(int C, int H, int R) { return (long long)(C + R) * H + 64; }
@@ -729,7 +737,7 @@ int lt_joint_weights_backward_workspace_bytes(int64_t rows, int32_t num_states, 
                                               int32_t out_dim, size_t* bytes) {
   if (!bytes || rows < 0 || num_states < 1 || hidden < 32 || out_dim < 1)
     return lt_impl::set_error(LT_EINVAL, "lt_joint_weights_backward_workspace_bytes: bad arguments");
-  *bytes = 4 * (size_t)bwd_grid(rows, num_states, hidden) * bwd_stride(num_states, hidden, out_dim);
+  *bytes = 4 * (size_t)bwd_grid(rows, num_states, hidden, out_dim) * bwd_stride(num_states, hidden, out_dim);
   return LT_OK;
 }
 
@@ -768,7 +776,7 @@ int lt_joint_weights_backward(int64_t rows, int32_t num_states, int32_t hidden, 
   a.pc = ctx_proj; a.pf = frame_proj; a.wo = out_weight; a.g = grad_W;
   a.dpf = d_frame_proj; a.part = (float*)workspace;
   a.rows = rows; a.C = C; a.H = H; a.R = R;
-  const int grid = bwd_grid(rows, C, H);
+  const int grid = bwd_grid(rows, C, H, R);
   const int nw = bwd_waves(H);
   const int KB = (R + 15) / 16;
   const void* k = KB == 1 ? pick_nw<1, false>(nw) : KB == 2 ? pick_nw<2, false>(nw)

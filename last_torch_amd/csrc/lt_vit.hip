@@ -41,6 +41,11 @@ constexpr int kHalf = 17;  // sources per half (p < 17 in h = 0)
 // (16-byte aligned for the b128 reads)
 LT_DEVINL int aslot(int p) { return p < kHalf ? p : p + 3; }
 
+LT_DEVINL float max_raw(float x, float y) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
 LT_DEVINL float max3_raw(float x, float y, float z) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
@@ -88,43 +93,53 @@ LT_DEVINL float vlds(const unsigned char* fr, int off) {
   else return *(const float*)(fr + off);
 }
 
-// The alpha chain and the backpointers on separate waves of one workgroup
-// (cfg4: 0.882 ms with both on one wave, 0.831 ms with one backpointer wave,
-// 0.742 ms with kBpWaves = 2 dealing the frames round robin, round 3). Wave 0 runs the
-// chain alone -- weights, alpha, the max3 tree, the LDS-DMA ring -- and
-// publishes alpha rows through an LDS progress word; the backpointer waves
-// follow, re-form frame t's terms from the same alpha_t and weights (the
-// same additions, so the same floats), take the first term equal to
-// alpha_{t+1}[q] and store the backpointer byte.
-// Round 4: the chain step keeps only alpha's LDS round trip on its critical
-// path -- frame t+1's weights are read into registers during step t (the
-// ring runs kSAhead = 8 frames ahead, so the frame has long landed), the
-// progress word is published every kPub frames (its lgkmcnt wait no longer
-// stalls every step), and the backpointer waves' slack (kSSlots - kSAhead -
-// 1 = 15 frames of ring, kSAl = 16 alpha rows) is checked against their
-// progress as last read, re-read only when it runs short.
-constexpr int kSAhead = 8;
-constexpr int kSSlots = 24;
-constexpr int kSAl = 16;
+// The alpha chain, a loader and the backpointers on separate waves of one
+// workgroup (round 3: chain and backpointers apart, 0.882 -> 0.742 ms at
+// cfg4 with two backpointer waves dealing the frames round robin).
+//   wave 0, the chain: per frame one LDS round trip for alpha (5 b128 reads,
+//     one store), 17 adds and a max3 tree, one permlane32 swap. Its weights
+//     come from the transposed frame (below): 5 b128 reads issued during the
+//     previous step, behind alpha's store. It issues no DMA and reads no raw
+//     frame.
+//   wave 1, the loader: streams the frames into an LDS-DMA ring kRing - 2
+//     frames ahead (counted vmcnt waits) and writes each frame transposed
+//     for the lanes -- lane l's 17 source weights, its blank self loop and
+//     w[0][0] as five 16-byte groups at g * 1 KiB + 16 l (conflict-free b128
+//     reads, fp32 whatever W's dtype) -- into a kTw-slot ring, published
+//     through its progress word; a slot is reused once the chain and the
+//     backpointer wave that own its frame are past it.
+//   waves 2.., the backpointers: re-form frame t's terms from the same
+//     alpha_t and weights (the same additions, so the same floats), take the
+//     first term equal to alpha_{t+1}[q] and store the backpointer byte.
+// The chain publishes its progress every kPub frames; the backpointer waves'
+// slack on the alpha rows (kSAl) is checked against their progress as last
+// read, re-read only when it runs short. Waits are bounded: a timed-out wait
+// makes the utterance's distance NaN (no silent result).
+constexpr int kRing = 10;  // raw frames: kRing - 2 in flight, taken in pairs
+constexpr int kTw = 16;    // transposed frames
+constexpr int kSAl = 16;   // alpha rows
 constexpr int kPub = 4;
 #ifndef LT_VIT_BPW
 #define LT_VIT_BPW 2
 #endif
 constexpr int kBpWaves = LT_VIT_BPW;  // backpointer waves (frames dealt round robin)
 static_assert(kBpWaves >= 1 && kBpWaves <= 8, "backpointer waves");
-static_assert(kSSlots - kSAhead - 1 >= 2 * kPub, "the ring must leave the backpointer waves slack");
+static_assert(kTw > 2 * kPub + 2 && kSAl > 2 * kPub + 3, "rings must leave the followers slack");
 [[maybe_unused]] constexpr int kVitStampSteps = 128;  // diagnostic stamps (LT_DIAG)
 constexpr int kWaitSpins = 1 << 24;                   // progress waits time out (the result is NaN)
+constexpr int kPL = 1 + kBpWaves;                     // s_prog index of the loader
 
 template <bool BF16, bool FULL>
-__global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const VitArgs a) {
+__global__ __launch_bounds__(64 * (2 + kBpWaves)) void vit_split_kernel(const VitArgs a) {
   // alpha rows: [0, 17) and [20, 36) the two halves' sources (b128 reads),
   // [40, 72) spare slots for the chain's branch-free store
   __shared__ __attribute__((aligned(16))) float s_al[kSAl][72];
-  __shared__ __attribute__((aligned(16))) unsigned char s_ring[kSSlots][5 * 1024];
-  __shared__ int s_prog[1 + kBpWaves];  // [0] chain: alpha rows published; [1 + k] backpointer
-                                       // wave k: 1 + its last frame done
-  __shared__ int s_err;                 // a progress wait timed out
+  __shared__ __attribute__((aligned(16))) unsigned char s_ring[kRing][5 * 1024];
+  __shared__ __attribute__((aligned(16))) float4 s_tw[kTw][5][64];
+  // [0] chain: alpha rows published; [1 + k] backpointer wave k: 1 + its last
+  // frame done; [kPL] loader: transposed frames published
+  __shared__ int s_prog[2 + kBpWaves];
+  __shared__ int s_err;  // a progress wait timed out
 #ifdef LT_DIAG
   __shared__ long long s_st[kVitStampSteps][4];
   const bool stamp = a.stamps != nullptr && blockIdx.x == 0;
@@ -143,44 +158,68 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
   const int q = j + 1;
   const bool live = j < V;
   const int p0 = kHalf * h;
-  const int vb = (p0 * R + min(q, V)) * es;
-  const int vself = min(q, V) * R * es;
   const long long fbytes = (long long)C * R * es;
+#ifdef LT_DIAG
+  // timing ablations (wrong results): 1 the backpointer waves only publish,
+  // 2 the loader skips the transposition, 4 the loader skips the DMA
+  const int abl = a.dbg;
+#else
+  constexpr int abl = 0;
+#endif
   const long long goff0 = (long long)b * a.T * fbytes;
   auto fclamp = [&](int t) { return min(t, max(nf - 1, 0)); };
-  // alpha_0: the start state (MaxTropical one = 0), every other state zero
-  if (tid < 40) s_al[0][tid] = tid == 0 ? 0.f : -kInf;
-  if (tid < 1 + kBpWaves) s_prog[tid] = 0;
+  // alpha_0: the start state (MaxTropical one = 0), every other state zero;
+  // every row's slots of absent sources (past V, and p = 33 of the upper
+  // half) stay zero (-inf) for good, so a term is always alpha + w (the
+  // loader writes 0 for an absent source's weight): no mask in the chain
+  for (int e = tid; e < kSAl * 40; e += blockDim.x) (&s_al[0][0])[(e / 40) * 72 + e % 40] =
+      e == 0 ? 0.f : -kInf;
+  if (tid < 2 + kBpWaves) s_prog[tid] = 0;
   if (tid == 0) s_err = 0;
   __syncthreads();
-  auto frame = [&](int t) {
-    return &s_ring[t % kSSlots][0] + ((goff0 + (long long)fclamp(t) * fbytes) & 15);
-  };
-  // frame t's weights of the lane: its sources' arcs, the blank self loop,
-  // and w[0][0] (the start state's self loop)
+  // frame t's weights of the lane from the transposed ring: its sources'
+  // arcs, the blank self loop, w[0][0] (the start state's self loop)
   auto weights = [&](int t, float* w, float& self, float& w00) {
-    const unsigned char* fr = frame(t);
+    const float4* tw = &s_tw[t % kTw][0][lane];
+    float v[20];
 #pragma unroll
-    for (int m = 0; m < kHalf; ++m) w[m] = vlds<BF16>(fr, vb + m * (FULL ? 33 : R) * es);
-    self = vlds<BF16>(fr, vself);
-    w00 = vlds<BF16>(fr, 0);
+    for (int g = 0; g < 5; ++g) {
+      const float4 x = tw[64 * g];
+      v[4 * g] = x.x; v[4 * g + 1] = x.y; v[4 * g + 2] = x.z; v[4 * g + 3] = x.w;
+    }
+#pragma unroll
+    for (int m = 0; m < kHalf; ++m) w[m] = v[m];
+    self = v[17];
+    w00 = v[18];
   };
-  // frame t's terms x (the lane's sources) and xs (the blank self loop)
-  auto terms_w = [&](int t, const float* w, float self, float* x, float& xs) {
+  // alpha_t of the lane's sources (al[0..16]) and of its destination (aq)
+  auto alpha_rd = [&](int t, float* al, float& aq) {
     const float* acur = s_al[t % kSAl];
-    float al[20];
+    aq = acur[aslot(min(q, V))];  // first: its address register is then free
 #pragma unroll
     for (int g = 0; g < 5; ++g) {
       const float4 v = *(const float4*)(acur + 20 * h + 4 * g);
       al[4 * g + 0] = v.x; al[4 * g + 1] = v.y; al[4 * g + 2] = v.z; al[4 * g + 3] = v.w;
     }
-    const float aq = acur[aslot(min(q, V))];
+  };
+  // frame t's terms x (the lane's sources; absent ones -inf + 0) and xs (the
+  // blank self loop), in packed adds
+  auto terms_of = [&](const float* al, float aq, const float* w, float self, float* x, float& xs) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int m = 0; m < kHalf; ++m) {
-      const bool ok = FULL ? (m < kHalf - 1 || h == 0) : p0 + m <= V;
-      x[m] = ok ? al[m] + w[m] : -kInf;
+    for (int m = 0; m < kHalf - 1; m += 2) {
+      const f2 s2 = f2{al[m], al[m + 1]} + f2{w[m], w[m + 1]};
+      x[m] = s2.x;
+      x[m + 1] = s2.y;
     }
-    xs = aq + self;
+    const f2 s2 = f2{al[kHalf - 1], aq} + f2{w[kHalf - 1], self};
+    x[kHalf - 1] = s2.x;
+    xs = s2.y;
+  };
+  auto terms_w = [&](int t, const float* w, float self, float* x, float& xs) {
+    float al[20], aq;
+    alpha_rd(t, al, aq);
+    terms_of(al, aq, w, self, x, xs);
   };
   auto wait_prog = [&](int k, int want) {
     int n = 0;
@@ -190,7 +229,7 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
       if (v >= want) break;
       __builtin_amdgcn_s_sleep(1);
     }
-    if (n == kWaitSpins && lane == 0) s_err = 1;  // the distance becomes NaN (no silent result)
+    if (n == kWaitSpins && lane == 0) s_err = 1;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
   auto publish = [&](int k, int v) {
@@ -198,61 +237,46 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(&s_prog[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  const int ni = (int)(((fbytes + 30) / 16 + 63) / 64);
-  // wave-instructions that never leave the frame: 4 (fp32 V = 32), 2 (bf16)
-  const int kf = (int)min((long long)min(ni, 4), fbytes / 16 / 64);
-  auto issue = [&](int t) {  // frame t (clamped) -> slot t % kSSlots
-    const long long off = goff0 + (long long)fclamp(t) * fbytes;
-    const long long a0 = off & ~15LL;
-    const int n16 = (int)((off + fbytes - a0 + 15) >> 4);
-    const unsigned dst = lds_base_addr(&s_ring[t % kSSlots][0]);
-    // the first kf wave-instructions never leave the frame (or W): one lane
-    // address, the instruction's 1 KiB step as its immediate offset (global
-    // and LDS alike); the rest clamp each lane to the frame's last 16 bytes
-    // (inline asm, as glds16: the compiler sees no LDS write to order its
-    // LDS reads behind, so the ring's counted vmcnt waits stay partial)
-    const unsigned char* gb = a.W + a0 + 16 * lane;
-    if (kf == 4) glds16x4(gb, dst);
-    else if (kf == 2) glds16x2(gb, dst);
-    for (int i = (kf == 4 || kf == 2) ? kf : 0; i < ni; ++i) {
-      int g = lane + 64 * i;
-      g = g < n16 ? g : n16 - 1;
-      glds16(a.W + a0 + 16LL * g, dst + 1024u * i);
-    }
+  // backpointer wave k (1-based) owns frames k - 1, k - 1 + kBpWaves, ...:
+  // the progress it must reach to have done every frame of its below `want`
+  auto bp_need = [&](int k, int want) {
+    const int lim = min(want, nf) - 1 - (k - 1);
+    return lim < 0 ? 0 : (k - 1) + (lim / kBpWaves) * kBpWaves + 1;
   };
   if (wave == 0) {
-    // ---- the chain: every step issues one frame (clamped past the end), so
-    // the ring's vmcnt counts stay uniform to the last frame
-    if (nf > 0)
-      for (int d = 0; d < kSAhead; ++d) issue(d);
+    // ---- the chain
     float a0 = 0.f;
     int bseen = 0;  // min over the backpointer waves of their progress as last read
-    float w[kHalf], self = 0.f, w00 = 0.f;
+    int lseen = 0;  // the loader's progress as last read
+    float w[kHalf], self = 0.f, w00 = 0.f, al[20], aq = 0.f;
     if (nf > 0) {
-      wait_vmcnt((kSAhead - 1) * ni);  // frame 0 landed (the only VMEM ops are the ring's)
+      wait_prog(kPL, 1);
+      lseen = __builtin_amdgcn_readfirstlane(s_prog[kPL]);
+      alpha_rd(0, al, aq);
       weights(0, w, self, w00);
     }
     for (int t = 0; t < nf; ++t) {
       VSTAMP(t, 0);
       float x[kHalf], xs;
-      terms_w(t, w, self, x, xs);
+      terms_of(al, aq, w, self, x, xs);
 #ifdef LT_DIAG
       if (stamp) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         VSTAMP(t, 1);
       }
 #endif
-      float mx = max3_raw(h ? x[16] : xs, x[0], x[1]);
-      mx = max3_raw(mx, x[2], x[3]);
-      const float m1 = max3_raw(x[4], x[5], x[6]);
-      const float m2 = max3_raw(x[7], x[8], x[9]);
-      const float m3 = max3_raw(x[10], x[11], x[12]);
-      const float m4 = max3_raw(x[13], x[14], x[15]);
-      mx = max3_raw(mx, m1, m2);
-      mx = max3_raw(mx, m3, m4);
-      if (h == 0) mx = fmaxf(mx, x[16]);
+      // the max of the lane's 18 terms (the blank self loop on the lower
+      // half only; absent sources are -inf), branch-free: 8 max3 + 1 max
+      const float xb = h ? -kInf : xs;
+      const float m0 = max3_raw(xb, x[0], x[1]);
+      const float m1 = max3_raw(x[2], x[3], x[4]);
+      const float m2 = max3_raw(x[5], x[6], x[7]);
+      const float m3 = max3_raw(x[8], x[9], x[10]);
+      const float m4 = max3_raw(x[11], x[12], x[13]);
+      const float m5 = max3_raw(x[14], x[15], x[16]);
+      const float mx = max_raw(max3_raw(m0, m1, m2), max3_raw(m3, m4, m5));
       auto pv = __builtin_amdgcn_permlane32_swap(__float_as_int(mx), __float_as_int(mx), false, false);
-      const float r = fmaxf(mx, __int_as_float(h ? pv[0] : pv[1]));
+      const float r = max_raw(mx, __int_as_float(h ? pv[0] : pv[1]));
       // one store for every lane, no exec branch: the destination's value
       // (lower half), alpha[0] (lane 32), else a spare slot of the row
       float* anxt = s_al[(t + 1) % kSAl];
@@ -261,31 +285,31 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
       anxt[wslot] = lane == 32 ? a0 : r;
       if ((t + 1) % kPub == 0 || t + 1 == nf) publish(0, t + 1);
       VSTAMP(t, 2);
-      // frame t + 1's weights, behind alpha's store (LDS keeps a wave's order)
+      // step t + 1's operands: alpha_{t+1} read right behind its store (LDS
+      // keeps a wave's order), its latency under the rest of the step, then
+      // frame t + 1's weights
       if (t + 1 < nf) {
-        wait_vmcnt((kSAhead - 2) * ni);  // frame t + 1 landed
+        alpha_rd(t + 1, al, aq);
+        if (lseen < t + 2) {
+          wait_prog(kPL, t + 2);
+          lseen = __builtin_amdgcn_readfirstlane(s_prog[kPL]);
+        }
         weights(t + 1, w, self, w00);
       }
-      // the slot of frame t + kSAhead held frame t + kSAhead - kSSlots, and
       // step t + 1 overwrites the alpha row alpha_{t + 2 - kSAl}: every
-      // backpointer wave must be past both (all frames below `want` done)
-      const int want = max(t + kSAhead - kSSlots + 1, t + 3 - kSAl);
+      // backpointer wave must be past frame t + 2 - kSAl
+      const int want = t + 3 - kSAl;
       if (bseen < want) {
         int m = 0x7fffffff;
         for (int k = 1; k <= kBpWaves; ++k) {
-          // wave k's frames are k - 1, k - 1 + kBpWaves, ...: its progress
-          // must pass the last of them below `want` (and below nf)
-          const int lim = min(want, nf) - 1 - (k - 1);
-          const int need = lim < 0 ? 0 : (k - 1) + (lim / kBpWaves) * kBpWaves + 1;
+          const int need = bp_need(k, want);
           if (need > 0) wait_prog(k, need);
           m = min(m, __builtin_amdgcn_readfirstlane(s_prog[k]));
         }
         bseen = m;
       }
-      issue(t + kSAhead);
       VSTAMP(t, 3);
     }
-    wait_vmcnt(0);
 #ifdef LT_DIAG
     if (stamp) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -307,19 +331,109 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
       a.dist[b] = r;
       a.qstar[b] = ri;
     }
+  } else if (wave == 1) {
+    // ---- the loader: raw frames by LDS-DMA, transposed for the lanes
+    const int ni = (int)(((fbytes + 30) / 16 + 63) / 64);
+    // wave-instructions that never leave the frame: 4 (fp32 V = 32), 2 (bf16)
+    const int kf = (int)min((long long)min(ni, 4), fbytes / 16 / 64);
+    auto issue = [&](int t) {  // frame t (clamped) -> slot t % kRing
+      if (abl & 4) return;
+      const long long off = goff0 + (long long)fclamp(t) * fbytes;
+      const long long a0 = off & ~15LL;
+      const int n16 = (int)((off + fbytes - a0 + 15) >> 4);
+      const unsigned dst = lds_base_addr(&s_ring[t % kRing][0]);
+      // the first kf wave-instructions never leave the frame (or W): one lane
+      // address, the instruction's 1 KiB step as its immediate offset; the
+      // rest clamp each lane to the frame's last 16 bytes (inline asm, as
+      // glds16: the compiler sees no LDS write to order its LDS reads behind)
+      const unsigned char* gb = a.W + a0 + 16 * lane;
+      if (kf == 4) glds16x4(gb, dst);
+      else if (kf == 2) glds16x2(gb, dst);
+      for (int i = (kf == 4 || kf == 2) ? kf : 0; i < ni; ++i) {
+        int g = lane + 64 * i;
+        g = g < n16 ? g : n16 - 1;
+        glds16(a.W + a0 + 16LL * g, dst + 1024u * i);
+      }
+    };
+    const int vb = (p0 * R + min(q, V)) * es;
+    const int vself = min(q, V) * R * es;
+    // frames in pairs: one LDS round trip and one progress store per two
+    // frames (the loader paced the chain with one frame per trip)
+    if (nf > 0)
+      for (int d = 0; d < kRing - 2; ++d) issue(d);
+    int cseen = 0, bseen = 0;
+    for (int f = 0; f < nf; f += 2) {
+      if (!(abl & 4)) wait_vmcnt((kRing - 4) * ni);  // frames f, f + 1 landed
+      // the transposed slots held frames f - kTw and f + 1 - kTw: the chain
+      // (it reads frame f' during step f' - 1; its progress f' + 1 covers
+      // those reads) and the backpointer waves owning them must be past them
+      const int fo = f + 1 - kTw;
+      if (fo >= 0) {
+        if (cseen < fo + 1) {
+          wait_prog(0, min(fo + 1 + kPub, nf));
+          cseen = __builtin_amdgcn_readfirstlane(s_prog[0]);
+        }
+        if (bseen < fo + 1) {
+          int m = 0x7fffffff;
+          for (int k = 1; k <= kBpWaves; ++k) {
+            const int need = bp_need(k, fo + 1);
+            if (need > 0) wait_prog(k, need);
+            m = min(m, __builtin_amdgcn_readfirstlane(s_prog[k]));
+          }
+          bseen = m;
+        }
+      }
+      if (!(abl & 2)) {
+        float v[2][20];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const unsigned char* fr =
+              &s_ring[(f + e) % kRing][0] + ((goff0 + (long long)fclamp(f + e) * fbytes) & 15);
+#pragma unroll
+          for (int m = 0; m < kHalf; ++m) {
+            // an absent source (past V; p = 33 of the upper half): 0 (its
+            // alpha slot is -inf for good)
+            const bool ok = FULL ? (m < kHalf - 1 || h == 0) : p0 + m <= V;
+            v[e][m] = ok ? vlds<BF16>(fr, vb + m * (FULL ? 33 : R) * es) : 0.f;
+          }
+          v[e][17] = vlds<BF16>(fr, vself);
+          v[e][18] = vlds<BF16>(fr, 0);
+          v[e][19] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          float4* tw = &s_tw[(f + e) % kTw][0][lane];
+#pragma unroll
+          for (int g = 0; g < 5; ++g)
+            tw[64 * g] = make_float4(v[e][4 * g], v[e][4 * g + 1], v[e][4 * g + 2], v[e][4 * g + 3]);
+        }
+      }
+      // the raw slots of frames f - 2, f - 1 are free once this wave's reads
+      // of them are done (the DMA writes LDS outside the wave's LDS order)
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      issue(f + kRing - 2);
+      issue(f + kRing - 1);
+      publish(kPL, f + 2);
+    }
+    wait_vmcnt(0);
   } else {
-    // ---- the backpointers (wave 1 + k takes frames k, k + kBpWaves, ...):
+    // ---- the backpointers (wave 2 + k takes frames k, k + kBpWaves, ...):
     // the first term equal to alpha_{t+1}[q]
     // (group_reduce's first-maximum rule), the lower half first
+    const int k1 = wave - 1;  // 1-based index of this backpointer wave
     const __amdgpu_buffer_rsrc_t bpr =
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.bp + (long long)b * a.T * C), (short)0,
                                           a.T * C, 0x00020000);
     const int ib = h ? 18 : 1;  // term index of x[0]
     int seen = 0;  // the chain's progress as last read
-    for (int t = wave - 1; t < nf; t += kBpWaves) {
+    for (int t = k1 - 1; t < nf; t += kBpWaves) {
       if (seen < t + 1) {
         wait_prog(0, t + 1);
         seen = __builtin_amdgcn_readfirstlane(s_prog[0]);
+      }
+      if (abl & 1) {
+        publish(k1, t + 1);
+        continue;
       }
       float w[kHalf], self, w00, x[kHalf], xs;
       weights(t, w, self, w00);
@@ -332,9 +446,9 @@ __global__ __launch_bounds__(64 * (1 + kBpWaves)) void vit_split_kernel(const Vi
       auto pi = __builtin_amdgcn_permlane32_swap(ri, ri, false, false);
       const int rlo = h ? pi[0] : ri, rhi = h ? ri : pi[1];
       const int bpv = lane == 32 ? 0 : (rlo < 99 ? rlo : rhi);
-      if ((h == 0 && live) || lane == 32)
+      if (((h == 0 && live) || lane == 32) && !(abl & 1))
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bpv, bpr, lane == 32 ? 0 : q, t * C, 0);
-      publish(wave, t + 1);
+      publish(k1, t + 1);
       (void)w00;
     }
   }
@@ -483,7 +597,7 @@ int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, 
                                : (const void*)vit_split_kernel<false, false>);
   void* args[] = {(void*)&a};
   hipError_t e =
-      hipLaunchKernel(k, dim3(a.B), dim3(64 * (1 + kBpWaves)), args, 0, (hipStream_t)stream);
+      hipLaunchKernel(k, dim3(a.B), dim3(64 * (2 + kBpWaves)), args, 0, (hipStream_t)stream);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;
