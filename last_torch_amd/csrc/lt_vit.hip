@@ -115,13 +115,22 @@ LT_DEVINL float vlds(const unsigned char* fr, int off) {
 // slack on the alpha rows (kSAl) is checked against their progress as last
 // read, re-read only when it runs short. Waits are bounded: a timed-out wait
 // makes the utterance's distance NaN (no silent result).
-constexpr int kRing = 10;  // raw frames: kRing - 2 in flight, taken in pairs
-constexpr int kTw = 16;    // transposed frames
-constexpr int kSAl = 16;   // alpha rows
-constexpr int kPub = 4;
 #ifndef LT_VIT_BPW
 #define LT_VIT_BPW 2
 #endif
+#ifndef LT_VIT_PUB
+#define LT_VIT_PUB 4
+#endif
+#ifndef LT_VIT_TW
+#define LT_VIT_TW 16
+#endif
+#ifndef LT_VIT_SAL
+#define LT_VIT_SAL 16
+#endif
+constexpr int kRing = 10;          // raw frames: kRing - 2 in flight, taken in pairs
+constexpr int kTw = LT_VIT_TW;     // transposed frames
+constexpr int kSAl = LT_VIT_SAL;   // alpha rows
+constexpr int kPub = LT_VIT_PUB;   // the chain publishes its progress every kPub frames
 constexpr int kBpWaves = LT_VIT_BPW;  // backpointer waves (frames dealt round robin)
 static_assert(kBpWaves >= 1 && kBpWaves <= 8, "backpointer waves");
 static_assert(kTw > 2 * kPub + 2 && kSAl > 2 * kPub + 3, "rings must leave the followers slack");
