@@ -27,5 +27,5 @@ for _ in range(5):
   out = nat.loss_grad(W, nf, lab, nl, V, n, False, workspace=ws)
 e1.record()
 torch.cuda.synchronize()
-print(f"LT_CHECKPOINTS={os.environ.get('LT_CHECKPOINTS', 'default')}: {e0.elapsed_time(e1) / 5:.2f} ms, "
+print(f"lib={os.environ.get('LT_LIB_PATH', 'prod')} mid={os.environ.get('LT_TRI_MID', 'default')}: {e0.elapsed_time(e1) / 5:.2f} ms, "
       f"loss[0]={out[0][0].item():.4f}", flush=True)
