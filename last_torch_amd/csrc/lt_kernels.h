@@ -1885,8 +1885,11 @@ int chunk_loss_grad(const lt_problem* pb, int local_norm, const void* W, const i
                     size_t scratch_bytes, void* stream);
 // lt_vit.hip: bigram MaxTropical forward (distance, best final state, backpointers)
 bool vit_bigram_eligible(const lt_problem* pb);
-int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, unsigned char* bp,
-                       int* qstar, float* dist, void* stream);
+// forward + backtrace (one launch when the backpointers fit its LDS);
+// LT_EUNSUPPORTED after the forward: the caller runs the generic backtrace
+int vit_bigram(const lt_problem* pb, const void* W, const int32_t* nfr, unsigned char* bp,
+               int* qstar, float* dist, const float* grad, int64_t* labels, void* arcs,
+               int32_t conv, void* stream);
 int vit_backtrace_lds(const lt_problem* pb, int* seg);
 int vit_backtrace(const lt_problem* pb, const unsigned char* bp, const int* qstar,
                   const int32_t* nfr, const float* grad, int64_t* labels, void* arcs,

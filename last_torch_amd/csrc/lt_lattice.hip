@@ -1181,9 +1181,11 @@ int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   hipStream_t st = (hipStream_t)stream;
   if (lt_impl::vit_bigram_eligible(pb)) {
-    // bigram: one wave per utterance, the chain in registers (lt_vit.hip)
-    if ((rc = lt_impl::vit_bigram_forward(pb, W, num_frames, bp, qstar, path_weight, stream)))
-      return rc;
+    // bigram: the chain, loader and backpointer waves of lt_vit.hip, the
+    // backtrace in the same launch when it fits
+    rc = lt_impl::vit_bigram(pb, W, num_frames, bp, qstar, path_weight, grad, labels, arcs,
+                             label_convention, stream);
+    if (rc != LT_EUNSUPPORTED) return rc;
   } else {
     lt_problem p2 = *pb;
     p2.max_labels = 0;
@@ -1196,10 +1198,6 @@ int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
     pl.a.qstar = qstar;
     if ((rc = launch_fwd(M_MAX, pl, bf16, pb->batch, st))) return rc;
   }
-  int seg = 0;
-  if (lt_impl::vit_bigram_eligible(pb) && lt_impl::vit_backtrace_lds(pb, &seg) > 0)
-    return lt_impl::vit_backtrace(pb, bp, qstar, num_frames, grad, labels, arcs, label_convention,
-                                  stream);
   BtArgs bt;
   bt.bp = bp; bt.qstar = qstar; bt.nfr = num_frames; bt.grad = grad;
   bt.labels = (long long*)labels; bt.arcs = arcs;

@@ -93,6 +93,110 @@ LT_DEVINL float vlds(const unsigned char* fr, int off) {
   else return *(const float*)(fr + off);
 }
 
+// Backtrace of the bigram backpointers in segments (one workgroup per
+// utterance, the utterance's backpointers staged in LDS): every segment of S
+// frames walks back from each of its C possible end states at once (the
+// segment's start state per end state), one thread composes the segments
+// from the best final state, then every segment emits its own frames'
+// labels. Serial depth S + T/S + S instead of T. The walk itself is the
+// generic backtrace's (lattices.py:229-247 through the one-hot arcs):
+// backpointer 0 = the blank self loop (label 0, state kept), k + 1 = the
+// arc from source k with label q.
+struct VbtArgs {
+  const unsigned char* bp;
+  const int* qstar;
+  const int* nfr;
+  const float* grad;
+  long long* labels;  // [B,T]
+  void* arcs;         // [B,T,C,R] or null
+  int B, T, C, R, conv, S;
+};
+
+template <bool BF16>
+LT_DEVINL void st_arc(void* arcs, long long e, float v) {
+  if constexpr (BF16) ((unsigned short*)arcs)[e] = (unsigned short)(__float_as_uint(v) >> 16);
+  else ((float*)arcs)[e] = v;
+}
+
+// utterance b's backtrace by one workgroup of 256 threads, its backpointers
+// staged in `lds` (vit_backtrace_lds bytes)
+template <bool BF16>
+LT_DEVINL void backtrace_body(const VbtArgs& a, int b, int tid, unsigned char* lds) {
+  const int C = a.C, R = a.R, S = a.S;
+  const long long FR = (long long)C * R;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  long long* lab = a.labels + (long long)b * a.T;
+  for (int t = nf + tid; t < a.T; t += 256) lab[t] = 0;  // padding frames
+  if (a.arcs) {
+    const long long n = (long long)a.T * FR;
+    for (long long e = tid; e < n; e += 256) st_arc<BF16>(a.arcs, (long long)b * a.T * FR + e, 0.f);
+  }
+  const int nseg = (nf + S - 1) / S;
+  unsigned char* rows = lds;                          // [nf][C]
+  unsigned char* start = lds + ((nf * C + 15) & ~15);  // [nseg][C]
+  int* endq = (int*)(start + ((nseg * C + 15) & ~15));  // [nseg]
+  const unsigned char* src = a.bp + (long long)b * a.T * C;
+  const int nb = nf * C;
+  if ((((uintptr_t)src) & 15) == 0) {
+    // 16-byte loads, four in flight per thread before their LDS stores
+    const int n16 = nb >> 4;
+    for (int e = tid; e < n16; e += 1024) {
+      uint4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (e + 256 * k < n16) v[k] = ((const uint4*)src)[e + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (e + 256 * k < n16) ((uint4*)rows)[e + 256 * k] = v[k];
+    }
+    for (int e = (n16 << 4) + tid; e < nb; e += 256) rows[e] = src[e];
+  } else {
+    for (int e = tid * 4; e < nb; e += 1024) {
+      if (e + 4 <= nb && ((((uintptr_t)(src + e)) & 3) == 0)) {
+        *(unsigned*)(rows + e) = *(const unsigned*)(src + e);
+      } else {
+        for (int k = e; k < nb && k < e + 4; ++k) rows[k] = src[k];
+      }
+    }
+  }
+  __syncthreads();
+  // each (segment, end state): the state before the segment's first frame
+  for (int x = tid; x < nseg * C; x += 256) {
+    const int sg = x / C;
+    int q = x - sg * C;
+    const int t1 = min(nf, (sg + 1) * S);
+    for (int t = t1 - 1; t >= sg * S; --t) {
+      const int i = rows[t * C + q];
+      q = i ? i - 1 : q;
+    }
+    start[x] = (unsigned char)q;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int q = nf > 0 ? a.qstar[b] : 0;
+    for (int sg = nseg - 1; sg >= 0; --sg) {
+      endq[sg] = q;
+      q = start[sg * C + q];
+    }
+  }
+  __syncthreads();
+  if (a.arcs) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // zero fill before the scatter
+  __syncthreads();
+  const float gb = a.grad ? a.grad[b] : 1.f;
+  for (int sg = tid; sg < nseg; sg += 256) {
+    int q = endq[sg];
+    const int t1 = min(nf, (sg + 1) * S);
+    for (int t = t1 - 1; t >= sg * S; --t) {
+      const int i = rows[t * C + q];
+      const int p = i ? i - 1 : q, y = i ? q : 0;
+      lab[t] = i ? (a.conv == LT_LABELS_REFERENCE ? (long long)(y - 1) : (long long)y) : 0LL;
+      if (a.arcs) st_arc<BF16>(a.arcs, ((long long)b * a.T + t) * FR + (long long)p * R + y, gb);
+      q = p;
+    }
+  }
+}
+
 // The alpha chain, a loader and the backpointers on separate waves of one
 // workgroup (round 3: chain and backpointers apart, 0.882 -> 0.742 ms at
 // cfg4 with two backpointer waves dealing the frames round robin).
@@ -127,6 +231,9 @@ LT_DEVINL float vlds(const unsigned char* fr, int off) {
 #ifndef LT_VIT_SAL
 #define LT_VIT_SAL 16
 #endif
+#ifndef LT_VIT_BT_FUSE
+#define LT_VIT_BT_FUSE 1  // the backtrace in the forward's launch when it fits
+#endif
 constexpr int kRing = 10;          // raw frames: kRing - 2 in flight, taken in pairs
 constexpr int kTw = LT_VIT_TW;     // transposed frames
 constexpr int kSAl = LT_VIT_SAL;   // alpha rows
@@ -139,7 +246,7 @@ constexpr int kWaitSpins = 1 << 24;                   // progress waits time out
 constexpr int kPL = 1 + kBpWaves;                     // s_prog index of the loader
 
 template <bool BF16, bool FULL>
-__global__ __launch_bounds__(64 * (2 + kBpWaves)) void vit_split_kernel(const VitArgs a) {
+__global__ __launch_bounds__(64 * (2 + kBpWaves)) void vit_split_kernel(const VitArgs a, const VbtArgs bt) {
   // alpha rows: [0, 17) and [20, 36) the two halves' sources (b128 reads),
   // [40, 72) spare slots for the chain's branch-free store
   __shared__ __attribute__((aligned(16))) float s_al[kSAl][72];
@@ -461,112 +568,21 @@ __global__ __launch_bounds__(64 * (2 + kBpWaves)) void vit_split_kernel(const Vi
       (void)w00;
     }
   }
+  // every wave's global stores (the backpointers, qstar) done before the barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0 && s_err) a.dist[b] = __builtin_nanf("");  // a timed-out wait: no silent result
-}
-
-// Backtrace of the bigram backpointers in segments (one workgroup per
-// utterance, the utterance's backpointers staged in LDS): every segment of S
-// frames walks back from each of its C possible end states at once (the
-// segment's start state per end state), one thread composes the segments
-// from the best final state, then every segment emits its own frames'
-// labels. Serial depth S + T/S + S instead of T. The walk itself is the
-// generic backtrace's (lattices.py:229-247 through the one-hot arcs):
-// backpointer 0 = the blank self loop (label 0, state kept), k + 1 = the
-// arc from source k with label q.
-struct VbtArgs {
-  const unsigned char* bp;
-  const int* qstar;
-  const int* nfr;
-  const float* grad;
-  long long* labels;  // [B,T]
-  void* arcs;         // [B,T,C,R] or null
-  int B, T, C, R, conv, S;
-};
-
-template <bool BF16>
-LT_DEVINL void st_arc(void* arcs, long long e, float v) {
-  if constexpr (BF16) ((unsigned short*)arcs)[e] = (unsigned short)(__float_as_uint(v) >> 16);
-  else ((float*)arcs)[e] = v;
+  // the backtrace in the same workgroup (bt.labels set when the utterance's
+  // backpointers fit the transposed ring's LDS, vit_backtrace_lds): they are
+  // this workgroup's own stores, read back after the barrier; no second
+  // launch (cfg4: 0.636 -> 0.633 ms)
+  if (bt.labels) backtrace_body<BF16>(bt, b, tid, (unsigned char*)&s_tw[0][0][0]);
 }
 
 template <bool BF16>
 __global__ __launch_bounds__(256) void vit_backtrace_kernel(const VbtArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int C = a.C, R = a.R, S = a.S;
-  const long long FR = (long long)C * R;
-  int nf = a.nfr[b];
-  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
-  long long* lab = a.labels + (long long)b * a.T;
-  for (int t = nf + tid; t < a.T; t += 256) lab[t] = 0;  // padding frames
-  if (a.arcs) {
-    const long long n = (long long)a.T * FR;
-    for (long long e = tid; e < n; e += 256) st_arc<BF16>(a.arcs, (long long)b * a.T * FR + e, 0.f);
-  }
-  const int nseg = (nf + S - 1) / S;
-  unsigned char* rows = lds;                          // [nf][C]
-  unsigned char* start = lds + ((nf * C + 15) & ~15);  // [nseg][C]
-  int* endq = (int*)(start + ((nseg * C + 15) & ~15));  // [nseg]
-  const unsigned char* src = a.bp + (long long)b * a.T * C;
-  const int nb = nf * C;
-  if ((((uintptr_t)src) & 15) == 0) {
-    // 16-byte loads, four in flight per thread before their LDS stores
-    const int n16 = nb >> 4;
-    for (int e = tid; e < n16; e += 1024) {
-      uint4 v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (e + 256 * k < n16) v[k] = ((const uint4*)src)[e + 256 * k];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (e + 256 * k < n16) ((uint4*)rows)[e + 256 * k] = v[k];
-    }
-    for (int e = (n16 << 4) + tid; e < nb; e += 256) rows[e] = src[e];
-  } else {
-    for (int e = tid * 4; e < nb; e += 1024) {
-      if (e + 4 <= nb && ((((uintptr_t)(src + e)) & 3) == 0)) {
-        *(unsigned*)(rows + e) = *(const unsigned*)(src + e);
-      } else {
-        for (int k = e; k < nb && k < e + 4; ++k) rows[k] = src[k];
-      }
-    }
-  }
-  __syncthreads();
-  // each (segment, end state): the state before the segment's first frame
-  for (int x = tid; x < nseg * C; x += 256) {
-    const int sg = x / C;
-    int q = x - sg * C;
-    const int t1 = min(nf, (sg + 1) * S);
-    for (int t = t1 - 1; t >= sg * S; --t) {
-      const int i = rows[t * C + q];
-      q = i ? i - 1 : q;
-    }
-    start[x] = (unsigned char)q;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int q = nf > 0 ? a.qstar[b] : 0;
-    for (int sg = nseg - 1; sg >= 0; --sg) {
-      endq[sg] = q;
-      q = start[sg * C + q];
-    }
-  }
-  __syncthreads();
-  if (a.arcs) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // zero fill before the scatter
-  __syncthreads();
-  const float gb = a.grad ? a.grad[b] : 1.f;
-  for (int sg = tid; sg < nseg; sg += 256) {
-    int q = endq[sg];
-    const int t1 = min(nf, (sg + 1) * S);
-    for (int t = t1 - 1; t >= sg * S; --t) {
-      const int i = rows[t * C + q];
-      const int p = i ? i - 1 : q, y = i ? q : 0;
-      lab[t] = i ? (a.conv == LT_LABELS_REFERENCE ? (long long)(y - 1) : (long long)y) : 0LL;
-      if (a.arcs) st_arc<BF16>(a.arcs, ((long long)b * a.T + t) * FR + (long long)p * R + y, gb);
-      q = p;
-    }
-  }
+  backtrace_body<BF16>(a, blockIdx.x, threadIdx.x, lds);
 }
 
 }  // namespace
@@ -579,8 +595,9 @@ bool vit_bigram_eligible(const lt_problem* pb) {
 
 // MaxTropical forward (distance, best final state, backpointers) of every
 // utterance; lt_viterbi's backtrace reads the backpointers.
+namespace {
 int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, unsigned char* bp,
-                       int* qstar, float* dist, void* stream) {
+                       int* qstar, float* dist, void* stream, const VbtArgs* bt) {
   VitArgs a;
   a.W = (const unsigned char*)W;
   a.nfr = nfr;
@@ -604,13 +621,15 @@ int vit_bigram_forward(const lt_problem* pb, const void* W, const int32_t* nfr, 
                                : (const void*)vit_split_kernel<false, true>)
                        : (bf16 ? (const void*)vit_split_kernel<true, false>
                                : (const void*)vit_split_kernel<false, false>);
-  void* args[] = {(void*)&a};
+  VbtArgs none{};
+  void* args[] = {(void*)&a, (void*)(bt ? bt : &none)};
   hipError_t e =
       hipLaunchKernel(k, dim3(a.B), dim3(64 * (2 + kBpWaves)), args, 0, (hipStream_t)stream);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;
 }
+}  // namespace
 
 // LDS bytes of vit_backtrace for T frames (0: too long, use the generic one)
 int vit_backtrace_lds(const lt_problem* pb, int* seg) {
@@ -622,13 +641,37 @@ int vit_backtrace_lds(const lt_problem* pb, int* seg) {
   return bytes <= 144 * 1024 ? (int)bytes : 0;
 }
 
-int vit_backtrace(const lt_problem* pb, const unsigned char* bp, const int* qstar,
-                  const int32_t* nfr, const float* grad, int64_t* labels, void* arcs,
-                  int32_t conv, void* stream) {
+namespace {
+VbtArgs bt_args(const lt_problem* pb, const unsigned char* bp, const int* qstar, const int32_t* nfr,
+                const float* grad, int64_t* labels, void* arcs, int32_t conv) {
   VbtArgs a;
   a.bp = bp; a.qstar = qstar; a.nfr = nfr; a.grad = grad;
   a.labels = (long long*)labels; a.arcs = arcs;
   a.B = pb->batch; a.T = pb->max_frames; a.C = pb->vocab_size + 1; a.R = a.C; a.conv = conv;
+  a.S = 0;
+  return a;
+}
+}  // namespace
+
+// the bigram forward and its backtrace in ONE launch while the utterance's
+// backpointers fit the forward's transposed-ring LDS, else the two launches
+int vit_bigram(const lt_problem* pb, const void* W, const int32_t* nfr, unsigned char* bp,
+               int* qstar, float* dist, const float* grad, int64_t* labels, void* arcs,
+               int32_t conv, void* stream) {
+  VbtArgs bt = bt_args(pb, bp, qstar, nfr, grad, labels, arcs, conv);
+  const int lds = vit_backtrace_lds(pb, &bt.S);
+  if (LT_VIT_BT_FUSE && lds > 0 && lds <= (int)(kTw * 5 * 64 * sizeof(float4)))
+    return vit_bigram_forward(pb, W, nfr, bp, qstar, dist, stream, &bt);
+  int rc = vit_bigram_forward(pb, W, nfr, bp, qstar, dist, stream, nullptr);
+  if (rc) return rc;
+  if (lds > 0) return vit_backtrace(pb, bp, qstar, nfr, grad, labels, arcs, conv, stream);
+  return LT_EUNSUPPORTED;  // the caller runs the generic backtrace
+}
+
+int vit_backtrace(const lt_problem* pb, const unsigned char* bp, const int* qstar,
+                  const int32_t* nfr, const float* grad, int64_t* labels, void* arcs,
+                  int32_t conv, void* stream) {
+  VbtArgs a = bt_args(pb, bp, qstar, nfr, grad, labels, arcs, conv);
   const int lds = vit_backtrace_lds(pb, &a.S);
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   const void* k = bf16 ? (const void*)vit_backtrace_kernel<true> : (const void*)vit_backtrace_kernel<false>;
