@@ -51,6 +51,11 @@
 // throughout.
 #include "lt_kernels.h"
 
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+
 namespace {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
@@ -99,8 +104,13 @@ struct CkArgs {
   float* nabd;             // [B,K+1,NPG] num alpha at chunk starts
   float* nbbd;             // [B,K+1,NPG] num beta at chunk starts
   float* cf;               // [B,T] frame offsets c_t = ceil(max W_t) (phase A's)
-  unsigned* ready;         // [B,K] chunk k's record and bands published (scratch, zeroed per call)
-  unsigned* prog;          // [B,4] phase 2's boundaries done per walk (zeroed with ready)
+  // hand-off words, tagged per call (no zeroing pass): a word carries this
+  // call's tag or is not yet written in this call (an older call's tag, or
+  // whatever the scratch held: a 62-bit / 40-bit random tag matches it with
+  // probability 2^-62 / 2^-40)
+  unsigned long long* ready;  // [B,K] ep_tag | state (1 ok, 2 / 3 out of range) of chunk k
+  unsigned long long* prog;   // [B,4] pg_tag | phase 2's boundaries done per walk (< 2^24)
+  unsigned long long ep_tag, pg_tag;
   float* mid;              // [B,2] phase 1's den alpha and num alpha offsets at the middle
   float* loss;
   float* log_z;            // state copies (read by C)
@@ -377,6 +387,7 @@ LT_DEVINL void mask_frame(int V, int lane, const int* boff, const int* loff,
 }
 
 typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // Write-through (sc1) stores for what phase B reads in the same launch: the
@@ -624,8 +635,8 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   // its walks take the hand-off timeout route (tests/test_gpu_diag.py)
   const bool withhold = LT_ABL(a, 512) && b == 0 && k == 1;
   if (lane == 0 && !withhold)
-    __hip_atomic_store((gu32*)(a.ready + id), bad ? (unsigned)bad : 1u, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu64*)(a.ready + id), a.ep_tag | (bad ? (unsigned)bad : 1u),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Phase B's side of the hand-off, one wave: chunks [0, hi] (forward walks)
@@ -641,19 +652,28 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
 // its own vmcnt(0): the compiler sees no memory instruction of its own in a
 // walk's step loop, so it has no reason to drain the walk's in-flight
 // LDS-DMA record loads at every step (it did for the builtin forms).
-LT_DEVINL unsigned poll_flag(const unsigned* p) {
-  unsigned v;
-  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+LT_DEVINL unsigned long long poll_flag(const unsigned long long* p) {
+  unsigned long long v;
+  asm volatile("global_load_dwordx2 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
   return v;
+}
+// a chunk's state in this call (0: not yet published)
+LT_DEVINL unsigned flag_state(unsigned long long v, unsigned long long tag) {
+  return (v & ~3ull) == tag ? (unsigned)(v & 3) : 0u;
+}
+// boundaries a phase-2 walk has done in this call
+LT_DEVINL int prog_count(unsigned long long v, unsigned long long tag) {
+  return (v & ~0xFFFFFFull) == tag ? (int)(v & 0xFFFFFF) : 0;
 }
 LT_DEVINL void acquire_agent() {
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
 }
 struct ChunkReady {
-  const unsigned* f;
+  const unsigned long long* f;
+  unsigned long long tag;
   int lo, hi, Kl, ok, bad, strict;
-  LT_DEVINL ChunkReady(const unsigned* flags, int kl, int st)
-      : f(flags), lo(kl), hi(-1), Kl(kl), ok(1), bad(0), strict(st) {}
+  LT_DEVINL ChunkReady(const unsigned long long* flags, unsigned long long tg, int kl, int st)
+      : f(flags), tag(tg), lo(kl), hi(-1), Kl(kl), ok(1), bad(0), strict(st) {}
   LT_DEVINL void take(unsigned v, int lane, int* c) {
     const unsigned long long m = __builtin_amdgcn_ballot_w64(v != 0);
     *c = m == ~0ull ? 64 : __builtin_ctzll(~m);
@@ -669,7 +689,7 @@ struct ChunkReady {
     k = min(k, Kl - 1);
     for (unsigned spins = 0; k > hi; ++spins) {
       const int x = hi + 1 + lane;
-      const unsigned v = poll_flag(f + min(x, Kl - 1)) & (x < Kl ? ~0u : 0u);
+      const unsigned v = flag_state(poll_flag(f + min(x, Kl - 1)), tag) & (x < Kl ? ~0u : 0u);
       int c;
       take(v, lane, &c);
       if (c) {
@@ -686,7 +706,7 @@ struct ChunkReady {
     k = max(k, 0);
     for (unsigned spins = 0; k < lo; ++spins) {
       const int x = lo - 1 - lane;
-      const unsigned v = poll_flag(f + max(x, 0)) & (x >= 0 ? ~0u : 0u);
+      const unsigned v = flag_state(poll_flag(f + max(x, 0)), tag) & (x >= 0 ? ~0u : 0u);
       int c;
       take(v, lane, &c);
       if (c) {
@@ -760,7 +780,7 @@ LT_DEVINL void bd_store(float* p, float v, bool wt) {
 LT_DEVINL void prog_publish(const CkArgs& a, int b, int w, int n, int lane) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0)
-    __hip_atomic_store((gu32*)(a.prog + 4LL * b + w), (unsigned)n, __ATOMIC_RELAXED,
+    __hip_atomic_store((gu64*)(a.prog + 4LL * b + w), a.pg_tag | (unsigned)n, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -976,7 +996,7 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave, unsigned char* dyn
   if (threadIdx.x == 0) *wl.bad = 0;
   __syncthreads();
   CK_WSTAMP(2 * wave);
-  ChunkReady rd(a.ready + (long long)b * a.K, Kl, a.strict);
+  ChunkReady rd(a.ready + (long long)b * a.K, a.ep_tag, Kl, a.strict);
   if (ph == kWalkRest) {  // every chunk published (phase A's launch is over)
     rd.lo = 0;
     rd.hi = Kl - 1;
@@ -1329,14 +1349,16 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   // before any wave's loads of them (after the barriers below)
   if (a.cont && tid == 0) {
     const int need_a = k - Kh, need_b = Kh - (k + 1);
-    const unsigned* pg = a.prog + 4LL * b;
+    const unsigned long long* pg = a.prog + 4LL * b;
     int ok = 1;
     for (unsigned spins = 0;; ++spins) {
       bool done = true;
       if (need_a > 0)
-        done = (a.local || (int)poll_flag(pg + 0) >= need_a) && (int)poll_flag(pg + 2) >= need_a;
+        done = (a.local || prog_count(poll_flag(pg + 0), a.pg_tag) >= need_a) &&
+               prog_count(poll_flag(pg + 2), a.pg_tag) >= need_a;
       if (done && need_b > 0)
-        done = (a.local || (int)poll_flag(pg + 1) >= need_b) && (int)poll_flag(pg + 3) >= need_b;
+        done = (a.local || prog_count(poll_flag(pg + 1), a.pg_tag) >= need_b) &&
+               prog_count(poll_flag(pg + 3), a.pg_tag) >= need_b;
       if (done) break;
       if (spins > kSpinMax) {  // phase 2 never ran (a placement that starves it)
         ok = 0;
@@ -1898,6 +1920,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   a->c_bytes = c_bytes(L, a);
   a->L = L;
   a->K = std::max(1, (a->T + L - 1) / L);
+  if (a->K >= (1 << 24)) return lt_impl::set_error(LT_EUNSUPPORTED, "chunk: too many frames");
   a->NGc = (L + kGrp - 1) / kGrp;
   // workspace
   const long long B = a->B, K = a->K, T = a->T;
@@ -1913,7 +1936,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   w->mid = o; o += up256(8 * B);
   w->state = o;
   size_t s = 0;
-  w->ready = s; s += up256(4LL * B * K + 16LL * B);  // ready flags, then the progress words
+  w->ready = s; s += up256(8LL * B * K + 32LL * B);  // ready flags, then the progress words
   w->rec = s; s += up256(4LL * B * K * kRec);
   a->nbs = (a->NGc * (kGrp + 1) * a->NPG + 31) & ~31;
   w->nb = s; s += up256(4LL * B * K * a->nbs);
@@ -1943,8 +1966,8 @@ void ck_bind(CkArgs* a, const CkLayout& w, void* state, void* scratch) {
   a->mid = (float*)(st + w.mid);
   a->rec = sc ? (float*)(sc + w.rec) : nullptr;
   a->nb = sc ? (float*)(sc + w.nb) : nullptr;
-  a->ready = sc ? (unsigned*)(sc + w.ready) : nullptr;
-  a->prog = sc ? (unsigned*)(sc + w.ready) + (long long)a->B * a->K : nullptr;
+  a->ready = sc ? (unsigned long long*)(sc + w.ready) : nullptr;
+  a->prog = sc ? (unsigned long long*)(sc + w.ready) + (long long)a->B * a->K : nullptr;
 }
 
 int ck_launch(const void* k, int grid, int lds, hipStream_t st, const CkArgs& a,
@@ -1994,8 +2017,26 @@ int ck_cus() {
     cus[dev] = 0;
   return cus[dev];
 }
-// Phases A and B: the ready flags zeroed (a memset node under capture), then
-// ONE launch with the walks among its workgroups, or A and B as two launches
+// This call's hand-off tags (CkArgs::ready / prog): splitmix64 over a
+// per-process counter seeded from the clock and the pid, so consecutive calls
+// never share a tag and a stale word from an earlier call (or scratch
+// garbage) reads as "not yet published"; no memset before the launch.
+unsigned long long ck_seed() {
+  unsigned long long z = (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count();
+  z ^= (unsigned long long)getpid() << 32;
+  z ^= (unsigned long long)(uintptr_t)&ck_cus;
+  return z;
+}
+void ck_tags(CkArgs& a) {
+  static std::atomic<unsigned long long> ctr{ck_seed()};
+  unsigned long long z = ctr.fetch_add(0x9E3779B97F4A7C15ull) + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  a.ep_tag = ((z >> 2) | (1ull << 61)) << 2;                 // bits 2..63, never 0
+  a.pg_tag = ((z & 0xFFFFFFFFFFull) | (1ull << 39)) << 24;  // bits 24..63, never 0
+}
+// Phases A and B: ONE launch with the walks among its workgroups, or A and B as two launches
 // when the walks (one workgroup per utterance, at most one of the two
 // workgroup slots per CU the launch's registers allow) could hold half the
 // chip's slots while they wait (B > CUs), or LT_CHUNK_FUSE=0. The walks'
@@ -2005,8 +2046,7 @@ int ck_cus() {
 // (tools/walk_sweep.py: B = 64 best at 0-25 %, B = 128 at 50-65 %;
 // LT_CHUNK_WALK_AT overrides, in percent).
 int ck_launch_ab(CkArgs& a, bool bf16, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(a.ready, 0, 4LL * a.B * a.K + 16LL * a.B, st);
-  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  ck_tags(a);
   const bool fuse = a.B <= ck_cus() && ck_env("LT_CHUNK_FUSE", 1) != 0;
   a.nc = fuse ? a.B : 0;
   const long long items = 2LL * a.B * ((a.K + 1) / 2);

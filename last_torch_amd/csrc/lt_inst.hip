@@ -56,6 +56,25 @@ int LT_CAT4(launch_fwdbwd_, LT_LGN, _, LT_P)(const Plan& pf, const Plan& pb, boo
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;
 }
+// the frame-serial fallback's forward and backward in one launch (same
+// geometry for both plans, direct dW stores)
+int LT_CAT4(launch_serial_, LT_LGN, _, LT_P)(const Plan& pf, const Plan& pb, bool bf16, int nb,
+                                           hipStream_t st) {
+  if (nb == 0) return LT_OK;
+  const void* k = bf16 ? (pf.wst ? (const void*)serial_kernel<true, true, true, LT_LG, LT_P>
+                                 : (const void*)serial_kernel<true, false, true, LT_LG, LT_P>)
+                       : (pf.wst ? (const void*)serial_kernel<false, true, true, LT_LG, LT_P>
+                                 : (const void*)serial_kernel<false, false, true, LT_LG, LT_P>);
+  const int lds = pf.lds_bytes > pb.lds_bytes ? pf.lds_bytes : pb.lds_bytes;
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  KArgs af = pf.a, ab = pb.a;
+  void* args[] = {(void*)&af, (void*)&ab};
+  e = hipLaunchKernel(k, dim3(nb), dim3(pf.threads), args, lds, st);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  return LT_OK;
+}
 int LT_CAT4(launch_bwd_, LT_LGN, _, LT_P)(const Plan& pl, bool bf16, int grid, hipStream_t st) {
   if (pl.ck) {
     if (bf16) return pl.wst ? launch_one(bwd_kernel<true, true, false, LT_LG, LT_P, true>, pl, grid, st)

@@ -1832,6 +1832,20 @@ template <bool BF16, bool WST, bool DST, int LG, int P, bool CK = false>
 __global__ __launch_bounds__(1024) void bwd_kernel(const KArgs a) {
   bwd_body<BF16, WST, DST, LG, P, CK>(a, blockIdx.x);
 }
+// The frame-serial loss + dW of one utterance in ONE launch (lt_loss_grad's
+// fallback for the utterances only[b] marks): the Log forward (alpha,
+// alpha^n, loss) and then, in the same workgroup, the backward with the
+// marginals. The forward's global stores (checkpoints, log_z, num) are this
+// workgroup's own, so a vmcnt drain and the barrier hand them over; every
+// other workgroup returns at once (one launch a call instead of two).
+template <bool BF16, bool WST, bool DST, int LG, int P>
+__global__ __launch_bounds__(1024) void serial_kernel(const KArgs af, const KArgs ab) {
+  fwd_body<M_LOG, BF16, WST, LG, P>(af, blockIdx.x);
+  if (af.only && !af.only[blockIdx.x]) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bwd_body<BF16, WST, DST, LG, P, false, (int)sizeof(KArgs)>(ab, blockIdx.x);
+}
 // The checkpointing pair in one launch: workgroups [0, nb) run the Log
 // forward (alpha, alpha^n, loss) and [nb, 2 nb) the checkpointing backward
 // (beta, beta^n). Both depend only on W, so they run side by side, as
@@ -1863,7 +1877,8 @@ struct Plan {
 #define LT_DECL(LG, P)                                                                   \
   int launch_fwd_##LG##_##P(int mode, const Plan& pl, bool bf16, int grid, hipStream_t st); \
   int launch_bwd_##LG##_##P(const Plan& pl, bool bf16, int grid, hipStream_t st);          \
-  int launch_fwdbwd_##LG##_##P(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStream_t st);
+  int launch_fwdbwd_##LG##_##P(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStream_t st); \
+  int launch_serial_##LG##_##P(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStream_t st);
 LT_VARIANTS(LT_DECL)
 #undef LT_DECL
 int set_error(int code, const char* msg);

@@ -857,8 +857,7 @@ int serial_loss(const lt_problem* pb, int local_norm, const void* W, const int32
     if ((rc = hip_check(hipMemsetAsync(log_z, 0, sizeof(float) * pb->batch, st), "memset")))
       return rc;
   }
-  if ((rc = launch_fwd(M_LOG, pf, bf16, pb->batch, st))) return rc;
-  if (!dW) return LT_OK;
+  if (!dW) return launch_fwd(M_LOG, pf, bf16, pb->batch, st);
   Plan pl;
   if ((rc = plan(pb, g, 1, F_NUM | (local_norm ? F_LOCAL : F_DEN), &pl))) return rc;
   bind_streams(pl.a, W, local_norm ? nullptr : alpha, alpha_num);
@@ -866,6 +865,16 @@ int serial_loss(const lt_problem* pb, int local_norm, const void* W, const int32
   a.nfr = num_frames; a.labels = labels; a.nlab = num_labels;
   a.log_z_in = log_z; a.num_in = num; a.grad = grad; a.dW = dW;
   a.only = only;
+  // forward and backward in one launch when the two plans share a geometry
+  // (the usual case): lt_loss_grad's fallback then costs one (empty) launch
+  if (pl.dst && pf.lg == pl.lg && pf.tmax == pl.tmax && pf.wst == pl.wst &&
+      pf.threads == pl.threads) {
+#define LT_CASE(LG, P) \
+  if (pf.lg == LG && pf.tmax == P) return lt_impl::launch_serial_##LG##_##P(pf, pl, bf16, pb->batch, st);
+    LT_VARIANTS(LT_CASE)
+#undef LT_CASE
+  }
+  if ((rc = launch_fwd(M_LOG, pf, bf16, pb->batch, st))) return rc;
   if (!pl.dst) {
     const long long NP = pb->max_labels + 1;
     const long long nm = (long long)pb->batch * pb->max_frames * NP * 2 * 4;
