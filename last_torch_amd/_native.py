@@ -277,8 +277,8 @@ def loss_backward(W, num_frames, labels, num_labels, log_z, num, alpha, alpha_nu
 def chunk_path(batch, frames, labels, vocab_size, context_size, device=None):
   """Whether lt_loss_grad runs the chunked two-level scan (lt_chunk.hip) for
   this shape; mirrors lt_impl::chunk_preferred: an eligible shape and
-  5 * batch <= 3 * CUs (beyond that the frame-serial checkpointing design is
-  faster, tools/design_ab.py)."""
+  16 * batch <= 11 * CUs (beyond that the frame-serial checkpointing design is
+  faster, profiles/r04_design_crossover.txt)."""
   if context_size != 1 or not 1 <= vocab_size <= 32 or labels + 1 > 128 or frames < 1:
     return False
   C = vocab_size + 1
@@ -287,7 +287,7 @@ def chunk_path(batch, frames, labels, vocab_size, context_size, device=None):
   if not torch.cuda.is_available():
     return True
   cus = torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
-  return 5 * batch <= 3 * cus
+  return 16 * batch <= 11 * cus
 
 
 def fused_path(batch, frames, labels, vocab_size, context_size, device=None, bf16=False):

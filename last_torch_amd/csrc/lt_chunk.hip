@@ -2092,14 +2092,16 @@ bool chunk_eligible(const lt_problem* pb) {
 // The chunked scan's phases A and C are throughput work that grows with B,
 // while the frame-serial checkpointing design (pipe_kernel + marg_kernel)
 // hides its chains behind idle CUs until 2B recursions fill them: measured
-// crossover B ~ 150 on 256 CUs (tools/design_ab.py: chunk 0.377 / 0.691 /
-// 1.005 / 1.309 ms against 0.586 / 0.752 / 0.887 / 1.127 ms at B = 64 / 128 /
-// 192 / 256). LT_CHUNK=1 forces the chunked scan, LT_CHUNK=0 forbids it.
+// crossover B ~ 178 on 256 CUs (round 4, profiles/r04_design_crossover.txt:
+// chunk 0.641 / 0.801 / 0.966 / 1.130 / 1.294 ms against 0.746 / 0.863 /
+// 0.924 / 0.994 / 1.121 ms at B = 128 / 160 / 192 / 224 / 256), so the chunked
+// scan while 16 B <= 11 CUs (B <= 176). LT_CHUNK=1 forces the chunked scan,
+// LT_CHUNK=0 forbids it.
 bool chunk_preferred(const lt_problem* pb) {
   if (!chunk_eligible(pb)) return false;
   if (ck_env("LT_CHUNK", -1) == 1) return true;
   const long long cus = ck_cus();
-  return cus <= 0 || 5LL * pb->batch <= 3LL * cus;
+  return cus <= 0 || 16LL * pb->batch <= 11LL * cus;
 }
 }  // namespace lt_impl
 

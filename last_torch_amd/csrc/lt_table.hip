@@ -111,29 +111,36 @@ LT_DEVINL float t_times(float a, float b) { return SR == M_REAL ? a * b : a + b;
 
 constexpr int kTabMaxThreads = 512;
 
-// Maximum over the workgroup (every thread passes its value, every thread
-// gets the result); two barriers.
-LT_DEVINL float t_block_max(float v) {
-  __shared__ float red[kTabMaxThreads / 64];
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  float m = red[0];
-  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
-  __syncthreads();
-  return m;
-}
-
 // Log vectors are kept relative to an integer offset near their maximum
 // (exact in fp32), so a recursion over T frames rounds small numbers, not
 // values of magnitude |log_z| (the tuned kernels' scheme): the
-// offset after a frame whose new vector is v. Every thread returns it.
-LT_DEVINL float t_renorm_shift(const float* v, int S) {
-  float m = -kInf;
-  for (int q = threadIdx.x; q < S; q += blockDim.x) m = fmaxf(m, v[q]);
-  m = t_block_max(m);
-  return __builtin_isfinite(m) ? floorf(m) : 0.f;
+// offset after a frame is floor(max) of its new vector.
+// That offset without a pass of its own: the threads that write the new
+// vector's values fold them into an LDS slot (ds_max on an order-preserving
+// int image) and, after the barrier that publishes the vector, every thread
+// reads the slot. Three slots rotate: frame t writes slot t % 3, reads it
+// after its barrier, and resets slot (t + 1) % 3 for the next frame (the
+// last frame that read it was t - 2).
+LT_DEVINL int t_ord(float f) {
+  const int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7fffffff;
 }
+LT_DEVINL float t_unord(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
+struct MaxSlots {
+  int* s;  // [3] in LDS
+  LT_DEVINL void init() const {
+    if (threadIdx.x < 3) s[threadIdx.x] = t_ord(-kInf);
+  }
+  LT_DEVINL void put(int t, float v) const { atomicMax(s + t % 3, t_ord(v)); }
+  LT_DEVINL void reset_next(int t) const {
+    if (threadIdx.x == 0) s[(t + 1) % 3] = t_ord(-kInf);
+  }
+  // after the barrier: the integer offset floor(max) (0 when not finite)
+  LT_DEVINL float shift(int t) const {
+    const float m = t_unord(s[t % 3]);
+    return __builtin_isfinite(m) ? floorf(m) : 0.f;
+  }
+};
 
 // Graph accessors: the context lattice (states p, in-arcs from the CSR) and
 // the string acceptor (positions u, one in-arc from u-1; lattices.py:314-338).
@@ -519,6 +526,9 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   for (int q = tid; q < S; q += nthr) va[q] = q == 0 ? t_one<SR>() : t_zero<SR>();
   if (NUM && tid == 0) t_walk(a, b, ctx, yn);
+  __shared__ int slot_mem[3];
+  const MaxSlots slots{slot_mem};
+  slots.init();
   __syncthreads();
   using DG = typename std::conditional<STAGE, DenGraphP, DenGraph>::type;
   DG dg{g_off, g_arc, a.V, R};
@@ -539,10 +549,11 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
   if (NUM) cs.fetch(nf > 0 ? 2 * S : 0, ldc(wb));
   constexpr bool kOff = SR == M_LOG;  // Log: va relative to the integer offset O
   float O = 0.f;
-  // the vector after a frame: Log renormalised to a new integer offset
-  auto settle = [&](const float* src) {
+  // the vector after frame t (its writers put every value into the slot,
+  // then a barrier): Log renormalised to a new integer offset
+  auto settle = [&](int t, const float* src) {
     if constexpr (kOff) {
-      const float sp = t_renorm_shift(src, S);
+      const float sp = slots.shift(t);
       for (int q = tid; q < S; q += nthr) va[q] = src[q] - sp;
       O += sp;
     } else {
@@ -587,9 +598,11 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
           o = bt + r;
         }
         vn[q] = o;
+        if (kOff) slots.put(t, o);
       }
+      if (kOff) slots.reset_next(t);
       __syncthreads();
-      settle(vn);
+      settle(t, vn);
       __syncthreads();
       continue;
     }
@@ -619,6 +632,7 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
         const float term = t_times<SR>(vn[q], wr(bi));
         if constexpr (SR == M_LOG) {
           acc[q] = t_lae(acc[q], term);
+          if (i == K) slots.put(t, acc[q]);
         } else if constexpr (SR == M_MAX) {
           if (term > acc[q]) {
             acc[q] = term;
@@ -629,9 +643,10 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
         }
         vl[q] = vn[q];
       }
+      if (kOff && i == K) slots.reset_next(t);
       __syncthreads();
     }
-    settle(acc);
+    settle(t, acc);
     __syncthreads();
   }
   if (tid == 0) {
@@ -814,7 +829,7 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
   const float gb = a.gin ? a.gin[b] : 1.f;
   const bool live = !a.local && __builtin_isfinite(nm) && __builtin_isfinite(lz) && gb != 0.f;
   const long long FR = (long long)C * R;
-  // Log: beta relative to the integer offset Ob (t_renorm_shift); an arc's
+  // Log: beta relative to the integer offset Ob (MaxSlots); an arc's
   // marginal exp(alpha + w + beta' - log_z) takes the large terms first,
   // ((alpha - log_z) + Ob) + (w + beta'_rel)
   float Ob = 0.f;
@@ -830,6 +845,9 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
     else return alv;
   };
   for (int q = tid; q < C; q += nthr) beta[q] = t_one<SR>();  // every state final
+  __shared__ int slot_mem[3];
+  const MaxSlots slots{slot_mem};
+  slots.init();
   __syncthreads();
   using DG = typename std::conditional<STAGE, DenGraphP, DenGraph>::type;
   DG dg{g_off, g_arc, V, R};
@@ -843,6 +861,7 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
   RegStage<1> hs;
   if (live && nf > 0) hs.fetch(C, ldh(nf - 1));
   for (int t = a.T - 1; t >= 0; --t) {
+    const int it = a.T - 1 - t;  // the frames' order here (the offset slots rotate with it)
     const long long fo = ((long long)b * a.T + t) * FR;
     if (t >= nf || !live) {
       for (long long e = tid; e < FR; e += nthr) stw<false>(a.dW, fo + e, 0.f);
@@ -888,6 +907,7 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
       if (K == 0) {
         stw<false>(a.dW, fo + p * R, mg(af(la[p]), SR == M_LOG ? bb : beta[p]));
         nbA[p] = t_plus<SR>(bb, sv);
+        if (SR == M_LOG) slots.put(it, nbA[p]);
       } else {
         float mb = 0.f;
         for (int i = 0; i <= K; ++i)
@@ -896,6 +916,7 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
         nbA[p] = bb;  // blank[K] + beta
       }
     }
+    if (SR == M_LOG && K == 0) slots.reset_next(it);
     __syncthreads();
     float* cur = nbA;
     float* nxt = nbB;
@@ -925,15 +946,19 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
           }
         }
         const float sv = s.merge();
-        if (valid && !jg) nxt[p] = t_plus<SR>(t_times<SR>(wr(p * R), beta[p]), sv);
+        if (valid && !jg) {
+          nxt[p] = t_plus<SR>(t_times<SR>(wr(p * R), beta[p]), sv);
+          if (SR == M_LOG && j == 0) slots.put(it, nxt[p]);
+        }
       }
+      if (SR == M_LOG && j == 0) slots.reset_next(it);
       __syncthreads();
       float* tmp = cur;
       cur = nxt;
       nxt = tmp;
     }
     if constexpr (SR == M_LOG) {
-      const float sp = t_renorm_shift(cur, C);
+      const float sp = slots.shift(it);
       for (int p = tid; p < C; p += nthr) beta[p] = cur[p] - sp;
       Ob += sp;
     } else {

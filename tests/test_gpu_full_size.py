@@ -243,7 +243,7 @@ def test_cfg5_trigram_bf16(cuda):
   assert_grad_marginal_close(dW[idx].float().cpu().numpy(), rdW, den, rlz, rnum, bf16=True)
 
 
-@pytest.mark.parametrize('B', [8, 64, 120, 160, 192, 256, 512])
+@pytest.mark.parametrize('B', [8, 64, 120, 160, 176, 177, 192, 256, 512])
 def test_design_query_matches_python_mirrors(cuda, B):
   """lt_loss_grad_design (the C dispatch) and the Python mirrors the autograd
   path and bench.py use agree at the bench shape for every batch size."""
