@@ -228,15 +228,18 @@ struct RegStage {
 };
 
 // (+) over the in-arcs of q of x[src] (x) w; MaxTropical keeps the first max
+// xo: an offset taken off every x (the pending integer shift of a vector
+// kept unshifted; 0 leaves x exact)
 template <int SR, typename G, typename WR>
-LT_DEVINL float t_reduce(const G& g, int q, const float* x, const WR& wr, int* argpos) {
+LT_DEVINL float t_reduce(const G& g, int q, const float* x, const WR& wr, int* argpos,
+                         float xo = 0.f) {
   const int n = g.nin(q), p0 = g.pos0(q);
   if constexpr (SR == M_LOG) {
     Lse l;
     for (int k = 0; k < n; ++k) {
       int src, wi;
       g.arc(p0 + k, q, &src, &wi);
-      l.add(x[src] + wr(wi));
+      l.add((x[src] - xo) + wr(wi));
     }
     return l.get();
   } else if constexpr (SR == M_MAX) {
@@ -245,7 +248,7 @@ LT_DEVINL float t_reduce(const G& g, int q, const float* x, const WR& wr, int* a
     for (int k = 0; k < n; ++k) {
       int src, wi;
       g.arc(p0 + k, q, &src, &wi);
-      const float v = x[src] + wr(wi);
+      const float v = (x[src] - xo) + wr(wi);
       if (ra < 0 || v > r) {
         r = v;
         ra = p0 + k;
@@ -285,9 +288,9 @@ LT_DEVINL void lse_merge(Lse& l) {
 // as the serial reduce). `valid` false: the lane joins the shuffles only.
 template <int SR, int G, typename Gr, typename WR>
 LT_DEVINL float t_reduce_g(const Gr& g, int q, bool valid, const float* x, const WR& wr,
-                           int* argpos) {
+                           int* argpos, float xo = 0.f) {
   if constexpr (G == 1) {
-    return valid ? t_reduce<SR>(g, q, x, wr, argpos) : t_zero<SR>();
+    return valid ? t_reduce<SR>(g, q, x, wr, argpos, xo) : t_zero<SR>();
   } else {
     // the lane's terms are gathered NU at a time (independent LDS reads in
     // flight together), then folded in CSR order
@@ -306,7 +309,7 @@ LT_DEVINL float t_reduce_g(const Gr& g, int q, bool valid, const float* x, const
         if (k < n) {
           int src, wi;
           g.arc(p0 + k, q, &src, &wi);
-          v[i] = SR == M_REAL ? x[src] * wr(wi) : x[src] + wr(wi);
+          v[i] = SR == M_REAL ? x[src] * wr(wi) : (x[src] - xo) + wr(wi);
         }
       }
       if constexpr (SR == M_LOG) {
@@ -447,6 +450,43 @@ LT_DEVINL void tab_str_fwd_log(const TArgs& a, const int b, float* sm) {
   };
   RegStage<2> cs;
   cs.fetch(nf > 0 ? 2 * S : 0, ldc(wb));
+  if (K == 0) {
+    // FrameDependent: ONE barrier a frame -- (ia, fa) and (ic, fc) swap
+    // roles each frame, and the next frame's two weights per position go to
+    // the other compact buffer (il / fl, unused without expansions) while
+    // this frame reads its own
+    float* wl1 = il;  // [2S]
+    if (nf > 0) {
+      cs.store(wl, 2 * S, ldc(wb));
+      cs.fetch(nf > 1 ? 2 * S : 0, ldc(wb + fbytes));
+    }
+    __syncthreads();
+    float *pi = ia, *pf = fa, *qi = ic, *qf = fc;
+    for (int t = 0; t < a.T; ++t) {
+      if (a.alpha)
+        for (int u = tid; u < S; u += nthr) a.alpha[((long long)b * a.T + t) * S + u] = pi[u] + pf[u];
+      if (t >= nf) continue;  // padding frames carry alpha (lattices.py:460-461)
+      const float* w = (t & 1) ? wl1 : wl;
+      for (int u = tid; u < S; u += nthr)
+        lae_split(pi[u], pf[u] + w[2 * u], u >= 1 ? pi[u - 1] : -kInf,
+                  u >= 1 ? pf[u - 1] + w[2 * u - 1] : 0.f, qi[u], qf[u]);
+      if (t + 1 < nf) {
+        const unsigned char* wn = wb + (t + 1) * fbytes;
+        cs.store((t & 1) ? wl : wl1, 2 * S, ldc(wn));
+        cs.fetch(t + 2 < nf ? 2 * S : 0, ldc(wn + fbytes));
+      }
+      __syncthreads();
+      float* ti = pi; pi = qi; qi = ti;
+      float* tf = pf; pf = qf; qf = tf;
+    }
+    if (tid == 0) {
+      const int nl = a.nlab[b];
+      const float r = (nl >= 0 && nl <= a.U) ? pi[nl] + pf[nl] : -kInf;
+      a.dist[b] = r;  // lattices.py:375-377
+      if (a.loss) a.loss[b] = a.local ? -r : a.den_in[b] - r;  // lattices.py:131-183
+    }
+    return;
+  }
   for (int t = 0; t < a.T; ++t) {
     if (a.alpha)
       for (int u = tid; u < S; u += nthr) a.alpha[((long long)b * a.T + t) * S + u] = ia[u] + fa[u];
@@ -499,6 +539,119 @@ LT_DEVINL void tab_str_fwd_log(const TArgs& a, const int b, float* sm) {
   }
 }
 
+// ---- forward, FrameDependent (K = 0) context lattice: ONE barrier a frame --
+// The vector of frame t is kept unshifted in one of two LDS buffers, its
+// pending integer shift applied where it is read ((v - sp) + w, the same two
+// roundings as a shifted copy would take); the frame's weights are staged in
+// the other of two LDS frame buffers by the previous frame (registers loaded
+// a frame ahead). So a frame is: reduce (reads v_t, writes v_{t+1} and its
+// max slot, stores frame t + 1's weights), barrier.
+template <bool BF16, int SR, bool VIT, bool STAGE>
+LT_DEVINL void tab_fwd_k0_body(const TArgs& a, const int b, float* sm) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int S = a.C, R = a.R;
+  int* gsm = (int*)sm;
+  const int* g_off;
+  const int* g_arc;
+  const int* g_tab;
+  t_graph<STAGE>(a, gsm, &g_off, &g_arc, &g_tab);
+  (void)g_tab;
+  float* base = sm + (STAGE ? (a.C + 1 + 2 * a.C * a.V + 3) / 4 * 4 : 0);
+  float* cur = base;       // [S] frame t's vector (unshifted)
+  float* nxt = base + S;   // [S]
+  const long long FR = (long long)a.C * R;
+  float* w0 = base + 6 * S;  // STAGE: [2][FR] (the host's fwd_lds(S) + 4 FR more)
+  float* w1 = w0 + FR;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  for (int q = tid; q < S; q += nthr) cur[q] = q == 0 ? t_one<SR>() : t_zero<SR>();
+  __shared__ int slot_mem[3];
+  const MaxSlots slots{slot_mem};
+  slots.init();
+  using DG = typename std::conditional<STAGE, DenGraphP, DenGraph>::type;
+  DG dg{g_off, g_arc, a.V, R};
+  constexpr int G = 8;
+  constexpr bool kOff = SR == M_LOG;
+  const long long fbytes = FR * (BF16 ? 2 : 4);
+  const unsigned char* wb = a.W + (long long)b * a.T * fbytes;
+  FrameStage<BF16> fs;
+  if (STAGE && nf > 0) {
+    fs.fetch(wb, FR);
+    fs.store(w0, wb, FR);
+    fs.fetch(nf > 1 ? wb + fbytes : nullptr, FR);
+  }
+  __syncthreads();
+  float O = 0.f, sp = 0.f;  // the offset of cur - sp (sp included)
+  for (int t = 0; t < a.T; ++t) {
+    if (kOff && t >= 1 && t - 1 < nf) {  // frame t - 1's shift, once
+      sp = slots.shift(t - 1);
+      O += sp;
+    }
+    if (a.alpha)
+      for (int q = tid; q < S; q += nthr)
+        a.alpha[((long long)b * a.T + t) * S + q] = O + (cur[q] - sp);
+    if (t >= nf) continue;  // padding frames carry alpha (lattices.py:460-461)
+    const unsigned char* wf = wb + t * fbytes;
+    const float* wl = (t & 1) ? w1 : w0;
+    auto wr = [&](int i) { return STAGE ? wl[i] : ldw<BF16>(wf, i); };
+    int* bpt = VIT ? a.bp + ((long long)b * a.T + t) * a.C : nullptr;
+    for (int q0 = 0; q0 < S; q0 += nthr / G) {  // FrameDependent.forward, alignments.py:286-297
+      const int q = q0 + tid / G;
+      const bool valid = q < S;
+      int ap = -1;
+      const float r = t_reduce_g<SR, G>(dg, q, valid, cur, wr, &ap, sp);
+      if (!valid || (tid & (G - 1))) continue;
+      const float bt = t_times<SR>(cur[q] - sp, wr(dg.blank(q)));
+      float o;
+      if constexpr (SR == M_LOG) {
+        o = t_lae(bt, r);
+      } else if constexpr (SR == M_MAX) {
+        const bool keep = ap < 0 || bt >= r;  // Maximum keeps a iff a >= b
+        o = keep ? bt : r;
+        if (VIT) bpt[q] = keep ? -1 : ap;
+      } else {
+        o = bt + r;
+      }
+      nxt[q] = o;
+      if (kOff) slots.put(t, o);
+    }
+    if (STAGE && t + 1 < nf) {  // frame t + 1 into the other buffer, t + 2 in flight
+      fs.store((t & 1) ? w0 : w1, wf + fbytes, FR);
+      fs.fetch(t + 2 < nf ? wf + 2 * fbytes : nullptr, FR);
+    }
+    if (kOff) slots.reset_next(t);
+    __syncthreads();
+    float* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+  }
+  if (kOff && nf >= 1 && nf == a.T) {  // the last frame's shift (no padding frame applied it)
+    sp = slots.shift(nf - 1);
+    O += sp;
+  }
+  if (tid == 0) {
+    // (+)_q alpha_T[q] (lattices.py:496); MaxTropical: first max state
+    float r = t_zero<SR>();
+    int qs = 0;
+    if constexpr (SR == M_LOG) {
+      Lse l;
+      for (int q = 0; q < S; ++q) l.add(cur[q] - sp);
+      r = O + l.get();
+    } else if constexpr (SR == M_MAX) {
+      r = cur[0];
+      for (int q = 1; q < S; ++q)
+        if (cur[q] > r) {
+          r = cur[q];
+          qs = q;
+        }
+    } else {
+      for (int q = 0; q < S; ++q) r += cur[q];
+    }
+    a.dist[b] = r;
+    if (VIT) a.qstar[b] = qs;
+  }
+}
+
 // ---- forward: den (NUM = false) or string (NUM = true) shortest distance ----
 // STAGE: the frame's weights are copied to LDS once (coalesced) and the
 // in-arc gathers read LDS; otherwise they read W from global memory.
@@ -507,6 +660,12 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
   if constexpr (NUM && SR == M_LOG) {
     tab_str_fwd_log<BF16>(a, b, sm);
     return;
+  }
+  if constexpr (!NUM) {
+    if (a.K == 0) {
+      tab_fwd_k0_body<BF16, SR, VIT, STAGE>(a, b, sm);
+      return;
+    }
   }
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int S = NUM ? a.U + 1 : a.C, K = a.K, R = a.R;
@@ -807,8 +966,128 @@ struct OutSum {
   }
 };
 
+// ---- backward, FrameDependent (K = 0) context lattice: ONE barrier a frame --
+// As tab_fwd_k0_body: beta kept unshifted in two buffers (its pending integer
+// shift applied where it is read), the frame's weights and alpha row staged
+// by the previous frame in the other of two LDS buffers. A frame: marginals
+// and the new beta (and its max slot), the next frame's staging, barrier.
+template <bool BF16, bool STAGE, int SR>
+LT_DEVINL void tab_bwd_den_k0_body(const TArgs& a, const int b, float* sm) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int C = a.C, V = a.V, R = a.R;
+  int* gsm = (int*)sm;
+  const int* g_off;
+  const int* g_arc;
+  const int* g_tab;
+  t_graph<STAGE>(a, gsm, &g_off, &g_arc, &g_tab);
+  float* base = sm + (STAGE ? (C + 1 + 2 * C * V + 3) / 4 * 4 : 0);
+  float* cur = base;          // [C] beta_{t+1} (unshifted)
+  float* nxt = base + C;      // [C]
+  float* la0 = base + 2 * C;  // [2][C] alpha rows
+  const long long FR = (long long)C * R;
+  float* w0 = base + 4 * C;   // STAGE: [2][FR]
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const float lz = (a.local || SR == M_REAL) ? 0.f : a.den_in[b];
+  const float nm = a.num_in[b];
+  const float gb = a.gin ? a.gin[b] : 1.f;
+  const bool live = !a.local && __builtin_isfinite(nm) && __builtin_isfinite(lz) && gb != 0.f;
+  constexpr bool kOff = SR == M_LOG;
+  float Ob = 0.f, sp = 0.f;
+  auto mg = [&](float al_or_lo, float x) {
+    if constexpr (SR == M_LOG) return lt_exp(al_or_lo + x) * gb;
+    else return al_or_lo * x * gb;
+  };
+  auto af = [&](float alv) {
+    if constexpr (SR == M_LOG) return (alv - lz) + Ob;
+    else return alv;
+  };
+  for (int q = tid; q < C; q += nthr) cur[q] = t_one<SR>();  // every state final
+  __shared__ int slot_mem[3];
+  const MaxSlots slots{slot_mem};
+  slots.init();
+  using DG = typename std::conditional<STAGE, DenGraphP, DenGraph>::type;
+  DG dg{g_off, g_arc, V, R};
+  (void)dg;
+  constexpr int G = 8;  // lanes per state
+  const int esz = BF16 ? 2 : 4;
+  auto ldh = [&](int t) {  // alpha row of frame t, gathered one frame ahead
+    return [=](int e) { return a.hist[((long long)b * a.T + t) * C + e]; };
+  };
+  FrameStage<BF16> fs;
+  RegStage<1> hs;
+  if (live && nf > 0) {
+    const unsigned char* wl = a.W + ((long long)b * a.T + nf - 1) * FR * esz;
+    if (STAGE) {
+      fs.fetch(wl, FR);
+      fs.store(w0 + ((nf - 1) & 1) * FR, wl, FR);
+      fs.fetch(nf > 1 ? wl - FR * esz : nullptr, FR);
+    }
+    hs.fetch(C, ldh(nf - 1));
+    hs.store(la0 + ((nf - 1) & 1) * C, C, ldh(nf - 1));
+    hs.fetch(nf > 1 ? C : 0, ldh(nf - 2));
+  }
+  __syncthreads();
+  const int jg = tid & (G - 1);
+  for (int t = a.T - 1; t >= 0; --t) {
+    const int it = a.T - 1 - t;  // the order the frames run in (the slots rotate with it)
+    const long long fo = ((long long)b * a.T + t) * FR;
+    if (t >= nf || !live) {
+      for (long long e = tid; e < FR; e += nthr) stw<false>(a.dW, fo + e, 0.f);
+      continue;
+    }
+    if (kOff && t + 1 < nf) {  // frame t + 1's shift, once
+      sp = slots.shift(it - 1);
+      Ob += sp;
+    }
+    const unsigned char* wf = a.W + fo * esz;
+    const float* wl = w0 + (t & 1) * FR;
+    const float* la = la0 + (t & 1) * C;
+    auto wr = [&](int i) { return STAGE ? wl[i] : ldw<BF16>(wf, i); };
+    // G lanes per source state p: lane jg takes the labels y = jg+1, jg+1+G, ...
+    for (int p0 = 0; p0 < C; p0 += nthr / G) {
+      const int p = p0 + tid / G;
+      const bool valid = p < C;
+      const float bb = valid ? t_times<SR>(wr(p * R), cur[p] - sp) : 0.f;
+      OutSum<SR, G> s;
+      if (valid) {
+        const float a0 = af(la[p]);
+#pragma unroll 4
+        for (int y = 1 + jg; y <= V; y += G) {
+          const float bq = cur[g_tab[p * V + y - 1]] - sp;
+          const float lb = t_times<SR>(wr(p * R + y), bq);
+          stw<false>(a.dW, fo + p * R + y, mg(a0, SR == M_LOG ? lb : bq));
+          s.add(lb);
+        }
+      }
+      const float sv = s.merge();
+      if (!valid || jg) continue;
+      stw<false>(a.dW, fo + p * R, mg(af(la[p]), SR == M_LOG ? bb : cur[p] - sp));
+      nxt[p] = t_plus<SR>(bb, sv);
+      if (kOff) slots.put(it, nxt[p]);
+    }
+    if (t >= 1) {  // frame t - 1's weights and alpha row into the other buffers
+      if (STAGE) {
+        fs.store(w0 + ((t - 1) & 1) * FR, wf - FR * esz, FR);
+        fs.fetch(t >= 2 ? wf - 2 * FR * esz : nullptr, FR);
+      }
+      hs.store(la0 + ((t - 1) & 1) * C, C, ldh(t - 1));
+      hs.fetch(t >= 2 ? C : 0, ldh(t - 2));
+    }
+    if (kOff) slots.reset_next(it);
+    __syncthreads();
+    float* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+  }
+}
+
 template <bool BF16, bool STAGE, int SR>
 LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
+  if (a.K == 0) {
+    tab_bwd_den_k0_body<BF16, STAGE, SR>(a, b, sm);
+    return;
+  }
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int C = a.C, V = a.V, R = a.R, K = a.K;
   int* gsm = (int*)sm;
@@ -1013,8 +1292,140 @@ __global__ void tab_onehot_kernel(const TArgs a) {
 // The same recursion on the string acceptor; string arcs that share a lattice
 // arc are summed by their chain head in ascending order (one writer per
 // element and frame: deterministic).
+// ---- string backward, FrameDependent (K = 0): ONE barrier a frame ----------
+// Frame t's pass (marginals of its string arcs into mb / ml of parity t, the
+// new beta into the other (i, f) buffer) runs beside frame t + 1's chain-head
+// sums (mb / ml of the other parity) and the staging of frame t - 1's alpha
+// row and weights; dh is read and rewritten by the same thread (its heads'
+// index set), so it needs no second buffer.
+template <bool BF16>
+LT_DEVINL void tab_bwd_num_k0_body(const TArgs& a, const int b, float* sm) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int U = a.U, S = U + 1, NK = 2 * S;
+  float* b0i = sm;  // [2] x (i [S], f [S]): beta_{t+1} and the new beta
+  float* mb0 = b0i + 4 * S;  // [2] x (mb [S], ml [S])
+  float* la0 = mb0 + 4 * S;  // [2][S] alpha history rows
+  int* ctx = (int*)(la0 + 2 * S);
+  int* yn = ctx + S;
+  int* link = yn + S;               // [NK]
+  float* wc0 = (float*)(link + NK);  // [2][2S]
+  float* dh = wc0 + 4 * S;           // [NK]
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const float nm = a.num_in[b];
+  const float lz = a.local ? 0.f : a.den_in[b];
+  const bool live = __builtin_isfinite(nm) && (a.local || __builtin_isfinite(lz));
+  if (!live) {  // the denominator kernel wrote zeros
+    if (a.ntab)
+      for (int k = tid; k < NK; k += nthr) a.ntab[(long long)b * NK + k] = -1;
+    return;
+  }
+  const int nl = a.nlab[b];
+  if (tid == 0) t_walk(a, b, ctx, yn);
+  for (int u = tid; u < S; u += nthr) {
+    b0i[u] = u == nl ? 0.f : -kInf;
+    b0i[S + u] = 0.f;
+  }
+  __syncthreads();
+  auto elem = [&](int k) {  // W element of string entry k = 2u + kind, or -1
+    const int u = k >> 1;
+    return (k & 1) == 0 ? ctx[u] : (u < U ? ctx[u] + yn[u] : -1);
+  };
+  for (int k = tid; k < NK; k += nthr) {
+    const int o = elem(k);
+    int head = o >= 0 ? 1 : 0, nxt = -1;
+    if (o >= 0)
+      for (int k2 = 0; k2 < NK; ++k2) {
+        if (elem(k2) != o) continue;
+        if (k2 < k) head = 0;
+        else if (k2 > k && nxt < 0) nxt = k2;
+      }
+    link[k] = (head << 30) | (nxt + 1);
+    if (a.ntab) a.ntab[(long long)b * NK + k] = head ? o : -1;
+  }
+  __syncthreads();
+  const long long FR = (long long)a.C * a.R;
+  auto ldh = [&](int t) {
+    return [=](int e) { return a.hist[((long long)b * a.T + t) * S + e]; };
+  };
+  auto ldc = [&](int t) {
+    const unsigned char* w = a.W + ((long long)b * a.T + t) * FR * (BF16 ? 2 : 4);
+    return [=](int e) { return ldw<BF16>(w, ctx[e >> 1] + ((e & 1) ? yn[e >> 1] : 0)); };
+  };
+  auto ldd = [&](int t) {
+    const long long fo = ((long long)b * a.T + t) * FR;
+    return [=](int k) {
+      return (!a.nsub && (link[k] >> 30)) ? ldw<false>((const unsigned char*)a.dW, fo + elem(k))
+                                          : 0.f;
+    };
+  };
+  auto marg = [&](float alv, float i, float f) { return lt_exp(((alv - nm) + i) + f); };
+  // the chain heads of frame t (its mb / ml parity, dh): nsub or dW
+  auto heads = [&](int t) {
+    const float* mb = mb0 + (t & 1) * 2 * S;
+    const float* ml = mb + S;
+    const long long fo = ((long long)b * a.T + t) * FR;
+    for (int k = tid; k < NK; k += nthr) {
+      const int lk = link[k];
+      if (!(lk >> 30)) continue;
+      float s = 0.f;
+      for (int kk = k; kk >= 0; kk = (link[kk] & 0x3fffffff) - 1)
+        s += (kk & 1) ? ml[kk >> 1] : mb[kk >> 1];
+      if (a.nsub) a.nsub[((long long)b * a.T + t) * NK + k] = s;
+      else stw<false>(a.dW, fo + elem(k), dh[k] - s);
+    }
+  };
+  RegStage<1> hs;
+  RegStage<2> cs, ds;
+  if (nf > 0) {
+    hs.fetch(S, ldh(nf - 1));
+    cs.fetch(2 * S, ldc(nf - 1));
+    hs.store(la0 + ((nf - 1) & 1) * S, S, ldh(nf - 1));
+    cs.store(wc0 + ((nf - 1) & 1) * 2 * S, 2 * S, ldc(nf - 1));
+    hs.fetch(nf > 1 ? S : 0, ldh(nf - 2));
+    cs.fetch(nf > 1 ? 2 * S : 0, ldc(nf - 2));
+    ds.fetch(NK, ldd(nf - 1));
+  }
+  __syncthreads();
+  float *bi = b0i, *bf = b0i + S, *ci = b0i + 2 * S, *cf = b0i + 3 * S;
+  for (int t = nf - 1; t >= 0; --t) {
+    const float* la = la0 + (t & 1) * S;
+    const float* wc = wc0 + (t & 1) * 2 * S;
+    float* mb = mb0 + (t & 1) * 2 * S;
+    float* ml = mb + S;
+    for (int u = tid; u < S; u += nthr) {
+      const float bbf = wc[2 * u] + bf[u];  // blank + beta: (bi[u], bbf)
+      const bool lex = u < U;
+      const float li = lex ? bi[u + 1] : -kInf, lf = lex ? wc[2 * u + 1] + bf[u + 1] : 0.f;
+      mb[u] = marg(la[u], bi[u], bbf);
+      ml[u] = lex ? marg(la[u], li, lf) : 0.f;
+      lae_split(bi[u], bbf, li, lf, ci[u], cf[u]);
+    }
+    if (t + 1 < nf) heads(t + 1);  // (its dh in place: read before this thread's restage)
+    ds.store(dh, NK, ldd(t));
+    ds.fetch(t >= 1 ? NK : 0, ldd(t - 1));
+    if (t >= 1) {
+      hs.store(la0 + ((t - 1) & 1) * S, S, ldh(t - 1));
+      cs.store(wc0 + ((t - 1) & 1) * 2 * S, 2 * S, ldc(t - 1));
+      hs.fetch(t >= 2 ? S : 0, ldh(t - 2));
+      cs.fetch(t >= 2 ? 2 * S : 0, ldc(t - 2));
+    }
+    __syncthreads();
+    float* ti = bi; bi = ci; ci = ti;
+    float* tf = bf; bf = cf; cf = tf;
+  }
+  if (nf > 0) {
+    heads(0);
+    __syncthreads();
+  }
+}
+
 template <bool BF16>
 LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
+  if (a.K == 0) {
+    tab_bwd_num_k0_body<BF16>(a, b, sm);
+    return;
+  }
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int U = a.U, S = U + 1, K = a.K, NK = 2 * S;
   // beta and the backward chain in the (i, f) representation of
@@ -1303,7 +1714,8 @@ int launch_t_fwd(int sr, bool num, bool vit, const TArgs& a0, hipStream_t st) {
   const int lds = fwd_lds(S) + (num ? 16 * S : 0);
   // STAGE: graph and frame in LDS (when both fit; the string forward reads
   // two weights per position and stages nothing)
-  const long long staged = (long long)lds + graph_lds(a) + 4 * FR;
+  // (K = 0: tab_fwd_k0_body stages two frames)
+  const long long staged = (long long)lds + graph_lds(a) + (a.K == 0 ? 8 : 4) * FR;
   if (!num && staged <= kStageBudget)
     return launch_t_fwd_s<BF16, true>(sr, num, vit, a, (int)staged, st);
   return launch_t_fwd_s<BF16, false>(sr, num, vit, a, lds, st);
@@ -1422,7 +1834,7 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   if (!local_norm) {
     const int ln = fwd_lds(S) + 16 * S;
     const int ld = fwd_lds(C);
-    const long long staged = (long long)ld + graph_lds(a) + 4 * FR;
+    const long long staged = (long long)ld + graph_lds(a) + (a.K == 0 ? 8 : 4) * FR;
     if (staged <= kStageBudget) {
       const int l2 = std::max((int)staged, ln);
       rc = bf16 ? t_launch2(tab_fwd2_kernel<true, true>, 2 * a.B, l2, st, ad, an)
@@ -1458,11 +1870,15 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   ad.ntab = nullptr;
   an.hist = hn;
   const int lds_d = 4 * (3 * C + (K + 1) * C);
-  const int lds_n = 4 * (8 * S + (K + 1) * S) + 4 * (2 * S + 2 * S) + 4 * (2 * S + 2 * S);
-  if (lds_d + graph_lds(a) + 4 * FR <= kStageBudget) {
+  // (K = 0: the one-barrier string backward double-buffers its rows, 80 S)
+  const int lds_n = 4 * (8 * S + (K + 1) * S) + 4 * (2 * S + 2 * S) + 4 * (2 * S + 2 * S) +
+                    (K == 0 ? 12 * S : 0);
+  // K = 0: the one-barrier den backward stages two frames
+  if (lds_d + graph_lds(a) + (K == 0 ? 8 : 4) * FR <= kStageBudget) {
     // + the lexical dW sums of FrameLabelDependent(K > 0) when they fit too
     ad.acc = K > 0 && lds_d + graph_lds(a) + 8 * FR <= kStageBudget;
-    const int l2 = std::max((int)(lds_d + graph_lds(a) + (ad.acc ? 8 : 4) * FR), lds_n);
+    const int l2 =
+        std::max((int)(lds_d + graph_lds(a) + ((ad.acc || K == 0) ? 8 : 4) * FR), lds_n);
     rc = bf16 ? t_launch2(tab_bwd2_kernel<true, true>, 2 * a.B, l2, st, ad, an)
               : t_launch2(tab_bwd2_kernel<false, true>, 2 * a.B, l2, st, ad, an);
   } else {
@@ -1563,9 +1979,9 @@ int lt_table_den_backward(const lt_graph* g, const lt_table_problem* pb, int32_t
     a.den_in = dist;
     a.num_in = dist;  // the den-only backward: live while the distance is finite
     const int lds_d = 4 * (3 * C + (K + 1) * C);
-    if (lds_d + graph_lds(a) + 4 * FR <= kStageBudget) {
+    if (lds_d + graph_lds(a) + (K == 0 ? 8 : 4) * FR <= kStageBudget) {
       a.acc = K > 0 && lds_d + graph_lds(a) + 8 * FR <= kStageBudget;
-      const int lds = (int)(lds_d + graph_lds(a) + (a.acc ? 8 : 4) * FR);
+      const int lds = (int)(lds_d + graph_lds(a) + ((a.acc || K == 0) ? 8 : 4) * FR);
       if (semiring == M_LOG)
         rc = bf16 ? t_launch(tab_bwd_den_kernel<true, true, M_LOG>, a.B, lds, st, a)
                   : t_launch(tab_bwd_den_kernel<false, true, M_LOG>, a.B, lds, st, a);
