@@ -116,17 +116,30 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, chec
   if dist_on:
     torch.distributed.barrier()
   torch.cuda.synchronize()
+  # one C-ABI call per step with no collective (N = 1): two HIP events around
+  # the whole timed loop give the call's average (event records between the
+  # calls cost the stream a few microseconds each); otherwise a pair per step
+  # separates the call from the step's collective
+  whole = events and fused and not dist_on
   evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)] \
-      if events else [None] * steps
+      if events and not whole else [None] * steps
+  ew = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if whole else None
   t0 = time.perf_counter()
+  if whole:
+    ew[0].record()
   for i in range(steps):
     step(evs[i])
+  if whole:
+    ew[1].record()
   torch.cuda.synchronize()
   if dist_on:
     torch.distributed.barrier()
   torch.cuda.synchronize()
   wall = time.perf_counter() - t0
-  fwd_ms = [e[0].elapsed_time(e[1]) for e in evs] if events else []
+  if whole:
+    fwd_ms = [ew[0].elapsed_time(ew[1]) / steps] * steps
+  else:
+    fwd_ms = [e[0].elapsed_time(e[1]) for e in evs] if events else []
   bwd_ms = [e[1].elapsed_time(e[2]) for e in evs] if (events and not fused) else []
   return wall, fwd_ms, bwd_ms, bucket.calls
 
