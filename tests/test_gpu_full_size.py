@@ -223,6 +223,26 @@ def test_cfg4_viterbi_t2000_every_utterance(cuda):
     np.testing.assert_array_equal(weights.cpu().numpy(), rw)
 
 
+@pytest.mark.parametrize('T', [2400, 4500])
+def test_viterbi_long_utterances_backtrace_routes(cuda, T):
+  """Viterbi past the length whose backpointers fit the forward's LDS (T <=
+  2,300 at V = 32: the backtrace in the same launch): T = 2400 runs the
+  separate segmented backtrace launch, T = 4500 (beyond its 144 KB) the
+  generic one. Labels, path weights and the one-hot arcs (the gradient of
+  the distance) bit-exact against the oracle, varied lengths, both
+  conventions."""
+  V, n, B = 32, 1, 4
+  W, nf, _, _ = _bench_inputs(B, T, 10, V, n, cuda, seed=T)
+  nf = torch.tensor([T, T - 1, T // 2, 1], dtype=torch.int32, device=cuda)
+  Wc, nfc = _np(W, nf)
+  for conv in (nat.LABELS_REFERENCE, nat.LABELS_TRUE):
+    labels, weights, arcs = nat.viterbi(W, nf, V, n, conv, want_arcs=True)
+    rlab, rw, rarcs = _orc().viterbi(Wc, nfc, V, n, convention=conv, want_arcs=True)
+    np.testing.assert_array_equal(labels.cpu().numpy(), rlab)
+    np.testing.assert_array_equal(weights.cpu().numpy(), rw)
+    np.testing.assert_array_equal(arcs.cpu().numpy(), rarcs)
+
+
 def test_cfg5_trigram_bf16(cuda):
   """cfg5: trigram (|ctx| = 1057) bf16 arc weights at B=32, T=1000, U=100:
   losses of a sample and every dW element of four utterances against the
