@@ -146,10 +146,11 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
  * -- what RecognitionLattice.forward followed by loss.sum().backward() means
  * to produce (lattices.py:131-183 with the backward of alignments.py:300-318;
  * D1/D3 in the reference). Utterances with num = -inf get dW = 0.
- * For the bigram (FullNGram n = 1, V <= 32, U <= 127) this is the chunked
- * two-level scan below (two launches after a flag memset, plus the
- * frame-serial pair whose workgroups exit at once unless an utterance is out
- * of its range or a hand-off wait timed out). Other
+ * For the bigram (FullNGram n = 1, V <= 32, U <= 127) while 16 B <= 11 CUs
+ * this is the chunked two-level scan below (two launches, plus one
+ * frame-serial launch whose workgroups exit at once unless an utterance is
+ * out of its range or a hand-off wait timed out; no memset: the hand-off
+ * words carry a per-call tag, so the workspace's contents do not matter). Other
  * bigram shapes with 2B below the CU count run ONE fused launch (alpha and
  * beta recursions plus workgroups that turn every frame into marginals as
  * soon as both recursions have passed it; should a hand-off wait time out,
@@ -186,7 +187,8 @@ int lt_scale_grad(const lt_problem* pb, const float* grad, void* dW,
  * the same calls (same results, slower). Sizes from
  * lt_chunk_workspace_bytes(); both buffers 16-byte aligned.
  * Phase A (chunk transfers) and phase B (the boundary walks) share one
- * launch while B <= CUs: per-chunk ready flags, write-through stores,
+ * launch while B <= CUs: per-chunk ready flags tagged per call (62-bit;
+ * whatever `scratch` held reads as "not published"), write-through stores,
  * agent-scope acquire on the walks' side; a walk that never sees its chunk
  * times out and sends its utterance to the frame-serial kernels.
  * lt_loss_grad runs the same launches for every shape they take. */
@@ -211,7 +213,10 @@ int lt_chunk_backward(const lt_problem* pb, int32_t local_norm, const void* W,
  *   arcs   [B,T,C,V+1] (nullable, W's dtype): if given, receives grad[b] on
  *          every arc of the best path and 0 elsewhere -- the vjp of
  *          _forward(MaxTropical) (grad nullable = ones).
- *   workspace: lt_viterbi_workspace_bytes() bytes of device memory. */
+ *   workspace: lt_viterbi_workspace_bytes() bytes of device memory.
+ * The bigram (V <= 32) decodes and backtracks in one launch while an
+ * utterance's backpointers fit the forward's LDS (T <= 2,300 at V = 32),
+ * else the backtrace is a second launch. */
 int lt_viterbi_workspace_bytes(const lt_problem* pb, size_t* bytes);
 int lt_viterbi(const lt_problem* pb, const void* W, const int32_t* num_frames,
                int32_t label_convention, int64_t* labels, float* path_weight,

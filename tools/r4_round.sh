@@ -38,3 +38,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/kt5 -o run -- python 
   python3 $R/tools/chunk_prof.py > $R/$out/pmc_write.log 2>&1) || exit $?
 HS=32,64,128,512 timeout -k 10 300 python -u tools/joint_step_bench.py > $out/joint_step.jsonl 2> $out/joint_step.err || exit $?
 echo done > $out/done.txt
+timeout -k 10 300 python3 -u tools/table_bench.py > $out/table_bench.jsonl 2> $out/table_bench.err || exit $?
+echo done2 >> $out/done.txt
