@@ -18,14 +18,15 @@ nf = torch.full([B], T, dtype=torch.int32, device='cuda')
 lab = torch.randint(1, V + 1, (B, U), generator=g, device='cuda', dtype=torch.int32)
 nl = torch.full([B], U, dtype=torch.int32, device='cuda')
 ws = torch.empty([nat.loss_grad_workspace_bytes(W, V, n, U, False)], dtype=torch.uint8, device='cuda')
-for _ in range(2):
+WARM, N = int(os.environ.get('WARM', 2)), int(os.environ.get('N', 5))
+for _ in range(WARM):
   out = nat.loss_grad(W, nf, lab, nl, V, n, False, workspace=ws)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
 e0.record()
-for _ in range(5):
+for _ in range(N):
   out = nat.loss_grad(W, nf, lab, nl, V, n, False, workspace=ws)
 e1.record()
 torch.cuda.synchronize()
-print(f"lib={os.environ.get('LT_LIB_PATH', 'prod')} mid={os.environ.get('LT_TRI_MID', 'default')}: {e0.elapsed_time(e1) / 5:.2f} ms, "
+print(f"lib={os.environ.get('LT_LIB_PATH', 'prod')} mid={os.environ.get('LT_TRI_MID', 'default')}: {e0.elapsed_time(e1) / N:.2f} ms, "
       f"loss[0]={out[0][0].item():.4f}", flush=True)

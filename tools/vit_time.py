@@ -14,13 +14,15 @@ g = torch.Generator(device='cuda')
 g.manual_seed(0)
 W = torch.randn([B, T, V + 1, V + 1], generator=g, device='cuda')
 nf = torch.full([B], T, dtype=torch.int32, device='cuda')
-for _ in range(2):
+WARM, N = int(os.environ.get('WARM', 2)), int(os.environ.get('N', 10))
+for _ in range(WARM):
   nat.viterbi(W, nf, V, 1, nat.LABELS_REFERENCE)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
 e0.record()
-for _ in range(10):
+for _ in range(N):
   nat.viterbi(W, nf, V, 1, nat.LABELS_REFERENCE)
 e1.record()
 torch.cuda.synchronize()
-print(f"{os.environ.get('TAG', '')} lt_viterbi B={B} T={T}: {e0.elapsed_time(e1) / 10:.3f} ms", flush=True)
+print(f"{os.environ.get('TAG', '')} lt_viterbi B={B} T={T}: {e0.elapsed_time(e1) / N:.3f} ms "
+      f"({WARM} warmup, {N} timed calls)", flush=True)
