@@ -139,7 +139,7 @@ def _gloo_worker(rank, world, port, payload, out_q):
     if rank == 1:
       skipped.grad = torch.ones(2)
     sharding.all_reduce_step(loss, [skipped], skip_unused=True)
-    skip_ok = (skipped.grad is None) if rank == 0 else bool((skipped.grad == 1).all())
+    skip_ok = (skipped.grad is None) if rank != 1 else bool((skipped.grad == 1).all())
     out_q.put((rank, idx, loss.detach().numpy(), table.grad.numpy().copy(), totals, head_grads,
                p.grad.numpy().copy(), partial.grad.numpy().copy(), skip_ok, total3,
                bucket.calls))
@@ -147,11 +147,12 @@ def _gloo_worker(rank, world, port, payload, out_q):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_sharded_loss_matches_full_batch():
-  """world_size-2 gloo: each rank's shard through the product's CPU path;
-  per-shard losses and dW reassemble to the oracle's full batch, and the one
-  all-reduce per step gives the global loss sum and the summed head
-  gradient on both ranks, on two consecutive steps (zero_grad between)."""
+@pytest.mark.parametrize('world', [2, 4])
+def test_gloo_world2_sharded_loss_matches_full_batch(world):
+  """world_size-2 (and 4) gloo: each rank's shard through the product's CPU
+  path; per-shard losses and dW reassemble to the oracle's full batch, and the
+  one all-reduce per step gives the global loss sum and the summed head
+  gradient on every rank, on two consecutive steps (zero_grad between)."""
   from oracle import oracle as orc  # the checker
   rng = np.random.default_rng(3)
   B, T, U, V, n = 6, 9, 3, 3, 1
@@ -164,9 +165,9 @@ def test_gloo_world2_sharded_loss_matches_full_batch():
 
   ctx = mp.get_context('spawn')
   q = ctx.Queue()
-  port = 29500 + (os.getpid() % 2000)
-  procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, (W, nf, lab, nl, V, n), q))
-           for r in range(2)]
+  port = 29500 + (os.getpid() % 2000) + 2100 * (world // 4)
+  procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, (W, nf, lab, nl, V, n), q))
+           for r in range(world)]
   for p in procs:
     p.start()
   res = [q.get(timeout=120) for _ in procs]
@@ -183,7 +184,7 @@ def test_gloo_world2_sharded_loss_matches_full_batch():
     # the head's gradient is the sum of every utterance's dW, on both steps
     for hg in head_grads:
       np.testing.assert_allclose(hg, full_dW.sum(axis=(0, 1)), atol=1e-5)
-    np.testing.assert_array_equal(pgrad, np.full(5, 3.0))  # 1 + 2
+    np.testing.assert_array_equal(pgrad, np.full(5, world * (world + 1) / 2))  # 1 + ... + world
     np.testing.assert_array_equal(partial_grad, [1.0, 2.0, 3.0])  # same on both ranks
     assert skip_ok
     assert calls == 2  # one all-reduce per step
