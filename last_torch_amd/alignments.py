@@ -79,6 +79,45 @@ def check_num_weights(alignment: TimeSyncAlignmentLattice, blank: Sequence[torch
                      f'but got length {len(lexical)}')
 
 
+def _reach(alpha, lexical, step):
+  """[alpha, L alpha, L^2 alpha, ...]: the context vectors of the frame-local
+  states reached after 0, 1, ... lexical arcs, one per weight array in
+  ``lexical`` (``step(v, w)`` takes one arc)."""
+  reached = [alpha]
+  for w in lexical:
+    reached.append(step(reached[-1], w))
+  return reached
+
+
+def _context_step(context, semiring):
+  return lambda v, w: context.forward_reduce(semiring.times(v[..., None], w), semiring)
+
+
+def _string_step(semiring):
+  return lambda v, w: shift_down(semiring.times(v, w), semiring)
+
+
+def _completions(blank, lex_to, beta):
+  """Log-space completion weights of one frame, last alignment state first.
+
+  ``done[i]`` is the total weight from alignment state i to the end of the
+  lattice through this frame's blank (which closes the frame onto beta) or a
+  lexical arc to ``lex_to(i)``; returns ``done`` and the per-arc lexical
+  totals ``lex[i] = lexical_i + beta_of(lex_to(i))`` the marginals share.
+  """
+  k = len(blank)
+  done, lex = [None] * k, [None] * k
+  for i in range(k - 1, -1, -1):
+    closed = blank[i] + beta
+    target = lex_to(i, done)
+    if target is None:
+      done[i] = closed
+      continue
+    lex[i] = target
+    done[i] = semirings.Log.plus(closed, semirings.Log.sum(target, dim=-1))
+  return done, lex
+
+
 class FrameDependent(TimeSyncAlignmentLattice):
   """Each frame emits exactly one blank or one lexical label
   (alignments.py:266-329)."""
@@ -99,25 +138,25 @@ class FrameDependent(TimeSyncAlignmentLattice):
     return [0]
 
   def forward(self, alpha, blank, lexical, context, semiring):
+    """alignments.py:286-298: alpha (x) blank (+) the label arcs' reduce."""
     check_num_weights(self, blank, lexical)
-    stay = semiring.times(alpha, blank[0])
-    move = context.forward_reduce(semiring.times(alpha[..., None], lexical[0]), semiring)
-    return semiring.plus(stay, move)
+    emitted = _context_step(context, semiring)(alpha, lexical[0])
+    return semiring.plus(semiring.times(alpha, blank[0]), emitted)
 
   def backward(self, alpha, blank, lexical, beta, log_z, context):
+    """alignments.py:300-318: both arcs leave the frame, so the lexical arcs
+    land on beta_{t+1} itself."""
     check_num_weights(self, blank, lexical)
-    blank_beta = blank[0] + beta
-    lexical_beta = lexical[0] + context.backward_broadcast(beta)
-    scale = alpha - log_z[..., None]
-    blank_marginal = torch.exp(blank_beta + scale)
-    lexical_marginal = torch.exp(lexical_beta + scale[..., None])
-    next_beta = semirings.Log.plus(blank_beta, semirings.Log.sum(lexical_beta, dim=-1))
-    return next_beta, [blank_marginal], [lexical_marginal]
+    done, lex = _completions(blank, lambda i, _: lexical[0] + context.backward_broadcast(beta),
+                             beta)
+    rel = alpha - log_z[..., None]
+    return done[0], [torch.exp(rel + blank[0] + beta)], [torch.exp(rel[..., None] + lex[0])]
 
   def string_forward(self, alpha, blank, lexical, semiring):
+    """alignments.py:320-329 on the string acceptor (shift_down)."""
     check_num_weights(self, blank, lexical)
     return semiring.plus(semiring.times(alpha, blank[0]),
-                         shift_down(semiring.times(alpha, lexical[0]), semiring))
+                         _string_step(semiring)(alpha, lexical[0]))
 
 
 class FrameLabelDependent(TimeSyncAlignmentLattice):
@@ -145,45 +184,33 @@ class FrameLabelDependent(TimeSyncAlignmentLattice):
   def topological_visit(self) -> list[int]:
     return list(range(self.max_expansions + 1))
 
+  def _closed(self, reached, blank, semiring):
+    return semiring.sum(torch.stack([semiring.times(v, w) for v, w in zip(reached, blank)]), dim=0)
+
   def forward(self, alpha, blank, lexical, context, semiring):
-    """alignments.py:363-377: sum_i (L^i alpha) (x) blank[i]."""
+    """alignments.py:363-377: (+)_i (L^i alpha) (x) blank[i]."""
     check_num_weights(self, blank, lexical)
-    terminated = [semiring.times(alpha, blank[0])]
-    last = alpha
-    for i in range(self.max_expansions):
-      last = context.forward_reduce(semiring.times(last[..., None], lexical[i]), semiring)
-      terminated.append(semiring.times(last, blank[i + 1]))
-    return semiring.sum(torch.stack(terminated), dim=0)
+    reached = _reach(alpha, lexical[:self.max_expansions], _context_step(context, semiring))
+    return self._closed(reached, blank, semiring)
 
   def backward(self, alpha, blank, lexical, beta, log_z, context):
     """alignments.py:379-419: (beta_t, blank marginals [K+1], lexical
-    marginals [K+1], the last all zero) of one frame, Log semiring."""
+    marginals [K+1], the last all zero) of one frame, Log semiring. State i's
+    lexical arcs lead to state i + 1 of the same frame; state K has none."""
     check_num_weights(self, blank, lexical)
     K = self.max_expansions
-    la = [alpha]
-    last = alpha
-    for i in range(K):
-      last = context.forward_reduce(last[..., None] + lexical[i], semirings.Log)
-      la.append(last)
-    scale = beta - log_z[..., None]
-    blank_marginals = [torch.exp(la[i] + blank[i] + scale) for i in range(K + 1)]
-    next_beta = blank[K] + beta
-    lexical_marginals = []
-    for i in range(K):
-      j = K - 1 - i
-      lexical_beta = lexical[j] + context.backward_broadcast(next_beta)
-      lexical_marginals.append(torch.exp(lexical_beta + (la[j] - log_z[..., None])[..., None]))
-      next_beta = semirings.Log.plus(blank[j] + beta, semirings.Log.sum(lexical_beta, dim=-1))
-    lexical_marginals.reverse()
-    lexical_marginals.append(torch.zeros_like(lexical[K]))
-    return next_beta, blank_marginals, lexical_marginals
+    reached = _reach(alpha, lexical[:K], _context_step(context, semirings.Log))
+    done, lex = _completions(
+        blank,
+        lambda i, d: None if i == K else lexical[i] + context.backward_broadcast(d[i + 1]),
+        beta)
+    rel = [v - log_z[..., None] for v in reached]
+    blank_m = [torch.exp(r + w + beta) for r, w in zip(rel, blank)]
+    lex_m = [torch.exp(rel[i][..., None] + lex[i]) for i in range(K)]
+    return done[0], blank_m, lex_m + [torch.zeros_like(lexical[K])]
 
   def string_forward(self, alpha, blank, lexical, semiring):
     """alignments.py:421-432 on the string acceptor (shift_down)."""
     check_num_weights(self, blank, lexical)
-    terminated = [semiring.times(alpha, blank[0])]
-    last = alpha
-    for i in range(self.max_expansions):
-      last = shift_down(semiring.times(last, lexical[i]), semiring)
-      terminated.append(semiring.times(last, blank[i + 1]))
-    return semiring.sum(torch.stack(terminated), dim=0)
+    reached = _reach(alpha, lexical[:self.max_expansions], _string_step(semiring))
+    return self._closed(reached, blank, semiring)

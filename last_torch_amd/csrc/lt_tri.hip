@@ -12,8 +12,12 @@ namespace {
 // VT = 32: V a compile-time constant; VT = 1: any V <= 32
 template <bool BF16, int VT>
 __global__ __launch_bounds__(1024) void tri_fwdbwd_kernel(const KArgs af, const KArgs ab, int nb) {
-  if ((int)blockIdx.x < nb) fwd_body<M_LOG, BF16, true, 2, 9, VT>(af, blockIdx.x);
-  else bwd_body<BF16, true, false, 2, 9, true, (int)sizeof(KArgs), VT>(ab, blockIdx.x - nb);
+  // diagnostic builds: LT_DBG 16 / 32 time one direction alone (results wrong)
+  if ((int)blockIdx.x < nb) {
+    if (!LT_ABL(af, 16)) fwd_body<M_LOG, BF16, true, 2, 9, VT>(af, blockIdx.x);
+  } else if (!LT_ABL(af, 32)) {
+    bwd_body<BF16, true, false, 2, 9, true, (int)sizeof(KArgs), VT>(ab, blockIdx.x - nb);
+  }
 }
 }  // namespace
 

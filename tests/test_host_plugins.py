@@ -113,6 +113,31 @@ def test_frame_dependent_closed_forms():
     fd.forward(alpha, [blank, blank], [lexical], ctx, lt.semirings.Real)
 
 
+@pytest.mark.parametrize('align', ['fd', 'fld1', 'fld3'])
+def test_alignment_backward_is_forward_vjp(align):
+  """One frame's backward (alignments.py:300-318, :379-419) against autograd
+  of its forward: with log_z the frame's total into beta, the marginals are
+  d log_z / d weights and beta_t satisfies log_z = (+) alpha + beta_t."""
+  torch.manual_seed(0)
+  al = (lt.alignments.FrameDependent() if align == 'fd' else
+        lt.alignments.FrameLabelDependent(max_expansions=int(align[3:])))
+  ctx = lt.contexts.FullNGram(vocab_size=3, context_size=2)
+  C, V, k = ctx.num_states(), 3, al.num_states()
+  Log = lt.semirings.Log
+  alpha, beta = torch.randn(2, C, dtype=torch.float64), torch.randn(2, C, dtype=torch.float64)
+  blank = [torch.randn(2, C, dtype=torch.float64, requires_grad=True) for _ in range(k)]
+  lexical = [torch.randn(2, C, V, dtype=torch.float64, requires_grad=True) for _ in range(k)]
+  log_z = Log.sum(al.forward(alpha, blank, lexical, ctx, Log) + beta, dim=-1)
+  grads = torch.autograd.grad(log_z.sum(), blank + lexical, allow_unused=True)
+  nb, bm, lm = al.backward(alpha, [b.detach() for b in blank], [w.detach() for w in lexical],
+                           beta, log_z.detach(), ctx)
+  np.testing.assert_allclose(Log.sum(alpha + nb, dim=-1).numpy(), log_z.detach().numpy(),
+                             rtol=1e-12)
+  for got, want, ref in zip(bm + lm, grads, blank + lexical):
+    want = torch.zeros_like(ref) if want is None else want
+    np.testing.assert_allclose(got.detach().numpy(), want.numpy(), rtol=1e-10, atol=1e-12)
+
+
 def test_lattice_validates_batch_dims():
   """RecognitionLattice.forward's shape checks (lattices.py:157-166) fire
   before any device work, with the reference's messages."""
