@@ -476,6 +476,7 @@ struct KArgs {
   int st_off[kMaxStreams];         // byte offset inside a slot
   int gw0, gw1;                    // instructions per frame of loader wave 0 / 1
   int off_ring, off_a, off_na, off_ctx, off_ylab, off_dbuf, off_nbuf, off_misc;
+  int off_tb;        // trigram V = 32 backward: the padded beta rows [2][kTriBPad]
 };
 
 // The kernel arguments re-read from the kernarg segment through a pointer
@@ -980,10 +981,12 @@ LT_DEVINL float den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, in
 // 2 x (V+2) of their terms in registers: no lane groups, no cross-lane sums,
 // one pass per frame. alpha[p_k] is one address per block (four blocks a
 // wave: four banks), the W reads are 16 consecutive labels per block.
-// The backward lane owns two source rows p and p + 576 and walks its V
-// labels from a lane-dependent start, so that 32 consecutive sources read 32
-// different banks both in W (rows 66 B apart) and in beta (next(p, y) =
-// nb(p) + y, one block of V per source, blocks V floats apart).
+// The backward lane owns two source rows p and p + 576. At V = 32
+// (den_bwd_tri32) the beta rows are padded to blocks 33 floats apart and the
+// labels walked in natural order from immediate offsets; at runtime V the
+// lane walks its labels from a lane-dependent start. Either way 32
+// consecutive sources read 32 different banks both in W (rows 66 B apart)
+// and in beta (next(p, y) = nb(p) + y, one block of V per source).
 // Log vectors stay relative to an integer offset: the max of the vector a
 // step writes goes through an LDS slot (ds_max on an order-preserving int
 // image, three slots in rotation) to the next step, which subtracts its
@@ -1464,9 +1467,110 @@ LT_DEVINL void den_bwd_loop(const KArgs& a, unsigned char* lds, float* bbuf, flo
 // = (+)_y W[p, y] + beta_{t+1}[next(p, y)] (alignments.py:315-316,
 // contexts.py:232-256) for the sources p = tid and tid + 576 of this lane;
 // beta_t is frame t-1's checkpoint row (the CK convention of den_bwd_loop).
+// V = 32: beta rows kept padded in LDS, each next-state block of 32 followed
+// by one unused float (block b at 33 b, state (b, y) at 33 b + y - 1), so
+// a lane reads its block and its W row in natural label order at immediate
+// offsets from two lane bases: consecutive sources (consecutive b) then sit
+// 33 floats apart, 32 different banks, with no per-term address arithmetic
+// (the skewed order above cost two integer ops a term and was the long pole
+// of the launch)
+constexpr int kTriBPad = 1088;  // padded row: 33 + 33 * 32 - 1 floats
+LT_DEVINL int tri_pad(int s) { return s < 33 ? s : s + ((s - 33) >> 5); }
+
+// a W row of 33 weights from LDS. The row's 2-byte alignment varies with p
+// (66 B rows): plain loads would be merged into unaligned 16-byte reads,
+// measured 0.7 ms slower per cfg5 call than one read per weight
+template <bool BF16>
+LT_DEVINL void tri_row(const unsigned char* wrow, int e, float* w) {
+  // volatile LDS (address space 3) loads: one ds_read per weight, unmerged
+  typedef const volatile __attribute__((address_space(3))) unsigned short lds_u16;
+  typedef const volatile __attribute__((address_space(3))) float lds_f32;
+#pragma unroll
+  for (int k = 0; k < 33; ++k) {
+    if constexpr (BF16)
+      w[k] = __uint_as_float((unsigned)((lds_u16*)wrow)[e + k] << 16);
+    else
+      w[k] = ((lds_f32*)wrow)[e + k];
+  }
+}
+
+template <bool BF16, bool WST>
+LT_DEVINL void den_bwd_tri32(const KArgs& a, unsigned char* lds, int b, int nf, int tid) {
+  static_assert(WST, "the V = 32 role reads W from the LDS ring");
+  constexpr int V = 32, R = 33, C = 1 + 32 + 32 * 32;
+  int* slot = (int*)(lds + a.off_misc) + 2;
+  float* pbuf = (float*)(lds + a.off_tb);  // [2][kTriBPad]
+  const int nthr = kTriDenWaves * 64;
+  const bool h0 = tid < C, h1 = tid + nthr < C;
+  const int p0 = h0 ? tid : 0, p1 = h1 ? tid + nthr : 0;
+  // next(p, y) = nb + y (nb = 32 b, or 0 for the start state): padded 33 b - 1 + y
+  bool z;
+  const int n0 = next_base(a.g, p0, &z), n1 = next_base(a.g, p1, &z);
+  const int nb0 = n0 ? n0 + (n0 >> 5) - 1 : 0, nb1 = n1 ? n1 + (n1 >> 5) - 1 : 0;
+  const int q0 = tri_pad(p0), q1 = tri_pad(p1);
+  // beta_T = 0 (before the loop's first barrier)
+  for (int e = tid; e < kTriBPad; e += nthr) pbuf[e] = 0.f;
+  if (tid == 0) {
+    slot[0] = tri_enc(0.f);  // max of beta_T = 0
+    slot[1] = tri_enc(-kInf);
+    slot[2] = tri_enc(-kInf);
+  }
+  const unsigned char* ring = lds + a.off_ring + a.st_off[0];
+  const long long t_last = (long long)b * a.T + (nf - 1);
+  Cursor cw = make_cursor(a.st_row[0] > 0 ? a.st_row[0] : (long long)a.FR * (BF16 ? 2 : 4),
+                          t_last, true);
+  float* brow = a.beta ? a.beta + (t_last - 1) * C : nullptr;
+  float Ob = 0.f;
+  for (int i = 0; i < nf; ++i) {
+    lds_barrier();
+    const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
+    const float* bcur = pbuf + (i & 1) * kTriBPad;
+    float* bnxt = pbuf + ((i + 1) & 1) * kTriBPad;
+    const int s3 = i % 3;
+    const float mprev = tri_dec(slot[s3]);
+    const float sp = __builtin_isfinite(mprev) ? floorf(mprev) : 0.f;
+    if (tid == 0) slot[s3 == 0 ? 2 : s3 - 1] = tri_enc(-kInf);
+    float* crow = (brow && i < nf - 1) ? brow : nullptr;
+    float lmax = -kInf;
+#pragma unroll 1
+    for (int d = 0; d < 2; ++d) {
+      if (!(d ? h1 : h0)) break;
+      const int p = d ? p1 : p0;
+      const float* bn = bcur + (d ? nb1 : nb0);
+      float w[R];
+      tri_row<BF16>(wrow, p * R, w);
+      float x[V];
+      const float tp = w[0] + bcur[d ? q1 : q0];  // blank self loop
+      float m = tp;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        x[k] = w[k + 1] + bn[k + 1];
+        m = fmaxf(m, x[k]);
+      }
+      const float c = __builtin_isfinite(m) ? m : 0.f;
+      const float l = c * kLog2e;
+      float s = lt_exp_off(tp, l);
+#pragma unroll
+      for (int k = 0; k < V; ++k) s += lt_exp_off(x[k], l);
+      const float r = (c + lt_log(s)) - sp;
+      bnxt[d ? q1 : q0] = r;
+      if (crow) crow[p] = (Ob + sp) + r;
+      lmax = fmaxf(lmax, r);
+    }
+    tri_publish_max(slot + (s3 == 2 ? 0 : s3 + 1), lmax);
+    Ob += sp;
+    advance(cw, a);
+    if (brow) brow -= C;
+  }
+}
+
 template <bool BF16, bool WST, int VT>
 LT_DEVINL void den_bwd_tri(const KArgs& a, unsigned char* lds, float* bbuf, int b, int nf,
                            int tid) {
+  if constexpr (VT == 32) {
+    den_bwd_tri32<BF16, WST>(a, lds, b, nf, tid);
+    return;
+  }
   const NGram& g = a.g;
   const int V = VT > 0 ? VT : g.V, R = V + 1;
   const int C = VT > 0 ? 1 + VT + VT * VT : g.C;
@@ -1476,7 +1580,7 @@ LT_DEVINL void den_bwd_tri(const KArgs& a, unsigned char* lds, float* bbuf, int 
   const int p0 = h0 ? tid : 0, p1 = h1 ? tid + nthr : 0;
   bool z;
   const int nb0 = next_base(g, p0, &z), nb1 = next_base(g, p1, &z);
-  const int ys = VT > 0 ? (tid & (VT - 1)) : (tid & 63) % V;  // the lane's first label - 1
+  const int ys = (tid & 63) % V;  // the lane's first label - 1
   if (tid == 0) {
     slot[0] = tri_enc(0.f);  // max of beta_T = 0
     slot[1] = tri_enc(-kInf);
@@ -1510,13 +1614,8 @@ LT_DEVINL void den_bwd_tri(const KArgs& a, unsigned char* lds, float* bbuf, int 
 #pragma unroll
       for (int k = 0; k < 32; ++k) {
         if (k < V) {
-          if constexpr (VT == 32) {
-            const int yk = ((ys + k) & 31) + 1;
-            x[k] = ldw<BF16>(wrow, p * R + yk) + bcur[nb + yk];
-          } else {
-            x[k] = ldw<BF16>(wrow, p * R + y) + bcur[nb + y];
-            y = y == V ? 1 : y + 1;
-          }
+          x[k] = ldw<BF16>(wrow, p * R + y) + bcur[nb + y];
+          y = y == V ? 1 : y + 1;
         } else {
           x[k] = -kInf;
         }

@@ -1019,7 +1019,11 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   // state pair, every term in registers) in the same side-by-side launch
   if (ck && !local_norm && g.n == 2 && g.V >= 2 && g.V <= 32 && pf.wst && pbk.wst &&
       pf.a.aux_waves == pbk.a.aux_waves && pf.a.slot_bytes == pbk.a.slot_bytes &&
-      env_int("LT_NO_TRI", 0) == 0) {
+      (g.V != 32 || pbk.lds_bytes + 8 * kTriBPad <= kLdsMax) && env_int("LT_NO_TRI", 0) == 0) {
+    if (g.V == 32) {  // den_bwd_tri32's padded beta rows, past the ring
+      pbk.a.off_tb = pbk.lds_bytes;
+      pbk.lds_bytes += 8 * kTriBPad;
+    }
     for (Plan* pl : {&pf, &pbk}) {
       // four loader waves: a frame is 69 LDS-DMA wave instructions (bf16),
       // whose issue cost alone is a microsecond on two waves
