@@ -248,6 +248,26 @@ def test_random_checkpointing_vs_oracle(cuda, B, T, U, V, n, dt):
     assert_grad_marginal_close(dW.float().cpu().numpy(), rdW, den, rlz, rnum, bf16)
 
 
+def test_trigram_v32_short_and_empty_utterances(cuda):
+  """The trigram den roles at V = 32 (lt_tri.hip; the backward's padded beta
+  rows, den_bwd_tri32) on utterances of 0, 1, 2, T-1 and T frames, bf16,
+  against the oracle: loss, and dW under the per-element marginal bound."""
+  orc = _orc()
+  B, T, U, V, n = 5, 24, 6, 32, 2
+  W, _, lab, _ = _random_problem(B, T, U, V, n, seed=4242)
+  nf = np.array([T, 0, 1, 2, T - 1], dtype=np.int32)
+  nl = np.array([U, 0, 1, 2, U - 1], dtype=np.int32)
+  W = torch.tensor(W).bfloat16().float().numpy()
+  Wd = torch.tensor(W).to(torch.bfloat16).to(cuda)
+  nfd, labd, nld = (torch.tensor(x).to(cuda) for x in (nf, lab, nl))
+  out = nat.loss_forward(Wd, nfd, labd, nld, V, n, False, checkpoints=True)
+  dW = nat.loss_backward(Wd, nfd, labd, nld, *out[1:5], None, V, n, False, ck=out[5])
+  rl, rlz, rnum, rdW = orc.loss_grad(W, nf, lab, nl, V, n)
+  assert_loss_close(out[0].cpu().numpy(), rl)
+  assert_grad_marginal_close(dW.float().cpu().numpy(), rdW, orc.den_grad(W, nf, V, n)[1], rlz,
+                             rnum, True)
+
+
 @pytest.mark.parametrize('B,T,U,V,n,dt', RANDOM)
 def test_random_vs_oracle(cuda, B, T, U, V, n, dt):
   orc = _orc()
