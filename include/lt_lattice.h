@@ -288,8 +288,10 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
  *   LT_SEMIRING_MAX   dW = grad_b on every arc of the best path (the first
  *                     maximum, as lt_table_viterbi), 0 elsewhere; dist and
  *                     alpha are not read (may be NULL)
- * grad [B] nullable (1). Padding frames and utterances of non-finite distance
- * get dW = 0. workspace: lt_table_den_backward_workspace_bytes() (0 bytes for
+ * grad [B] nullable (1). Padding frames get dW = 0; in Log / Real so do
+ * utterances of non-finite distance, while MaxTropical marks the first
+ * maximum's path whatever its weight (an all -inf utterance: the tie rules'
+ * path, as the reference's argmax backward). workspace: lt_table_den_backward_workspace_bytes() (0 bytes for
  * fp32 W in Log / Real). */
 int lt_table_den_backward_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
                                           int32_t semiring, size_t* bytes);

@@ -2047,6 +2047,15 @@ void ck_tags(CkArgs& a) {
 // LT_CHUNK_WALK_AT overrides, in percent).
 int ck_launch_ab(CkArgs& a, bool bf16, hipStream_t st) {
   ck_tags(a);
+  // Under stream capture the tag above is baked into the graph, so every
+  // replay would carry the same one and see the previous replay's words as
+  // published: zero them by a memset node instead (any nonzero tag is then
+  // fresh). Eager calls keep the per-call tag and no memset.
+  if (lt_impl::stream_capturing(st)) {
+    const hipError_t e =
+        hipMemsetAsync(a.ready, 0, 8ull * a.B * a.K + 32ull * a.B, st);
+    if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+  }
   const bool fuse = a.B <= ck_cus() && ck_env("LT_CHUNK_FUSE", 1) != 0;
   a.nc = fuse ? a.B : 0;
   const long long items = 2LL * a.B * ((a.K + 1) / 2);

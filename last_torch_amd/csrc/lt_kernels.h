@@ -1981,6 +1981,13 @@ struct Plan {
 LT_VARIANTS(LT_DECL)
 #undef LT_DECL
 int set_error(int code, const char* msg);
+// Whether `st` is being captured into a graph: launches whose hand-off words
+// carry a host-chosen per-call tag then zero those words by a memset node,
+// since every replay of the graph reuses the captured tag.
+inline bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+}
 // lt_tri.hip: the trigram checkpointing pair (den_fwd_tri / den_bwd_tri roles)
 int launch_tri_fwdbwd(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStream_t st);
 // lt_lattice.hip: frame-serial loss (+ dW) for the utterances with only[b] != 0

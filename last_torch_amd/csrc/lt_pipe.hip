@@ -1413,7 +1413,13 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
     }
     a.epoch = ep;
     if (W) {
-      const hipError_t e = hipMemsetAsync(a.err, 0, sizeof(int), st);
+      // a captured graph replays this epoch: zero the granules and band
+      // flags per replay (a memset node), so no replay reads the last one's
+      const size_t zb = lt_impl::stream_capturing(st)
+                            ? (size_t)((char*)a.err - (char*)mws) + sizeof(int)
+                            : sizeof(int);
+      const hipError_t e =
+          hipMemsetAsync(zb == sizeof(int) ? (void*)a.err : mws, 0, zb, st);
       if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
     }
   }

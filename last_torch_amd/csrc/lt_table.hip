@@ -1263,6 +1263,10 @@ __global__ __launch_bounds__(kTabMaxThreads) void tab_bwd_den_kernel(const TArgs
 __global__ void tab_onehot_kernel(const TArgs a) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= a.B) return;
+  // An utterance of distance -inf (every path masked) still gets the first
+  // maximum's path, as the reference's argmax backward gives it
+  // (semirings.py:354-401: ties go to the blank / the first source), so
+  // this walks the all-tie backpointers like any other.
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const int K = a.K, KK = K > 0 ? K : 1;
@@ -1915,7 +1919,8 @@ static DenBwdLayout den_bwd_layout(const lt_graph* g, const lt_table_problem* pb
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   DenBwdLayout l;
   l.dwf = 0;
-  l.bp = (bf16 || semiring == M_MAX) ? up(4 * BT * g->num_states * (g->vocab_size + 1)) : 0;
+  // the fp32 gradient only for bf16 W (fp32 W accumulates straight into dW)
+  l.bp = bf16 ? up(4 * BT * g->num_states * (g->vocab_size + 1)) : 0;
   l.win = l.bp;
   l.qstar = l.bp;
   l.dist = l.bp;

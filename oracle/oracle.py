@@ -54,8 +54,10 @@ def lib():
                                                  _F, _F, _F, ctypes.c_void_p])
     l.tab_viterbi.argtypes = [_c_int] * 5 + [_I, _F, _I, _c_int, _L, _F]
     l.tab_den_grad.argtypes = [_c_int] * 5 + [_I, _F, _I, _F, _F]
+    l.tab_dist_grad.argtypes = ([_c_int] * 6 + [_I, _F, _I, ctypes.c_void_p, ctypes.c_void_p,
+                                                 _c_int, _c_int, ctypes.c_void_p, _F, _F])
     for f in ('tab_den_forward', 'tab_num_forward', 'tab_loss_grad', 'tab_viterbi',
-              'tab_den_grad'):
+              'tab_den_grad', 'tab_dist_grad'):
       getattr(l, f).restype = None
     _lib = l
   return _lib
@@ -216,3 +218,22 @@ def tab_viterbi(table, W, num_frames, K, convention=1):
   weight = np.zeros([B], np.float32)
   lib().tab_viterbi(B, T, C, V, K, table, W, _i32(num_frames), convention, labels, weight)
   return labels, weight
+
+
+def tab_dist_grad(table, W, num_frames, K, semiring, labels=None, num_labels=None, grad=None):
+  """(dist [B], d dist / dW [B,T,C,V+1]) under `semiring` for any next-state
+  table and alignment K: the denominator (_forward, lattices.py:379-496) when
+  `labels` is None, else the numerator (_string_forward, lattices.py:250-377).
+  Log: the arc marginals; MaxTropical: `grad` on the first-maximum path's
+  arcs (semirings.py:354-401); Real: alpha * beta' (semirings.py:143-173)."""
+  table, W, B, T, C, V = _tab(table, W)
+  string = labels is not None
+  lab = _i32(labels) if string else None
+  U = lab.shape[1] if string else 0
+  nl = _i32(num_labels) if string else None
+  dist = np.zeros([B], np.float32)
+  dW = np.zeros_like(W)
+  g = None if grad is None else _f32(grad)
+  lib().tab_dist_grad(B, T, U, C, V, K, table, W, _i32(num_frames), _ptr(lab), _ptr(nl),
+                      semiring, int(string), _ptr(g), dist, dW)
+  return dist, dW

@@ -509,3 +509,168 @@ void tab_viterbi(int B, int T, int C, int V, int K, const int* table, const floa
   free(a); free(na); free(last); free(nxt); free(terms); free(win); free(argk);
   graph_free(&g);
 }
+
+/* MaxTropical gradient of one utterance over graph g: the reference
+ * differentiates its MaxTropical distance through Maximum (a >= b keeps a,
+ * semirings.py:354-371) and Max (first argmax, :373-401), so the gradient is
+ * `scale` on every arc of the first-maximum path (an arc used twice in a
+ * frame gets it twice). fin < 0: the distance is the Max over all states
+ * (lattices.py:482-496); fin >= 0: the Max over where(is_final, alpha, -inf)
+ * (lattices.py:375-377), whose argmax is fin while alpha_T[fin] > -inf and
+ * position 0 otherwise -- the gradient then reaches alpha only if fin == 0.
+ * Padding frames carry alpha (lattices.py:357-358, 460-461): no arcs. */
+static void grad_max(const graph_t* g, int K, long long FR, const float* W, int nf, int fin,
+                     double scale, double* acc, float* dist) {
+  const int S = g->S, KK = K == 0 ? 1 : K;
+  float* a = (float*)malloc(sizeof(float) * S);
+  float* na = (float*)malloc(sizeof(float) * S);
+  float* last = (float*)malloc(sizeof(float) * S);
+  float* nxt = (float*)malloc(sizeof(float) * S);
+  float* terms = (float*)malloc(sizeof(float) * (size_t)(K + 1) * S);
+  int* win = (int*)malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1) * S);
+  int* argk = (int*)malloc(sizeof(int) * (size_t)(nf > 0 ? nf : 1) * KK * S);
+  for (int q = 0; q < S; ++q) a[q] = q == 0 ? 0.f : -INFINITY;
+  for (int t = 0; t < nf; ++t) {
+    frame_max(g, K, W + (long long)t * FR, a, na, last, nxt, terms, win + (long long)t * S,
+              argk + (long long)t * KK * S);
+    memcpy(a, na, sizeof(float) * S);
+  }
+  int q = -1;
+  if (fin < 0) {
+    q = 0;
+    for (int s = 1; s < S; ++s) if (a[s] > a[q]) q = s;
+    *dist = a[q];
+  } else {
+    *dist = fin < S ? a[fin] : -INFINITY;
+    if (fin < S) q = a[fin] > -INFINITY ? fin : (fin == 0 ? 0 : -1);
+  }
+  for (int t = nf - 1; t >= 0 && q >= 0; --t) {
+    double* dw = acc + (long long)t * FR;
+    const int* ak = argk + (long long)t * KK * S;
+    if (K == 0) {
+      const int arc = ak[q];
+      if (arc < 0) {
+        dw[g->blank[q]] += scale;
+      } else {
+        dw[g->wix[arc]] += scale;
+        q = g->src[arc];
+      }
+    } else {
+      dw[g->blank[q]] += scale;  /* the terminating blank of the winning term */
+      for (int j = win[(long long)t * S + q]; j >= 1; --j) {
+        const int arc = ak[(long long)(j - 1) * S + q];
+        dw[g->wix[arc]] += scale;
+        q = g->src[arc];
+      }
+    }
+  }
+  free(a); free(na); free(last); free(nxt); free(terms); free(win); free(argk);
+}
+
+/* Real-semiring gradient of one utterance over graph g (the reference's
+ * Real autograd is plain arithmetic, semirings.py:143-173): d dist / dW by
+ * reverse accumulation in double through each frame's recursion --
+ *   FrameDependent  a'[q] = a[q] w_b[q] + sum_{p->q} a[p] w          (alignments.py:320-329, 286-297)
+ *   FrameLabelDependent  L_0 = a, L_i[q] = sum_{p->q} L_{i-1}[p] w,
+ *                   a'[q] = w_b[q] sum_i L_i[q]                      (alignments.py:362-377, 420-432)
+ * fin < 0: dist = sum_q a_T[q]; fin >= 0: a_T[fin] (0 when fin >= S). */
+static void grad_real(const graph_t* g, int K, int T, long long FR, const float* W, int nf, int fin,
+                      double scale, double* acc, float* dist) {
+  const int S = g->S;
+  double* ah = (double*)malloc(sizeof(double) * (size_t)(T + 1) * S);
+  *dist = (float)forward_d(g, K, TAB_REAL, T, FR, W, nf, 0, ah, NULL, fin);
+  double* beta = (double*)malloc(sizeof(double) * S);
+  double* nb = (double*)malloc(sizeof(double) * S);
+  double* la = (double*)malloc(sizeof(double) * (size_t)(K + 1) * S);
+  double* dl = (double*)malloc(sizeof(double) * S);
+  double* dn = (double*)malloc(sizeof(double) * S);
+  for (int q = 0; q < S; ++q) beta[q] = (fin < 0 || q == fin) ? scale : 0.0;
+  for (int t = nf - 1; t >= 0; --t) {
+    const float* w = W + (long long)t * FR;
+    const double* al = ah + (long long)t * S;
+    double* dw = acc + (long long)t * FR;
+    if (K == 0) {
+      for (int p = 0; p < S; ++p) {
+        dw[g->blank[p]] += al[p] * beta[p];
+        double r = w[g->blank[p]] * beta[p];
+        for (int o = g->out_off[p]; o < g->out_off[p + 1]; ++o) {
+          const int a = g->out_arc[o];
+          dw[g->wix[a]] += al[p] * beta[g->dst[a]];
+          r += w[g->wix[a]] * beta[g->dst[a]];
+        }
+        nb[p] = r;
+      }
+    } else {
+      memcpy(la, al, sizeof(double) * S);
+      for (int i = 1; i <= K; ++i)
+        for (int q = 0; q < S; ++q) {
+          double r = 0.0;
+          for (int a = g->in_off[q]; a < g->in_off[q + 1]; ++a)
+            r += la[(long long)(i - 1) * S + g->src[a]] * w[g->wix[a]];
+          la[(long long)i * S + q] = r;
+        }
+      for (int q = 0; q < S; ++q) {
+        double s = 0.0;
+        for (int i = 0; i <= K; ++i) s += la[(long long)i * S + q];
+        dw[g->blank[q]] += beta[q] * s;
+        dl[q] = beta[q] * w[g->blank[q]];  /* dL_K */
+      }
+      for (int i = K - 1; i >= 0; --i) {
+        for (int p = 0; p < S; ++p) {
+          double r = beta[p] * w[g->blank[p]];
+          for (int o = g->out_off[p]; o < g->out_off[p + 1]; ++o) {
+            const int a = g->out_arc[o];
+            dw[g->wix[a]] += la[(long long)i * S + p] * dl[g->dst[a]];
+            r += w[g->wix[a]] * dl[g->dst[a]];
+          }
+          dn[p] = r;
+        }
+        memcpy(dl, dn, sizeof(double) * S);
+      }
+      memcpy(nb, dl, sizeof(double) * S);
+    }
+    memcpy(beta, nb, sizeof(double) * S);
+  }
+  free(ah); free(beta); free(nb); free(la); free(dl); free(dn);
+}
+
+/* The gradient of the distance under semiring sr, per utterance scaled by
+ * grad[b] (nullable: 1): string = 0 the denominator (_forward over the
+ * context graph, lattices.py:379-496), string = 1 the numerator
+ * (_string_forward over the string acceptor, lattices.py:250-377). dist [B]
+ * gets the distance. Log: the marginals (backward_d), zero for a non-finite
+ * distance; MaxTropical: grad_max; Real: grad_real. */
+void tab_dist_grad(int B, int T, int U, int C, int V, int K, const int* table, const float* W,
+                   const int* nf, const int* labels, const int* nl, int sr, int string,
+                   const float* grad, float* dist, float* dW) {
+  graph_t gd;
+  context_graph(C, V, table, &gd);
+  const long long FR = (long long)C * (V + 1);
+  const int NP = U + 1;
+  const int SM = C > NP ? C : NP;
+  double* hist = (double*)malloc(sizeof(double) * (size_t)(T + 1) * SM);
+  double* acc = (double*)malloc(sizeof(double) * (size_t)(T > 0 ? T : 1) * FR);
+  for (int b = 0; b < B; ++b) {
+    graph_t gs;
+    if (string) string_graph(C, V, table, U, labels + (long long)b * U, &gs);
+    const graph_t* g = string ? &gs : &gd;
+    const int nfb = nf[b] < 0 ? 0 : (nf[b] > T ? T : nf[b]);
+    const float* Wb = W + (long long)b * T * FR;
+    const int fin = string ? ((nl[b] >= 0 && nl[b] <= U) ? nl[b] : NP) : -1;
+    const double gb = grad ? grad[b] : 1.0;
+    memset(acc, 0, sizeof(double) * (size_t)T * FR);
+    if (sr == TAB_MAX) {
+      grad_max(g, K, FR, Wb, nfb, fin, gb, acc, dist + b);
+    } else if (sr == TAB_REAL) {
+      grad_real(g, K, T, FR, Wb, nfb, fin, gb, acc, dist + b);
+    } else {
+      const double d = forward_d(g, K, TAB_LOG, T, FR, Wb, nfb, 0, hist, NULL, fin);
+      dist[b] = (float)d;
+      if (isfinite(d)) backward_d(g, K, FR, Wb, nfb, hist, d, fin, gb, acc);
+    }
+    for (long long e = 0; e < (long long)T * FR; ++e) dW[(long long)b * T * FR + e] = (float)acc[e];
+    if (string) graph_free(&gs);
+  }
+  free(hist); free(acc);
+  graph_free(&gd);
+}
