@@ -14,7 +14,7 @@ lg_of = $(subst M1,-1,$(word 1,$(subst _, ,$(1))))
 lgn_of = $(word 1,$(subst _, ,$(1)))
 p_of = $(word 2,$(subst _, ,$(1)))
 LIB := last_torch_amd/liblt_lattice.so
-DEPS := $(CSRC)/lt_kernels.h include/lt_lattice.h
+DEPS := $(CSRC)/lt_kernels.h $(CSRC)/lt_joint.h include/lt_lattice.h
 
 CPULIB := last_torch_amd/liblt_lattice_cpu.so
 CXX ?= g++
@@ -58,7 +58,11 @@ $(OBJ)/lt_producer.o: $(CSRC)/lt_producer.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_vit.o $(OBJ)/lt_tri.o $(INST_OBJS)
+$(OBJ)/lt_joint.o: $(CSRC)/lt_joint.hip $(DEPS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(OBJ)/lt_tri.o $(INST_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
 oracle:
@@ -85,7 +89,7 @@ $(STAMP_OBJ)/lt_pipe.o: $(CSRC)/lt_pipe.hip $(DEPS)
 $(STAMP_OBJ)/lt_tri.o: $(CSRC)/lt_tri.hip $(DEPS)
 	@mkdir -p $(STAMP_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -c -o $@ $<
-stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_vit.o $(STAMP_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
+stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(STAMP_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(STAMP_OBJ)/liblt_lattice_stamps.so $^
 .PHONY: stamps
 
@@ -98,6 +102,6 @@ $(DIAG_OBJ)/lt_inst_%.o: $(CSRC)/lt_inst.hip $(DEPS)
 $(DIAG_OBJ)/%.o: $(CSRC)/%.hip $(DEPS)
 	@mkdir -p $(DIAG_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_DIAG -c -o $@ $<
-diag: $(DIAG_OBJ)/lt_lattice.o $(DIAG_OBJ)/lt_pipe.o $(DIAG_OBJ)/lt_chunk.o $(DIAG_OBJ)/lt_table.o $(DIAG_OBJ)/lt_producer.o $(DIAG_OBJ)/lt_vit.o $(DIAG_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(DIAG_OBJ)/lt_inst_$(v).o)
+diag: $(DIAG_OBJ)/lt_lattice.o $(DIAG_OBJ)/lt_pipe.o $(DIAG_OBJ)/lt_chunk.o $(DIAG_OBJ)/lt_table.o $(DIAG_OBJ)/lt_producer.o $(DIAG_OBJ)/lt_joint.o $(DIAG_OBJ)/lt_vit.o $(DIAG_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(DIAG_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(DIAG_OBJ)/liblt_lattice_diag.so $^
 .PHONY: diag

@@ -150,7 +150,9 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
  * this is the chunked two-level scan below (two launches, plus one
  * frame-serial launch whose workgroups exit at once unless an utterance is
  * out of its range or a hand-off wait timed out; no memset: the hand-off
- * words carry a per-call tag, so the workspace's contents do not matter). Other
+ * words carry a per-call tag, so the workspace's contents do not matter;
+ * under stream capture, where every replay would reuse the captured tag, a
+ * memset node zeroes them instead). Other
  * bigram shapes with 2B below the CU count run ONE fused launch (alpha and
  * beta recursions plus workgroups that turn every frame into marginals as
  * soon as both recursions have passed it; should a hand-off wait time out,
@@ -300,6 +302,32 @@ int lt_table_den_backward(const lt_graph* g, const lt_table_problem* pb, int32_t
                           const float* alpha, const float* grad, void* dW, void* workspace,
                           size_t workspace_bytes, void* stream);
 
+/* The gradient of lt_table_num_forward's string distance
+ * (RecognitionLattice._string_forward under autograd, lattices.py:250-377,
+ * through FrameDependent.string_forward alignments.py:320-329 or
+ * FrameLabelDependent.string_forward :420-432):
+ *   LT_SEMIRING_MAX   dW = grad_b on every arc of the best string-aligned
+ *                     path (ties: the blank term / the fewest expansions,
+ *                     semirings.py:354-401; an arc taken twice in a frame
+ *                     gets 2 grad_b), walked back from num_labels -- or from
+ *                     position 0 when alpha_T[num_labels] is -inf, which
+ *                     carries a gradient only if num_labels == 0, as the
+ *                     reference's Max over where(is_final, ...) does
+ *   LT_SEMIRING_REAL  dW = grad_b * d num / dW (semirings.py:143-173)
+ * Log: LT_EUNSUPPORTED (its gradient is lt_table_loss_grad with local_norm,
+ * negated). grad [B] nullable (1); num [B] nullable out (the distance);
+ * dW W's dtype and shape, zero off the string's arcs and on padding frames.
+ * Arcs of several string positions on one lattice element sum in ascending
+ * position order (deterministic). Any next-state table: FullNGram through
+ * its next_state_table() (contexts.py:258-263). workspace:
+ * lt_table_num_backward_workspace_bytes(). */
+int lt_table_num_backward_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
+                                          int32_t semiring, size_t* bytes);
+int lt_table_num_backward(const lt_graph* g, const lt_table_problem* pb, int32_t semiring,
+                          const void* W, const int32_t* num_frames, const int32_t* labels,
+                          const int32_t* num_labels, const float* grad, float* num, void* dW,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
 /* RecognitionLattice.shortest_path (lattices.py:185-247), per utterance (no
  * D6 aliasing): labels [B, T*A] int64 with A = 1 (FrameDependent) or K+1
  * (FrameLabelDependent): slot i of frame t = label of the (i+1)-th lexical
@@ -393,6 +421,50 @@ int lt_joint_weights_backward(int64_t rows, int32_t num_states, int32_t hidden, 
                               const float* out_weight, const float* grad_W, float* d_ctx_proj,
                               float* d_frame_proj, float* d_out_weight, float* d_out_bias,
                               void* workspace, size_t workspace_bytes, void* stream);
+
+/* The joint weight function fused into the lattice loss (SURVEY.md 8(f)
+ * rank 1; replaces lt_joint_weights -> lt_loss_grad -> lt_joint_weights_backward
+ * for RecognitionLattice(JointWeightFn).forward + .backward, weight_fns.py:
+ * 174-227 consumed at lattices.py:446): the loss of FullNGram n = 1 (16 <
+ * vocab_size <= 32) x FrameDependent under Log, fp32, with
+ *   W[b,t,c,y] = out_bias[y] + sum_h out_weight[y,h] tanh(ctx_proj[c,h] + frame_proj[b*T+t,h])
+ * formed on the matrix cores where the recursions and the marginal pass use
+ * it -- bit-identical to lt_joint_weights_ex's W in the same precision -- and
+ * the parameter gradients formed from the marginals in LDS: neither W nor
+ * d loss / dW is ever written to memory.
+ *   lt_loss_joint_forward   loss [B] (log_z, num [B] nullable), keeping the
+ *                           recursions' checkpoints in `state`
+ *   lt_loss_joint_backward  d_ctx_proj [C,H], d_frame_proj [B*T,H],
+ *                           d_out_weight [V+1,H], d_out_bias [V+1] of
+ *                           sum_b grad[b] loss_b (grad nullable = ones;
+ *                           unreachable strings contribute 0), from `state`
+ *   lt_loss_grad_joint      both, one workspace (state then scratch)
+ * hidden: 32, 64, ..., 256. max_labels < 128. The d_ctx_proj / d_out_weight /
+ * d_out_bias sums run in a fixed order (deterministic). */
+typedef struct lt_joint_params {
+  int32_t hidden;           /* H */
+  int32_t precision;        /* LT_JOINT_SPLIT or LT_JOINT_BF16 (forward products) */
+  const float* ctx_proj;    /* [C, H]    */
+  const float* frame_proj;  /* [B*T, H]  */
+  const float* out_weight;  /* [V+1, H]: row 0 blank, row y label y */
+  const float* out_bias;    /* [V+1]     */
+} lt_joint_params;
+int lt_loss_joint_workspace_bytes(const lt_problem* pb, const lt_joint_params* jp,
+                                  size_t* state_bytes, size_t* scratch_bytes);
+int lt_loss_joint_forward(const lt_problem* pb, const lt_joint_params* jp,
+                          const int32_t* num_frames, const int32_t* labels,
+                          const int32_t* num_labels, float* loss, float* log_z, float* num,
+                          void* state, size_t state_bytes, void* stream);
+int lt_loss_joint_backward(const lt_problem* pb, const lt_joint_params* jp,
+                           const int32_t* num_frames, const float* grad, float* d_ctx_proj,
+                           float* d_frame_proj, float* d_out_weight, float* d_out_bias,
+                           void* state, size_t state_bytes, void* scratch, size_t scratch_bytes,
+                           void* stream);
+int lt_loss_grad_joint(const lt_problem* pb, const lt_joint_params* jp, const int32_t* num_frames,
+                       const int32_t* labels, const int32_t* num_labels, const float* grad,
+                       float* loss, float* log_z, float* num, float* d_ctx_proj,
+                       float* d_frame_proj, float* d_out_weight, float* d_out_bias,
+                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* Thread-local description of the last error; never NULL. */
 const char* lt_last_error(void);

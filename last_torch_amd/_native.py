@@ -46,6 +46,13 @@ class TableProblem(ctypes.Structure):
               ('max_labels', ctypes.c_int32), ('weight_dtype', ctypes.c_int32)]
 
 
+class JointParams(ctypes.Structure):
+  """lt_joint_params: the joint weight function's operands (device pointers)."""
+  _fields_ = [('hidden', ctypes.c_int32), ('precision', ctypes.c_int32),
+              ('ctx_proj', ctypes.c_void_p), ('frame_proj', ctypes.c_void_p),
+              ('out_weight', ctypes.c_void_p), ('out_bias', ctypes.c_void_p)]
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _G = ctypes.POINTER(Graph)
@@ -80,6 +87,8 @@ _SIG = {
     'lt_table_loss_grad': [_G, _TP, _I32] + [_P] * 9 + [ctypes.c_size_t, _P],
     'lt_table_den_backward_workspace_bytes': [_G, _TP, _I32, ctypes.POINTER(ctypes.c_size_t)],
     'lt_table_den_backward': [_G, _TP, _I32] + [_P] * 7 + [ctypes.c_size_t, _P],
+    'lt_table_num_backward_workspace_bytes': [_G, _TP, _I32, ctypes.POINTER(ctypes.c_size_t)],
+    'lt_table_num_backward': [_G, _TP, _I32] + [_P] * 8 + [ctypes.c_size_t, _P],
     'lt_table_viterbi_workspace_bytes': [_G, _TP, ctypes.POINTER(ctypes.c_size_t)],
     'lt_table_viterbi': [_G, _TP, _P, _P, _I32, _P, _P, _P, ctypes.c_size_t, _P],
     'lt_joint_weights_workspace_bytes': [ctypes.c_int64, _I32, _I32,
@@ -92,6 +101,15 @@ _SIG = {
                                                   ctypes.POINTER(ctypes.c_size_t)],
     'lt_joint_weights_backward': [ctypes.c_int64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P,
                                   _P, _P, ctypes.c_size_t, _P],
+    'lt_loss_joint_workspace_bytes': [ctypes.POINTER(Problem), ctypes.POINTER(JointParams),
+                                      ctypes.POINTER(ctypes.c_size_t),
+                                      ctypes.POINTER(ctypes.c_size_t)],
+    'lt_loss_joint_forward': [ctypes.POINTER(Problem), ctypes.POINTER(JointParams)] + [_P] * 7 +
+                             [ctypes.c_size_t, _P],
+    'lt_loss_joint_backward': [ctypes.POINTER(Problem), ctypes.POINTER(JointParams)] + [_P] * 7 +
+                              [ctypes.c_size_t, _P, ctypes.c_size_t, _P],
+    'lt_loss_grad_joint': [ctypes.POINTER(Problem), ctypes.POINTER(JointParams)] + [_P] * 12 +
+                          [ctypes.c_size_t, _P],
     'lt_viterbi_workspace_bytes': [ctypes.POINTER(Problem), ctypes.POINTER(ctypes.c_size_t)],
     'lt_viterbi': [ctypes.POINTER(Problem), _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_size_t,
                    _P],
@@ -546,6 +564,29 @@ def table_den_backward(graph, W, num_frames, semiring, dist=None, alpha=None, gr
   return dW
 
 
+def table_num_backward(graph, W, num_frames, labels, num_labels, semiring, grad=None):
+  """lt_table_num_backward: (num [B], dW [B,T,C,V+1] in W's dtype) = the
+  string distance and grad_b * its gradient in MaxTropical (the best
+  string-aligned path's arcs) or Real (alpha * beta' on the string
+  acceptor)."""
+  pb = _tproblem(graph, W, labels.shape[-1])
+  B = W.shape[0]
+  nbytes = ctypes.c_size_t(0)
+  _check(lib().lt_table_num_backward_workspace_bytes(ctypes.byref(graph.g), ctypes.byref(pb),
+                                                     semiring, ctypes.byref(nbytes)),
+         'lt_table_num_backward_workspace_bytes')
+  ws = torch.empty([max(nbytes.value, 1)], dtype=torch.uint8, device=W.device)
+  num = _f32([B], W)
+  dW = torch.empty_like(W)
+  if grad is not None:
+    grad = grad.to(device=W.device, dtype=torch.float32).reshape(B).contiguous()
+  _check(lib().lt_table_num_backward(ctypes.byref(graph.g), ctypes.byref(pb), semiring, _ptr(W),
+                                     _ptr(num_frames), _ptr(labels), _ptr(num_labels), _ptr(grad),
+                                     _ptr(num), _ptr(dW), _ptr(ws), nbytes.value, _stream()),
+         'lt_table_num_backward')
+  return num, dW
+
+
 def table_viterbi(graph, W, num_frames, label_convention):
   """lt_table_viterbi: (labels int64 [B, T*A], path weights [B])."""
   pb = _tproblem(graph, W)
@@ -633,3 +674,115 @@ def joint_weights_backward(ctx_proj, frame_proj, out_weight, grad_W):
                                          _ptr(dpc), _ptr(dpf), _ptr(dwo), _ptr(dbias), _ptr(ws),
                                          ws.numel() * 4, _stream()), 'lt_joint_weights_backward')
   return dpc, dpf.reshape(frame_proj.shape), dwo, dbias
+
+
+# ---------------------------------------------------------------------------
+# The joint weight function fused into the lattice loss (lt_joint.hip)
+# ---------------------------------------------------------------------------
+def _joint(ctx_proj, frame_proj, out_weight, out_bias, precision):
+  for name, t in (('ctx_proj', ctx_proj), ('frame_proj', frame_proj),
+                  ('out_weight', out_weight), ('out_bias', out_bias)):
+    if not t.is_cuda:
+      raise LatticeLibraryError(f'joint loss: {name} must be on a ROCm device')
+    if t.dtype != torch.float32:
+      raise TypeError(f'joint loss: {name} must be float32, got {t.dtype}')
+  C, H = ctx_proj.shape
+  ops = tuple(x.contiguous() for x in (ctx_proj, frame_proj.reshape(-1, H), out_weight, out_bias))
+  jp = JointParams(H, JOINT_SPLIT if precision == 'fp32' else JOINT_BF16,
+                   *(x.data_ptr() for x in ops))
+  return jp, ops
+
+
+def joint_problem(batch, frames, labels, vocab_size):
+  return Problem(batch, frames, vocab_size, 1, labels, LT_DTYPE_F32)
+
+
+def joint_loss_supported(batch, frames, labels, vocab_size, context_size, hidden):
+  """Shapes lt_loss_grad_joint takes: FullNGram n = 1, 16 < V <= 32, U < 128,
+  hidden in {32, 64, ..., 256} (fp32)."""
+  if context_size != 1 or not 16 < vocab_size <= 32 or labels + 1 > 128:
+    return False
+  if hidden % 32 or not 32 <= hidden <= 256:
+    return False
+  return batch * frames * (vocab_size + 1) ** 2 * 4 < 0xFFFFFFF0
+
+
+def joint_loss_workspace_bytes(batch, frames, labels, vocab_size, hidden, precision='fp32'):
+  """(state_bytes, scratch_bytes) of lt_loss_joint_forward / _backward."""
+  pb = joint_problem(batch, frames, labels, vocab_size)
+  jp = JointParams(hidden, JOINT_SPLIT if precision == 'fp32' else JOINT_BF16, None, None, None,
+                   None)
+  st, sc = ctypes.c_size_t(0), ctypes.c_size_t(0)
+  _check(lib().lt_loss_joint_workspace_bytes(ctypes.byref(pb), ctypes.byref(jp), ctypes.byref(st),
+                                             ctypes.byref(sc)), 'lt_loss_joint_workspace_bytes')
+  return st.value, sc.value
+
+
+def joint_loss_forward(ctx_proj, frame_proj, out_weight, out_bias, num_frames, labels, num_labels,
+                       precision='fp32'):
+  """lt_loss_joint_forward: (loss [B], log_z, num, state) with W formed on the
+  matrix cores where the recursions use it; frame_proj [B, T, H]."""
+  B, T, H = frame_proj.shape
+  V = out_weight.shape[0] - 1
+  U = labels.shape[-1]
+  jp, ops = _joint(ctx_proj, frame_proj, out_weight, out_bias, precision)
+  pb = joint_problem(B, T, U, V)
+  st, _ = joint_loss_workspace_bytes(B, T, U, V, H, precision)
+  state = torch.empty([max(st, 16)], dtype=torch.uint8, device=frame_proj.device)
+  loss, log_z, num = (_f32([B], frame_proj) for _ in range(3))
+  _check(lib().lt_loss_joint_forward(ctypes.byref(pb), ctypes.byref(jp), _ptr(num_frames),
+                                     _ptr(labels), _ptr(num_labels), _ptr(loss), _ptr(log_z),
+                                     _ptr(num), _ptr(state), state.numel(), _stream()),
+         'lt_loss_joint_forward')
+  del ops  # the launch is queued on the stream; the caching allocator orders reuse
+  return loss, log_z, num, state
+
+
+def joint_loss_backward(ctx_proj, frame_proj, out_weight, out_bias, num_frames, labels, state,
+                        grad=None, precision='fp32'):
+  """lt_loss_joint_backward: (d_ctx_proj, d_frame_proj [B, T, H], d_out_weight,
+  d_out_bias) of sum_b grad[b] loss_b from the forward's `state`."""
+  B, T, H = frame_proj.shape
+  V = out_weight.shape[0] - 1
+  U = labels.shape[-1]
+  jp, ops = _joint(ctx_proj, frame_proj, out_weight, out_bias, precision)
+  pb = joint_problem(B, T, U, V)
+  st, sc = joint_loss_workspace_bytes(B, T, U, V, H, precision)
+  scratch = torch.empty([max(sc, 16)], dtype=torch.uint8, device=frame_proj.device)
+  dpc = torch.empty_like(ops[0])
+  dpf = torch.empty_like(ops[1])
+  dwo = torch.empty_like(ops[2])
+  dbias = torch.empty_like(ops[3])
+  g = None if grad is None else grad.to(torch.float32).reshape(B).contiguous()
+  _check(lib().lt_loss_joint_backward(ctypes.byref(pb), ctypes.byref(jp), _ptr(num_frames), _ptr(g),
+                                      _ptr(dpc), _ptr(dpf), _ptr(dwo), _ptr(dbias), _ptr(state),
+                                      state.numel(), _ptr(scratch), scratch.numel(), _stream()),
+         'lt_loss_joint_backward')
+  return dpc, dpf.reshape(B, T, H), dwo, dbias
+
+
+def loss_grad_joint(ctx_proj, frame_proj, out_weight, out_bias, num_frames, labels, num_labels,
+                    grad=None, precision='fp32', workspace=None):
+  """lt_loss_grad_joint: (loss, log_z, num, d_ctx_proj, d_frame_proj, d_out_weight,
+  d_out_bias) in one call; `workspace` (uint8, state + scratch bytes) reused
+  when given."""
+  B, T, H = frame_proj.shape
+  V = out_weight.shape[0] - 1
+  U = labels.shape[-1]
+  jp, ops = _joint(ctx_proj, frame_proj, out_weight, out_bias, precision)
+  pb = joint_problem(B, T, U, V)
+  st, sc = joint_loss_workspace_bytes(B, T, U, V, H, precision)
+  if workspace is None or workspace.numel() < st + sc:
+    workspace = torch.empty([st + sc], dtype=torch.uint8, device=frame_proj.device)
+  loss, log_z, num = (_f32([B], frame_proj) for _ in range(3))
+  dpc = torch.empty_like(ops[0])
+  dpf = torch.empty_like(ops[1])
+  dwo = torch.empty_like(ops[2])
+  dbias = torch.empty_like(ops[3])
+  g = None if grad is None else grad.to(torch.float32).reshape(B).contiguous()
+  _check(lib().lt_loss_grad_joint(ctypes.byref(pb), ctypes.byref(jp), _ptr(num_frames),
+                                  _ptr(labels), _ptr(num_labels), _ptr(g), _ptr(loss), _ptr(log_z),
+                                  _ptr(num), _ptr(dpc), _ptr(dpf), _ptr(dwo), _ptr(dbias),
+                                  _ptr(workspace), workspace.numel(), _stream()),
+         'lt_loss_grad_joint')
+  return loss, log_z, num, dpc, dpf.reshape(B, T, H), dwo, dbias

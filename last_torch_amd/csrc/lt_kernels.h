@@ -2015,13 +2015,23 @@ int vit_backtrace_lds(const lt_problem* pb, int* seg);
 int vit_backtrace(const lt_problem* pb, const unsigned char* bp, const int* qstar,
                   const int32_t* nfr, const float* grad, int64_t* labels, void* arcs,
                   int32_t conv, void* stream);
+// The joint weight function's operands for the fused paths (lt_joint.hip):
+// W[f, c, y] = bias[y] + sum_h wo[y, h] tanh(pc[c, h] + pf[f, h])
+struct JointOps {
+  int H;                  // hidden units (a multiple of 32)
+  int prod;               // 1: split-bf16 products, 2: bf16 products
+  const float *pc, *ec;   // [C, H] Pc and e^{2 Pc}
+  const float *pf, *ef;   // [B*T, H] Pf and e^{2 Pf}
+  const int *cbig, *fbig; // [1], [ceil(B*T / 32)]: some |projection| > 40 (direct tanh)
+  const float *wo, *bias; // [R, H], [R]
+};
 // lt_pipe.hip: pipelined bigram Log recursions (alpha, and beta when dirs == 2)
 bool pipe_eligible(const lt_problem* pb);
 int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32_t* nfr,
                 const int32_t* labels, const int32_t* nlab, float* loss, float* log_z,
                 float* num, float* alpha, float* alpha_num, float* beta, float* beta_num,
                 int32_t* arcs, int dirs, int* err, void* stream, void* dW = nullptr,
-                int mid = 0, void* mws = nullptr);
+                int mid = 0, void* mws = nullptr, const JointOps* jo = nullptr);
 // mid mode (lt_loss_grad at large batches): workspace bytes; whether the
 // grid fits co-resident (launch_pipe with W == nullptr answers the same)
 size_t pipe_mid_workspace_bytes(const lt_problem* pb);

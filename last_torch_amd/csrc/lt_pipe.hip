@@ -41,7 +41,7 @@
 // (consumers); there is no workgroup barrier inside the frame loop. Every
 // wait is bounded: a stalled pipeline raises an abort flag and the kernel
 // drains instead of hanging.
-#include "lt_kernels.h"
+#include "lt_joint.h"
 
 #include <atomic>
 
@@ -95,6 +95,19 @@ struct PArgs {
   unsigned long long* gnum[2];  // [B,T,NP] alpha^n rows, beta^n rows
   unsigned epoch;               // per call: tag = epoch * T + t
   unsigned long long* mflag;    // [2][B] band zeroed: (epoch, ~epoch), alpha side then beta side
+  // ---- producer helpers (lt_loss_grad_joint): the helpers form each frame's
+  // W from the joint weight function's projections (W never in HBM)
+  int prod;            // 0: W from HBM; 1: split-bf16 products; 2: bf16 products
+  int jH;              // hidden units H (a multiple of 32)
+  const float* jpc;    // [C, H]  Pc (the direct path's operand)
+  const float* jec;    // [C, H]  e^{2 Pc}
+  const float* jpf;    // [B*T, H] Pf
+  const float* jef;    // [B*T, H] e^{2 Pf}
+  const int* jcbig;    // [1] some |Pc| > kSplitMax
+  const int* jfbig;    // [ceil(B*T / 32)] some |Pf| of the 32-row block > kSplitMax
+  const float* jwo;    // [R, H] Wo (blank row first)
+  const float* jbias;  // [R]
+  int off_wo, off_ec;  // LDS: Wo bf16 (hi, lo), e^{2 Pc} fp32 [C][H]
 };
 constexpr int kMidBand = 32;    // frames next to the middle zeroed before the granules flow
 // floats per slot of the den (hring) and numerator (nring) row rings
@@ -795,6 +808,101 @@ LT_DEVINL void helper_pipe(const PArgs& a, unsigned char* lds, int b, int nf, in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---- producer helpers (lt_loss_grad_joint) ----------------------------------
+// Helper hw forms frame t's arc weights itself instead of loading them: the
+// joint weight function W[p, y] = bias[y] + sum_h Wo[y, h] tanh(Pc[p, h] +
+// Pf[f, h]) (weight_fns.py:174-227) as two 32-state row tiles (states 0..31,
+// then 32) x two 32-label column tiles on the matrix cores -- joint_tile,
+// the producer's own K steps, so every element is bit-identical to
+// lt_joint_weights_ex's W -- then the frame max, raw W and E = exp(W - c)
+// into the slot as helper_pipe leaves them. The split (e^{2 Pc} e^{2 Pf}) or
+// direct tanh is chosen per 32-row block of Pf as lt_joint_weights does. W
+// never exists in HBM; the helpers work in the shadow of the frame chain.
+template <bool REV, bool SP>
+LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, int hw, int lane) {
+  lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
+  const int R = a.R, C = a.C, H = a.jH, HP = H + 8;
+  const int WL = (R * HP + 7) & ~7;
+  const unsigned short* wo = (const unsigned short*)(lds + a.off_wo);
+  const float* ecl = (const float*)(lds + a.off_ec);
+  const bool csplit = *a.jcbig == 0;
+  const int r = lane & 31, hk = 8 * (lane >> 5), half = lane >> 5;
+  const int y0 = r, y1 = 32 + r;
+  const bool v0 = y0 < R, v1 = y1 < R;
+  const float b0 = v0 ? a.jbias[y0] : 0.f, b1 = v1 ? a.jbias[y1] : 0.f;
+  const unsigned short* w0 = wo + (v0 ? y0 : R - 1) * HP + hk;
+  const unsigned short* w1 = wo + (v1 ? y1 : R - 1) * HP + hk;
+  const unsigned short* w0l = w0 + WL;
+  const unsigned short* w1l = w1 + WL;
+  // E's byte offset in a slot for element (p, y) (helper_pipe's layout)
+  auto eoff = [&](int p, int y) {
+    if (y == 0) return a.soff_eb + 4 * p;
+    const int row = REV ? p : y - 1, kk = REV ? y - 1 : p;
+    return a.soff_e + 4 * (row * a.rowE + (kk / a.J) * a.JP + (kk % a.J));
+  };
+  int seen_den = 0, seen_num = 0;
+  int slot = hw;
+  for (int i = hw; i < nf; i += a.NH) {
+    const int need = i - a.K + 1;  // the slot's previous frame (step i - K) must be consumed
+    if (need > 0) {
+      if (seen_den < need) {
+        if (!wait_ge(ctl + CTL_DEN, need, ctl + CTL_ABORT, a.err)) return;
+        seen_den = ctl[CTL_DEN];
+      }
+      if (seen_num < need) {
+        if (!wait_ge(ctl + CTL_NUM, need, ctl + CTL_ABORT, a.err)) return;
+        seen_num = ctl[CTL_NUM];
+      }
+    }
+    const int t = REV ? nf - 1 - i : i;
+    const long long f = (long long)b * a.T + t;
+    const bool split = csplit && a.jfbig[f >> 5] == 0;
+    const float* pfr = (split ? a.jef : a.jpf) + f * H + hk;
+    f32x16 acc[2][2] = {};
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int p = min(32 * rt + r, C - 1);  // rows past C repeat the last state, never stored
+      const float* pcr = split ? ecl + p * H + hk : a.jpc + p * H + hk;
+      joint_tile<SP, true>(split, pcr, pfr, H, w0, w1, w0l, w1l, acc[rt][0], acc[rt][1]);
+    }
+    // W = acc + bias (the producer's own rounding), the frame max over it
+    float mx = -kInf;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int p = 32 * rt + (k & 3) + 8 * (k >> 2) + 4 * half;
+        acc[rt][0][k] += b0;
+        acc[rt][1][k] += b1;
+        if (p < C) mx = fmaxf(mx, v1 ? fmaxf(acc[rt][0][k], acc[rt][1][k]) : acc[rt][0][k]);
+      }
+    const float c = safe(wave_max(mx));
+    const float cl = c * kLog2e;
+    unsigned char* sb = lds + a.off_ring + slot * a.slot_bytes;
+    lds_float* Wr = (lds_float*)as3(sb);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int p = 32 * rt + (k & 3) + 8 * (k >> 2) + 4 * half;
+        if (p < C) {
+          Wr[p * R + y0] = acc[rt][0][k];
+          *(lds_float*)(as3(sb) + eoff(p, y0)) = lt_exp_off(acc[rt][0][k], cl);
+          if (v1) {
+            Wr[p * R + y1] = acc[rt][1][k];
+            *(lds_float*)(as3(sb) + eoff(p, y1)) = lt_exp_off(acc[rt][1][k], cl);
+          }
+        }
+      }
+    if (lane == 0) {
+      *(lds_float*)(as3(sb) + a.soff_c) = c;
+      lds_release_store(ctl + CTL_TAG + slot, i + 1);
+    }
+    slot += a.NH;
+    if (slot >= a.K) slot -= a.K;
+  }
+}
+
 // ---- in-workgroup marginals (mid mode) --------------------------------------
 // Marginal wave m of a recursion workgroup turns the frames of its steps
 // i = s0 + m, s0 + m + NM, ... (the workgroup's far half: alpha frames
@@ -1073,7 +1181,7 @@ LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m
   }
 }
 
-template <int J, bool BF16, int PN, int D>
+template <int J, bool BF16, int PN, int D, int PROD = 0>
 __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void pipe_kernel(const PArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int blk = (int)blockIdx.x;
@@ -1104,6 +1212,14 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void
   int* ctx = (int*)(lds + a.off_ctx);
   int* ylab = (int*)(lds + a.off_ylab);
   for (int u = tid; u < a.U; u += nthr) ylab[u] = a.labels[(long long)b * a.U + u];
+  if constexpr (PROD != 0) {
+    // the producer helpers' operands: Wo as bf16 (hi, and lo for split
+    // products) with padded rows, e^{2 Pc} in fp32
+    const int H = a.jH, HP = H + 8, WL = (a.R * HP + 7) & ~7;
+    stage_wo<PROD == 1>(a.jwo, (unsigned short*)(lds + a.off_wo), a.R, H, HP, WL, tid, nthr);
+    float* ec = (float*)(lds + a.off_ec);
+    for (int k = tid; k < a.C * H; k += nthr) ec[k] = a.jec[k];
+  }
   __syncthreads();
   if (tid == 0) {
     // walk_states (contexts.py:109-146) with the lattices.py:314-338 label rules
@@ -1161,8 +1277,13 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void
     else num_pipe<PN, false>(a, lds, b, nf, lane);
   } else if (wave - 2 < a.NH) {
     constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
-    if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, wave - 2, lane);
-    else helper_pipe<BF16, NL, false>(a, lds, b, nf, wave - 2, lane);
+    if constexpr (PROD != 0) {
+      if (rev) helper_prod<true, PROD == 1>(a, lds, b, nf, wave - 2, lane);
+      else helper_prod<false, PROD == 1>(a, lds, b, nf, wave - 2, lane);
+    } else {
+      if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, wave - 2, lane);
+      else helper_pipe<BF16, NL, false>(a, lds, b, nf, wave - 2, lane);
+    }
   } else if (a.mid && wave - 2 - a.NH < a.NM) {
     if constexpr (PN <= 2) {  // mid mode: U < 128 (pipe_mid_fits)
       constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
@@ -1221,6 +1342,22 @@ int pipe_env(const char* name, int dflt) { return lt_impl::tune_int(name, dflt);
 template <int J, bool BF16, int PN>
 int launch_pipe_t(const PArgs& a, int grid, int threads, int lds, hipStream_t st) {
   constexpr int D = 4;
+  if (a.prod) {  // producer helpers: fp32 weights, V in (16, 32]
+    if constexpr (J == 17 && !BF16) {
+      const void* kp = a.prod == 1 ? (const void*)pipe_kernel<J, false, PN, D, 1>
+                                   : (const void*)pipe_kernel<J, false, PN, D, 2>;
+      hipError_t e = hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+      if (a.prod == 1)
+        hipLaunchKernelGGL((pipe_kernel<J, false, PN, D, 1>), dim3(grid), dim3(threads), lds, st, a);
+      else
+        hipLaunchKernelGGL((pipe_kernel<J, false, PN, D, 2>), dim3(grid), dim3(threads), lds, st, a);
+      e = hipGetLastError();
+      return e == hipSuccess ? LT_OK : lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
+    } else {
+      return lt_impl::set_error(LT_EUNSUPPORTED, "pipe producer helpers: fp32, 16 < V <= 32");
+    }
+  }
   const void* k = (const void*)pipe_kernel<J, BF16, PN, D>;
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
@@ -1303,7 +1440,7 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
                 const int32_t* labels, const int32_t* nlab, float* loss, float* log_z,
                 float* num, float* alpha, float* alpha_num, float* beta, float* beta_num,
                 int32_t* arcs, int dirs, int* err, void* stream, void* dW, int mid,
-                void* mws) {
+                void* mws, const JointOps* jo) {
   if (!pipe_eligible(pb)) return set_error(LT_EUNSUPPORTED, "pipe: shape not eligible");
   if (mid && (dirs != 2 || (!dW && W) || (!mws && W)))
     return set_error(LT_EINVAL, "pipe mid: both directions, dW and the workspace");
@@ -1353,6 +1490,17 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   a.off_u = off; off += al16((a.rowE + 4) * 4);
   a.off_ctx = off; off += al16(NP * 4);
   a.off_ylab = off; off += al16(NP * 4);
+  if (jo) {  // producer helpers: Wo bf16 (hi, lo) and e^{2 Pc} in LDS
+    if (mid || bf16 || jo->H % 32 || jo->H < 32)
+      return set_error(LT_EUNSUPPORTED, "pipe producer helpers: fp32, no mid mode, H % 32 == 0");
+    a.prod = jo->prod;
+    a.jH = jo->H;
+    a.jpc = jo->pc; a.jec = jo->ec; a.jpf = jo->pf; a.jef = jo->ef;
+    a.jcbig = jo->cbig; a.jfbig = jo->fbig; a.jwo = jo->wo; a.jbias = jo->bias;
+    const int WL = (R * (jo->H + 8) + 7) & ~7;
+    a.off_wo = off; off += al16((jo->prod == 1 ? 4LL : 2LL) * WL);
+    a.off_ec = off; off += al16(4LL * C * jo->H);
+  }
   int so = 0;
   const int NLc = a.J == 17 ? 18 : (a.J == 5 ? 5 : (a.J == 2 ? 2 : 1));
   if (NLc * 64 < FR) return set_error(LT_EUNSUPPORTED, "pipe: helper load plan");

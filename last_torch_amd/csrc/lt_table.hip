@@ -1619,6 +1619,230 @@ __global__ __launch_bounds__(256) void tab_to_bf16_kernel(const float* src, unsi
     dst[i] = f2bf(src[i]);
 }
 
+// ---- gradients of the string distance, MaxTropical and Real ----------------
+// RecognitionLattice._string_forward (lattices.py:250-377) differentiated as
+// the reference's autograd does it, for FrameDependent (alignments.py:320-329)
+// and FrameLabelDependent(K) (:420-432) string forwards over any next-state
+// table (walk_states, contexts.py:109-146):
+//   forward   term_i[u] = L_i[u] (x) bl[u], L_0 = alpha, L_i[u] = L_{i-1}[u-1]
+//             (x) lx[u-1] (shift_down's zero below i); alpha'[u] = (+)_i term_i
+//             (FrameDependent: alpha[u] bl[u] (+) alpha[u-1] lx[u-1])
+//   MaxTropical: Maximum keeps the blank term on ties (semirings.py:363) and
+//             Max the first expansion count i (:382); the gradient is grad_b
+//             on the arcs of the winning path, walked back from the final
+//             position -- num_labels while alpha_T there is above -inf, else
+//             position 0 of where(is_final, ...), which passes a gradient
+//             only when num_labels == 0 (lattices.py:375-377)
+//   Real:     reverse accumulation of the same recursion (semirings.py:143-173)
+// Positions whose arcs hit one lattice element (epsilon labels, a context
+// revisited) are summed by their chain head in ascending position order, one
+// writer per element and frame (deterministic). One workgroup per utterance.
+// Workspace: MaxTropical the winning term per (t, u) (bytes), Real the alpha
+// history (fp32). dW is zeroed by the caller's memset.
+constexpr int kStrChunk = 32768;  // bytes of decisions staged per chunk (MaxTropical walk)
+template <bool BF16, int SR>
+__global__ __launch_bounds__(kTabMaxThreads) void tab_str_grad_kernel(const TArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  const int U = a.U, S = U + 1, K = a.K, T = a.T;
+  const float zero = t_zero<SR>();
+  int* ctx = (int*)sm;    // [S] context state of position u, times R
+  int* yn = ctx + S;      // [S] label class of the arc leaving u
+  int* nxb = yn + S;      // [S] next position with the same blank element (-1)
+  int* nxl = nxb + S;     // [S] next position with the same lexical element (-1)
+  int* hd = nxl + S;      // [S] bit 0 / 1: head of its blank / lexical chain
+  float* xa = (float*)(hd + S);  // [S] alpha_t (forward) / alpha_t of the frame (backward)
+  float* xb = xa + S;     // [S] alpha_{t+1} / beta_{t+1}
+  float* xc = xb + S;     // [S] beta_t
+  float* wb = xc + S;     // [S] the frame's blank weights
+  float* wl = wb + S;     // [S] the frame's lexical weights (u < U)
+  float* gb = wl + S;     // [S] blank gradients of the frame
+  float* gl = gb + S;     // [S] lexical gradients
+  float* L = gl + S;      // [K+1][S] Real FrameLabelDependent: L_i
+  float* d0 = L + (K + 1) * S;  // [S] dL_{i+1}
+  float* d1 = d0 + S;           // [S] dL_i
+  int* marks = (int*)(d1 + S) + 4;  // [K+1][2] MaxTropical: a frame's marked elements, counts
+  unsigned char* wc = (unsigned char*)(marks + ((2 * (K + 1) + 3) & ~3));  // decision chunk
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > T ? T : nf);
+  const long long FR = (long long)a.C * a.R;
+  const unsigned char* wbase = a.W + (long long)b * T * FR * (BF16 ? 2 : 4);
+  unsigned char* dwbase = (unsigned char*)a.dW + (long long)b * T * FR * (BF16 ? 2 : 4);
+  if (tid == 0) t_walk(a, b, ctx, yn);
+  __syncthreads();
+  for (int u = tid; u < S; u += nthr) {
+    const int kb = ctx[u], kl = u < U ? ctx[u] + yn[u] : -1;
+    int nB = -1, nL = -1, h = u < U ? 3 : 1;
+    for (int v = u + 1; v < S && (nB < 0 || (kl >= 0 && nL < 0)); ++v) {
+      if (nB < 0 && ctx[v] == kb) nB = v;
+      if (kl >= 0 && nL < 0 && v < U && ctx[v] + yn[v] == kl) nL = v;
+    }
+    for (int v = 0; v < u; ++v) {
+      if (ctx[v] == kb) h &= ~1;
+      if (kl >= 0 && ctx[v] + yn[v] == kl) h &= ~2;
+    }
+    nxb[u] = nB;
+    nxl[u] = nL;
+    hd[u] = h;
+    xa[u] = u == 0 ? t_one<SR>() : zero;
+  }
+  __syncthreads();
+  // ---- forward: alpha_t (Real: to the history) / the winning term (Max)
+  for (int t = 0; t < nf; ++t) {
+    const unsigned char* wf = wbase + t * FR * (BF16 ? 2 : 4);
+    for (int u = tid; u < S; u += nthr) {
+      wb[u] = ldw<BF16>(wf, ctx[u]);
+      wl[u] = u < U ? ldw<BF16>(wf, ctx[u] + yn[u]) : zero;
+      if (SR == M_REAL) a.alpha[((long long)b * T + t) * S + u] = xa[u];
+    }
+    __syncthreads();
+    for (int u = tid; u < S; u += nthr) {
+      float r;
+      int wi = 0;
+      if (K == 0) {
+        if constexpr (SR == M_MAX) {
+          const float x = xa[u] + wb[u];
+          const float y = u >= 1 ? xa[u - 1] + wl[u - 1] : zero;
+          wi = (u >= 1 && !(x >= y)) ? 1 : 0;  // a NaN blank term at u = 0 ends the path there
+          r = x >= y ? x : y;
+        } else {
+          r = xa[u] * wb[u] + (u >= 1 ? xa[u - 1] * wl[u - 1] : 0.f);
+        }
+      } else {
+        r = t_times<SR>(xa[u], wb[u]);
+        for (int i = 1; i <= K; ++i) {
+          float l = zero;
+          if (u >= i) {
+            l = t_times<SR>(xa[u - i], wl[u - i]);
+            for (int j = u - i + 1; j < u; ++j) l = t_times<SR>(l, wl[j]);
+          }
+          const float term = t_times<SR>(l, wb[u]);
+          if constexpr (SR == M_MAX) {
+            if (term > r) {
+              r = term;
+              wi = i;
+            }
+          } else {
+            r += term;
+          }
+        }
+      }
+      xb[u] = r;
+      if (SR == M_MAX) a.win[((long long)b * T + t) * S + u] = (unsigned char)wi;
+    }
+    __syncthreads();
+    for (int u = tid; u < S; u += nthr) xa[u] = xb[u];
+    __syncthreads();
+  }
+  const int nlb = a.nlab[b];
+  const int fin = (nlb >= 0 && nlb <= U) ? nlb : -1;
+  const float gv = a.gin ? a.gin[b] : 1.f;
+  if (tid == 0 && a.dist) a.dist[b] = fin >= 0 ? xa[fin] : zero;
+  if constexpr (SR == M_MAX) {
+    // ---- backward: one thread walks the decisions, staged in chunks
+    int q = fin < 0 ? -1 : (xa[fin] > -kInf ? fin : (fin == 0 ? 0 : -1));
+    const int F = max(1, kStrChunk / S);
+    for (int t1 = nf; t1 > 0; t1 -= F) {
+      const int t0 = max(0, t1 - F);
+      const unsigned char* src = a.win + ((long long)b * T + t0) * S;
+      for (int i = tid; i < (t1 - t0) * S; i += nthr) wc[i] = src[i];
+      __syncthreads();
+      if (tid == 0 && q >= 0) {
+        for (int t = t1 - 1; t >= t0; --t) {
+          const int wi = wc[(t - t0) * S + q];
+          int nm = 0;
+          auto mark = [&](int e) {
+            for (int m = 0; m < nm; ++m)
+              if (marks[2 * m] == e) {
+                ++marks[2 * m + 1];
+                return;
+              }
+            marks[2 * nm] = e;
+            marks[2 * nm + 1] = 1;
+            ++nm;
+          };
+          if (K == 0) {
+            mark(wi ? ctx[q - 1] + yn[q - 1] : ctx[q]);
+            q -= wi;
+          } else {
+            mark(ctx[q]);
+            for (int j = q - wi; j < q; ++j) mark(ctx[j] + yn[j]);
+            q -= wi;
+          }
+          unsigned char* dwf = dwbase + (long long)t * FR * (BF16 ? 2 : 4);
+          for (int m = 0; m < nm; ++m) stw<BF16>(dwf, marks[2 * m], (float)marks[2 * m + 1] * gv);
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+    // ---- backward: beta and the arc gradients frame by frame
+    for (int u = tid; u < S; u += nthr) xb[u] = u == fin ? gv : 0.f;
+    __syncthreads();
+    for (int t = nf - 1; t >= 0; --t) {
+      const unsigned char* wf = wbase + t * FR * (BF16 ? 2 : 4);
+      for (int u = tid; u < S; u += nthr) {
+        wb[u] = ldw<BF16>(wf, ctx[u]);
+        wl[u] = u < U ? ldw<BF16>(wf, ctx[u] + yn[u]) : 0.f;
+        xa[u] = a.alpha[((long long)b * T + t) * S + u];
+      }
+      __syncthreads();
+      if (K == 0) {
+        for (int u = tid; u < S; u += nthr) {
+          gb[u] = xa[u] * xb[u];
+          gl[u] = u < U ? xa[u] * xb[u + 1] : 0.f;
+          xc[u] = wb[u] * xb[u] + (u < U ? wl[u] * xb[u + 1] : 0.f);
+        }
+      } else {
+        for (int u = tid; u < S; u += nthr) {
+          float s = xa[u];
+          L[u] = xa[u];
+          for (int i = 1; i <= K; ++i) {
+            float l = 0.f;
+            if (u >= i) {
+              l = xa[u - i] * wl[u - i];
+              for (int j = u - i + 1; j < u; ++j) l *= wl[j];
+            }
+            L[i * S + u] = l;
+            s += l;
+          }
+          gb[u] = xb[u] * s;
+          gl[u] = 0.f;
+          d0[u] = xb[u] * wb[u];  // dL_K
+        }
+        __syncthreads();
+        for (int i = K - 1; i >= 0; --i) {
+          for (int u = tid; u < S; u += nthr) {
+            const float up = u < U ? d0[u + 1] : 0.f;
+            d1[u] = xb[u] * wb[u] + (u < U ? wl[u] * up : 0.f);
+            if (u < U) gl[u] += L[i * S + u] * up;
+          }
+          __syncthreads();
+          for (int u = tid; u < S; u += nthr) d0[u] = d1[u];
+          __syncthreads();
+        }
+        for (int u = tid; u < S; u += nthr) xc[u] = d0[u];
+      }
+      __syncthreads();
+      unsigned char* dwf = dwbase + (long long)t * FR * (BF16 ? 2 : 4);
+      for (int u = tid; u < S; u += nthr) {
+        if (hd[u] & 1) {
+          float s = 0.f;
+          for (int v = u; v >= 0; v = nxb[v]) s += gb[v];
+          stw<BF16>(dwf, ctx[u], s);
+        }
+        if (hd[u] & 2) {
+          float s = 0.f;
+          for (int v = u; v >= 0; v = nxl[v]) s += gl[v];
+          stw<BF16>(dwf, ctx[u] + yn[u], s);
+        }
+        xb[u] = xc[u];
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -2007,6 +2231,56 @@ int lt_table_den_backward(const lt_graph* g, const lt_table_problem* pb, int32_t
   const int blocks = (int)std::min<long long>(4096, (n + 255) / 256);
   hipLaunchKernelGGL(tab_to_bf16_kernel, dim3(blocks), dim3(256), 0, st, dwf, (unsigned short*)dW, n);
   return t_hip(hipGetLastError(), "bf16 conversion launch");
+}
+
+static size_t str_grad_bytes(const lt_table_problem* pb, int semiring) {
+  const long long BTS = (long long)pb->batch * pb->max_frames * (pb->max_labels + 1);
+  return (size_t)((semiring == M_MAX ? BTS : 4 * BTS) + 255) & ~(size_t)255;
+}
+
+int lt_table_num_backward_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
+                                          int32_t semiring, size_t* bytes) {
+  if (int rc = t_check(g, pb)) return rc;
+  if (semiring != M_MAX && semiring != M_REAL)
+    return t_fail(LT_EUNSUPPORTED, "lt_table_num_backward: MaxTropical or Real (Log: "
+                                   "lt_table_loss_grad with local_norm)");
+  if (bytes) *bytes = str_grad_bytes(pb, semiring);
+  return LT_OK;
+}
+
+int lt_table_num_backward(const lt_graph* g, const lt_table_problem* pb, int32_t semiring,
+                          const void* W, const int32_t* num_frames, const int32_t* labels,
+                          const int32_t* num_labels, const float* grad, float* num, void* dW,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  size_t need = 0;
+  if (int rc = lt_table_num_backward_workspace_bytes(g, pb, semiring, &need)) return rc;
+  if (pb->batch == 0) return LT_OK;
+  if ((!W && pb->max_frames > 0) || !num_frames || !num_labels || (!dW && pb->max_frames > 0) ||
+      (pb->max_labels > 0 && !labels))
+    return t_fail(LT_EINVAL, "null pointer");
+  if (need && (!workspace || workspace_bytes < need)) return t_fail(LT_EINVAL, "workspace too small");
+  const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
+  hipStream_t st = (hipStream_t)stream;
+  TArgs a = t_args(g, pb, W, num_frames);
+  a.labels = labels;
+  a.nlab = num_labels;
+  a.gin = grad;
+  a.dist = num;
+  a.dW = (float*)dW;
+  const int S = a.U + 1, K = a.K;
+  if (semiring == M_MAX) a.win = (unsigned char*)workspace;
+  else a.alpha = (float*)workspace;
+  const long long n = (long long)a.B * a.T * a.C * a.R;
+  if (n > 0)
+    if (int rc = t_hip(hipMemsetAsync(dW, 0, (size_t)n * (bf16 ? 2 : 4), st), "memset")) return rc;
+  const long long lds = 4LL * (5 * S + (9 + K + 1 + 2) * S + 4 + ((K + 1 + 3) & ~3) * 2) +
+                        (semiring == M_MAX ? std::max(kStrChunk, S) : 0);
+  if (lds > kTabLds) return t_fail(LT_EUNSUPPORTED, "string gradient: labels exceed LDS");
+  if (semiring == M_MAX)
+    return bf16 ? t_launch(tab_str_grad_kernel<true, M_MAX>, a.B, (int)lds, st, a)
+                : t_launch(tab_str_grad_kernel<false, M_MAX>, a.B, (int)lds, st, a);
+  return bf16 ? t_launch(tab_str_grad_kernel<true, M_REAL>, a.B, (int)lds, st, a)
+              : t_launch(tab_str_grad_kernel<false, M_REAL>, a.B, (int)lds, st, a);
 }
 
 int lt_table_viterbi_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,

@@ -13,7 +13,8 @@ weights once through the ``WeightFn`` plugin as a contiguous
                      lt_table_den_backward (Real)
   _forward_backward -> lt_den_forward + lt_den_backward
   _backward       -> lt_den_backward marginals, streamed to the callback
-  _string_forward -> lt_num_forward
+  _string_forward -> lt_num_forward; autograd: lt_loss_backward (Log) /
+                     lt_table_num_backward (MaxTropical, Real)
   shortest_path   -> lt_viterbi
 
 The device of the arc weights picks the implementation, as in the
@@ -238,22 +239,30 @@ class _TableNumFn(torch.autograd.Function):
 
   @staticmethod
   def backward(ctx, g):
-    if ctx.sid != _native.SEMIRING_LOG:
-      raise NotImplementedError('string-distance gradients are supported for Log only')
     W, nf, labels, nl = ctx.saved_tensors
+    if ctx.sid != _native.SEMIRING_LOG:
+      # MaxTropical: the best string-aligned path's arcs; Real: alpha * beta'
+      # (lt_table_num_backward, the reference's autograd through
+      # semirings.py:143-173 / 354-401)
+      _, dW = _native.table_num_backward(ctx.graph, W, nf, labels, nl, ctx.sid, g.float())
+      return dW, None, None, None, None, None
     _, _, _, dW = _native.table_loss_grad(ctx.graph, W, nf, labels, nl, True)
     # an unreachable string has num = -inf and dW = 0 already
     return dW * (-g).to(dW.dtype)[:, None, None, None], None, None, None, None, None
 
 
 class _NumFn(torch.autograd.Function):
-  """Numerator (string) shortest distance; Log gradient = string marginals."""
+  """Numerator (string) shortest distance; gradient = the string marginals
+  (Log), the best string-aligned path's arcs (MaxTropical) or alpha * beta'
+  (Real)."""
 
   @staticmethod
-  def forward(ctx, W, nf, labels, nl, V, n, sid):
-    num, an = _native.num_forward(W, nf, labels, nl, V, n, sid, want_alpha=True)
+  def forward(ctx, W, nf, labels, nl, V, n, sid, graph=None):
+    num, an = _native.num_forward(W, nf, labels, nl, V, n, sid,
+                                  want_alpha=sid == _native.SEMIRING_LOG)
     ctx.save_for_backward(W, nf, labels, nl, num, an)
     ctx.cfg = (V, n, sid)
+    ctx.graph = graph
     return num
 
   @staticmethod
@@ -261,11 +270,16 @@ class _NumFn(torch.autograd.Function):
     W, nf, labels, nl, num, an = ctx.saved_tensors
     V, n, sid = ctx.cfg
     if sid != _native.SEMIRING_LOG:
-      raise NotImplementedError('string-distance gradients are supported for Log only')
+      # the general string-gradient kernel on FullNGram.next_state_table()
+      # (the same state numbering): lt_table_num_backward
+      if ctx.graph is None:
+        raise NotImplementedError('MaxTropical / Real string gradients need the lattice graph')
+      _, dW = _native.table_num_backward(ctx.graph, W, nf, labels, nl, sid, g.float())
+      return dW, None, None, None, None, None, None, None
     # local-norm loss backward gives -grad * num marginals; feed -g.
     dW = _native.loss_backward(W, nf, labels, nl, None, num, None, an,
                                (-g).float().contiguous(), V, n, True)
-    return dW, None, None, None, None, None, None
+    return dW, None, None, None, None, None, None, None
 
 
 class RecognitionLattice(nn.Module, Generic[T]):
@@ -457,7 +471,8 @@ class RecognitionLattice(nn.Module, Generic[T]):
     elif self._table_path():
       num = _TableNumFn.apply(W, nf, lab.contiguous(), nl, self._graph(W.device), sid)
     else:
-      num = _NumFn.apply(W, nf, lab.contiguous(), nl, V, n, sid)
+      graph = self._graph(W.device) if sid != _native.SEMIRING_LOG else None
+      num = _NumFn.apply(W, nf, lab.contiguous(), nl, V, n, sid, graph)
     return self._home(num.reshape(batch_dims), frames)
 
   def _forward(self, cache: T, frames: torch.Tensor, num_frames: torch.Tensor,

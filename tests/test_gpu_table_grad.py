@@ -5,10 +5,11 @@
   lattices: Log -> the arc marginals (the reference's FrameLabelDependent
   fixtures' den_grad, or golden_cases.table_den_marginals from the pinned
   table oracle), element by element within golden_cases.marginal_scale;
-  MaxTropical -> the best path's arcs (their labels = the table Viterbi's,
-  their weights re-sum to the distance); Real -> alpha * beta' against a
-  float64 PyTorch autograd of the same Real recursion (cpu.py, plain
-  arithmetic as the reference's Real semiring, semirings.py:143-173).
+  MaxTropical -> the best path's arcs, element by element against the
+  pinned oracle (table_oracle.c tab_dist_grad) plus properties (labels = the
+  table Viterbi's, weights re-sum to the distance); Real -> alpha * beta'
+  against the pinned oracle (both pinned to the reference's own autograd,
+  tests/golden/grads_*.npz, tests/test_oracle_grads.py).
 * ``_string_forward`` (Log) on the table path: d num / dW against the table
   oracle's string-only loss gradient.
 * ``_backward`` with a callback on a FrameLabelDependent lattice
@@ -21,7 +22,6 @@ import pytest
 import torch
 
 import last_torch_amd as lt
-from last_torch_amd import cpu
 from last_torch_amd import _native as nat
 from golden_cases import (FLD_CASES, LATTICE_CASES, assert_grad_marginal_close, assert_loss_close,
                           load, load_fld, table_den_marginals)
@@ -50,13 +50,12 @@ def _fld(c):
           lt.alignments.FrameLabelDependent(max_expansions=c['K']))
 
 
-def _real_ref(W, nf, context, alignment):
-  """d dist / dW of the Real distance in float64 (cpu.py autograd)."""
-  Wd = torch.tensor(np.asarray(W, np.float64), requires_grad=True)
-  dist, _ = cpu.den_forward(Wd, torch.as_tensor(np.asarray(nf)).long(), context, alignment,
-                            lt.semirings.Real)
-  (g,) = torch.autograd.grad(dist.sum(), Wd)
-  return dist.detach().numpy(), g.numpy()
+def _real_ref(W, nf, V, n, K):
+  """(dist, d dist / dW) of the Real distance from the pinned oracle
+  (table_oracle.c tab_dist_grad, double; checked against the reference's
+  own Real autograd by tests/test_oracle_grads.py)."""
+  orc = _orc()
+  return orc.tab_dist_grad(orc.full_ngram_table(V, n), W, nf, K, orc.REAL)
 
 
 def _assert_real_grad(got, ref):
@@ -103,10 +102,15 @@ def test_fld_forward_gradients(cuda, case):
   nlex = (labels > 0).sum(-1)
   lexsum = g[..., 1:].sum((-2, -1)) / w.cpu().numpy()[:, None]
   np.testing.assert_allclose(lexsum, nlex * live, atol=1e-6)
-  # Real: alpha * beta' against float64 autograd
+  # and element by element: the oracle's first-maximum path, scaled by w
+  orc = _orc()
+  _, rg = orc.tab_dist_grad(orc.full_ngram_table(c['V'], c['n']), c['W'], c['num_frames'], K,
+                            orc.MAX, grad=w.cpu().numpy())
+  np.testing.assert_array_equal(g, rg)
+  # Real: alpha * beta' against the pinned oracle
   table.grad = None
   d, _ = lat._forward(None, frames, nf, lt.semirings.Real)
-  rd, rg = _real_ref(c['W'], c['num_frames'], ctx, align)
+  rd, rg = _real_ref(c['W'], c['num_frames'], c['V'], c['n'], K)
   np.testing.assert_allclose(d.detach().cpu().numpy(), rd,
                              rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(rd).max())))
   d.sum().backward()
@@ -125,7 +129,7 @@ def test_real_semiring_gradient_full_ngram(cuda, case):
   lat = _lattice(ctx, align, table)
   nf = torch.tensor(c['num_frames'])
   d, _ = lat._forward(None, _frames(B, T, cuda), nf, lt.semirings.Real)
-  rd, rg = _real_ref(c['W'], c['num_frames'], ctx, align)
+  rd, rg = _real_ref(c['W'], c['num_frames'], c['V'], c['n'], 0)
   np.testing.assert_allclose(d.detach().cpu().numpy(), rd,
                              rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(rd).max())))
   g = torch.linspace(-1.0, 1.5, B, device=cuda)

@@ -37,6 +37,7 @@ def _load(name):
 def assert_real_grad_close(got, ref):
   """rtol 1e-4 plus 1e-5 of each utterance's largest |element|."""
   got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+  assert np.isfinite(ref).all() and np.isfinite(got).all()
   scale = np.abs(ref).reshape(ref.shape[0], -1).max(-1)
   tol = 1e-4 * np.abs(ref) + 1e-5 * scale.reshape(-1, *([1] * (ref.ndim - 1))) + 1e-30
   bad = np.abs(got - ref) > tol
