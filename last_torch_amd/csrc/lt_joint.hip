@@ -71,7 +71,7 @@ template <int NW>
 constexpr int jf_threads() { return 64 * NW; }
 
 struct JfLds {
-  int wo, A, Bt, AN, BN, aoff, hd, gt, dpc, total;
+  int wo, A, Bt, AN, BN, aoff, hd, gt, dpc, ec, ef, total;
 };
 JfLds jf_lds(int C, int R, int H, int NP, bool sp) {
   auto al16 = [](long long x) { return (int)((x + 15) & ~15LL); };
@@ -87,8 +87,30 @@ JfLds jf_lds(int C, int R, int H, int NP, bool sp) {
   l.hd = o; o += al16(4LL * C * R);
   l.gt = o; o += al16(4LL * 2 * 32 * kJfGS);
   l.dpc = o; o += al16(4LL * C * H);
+  l.ec = o; o += al16(4LL * C * H);   // e^{2 Pc} (or Pc on the direct path)
+  l.ef = o; o += al16(4LL * 32 * H);  // the block's e^{2 Pf} rows (or Pf)
   l.total = o;
   return l;
+}
+
+// n 4-byte words global -> LDS with 8 loads in flight per thread (a plain
+// strided copy loop waits one memory latency per trip)
+template <typename Tw>
+LT_DEVINL void stage_words(Tw* dst, const Tw* src, int n, int tid, int nthr) {
+  constexpr int U = 8;
+  for (int e0 = tid; e0 < n; e0 += U * nthr) {
+    Tw v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * nthr;
+      if (e < n) v[u] = src[e];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * nthr;
+      if (e < n) dst[e] = v[u];
+    }
+  }
 }
 
 // One workgroup per (utterance b, block of 32 frames); NW = H / 32 waves,
@@ -97,9 +119,13 @@ JfLds jf_lds(int C, int R, int H, int NP, bool sp) {
 // tile of state c and its marginals, then every wave runs the backward of
 // that tile -- the split-bf16 products and K orders of joint_backward_kernel.
 template <int NW, bool SP>
-__global__ __launch_bounds__(64 * NW) void jf_marg_kernel(const JFArgs a, const JfLds l) {
+__global__ __launch_bounds__(64 * (NW < 2 ? 2 : NW), 2) void jf_marg_kernel(const JFArgs a,
+                                                                          const JfLds l) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  constexpr int KB = kJfKB, GS = kJfGS, nthr = 64 * NW;
+  // NW backward waves own the hidden columns; at least two waves, so one
+  // forms the next tile's W and marginals while another runs a backward
+  constexpr int NT = NW < 2 ? 2 : NW;
+  constexpr int KB = kJfKB, GS = kJfGS, nthr = 64 * NT;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int half = lane >> 5, col = lane & 31;
@@ -126,7 +152,7 @@ __global__ __launch_bounds__(64 * NW) void jf_marg_kernel(const JFArgs a, const 
   // an unreachable string (num = -inf) or a dead lattice: no gradient
   // (lt_loss_backward's rule)
   if (!__builtin_isfinite(nm) || !__builtin_isfinite(lz)) gb = 0.f;
-  const int hl = wave * 32 + col;  // this lane's hidden column
+  const int hl = min(wave, NW - 1) * 32 + col;  // this lane's hidden column (backward waves)
   float* part = a.part + (long long)blockIdx.x * jf_stride(C, R, H);
   if (Fl == 0 || gb == 0.f) {  // padding frames / no gradient: zeros out
     for (int e = tid; e < 32 * H; e += nthr) {
@@ -138,26 +164,40 @@ __global__ __launch_bounds__(64 * NW) void jf_marg_kernel(const JFArgs a, const 
   }
   // ---- staging: Wo bf16, the checkpoint rows, the string arc table
   stage_wo<SP>(a.wo, wol, R, H, HP, WL, tid, nthr);
-  for (int e = tid; e < Fl * C; e += nthr) {
-    A[e] = a.alpha[row0 * C + e];
-    Bt[e] = a.beta[row0 * C + e];
-  }
-  for (int e = tid; e < Fl * NP; e += nthr) {
-    AN[e] = a.alpha_num[row0 * NP + e];
-    BN[e] = a.beta_num[row0 * NP + e];
-  }
-  const int* arcsrc = a.arcs + (long long)b * 2 * NK;
-  for (int e = tid; e < 2 * NK; e += nthr) aoff[e] = arcsrc[e];
+  stage_words(A, a.alpha + row0 * C, Fl * C, tid, nthr);
+  stage_words(Bt, a.beta + row0 * C, Fl * C, tid, nthr);
+  stage_words(AN, a.alpha_num + row0 * NP, Fl * NP, tid, nthr);
+  stage_words(BN, a.beta_num + row0 * NP, Fl * NP, tid, nthr);
+  stage_words(aoff, a.arcs + (long long)b * 2 * NK, 2 * NK, tid, nthr);
   for (int e = tid; e < C * R; e += nthr) hd[e] = -1;
   for (int e = tid; e < 2 * 32 * GS; e += nthr) gt[e] = 0.f;  // columns past R stay 0
   for (int e = tid; e < C * H; e += nthr) dpc[e] = 0.f;
+  // the forward tiles' operands in LDS: e^{2 Pc} (Pc on the direct path)
+  // and this block's rows of e^{2 Pf} (Pf for a block over kSplitMax)
+  const bool csplit = *a.cbig == 0;
+  float* ecl = (float*)(lds + l.ec);
+  float* efl = (float*)(lds + l.ef);
+  {
+    stage_words(ecl, csplit ? a.ec : a.pc, C * H, tid, nthr);
+    // rows of one 32-row block of the flattened rows share a source: at most
+    // two blocks meet in this one
+    const long long fa = row0, fb = row0 + Fh - 1;
+    const bool sa = csplit && a.fbig[fa >> 5] == 0, sb = csplit && a.fbig[fb >> 5] == 0;
+    if (sa == sb) {
+      stage_words(efl, (sa ? a.ef : a.pf) + row0 * H, Fh * H, tid, nthr);
+    } else {
+      for (int e = tid; e < Fh * H; e += nthr) {
+        const long long f = row0 + e / H;
+        efl[e] = ((f >> 5) == (fa >> 5) ? (sa ? a.ef : a.pf) : (sb ? a.ef : a.pf))[row0 * H + e];
+      }
+    }
+  }
   __syncthreads();
   for (int k = tid; k < NK; k += nthr)
     if ((alink[k] >> 30) && aoff[k] >= 0) hd[aoff[k]] = k;  // one head per element
   __syncthreads();
 
   // ---- the forward tiles' lane state: row m = col (frame t0 + m), columns y0 / y1
-  const bool csplit = *a.cbig == 0;
   const int y0 = col, y1 = 32 + col;
   const bool v1 = y1 < R;
   const float b0 = a.bias[y0], b1 = v1 ? a.bias[y1] : 0.f;
@@ -165,7 +205,10 @@ __global__ __launch_bounds__(64 * NW) void jf_marg_kernel(const JFArgs a, const 
   const unsigned short* w1 = wol + (v1 ? y1 : R - 1) * HP + 8 * half;
   const long long fr = row0 + min(col, Fh - 1);
   const bool split = csplit && a.fbig[fr >> 5] == 0;
-  const float* pfr = (split ? a.ef : a.pf) + fr * H + 8 * half;
+  const float* pfr = efl + col * H + 8 * half;
+  // a block mixing split rows with a direct one (|Pf| > kSplitMax in another
+  // 32-row block of the flattened rows) reads Pc from global on the direct rows
+  const bool dir_mix = !split && csplit;
   // ---- the backward's lane state (joint_backward_kernel's): Wo as the B
   // operand of gw, this lane's 16 frames' Pf, the d_Pf / d_Wo accumulators
   bf16x8 woh[KB], wolo[KB];
@@ -191,37 +234,70 @@ __global__ __launch_bounds__(64 * NW) void jf_marg_kernel(const JFArgs a, const 
 
   for (int c = 0, buf = 0; c < C; ++c, buf ^= 1) {
     float* g = gt + buf * 32 * GS;
-    if (wave == c % NW) {
+    if (wave == c % NT) {
       // W tile of state c: rows = the block's frames, columns = labels
       f32x16 acc0 = {}, acc1 = {};
-      const float* pcr = (split ? a.ec : a.pc) + (long long)c * H + 8 * half;
+      const float* pcr = (dir_mix ? a.pc : ecl) + (long long)c * H + 8 * half;
       joint_tile<SP, true>(split, pcr, pfr, H, w0, w1, w0 + WL, w1 + WL, acc0, acc1);
       // den - num marginals (marg_tile's arithmetic): den = gb e^{alpha +
       // w + beta' - log_z}, num = gb sum over the string arcs on (c, y) of
       // e^{alpha^n + w + beta^n' - num}, chained in ascending arc order
-      auto marg = [&](int m, int y, float w) {
-        const int q = y == 0 ? c : y;  // next(c, y) of the bigram (contexts.py:190-205)
-        const float den = gb * lt_exp(A[m * C + c] + w + Bt[m * C + q] - lz);
-        float sacc = 0.f;
-        for (int kk = hd[c * R + y]; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
-          const int u = kk >> 1;
-          const float bn = BN[m * NP + ((kk & 1) ? u + 1 : u)];
-          sacc += lt_exp(AN[m * NP + u] + w + bn - nm);
-        }
-        return den - gb * sacc;
-      };
+      // W into the tile (the accumulators die here), then den - num in place,
+      // four rows at a time with their operands gathered first (independent
+      // LDS reads in flight together): den = gb e^{alpha + w + beta' - log_z},
+      // and on the rare elements with string arcs num = gb sum e^{alpha^n + w
+      // + beta^n' - num} in ascending arc order (marg_tile's arithmetic, no
+      // contraction: it subtracts the chains' sum stored apart)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
-        const bool live = m < Fl;
-        g[m * GS + y0] = live ? marg(m, y0, acc0[i] + b0) : 0.f;
-        if (v1) g[m * GS + y1] = live ? marg(m, y1, acc1[i] + b1) : 0.f;
+        g[m * GS + y0] = acc0[i] + b0;
+        if (v1) g[m * GS + y1] = acc1[i] + b1;
       }
+      auto column = [&](int y) {
+        const int q = y == 0 ? c : y;  // next(c, y) of the bigram (contexts.py:190-205)
+        const int k0 = hd[c * R + y];
+#pragma unroll 1
+        for (int i0 = 0; i0 < 16; i0 += 4) {
+          float av[4], bv[4], wv[4], d[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int m = ((i0 + j) & 3) + 8 * ((i0 + j) >> 2) + 4 * half;
+            av[j] = A[m * C + c];
+            bv[j] = Bt[m * C + q];
+            wv[j] = g[m * GS + y];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int m = ((i0 + j) & 3) + 8 * ((i0 + j) >> 2) + 4 * half;
+            d[j] = m < Fl ? gb * lt_exp(av[j] + wv[j] + bv[j] - lz) : 0.f;
+            if (k0 >= 0 && m < Fl) {
+              float sacc = 0.f;
+              for (int kk = k0; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
+                const int u = kk >> 1;
+                const float bn = BN[m * NP + ((kk & 1) ? u + 1 : u)];
+                sacc += lt_exp(AN[m * NP + u] + wv[j] + bn - nm);
+              }
+              d[j] = __fsub_rn(d[j], __fmul_rn(gb, sacc));
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            g[(((i0 + j) & 3) + 8 * ((i0 + j) >> 2) + 4 * half) * GS + y] = d[j];
+        }
+      };
+      column(y0);
+      if (v1) column(y1);
     }
     __syncthreads();  // one barrier a tile: the other buffer is written next
-    // ---- backward of tile c (every wave, its own hidden columns)
-    if (tid < R)
-      for (int m = 0; m < 32; ++m) dbias += g[m * GS + tid];
+    if (wave >= NW) continue;  // a forward-only wave
+    // ---- backward of tile c (the NW backward waves, each its hidden columns)
+    if (tid < R) {  // eight partial sums: the loads in flight together
+      float p8[8] = {};
+#pragma unroll
+      for (int m = 0; m < 32; ++m) p8[m & 7] += g[m * GS + tid];
+      dbias += ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
+    }
     const float pcv = a.pc[(long long)c * H + hl];
     f32x16 gw = {};
 #pragma unroll
@@ -265,16 +341,18 @@ __global__ __launch_bounds__(64 * NW) void jf_marg_kernel(const JFArgs a, const 
     if (half == 0) dpc[c * H + hl] += csum;  // this wave owns column hl
   }
   // ---- outputs: d_Pf rows (the block owns its frames), the partials
+  if (wave < NW) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
-    if (m < Fh) a.dpf[(row0 + m) * H + hl] = dpf[i];
-  }
+    for (int i = 0; i < 16; ++i) {
+      const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
+      if (m < Fh) a.dpf[(row0 + m) * H + hl] = dpf[i];
+    }
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int r = (i & 3) + 8 * (i >> 2) + 4 * half;
-    if (r < R) part[(long long)(C + r) * H + hl] = dwo0[i];
-    if (r + 32 < R) part[(long long)(C + r + 32) * H + hl] = dwo1[i];
+    for (int i = 0; i < 16; ++i) {
+      const int r = (i & 3) + 8 * (i >> 2) + 4 * half;
+      if (r < R) part[(long long)(C + r) * H + hl] = dwo0[i];
+      if (r + 32 < R) part[(long long)(C + r + 32) * H + hl] = dwo1[i];
+    }
   }
   if (tid < R) part[(long long)(C + R) * H + tid] = dbias;
   __syncthreads();
@@ -364,10 +442,11 @@ int jf_launch_marg(const JFArgs& a, const JfLds& l, bool sp, hipStream_t st) {
     if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   }
   const int grid = a.B * a.nblk;
+  const int threads = 64 * (NW < 2 ? 2 : NW);
   if (sp)
-    hipLaunchKernelGGL((jf_marg_kernel<NW, true>), dim3(grid), dim3(64 * NW), l.total, st, a, l);
+    hipLaunchKernelGGL((jf_marg_kernel<NW, true>), dim3(grid), dim3(threads), l.total, st, a, l);
   else
-    hipLaunchKernelGGL((jf_marg_kernel<NW, false>), dim3(grid), dim3(64 * NW), l.total, st, a, l);
+    hipLaunchKernelGGL((jf_marg_kernel<NW, false>), dim3(grid), dim3(threads), l.total, st, a, l);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? LT_OK : lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
 }

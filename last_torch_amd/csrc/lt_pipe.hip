@@ -108,6 +108,7 @@ struct PArgs {
   const float* jwo;    // [R, H] Wo (blank row first)
   const float* jbias;  // [R]
   int off_wo, off_ec;  // LDS: Wo bf16 (hi, lo), e^{2 Pc} fp32 [C][H]
+  int off_jf;          // LDS: per producer helper two 1 KB slots of e^{2 Pf} rows
 };
 constexpr int kMidBand = 32;    // frames next to the middle zeroed before the granules flow
 // floats per slot of the den (hring) and numerator (nring) row rings
@@ -131,8 +132,8 @@ constexpr int kHS = 64;
 #define LT_PIPE_MID 2
 #endif
 constexpr int kPipeMidWaves = LT_PIPE_MID;  // marginal waves per workgroup in mid mode
-enum { CTL_TAG = 0, CTL_DEN = kPipeMaxSlots, CTL_NUM, CTL_ABORT, CTL_FIN0, CTL_FIN1, CTL_MRG,
-       CTL_N = CTL_MRG + kPipeMidWaves };
+enum { CTL_TAG = 0, CTL_DEN = kPipeMaxSlots, CTL_NUM, CTL_ABORT, CTL_FIN0, CTL_FIN1, CTL_JBIG,
+       CTL_MRG, CTL_N = CTL_MRG + kPipeMidWaves };
 
 typedef __attribute__((address_space(3))) volatile int lds_vint;
 typedef __attribute__((address_space(3))) float lds_float;
@@ -818,8 +819,9 @@ LT_DEVINL void helper_pipe(const PArgs& a, unsigned char* lds, int b, int nf, in
 // into the slot as helper_pipe leaves them. The split (e^{2 Pc} e^{2 Pf}) or
 // direct tanh is chosen per 32-row block of Pf as lt_joint_weights does. W
 // never exists in HBM; the helpers work in the shadow of the frame chain.
-template <bool REV, bool SP>
+template <bool REV, bool SP, int J>
 LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, int hw, int lane) {
+  constexpr int JP = J >= 4 ? (J + 3) / 4 * 4 : J;  // launch_pipe's padded part length
   lds_vint* ctl = (lds_vint*)(as3(lds) + a.off_ctl);
   const int R = a.R, C = a.C, H = a.jH, HP = H + 8;
   const int WL = (R * HP + 7) & ~7;
@@ -834,64 +836,92 @@ LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, in
   const unsigned short* w1 = wo + (v1 ? y1 : R - 1) * HP + hk;
   const unsigned short* w0l = w0 + WL;
   const unsigned short* w1l = w1 + WL;
-  // E's byte offset in a slot for element (p, y) (helper_pipe's layout)
+  // the two row tiles' e^{2 Pc} rows (states r and 32 + r; rows past C
+  // repeat the last state and are never stored)
+  const float* ec0 = ecl + min(r, C - 1) * H + hk;
+  const float* ec1 = ecl + min(32 + r, C - 1) * H + hk;
+  // E's byte offset in a slot for element (p, y) (helper_pipe's layout):
+  // y is fixed per lane and p an unrolled constant plus 4 half, so with J a
+  // compile-time constant no element pays a division
   auto eoff = [&](int p, int y) {
     if (y == 0) return a.soff_eb + 4 * p;
     const int row = REV ? p : y - 1, kk = REV ? y - 1 : p;
-    return a.soff_e + 4 * (row * a.rowE + (kk / a.J) * a.JP + (kk % a.J));
+    return a.soff_e + 4 * (row * a.rowE + (kk / J) * JP + (kk % J));
+  };
+  // e^{2 Pf} rows come through a two-slot LDS ring of this helper, one
+  // LDS-DMA instruction a frame issued a step ahead, so no frame waits on
+  // its own global load
+  unsigned char* ring = lds + a.off_jf + hw * 2048;
+  const unsigned ring_a = lds_base_addr(ring);
+  auto row_of = [&](int i) {
+    const int t = REV ? nf - 1 - i : i;
+    return (long long)b * a.T + t;
+  };
+  auto issue = [&](int i, int sl) {
+    const long long f = row_of(min(i, nf - 1));
+    glds16(a.jef + f * H + 4 * min(lane, H / 4 - 1), ring_a + 1024u * sl);
   };
   int seen_den = 0, seen_num = 0;
-  int slot = hw;
-  for (int i = hw; i < nf; i += a.NH) {
+  int slot = hw, rs = 0;
+  // the prologue's per-utterance flag: no 32-row block of this utterance's
+  // Pf rows exceeds kSplitMax (the common case: no per-frame flag read, whose
+  // scalar load would share lgkmcnt with every LDS wait of the frame)
+  const bool utt_split = *(const lds_vint*)(as3(lds) + a.off_ctl + 4 * CTL_JBIG) == 0;
+  if (hw < nf) issue(hw, 0);
+  for (int i = hw; i < nf; i += a.NH, rs ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this frame's row is in the ring
+    issue(i + a.NH, rs ^ 1);                             // the next one in flight
+    const long long f = row_of(i);
+    const bool split = csplit && (utt_split || a.jfbig[f >> 5] == 0);
+    const float* efr = (const float*)(ring + 1024 * rs) + hk;
     const int need = i - a.K + 1;  // the slot's previous frame (step i - K) must be consumed
     if (need > 0) {
       if (seen_den < need) {
-        if (!wait_ge(ctl + CTL_DEN, need, ctl + CTL_ABORT, a.err)) return;
+        if (!wait_ge(ctl + CTL_DEN, need, ctl + CTL_ABORT, a.err)) break;
         seen_den = ctl[CTL_DEN];
       }
       if (seen_num < need) {
-        if (!wait_ge(ctl + CTL_NUM, need, ctl + CTL_ABORT, a.err)) return;
+        if (!wait_ge(ctl + CTL_NUM, need, ctl + CTL_ABORT, a.err)) break;
         seen_num = ctl[CTL_NUM];
       }
     }
-    const int t = REV ? nf - 1 - i : i;
-    const long long f = (long long)b * a.T + t;
-    const bool split = csplit && a.jfbig[f >> 5] == 0;
-    const float* pfr = (split ? a.jef : a.jpf) + f * H + hk;
-    f32x16 acc[2][2] = {};
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const int p = min(32 * rt + r, C - 1);  // rows past C repeat the last state, never stored
-      const float* pcr = split ? ecl + p * H + hk : a.jpc + p * H + hk;
-      joint_tile<SP, true>(split, pcr, pfr, H, w0, w1, w0l, w1l, acc[rt][0], acc[rt][1]);
-    }
-    // W = acc + bias (the producer's own rounding), the frame max over it
+    unsigned char* sb = lds + a.off_ring + slot * a.slot_bytes;
+    lds_float* Wr = (lds_float*)as3(sb);
+    // one row tile at a time (one accumulator pair live): W = acc + bias
+    // (the producer's own rounding) straight into the slot's raw W, the
+    // frame max on the side; E = exp(W - c) once the max is known
     float mx = -kInf;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < 2; ++rt) {
+      f32x16 acc0 = {}, acc1 = {};
+      if (split) {
+        joint_tile<SP, true>(true, rt ? ec1 : ec0, efr, H, w0, w1, w0l, w1l, acc0, acc1);
+      } else {  // a projection beyond kSplitMax: the direct tanh from Pc + Pf (rare)
+        joint_tile<SP, true>(false, a.jpc + min(32 * rt + r, C - 1) * H + hk, a.jpf + f * H + hk,
+                             H, w0, w1, w0l, w1l, acc0, acc1);
+      }
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int p = 32 * rt + (k & 3) + 8 * (k >> 2) + 4 * half;
-        acc[rt][0][k] += b0;
-        acc[rt][1][k] += b1;
-        if (p < C) mx = fmaxf(mx, v1 ? fmaxf(acc[rt][0][k], acc[rt][1][k]) : acc[rt][0][k]);
+        const float x0 = acc0[k] + b0, x1 = acc1[k] + b1;
+        if (p < C) {
+          Wr[p * R + y0] = x0;
+          if (v1) Wr[p * R + y1] = x1;
+          mx = fmaxf(mx, v1 ? fmaxf(x0, x1) : x0);
+        }
       }
+    }
     const float c = safe(wave_max(mx));
     const float cl = c * kLog2e;
-    unsigned char* sb = lds + a.off_ring + slot * a.slot_bytes;
-    lds_float* Wr = (lds_float*)as3(sb);
-#pragma unroll
+    // (rolled: 64 unrolled offsets would each hold a register)
+#pragma unroll 1
     for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
+#pragma unroll 2
       for (int k = 0; k < 16; ++k) {
         const int p = 32 * rt + (k & 3) + 8 * (k >> 2) + 4 * half;
         if (p < C) {
-          Wr[p * R + y0] = acc[rt][0][k];
-          *(lds_float*)(as3(sb) + eoff(p, y0)) = lt_exp_off(acc[rt][0][k], cl);
-          if (v1) {
-            Wr[p * R + y1] = acc[rt][1][k];
-            *(lds_float*)(as3(sb) + eoff(p, y1)) = lt_exp_off(acc[rt][1][k], cl);
-          }
+          *(lds_float*)(as3(sb) + eoff(p, y0)) = lt_exp_off(Wr[p * R + y0], cl);
+          if (v1) *(lds_float*)(as3(sb) + eoff(p, y1)) = lt_exp_off(Wr[p * R + y1], cl);
         }
       }
     if (lane == 0) {
@@ -901,6 +931,7 @@ LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, in
     slot += a.NH;
     if (slot >= a.K) slot -= a.K;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into LDS outlives the wave
 }
 
 // ---- in-workgroup marginals (mid mode) --------------------------------------
@@ -1221,6 +1252,13 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void
     for (int k = tid; k < a.C * H; k += nthr) ec[k] = a.jec[k];
   }
   __syncthreads();
+  if constexpr (PROD != 0) {
+    // any 32-row block of this utterance's Pf rows over kSplitMax (ctl was
+    // zeroed above, before the barrier)
+    const long long r0 = (long long)b * a.T;
+    for (long long k = (r0 >> 5) + tid; k <= ((r0 + a.T - 1) >> 5); k += nthr)
+      if (a.jfbig[k]) ctl[CTL_JBIG] = 1;
+  }
   if (tid == 0) {
     // walk_states (contexts.py:109-146) with the lattices.py:314-338 label rules
     const int R = a.R;
@@ -1278,8 +1316,8 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void
   } else if (wave - 2 < a.NH) {
     constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
     if constexpr (PROD != 0) {
-      if (rev) helper_prod<true, PROD == 1>(a, lds, b, nf, wave - 2, lane);
-      else helper_prod<false, PROD == 1>(a, lds, b, nf, wave - 2, lane);
+      if (rev) helper_prod<true, PROD == 1, J>(a, lds, b, nf, wave - 2, lane);
+      else helper_prod<false, PROD == 1, J>(a, lds, b, nf, wave - 2, lane);
     } else {
       if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, wave - 2, lane);
       else helper_pipe<BF16, NL, false>(a, lds, b, nf, wave - 2, lane);
@@ -1500,6 +1538,8 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
     const int WL = (R * (jo->H + 8) + 7) & ~7;
     a.off_wo = off; off += al16((jo->prod == 1 ? 4LL : 2LL) * WL);
     a.off_ec = off; off += al16(4LL * C * jo->H);
+    a.off_jf = off; off += kPipeMaxHelpers * 2048;
+    if (jo->H > 256) return set_error(LT_EUNSUPPORTED, "pipe producer helpers: H <= 256");
   }
   int so = 0;
   const int NLc = a.J == 17 ? 18 : (a.J == 5 ? 5 : (a.J == 2 ? 2 : 1));

@@ -406,6 +406,9 @@ class RecognitionLattice(nn.Module, Generic[T]):
     if tuple(num_labels.shape) != batch_dims:
       raise ValueError('num_labels and num_frames have different batch_dims: '
                        f'{tuple(num_labels.shape)} vs {batch_dims}')
+    fused = self._fused_joint_loss(cache, frames, num_frames, labels, num_labels)
+    if fused is not None:
+      return self._home(fused.reshape(batch_dims), frames)
     W, nf, batch_dims, B, V, n, cache = self._prepare(cache, frames, num_frames)
     lab = torch.as_tensor(labels).reshape(B, -1).to(device=W.device, dtype=torch.int32)
     nl = _lengths(num_labels, B, W.device)
@@ -420,6 +423,23 @@ class RecognitionLattice(nn.Module, Generic[T]):
     else:
       loss = _LossFn.apply(W, nf, lab.contiguous(), nl, V, n, local)
     return self._home(loss.reshape(batch_dims), frames)
+
+  def _fused_joint_loss(self, cache, frames, num_frames, labels, num_labels):
+    """The loss through the fused joint weight function + lattice kernels
+    (JointWeightFn.fused_lattice_loss, lt_loss_joint_forward / _backward) when
+    the weight function takes that path: FullNGram x FrameDependent on a ROCm
+    device, one batch dim; else None."""
+    fn = getattr(self.weight_fn, 'fused_lattice_loss', None)
+    if fn is None or self._table_path() or frames.ndim != 3 or not frames.is_cuda:
+      return None
+    if cache is None:
+      cache = self.weight_fn_cacher()
+    dev = frames.device
+    B = frames.shape[0]
+    nf = _lengths(num_frames, B, dev)
+    lab = torch.as_tensor(labels).reshape(B, -1).to(device=dev, dtype=torch.int32).contiguous()
+    nl = _lengths(num_labels, B, dev)
+    return fn(cache, frames, nf, lab, nl, self.context.vocab_size, self.context.context_size)
 
   def shortest_path(self, frames: torch.Tensor, num_frames: torch.Tensor,
                     cache: Optional[T] = None, label_convention: str = 'reference'):

@@ -51,13 +51,15 @@ def all_reduce_step(loss: torch.Tensor, params: Iterable[torch.nn.Parameter] = (
   Without an initialised process group this is the identity.
 
   A parameter without a gradient on this rank (unused here, or an empty
-  shard) contributes zeros, so every rank all-reduces the same layout, and
-  by default receives the summed gradient as a fresh .grad: every rank ends
-  the step with the same gradients, so the replicas' optimizer updates stay
-  identical. ``skip_unused=True`` leaves such a .grad None on this rank
-  (the other ranks' sum is then not applied here, and the replicas may
-  drift apart; only for callers that re-synchronise parameters
-  themselves)."""
+  shard) contributes zeros, so every rank all-reduces the same layout. The
+  same all-reduce carries one "used" count per parameter: a parameter some
+  rank produced a gradient for gets the summed gradient on every rank (a
+  fresh .grad where it had none), so the replicas' optimizer updates stay
+  identical; a parameter no rank used keeps .grad None everywhere, so
+  optimizers with weight decay or momentum skip it as they would without
+  the collective. ``skip_unused=True`` leaves a None .grad None on this rank
+  even when other ranks used the parameter (the replicas may then drift
+  apart; only for callers that re-synchronise parameters themselves)."""
   total = loss.detach().sum().reshape(1).to(torch.float32)
   if not (dist.is_available() and dist.is_initialized()):
     return total[0]
@@ -66,15 +68,18 @@ def all_reduce_step(loss: torch.Tensor, params: Iterable[torch.nn.Parameter] = (
   for p in params:
     parts.append(torch.zeros([p.numel()], dtype=torch.float32, device=total.device)
                  if p.grad is None else p.grad.reshape(-1).to(torch.float32))
+  parts.append(torch.tensor([0.0 if p.grad is None else 1.0 for p in params],
+                            dtype=torch.float32, device=total.device))
   flat = torch.cat(parts)
   dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+  used = flat[flat.numel() - len(params):].tolist()
   off = 1
-  for p in params:
+  for p, u in zip(params, used):
     k = p.numel()
     red = flat[off:off + k].view(p.shape)
     if p.grad is not None:
       p.grad.copy_(red.to(p.grad.dtype))
-    elif not skip_unused:
+    elif u > 0 and not skip_unused:
       p.grad = red.to(p.dtype).clone()
     off += k
   return flat[0]

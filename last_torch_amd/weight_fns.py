@@ -126,6 +126,29 @@ class _JointWeightsFn(torch.autograd.Function):
     return dpc, dpf.reshape(pf.shape), dwo, g2.sum((0, 1)), None, None
 
 
+class _JointLossFn(torch.autograd.Function):
+  """RecognitionLattice.forward's loss with JointWeightFn's arc weights fused
+  into the lattice kernels (lt_loss_joint_forward / _backward, lt_joint.hip):
+  W and d loss / dW are never materialised; the backward gives the
+  projections' and the output layer's gradients directly."""
+
+  @staticmethod
+  def forward(ctx, pc, pf, wo, bias, nf, labels, nl, precision):
+    from last_torch_amd import _native
+    loss, _, _, state = _native.joint_loss_forward(pc, pf, wo, bias, nf, labels, nl, precision)
+    ctx.save_for_backward(pc, pf, wo, bias, nf, labels, state)
+    ctx.precision = precision
+    return loss
+
+  @staticmethod
+  def backward(ctx, g):
+    from last_torch_amd import _native
+    pc, pf, wo, bias, nf, labels, state = ctx.saved_tensors
+    dpc, dpf, dwo, dbias = _native.joint_loss_backward(pc, pf, wo, bias, nf, labels, state,
+                                                       grad=g, precision=ctx.precision)
+    return dpc, dpf.reshape(pf.shape), dwo, dbias, None, None, None, None
+
+
 class JointWeightFn(WeightFn[torch.Tensor]):
   """tanh(P_c ctx_emb[c] + P_f frame) -> (blank, V lexical) logits: the
   shared-emb / shared-rnn weight function (weight_fns.py:174-227).
@@ -135,13 +158,24 @@ class JointWeightFn(WeightFn[torch.Tensor]):
   hidden_size a multiple of 16, vocab_size < 64). ``precision`` 'fp32'
   (default, faithful to the reference's fp32 layers): split-bf16 products,
   about 16 mantissa bits each, as the backward; 'bf16': one bf16 product
-  (faster, ~2^-8 relative per product)."""
+  (faster, ~2^-8 relative per product).
+
+  ``lattice_fusion``: whether ``RecognitionLattice.forward`` hands this
+  weight function's projections to the fused joint lattice loss
+  (lt_loss_grad_joint: W and dW never in HBM) instead of materialising W.
+  'auto' takes it where it measured faster than the separate launches
+  (``fused_lattice_preferred``), 'on' whenever the shape allows it, 'off'
+  never."""
 
   def __init__(self, vocab_size: int, hidden_size: int, device=None, fused: bool = True,
-               backward_chunk: int = 16384, precision: str = 'fp32'):
+               backward_chunk: int = 16384, precision: str = 'fp32',
+               lattice_fusion: str = 'auto'):
     super().__init__()
     if precision not in ('fp32', 'bf16'):
       raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+    if lattice_fusion not in ('auto', 'on', 'off'):
+      raise ValueError(f"lattice_fusion must be 'auto', 'on' or 'off', got {lattice_fusion!r}")
+    self.lattice_fusion = lattice_fusion
     self.vocab_size = vocab_size
     self.hidden_size = hidden_size
     self.fused = fused
@@ -173,6 +207,26 @@ class JointWeightFn(WeightFn[torch.Tensor]):
     blank, lexical = self.forward(cache, frame)
     return torch.cat([blank[..., None], lexical], dim=-1)
 
+  def fused_lattice_loss(self, cache, frames, num_frames, labels, num_labels, vocab_size,
+                         context_size):
+    """The lattice loss with the arc weights formed inside the lattice kernels
+    (lt_loss_joint_forward / _backward), or None where this weight function
+    does not take that path (lattice_fusion, device, shape)."""
+    from last_torch_amd import _native
+    if self.lattice_fusion == 'off' or not self._use_kernel(frames) or frames.ndim != 3:
+      return None
+    B, T = frames.shape[:2]
+    U = labels.shape[-1]
+    if not _native.joint_loss_supported(B, T, U, vocab_size, context_size, self.hidden_size):
+      return None
+    if self.lattice_fusion == 'auto' and not fused_lattice_preferred(B, T, U, self.hidden_size):
+      return None
+    pc = self.context_projection(cache)
+    pf = self.frame_projection(frames)
+    wo = torch.cat([self.to_blank.weight, self.to_vocab.weight], 0)
+    bias = torch.cat([self.to_blank.bias, self.to_vocab.bias], 0)
+    return _JointLossFn.apply(pc, pf, wo, bias, num_frames, labels, num_labels, self.precision)
+
   def forward(self, cache, frame, state=None):
     ctx = cache
     if state is None and self._use_kernel(frame):
@@ -186,6 +240,19 @@ class JointWeightFn(WeightFn[torch.Tensor]):
       joint = self.context_projection(ctx) + self.frame_projection(frame)
     joint = torch.tanh(joint)
     return self.to_blank(joint)[..., 0], self.to_vocab(joint)
+
+
+def fused_lattice_preferred(batch, frames, labels, hidden):
+  """Where the fused joint lattice loss (lt_loss_grad_joint) measured faster
+  than the separate launches (lt_joint_weights -> lt_loss_grad ->
+  lt_joint_weights_backward) on MI355X: profiles/r05_joint_step.jsonl. At
+  the bench shape (T = 1000, U = 100, V = 32, B = 64 and 256, H = 32..128)
+  it measured slower everywhere -- the producer is issue-bound, so forming W
+  inside the latency-bound recursions and again in the marginal pass costs
+  more than W's HBM round trip saves -- so 'auto' keeps the
+  separate launches."""
+  del batch, frames, labels, hidden
+  return False
 
 
 class SharedEmbCacher(WeightFnCacher[torch.Tensor]):

@@ -140,6 +140,11 @@ def _gloo_worker(rank, world, port, payload, out_q):
       skipped.grad = torch.ones(2)
     sharding.all_reduce_step(loss, [skipped], skip_unused=True)
     skip_ok = (skipped.grad is None) if rank != 1 else bool((skipped.grad == 1).all())
+    # a parameter no rank used keeps .grad None on every rank (weight decay /
+    # momentum must not see a zero gradient for it)
+    idle = torch.nn.Parameter(torch.zeros(4))
+    sharding.all_reduce_step(loss, [idle])
+    skip_ok = skip_ok and idle.grad is None
     out_q.put((rank, idx, loss.detach().numpy(), table.grad.numpy().copy(), totals, head_grads,
                p.grad.numpy().copy(), partial.grad.numpy().copy(), skip_ok, total3,
                bucket.calls))
