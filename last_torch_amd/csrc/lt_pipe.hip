@@ -107,7 +107,7 @@ struct PArgs {
   const int* jfbig;    // [ceil(B*T / 32)] some |Pf| of the 32-row block > kSplitMax
   const float* jwo;    // [R, H] Wo (blank row first)
   const float* jbias;  // [R]
-  int off_wo, off_ec;  // LDS: Wo bf16 (hi, lo), e^{2 Pc} fp32 [C][H]
+  int off_wo, off_ec;  // LDS: Wo bf16 (hi, lo), e^{2 Pc} fp32 [C][H + 4]
   int off_jf;          // LDS: per producer helper two 1 KB slots of e^{2 Pf} rows
 };
 constexpr int kMidBand = 32;    // frames next to the middle zeroed before the granules flow
@@ -838,8 +838,8 @@ LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, in
   const unsigned short* w1l = w1 + WL;
   // the two row tiles' e^{2 Pc} rows (states r and 32 + r; rows past C
   // repeat the last state and are never stored)
-  const float* ec0 = ecl + min(r, C - 1) * H + hk;
-  const float* ec1 = ecl + min(32 + r, C - 1) * H + hk;
+  const float* ec0 = ecl + min(r, C - 1) * (H + 4) + hk;
+  const float* ec1 = ecl + min(32 + r, C - 1) * (H + 4) + hk;
   // E's byte offset in a slot for element (p, y) (helper_pipe's layout):
   // y is fixed per lane and p an unrolled constant plus 4 half, so with J a
   // compile-time constant no element pays a division
@@ -869,6 +869,7 @@ LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, in
   const bool utt_split = *(const lds_vint*)(as3(lds) + a.off_ctl + 4 * CTL_JBIG) == 0;
   if (hw < nf) issue(hw, 0);
   for (int i = hw; i < nf; i += a.NH, rs ^= 1) {
+    PSTAMP(a, 2 + hw, i, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this frame's row is in the ring
     issue(i + a.NH, rs ^ 1);                             // the next one in flight
     const long long f = row_of(i);
@@ -885,49 +886,66 @@ LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, in
         seen_num = ctl[CTL_NUM];
       }
     }
+    PSTAMP(a, 2 + hw, i, 1);
     unsigned char* sb = lds + a.off_ring + slot * a.slot_bytes;
     lds_float* Wr = (lds_float*)as3(sb);
-    // one row tile at a time (one accumulator pair live): W = acc + bias
-    // (the producer's own rounding) straight into the slot's raw W, the
-    // frame max on the side; E = exp(W - c) once the max is known
+    // W = acc + bias (the producer's own rounding) into the slot's raw W and
+    // kept in registers for E = exp(W - c) once the frame max is known. Row
+    // tile 0 holds states 0..31; of row tile 1 only state 32 (k = 0 of the
+    // lower half) exists, since C <= 33 here (V <= 32, one context label).
+    f32x16 x0 = {}, x1 = {};
+    if (split) {
+      joint_tile<SP, true>(true, ec0, efr, H, w0, w1, w0l, w1l, x0, x1);
+    } else {  // a projection beyond kSplitMax: the direct tanh from Pc + Pf (rare)
+      joint_tile<SP, true>(false, a.jpc + min(r, C - 1) * H + hk, a.jpf + f * H + hk, H, w0, w1,
+                           w0l, w1l, x0, x1);
+    }
     float mx = -kInf;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      f32x16 acc0 = {}, acc1 = {};
+    for (int k = 0; k < 16; ++k) {
+      const int p = (k & 3) + 8 * (k >> 2) + 4 * half;
+      x0[k] += b0;
+      x1[k] += b1;
+      Wr[p * R + y0] = x0[k];
+      if (v1) Wr[p * R + y1] = x1[k];
+      mx = fmaxf(mx, v1 ? fmaxf(x0[k], x1[k]) : x0[k]);
+    }
+    float z0 = 0.f, z1 = 0.f;
+    const bool last = C > 32 && half == 0;  // this lane holds state 32's W
+    if (C > 32) {
+      f32x16 t0 = {}, t1 = {};
       if (split) {
-        joint_tile<SP, true>(true, rt ? ec1 : ec0, efr, H, w0, w1, w0l, w1l, acc0, acc1);
-      } else {  // a projection beyond kSplitMax: the direct tanh from Pc + Pf (rare)
-        joint_tile<SP, true>(false, a.jpc + min(32 * rt + r, C - 1) * H + hk, a.jpf + f * H + hk,
-                             H, w0, w1, w0l, w1l, acc0, acc1);
+        joint_tile<SP, true>(true, ec1, efr, H, w0, w1, w0l, w1l, t0, t1);
+      } else {
+        joint_tile<SP, true>(false, a.jpc + min(32 + r, C - 1) * H + hk, a.jpf + f * H + hk, H,
+                             w0, w1, w0l, w1l, t0, t1);
       }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int p = 32 * rt + (k & 3) + 8 * (k >> 2) + 4 * half;
-        const float x0 = acc0[k] + b0, x1 = acc1[k] + b1;
-        if (p < C) {
-          Wr[p * R + y0] = x0;
-          if (v1) Wr[p * R + y1] = x1;
-          mx = fmaxf(mx, v1 ? fmaxf(x0, x1) : x0);
-        }
+      z0 = t0[0] + b0;
+      z1 = t1[0] + b1;
+      if (last) {
+        Wr[32 * R + y0] = z0;
+        if (v1) Wr[32 * R + y1] = z1;
+        mx = fmaxf(mx, v1 ? fmaxf(z0, z1) : z0);
       }
     }
     const float c = safe(wave_max(mx));
     const float cl = c * kLog2e;
-    // (rolled: 64 unrolled offsets would each hold a register)
-#pragma unroll 1
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll 2
-      for (int k = 0; k < 16; ++k) {
-        const int p = 32 * rt + (k & 3) + 8 * (k >> 2) + 4 * half;
-        if (p < C) {
-          *(lds_float*)(as3(sb) + eoff(p, y0)) = lt_exp_off(Wr[p * R + y0], cl);
-          if (v1) *(lds_float*)(as3(sb) + eoff(p, y1)) = lt_exp_off(Wr[p * R + y1], cl);
-        }
-      }
+    PSTAMP(a, 2 + hw, i, 2);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int p = (k & 3) + 8 * (k >> 2) + 4 * half;
+      *(lds_float*)(as3(sb) + eoff(p, y0)) = lt_exp_off(x0[k], cl);
+      if (v1) *(lds_float*)(as3(sb) + eoff(p, y1)) = lt_exp_off(x1[k], cl);
+    }
+    if (last) {
+      *(lds_float*)(as3(sb) + eoff(32, y0)) = lt_exp_off(z0, cl);
+      if (v1) *(lds_float*)(as3(sb) + eoff(32, y1)) = lt_exp_off(z1, cl);
+    }
     if (lane == 0) {
       *(lds_float*)(as3(sb) + a.soff_c) = c;
       lds_release_store(ctl + CTL_TAG + slot, i + 1);
     }
+    PSTAMP(a, 2 + hw, i, 3);
     slot += a.NH;
     if (slot >= a.K) slot -= a.K;
   }
@@ -1213,7 +1231,7 @@ LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m
 }
 
 template <int J, bool BF16, int PN, int D, int PROD = 0>
-__global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void pipe_kernel(const PArgs a) {
+__global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), PROD ? 2 : 4) void pipe_kernel(const PArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int blk = (int)blockIdx.x;
   const bool rev = a.dirs == 2 && blk >= a.B;
@@ -1245,11 +1263,12 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), 4) void
   for (int u = tid; u < a.U; u += nthr) ylab[u] = a.labels[(long long)b * a.U + u];
   if constexpr (PROD != 0) {
     // the producer helpers' operands: Wo as bf16 (hi, and lo for split
-    // products) with padded rows, e^{2 Pc} in fp32
+    // products) with padded rows, e^{2 Pc} in fp32 rows of H + 4 (the helpers'
+    // 16-byte row reads then fall in distinct banks)
     const int H = a.jH, HP = H + 8, WL = (a.R * HP + 7) & ~7;
     stage_wo<PROD == 1>(a.jwo, (unsigned short*)(lds + a.off_wo), a.R, H, HP, WL, tid, nthr);
     float* ec = (float*)(lds + a.off_ec);
-    for (int k = tid; k < a.C * H; k += nthr) ec[k] = a.jec[k];
+    for (int k = tid; k < a.C * H; k += nthr) ec[k + 4 * (k / H)] = a.jec[k];
   }
   __syncthreads();
   if constexpr (PROD != 0) {
@@ -1537,7 +1556,7 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
     a.jcbig = jo->cbig; a.jfbig = jo->fbig; a.jwo = jo->wo; a.jbias = jo->bias;
     const int WL = (R * (jo->H + 8) + 7) & ~7;
     a.off_wo = off; off += al16((jo->prod == 1 ? 4LL : 2LL) * WL);
-    a.off_ec = off; off += al16(4LL * C * jo->H);
+    a.off_ec = off; off += al16(4LL * C * (jo->H + 4));
     a.off_jf = off; off += kPipeMaxHelpers * 2048;
     if (jo->H > 256) return set_error(LT_EUNSUPPORTED, "pipe producer helpers: H <= 256");
   }
