@@ -86,10 +86,13 @@ $(STAMP_OBJ)/lt_lattice.o: $(CSRC)/lt_lattice.hip $(DEPS)
 $(STAMP_OBJ)/lt_pipe.o: $(CSRC)/lt_pipe.hip $(DEPS)
 	@mkdir -p $(STAMP_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -DLT_DIAG -c -o $@ $<
+$(STAMP_OBJ)/lt_joint.o: $(CSRC)/lt_joint.hip $(DEPS)
+	@mkdir -p $(STAMP_OBJ)
+	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -DLT_DIAG -c -o $@ $<
 $(STAMP_OBJ)/lt_tri.o: $(CSRC)/lt_tri.hip $(DEPS)
 	@mkdir -p $(STAMP_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -DLT_DIAG -c -o $@ $<
-stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(STAMP_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
+stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(STAMP_OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(STAMP_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(STAMP_OBJ)/liblt_lattice_stamps.so $^
 .PHONY: stamps
 

@@ -37,7 +37,26 @@ struct JFArgs {
   float* dpf;   // [B*T, H]
   float* part;  // [B * nblk][(C + R) H + 64] per-block d_Pc, d_Wo, d_bias
   int B, T, U, C, R, H, NP, nblk;
+  long long* stamps;  // diagnostic build (-DLT_STAMPS) only: [block][8] s_memtime
 };
+
+#ifdef LT_STAMPS
+#define JSTAMP(a, k, v)                                                  \
+  do {                                                                   \
+    if ((a).stamps && (threadIdx.x & 63) == 0 && threadIdx.x < 64)       \
+      (a).stamps[(long long)blockIdx.x * 8 + (k)] = (v);                 \
+  } while (0)
+#define JCLK() ((long long)__builtin_amdgcn_s_memtime())
+#define JWAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#else
+#define JSTAMP(a, k, v) \
+  do {                  \
+  } while (0)
+#define JCLK() 0LL
+#define JWAIT() \
+  do {          \
+  } while (0)
+#endif
 
 __host__ __device__ inline long long jf_stride(int C, int R, int H) { return (long long)(C + R) * H + 64; }
 
@@ -71,7 +90,7 @@ template <int NW>
 constexpr int jf_threads() { return 64 * NW; }
 
 struct JfLds {
-  int wo, A, Bt, AN, BN, aoff, hd, gt, dpc, ec, ef, total;
+  int wo, A, Bt, AN, BN, aoff, hd, gt, wt, dpc, ec, ef, total;
 };
 JfLds jf_lds(int C, int R, int H, int NP, bool sp) {
   auto al16 = [](long long x) { return (int)((x + 15) & ~15LL); };
@@ -86,6 +105,7 @@ JfLds jf_lds(int C, int R, int H, int NP, bool sp) {
   l.aoff = o; o += al16(4LL * 4 * NP);
   l.hd = o; o += al16(4LL * C * R);
   l.gt = o; o += al16(4LL * 2 * 32 * kJfGS);
+  l.wt = o; o += al16(4LL * 32 * R);  // the raw W tile of the forward in progress
   l.dpc = o; o += al16(4LL * C * H);
   l.ec = o; o += al16(4LL * C * H);   // e^{2 Pc} (or Pc on the direct path)
   l.ef = o; o += al16(4LL * 32 * H);  // the block's e^{2 Pf} rows (or Pf)
@@ -142,6 +162,7 @@ __global__ __launch_bounds__(64 * (NW < 2 ? 2 : NW), 2) void jf_marg_kernel(cons
   int* hd = (int*)(lds + l.hd);
   float* gt = (float*)(lds + l.gt);
   float* dpc = (float*)(lds + l.dpc);
+  float* wtl = (float*)(lds + l.wt);
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const int Fh = min(32, a.T - t0);             // frames of the block in the utterance
@@ -162,6 +183,7 @@ __global__ __launch_bounds__(64 * (NW < 2 ? 2 : NW), 2) void jf_marg_kernel(cons
     for (long long e = tid; e < jf_stride(C, R, H); e += nthr) part[e] = 0.f;
     return;
   }
+  JSTAMP(a, 0, JCLK());
   // ---- staging: Wo bf16, the checkpoint rows, the string arc table
   stage_wo<SP>(a.wo, wol, R, H, HP, WL, tid, nthr);
   stage_words(A, a.alpha + row0 * C, Fl * C, tid, nthr);
@@ -231,65 +253,76 @@ __global__ __launch_bounds__(64 * (NW < 2 ? 2 : NW), 2) void jf_marg_kernel(cons
   }
   f32x16 dwo0 = {}, dwo1 = {};
   float dbias = 0.f;  // thread tid < R: sum of g[:, tid]
+  JSTAMP(a, 1, JCLK());
+  long long tf = 0, tc = 0, tb = 0, tw = 0;  // wave 0: W tile, marginals, barrier, backward
 
   for (int c = 0, buf = 0; c < C; ++c, buf ^= 1) {
     float* g = gt + buf * 32 * GS;
+    const long long q0 = JCLK();
     if (wave == c % NT) {
       // W tile of state c: rows = the block's frames, columns = labels
       f32x16 acc0 = {}, acc1 = {};
       const float* pcr = (dir_mix ? a.pc : ecl) + (long long)c * H + 8 * half;
       joint_tile<SP, true>(split, pcr, pfr, H, w0, w1, w0 + WL, w1 + WL, acc0, acc1);
-      // den - num marginals (marg_tile's arithmetic): den = gb e^{alpha +
-      // w + beta' - log_z}, num = gb sum over the string arcs on (c, y) of
-      // e^{alpha^n + w + beta^n' - num}, chained in ascending arc order
-      // W into the tile (the accumulators die here), then den - num in place,
-      // four rows at a time with their operands gathered first (independent
-      // LDS reads in flight together): den = gb e^{alpha + w + beta' - log_z},
-      // and on the rare elements with string arcs num = gb sum e^{alpha^n + w
-      // + beta^n' - num} in ascending arc order (marg_tile's arithmetic, no
-      // contraction: it subtracts the chains' sum stored apart)
+      JWAIT();
+      const long long qm = JCLK();
+      tf += qm - q0;
+      tc -= qm;
+      // den - num marginals (marg_tile's arithmetic, no contraction):
+      // den = gb e^{alpha + w + beta' - log_z} for every element, straight
+      // from the accumulators; then on the few elements with string arcs
+      // num = gb sum e^{alpha^n + w + beta^n' - num} over their chain
+      // (ascending arc order) and den - num in place
+      float* wt = wtl;  // the forward wave's raw W tile (one forward at a time)
+      const int q0 = y0 == 0 ? c : y0;        // next(c, y) of the bigram (contexts.py:190-205)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = (i & 3) + 8 * (i >> 2) + 4 * half;
-        g[m * GS + y0] = acc0[i] + b0;
-        if (v1) g[m * GS + y1] = acc1[i] + b1;
-      }
-      auto column = [&](int y) {
-        const int q = y == 0 ? c : y;  // next(c, y) of the bigram (contexts.py:190-205)
-        const int k0 = hd[c * R + y];
-#pragma unroll 1
-        for (int i0 = 0; i0 < 16; i0 += 4) {
-          float av[4], bv[4], wv[4], d[4];
+      for (int i0 = 0; i0 < 16; i0 += 4) {
+        float av[4], bv0[4], bv1[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int m = ((i0 + j) & 3) + 8 * ((i0 + j) >> 2) + 4 * half;
-            av[j] = A[m * C + c];
-            bv[j] = Bt[m * C + q];
-            wv[j] = g[m * GS + y];
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int m = ((i0 + j) & 3) + 8 * ((i0 + j) >> 2) + 4 * half;
-            d[j] = m < Fl ? gb * lt_exp(av[j] + wv[j] + bv[j] - lz) : 0.f;
-            if (k0 >= 0 && m < Fl) {
-              float sacc = 0.f;
-              for (int kk = k0; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
-                const int u = kk >> 1;
-                const float bn = BN[m * NP + ((kk & 1) ? u + 1 : u)];
-                sacc += lt_exp(AN[m * NP + u] + wv[j] + bn - nm);
-              }
-              d[j] = __fsub_rn(d[j], __fmul_rn(gb, sacc));
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            g[(((i0 + j) & 3) + 8 * ((i0 + j) >> 2) + 4 * half) * GS + y] = d[j];
+        for (int j = 0; j < 4; ++j) {
+          const int m = ((i0 + j) & 3) + 8 * ((i0 + j) >> 2) + 4 * half;
+          av[j] = A[m * C + c];
+          bv0[j] = Bt[m * C + q0];
+          bv1[j] = v1 ? Bt[m * C + y1] : 0.f;
         }
-      };
-      column(y0);
-      if (v1) column(y1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = i0 + j, m = (i & 3) + 8 * (i >> 2) + 4 * half;
+          const float x0 = acc0[i] + b0, x1 = acc1[i] + b1;
+          wt[m * R + y0] = x0;
+          g[m * GS + y0] = m < Fl ? gb * lt_exp(av[j] + x0 + bv0[j] - lz) : 0.f;
+          if (v1) {
+            wt[m * R + y1] = x1;
+            g[m * GS + y1] = m < Fl ? gb * lt_exp(av[j] + x1 + bv1[j] - lz) : 0.f;
+          }
+        }
+      }
+      // the labels of row c with string arcs, two at a time (one per half)
+      unsigned long long has = __ballot(lane < R && hd[c * R + lane] >= 0);
+      while (has) {
+        const int ya = __builtin_ctzll(has);
+        has &= has - 1;
+        const int yb = has ? __builtin_ctzll(has) : -1;
+        if (yb >= 0) has &= has - 1;
+        const int y = half ? yb : ya;
+        if (y >= 0) {
+          const int m = col;
+          const float w = wt[m * R + y];
+          float sacc = 0.f;
+          for (int kk = hd[c * R + y]; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
+            const int u = kk >> 1, ub = (kk & 1) ? u + 1 : u;
+            sacc += lt_exp(AN[m * NP + u] + w + BN[m * NP + ub] - nm);
+          }
+          if (m < Fl) g[m * GS + y] = __fsub_rn(g[m * GS + y], __fmul_rn(gb, sacc));
+        }
+      }
+      JWAIT();
+      tc += JCLK();
     }
+    const long long q1 = JCLK();
     __syncthreads();  // one barrier a tile: the other buffer is written next
+    const long long q2 = JCLK();
+    tw += q2 - q1;
     if (wave >= NW) continue;  // a forward-only wave
     // ---- backward of tile c (the NW backward waves, each its hidden columns)
     if (tid < R) {  // eight partial sums: the loads in flight together
@@ -339,7 +372,13 @@ __global__ __launch_bounds__(64 * (NW < 2 ? 2 : NW), 2) void jf_marg_kernel(cons
     }
     csum += __shfl_xor(csum, 32);
     if (half == 0) dpc[c * H + hl] += csum;  // this wave owns column hl
+    tb += JCLK() - q2;
   }
+  JSTAMP(a, 2, JCLK());
+  JSTAMP(a, 4, tf);
+  JSTAMP(a, 5, tc);
+  JSTAMP(a, 6, tw);
+  JSTAMP(a, 7, tb);
   // ---- outputs: d_Pf rows (the block owns its frames), the partials
   if (wave < NW) {
 #pragma unroll
@@ -357,6 +396,7 @@ __global__ __launch_bounds__(64 * (NW < 2 ? 2 : NW), 2) void jf_marg_kernel(cons
   if (tid < R) part[(long long)(C + R) * H + tid] = dbias;
   __syncthreads();
   for (int e = tid; e < C * H; e += nthr) part[e] = dpc[e];
+  JSTAMP(a, 3, JCLK());
 }
 
 // out[e] = sum over the blocks' partials in a fixed order (joint_reduce_kernel's
@@ -550,6 +590,13 @@ int lt_loss_joint_backward(const lt_problem* pb, const lt_joint_params* jp,
   a.grad = grad;
   a.dpf = d_frame_proj;
   a.part = (float*)scratch;
+  a.stamps = nullptr;
+#ifdef LT_STAMPS
+  {
+    const char* sp = lt_impl::tune_str("LT_JSTAMPS_PTR");
+    a.stamps = sp ? (long long*)strtoull(sp, nullptr, 0) : nullptr;
+  }
+#endif
   a.B = pb->batch; a.T = pb->max_frames; a.U = pb->max_labels; a.C = C; a.R = R; a.H = H;
   a.NP = pb->max_labels + 1;
   a.nblk = (pb->max_frames + 31) / 32;

@@ -109,6 +109,7 @@ struct PArgs {
   const float* jbias;  // [R]
   int off_wo, off_ec;  // LDS: Wo bf16 (hi, lo), e^{2 Pc} fp32 [C][H + 4]
   int off_jf;          // LDS: per producer helper two 1 KB slots of e^{2 Pf} rows
+  int off_j32;         // LDS: per producer helper state 32's W rows of its next 32 frames
 };
 constexpr int kMidBand = 32;    // frames next to the middle zeroed before the granules flow
 // floats per slot of the den (hring) and numerator (nring) row rings
@@ -132,6 +133,7 @@ constexpr int kHS = 64;
 #define LT_PIPE_MID 2
 #endif
 constexpr int kPipeMidWaves = LT_PIPE_MID;  // marginal waves per workgroup in mid mode
+constexpr int kProdHelpers = kPipeMaxHelpers + kPipeMidWaves;  // producer helpers at most
 enum { CTL_TAG = 0, CTL_DEN = kPipeMaxSlots, CTL_NUM, CTL_ABORT, CTL_FIN0, CTL_FIN1, CTL_JBIG,
        CTL_MRG, CTL_N = CTL_MRG + kPipeMidWaves };
 
@@ -867,8 +869,16 @@ LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, in
   // Pf rows exceeds kSplitMax (the common case: no per-frame flag read, whose
   // scalar load would share lgkmcnt with every LDS wait of the frame)
   const bool utt_split = *(const lds_vint*)(as3(lds) + a.off_ctl + 4 * CTL_JBIG) == 0;
+  // state 32 (C = 33) fills one row of a 32-row tile: with every frame on the
+  // split path its W rows are formed 32 frames at a time (tile rows = this
+  // helper's next 32 frames; an element's value does not depend on the other
+  // rows of its tile) and kept in LDS
+  const bool batch32 = C > 32 && csplit && utt_split;
+  lds_float* s32 = (lds_float*)(as3(lds) + a.off_j32 + hw * ((32 * R * 4 + 15) & ~15));
+  const float* ec32 = ecl + 32 * (H + 4) + hk;
+  int bn = 0;  // frames this helper has processed
   if (hw < nf) issue(hw, 0);
-  for (int i = hw; i < nf; i += a.NH, rs ^= 1) {
+  for (int i = hw; i < nf; i += a.NH, rs ^= 1, ++bn) {
     PSTAMP(a, 2 + hw, i, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this frame's row is in the ring
     issue(i + a.NH, rs ^ 1);                             // the next one in flight
@@ -912,7 +922,30 @@ LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, in
     }
     float z0 = 0.f, z1 = 0.f;
     const bool last = C > 32 && half == 0;  // this lane holds state 32's W
-    if (C > 32) {
+    if (batch32) {
+      if ((bn & 31) == 0) {  // rows: frames i + NH q, q = 0..31 (clamped)
+        const int fi = min(i + a.NH * r, nf - 1);
+        const float* efq = a.jef + row_of(fi) * H + hk;
+        f32x16 t0 = {}, t1 = {};
+        joint_tile<SP, true>(true, ec32, efq, H, w0, w1, w0l, w1l, t0, t1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int q = (k & 3) + 8 * (k >> 2) + 4 * half;
+          s32[q * R + y0] = t0[k] + b0;
+          if (v1) s32[q * R + y1] = t1[k] + b1;
+        }
+      }
+      if (last) {
+        const int q = bn & 31;
+        z0 = s32[q * R + y0];
+        Wr[32 * R + y0] = z0;
+        if (v1) {
+          z1 = s32[q * R + y1];
+          Wr[32 * R + y1] = z1;
+        }
+        mx = fmaxf(mx, v1 ? fmaxf(z0, z1) : z0);
+      }
+    } else if (C > 32) {
       f32x16 t0 = {}, t1 = {};
       if (split) {
         joint_tile<SP, true>(true, ec1, efr, H, w0, w1, w0l, w1l, t0, t1);
@@ -1557,7 +1590,11 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
     const int WL = (R * (jo->H + 8) + 7) & ~7;
     a.off_wo = off; off += al16((jo->prod == 1 ? 4LL : 2LL) * WL);
     a.off_ec = off; off += al16(4LL * C * (jo->H + 4));
-    a.off_jf = off; off += kPipeMaxHelpers * 2048;
+    // producer helpers take the mid-mode waves' places too when one
+    // workgroup holds a CU (their MFMA work bounds the step otherwise)
+    if (dirs * pb->batch <= 256) a.NH = std::max(a.NH, kProdHelpers);
+    a.off_jf = off; off += kProdHelpers * 2048;
+    a.off_j32 = off; off += kProdHelpers * al16(32LL * R * 4);
     if (jo->H > 256) return set_error(LT_EUNSUPPORTED, "pipe producer helpers: H <= 256");
   }
   int so = 0;
