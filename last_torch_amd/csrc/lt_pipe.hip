@@ -1590,9 +1590,10 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
     const int WL = (R * (jo->H + 8) + 7) & ~7;
     a.off_wo = off; off += al16((jo->prod == 1 ? 4LL : 2LL) * WL);
     a.off_ec = off; off += al16(4LL * C * (jo->H + 4));
-    // producer helpers take the mid-mode waves' places too when one
-    // workgroup holds a CU (their MFMA work bounds the step otherwise)
-    if (dirs * pb->batch <= 256) a.NH = std::max(a.NH, kProdHelpers);
+    // producer helpers take the mid-mode waves' places too: their registers
+    // (two waves per SIMD) leave one workgroup per CU at any grid, and their
+    // MFMA work bounds the step otherwise
+    a.NH = std::max(a.NH, kProdHelpers);
     a.off_jf = off; off += kProdHelpers * 2048;
     a.off_j32 = off; off += kProdHelpers * al16(32LL * R * 4);
     if (jo->H > 256) return set_error(LT_EUNSUPPORTED, "pipe producer helpers: H <= 256");
@@ -1607,7 +1608,7 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
   a.slot_bytes = so;
   // LDS budget: two workgroups per CU when the grid exceeds the CU count
   const int grid = dirs * pb->batch;
-  int cap = grid > 256 ? 80 * 1024 : 160 * 1024;
+  int cap = grid > 256 && !jo ? 80 * 1024 : 160 * 1024;
   cap = pipe_env("LT_PIPE_LDS", cap);
   // mid mode: the marginal waves' regions, and per ring slot the den and
   // numerator rows of its step
