@@ -108,3 +108,10 @@ $(DIAG_OBJ)/%.o: $(CSRC)/%.hip $(DEPS)
 diag: $(DIAG_OBJ)/lt_lattice.o $(DIAG_OBJ)/lt_pipe.o $(DIAG_OBJ)/lt_chunk.o $(DIAG_OBJ)/lt_table.o $(DIAG_OBJ)/lt_producer.o $(DIAG_OBJ)/lt_joint.o $(DIAG_OBJ)/lt_vit.o $(DIAG_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(DIAG_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(DIAG_OBJ)/liblt_lattice_diag.so $^
 .PHONY: diag
+
+# Clock probe (dev tool, tools/clock_probe.py): build/libclock_probe.so
+probe: build/libclock_probe.so
+build/libclock_probe.so: tools/probe/clock_probe.hip
+	@mkdir -p build
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -shared -fPIC -o $@ $<
+.PHONY: probe
