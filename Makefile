@@ -50,6 +50,10 @@ $(OBJ)/lt_tri.o: $(CSRC)/lt_tri.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+$(OBJ)/lt_tri4.o: $(CSRC)/lt_tri4.hip $(DEPS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
 $(OBJ)/lt_vit.o: $(CSRC)/lt_vit.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -62,7 +66,7 @@ $(OBJ)/lt_joint.o: $(CSRC)/lt_joint.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(OBJ)/lt_tri.o $(INST_OBJS)
+$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(OBJ)/lt_tri.o $(OBJ)/lt_tri4.o $(INST_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
 oracle:
@@ -89,10 +93,13 @@ $(STAMP_OBJ)/lt_pipe.o: $(CSRC)/lt_pipe.hip $(DEPS)
 $(STAMP_OBJ)/lt_joint.o: $(CSRC)/lt_joint.hip $(DEPS)
 	@mkdir -p $(STAMP_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -DLT_DIAG -c -o $@ $<
+$(STAMP_OBJ)/lt_tri4.o: $(CSRC)/lt_tri4.hip $(DEPS)
+	@mkdir -p $(STAMP_OBJ)
+	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -DLT_DIAG -c -o $@ $<
 $(STAMP_OBJ)/lt_tri.o: $(CSRC)/lt_tri.hip $(DEPS)
 	@mkdir -p $(STAMP_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_STAMPS -DLT_DIAG -c -o $@ $<
-stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(STAMP_OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(STAMP_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
+stamps: $(STAMP_OBJ)/lt_lattice.o $(STAMP_OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(STAMP_OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(STAMP_OBJ)/lt_tri.o $(STAMP_OBJ)/lt_tri4.o $(foreach v,$(VARIANTS),$(STAMP_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(STAMP_OBJ)/liblt_lattice_stamps.so $^
 .PHONY: stamps
 
@@ -105,7 +112,7 @@ $(DIAG_OBJ)/lt_inst_%.o: $(CSRC)/lt_inst.hip $(DEPS)
 $(DIAG_OBJ)/%.o: $(CSRC)/%.hip $(DEPS)
 	@mkdir -p $(DIAG_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DLT_DIAG -c -o $@ $<
-diag: $(DIAG_OBJ)/lt_lattice.o $(DIAG_OBJ)/lt_pipe.o $(DIAG_OBJ)/lt_chunk.o $(DIAG_OBJ)/lt_table.o $(DIAG_OBJ)/lt_producer.o $(DIAG_OBJ)/lt_joint.o $(DIAG_OBJ)/lt_vit.o $(DIAG_OBJ)/lt_tri.o $(foreach v,$(VARIANTS),$(DIAG_OBJ)/lt_inst_$(v).o)
+diag: $(DIAG_OBJ)/lt_lattice.o $(DIAG_OBJ)/lt_pipe.o $(DIAG_OBJ)/lt_chunk.o $(DIAG_OBJ)/lt_table.o $(DIAG_OBJ)/lt_producer.o $(DIAG_OBJ)/lt_joint.o $(DIAG_OBJ)/lt_vit.o $(DIAG_OBJ)/lt_tri.o $(DIAG_OBJ)/lt_tri4.o $(foreach v,$(VARIANTS),$(DIAG_OBJ)/lt_inst_$(v).o)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $(DIAG_OBJ)/liblt_lattice_diag.so $^
 .PHONY: diag
 

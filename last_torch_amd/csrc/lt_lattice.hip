@@ -1017,6 +1017,18 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
 #endif
   // trigram with W staged in LDS: the den roles of lt_tri.hip (one lane per
   // state pair, every term in registers) in the same side-by-side launch
+  // V = 32 trigram: the recursions on quads of four workgroups (lt_tri4.hip)
+  // while the 8B quad members fit the CUs at once
+  if (ck && !local_norm && g.n == 2 && g.V == 32 && alpha && beta) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        lt_impl::tri4_eligible(g.V, g.n, pb->batch, pb->max_labels, cus)) {
+      const long long wb = (long long)pb->batch * pb->max_frames * g.C * (g.V + 1) * (bf16 ? 2 : 4);
+      return lt_impl::launch_tri4(pf, bf16, alpha, beta, alpha_num, beta_num, log_z, num, loss,
+                                  wb, st);
+    }
+  }
   if (ck && !local_norm && g.n == 2 && g.V >= 2 && g.V <= 32 && pf.wst && pbk.wst &&
       pf.a.aux_waves == pbk.a.aux_waves && pf.a.slot_bytes == pbk.a.slot_bytes &&
       (g.V != 32 || pbk.lds_bytes + 8 * kTriBPad <= kLdsMax) && env_int("LT_NO_TRI", 0) == 0) {

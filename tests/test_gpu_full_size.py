@@ -244,10 +244,11 @@ def test_viterbi_long_utterances_backtrace_routes(cuda, T):
 
 
 def test_cfg5_trigram_bf16(cuda):
-  """cfg5: trigram (|ctx| = 1057) bf16 arc weights at B=32, T=1000, U=100:
-  losses of a sample and every dW element of four utterances against the
-  oracle on the bf16-rounded weights; per-frame marginal sums of the whole
-  batch."""
+  """cfg5: trigram (|ctx| = 1057) bf16 arc weights at B=32, T=1000, U=100
+  (the recursions on quads of four workgroups, lt_tri4.hip): losses and every
+  dW element of eight utterances spread over the batch (each quad group of
+  eight and both halves of the grid) against the oracle on the bf16-rounded
+  weights; per-frame marginal sums of the whole batch."""
   V, n = 32, 2
   W, nf, lab, nl = _bench_inputs(32, 1000, 100, V, n, cuda, seed=5, dtype=torch.bfloat16)
   loss, lz, num, dW = nat.loss_grad(W, nf, lab, nl, V, n, False)
@@ -255,7 +256,7 @@ def test_cfg5_trigram_bf16(cuda):
   # bf16 dW: each element carries 2^-9 relative rounding (in the sum: 2^-8 * 2)
   assert (s.abs() <= _frame_sum_tol(lz, num, bf16=True)).all()
   orc = _orc()
-  idx = [0, 9, 17, 31]
+  idx = [0, 5, 9, 14, 17, 22, 27, 31]
   Wc, nfc, labc, nlc = _np(W[idx], nf[idx], lab[idx], nl[idx])
   rl, rlz, rnum, rdW = orc.loss_grad(Wc, nfc, labc, nlc, V, n)
   _, den = orc.den_grad(Wc, nfc, V, n)
