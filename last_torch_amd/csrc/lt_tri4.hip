@@ -40,6 +40,15 @@
 // counter (whichever side finishes second writes it). The marginal pass
 // (marg_kernel) is unchanged.
 //
+// Measured (cfg5, B = 32, bf16): parity-green, but 3.3-3.5 us
+// a frame against the one-workgroup kernel's 2.7 (lt_tri.hip), so only the
+// diagnostic build runs it (LT_TRI4=1). The per-frame hand-off is the floor:
+// stamps (tools/tri4_stamps.py) show 2,400-2,900 cycles a frame from a
+// member's last store to its inputs all present, against the guide's 0.8-2.9
+// us for a data-tagged one-to-one hand-off between CUs that stream loads
+// (MI355X_MICROARCH.md, handoff-1to1), and ~2,800 cycles of compute whatever
+// the terms per lane (34 or 17) or the weight-read form.
+//
 // Scratch: one static device buffer (the exchange words, zeroed by the host
 // before every launch), so concurrent trigram losses on two streams of one
 // device must not overlap.
@@ -49,14 +58,17 @@ namespace {
 
 constexpr int kT4MaxB = 32;          // utterances per launch (8B quad workgroups <= CUs)
 constexpr int kT4Pub = 264;          // words a member publishes a frame (256 + 8 order-1)
-constexpr int kT4Waves = 8;          // 4 state waves, 1 aux wave, 2 loader waves, 1 numerator
+constexpr int kT4SW = 8;             // state waves: two lanes a state (the terms in halves)
+constexpr int kT4Aux = 8, kT4Ld = 9, kT4Num = 11;  // the aux wave, loaders 9-10, numerator
+constexpr int kT4Wr = 12;            // the checkpoint-row writer
+constexpr int kT4Waves = 13;
 constexpr unsigned kT4Spin = 1u << 21;
 constexpr int kT4ND = 8;             // numerator gather depth (frames in flight)
 
 struct T4Scratch {
   unsigned long long x[2 * kT4MaxB][2][4][kT4Pub];  // tagged values [quad][frame & 1][member]
   unsigned long long mx[2 * kT4MaxB][2][4];          // tagged member maxes
-  unsigned long long fin[kT4MaxB][20][2];            // forward: tagged final (max, sum) per wave
+  unsigned long long fin[kT4MaxB][36][2];            // forward: tagged final (max, sum) per wave
   float lz[kT4MaxB], num[kT4MaxB];
   unsigned long long xcc[2 * kT4MaxB][4];           // tagged XCD id of each member
   int cnt[kT4MaxB];
@@ -108,7 +120,7 @@ struct T4Geo {
   static constexpr int R0C = BF16 ? 6 : 10;          // chunks of row 0 (+ misalignment)
   static constexpr int NI = (NRC + R0C + 63) / 64;   // LDS-DMA instructions (16 B a lane)
   static constexpr int BLK = 1024 * NI;              // forward: blank weights (dword a lane)
-  static constexpr int P = BF16 ? 4 : 3;             // ring slots
+  static constexpr int P = BF16 ? 3 : 3;             // ring slots
   template <bool REV>
   static constexpr int slot() { return BLK + (REV ? 0 : 1024); }
   template <bool REV>
@@ -129,9 +141,10 @@ LT_DEVINL void t4_put(unsigned long long* p, unsigned long long v) {
 // A word for the quad: with every member on one XCD a plain store, which
 // keeps the line in that XCD's L2 where the readers' L1-bypassing polls find
 // it; else the write-through (sc1) store, which drops it from the L2.
+// (inline asm: no compiler-inserted wait for the wave's older stores)
 LT_DEVINL void t4_pub(unsigned long long* p, unsigned long long v, bool same_xcd) {
-  if (same_xcd) *(volatile unsigned long long*)p = v;
-  else t4_put(p, v);
+  if (same_xcd) asm volatile("global_store_dwordx2 %0, %1, off" : : "v"(p), "v"(v) : "memory");
+  else asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
 }
 LT_DEVINL unsigned t4_xcc() {
   unsigned v;
@@ -191,6 +204,18 @@ LT_DEVINL float t4_w(const unsigned char* p) {  // one weight from LDS, unmerged
     return *(lds_f32*)p;
 }
 
+// plain (pipelined) LDS weight reads, for terms whose addresses are not
+// contiguous (the compiler cannot merge them into unaligned wide reads)
+template <bool BF16>
+LT_DEVINL float t4_wn(const unsigned char* p) {
+  typedef const __attribute__((address_space(3))) unsigned short lds_u16;
+  typedef const __attribute__((address_space(3))) float lds_f32;
+  if constexpr (BF16)
+    return __uint_as_float((unsigned)*(lds_u16*)p << 16);
+  else
+    return *(lds_f32*)p;
+}
+
 // LDS of a member: the ring, then the staged sources [2][8][32], the
 // order-1 sources of state 0 (backward) [2][32], the order-1 alpha (forward)
 // [2][8], the max slots [3], the abort flag
@@ -203,7 +228,9 @@ struct T4Lds {
   static constexpr int own1 = stage1 + 2 * 32 * 4;
   static constexpr int maxs = own1 + 2 * 8 * 4;
   static constexpr int abrt = maxs + 4 * 4;
-  static constexpr int nring = abrt + 16;  // abrt: two flags, by step parity             // numerator weights [kT4ND][4][64] dwords
+  static constexpr int hv = abrt + 16;     // abrt: two flags, by step parity
+  static constexpr int spb = hv + 2 * 272 * 4;  // the states' values [2][265] for the writer
+  static constexpr int nring = spb + 16;        // the offsets sp [2]             // numerator weights [kT4ND][4][64] dwords
   static constexpr int total = nring + kT4ND * 1024;
 };
 
@@ -411,6 +438,29 @@ struct T4Numer {
   }
 };
 
+// One checkpoint row of a member's states (the writer wave): forward, alpha
+// rows [B][T][C] at row t; backward, beta rows, value vals[li] + O, the
+// member's 256 order-2 states, 8 order-1 states and (member 0) state 0
+template <bool REV>
+LT_DEVINL void t4_rows(const T4Args& a, int b, int k, int t, const float* vals, float O, int lane) {
+  float* base = REV ? a.beta : a.alpha;
+  if (!base || t < 0) return;
+  float* row = base + ((long long)b * a.T + t) * kC;
+  for (int li = lane; li < 265; li += 64) {
+    int p;
+    if (li < 256) {
+      const int hi = li >> 5, lo = li & 31;
+      p = REV ? 33 + 32 * lo + 8 * k + hi : 33 + 32 * (8 * k + hi) + lo;
+    } else if (li < 264) {
+      p = 1 + 8 * k + (li - 256);
+    } else {
+      if (k != 0) break;
+      p = 0;
+    }
+    row[p] = O + vals[li];
+  }
+}
+
 template <bool BF16, bool REV>
 LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) {
   typedef T4Geo<BF16> Gm;
@@ -427,31 +477,39 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
   float* own1 = (float*)(lds + L::own1);
   int* maxs = (int*)(lds + L::maxs);
   int* abrt = (int*)(lds + L::abrt);
+  float* hv = (float*)(lds + L::hv);
+  float* spb = (float*)(lds + L::spb);
   unsigned long long(*X)[4][kT4Pub] = g_t4.x[q];
   unsigned long long(*MX)[4] = g_t4.mx[q];
   if (tid < 3) maxs[tid] = tri_enc(-kInf);
   if (tid == 3) abrt[0] = abrt[1] = 0;
   if (tid == 0) t4_put(&g_t4.xcc[q][k], t4_word(1u, __uint_as_float(t4_xcc())));
   // ---- prologue: loaders put frames 0 .. P-2 in flight
-  if (wave == 5 || wave == 6) {
-    for (int i = 0; i < Gm::P - 1; ++i) t4_issue<BF16, REV>(a, b, k, nf, i, wave - 5, lane, ldsb);
+  const bool loader = wave == kT4Ld || wave == kT4Ld + 1;
+  if (loader) {
+    for (int i = 0; i < Gm::P - 1; ++i) t4_issue<BF16, REV>(a, b, k, nf, i, wave - kT4Ld, lane, ldsb);
   }
   T4Numer<BF16, REV> nu;
-  const bool numer = wave == 7 && k == 0;
+  const bool numer = wave == kT4Num && k == 0;
   if (numer) nu.init(a, ka, b, lane, nf, s_ctx, s_ylab, ldsb + L::nring);
   __syncthreads();
-  // the lane's state: waves 0-3 one state each, wave 4 lanes 0..7 the
-  // order-1 states, lane 8 state 0
-  const int e = tid;                   // waves 0-3: 0..255
-  const int hi = e >> 5, lo = e & 31;  // forward (jl, y - 1); backward (zl, x - 1)
-  int p = -1;                          // the lane's state
-  if (wave < 4) p = REV ? 33 + 32 * lo + 8 * k + hi : 33 + 32 * (8 * k + hi) + lo;
-  else if (wave == 4 && lane < 8) p = 1 + 8 * k + lane;
-  else if (wave == 4 && lane == 8) p = 0;
+  // the lane's state: state waves two lanes a state (h: which half of its
+  // terms), the aux wave's lanes 0..7 the order-1 states, lane 8 state 0
+  const int e = tid >> 1, h = tid & 1;  // state waves: state 0..255
+  const int hi = e >> 5, lo = e & 31;   // forward (jl, y - 1); backward (zl, x - 1)
+  const bool sw = wave < kT4SW, aux = wave == kT4Aux;
+  int p = -1;                           // the lane's state
+  if (sw) p = REV ? 33 + 32 * lo + 8 * k + hi : 33 + 32 * (8 * k + hi) + lo;
+  else if (aux && lane < 8) p = 1 + 8 * k + lane;
+  else if (aux && lane == 8) p = 0;
+  const bool lead = !sw || h == 0;      // the lane that writes the state's words and rows
+  // the state's slot in the writer's buffer
+  const int li = sw ? e : (lane < 8 ? 256 + lane : 264);
   // alpha_0: state 0 = 0, else -inf; beta at the last frame: 0 everywhere
   float v = REV ? 0.f : (p == 0 ? 0.f : -kInf);
-  const bool writes_hist = p > 0 || (p == 0 && k == 0);
-  if (wave == 4 && lane < 8 && !REV) own1[lane] = -kInf;  // alpha_0 of the order-1 states
+  const bool writes_hist = lead && (p > 0 || (p == 0 && k == 0));
+  if (p >= 0 && lead) hv[li] = v;
+  if (aux && lane < 8 && !REV) own1[lane] = -kInf;  // alpha_0 of the order-1 states
   if (REV && writes_hist && nf > 0 && a.beta) a.beta[((long long)b * a.T + nf - 1) * kC + p] = 0.f;
   float O = 0.f;  // the common offset
   if (wave == 0) {  // are the four members on one XCD? (placement: speed only)
@@ -472,7 +530,7 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
     int* ab = abrt + (i & 1);
     float m4 = -kInf;  // the max of the vector one step older: this step's offset
     // ---- this step's inputs (the words of step i), before the barrier
-    if (wave < 5) {
+    if (sw || aux) {
       if (i >= 1) {
         const float mv = t4_take(&MX[(i - 1) & 1][lane & 3], (unsigned)i, lane < 4, ab);
         m4 = lane < 4 ? mv : -kInf;
@@ -480,9 +538,9 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
       m4 = fmaxf(m4, __shfl_xor(m4, 1));
       m4 = fmaxf(m4, __shfl_xor(m4, 2));
       m4 = __shfl(m4, 0);
-      if (wave < 4) {
+      if (sw) {
         // forward: stage[jl][x - 1] = alpha_i[(x, j+1)]; backward:
-        // stage[zl][y - 1] = beta_{t+1}[(z, y)]
+        // stage[zl][y - 1] = beta_{t+1}[(z, y)] (the lead lanes, one word each)
         int m, idx, row, col;
         if (!REV) {
           const int jl = e & 7, xi = e >> 3;
@@ -498,8 +556,8 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
           col = yi;
         }
         float sv = REV ? 0.f : -kInf;  // step 0: alpha_0 (order 2) = -inf, beta = 0
-        if (i >= 1) sv = t4_take(&X[i & 1][m][idx], (unsigned)i, true, ab);
-        stage[(i & 1) * 256 + row * 32 + col] = sv;
+        if (i >= 1) sv = t4_take(&X[i & 1][m][idx], (unsigned)i, lead, ab);
+        if (lead) stage[(i & 1) * 256 + row * 32 + col] = sv;
       } else if (REV && k == 0) {
         // state 0's order-1 sources beta_{t+1}[y], y = lane + 1
         float sv = 0.f;
@@ -507,9 +565,9 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
           sv = t4_take(&X[i & 1][(lane & 31) >> 3][256 + (lane & 7)], (unsigned)i, lane < 32, ab);
         if (lane < 32) stage1[(i & 1) * 32 + lane] = sv;
       }
-    } else if (wave < 7) {
+    } else if (loader) {
       // loaders: frame i landed (frames i+1 .. i+P-2 may stay in flight)
-      const int mine = (Gm::template ninstr<REV>() - (wave - 5) + 1) / 2;
+      const int mine = (Gm::template ninstr<REV>() - (wave - kT4Ld) + 1) / 2;
       wait_vmcnt((Gm::P - 2) * mine);
     } else if (numer) {
       nu.step(lds, a, b, lane, i);
@@ -518,52 +576,118 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
     lds_barrier();
     T4STAMP(a, q, k, wave, i, 2);
     if (*(volatile int*)ab) break;
-    if (wave >= 5) {
+    if (!sw && !aux) {
       // loaders: frame i - 1's slot is free, the frame P - 1 ahead goes in
-      if (wave < 7) t4_issue<BF16, REV>(a, b, k, nf, i + Gm::P - 1, wave - 5, lane, ldsb);
+      if (loader) t4_issue<BF16, REV>(a, b, k, nf, i + Gm::P - 1, wave - kT4Ld, lane, ldsb);
+      // the writer: the checkpoint rows of the vector of step i (forward:
+      // frame i's alpha; backward: the beta after frame nf - 1 - i, row
+      // nf - 1 - i), from the values the state lanes left, and its offset
+      if (wave == kT4Wr) {
+        if (i >= 1) O += spb[(i - 1) & 1];
+        if (!REV || i >= 1) t4_rows<REV>(a, b, k, REV ? nf - 1 - i : i, hv + (i & 1) * 272, O, lane);
+      }
       continue;
     }
     // this member's max of the vector of step i (gathered during step i - 1)
-    if (wave == 4 && lane == 0) {
+    if (aux && lane == 0) {
       const float mm = tri_dec(maxs[i % 3]);
       maxs[i % 3] = tri_enc(-kInf);
       t4_pub(&MX[i & 1][k], t4_word((unsigned)(i + 1), mm), same_xcd);
     }
     const float sp = i == 0 ? 0.f : (__builtin_isfinite(m4) ? floorf(m4) : 0.f);
+    if (wave == 0 && lane == 0) spb[i & 1] = sp;
     const long long fb = ((long long)b * a.T + f) * (long long)(kC * Gm::RB);
     const unsigned char* slot = lds + (i % Gm::P) * Gm::template slot<REV>();
     const int mis = (int)((fb + (long long)(1 + 8 * k) * Gm::RB) & 15);  // every run's
     const unsigned char* row0 = slot + 16 * Gm::NRC + (int)(fb & 15);
     const float* st = stage + (i & 1) * 256;
-    const float a0 = __shfl(v, 8);  // wave 4: alpha_i[0] (lane 8), forward
+    const float a0 = __shfl(v, 8);  // aux wave: alpha_i[0] (lane 8), forward
     float r = -kInf;
-    if (p >= 0) {
+    if (sw) {
+      // half h of the state's terms, then the pair's logsumexp: each half's
+      // safe max and sum, combined across the two lanes
+      float t[17];
       if (!REV) {
-        // alpha_i's checkpoint row
-        if (writes_hist && a.alpha) a.alpha[((long long)b * a.T + f) * kC + p] = O + v;
-        if (wave < 4) {
-          const int jl = hi, y = lo + 1;
-          const unsigned char* vb = slot + mis + (jl * kR + y) * Gm::es;
+        const int jl = hi, y = lo + 1;
+        const unsigned char* vb = slot + mis + (jl * kR + y) * Gm::es + 16 * h * Gm::RUNB;
+        const float* sx = st + jl * 32 + 16 * h;
+        if (h == 0) {
           float wb;
-          {
-            const unsigned dw = *(const volatile __attribute__((address_space(3))) unsigned*)(
-                slot + Gm::BLK + 4 * e);
-            if constexpr (BF16) {
-              const long long row = 33 + 32 * (8 * k + jl) + (y - 1);
-              const int hs = (int)((fb + row * Gm::RB) & 2);
-              wb = __uint_as_float((hs ? dw >> 16 : dw & 0xffffu) << 16);
-            } else {
-              wb = __uint_as_float(dw);
-            }
+          const unsigned dw = *(const volatile __attribute__((address_space(3))) unsigned*)(
+              slot + Gm::BLK + 4 * e);
+          if constexpr (BF16) {
+            const long long row = 33 + 32 * (8 * k + jl) + (y - 1);
+            const int hs = (int)((fb + row * Gm::RB) & 2);
+            wb = __uint_as_float((hs ? dw >> 16 : dw & 0xffffu) << 16);
+          } else {
+            wb = __uint_as_float(dw);
           }
-          float x[33];
-          x[0] = own1[(i & 1) * 8 + jl] + t4_w<BF16>(vb);  // from the order-1 state j+1
+          t[16] = v + wb;                                   // the blank self loop
+          t[0] = own1[(i & 1) * 8 + jl] + t4_w<BF16>(vb);  // from the order-1 state j+1
+        } else {
+          t[16] = -kInf;
+          t[0] = sx[-1] + t4_wn<BF16>(vb);                  // x = 16
+        }
+        // terms x = 16 h + 1 .. 16 h + 15 (h = 1: 17 .. 31, and x = 32 below)
 #pragma unroll
-          for (int xx = 1; xx <= 32; ++xx)
-            x[xx] = st[jl * 32 + xx - 1] + t4_w<BF16>(vb + xx * Gm::RUNB);
-          r = t4_lse(v + wb, x, sp);
-          t4_pub(&X[(i + 1) & 1][k][jl * 32 + y - 1], t4_word((unsigned)(i + 1), r), same_xcd);
-        } else if (lane < 8) {  // order-1 state 1 + 8k + lane
+        for (int xx = 1; xx < 16; ++xx) t[xx] = sx[xx - 1] + t4_wn<BF16>(vb + xx * Gm::RUNB);
+        if (h == 1) t[16] = sx[15] + t4_wn<BF16>(vb + 16 * Gm::RUNB);  // x = 32
+      } else {
+        const int zl = hi, xx = lo + 1;
+        const unsigned char* vb = slot + mis + xx * Gm::RUNB + zl * kR * Gm::es + 16 * h * Gm::es;
+        const float* sy = st + zl * 32 + 16 * h;
+        // h = 0: the blank and labels 1..16; h = 1: labels 17..32 (row
+        // positions 0..16 from vb)
+        float w[17];
+        if constexpr (BF16) {
+          // nine aligned dwords and a funnel shift per pair: the row's
+          // 2-byte alignment varies by lane
+          typedef const __attribute__((address_space(3))) unsigned lds_u32;
+          const uintptr_t va = (uintptr_t)vb;
+          const unsigned char* b4 = (const unsigned char*)(va & ~(uintptr_t)3);
+          const unsigned sh = (unsigned)(va & 2) * 8;
+          unsigned d[9];
+#pragma unroll
+          for (int m = 0; m < 9; ++m) d[m] = *(lds_u32*)(b4 + 4 * m);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) {
+            const unsigned pr = __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
+            w[2 * m] = __uint_as_float(pr << 16);
+            w[2 * m + 1] = __uint_as_float(pr & 0xffff0000u);
+          }
+          w[16] = __uint_as_float((sh ? d[8] >> 16 : d[8] & 0xffffu) << 16);
+        } else {
+#pragma unroll
+          for (int y = 0; y <= 16; ++y) w[y] = t4_wn<BF16>(vb + y * Gm::es);
+        }
+        t[0] = h == 0 ? v + w[0] : -kInf;
+#pragma unroll
+        for (int y = 1; y <= 16; ++y) t[y] = w[y] + sy[y - 1];
+      }
+      float m = t[0];
+#pragma unroll
+      for (int u = 1; u < 17; ++u) m = fmaxf(m, t[u]);
+      const float c = __builtin_isfinite(m) ? m : 0.f;
+      const float l = c * kLog2e;
+      float ss = 0.f;
+#pragma unroll
+      for (int u = 0; u < 17; ++u) ss += lt_exp_off(t[u], l);
+      const float co = __shfl_xor(c, 1), so = __shfl_xor(ss, 1);
+      const float cc = fmaxf(ss > 0.f ? c : -kInf, so > 0.f ? co : -kInf);
+      const float cf = __builtin_isfinite(cc) ? cc : 0.f;
+      const float tot = ss * lt_exp(c - cf) + so * lt_exp(co - cf);
+      // the pair adds in lane order, so both lanes hold the same value
+      const float tot2 = h == 0 ? tot : so * lt_exp(co - cf) + ss * lt_exp(c - cf);
+      r = (cf + lt_log(tot2)) - sp;
+      if (lead) {
+        t4_pub(&X[(i + 1) & 1][k][REV ? lo * 8 + hi : hi * 32 + lo], t4_word((unsigned)(i + 1), r),
+               same_xcd);
+        hv[((i + 1) & 1) * 272 + li] = r;  // its checkpoint row: the writer wave
+      }
+      v = r;
+    } else if (p >= 0) {  // the aux wave's states
+      if (!REV) {
+        if (lane < 8) {  // order-1 state 1 + 8k + lane
           const float tb = v + t4_w<BF16>(slot + mis + lane * kR * Gm::es);
           const float tl = a0 + t4_w<BF16>(row0 + p * Gm::es);
           r = log_plus(tb, tl) - sp;
@@ -574,13 +698,7 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
       } else {
         float x[33];
         float tb;
-        if (wave < 4) {  // source (x, z): row (x, z) of run x, labels in natural order
-          const int zl = hi, xx = lo + 1;
-          const unsigned char* vb = slot + mis + xx * Gm::RUNB + zl * kR * Gm::es;
-          tb = v + t4_w<BF16>(vb);
-#pragma unroll
-          for (int y = 1; y <= 32; ++y) x[y - 1] = t4_w<BF16>(vb + y * Gm::es) + st[zl * 32 + y - 1];
-        } else if (lane < 8) {  // order-1 source z = 1 + 8k + lane: row z of run 0
+        if (lane < 8) {  // order-1 source z = 1 + 8k + lane: row z of run 0
           const unsigned char* vb = slot + mis + lane * kR * Gm::es;
           tb = v + t4_w<BF16>(vb);
 #pragma unroll
@@ -593,14 +711,9 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
         }
         x[32] = -kInf;
         r = t4_lse(tb, x, sp);
-        if (wave < 4)
-          t4_pub(&X[(i + 1) & 1][k][lo * 8 + hi], t4_word((unsigned)(i + 1), r), same_xcd);
-        else if (lane < 8)
-          t4_pub(&X[(i + 1) & 1][k][256 + lane], t4_word((unsigned)(i + 1), r), same_xcd);
-        // beta checkpoint: row f - 1 holds the vector after frame f - 1
-        if (writes_hist && a.beta && i < nf - 1)
-          a.beta[((long long)b * a.T + f - 1) * kC + p] = (O + sp) + r;
+        if (lane < 8) t4_pub(&X[(i + 1) & 1][k][256 + lane], t4_word((unsigned)(i + 1), r), same_xcd);
       }
+      hv[((i + 1) & 1) * 272 + li] = r;
       v = r;
     }
     // this member's max of the new vector (state 0: every forward member holds
@@ -611,12 +724,23 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
     O += sp;
     T4STAMP(a, q, k, wave, i, 3);
   }
-  if (wave == 5 || wave == 6) {
+  lds_barrier();  // the last step's values and offset, for the writer
+  if (wave == kT4Wr) {
+    // forward: the padding frames carry alpha_nf (lattices.py:460-461)
+    if (!REV && nf > 0 && !(abrt[0] | abrt[1])) {
+      O += spb[(nf - 1) & 1];
+      for (int t = nf; t < a.T; ++t) t4_rows<REV>(a, b, k, t, hv + (nf & 1) * 272, O, lane);
+    } else if (!REV && nf == 0) {
+      for (int t = 0; t < a.T; ++t) t4_rows<REV>(a, b, k, t, hv, 0.f, lane);
+    }
+    return;
+  }
+  if (loader) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the wave
     return;
   }
   const bool aborted = (*(volatile int*)abrt | *(volatile int*)(abrt + 1)) != 0;
-  if (wave == 7) {
+  if (wave == kT4Num) {
     if (numer) {
       if (aborted) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else nu.finish(a, b, lane);
@@ -634,18 +758,16 @@ LT_DEVINL void t4_member(const T4Args& a, const KArgs& ka, int q, int b, int k) 
   // ---- forward end: padding frames carry alpha_nf (lattices.py:460-461);
   // log_z = O + log sum_q exp(alpha_nf[q]) over the quad's states: every wave
   // of every member publishes its (max, sum), member 0 wave 0 combines them
-  if (p >= 0 && writes_hist && a.alpha)
-    for (int t = nf; t < a.T; ++t) a.alpha[((long long)b * a.T + t) * kC + p] = O + v;
-  const bool cnt = p > 0 || (p == 0 && k == 0);
+  const bool cnt = lead && (p > 0 || (p == 0 && k == 0));
   const float mx = gmax<6>(cnt ? v : -kInf, 6);
   const float c = __builtin_isfinite(mx) ? mx : 0.f;
   const float s = gsum<6>(cnt ? lt_exp(v - c) : 0.f, 6);
   if (lane == 0) {
-    t4_put(&g_t4.fin[b][5 * k + wave][0], t4_word(1u, c));
-    t4_put(&g_t4.fin[b][5 * k + wave][1], t4_word(1u, s));
+    t4_put(&g_t4.fin[b][9 * k + wave][0], t4_word(1u, c));
+    t4_put(&g_t4.fin[b][9 * k + wave][1], t4_word(1u, s));
   }
   if (k != 0 || wave != 0) return;
-  const bool want = lane < 20;
+  const bool want = lane < 36;
   const float pc = t4_take(&g_t4.fin[b][want ? lane : 0][0], 1u, want, abrt);
   const float ps = t4_take(&g_t4.fin[b][want ? lane : 0][1], 1u, want, abrt);
   float M = (want && ps > 0.f) ? pc : -kInf;
@@ -683,7 +805,9 @@ namespace lt_impl {
 // The quad design applies to V = 32 trigram Log checkpointing with B <= 32,
 // U < 128, while the 8B member workgroups fit the CUs at once.
 bool tri4_eligible(int V, int n, int B, int U, int cus) {
-  if (tune_int("LT_NO_TRI4", 0)) return false;
+  // measured slower than the one-workgroup recursions (header): only the
+  // diagnostic build runs it, on request (LT_TRI4=1)
+  if (!tune_int("LT_TRI4", 0)) return false;
   return V == 32 && n == 2 && B >= 1 && B <= kT4MaxB && U < 128 && 8 * B <= cus;
 }
 

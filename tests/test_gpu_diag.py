@@ -28,3 +28,15 @@ def test_chunk_handoff_timeout_route(cuda):
                      cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
   assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
   assert r.stdout.startswith('ok'), r.stdout[-2000:]
+
+
+def test_quad_trigram_recursions(cuda):
+  """The quad trigram recursions (lt_tri4.hip; diagnostic build only, they
+  measured slower than the one-workgroup kernel) still match the oracle."""
+  if not os.path.exists(DIAG):
+    pytest.skip('diagnostic build absent (make diag)')
+  env = dict(os.environ, LT_LIB_PATH=DIAG, LT_TRI4='1')
+  r = subprocess.run([sys.executable, os.path.join(ROOT, 'tests', 'diag_tri4_child.py')],
+                     cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+  assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+  assert r.stdout.startswith('ok'), r.stdout[-2000:]

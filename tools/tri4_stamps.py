@@ -13,8 +13,8 @@ sys.path.insert(0, ROOT)
 from last_torch_amd import _native as nat  # noqa: E402
 
 nat.LIB_PATH = os.path.join(ROOT, 'build', 'liblt_lattice_stamps.so')  # copied out of build/stamps
-W8 = 8
-NAMES = ['st0', 'st1', 'st2', 'st3', 'aux', 'ld0', 'ld1', 'num']
+W8 = 13
+NAMES = ['st%d' % w for w in range(8)] + ['aux', 'ld0', 'ld1', 'num', 'wr']
 
 
 def main():
