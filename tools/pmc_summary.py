@@ -42,6 +42,10 @@ def _kernel_key(name):
   if 'bwd_kernel' in name:
     args = name.split('bwd_kernel<', 1)[-1].split('>', 1)[0].split(',')
     return 'bwd_kernel_ck' if len(args) >= 6 and args[5].strip() == 'true' else 'bwd_kernel'
+  if 'tab_' in name:  # the general table kernels (lt_table.hip): their own names
+    import re
+    m = re.search(r'(tab_\w+)', name)
+    return m.group(1) if m else None
   for k in ('ck_ab_kernel', 'ck_combine_kernel', 'ck_marg_kernel',
             'fwd_kernel', 'marg_kernel', 'backtrace_kernel', 'num_scatter_kernel', 'pipe_kernel',
             'joint_weights_fb_kernel', 'joint_weights_kernel', 'joint_backward_kernel',

@@ -52,13 +52,19 @@ def run(name, table, K, B, T, U, dtype=torch.float32):
 
 
 def main():
+  # ONLY=fld2 (or fld1, dfa, fd): one workload (profiling runs)
   B, T, U = int(os.environ.get('B', 64)), 1000, 100
-  run('FrameLabelDependent(2) x FullNGram bigram V=32', full_ngram_table(32, 1), 2, B, T, U)
-  run('FrameLabelDependent(1) x FullNGram bigram V=32', full_ngram_table(32, 1), 1, B, T, U)
-  g = torch.Generator().manual_seed(1)
-  dfa = torch.randint(0, 64, (64, 32), generator=g, dtype=torch.int32)
-  run('FrameDependent x NextStateTable (random DFA, C=64, V=32)', dfa, 0, B, T, U)
-  run('FrameDependent x FullNGram bigram V=32 (table path)', full_ngram_table(32, 1), 0, B, T, U)
+  only = os.environ.get('ONLY')
+  if only in (None, 'fld2'):
+    run('FrameLabelDependent(2) x FullNGram bigram V=32', full_ngram_table(32, 1), 2, B, T, U)
+  if only in (None, 'fld1'):
+    run('FrameLabelDependent(1) x FullNGram bigram V=32', full_ngram_table(32, 1), 1, B, T, U)
+  if only in (None, 'dfa'):
+    g = torch.Generator().manual_seed(1)
+    dfa = torch.randint(0, 64, (64, 32), generator=g, dtype=torch.int32)
+    run('FrameDependent x NextStateTable (random DFA, C=64, V=32)', dfa, 0, B, T, U)
+  if only in (None, 'fd'):
+    run('FrameDependent x FullNGram bigram V=32 (table path)', full_ngram_table(32, 1), 0, B, T, U)
 
 
 if __name__ == '__main__':
