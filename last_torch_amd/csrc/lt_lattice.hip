@@ -60,6 +60,7 @@ struct MgArgs {
   int tiles;     // tiles per utterance
   unsigned mR, mF, mNK;  // magic multipliers for / (V+1), / FR, / NK
   int off_a, off_b, off_an, off_bn, off_arc, off_sub, off_nb, lds_bytes;
+  int dense;     // whole-frame tiles subtract the numerator through a per-element buffer
 };
 
 // n / d from the magic m = ceil(2^32 / d), corrected to exact.
@@ -182,7 +183,7 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   int* alink = aoff + NK;
   int* nbt = (int*)(lds + a.off_nb);      // [C] next_base (n >= 2)
   float* Sub = (float*)(lds + a.off_sub); // tpf == 1: [E] numerator marginals per element
-  const bool dense = a.do_num && !SLICED;
+  const bool dense = !SLICED && a.dense;
 
   // ---- phase 0: the first slice's W as 16-B units into registers; alpha /
   // beta (+num) rows and the arc table into LDS, once for every slice
@@ -751,9 +752,12 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
   m->off_an = off; off += do_num ? al16(4LL * m->F * NP) : 0;
   m->off_bn = off; off += do_num ? al16(4LL * m->F * NP) : 0;
   m->off_arc = off; off += do_num ? al16(8LL * NK) : 0;
-  // whole-frame tiles keep a dense numerator buffer (one float per element);
-  // frame slices (tpf > 1, large frames) rewrite the chain heads instead
-  m->off_sub = off; off += (do_num && m->tpf == 1) ? al16(4LL * m->F * FR) : 0;
+  // whole-frame tiles may keep a dense numerator buffer (one float per
+  // element); without it (and for frame slices, tpf > 1) the chain heads
+  // rewrite their elements after the tile's stores, and the tile's LDS is a
+  // quarter (more workgroups per CU)
+  m->dense = do_num && m->tpf == 1 && env_int("LT_MARG_DENSE", 1);
+  m->off_sub = off; off += m->dense ? al16(4LL * m->F * FR) : 0;
   m->lds_bytes = std::max(off, 16);
   if (off > kLdsMax) return fail(LT_EUNSUPPORTED, "marginal tile exceeds LDS");
   *grid = (long long)pb->batch * m->tiles;
