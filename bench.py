@@ -539,7 +539,7 @@ def main():
   ap.add_argument('--design', choices=['auto', 'checkpoints', 'recursion'], default='auto',
                   help='auto: lt_loss_grad (the chunked scan for the bigram); checkpoints / '
                        'recursion: the two-call lt_loss_forward + lt_loss_backward designs')
-  ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r04_pmc_summary.json'),
+  ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r05_pmc_summary.json'),
                   help='PMC summary (tools/pmc_summary.py) the traffic figure is read from')
   args = ap.parse_args()
 
