@@ -75,9 +75,11 @@ def make_inputs(B, T, U, V, C, device, seed, dtype=torch.float32):
 
 
 def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, checkpoints=True,
-              fused=False):
+              fused=False, settle_s=0.0, info=None):
   """Returns (wall seconds over `steps`, fwd ms list, bwd ms list, all-reduces
-  issued); fused:
+  issued). settle_s: untimed steps for that long before the `warmup` steps,
+  while the GPU's clock settles under the load (info['settle_calls'] counts
+  them); fused:
   lt_loss_grad in one C-ABI call (fwd list; bwd list empty), else
   lt_loss_forward (fwd list) + lt_loss_backward (bwd list)."""
   grad = torch.ones([W.shape[0]], dtype=torch.float32, device=W.device)
@@ -110,6 +112,19 @@ def run_steps(W, nf, labels, nl, V, n, steps, warmup, dist_on, events=True, chec
       bucket.all_reduce_step(loss)
     return dW
 
+  # the shader clock under this load rises from ~2.2 to ~2.39 GHz over the
+  # first 25-50 calls after an idle GPU (a probe beside the calls,
+  # profiles/r05_warmup_probe.jsonl): the timed steps measure the sustained
+  # rate, so the load runs until the clock has settled first
+  settle_calls = 0
+  t_settle = time.perf_counter()
+  while time.perf_counter() - t_settle < settle_s:
+    step()
+    settle_calls += 1
+    if settle_calls % 8 == 0:
+      torch.cuda.synchronize()
+  if info is not None:
+    info['settle_calls'] = settle_calls
   for _ in range(warmup):
     step()
   torch.cuda.synchronize()
@@ -510,9 +525,8 @@ def cpu_dist_step(args, world, rank):
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
-  # the defaults time the sustained rate: the first calls of a process run at
-  # a lower clock (0.361 ms/step at --warmup 3 --steps 20 against 0.336 ms at
-  # 20 / 100 on one box, profiles/r04_bench_warmup.txt); 120 calls take < 0.1 s
+  # the defaults time the sustained rate (--settle-ms below: the clock under
+  # load settles over the first 25-50 calls); 120 calls take < 0.1 s
   ap.add_argument('--steps', type=int, default=100)
   ap.add_argument('--warmup', type=int, default=20)
   ap.add_argument('--batch', type=int, default=64, help='utterances per GPU')
@@ -539,6 +553,9 @@ def main():
   ap.add_argument('--design', choices=['auto', 'checkpoints', 'recursion'], default='auto',
                   help='auto: lt_loss_grad (the chunked scan for the bigram); checkpoints / '
                        'recursion: the two-call lt_loss_forward + lt_loss_backward designs')
+  ap.add_argument('--settle-ms', type=float, default=60.0,
+                  help='untimed calls for this long before the warmup steps, while the GPU clock '
+                       'settles under the load (reported as settle_ms / settle_calls; 0: none)')
   ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'r05_pmc_summary.json'),
                   help='PMC summary (tools/pmc_summary.py) the traffic figure is read from')
   args = ap.parse_args()
@@ -588,8 +605,10 @@ def main():
   nf, labels, nl = (x[idx].to(device) for x in (nf_g, lab_g, nl_g))
   fused = args.design == 'auto'
   ckpt = args.design == 'checkpoints'
+  settle = {}
   wall, fwd_ms, bwd_ms, calls = run_steps(W, nf, labels, nl, V, n, args.steps, args.warmup,
-                                          dist_on, checkpoints=ckpt, fused=fused)
+                                          dist_on, checkpoints=ckpt, fused=fused,
+                                          settle_s=args.settle_ms * 1e-3, info=settle)
 
   t = torch.tensor([wall], dtype=torch.float64, device=device)
   if dist_on:
@@ -631,6 +650,8 @@ def main():
         'rccl_world_size': rccl_world,
         'steps': args.steps,
         'warmup': args.warmup,
+        'settle_ms': args.settle_ms,
+        'settle_calls': settle.get('settle_calls', 0),
         'ms_per_step': wall / args.steps * 1e3,
         'higher_is_better': True,
         'scaling': 'weak',
@@ -674,7 +695,7 @@ def main():
     steps2 = max(5, args.steps // 2)
     # warmup calls: the freshly allocated 1.1 GB W's first passes run slower
     wall2, f2, b2, _ = run_steps(W2, nf2, lab2, nl2, V, n, steps2, max(5, args.warmup), False,
-                                 checkpoints=ckpt, fused=fused)
+                                 checkpoints=ckpt, fused=fused, settle_s=args.settle_ms * 1e-3)
     ms2 = wall2 / steps2 * 1e3
     call2 = float(np.mean(f2)) + (float(np.mean(b2)) if b2 else 0.0)
     result['north_star_b256'] = {

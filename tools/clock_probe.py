@@ -79,6 +79,30 @@ def main():
   run('first calls of the process')
   time.sleep(2.0)
   run('after 2 s idle')
+  # the clock DURING the calls: the probe on a second stream, launched right
+  # behind each call and spinning about as long as the call (one wave on one
+  # CU beside the call's workgroups)
+  side = torch.cuda.Stream()
+  time.sleep(2.0)
+  torch.cuda.synchronize()
+  for i in range(n):
+    ev[i][0].record()
+    _native.loss_grad(W, nf, lab, nl, V, 1, False, workspace=ws)
+    ev[i][1].record()
+    with torch.cuda.stream(side):
+      probe.clock_probe(ctypes.c_void_p(clk[i].data_ptr()), 600000, ctypes.c_void_p(chain.data_ptr()),
+                        ctypes.c_void_p(side.cuda_stream))
+    torch.cuda.current_stream().wait_stream(side)
+  torch.cuda.synchronize()
+  c = clk.cpu().numpy()
+  mhz = c[:, 0] / np.maximum(c[:, 1], 1) * 100.0
+  ms = np.array([a.elapsed_time(b) for a, b in ev])
+  for lo, hi in ((0, 5), (5, 25), (25, 50), (50, 100), (100, 200)):
+    if hi <= n:
+      print(json.dumps({'phase': 'clock during the calls (side stream), after 2 s idle',
+                        'calls': f'{lo}-{hi - 1}',
+                        'shader_clock_mhz_median': round(float(np.median(mhz[lo:hi])), 1),
+                        'call_ms_median': round(float(np.median(ms[lo:hi])), 4)}), flush=True)
 
 
 if __name__ == '__main__':
