@@ -60,7 +60,12 @@ struct MgArgs {
   int tiles;     // tiles per utterance
   unsigned mR, mF, mNK;  // magic multipliers for / (V+1), / FR, / NK
   int off_a, off_b, off_an, off_bn, off_arc, off_sub, off_nb, lds_bytes;
-  int dense;     // whole-frame tiles subtract the numerator through a per-element buffer
+  // how a tile subtracts the numerator marginals (do_num): 0 the chain heads
+  // rewrite their elements after the tile's stores; 1 (whole-frame tiles) a
+  // dense per-element buffer; 2 a bit per element marks the heads, whose sums
+  // sit in a compact array by rank (the den pass subtracts before its store)
+  int nmode;
+  int off_hm, off_hp, off_hv;
 };
 
 // n / d from the magic m = ceil(2^32 / d), corrected to exact.
@@ -182,8 +187,12 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   int* aoff = (int*)(lds + a.off_arc);    // [NK] offsets, then [NK] links
   int* alink = aoff + NK;
   int* nbt = (int*)(lds + a.off_nb);      // [C] next_base (n >= 2)
-  float* Sub = (float*)(lds + a.off_sub); // tpf == 1: [E] numerator marginals per element
-  const bool dense = !SLICED && a.dense;
+  float* Sub = (float*)(lds + a.off_sub); // nmode 1: [E] numerator marginals per element
+  const bool dense = !SLICED && a.do_num && a.nmode == 1;
+  const bool sparse = a.do_num && a.nmode == 2;
+  unsigned* hm = (unsigned*)(lds + a.off_hm);  // nmode 2: a bit per tile element (chain heads)
+  int* hp = (int*)(lds + a.off_hp);            // nmode 2: exclusive popcount prefix of hm
+  float* hv = (float*)(lds + a.off_hv);        // nmode 2: the heads' numerator marginals by rank
 
   // ---- phase 0: the first slice's W as 16-B units into registers; alpha /
   // beta (+num) rows and the arc table into LDS, once for every slice
@@ -239,6 +248,9 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
     float4* S4 = (float4*)Sub;  // the region is padded to 16 bytes
     for (int e = tid; e < (x.E + 3) / 4; e += nthr) S4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  const int nhw = (x.E + 31) >> 5;  // words of the head bits
+  if (sparse)
+    for (int w = tid; w < nhw; w += nthr) hm[w] = 0u;
   __syncthreads();
 
   const bool den = a.do_den;
@@ -284,6 +296,48 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
       const int i = tid + r * 256;
       hel[r] = i < nI ? head(x, i, hf[r], hk[r]) : -1;
       if (hel[r] >= 0) hw[r] = ldw<BF16>(Wb, hel[r]);
+    }
+    // rank of a head element among the tile's heads (nmode 2)
+    auto hrank = [&](int el) {
+      return hp[el >> 5] + __builtin_popcount(hm[el >> 5] & ((1u << (el & 31)) - 1u));
+    };
+    if (sparse) {
+      // the heads' bits, the prefix of their counts (wave 0), then each
+      // head's numerator sum at its rank; three barriers, no buffer per element
+#pragma unroll
+      for (int r = 0; r < NH; ++r)
+        if (hel[r] >= 0) atomicOr(&hm[hel[r] >> 5], 1u << (hel[r] & 31));
+      for (int i = tid + NH * 256; i < nI; i += nthr) {
+        int f, k;
+        const int el = head(x, i, f, k);
+        if (el >= 0) atomicOr(&hm[el >> 5], 1u << (el & 31));
+      }
+      __syncthreads();
+      if (tid < 64) {
+        int carry = 0;
+        for (int c0 = 0; c0 < nhw; c0 += 64) {
+          const int w = c0 + tid;
+          const int pc = w < nhw ? __builtin_popcount(hm[w]) : 0;
+          int inc = pc;
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(inc, d);
+            if (tid >= d) inc += o;
+          }
+          if (w < nhw) hp[w] = carry + inc - pc;
+          carry += __shfl(inc, 63);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < NH; ++r)
+        if (hel[r] >= 0) hv[hrank(hel[r])] = chain(hf[r], hk[r], hw[r]);
+      for (int i = tid + NH * 256; i < nI; i += nthr) {
+        int f, k;
+        const int el = head(x, i, f, k);
+        if (el >= 0) hv[hrank(el)] = chain(f, k, ldw<BF16>(Wb, el));
+      }
+      __syncthreads();
     }
     if (dense) {  // whole frames: the chains' sums into Sub before the den pass
 #pragma unroll
@@ -354,6 +408,16 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
         if (dense) {
 #pragma unroll
           for (int c = 0; c < VE; ++c) v[r][c] -= Sub[x.h0 + u * VE + c];
+        } else if (sparse) {
+          const int e0 = x.h0 + u * VE, w0 = e0 >> 5, sh = e0 & 31;
+          unsigned bits = hm[w0] >> sh;
+          if (sh + VE > 32) bits |= hm[w0 + 1] << (32 - sh);
+          bits &= (1u << VE) - 1u;
+          if (bits) {
+#pragma unroll
+            for (int c = 0; c < VE; ++c)
+              if ((bits >> c) & 1u) v[r][c] -= hv[hrank(e0 + c)];
+          }
         }
         store_unit<BF16>(dWu + (long long)u * 16, v[r]);
       }
@@ -366,10 +430,11 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
       if (f < Fl) {
         if (den) xv = den_el(f, x.e_lo + e - f * x.Ew, ldw<BF16>(Wb, e));
         if (dense) xv -= Sub[e];
+        else if (sparse && ((hm[e >> 5] >> (e & 31)) & 1u)) xv -= hv[hrank(e)];
       }
       stw<BF16>(a.dW, x.base + e, xv);
     }
-    if (!a.do_num || dense) return;
+    if (!a.do_num || dense || sparse) return;
 
     // ---- phase 2 (frame slices): the chain heads rewrite their elements as
     // den - num once the slice's own stores have completed in every wave
@@ -756,8 +821,16 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
   // element); without it (and for frame slices, tpf > 1) the chain heads
   // rewrite their elements after the tile's stores, and the tile's LDS is a
   // quarter (more workgroups per CU)
-  m->dense = do_num && m->tpf == 1 && env_int("LT_MARG_DENSE", 1);
-  m->off_sub = off; off += m->dense ? al16(4LL * m->F * FR) : 0;
+  m->nmode = do_num ? env_int("LT_MARG_NMODE", 1) : 0;
+  if (m->nmode == 1 && m->tpf != 1) m->nmode = 0;  // no dense buffer for frame slices
+  m->off_sub = off; off += m->nmode == 1 ? al16(4LL * m->F * FR) : 0;
+  {
+    const long long E = m->tpf == 1 ? (long long)m->F * FR : m->TS;
+    const int nhw = (int)((E + 31) / 32);
+    m->off_hm = off; off += m->nmode == 2 ? al16(4LL * nhw) : 0;
+    m->off_hp = off; off += m->nmode == 2 ? al16(4LL * nhw) : 0;
+    m->off_hv = off; off += m->nmode == 2 ? al16(4LL * m->F * NK) : 0;
+  }
   m->lds_bytes = std::max(off, 16);
   if (off > kLdsMax) return fail(LT_EUNSUPPORTED, "marginal tile exceeds LDS");
   *grid = (long long)pb->batch * m->tiles;
