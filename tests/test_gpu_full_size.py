@@ -175,14 +175,15 @@ def test_cfg2_realistic_weights(cuda, kind):
 
 @pytest.mark.parametrize('design', ['auto', 'chunk', 'fused'])
 def test_north_star_b256(cuda, design):
-  """B=256 (the north-star shape): sampled utterances against the oracle and
-  the per-frame marginal sums of all of them -- the design lt_loss_grad picks
+  """B=256 (the north-star shape): sixteen utterances spread over the batch
+  (every quarter, both ends, neighbours of the 8-block XCD groups) against the
+  oracle, every dW element, and the per-frame marginal sums of all of them -- the design lt_loss_grad picks
   there (what bench.py times), the chunked scan and the one-launch fused pipe
   (lt_loss_grad_ex; its 2B recursion workgroups co-resident on 256 CUs)."""
   V, n = 32, 1
   d = {'auto': nat.DESIGN_AUTO, 'chunk': nat.DESIGN_CHUNK, 'fused': nat.DESIGN_FUSED_PIPE}[design]
   W, nf, lab, nl = _bench_inputs(256, 1000, 100, V, n, cuda, seed=99)
-  loss, lz, num, dW = _check_loss_grad(W, nf, lab, nl, V, n, idx=[0, 1, 63, 64, 128, 200, 254, 255],
+  loss, lz, num, dW = _check_loss_grad(W, nf, lab, nl, V, n, idx=[0, 1, 7, 8, 31, 63, 64, 95, 127, 128, 159, 191, 200, 223, 254, 255],
                                        design=d)
   s = _frame_sums(dW)
   assert (s.abs() <= _frame_sum_tol(lz, num)).all()
