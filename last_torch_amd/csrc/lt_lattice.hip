@@ -66,6 +66,7 @@ struct MgArgs {
   // sit in a compact array by rank (the den pass subtracts before its store)
   int nmode;
   int off_hm, off_hp, off_hv;
+  int xcd;       // frame slices: the tpf slices of a frame on one XCD (blocks 8 apart)
 };
 
 // n / d from the magic m = ceil(2^32 / d), corrected to exact.
@@ -459,7 +460,17 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
 template <bool BF16, bool SLICED>
 __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  marg_tile<BF16, SLICED>(a, (int)blockIdx.x, lds);
+  int job = (int)blockIdx.x;
+  if (SLICED && a.xcd) {
+    // blocks 8 g tpf + 8 s + x take slice s of frame 8 g + x: a frame's
+    // slices 8 block ids apart, so under round-robin dispatch they share one
+    // XCD's L2 for the frame's alpha / beta rows, which each of them reads
+    // (placement changes only speed)
+    const int gs = 8 * a.tpf, g = job / gs, r = job - g * gs;
+    job = (8 * g + (r & 7)) * a.tpf + (r >> 3);
+    if (job >= a.B * a.tiles) return;
+  }
+  marg_tile<BF16, SLICED>(a, job, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -834,6 +845,11 @@ int plan_marg(const lt_problem* pb, const NGram& g, bool do_den, bool do_num, Mg
   m->lds_bytes = std::max(off, 16);
   if (off > kLdsMax) return fail(LT_EUNSUPPORTED, "marginal tile exceeds LDS");
   *grid = (long long)pb->batch * m->tiles;
+  m->xcd = m->tpf > 1 ? env_int("LT_MARG_XCD", 0) : 0;  // measured: no change at cfg5
+  if (m->xcd) {  // whole groups of eight frames (the padding blocks return)
+    const long long frames = (long long)pb->batch * pb->max_frames;
+    *grid = (frames + 7) / 8 * 8 * m->tpf;
+  }
   if (*grid > 0x7fffffffLL) return fail(LT_EUNSUPPORTED, "marginal grid too large");
   return LT_OK;
 }
