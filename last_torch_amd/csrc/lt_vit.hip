@@ -223,7 +223,10 @@ LT_DEVINL void backtrace_body(const VbtArgs& a, int b, int tid, unsigned char* l
 #define LT_VIT_BPW 2
 #endif
 #ifndef LT_VIT_PUB
-#define LT_VIT_PUB 4
+#define LT_VIT_PUB 2
+#endif
+#ifndef LT_VIT_NAP
+#define LT_VIT_NAP 4  // s_sleep count of the followers' progress polls
 #endif
 #ifndef LT_VIT_TW
 #define LT_VIT_TW 16
@@ -343,7 +346,10 @@ __global__ __launch_bounds__(64 * (2 + kBpWaves)) void vit_split_kernel(const Vi
       const int v = __builtin_amdgcn_readfirstlane(
           __hip_atomic_load(&s_prog[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
       if (v >= want) break;
-      __builtin_amdgcn_s_sleep(1);
+      // the followers (loader, backpointer waves) poll less often: each poll
+      // is an LDS instruction beside the chain's round trips
+      if (wave == 0) __builtin_amdgcn_s_sleep(1);
+      else __builtin_amdgcn_s_sleep(LT_VIT_NAP);
     }
     if (n == kWaitSpins && lane == 0) s_err = 1;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
