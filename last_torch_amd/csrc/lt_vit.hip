@@ -225,6 +225,9 @@ LT_DEVINL void backtrace_body(const VbtArgs& a, int b, int tid, unsigned char* l
 #ifndef LT_VIT_PUB
 #define LT_VIT_PUB 2
 #endif
+#ifndef LT_VIT_PUBWAIT
+#define LT_VIT_PUBWAIT 1  // the chain's progress store waits for its row store
+#endif
 #ifndef LT_VIT_NAP
 #define LT_VIT_NAP 4  // s_sleep count of the followers' progress polls
 #endif
@@ -405,7 +408,19 @@ __global__ __launch_bounds__(64 * (2 + kBpWaves)) void vit_split_kernel(const Vi
       a0 += w00;
       const int wslot = h == 0 ? (live ? aslot(q) : 40 + j) : (lane == 32 ? 0 : 40 + j);
       anxt[wslot] = lane == 32 ? a0 : r;
-      if ((t + 1) % kPub == 0 || t + 1 == nf) publish(0, t + 1);
+      if ((t + 1) % kPub == 0 || t + 1 == nf) {
+        if (LT_VIT_PUBWAIT) {
+          publish(0, t + 1);
+        } else {
+          // the row store above and this progress store are LDS writes of
+          // one wave, which the LDS performs in issue order: a follower that
+          // reads the progress and then the row sees the row without this
+          // wave waiting for its store (the asm keeps the compiler's order)
+          asm volatile("" ::: "memory");
+          if (lane == 0)
+            __hip_atomic_store(&s_prog[0], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
       VSTAMP(t, 2);
       // step t + 1's operands: alpha_{t+1} read right behind its store (LDS
       // keeps a wave's order), its latency under the rest of the step, then
