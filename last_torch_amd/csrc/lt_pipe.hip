@@ -148,13 +148,21 @@ LT_DEVINL __attribute__((address_space(3))) unsigned char* as3(unsigned char* p)
 }
 
 // Bounded wait until *p >= v (LDS word written by another wave). Returns
-// false (and raises the abort flag) on timeout or abort.
+// false (and raises the abort flag) on timeout or abort. NAP is the s_sleep
+// argument between polls (64 clocks each): the recursion waves poll with 1;
+// the helper and marginal waves, which run ahead of or behind the chain with
+// slack, may nap longer (LT_PIPE_NAP) so their polls take fewer issue slots
+// from the chain on the same SIMD.
+#ifndef LT_PIPE_NAP
+#define LT_PIPE_NAP 1
+#endif
+template <int NAP = 1>
 LT_DEVINL bool wait_ge(lds_vint* p, int v, lds_vint* abort_flag, int* err) {
   int n = 0;
   while (*p < v) {
     if (*abort_flag) return false;
-    __builtin_amdgcn_s_sleep(1);
-    if (++n > (1 << 21)) {
+    __builtin_amdgcn_s_sleep(NAP);
+    if (++n > (1 << 21) / NAP) {
       *abort_flag = 1;
       if (err) atomicOr(err, 1);
       return false;
@@ -760,16 +768,16 @@ LT_DEVINL void helper_pipe(const PArgs& a, unsigned char* lds, int b, int nf, in
     PSTAMP(a, 2 + hw, i, 0);
     if (need > 0) {
       if (seen_den < need) {
-        if (!wait_ge(ctl + CTL_DEN, need, ctl + CTL_ABORT, a.err)) return false;
+        if (!wait_ge<LT_PIPE_NAP>(ctl + CTL_DEN, need, ctl + CTL_ABORT, a.err)) return false;
         seen_den = ctl[CTL_DEN];
       }
       if (seen_num < need) {
-        if (!wait_ge(ctl + CTL_NUM, need, ctl + CTL_ABORT, a.err)) return false;
+        if (!wait_ge<LT_PIPE_NAP>(ctl + CTL_NUM, need, ctl + CTL_ABORT, a.err)) return false;
         seen_num = ctl[CTL_NUM];
       }
       // mid mode: the marginal wave of the slot's previous step (need - 1)
       if (a.mid && need - 1 >= s0 &&
-          !wait_ge(ctl + CTL_MRG + (need - 1 - s0) % a.NM, need, ctl + CTL_ABORT, a.err))
+          !wait_ge<LT_PIPE_NAP>(ctl + CTL_MRG + (need - 1 - s0) % a.NM, need, ctl + CTL_ABORT, a.err))
         return false;
     }
     PSTAMP(a, 2 + hw, i, 1);
@@ -888,11 +896,11 @@ LT_DEVINL void helper_prod(const PArgs& a, unsigned char* lds, int b, int nf, in
     const int need = i - a.K + 1;  // the slot's previous frame (step i - K) must be consumed
     if (need > 0) {
       if (seen_den < need) {
-        if (!wait_ge(ctl + CTL_DEN, need, ctl + CTL_ABORT, a.err)) break;
+        if (!wait_ge<LT_PIPE_NAP>(ctl + CTL_DEN, need, ctl + CTL_ABORT, a.err)) break;
         seen_den = ctl[CTL_DEN];
       }
       if (seen_num < need) {
-        if (!wait_ge(ctl + CTL_NUM, need, ctl + CTL_ABORT, a.err)) break;
+        if (!wait_ge<LT_PIPE_NAP>(ctl + CTL_NUM, need, ctl + CTL_ABORT, a.err)) break;
         seen_num = ctl[CTL_NUM];
       }
     }
@@ -1115,8 +1123,8 @@ LT_DEVINL void mid_marg(const PArgs& a, unsigned char* lds, int b, int nf, int m
     const int t = REV ? nf - 1 - i : i;
     const int slot = i % a.K;
     // the own recursions are past step i: their rows of the step are in the rings
-    if (do_den && !wait_ge(ctl + CTL_DEN, i + 1, ctl + CTL_ABORT, a.err)) break;
-    if (!wait_ge(ctl + CTL_NUM, i + 1, ctl + CTL_ABORT, a.err)) break;
+    if (do_den && !wait_ge<LT_PIPE_NAP>(ctl + CTL_DEN, i + 1, ctl + CTL_ABORT, a.err)) break;
+    if (!wait_ge<LT_PIPE_NAP>(ctl + CTL_NUM, i + 1, ctl + CTL_ABORT, a.err)) break;
     // the other direction's rows of frame t: the prefetched granules, else
     // poll until every lane's tag matches (bounded; an abort drains)
     const unsigned tag = a.epoch * (unsigned)T + (unsigned)t;
