@@ -74,6 +74,12 @@ constexpr float kCert = 64.f;   // phase C's per-frame certificate: log2(max alp
 #endif
 constexpr int kAbWaves = LT_AB_WAVES;  // ck_ab_kernel: waves per SIMD its registers allow
 constexpr unsigned kSpinMax = 1u << 20;
+#ifndef LT_CK_ROT
+#define LT_CK_ROT 1
+#endif
+#ifndef LT_CK_PF
+#define LT_CK_PF 0
+#endif
 #ifndef LT_WALK_SLOTS
 #define LT_WALK_SLOTS 3
 #endif
@@ -129,6 +135,7 @@ struct CkArgs {
   int strict;              // 1 (lt_chunk_forward): a chunk outside the strict range (flag 3)
                            // leaves the fast path in B; 0: phase C's certificate decides
   int dbg;                 // diagnostic builds (LT_DIAG) only: role ablations
+  int pf;                  // phase C: prefetch distance in blocks (0: none), LT_CK_PF
   long long* stamps;       // diagnostic builds only: per-workgroup s_memtime marks
   long long FB;            // bytes per frame
   // phase A per-wave LDS carve
@@ -229,6 +236,31 @@ LT_DEVINL void dma_issue(const unsigned char* base, long long off, long long byt
     int g = lane + 64 * i;
     g = g < n16 ? g : n16 - 1;
     glds16(base + a0 + 16LL * g, lds_addr + 1024u * i);
+  }
+}
+
+// One LDS-DMA dword per 128-byte line of [off, off + bytes) of `base`, every
+// lane's dword landing in the same 256-byte LDS scratch (discarded): the
+// lines come into the XCD's L2 (and the memory-side cache) for a block that
+// will stage them later. 8 KiB of lines per wave instruction.
+LT_DEVINL void pf_lines(const unsigned char* base, long long off, long long bytes,
+                        unsigned lds_addr, int lane) {
+  const long long a0 = off & ~127LL;
+  const int nl = (int)((off + bytes - a0 + 127) >> 7);
+  lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+  for (int i = 0; 64 * i < nl; ++i) {
+    const int g = min(lane + 64 * i, nl - 1);
+    const void* src = base + a0 + 128LL * g;
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(lds_addr)
+        : "memory");
   }
 }
 
@@ -1288,7 +1320,9 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (a.cont && (int)blockIdx.x < a.B) {  // phase 2 of utterance blockIdx.x's walks
+    CK_STAMP(0);
     combine_role<PPL, kWalkDc<PPL>>(a, blockIdx.x, wave, lds, kWalkRest);
+    CK_STAMP(4);
     return;
   }
   // level j of utterance b: chunks middle-out (Kh, Kh - 1, Kh + 1, Kh - 2,
@@ -1367,6 +1401,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       __builtin_amdgcn_s_sleep(2);
     }
     acquire_agent();
+    CK_STAMP(6);
     fl[2 * a.L + 2] = ok;
   }
   gather_tables(a, b, labs, boff, loff, tid, blockDim.x);
@@ -1445,6 +1480,11 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_fetch_or(fl + f, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
+  // the recursion roles rotate over the waves by workgroup (LT_CK_ROT), so
+  // the two den chains of the workgroups sharing a CU need not sit on the
+  // same two SIMDs
+  const int role = LT_CK_ROT == 1 ? (wave + (int)(blockIdx.x >> 3)) & 3
+                 : LT_CK_ROT == 2 ? (wave + (int)blockIdx.x) & 3 : wave;
   auto mark_all = [&](int bit) {
     for (int f = 0; f < nt; ++f) mark(f, bit);
   };
@@ -1458,7 +1498,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
 
-  if (wave == 0 && !a.local && !LT_ABL(a, 4)) {
+  if (role == 0 && !a.local && !LT_ABL(a, 4)) {
     // ---- den alpha in scaled linear space. Lane p in [1, V]: alpha_f[p] =
     // al 2^S (log2 units relative to the walk's offset); each frame the
     // vector is taken over its own max, xa = alpha_f / 2^Ma with Ma = S + the
@@ -1539,7 +1579,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       __builtin_amdgcn_wave_barrier();
       mark(f, kFlA);
     }
-  } else if (wave == 1 && !a.local && !LT_ABL(a, 4)) {
+  } else if (role == 1 && !a.local && !LT_ABL(a, 4)) {
     // ---- den beta, the same scaled linear space; frame f gets beta_{f+1}.
     // Each frame the core vector over its own max: xb = beta_{f+1} / 2^Mb;
     // the step runs on xb. Lane (j, h): core source j+1 over labels y in
@@ -1614,7 +1654,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       __builtin_amdgcn_wave_barrier();
       mark(f, kFlB);
     }
-  } else if (wave == 2 && !LT_ABL(a, 8)) {
+  } else if (role == 2 && !LT_ABL(a, 8)) {
     // ---- num alpha (log2): al'[u] = al[u] + blank(u) (+) al[u-1] + arc(u)
     float al[PPL];
     const float* src = a.nabd + ((long long)b * (a.K + 1) + k) * NPG;
@@ -1641,7 +1681,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       __builtin_amdgcn_wave_barrier();
       mark(f, kFlNA);
     }
-  } else if (wave == 3 && !LT_ABL(a, 8)) {
+  } else if (role == 3 && !LT_ABL(a, 8)) {
     // ---- num beta (log2); frame f gets beta_{f+1}
     float be[PPL];
     const float* src = a.nbbd + ((long long)b * (a.K + 1) + k + 1) * NPG;
@@ -1650,6 +1690,20 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       const int u = lane + 64 * r, uc = min(u, NPG - 1);
       const float v = src[uc];
       be[r] = u < NPG ? v : -kInf;
+    }
+    if (a.pf) {  // the chunk of the block about a.pf dispatches later, into L2
+      const int c2 = c + a.pf;
+      if (c2 < a.B * a.K) {
+        const int j2 = c2 / a.B, b2 = c2 - j2 * a.B;
+        int nf2 = a.nfr[b2];
+        nf2 = nf2 < 0 ? 0 : (nf2 > a.T ? a.T : nf2);
+        const int Kl2 = (nf2 + a.L - 1) / a.L, Kh2 = Kl2 / 2;
+        const int k2 = j2 < 2 * Kh2 ? ((j2 & 1) ? Kh2 - 1 - (j2 >> 1) : Kh2 + (j2 >> 1)) : j2;
+        const int t02 = k2 * a.L, t12 = max(t02, min(t02 + a.L, nf2));
+        if (t12 > t02)
+          pf_lines(a.W, ((long long)b2 * a.T + t02) * FR * (BF16 ? 2 : 4),
+                   (long long)(t12 - t02) * a.FB, lds_base_addr((unsigned char*)buf), lane);
+      }
     }
     for (int f = nt - 1; f >= 0; --f) {
       float nx[PPL], nv[PPL];
@@ -1670,7 +1724,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       mark(f, kFlNB);
     }
   } else {  // a recursion this chunk does not run (local / ablations): nothing to wait for
-    mark_all(wave == 0 ? kFlA : wave == 1 ? kFlB : wave == 2 ? kFlNA : kFlNB);
+    mark_all(role == 0 ? kFlA : role == 1 ? kFlB : role == 2 ? kFlNA : kFlNB);
   }
   CK_STAMP(2);
 
@@ -1871,6 +1925,7 @@ int ck_plan(const lt_problem* pb, int local_norm, CkArgs* a, CkLayout* w) {
   a->local = local_norm ? 1 : 0;
 #ifdef LT_DIAG
   a->dbg = ck_env("LT_CK_DBG", 0);
+  a->pf = ck_env("LT_CK_PF", LT_CK_PF);
   if (const char* sp = lt_impl::tune_str("LT_CK_STAMPS")) a->stamps = (long long*)strtoull(sp, nullptr, 0);
 #endif
   a->FB = (long long)a->FR * es;
