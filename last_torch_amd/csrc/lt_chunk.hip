@@ -74,6 +74,9 @@ constexpr float kCert = 64.f;   // phase C's per-frame certificate: log2(max alp
 #endif
 constexpr int kAbWaves = LT_AB_WAVES;  // ck_ab_kernel: waves per SIMD its registers allow
 constexpr unsigned kSpinMax = 1u << 20;
+#ifndef LT_CK_SPLIT
+#define LT_CK_SPLIT 0
+#endif
 #ifndef LT_CK_ROT
 #define LT_CK_ROT 1
 #endif
@@ -261,6 +264,18 @@ LT_DEVINL void pf_lines(const unsigned char* base, long long off, long long byte
         : "=&s"(keep)
         : "v"(src), "s"(lds_addr)
         : "memory");
+  }
+}
+
+// dma_issue's copy, wave instructions [i0, i1) only (one wave)
+LT_DEVINL void dma_range(const unsigned char* base, long long off, long long bytes,
+                         unsigned lds_addr, int i0, int i1, int lane) {
+  const long long a0 = off & ~15LL;
+  const int n16 = (int)((off + bytes - a0 + 15) >> 4);
+  for (int i = i0; i < i1; ++i) {
+    int g = lane + 64 * i;
+    g = g < n16 ? g : n16 - 1;
+    glds16(base + a0 + 16LL * g, lds_addr + 1024u * i);
   }
 }
 
@@ -1361,9 +1376,28 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   }
   const int nt = t1 - t0;
   CK_STAMP(0);
+  // the recursion roles rotate over the waves by workgroup (LT_CK_ROT), so
+  // the two den chains of the workgroups sharing a CU need not sit on the
+  // same two SIMDs
+  const int role = LT_CK_ROT == 1 ? (wave + (int)(blockIdx.x >> 3)) & 3
+                 : LT_CK_ROT == 2 ? (wave + (int)blockIdx.x) & 3 : wave;
+  // split staging (LT_CK_SPLIT): each den chain stages the half of W it
+  // reads first (alpha frames [0, hs), beta [hs, nt)) and starts on it while
+  // the other waves gather the tables; the chains take the numerator's arc
+  // weights out of their own frames before forming E there, and the
+  // numerator waves follow the chains' frame bits. One barrier (tables,
+  // offsets, flags), not two, and no wave waits for the whole chunk's DMA.
+  const bool split = LT_CK_SPLIT && !a.local && !LT_ABL(a, 4 | 8);
+  const int hs = (nt + 1) / 2;
   // stage the chunk's live frames
   const long long off = e0 * (BF16 ? 2 : 4);
-  dma_issue(a.W, off, (long long)nt * a.FB, lds_base_addr(lds), a.c_ni, lane, wave, kMargWaves);
+  if (!split) {
+    dma_issue(a.W, off, (long long)nt * a.FB, lds_base_addr(lds), a.c_ni, lane, wave, kMargWaves);
+  } else if (role < 2) {
+    const int n1 = (int)(((off & 15) + (long long)hs * a.FB + 1023) >> 10);
+    dma_range(a.W, off, (long long)nt * a.FB, lds_base_addr(lds), role == 0 ? 0 : max(n1 - 1, 0),
+              role == 0 ? n1 : a.c_ni, lane);
+  }
   unsigned char* wch = lds + (off & 15);
   float* xa = (float*)(lds + a.c_off_ad);  // [L][CP] alpha_f, linear, max 1 (scale fs Ma)
   float* xb = (float*)(lds + a.c_off_bd);  // [L][CP] beta_{f+1} of the core, linear, max 1
@@ -1376,12 +1410,45 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   int* labs = loff + NPG;
   float* buf = (float*)(lds + a.c_off_buf) + 64 * wave;
   float* cfl = (float*)(lds + a.c_off_cf);
-  if (tid < nt) cfl[tid] = a.cf[(long long)b * a.T + t0 + tid];
   int* fl = (int*)(lds + a.c_off_fl);
+  int* ford = fl + a.L;
+  int* njob = ford + a.L;
+  int* cert_fail = njob + 1;  // a frame outside the certificate (any wave)
+  // per-frame progress bits for the marginal pass (kFl*), the frames in
+  // the order their inputs complete (middle first), a job counter
+  auto init_flags = [&](int t) {
+    if (t < nt) {
+      fl[t] = 0;
+      const int mid = (nt - 1) / 2;  // job j -> frames mid, mid+1, mid-1, mid+2, ...
+      const int k = (t + 1) / 2;
+      ford[t] = (t & 1) ? mid + k : mid - k;
+    }
+    if (t == 0) {
+      *njob = 0;
+      *cert_fail = 0;
+    }
+  };
+  // the split staging's tables, offsets and flags: the numerator waves
+  // (t2 = their thread in [0, 128)), the labels read by each of the two
+  if (split && role >= 2) {
+    const int t2 = (role - 2) * 64 + lane;
+    if (t2 < nt) cfl[t2] = a.cf[(long long)b * a.T + t0 + t2];
+    for (int j = lane; j < a.U; j += 64) labs[j] = a.labels[(long long)b * a.U + j];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    for (int u = t2; u < NPG; u += 128) {
+      int bo, lo;
+      string_offsets(a, labs, u, &bo, &lo);
+      boff[u] = bo < 0 ? 0 : bo;
+      loff[u] = lo;
+    }
+    init_flags(t2);
+  }
+  if (!split && tid < nt) cfl[tid] = a.cf[(long long)b * a.T + t0 + tid];
   // phase 2's boundaries this chunk needs (alpha at k, beta at k + 1): one
   // lane polls the walks' progress words, then the agent-scope acquire
-  // before any wave's loads of them (after the barriers below)
-  if (a.cont && tid == 0) {
+  // before any wave's loads of them (after the barriers below); split: a
+  // numerator wave's lane, whose loads do not queue behind the W DMA
+  if (a.cont && (split ? (role == 2 && lane == 0) : tid == 0)) {
     const int need_a = k - Kh, need_b = Kh - (k + 1);
     const unsigned long long* pg = a.prog + 4LL * b;
     int ok = 1;
@@ -1404,9 +1471,15 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     CK_STAMP(6);
     fl[2 * a.L + 2] = ok;
   }
-  gather_tables(a, b, labs, boff, loff, tid, blockDim.x);
-  wait_vmcnt(0);
-  __syncthreads();
+  if (!split) {
+    gather_tables(a, b, labs, boff, loff, tid, blockDim.x);
+    wait_vmcnt(0);
+    __syncthreads();
+  } else {  // LDS only: the den chains' W DMA stays in flight
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
   if (a.cont && !fl[2 * a.L + 2]) {
     if (tid == 0) a.uflag[b] = 1;
     return;
@@ -1420,7 +1493,6 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   // frames as E once that frame's bit is set. No pass and barrier of its
   // own, one exponential per element. The marginals read E_f and leave the
   // frame's dW in its place.
-  const int hs = (nt + 1) / 2;
   auto wrow = [&](int f) -> const unsigned char* { return wch + f * a.FB; };
   auto eptr = [&](int f) -> float* {
     return BF16 ? (float*)(lds + a.c_off_e) + f * FRP : (float*)(wch + f * a.FB);
@@ -1430,7 +1502,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   };
   // the numerator's arc weights leave W first (exact, log2); every read of
   // this pass issues before the barrier, every E store after it
-  {
+  if (!split) {
     float2 g2[4];
     const int nnw = nt * NPG;
 #pragma unroll
@@ -1453,23 +1525,24 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     for (int i = 0; i < 4; ++i)
       if (tid + 64 * kMargWaves * i < nnw) nw[tid + 64 * kMargWaves * i] = g2[i];
   }
-  if (tid < nt) fs[tid * kFs + kFsW00] = ldsw<BF16>(wch + tid * a.FB, 0) * kLog2e;
-  // per-frame progress bits for the marginal pass (kFl*), the frames in
-  // the order their inputs complete (middle first), a job counter
-  int* ford = fl + a.L;
-  int* njob = ford + a.L;
-  int* cert_fail = njob + 1;  // a frame outside the certificate (any wave)
-  if (tid < nt) {
-    fl[tid] = 0;
-    const int mid = (nt - 1) / 2;  // job j -> frames mid, mid+1, mid-1, mid+2, ...
-    const int k = (tid + 1) / 2;
-    ford[tid] = (tid & 1) ? mid + k : mid - k;
+  if (!split) {
+    if (tid < nt) fs[tid * kFs + kFsW00] = ldsw<BF16>(wch + tid * a.FB, 0) * kLog2e;
+    init_flags(tid);
+    __syncthreads();  // nw, fs, fl and the job order for every wave
   }
-  if (tid == 0) {
-    *njob = 0;
-    *cert_fail = 0;
-  }
-  __syncthreads();  // nw, fs, fl and the job order for every wave
+  // split: frame f's numerator arc weights and W00, taken by the den chain
+  // that owns f out of its W before E overwrites it (one wave, LDS in order)
+  auto own_arcs = [&](int f, const unsigned char* fr) -> float {
+    for (int u = lane; u < NPG; u += 64) {
+      const int lo = loff[u];
+      const float wb = ldsw<BF16>(fr, boff[u]), wl = ldsw<BF16>(fr, max(lo, 0));
+      nw[f * NPG + u] =
+          make_float2(u < NP ? wb * kLog2e : -kInf, (u >= 1 && u < NP) ? wl * kLog2e : -kInf);
+    }
+    const float w = ldsw<BF16>(fr, 0) * kLog2e;
+    if (lane == 0) fs[f * kFs + kFsW00] = w;
+    return w;
+  };
   CK_STAMP(5);
   // every LDS load below is unconditional (clamped index, unused values
   // masked afterwards): a load under a branch would pay its full latency
@@ -1480,11 +1553,6 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_fetch_or(fl + f, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  // the recursion roles rotate over the waves by workgroup (LT_CK_ROT), so
-  // the two den chains of the workgroups sharing a CU need not sit on the
-  // same two SIMDs
-  const int role = LT_CK_ROT == 1 ? (wave + (int)(blockIdx.x >> 3)) & 3
-                 : LT_CK_ROT == 2 ? (wave + (int)blockIdx.x) & 3 : wave;
   auto mark_all = [&](int bit) {
     for (int f = 0; f < nt; ++f) mark(f, bit);
   };
@@ -1518,13 +1586,15 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     float a0 = first_lane(x0);
     float S = wmax_u(core ? x0 : -kInf);  // -inf: no core state reached yet
     float al = (core && S != -kInf) ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
+    if (split) wait_vmcnt(0);  // this wave's half of W
     for (int f = 0; f < nt; ++f) {
       const unsigned char* fr = wrow(f);
       float* ef = eptr(f);
       const float cl = cfl[f];
-      const float w00 = fs[f * kFs + kFsW00];
+      float w00 = fs[f * kFs + kFsW00];
       float e[16], e32, eb;
       if (f < hs) {  // alpha's frame: E from W, stored to its home
+        if (split) w00 = own_arcs(f, fr);
 #pragma unroll
         for (int m = 0; m < 16; ++m) e[m] = ldsw<BF16>(fr, min(16 * h + m, C - 1) * R + qe);
         e32 = ldsw<BF16>(fr, min(32, C - 1) * R + qe);
@@ -1540,6 +1610,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         if (lane == 0) ef[0] = 0.f;  // (0, 0) is taken in log2 (xb[0] = 0)
       } else {       // beta's: E once beta has passed it
         wait_bits(f, kFlB);
+        if (split) w00 = fs[f * kFs + kFsW00];
 #pragma unroll
         for (int m = 0; m < 16; ++m) e[m] = ef[min(16 * h + m, C - 1) * R + qe];
         e32 = ef[min(32, C - 1) * R + qe];
@@ -1592,13 +1663,15 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     float b0 = first_lane(x0);
     float S = safe_max(wmax_u(core ? x0 : -kInf));
     float be = core ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
+    if (split) wait_vmcnt(0);  // this wave's half of W
     for (int f = nt - 1; f >= 0; --f) {
       const unsigned char* fr = wrow(f);
       float* ef = eptr(f);
       const float cl = cfl[f];
-      const float w00 = fs[f * kFs + kFsW00];
+      float w00 = fs[f * kFs + kFsW00];
       float e[16], eb, e0y;  // e0y = E[0][j+1]
       if (f >= hs) {  // beta's frame: E from W, stored to its home
+        if (split) w00 = own_arcs(f, fr);
 #pragma unroll
         for (int m = 0; m < 16; ++m) e[m] = ldsw<BF16>(fr, pe * R + min(16 * h + m + 1, V));
         eb = ldsw<BF16>(fr, pe * R);
@@ -1614,6 +1687,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         if (lane == 0) ef[0] = 0.f;
       } else {        // alpha's: E once alpha has passed it
         wait_bits(f, kFlA);
+        if (split) w00 = fs[f * kFs + kFsW00];
 #pragma unroll
         for (int m = 0; m < 16; ++m) e[m] = ef[pe * R + min(16 * h + m + 1, V)];
         eb = ef[pe * R];
@@ -1665,6 +1739,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       al[r] = u < NPG ? v : -kInf;
     }
     for (int f = 0; f < nt; ++f) {
+      if (split) wait_bits(f, f < hs ? kFlA : kFlB);  // nw[f] from its den chain
       float prev = -kInf, nv[PPL];
 #pragma unroll
       for (int r = 0; r < PPL; ++r) {
@@ -1706,6 +1781,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       }
     }
     for (int f = nt - 1; f >= 0; --f) {
+      if (split) wait_bits(f, f < hs ? kFlA : kFlB);
       float nx[PPL], nv[PPL];
 #pragma unroll
       for (int r = 0; r < PPL; ++r) nx[r] = rot_next(be[r]);
