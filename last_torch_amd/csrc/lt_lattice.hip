@@ -40,6 +40,16 @@ __global__ void num_scatter_kernel(const KArgs a) {
 // frame (large frames). Numerator entries that share an arc are summed by
 // the chain head in ascending order (deterministic).
 // ---------------------------------------------------------------------------
+// The marginal pass's experimental numerator mode 2 and XCD grouping exist
+// in diagnostic builds only: compiled into the product kernel they cost the
+// trigram slices 2.8 % even when off (cfg5 4.00 against 3.89 ms,
+// profiles/r05_marg_opts_ab.txt)
+#ifdef LT_DIAG
+#define LT_MARG_OPTS 1
+#else
+#define LT_MARG_OPTS 0
+#endif
+
 struct MgArgs {
   const unsigned char* W;
   const int* nfr;
@@ -190,7 +200,7 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   int* nbt = (int*)(lds + a.off_nb);      // [C] next_base (n >= 2)
   float* Sub = (float*)(lds + a.off_sub); // nmode 1: [E] numerator marginals per element
   const bool dense = !SLICED && a.do_num && a.nmode == 1;
-  const bool sparse = a.do_num && a.nmode == 2;
+  const bool sparse = LT_MARG_OPTS && a.do_num && a.nmode == 2;
   unsigned* hm = (unsigned*)(lds + a.off_hm);  // nmode 2: a bit per tile element (chain heads)
   int* hp = (int*)(lds + a.off_hp);            // nmode 2: exclusive popcount prefix of hm
   float* hv = (float*)(lds + a.off_hv);        // nmode 2: the heads' numerator marginals by rank
@@ -461,7 +471,7 @@ template <bool BF16, bool SLICED>
 __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   int job = (int)blockIdx.x;
-  if (SLICED && a.xcd) {
+  if (SLICED && LT_MARG_OPTS && a.xcd) {
     // blocks 8 g tpf + 8 s + x take slice s of frame 8 g + x: a frame's
     // slices 8 block ids apart, so under round-robin dispatch they share one
     // XCD's L2 for the frame's alpha / beta rows, which each of them reads
