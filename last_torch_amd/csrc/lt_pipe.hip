@@ -153,6 +153,9 @@ LT_DEVINL __attribute__((address_space(3))) unsigned char* as3(unsigned char* p)
 // the helper and marginal waves, which run ahead of or behind the chain with
 // slack, may nap longer (LT_PIPE_NAP) so their polls take fewer issue slots
 // from the chain on the same SIMD.
+#ifndef LT_PIPE_ROT
+#define LT_PIPE_ROT 0
+#endif
 #ifndef LT_PIPE_NAP
 #define LT_PIPE_NAP 1
 #endif
@@ -1363,29 +1366,37 @@ __global__ __launch_bounds__(64 * (2 + kPipeMaxHelpers + kPipeMidWaves), PROD ? 
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
-  if (wave == 0) {
+  // the roles may rotate over the waves by block (LT_PIPE_ROT), so the den
+  // chains of workgroups sharing a CU need not sit on one SIMD: measured
+  // 0.5-1.5 % slower at B = 256 for three rotations (r05_pipe_rot_ab.txt), off
+  const int nwv = nthr >> 6;
+  const int rot = LT_PIPE_ROT == 1 ? (blk >> 3) % nwv
+                : LT_PIPE_ROT == 2 ? blk % nwv
+                : LT_PIPE_ROT == 3 ? ((blk >> 8) & 1) * (nwv >> 1) : 0;
+  const int role = LT_PIPE_ROT ? (wave + rot) % nwv : wave;
+  if (role == 0) {
     __builtin_amdgcn_s_setprio(3);
     if (do_den) {
       if (rev) den_pipe<J, true>(a, lds, b, nf, lane);
       else den_pipe<J, false>(a, lds, b, nf, lane);
     }
-  } else if (wave == 1) {
+  } else if (role == 1) {
     __builtin_amdgcn_s_setprio(2);
     if (rev) num_pipe<PN, true>(a, lds, b, nf, lane);
     else num_pipe<PN, false>(a, lds, b, nf, lane);
-  } else if (wave - 2 < a.NH) {
+  } else if (role - 2 < a.NH) {
     constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
     if constexpr (PROD != 0) {
-      if (rev) helper_prod<true, PROD == 1, J>(a, lds, b, nf, wave - 2, lane);
-      else helper_prod<false, PROD == 1, J>(a, lds, b, nf, wave - 2, lane);
+      if (rev) helper_prod<true, PROD == 1, J>(a, lds, b, nf, role - 2, lane);
+      else helper_prod<false, PROD == 1, J>(a, lds, b, nf, role - 2, lane);
     } else {
-      if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, wave - 2, lane);
-      else helper_pipe<BF16, NL, false>(a, lds, b, nf, wave - 2, lane);
+      if (rev) helper_pipe<BF16, NL, true>(a, lds, b, nf, role - 2, lane);
+      else helper_pipe<BF16, NL, false>(a, lds, b, nf, role - 2, lane);
     }
-  } else if (a.mid && wave - 2 - a.NH < a.NM) {
+  } else if (a.mid && role - 2 - a.NH < a.NM) {
     if constexpr (PN <= 2) {  // mid mode: U < 128 (pipe_mid_fits)
       constexpr int NL = J == 17 ? 18 : (J == 5 ? 5 : (J == 2 ? 2 : 1));
-      const int m = wave - 2 - a.NH;
+      const int m = role - 2 - a.NH;
       // the other direction's band granules are zeroed (its flag carries this call's epoch)
       const unsigned long long want =
           (unsigned long long)a.epoch | ((unsigned long long)~a.epoch << 32);
