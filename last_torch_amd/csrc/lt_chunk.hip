@@ -77,6 +77,12 @@ constexpr unsigned kSpinMax = 1u << 20;
 #ifndef LT_CK_SPLIT
 #define LT_CK_SPLIT 0
 #endif
+#ifndef LT_CK_WPRIO
+#define LT_CK_WPRIO 3
+#endif
+#ifndef LT_CK_PRIO
+#define LT_CK_PRIO 3
+#endif
 #ifndef LT_CK_ROT
 #define LT_CK_ROT 1
 #endif
@@ -1276,6 +1282,7 @@ __global__ __launch_bounds__(256, kAbWaves) void ck_ab_kernel(const CkArgs a) {
   int x = blockIdx.x;
   if (x >= a.wpos && x < a.wpos + nc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char ck_dyn[];
+    if (LT_CK_WPRIO) __builtin_amdgcn_s_setprio(LT_CK_WPRIO);  // the walks' chains first
     combine_role<PPL, kWalkD<PPL>>(a, x - a.wpos, wave, ck_dyn, a.half ? kWalkFirst : kWalkFull);
     return;
   }
@@ -1336,6 +1343,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (a.cont && (int)blockIdx.x < a.B) {  // phase 2 of utterance blockIdx.x's walks
     CK_STAMP(0);
+    if (LT_CK_WPRIO) __builtin_amdgcn_s_setprio(LT_CK_WPRIO);
     combine_role<PPL, kWalkDc<PPL>>(a, blockIdx.x, wave, lds, kWalkRest);
     CK_STAMP(4);
     return;
@@ -1566,6 +1574,8 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
 
+  // LT_CK_PRIO: the den chains issue ahead of the other waves on their SIMD
+  if (LT_CK_PRIO && role < 2) __builtin_amdgcn_s_setprio(LT_CK_PRIO);
   if (role == 0 && !a.local && !LT_ABL(a, 4)) {
     // ---- den alpha in scaled linear space. Lane p in [1, V]: alpha_f[p] =
     // al 2^S (log2 units relative to the walk's offset); each frame the
@@ -1802,6 +1812,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
   } else {  // a recursion this chunk does not run (local / ablations): nothing to wait for
     mark_all(role == 0 ? kFlA : role == 1 ? kFlB : role == 2 ? kFlNA : kFlNB);
   }
+  if (LT_CK_PRIO && role < 2) __builtin_amdgcn_s_setprio(0);
   CK_STAMP(2);
 
   // ---- marginals, one wave per frame: den - num, each normalised by its
