@@ -50,10 +50,6 @@ $(OBJ)/lt_tri.o: $(CSRC)/lt_tri.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(OBJ)/lt_tri4.o: $(CSRC)/lt_tri4.hip $(DEPS)
-	@mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
-
 $(OBJ)/lt_vit.o: $(CSRC)/lt_vit.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -66,7 +62,7 @@ $(OBJ)/lt_joint.o: $(CSRC)/lt_joint.hip $(DEPS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(OBJ)/lt_tri.o $(OBJ)/lt_tri4.o $(INST_OBJS)
+$(LIB): $(OBJ)/lt_lattice.o $(OBJ)/lt_pipe.o $(OBJ)/lt_chunk.o $(OBJ)/lt_table.o $(OBJ)/lt_producer.o $(OBJ)/lt_joint.o $(OBJ)/lt_vit.o $(OBJ)/lt_tri.o $(INST_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^
 
 oracle:

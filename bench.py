@@ -715,9 +715,13 @@ def main():
     if not args.no_joint:
       result['joint_weight_fn_step'] = joint_step_leg(T, U, V, n, device)
 
+  if rank == 0 and args.cpu_twin_utts > 0:
+    # the C++ host twin beside every line, N > 1 included (rank 0, after the
+    # timed steps, so the other ranks only wait at the final barrier): at
+    # N > 1 a shorter sample (about 5 s), the same cells/s measure
+    result['cpu_baseline'] = cpu_twin(T, U, V, n, C, args.cpu_twin_utts,
+                                      min_seconds=10.0 if not dist_on else 5.0)
   if rank == 0 and not dist_on:
-    if args.cpu_twin_utts > 0:
-      result['cpu_baseline'] = cpu_twin(T, U, V, n, C, args.cpu_twin_utts)
     if args.cpu_ref_utts > 0:
       result['cpu_baseline_torch'] = cpu_ref(T, U, V, n, args.cpu_ref_utts)
     if args.cpu_utts > 0:

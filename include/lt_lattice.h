@@ -439,8 +439,13 @@ int lt_joint_weights_backward(int64_t rows, int32_t num_states, int32_t hidden, 
  *                           sum_b grad[b] loss_b (grad nullable = ones;
  *                           unreachable strings contribute 0), from `state`
  *   lt_loss_grad_joint      both, one workspace (state then scratch)
- * hidden: 32, 64, ..., 256. max_labels < 128. The d_ctx_proj / d_out_weight /
- * d_out_bias sums run in a fixed order (deterministic). */
+ * hidden: a multiple of 32 up to 256 whose marginal-pass LDS image fits the
+ * CU's 160 KB (lt_loss_joint_workspace_bytes returns LT_EUNSUPPORTED
+ * otherwise): at max_labels = 100, H <= 192 with split products, H <= 224
+ * with bf16 ones. max_labels < 128. A pipeline wait that timed out makes
+ * loss / log_z / num and every gradient NaN (never a silent result). The
+ * d_ctx_proj / d_out_weight / d_out_bias sums run in a fixed order
+ * (deterministic). */
 typedef struct lt_joint_params {
   int32_t hidden;           /* H */
   int32_t precision;        /* LT_JOINT_SPLIT or LT_JOINT_BF16 (forward products) */

@@ -564,6 +564,17 @@ def table_den_backward(graph, W, num_frames, semiring, dist=None, alpha=None, gr
   return dW
 
 
+def table_num_backward_check(graph, W, labels, semiring):
+  """Raises LatticeLibraryError now if lt_table_num_backward would refuse
+  this problem (its string-gradient LDS rule, the semiring): a host-only
+  query, no launch."""
+  pb = _tproblem(graph, W, labels.shape[-1])
+  nbytes = ctypes.c_size_t(0)
+  _check(lib().lt_table_num_backward_workspace_bytes(ctypes.byref(graph.g), ctypes.byref(pb),
+                                                     semiring, ctypes.byref(nbytes)),
+         'lt_table_num_backward_workspace_bytes')
+
+
 def table_num_backward(graph, W, num_frames, labels, num_labels, semiring, grad=None):
   """lt_table_num_backward: (num [B], dW [B,T,C,V+1] in W's dtype) = the
   string distance and grad_b * its gradient in MaxTropical (the best
@@ -697,14 +708,24 @@ def joint_problem(batch, frames, labels, vocab_size):
   return Problem(batch, frames, vocab_size, 1, labels, LT_DTYPE_F32)
 
 
-def joint_loss_supported(batch, frames, labels, vocab_size, context_size, hidden):
-  """Shapes lt_loss_grad_joint takes: FullNGram n = 1, 16 < V <= 32, U < 128,
-  hidden in {32, 64, ..., 256} (fp32)."""
-  if context_size != 1 or not 16 < vocab_size <= 32 or labels + 1 > 128:
+def joint_loss_supported(batch, frames, labels, vocab_size, context_size, hidden,
+                         precision='fp32'):
+  """Shapes lt_loss_grad_joint takes, as the library itself decides
+  (lt_loss_joint_workspace_bytes returns LT_EUNSUPPORTED otherwise): FullNGram
+  n = 1, 16 < V <= 32, U < 128, hidden a multiple of 32 up to 256 whose
+  marginal-pass LDS image (jf_lds: Wo rows, the checkpoint rows, the per-state
+  d_Pc and e^{2Pc} rows) fits the CU's 160 KB -- e.g. H = 256 at U = 100 does
+  not (about 193 KB), H = 160 does."""
+  if context_size != 1:
     return False
-  if hidden % 32 or not 32 <= hidden <= 256:
+  if batch * frames * (vocab_size + 1) ** 2 * 4 >= 0xFFFFFFF0:
     return False
-  return batch * frames * (vocab_size + 1) ** 2 * 4 < 0xFFFFFFF0
+  pb = joint_problem(batch, frames, labels, vocab_size)
+  jp = JointParams(hidden, JOINT_SPLIT if precision == 'fp32' else JOINT_BF16, None, None, None,
+                   None)
+  st, sc = ctypes.c_size_t(0), ctypes.c_size_t(0)
+  return lib().lt_loss_joint_workspace_bytes(ctypes.byref(pb), ctypes.byref(jp), ctypes.byref(st),
+                                             ctypes.byref(sc)) == 0  # LT_OK
 
 
 def joint_loss_workspace_bytes(batch, frames, labels, vocab_size, hidden, precision='fp32'):

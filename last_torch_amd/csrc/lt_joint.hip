@@ -34,6 +34,7 @@ struct JFArgs {
   const float *alpha, *beta, *alpha_num, *beta_num;  // pipe_kernel's checkpoints
   const int* arcs;                                   // [B][2 NK] string arc table
   const float *log_z, *num, *grad;
+  const int* err;  // the forward's pipeline-timeout word (nonzero: every output NaN)
   float* dpf;   // [B*T, H]
   float* part;  // [B * nblk][(C + R) H + 64] per-block d_Pc, d_Wo, d_bias
   int B, T, U, C, R, H, NP, nblk;
@@ -175,12 +176,16 @@ __global__ __launch_bounds__(64 * (NW < 2 ? 2 : NW), 2) void jf_marg_kernel(cons
   if (!__builtin_isfinite(nm) || !__builtin_isfinite(lz)) gb = 0.f;
   const int hl = min(wave, NW - 1) * 32 + col;  // this lane's hidden column (backward waves)
   float* part = a.part + (long long)blockIdx.x * jf_stride(C, R, H);
-  if (Fl == 0 || gb == 0.f) {  // padding frames / no gradient: zeros out
+  // a forward whose pipeline wait timed out left its checkpoints unfinished:
+  // NaN out, never a silent result
+  const bool bad = *a.err != 0;
+  if (Fl == 0 || gb == 0.f || bad) {  // padding frames / no gradient: zeros out
+    const float z = bad ? __builtin_nanf("") : 0.f;
     for (int e = tid; e < 32 * H; e += nthr) {
       const int m = e / H;
-      if (m < Fh) a.dpf[(row0 + m) * H + (e - m * H)] = 0.f;
+      if (m < Fh) a.dpf[(row0 + m) * H + (e - m * H)] = z;
     }
-    for (long long e = tid; e < jf_stride(C, R, H); e += nthr) part[e] = 0.f;
+    for (long long e = tid; e < jf_stride(C, R, H); e += nthr) part[e] = z;
     return;
   }
   JSTAMP(a, 0, JCLK());
@@ -474,6 +479,17 @@ int jf_check(const lt_problem* pb, const lt_joint_params* jp) {
   return LT_OK;
 }
 
+__global__ __launch_bounds__(64) void jf_err_kernel(const int* err, float* loss, float* lz,
+                                                     float* num, int B) {
+  if (*err == 0) return;
+  const float nan = __builtin_nanf("");
+  for (int b = threadIdx.x; b < B; b += 64) {
+    loss[b] = nan;
+    lz[b] = nan;
+    num[b] = nan;
+  }
+}
+
 template <int NW>
 int jf_launch_marg(const JFArgs& a, const JfLds& l, bool sp, hipStream_t st) {
   const void* k = sp ? (const void*)jf_marg_kernel<NW, true> : (const void*)jf_marg_kernel<NW, false>;
@@ -522,6 +538,7 @@ int lt_loss_joint_forward(const lt_problem* pb, const lt_joint_params* jp,
   char* sb = (char*)state;
   const long long BT = (long long)pb->batch * pb->max_frames;
   hipError_t e = hipMemsetAsync(sb + s.cbig, 0, s.ec - s.cbig, st);  // the flags
+  if (e == hipSuccess) e = hipMemsetAsync(sb + s.err, 0, sizeof(int), st);  // the timeout word
   if (e != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   {
     long long nc4 = (long long)C * H / 4, nf4 = BT * H / 4;
@@ -548,6 +565,11 @@ int lt_loss_joint_forward(const lt_problem* pb, const lt_joint_params* jp,
                                 (float*)(sb + s.beta), (float*)(sb + s.bn), (int32_t*)(sb + s.arcs),
                                 2, (int*)(sb + s.err), stream, nullptr, 0, nullptr, &jo);
   if (rc) return rc;
+  // a pipeline wait that timed out (the pipe raised its abort and drained):
+  // loss, log_z and num NaN, and the backward NaN too (jf_marg_kernel)
+  hipLaunchKernelGGL(jf_err_kernel, dim3(1), dim3(64), 0, st, (const int*)(sb + s.err), loss, lz,
+                     nm, (int)pb->batch);
+  if ((e = hipGetLastError()) != hipSuccess) return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   if (log_z && (e = hipMemcpyAsync(log_z, lz, 4 * pb->batch, hipMemcpyDeviceToDevice, st)) != hipSuccess)
     return lt_impl::set_error(LT_EHIP, hipGetErrorString(e));
   if (num && (e = hipMemcpyAsync(num, nm, 4 * pb->batch, hipMemcpyDeviceToDevice, st)) != hipSuccess)
@@ -588,6 +610,7 @@ int lt_loss_joint_backward(const lt_problem* pb, const lt_joint_params* jp,
   a.arcs = (const int*)(sb + s.arcs);
   a.log_z = (const float*)(sb + s.lz); a.num = (const float*)(sb + s.num);
   a.grad = grad;
+  a.err = (const int*)(sb + s.err);
   a.dpf = d_frame_proj;
   a.part = (float*)scratch;
   a.stamps = nullptr;

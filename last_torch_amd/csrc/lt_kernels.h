@@ -1990,7 +1990,8 @@ inline bool stream_capturing(hipStream_t st) {
 }
 // lt_tri.hip: the trigram checkpointing pair (den_fwd_tri / den_bwd_tri roles)
 int launch_tri_fwdbwd(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStream_t st);
-// lt_tri4.hip: the V = 32 trigram recursions on quads of four workgroups
+// lt_tri4.hip (diagnostic builds only): the V = 32 trigram recursions on
+// quads of four workgroups
 bool tri4_eligible(int V, int n, int B, int U, int cus);
 int launch_tri4(const Plan& pl, bool bf16, float* alpha, float* beta, float* alpha_num,
                 float* beta_num, float* log_z, float* num, float* loss, long long w_bytes,

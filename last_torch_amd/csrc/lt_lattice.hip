@@ -1119,9 +1119,11 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
   }
 #endif
   // trigram with W staged in LDS: the den roles of lt_tri.hip (one lane per
-  // state pair, every term in registers) in the same side-by-side launch
-  // V = 32 trigram: the recursions on quads of four workgroups (lt_tri4.hip)
-  // while the 8B quad members fit the CUs at once
+  // state pair, every term in registers) in the same side-by-side launch.
+  // Diagnostic builds only (LT_DIAG, LT_TRI4=1): the V = 32 recursions on
+  // quads of four workgroups (lt_tri4.hip, measured slower); the
+  // product library does not link lt_tri4.o
+#ifdef LT_DIAG
   if (ck && !local_norm && g.n == 2 && g.V == 32 && alpha && beta) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
@@ -1132,6 +1134,7 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
                                   wb, st);
     }
   }
+#endif
   if (ck && !local_norm && g.n == 2 && g.V >= 2 && g.V <= 32 && pf.wst && pbk.wst &&
       pf.a.aux_waves == pbk.a.aux_waves && pf.a.slot_bytes == pbk.a.slot_bytes &&
       (g.V != 32 || pbk.lds_bytes + 8 * kTriBPad <= kLdsMax) && env_int("LT_NO_TRI", 0) == 0) {

@@ -2238,12 +2238,24 @@ static size_t str_grad_bytes(const lt_table_problem* pb, int semiring) {
   return (size_t)((semiring == M_MAX ? BTS : 4 * BTS) + 255) & ~(size_t)255;
 }
 
+// LDS bytes of tab_str_grad_kernel: the string positions' rows and, for
+// MaxTropical, the decision chunk
+static long long str_grad_lds(const lt_graph* g, const lt_table_problem* pb, int32_t semiring) {
+  const long long S = pb->max_labels + 1, K = g->expansions;
+  return 4LL * (5 * S + (9 + K + 1 + 2) * S + 4 + ((K + 1 + 3) & ~3) * 2) +
+         (semiring == M_MAX ? std::max<long long>(kStrChunk, S) : 0);
+}
+
 int lt_table_num_backward_workspace_bytes(const lt_graph* g, const lt_table_problem* pb,
                                           int32_t semiring, size_t* bytes) {
   if (int rc = t_check(g, pb)) return rc;
   if (semiring != M_MAX && semiring != M_REAL)
     return t_fail(LT_EUNSUPPORTED, "lt_table_num_backward: MaxTropical or Real (Log: "
                                    "lt_table_loss_grad with local_norm)");
+  // the string-gradient kernel's LDS (tab_str_grad_kernel): refused here, so a
+  // caller asking before its forward learns it up front
+  if (str_grad_lds(g, pb, semiring) > kTabLds)
+    return t_fail(LT_EUNSUPPORTED, "string gradient: labels exceed LDS");
   if (bytes) *bytes = str_grad_bytes(pb, semiring);
   return LT_OK;
 }
@@ -2267,15 +2279,12 @@ int lt_table_num_backward(const lt_graph* g, const lt_table_problem* pb, int32_t
   a.gin = grad;
   a.dist = num;
   a.dW = (float*)dW;
-  const int S = a.U + 1, K = a.K;
   if (semiring == M_MAX) a.win = (unsigned char*)workspace;
   else a.alpha = (float*)workspace;
   const long long n = (long long)a.B * a.T * a.C * a.R;
   if (n > 0)
     if (int rc = t_hip(hipMemsetAsync(dW, 0, (size_t)n * (bf16 ? 2 : 4), st), "memset")) return rc;
-  const long long lds = 4LL * (5 * S + (9 + K + 1 + 2) * S + 4 + ((K + 1 + 3) & ~3) * 2) +
-                        (semiring == M_MAX ? std::max(kStrChunk, S) : 0);
-  if (lds > kTabLds) return t_fail(LT_EUNSUPPORTED, "string gradient: labels exceed LDS");
+  const long long lds = str_grad_lds(g, pb, semiring);  // checked by the workspace query
   if (semiring == M_MAX)
     return bf16 ? t_launch(tab_str_grad_kernel<true, M_MAX>, a.B, (int)lds, st, a)
                 : t_launch(tab_str_grad_kernel<false, M_MAX>, a.B, (int)lds, st, a);

@@ -118,19 +118,21 @@ LT_DEVINL void st_arc(void* arcs, long long e, float v) {
   else ((float*)arcs)[e] = v;
 }
 
-// utterance b's backtrace by one workgroup of 256 threads, its backpointers
-// staged in `lds` (vit_backtrace_lds bytes)
+// utterance b's backtrace by one workgroup of `nth` threads (any multiple of
+// 64: every loop strides by the block it runs in -- vit_backtrace_kernel's 256
+// or vit_split_kernel's 64 (2 + kBpWaves)), its backpointers staged in `lds`
+// (vit_backtrace_lds bytes)
 template <bool BF16>
-LT_DEVINL void backtrace_body(const VbtArgs& a, int b, int tid, unsigned char* lds) {
+LT_DEVINL void backtrace_body(const VbtArgs& a, int b, int tid, int nth, unsigned char* lds) {
   const int C = a.C, R = a.R, S = a.S;
   const long long FR = (long long)C * R;
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   long long* lab = a.labels + (long long)b * a.T;
-  for (int t = nf + tid; t < a.T; t += 256) lab[t] = 0;  // padding frames
+  for (int t = nf + tid; t < a.T; t += nth) lab[t] = 0;  // padding frames
   if (a.arcs) {
     const long long n = (long long)a.T * FR;
-    for (long long e = tid; e < n; e += 256) st_arc<BF16>(a.arcs, (long long)b * a.T * FR + e, 0.f);
+    for (long long e = tid; e < n; e += nth) st_arc<BF16>(a.arcs, (long long)b * a.T * FR + e, 0.f);
   }
   const int nseg = (nf + S - 1) / S;
   unsigned char* rows = lds;                          // [nf][C]
@@ -141,18 +143,18 @@ LT_DEVINL void backtrace_body(const VbtArgs& a, int b, int tid, unsigned char* l
   if ((((uintptr_t)src) & 15) == 0) {
     // 16-byte loads, four in flight per thread before their LDS stores
     const int n16 = nb >> 4;
-    for (int e = tid; e < n16; e += 1024) {
+    for (int e = tid; e < n16; e += 4 * nth) {
       uint4 v[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (e + 256 * k < n16) v[k] = ((const uint4*)src)[e + 256 * k];
+        if (e + nth * k < n16) v[k] = ((const uint4*)src)[e + nth * k];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (e + 256 * k < n16) ((uint4*)rows)[e + 256 * k] = v[k];
+        if (e + nth * k < n16) ((uint4*)rows)[e + nth * k] = v[k];
     }
-    for (int e = (n16 << 4) + tid; e < nb; e += 256) rows[e] = src[e];
+    for (int e = (n16 << 4) + tid; e < nb; e += nth) rows[e] = src[e];
   } else {
-    for (int e = tid * 4; e < nb; e += 1024) {
+    for (int e = tid * 4; e < nb; e += 4 * nth) {
       if (e + 4 <= nb && ((((uintptr_t)(src + e)) & 3) == 0)) {
         *(unsigned*)(rows + e) = *(const unsigned*)(src + e);
       } else {
@@ -162,7 +164,7 @@ LT_DEVINL void backtrace_body(const VbtArgs& a, int b, int tid, unsigned char* l
   }
   __syncthreads();
   // each (segment, end state): the state before the segment's first frame
-  for (int x = tid; x < nseg * C; x += 256) {
+  for (int x = tid; x < nseg * C; x += nth) {
     const int sg = x / C;
     int q = x - sg * C;
     const int t1 = min(nf, (sg + 1) * S);
@@ -184,7 +186,7 @@ LT_DEVINL void backtrace_body(const VbtArgs& a, int b, int tid, unsigned char* l
   if (a.arcs) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // zero fill before the scatter
   __syncthreads();
   const float gb = a.grad ? a.grad[b] : 1.f;
-  for (int sg = tid; sg < nseg; sg += 256) {
+  for (int sg = tid; sg < nseg; sg += nth) {
     int q = endq[sg];
     const int t1 = min(nf, (sg + 1) * S);
     for (int t = t1 - 1; t >= sg * S; --t) {
@@ -597,13 +599,13 @@ __global__ __launch_bounds__(64 * (2 + kBpWaves)) void vit_split_kernel(const Vi
   // backpointers fit the transposed ring's LDS, vit_backtrace_lds): they are
   // this workgroup's own stores, read back after the barrier; no second
   // launch (cfg4: 0.636 -> 0.633 ms)
-  if (bt.labels) backtrace_body<BF16>(bt, b, tid, (unsigned char*)&s_tw[0][0][0]);
+  if (bt.labels) backtrace_body<BF16>(bt, b, tid, (int)blockDim.x, (unsigned char*)&s_tw[0][0][0]);
 }
 
 template <bool BF16>
 __global__ __launch_bounds__(256) void vit_backtrace_kernel(const VbtArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  backtrace_body<BF16>(a, blockIdx.x, threadIdx.x, lds);
+  backtrace_body<BF16>(a, blockIdx.x, threadIdx.x, (int)blockDim.x, lds);
 }
 
 }  // namespace

@@ -491,7 +491,14 @@ class RecognitionLattice(nn.Module, Generic[T]):
     elif self._table_path():
       num = _TableNumFn.apply(W, nf, lab.contiguous(), nl, self._graph(W.device), sid)
     else:
-      graph = self._graph(W.device) if sid != _native.SEMIRING_LOG else None
+      # MaxTropical / Real gradients run on the general string-gradient kernel
+      # over FullNGram.next_state_table(): its graph is built only when a
+      # gradient can be asked for, and its LDS rule is checked here, before
+      # the forward, rather than mid-backward
+      graph = None
+      if sid != _native.SEMIRING_LOG and torch.is_grad_enabled() and W.requires_grad:
+        graph = self._graph(W.device)
+        _native.table_num_backward_check(graph, W, lab, sid)
       num = _NumFn.apply(W, nf, lab.contiguous(), nl, V, n, sid, graph)
     return self._home(num.reshape(batch_dims), frames)
 

@@ -217,7 +217,8 @@ class JointWeightFn(WeightFn[torch.Tensor]):
       return None
     B, T = frames.shape[:2]
     U = labels.shape[-1]
-    if not _native.joint_loss_supported(B, T, U, vocab_size, context_size, self.hidden_size):
+    if not _native.joint_loss_supported(B, T, U, vocab_size, context_size, self.hidden_size,
+                                        self.precision):
       return None
     if self.lattice_fusion == 'auto' and not fused_lattice_preferred(B, T, U, self.hidden_size):
       return None

@@ -181,3 +181,79 @@ def test_recognition_lattice_with_fused_joint_weight_fn(cuda, H):
                              atol=1e-3)
   for a, b in zip(out['on'][1], out['off'][1]):
     _close(a, b, 1e-4)
+
+
+@pytest.mark.parametrize('H', [32, 128])
+def test_fused_at_bench_shape_against_oracle(cuda, H):
+  """The shapes r05_joint_step.jsonl times (B=64, T=1000, U=100): the fused
+  loss against the oracle on the materialised W (the producer's W in the same
+  precision, bit-identical to the fused one), and the parameter gradients
+  against PyTorch fp32 autograd of the reference formulation pulled back from
+  the ORACLE's dW (orc.loss_grad), not the product's; plus the separate
+  launches at this shape."""
+  B, T, U = 64, 1000, 100
+  pc, pf, wo, bias, nf, lab, nl = _problem(B, T, U, H, cuda, seed=100 + H, varlen=False)
+  out = nat.loss_grad_joint(pc, pf, wo, bias, nf, lab, nl)
+  loss, lz, num, dpc, dpf, dwo, dbias = out
+  W = nat.joint_weights(pc, pf, wo, bias, precision='fp32')
+  torch.cuda.synchronize()
+  orc = _orc()
+  rl, rlz, rnum, rdW = orc.loss_grad(W.cpu().numpy(), nf.cpu().numpy(), lab.cpu().numpy(),
+                                     nl.cpu().numpy(), 32, 1)
+  assert_loss_close(loss.cpu().numpy(), rl)
+  assert_loss_close(lz.cpu().numpy(), rlz)
+  assert_loss_close(num.cpu().numpy(), rnum)
+  ps = [x.clone().requires_grad_(True) for x in (pc, pf, wo, bias)]
+  hid = torch.tanh(ps[0][None, None] + ps[1][:, :, None, :])  # [B, T, C, H] fp32
+  Wr = hid @ ps[2].t() + ps[3]
+  (Wr * torch.from_numpy(rdW).to(cuda)).sum().backward()
+  del hid, Wr
+  for got, p in zip((dpc, dpf, dwo, dbias), ps):
+    _close(got, p.grad, 1e-3)
+  _, sl, _, _, sdpc, sdpf, sdwo, sdbias = _separate(pc, pf, wo, bias, nf, lab, nl,
+                                                    torch.ones([B], device=cuda), 'fp32')
+  assert torch.equal(loss, sl)
+  for got, ref in ((dpc, sdpc), (dpf, sdpf), (dwo, sdwo), (dbias, sdbias)):
+    _close(got, ref, 1e-5)
+
+
+def test_fused_largest_hidden_and_unsupported_fallback(cuda):
+  """joint_loss_supported asks the library (its LDS rule): at
+  U = 100 the split-product marginal pass fits up to H = 192 and not at 224 /
+  256. H = 192 (six backward waves) runs against the separate launches; an
+  H = 256 JointWeightFn with lattice_fusion='on' falls back to the separate
+  launches instead of raising."""
+  import last_torch_amd as lt
+  U = 100
+  assert nat.joint_loss_supported(4, 64, U, 32, 1, 192)
+  assert not nat.joint_loss_supported(4, 64, U, 32, 1, 224)
+  assert not nat.joint_loss_supported(4, 64, U, 32, 1, 256)
+  assert nat.joint_loss_supported(4, 64, U, 32, 1, 224, precision='bf16')
+  B, T, H = 4, 300, 192
+  pc, pf, wo, bias, nf, lab, nl = _problem(B, T, U, H, cuda, seed=192)
+  gin = torch.tensor([1.0, 0.5, -1.0, 2.0], device=cuda)
+  loss, lz, num, dpc, dpf, dwo, dbias = nat.loss_grad_joint(pc, pf, wo, bias, nf, lab, nl,
+                                                            grad=gin)
+  _, rl, rlz, rnum, rdpc, rdpf, rdwo, rdbias = _separate(pc, pf, wo, bias, nf, lab, nl, gin, 'fp32')
+  torch.cuda.synchronize()
+  assert torch.equal(loss, rl) and torch.equal(lz, rlz) and torch.equal(num, rnum)
+  for got, ref in ((dpc, rdpc), (dpf, rdpf), (dwo, rdwo), (dbias, rdbias)):
+    _close(got, ref, 1e-5)
+  # the drop-in API at H = 256: 'on' cannot fuse here, so the separate launches run
+  V, F = 32, 16
+  ctx = lt.contexts.FullNGram(vocab_size=V, context_size=1)
+  cacher = lt.weight_fns.SharedEmbCacher(num_context_states=V + 1, embedding_size=8, device=cuda)
+  wfn = lt.weight_fns.JointWeightFn(vocab_size=V, hidden_size=256, device=cuda,
+                                    lattice_fusion='on')
+  lat = lt.RecognitionLattice(context=ctx, alignment=lt.alignments.FrameDependent(),
+                              weight_fn_cacher_factory=lambda _: cacher,
+                              weight_fn_factory=lambda _: wfn)
+  frames = torch.randn([2, 40, F], device=cuda)
+  nf2 = torch.tensor([40, 31], device=cuda)
+  lab2 = torch.randint(1, V + 1, [2, U], device=cuda)
+  nl2 = torch.tensor([12, 9], device=cuda)
+  l_on = lat(frames=frames, num_frames=nf2, labels=lab2, num_labels=nl2)
+  wfn.lattice_fusion = 'off'
+  l_off = lat(frames=frames, num_frames=nf2, labels=lab2, num_labels=nl2)
+  torch.cuda.synchronize()
+  assert torch.equal(l_on, l_off)

@@ -10,5 +10,5 @@ mkdir -p build/var
   -c -o build/var/vit_$name.o last_torch_amd/csrc/lt_vit.hip
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o build/var/vit_$name.so build/obj/lt_lattice.o \
   build/obj/lt_pipe.o build/obj/lt_chunk.o build/obj/lt_table.o build/obj/lt_producer.o \
-  build/var/vit_$name.o build/obj/lt_tri.o build/obj/lt_tri4.o build/obj/lt_joint.o build/obj/lt_inst_*.o
+  build/var/vit_$name.o build/obj/lt_tri.o build/obj/lt_joint.o build/obj/lt_inst_*.o
 echo build/var/vit_$name.so
