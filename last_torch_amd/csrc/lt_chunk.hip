@@ -73,6 +73,11 @@ constexpr float kCert = 64.f;   // phase C's per-frame certificate: log2(max alp
 #define LT_AB_WAVES 3
 #endif
 constexpr int kAbWaves = LT_AB_WAVES;  // ck_ab_kernel: waves per SIMD its registers allow
+#ifndef LT_CK_APF
+#define LT_CK_APF 1
+#endif
+constexpr int kApf = LT_CK_APF;  // phase A: frames in registers ahead (1 or 2)
+static_assert(kApf == 1 || kApf == 2, "phase A prefetch depth");
 constexpr unsigned kSpinMax = 1u << 20;
 #ifndef LT_CK_SPLIT
 #define LT_CK_SPLIT 0
@@ -89,6 +94,10 @@ constexpr unsigned kSpinMax = 1u << 20;
 #ifndef LT_CK_PF
 #define LT_CK_PF 0
 #endif
+#ifndef LT_CK_EPIPE
+#define LT_CK_EPIPE 0
+#endif
+constexpr bool kEpipe = LT_CK_EPIPE != 0;  // phase C den chains: the next frame's E a step ahead
 #ifndef LT_WALK_SLOTS
 #define LT_WALK_SLOTS 3
 #endif
@@ -605,7 +614,7 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     if (!cfin || __builtin_amdgcn_ballot_w64(lnan)) bad = 2;
     else if (bad == 0 && __builtin_amdgcn_ballot_w64(lwide)) bad = 3;
     const float w00 = F.w00;
-    if (reload) load_frame<BF16, PPL, FULL>(frame_ptr(f + 1), frame_bytes(f + 1), fo, F);
+    if (reload) load_frame<BF16, PPL, FULL>(frame_ptr(f + kApf), frame_bytes(f + kApf), fo, F);
 
     // state-0 row: r' = p00 * e0 + r Ec (VALU, beside the MFMAs), scaled by
     // a power of two so that its largest entry sits in [1/2, 1)
@@ -659,10 +668,22 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     for (int r = 0; r < 16; ++r) X[r] = ldexpf(D[r], -e);
     ej += e;
   };
-  // one frame in registers ahead (a frame step outlasts a load; a second
-  // buffer would cost the third wave per SIMD)
-  load_frame<BF16, PPL, FULL>(frame_ptr(0), frame_bytes(0), fo, fr);
-  for (int f = 0; f < nt; ++f) step(fr, f, f + 1 < nt);
+  if constexpr (kApf == 1) {
+    // one frame in registers ahead
+    load_frame<BF16, PPL, FULL>(frame_ptr(0), frame_bytes(0), fo, fr);
+    for (int f = 0; f < nt; ++f) step(fr, f, f + 1 < nt);
+  } else {
+    // two frames in registers ahead, the buffers alternating (the reloads
+    // are unconditional, clamped to the chunk's last frame, so the
+    // compiler's vmcnt count across the two buffers stays exact)
+    FrameRegs<BF16, PPL> fr2;
+    load_frame<BF16, PPL, FULL>(frame_ptr(0), frame_bytes(0), fo, fr);
+    load_frame<BF16, PPL, FULL>(frame_ptr(1), frame_bytes(1), fo, fr2);
+    for (int f = 0; f < nt; f += 2) {
+      step(fr, f, true);
+      if (f + 1 < nt) step(fr2, f + 1, true);
+    }
+  }
   CK_ASTAMP(2);
 
   const __amdgpu_buffer_rsrc_t rr = wt_rsrc(a.rec + (long long)id * kRec, 4 * kRec);
@@ -1597,13 +1618,15 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     float S = wmax_u(core ? x0 : -kInf);  // -inf: no core state reached yet
     float al = (core && S != -kInf) ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     if (split) wait_vmcnt(0);  // this wave's half of W
-    for (int f = 0; f < nt; ++f) {
+    // frame f's E terms of the lane (its sources' arcs into qe, source 32,
+    // qe's blank self loop) and W00: alpha's own frames [0, hs) from W, their
+    // E stored to its home; beta's once beta has passed them
+    auto get_e = [&](int f, float* e, float& e32, float& eb, float& w00) {
       const unsigned char* fr = wrow(f);
       float* ef = eptr(f);
       const float cl = cfl[f];
-      float w00 = fs[f * kFs + kFsW00];
-      float e[16], e32, eb;
-      if (f < hs) {  // alpha's frame: E from W, stored to its home
+      w00 = fs[f * kFs + kFsW00];
+      if (f < hs) {
         if (split) w00 = own_arcs(f, fr);
 #pragma unroll
         for (int m = 0; m < 16; ++m) e[m] = ldsw<BF16>(fr, min(16 * h + m, C - 1) * R + qe);
@@ -1618,7 +1641,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         ef[min(32, C - 1) * R + qe] = e32;
         ef[qe * R] = eb;
         if (lane == 0) ef[0] = 0.f;  // (0, 0) is taken in log2 (xb[0] = 0)
-      } else {       // beta's: E once beta has passed it
+      } else {
         wait_bits(f, kFlB);
         if (split) w00 = fs[f * kFs + kFsW00];
 #pragma unroll
@@ -1626,6 +1649,15 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         e32 = ef[min(32, C - 1) * R + qe];
         eb = ef[qe * R];
       }
+    };
+    // LT_CK_EPIPE: alpha's own frames' E a step ahead (only those: fetching
+    // one of beta's frames early would wait on beta while beta waits on this
+    // chain's previous frame)
+    float e[16], e32 = 0.f, eb = 0.f, w00 = 0.f;
+    if (kEpipe && nt > 0) get_e(0, e, e32, eb, w00);  // hs >= 1: frame 0 is alpha's
+    for (int f = 0; f < nt; ++f) {
+      const float cl = cfl[f];
+      if (!kEpipe || f >= hs) get_e(f, e, e32, eb, w00);
       const float mc = wmax_u(core ? al : 0.f);
       int ex;
       (void)frexpf(mc, &ex);
@@ -1639,6 +1671,11 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         fs[f * kFs + kFsMa] = Ma;
         fs[f * kFs + kFsA0] = a0;
       }
+      // LT_CK_EPIPE: the next frame's E under this step's LDS round trip
+      // (a wave issues in order: fetched at the top of the next step, its
+      // loads and exponentials sat on the chain)
+      float en[16], en32 = 0.f, enb = 0.f, wn00 = 0.f;
+      if (kEpipe && f + 1 < hs) get_e(f + 1, en, en32, enb, wn00);
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       float s0 = 0.f, s1 = 0.f;
@@ -1659,6 +1696,13 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       al = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
       mark(f, kFlA);
+      if (kEpipe && f + 1 < hs) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) e[m] = en[m];
+        e32 = en32;
+        eb = enb;
+        w00 = wn00;
+      }
     }
   } else if (role == 1 && !a.local && !LT_ABL(a, 4)) {
     // ---- den beta, the same scaled linear space; frame f gets beta_{f+1}.
@@ -1674,13 +1718,14 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     float S = safe_max(wmax_u(core ? x0 : -kInf));
     float be = core ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
     if (split) wait_vmcnt(0);  // this wave's half of W
-    for (int f = nt - 1; f >= 0; --f) {
+    // frame f's E terms of the lane (source pe's arcs, its blank, E[0][j+1])
+    // and W00: beta's own frames [hs, nt) from W, alpha's once alpha passed them
+    auto get_e = [&](int f, float* e, float& eb, float& e0y, float& w00) {
       const unsigned char* fr = wrow(f);
       float* ef = eptr(f);
       const float cl = cfl[f];
-      float w00 = fs[f * kFs + kFsW00];
-      float e[16], eb, e0y;  // e0y = E[0][j+1]
-      if (f >= hs) {  // beta's frame: E from W, stored to its home
+      w00 = fs[f * kFs + kFsW00];
+      if (f >= hs) {
         if (split) w00 = own_arcs(f, fr);
 #pragma unroll
         for (int m = 0; m < 16; ++m) e[m] = ldsw<BF16>(fr, pe * R + min(16 * h + m + 1, V));
@@ -1695,7 +1740,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         ef[pe * R] = eb;
         ef[min(j, V - 1) + 1] = e0y;
         if (lane == 0) ef[0] = 0.f;
-      } else {        // alpha's: E once alpha has passed it
+      } else {
         wait_bits(f, kFlA);
         if (split) w00 = fs[f * kFs + kFsW00];
 #pragma unroll
@@ -1703,6 +1748,13 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         eb = ef[pe * R];
         e0y = ef[min(j, V - 1) + 1];
       }
+    };
+    // LT_CK_EPIPE: beta's own frames' E a step ahead (as alpha's)
+    float e[16], eb = 0.f, e0y = 0.f, w00 = 0.f;  // e0y = E[0][j+1]
+    if (kEpipe && nt - 1 >= hs) get_e(nt - 1, e, eb, e0y, w00);
+    for (int f = nt - 1; f >= 0; --f) {
+      const float cl = cfl[f];
+      if (!kEpipe || f < hs) get_e(f, e, eb, e0y, w00);
       const float mc = wmax_u(be);
       int ex;
       (void)frexpf(mc, &ex);
@@ -1715,6 +1767,8 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
         fs[f * kFs + kFsMb] = Mb;
         fs[f * kFs + kFsB0] = b0;
       }
+      float en[16], enb = 0.f, en0y = 0.f, wn00 = 0.f;
+      if (kEpipe && f - 1 >= hs) get_e(f - 1, en, enb, en0y, wn00);
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       float s0 = 0.f, s1 = 0.f;
@@ -1737,6 +1791,13 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       be = core ? sh : 0.f;
       __builtin_amdgcn_wave_barrier();
       mark(f, kFlB);
+      if (kEpipe && f - 1 >= hs) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) e[m] = en[m];
+        eb = enb;
+        e0y = en0y;
+        w00 = wn00;
+      }
     }
   } else if (role == 2 && !LT_ABL(a, 8)) {
     // ---- num alpha (log2): al'[u] = al[u] + blank(u) (+) al[u-1] + arc(u)

@@ -7,5 +7,5 @@ cd "$(dirname "$0")/.."
 name=$1; src=$2; shift 2
 mkdir -p build/var
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I last_torch_amd/csrc -I include "$@" -c -o build/var/$name.o "$src"
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o build/var/$name.so build/obj/lt_lattice.o build/obj/lt_pipe.o build/var/$name.o build/obj/lt_table.o build/obj/lt_producer.o build/obj/lt_vit.o build/obj/lt_tri.o build/obj/lt_inst_*.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o build/var/$name.so build/obj/lt_lattice.o build/obj/lt_pipe.o build/var/$name.o build/obj/lt_table.o build/obj/lt_producer.o build/obj/lt_joint.o build/obj/lt_vit.o build/obj/lt_tri.o build/obj/lt_inst_*.o
 echo build/var/$name.so

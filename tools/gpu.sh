@@ -17,7 +17,8 @@
 #              the bench call (tools/chunk_prof.py) and of B=256
 #   ab         per-call time of the product library and every build/var/*.so, three interleaved
 #              rounds (tools/time_call.py; BS batch size, default 64)
-#   vitvar     every build/var/vit_*.so: the cfg4 / long-utterance Viterbi tests, then timings
+#   vitvar     every build/var/vit_*.so: the cfg4 / long-utterance Viterbi tests
+#   vart=EXPR  every build/var/*.so: pytest -m gpu -k EXPR (a variant's parity before its timing)
 #   cfg5       tools/cfg5_time.py, product and every build/var/*.so interleaved
 #   vit        tools/vit_time.py, product and every build/var/*.so interleaved
 #   joint      tools/joint_step_bench.py (HS hidden sizes, default 32,64,128,512)
@@ -98,6 +99,12 @@ for step in "$@"; do
       for lib in build/var/vit_*.so; do
         v=$(basename $lib .so)
         LT_LIB_PATH=$lib t_run t_$v.log 300 tests/test_gpu_full_size.py -v -k "cfg4 or viterbi_long"
+      done
+      ;;
+    vart=*)
+      for lib in build/var/*.so; do
+        v=$(basename $lib .so)
+        LT_LIB_PATH=$lib t_run vart_$v.log 500 tests -m gpu -q -k "${step#vart=}"
       done
       ;;
     cfg5|vit)
