@@ -94,6 +94,20 @@ constexpr unsigned kSpinMax = 1u << 20;
 #ifndef LT_CK_PF
 #define LT_CK_PF 0
 #endif
+// LT_CK_NOACQ: what one launch's workgroups hand each other (the records
+// and bands phase A publishes for the phase-1 walks; the boundary rows the
+// phase-2 walks publish for phase C) is read with sc1 loads, which bypass the
+// reading CU's L1, instead of plain loads behind an agent-scope acquire
+// (buffer_inv sc1: an L1 invalidation per poll, ~1.7 us and more with four
+// workgroups on the CU, MI355X_MICROARCH.md)
+#ifndef LT_CK_NOACQ
+#define LT_CK_NOACQ 1
+#endif
+constexpr bool kNoAcq = LT_CK_NOACQ != 0;
+#ifndef LT_CK_BANDMIX
+#define LT_CK_BANDMIX 0
+#endif
+constexpr bool kBandMix = LT_CK_BANDMIX != 0;  // phase A: band steps between the MFMAs
 #ifndef LT_CK_EPIPE
 #define LT_CK_EPIPE 0
 #endif
@@ -247,13 +261,15 @@ LT_DEVINL float ldsw(const unsigned char* fr, int e) {
 // at the 16-byte granule holding `off`: the data sits at lds + (off & 15)).
 // Lanes past the end re-load the last granule into the slack.
 LT_DEVINL void dma_issue(const unsigned char* base, long long off, long long bytes,
-                         unsigned lds_addr, int ni, int lane, int wave0 = 0, int nwaves = 1) {
+                         unsigned lds_addr, int ni, int lane, int wave0 = 0, int nwaves = 1,
+                         bool sc1 = false) {
   const long long a0 = off & ~15LL;
   const int n16 = (int)((off + bytes - a0 + 15) >> 4);
   for (int i = wave0; i < ni; i += nwaves) {
     int g = lane + 64 * i;
     g = g < n16 ? g : n16 - 1;
-    glds16(base + a0 + 16LL * g, lds_addr + 1024u * i);
+    if (sc1) glds16_sc1(base + a0 + 16LL * g, lds_addr + 1024u * i);
+    else glds16(base + a0 + 16LL * g, lds_addr + 1024u * i);
   }
 }
 
@@ -540,8 +556,25 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   auto step = [&](FrameRegs<BF16, PPL>& F, int f, bool reload) {
     mask_frame<BF16, PPL, FULL>(V, lane, boff, loff, F);
     // numerator: band step over the group (positions past the string read -inf)
-    {
-      const int j = f / kGrp, fl = f - j * kGrp;  // wave-uniform
+    // (diagnostic builds: LT_CK_DBG bit 1024 skips it -- timing only)
+    const bool bands = !LT_ABL(a, 1024);
+    const int jg = f / kGrp, flg = f - jg * kGrp;  // wave-uniform
+    if (kBandMix && bands) {
+      // LT_CK_BANDMIX: this frame's weights published now (F is reloaded
+      // below); the band steps themselves run between the core product's
+      // MFMAs, which they do not depend on
+#pragma unroll
+      for (int r = 0; r < PPL; ++r)
+        sg[lane + 64 * r] = make_float2(F.gb[r] * kLog2e, F.gl[r] * kLog2e);
+      if (flg == 0) {
+#pragma unroll
+        for (int r = 0; r < PPL; ++r)
+#pragma unroll
+          for (int d = 0; d <= kGrp; ++d) nbd[r][d] = d ? -kInf : 0.f;
+      }
+    }
+    if (!kBandMix && bands) {
+      const int j = jg, fl = flg;
 #pragma unroll
       for (int r = 0; r < PPL; ++r)
         sg[lane + 64 * r] = make_float2(F.gb[r] * kLog2e, F.gl[r] * kLog2e);
@@ -593,9 +626,17 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     // e >= 0); a weight below e^-61 of the frame's max, or -inf, gives
     // E < kEmin (outside the strict range, kept as an exact zero or a
     // small value: the relaxed path's per-frame certificate covers it).
-    const float dgv = (FULL || i < V) ? lt_exp_off(F.wdg, cl) : 0.f;
+    // (diagnostic builds: bit 4096 skips the exponentials and flags -- timing only)
+    const bool noexp = LT_ABL(a, 4096);
+    const float dgv = (FULL || i < V) ? (noexp ? F.wdg : lt_exp_off(F.wdg, cl)) : 0.f;
     if (lane < 32) sdg[lane] = dgv;
     float A[16];
+    float e0;
+    if (noexp) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) A[s] = F.w[s];
+      e0 = F.wr0;
+    } else {
     const float ebl = lt_exp_off(F.wbl, cl);
     bool lnan = (lane <= V) && !(ebl >= 0.f);
     bool lwide = (lane <= V) && !(ebl >= kEmin);
@@ -608,13 +649,16 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
       A[s] = live ? e : 0.f;
     }
     const float e0r = lt_exp_off(F.wr0, cl);
-    const float e0 = (FULL || i < V) ? e0r : 0.f;
+    e0 = (FULL || i < V) ? e0r : 0.f;
     lnan = lnan || ((FULL || i < V) && !(e0r >= 0.f));
     lwide = lwide || ((FULL || i < V) && !(e0r >= kEmin));
     if (!cfin || __builtin_amdgcn_ballot_w64(lnan)) bad = 2;
     else if (bad == 0 && __builtin_amdgcn_ballot_w64(lwide)) bad = 3;
+    }
     const float w00 = F.w00;
-    if (reload) load_frame<BF16, PPL, FULL>(frame_ptr(f + kApf), frame_bytes(f + kApf), fo, F);
+    // (diagnostic builds: bit 8192 keeps the chunk's first frame -- timing only)
+    if (reload && !LT_ABL(a, 8192))
+      load_frame<BF16, PPL, FULL>(frame_ptr(f + kApf), frame_bytes(f + kApf), fo, F);
 
     // state-0 row: r' = p00 * e0 + r Ec (VALU, beside the MFMAs), scaled by
     // a power of two so that its largest entry sits in [1/2, 1)
@@ -643,9 +687,51 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     csum += cl;
 
     // core: X <- E^T X on the matrix cores (exact f32 FMA chains)
+    // (diagnostic builds: bit 2048 skips the product and the column scales -- timing only)
+    if (LT_ABL(a, 2048)) return;
     v16f D = {};
+    if constexpr (kBandMix) {
+      // the numerator band steps (log space: two transcendentals each, every
+      // d of the group computed and kept only while d <= fl + 1) between the
+      // MFMAs of the core product: the wave issues them while its own
+      // dependent MFMA chain runs
+      float2 gv[PPL][kGrp + 1];
+      if (bands) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int s = 0; s < 16; ++s) D = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], X[s], D, 0, 0, 0);
+        for (int r = 0; r < PPL; ++r)
+#pragma unroll
+          for (int d = 0; d <= kGrp; ++d) gv[r][d] = sg[lane + 64 * r + d];
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        D = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], X[s], D, 0, 0, 0);
+        const int r = s / kGrp, d = kGrp - s % kGrp;
+        if (bands && r < PPL) {
+          const float nv = lse2_b2(nbd[r][d] + gv[r][d].x, nbd[r][d - 1] + gv[r][d].y);
+          nbd[r][d] = d <= flg + 1 ? nv : nbd[r][d];
+        }
+      }
+      if (bands) {
+#pragma unroll
+        for (int r = 0; r < PPL; ++r) nbd[r][0] += gv[r][0].x;
+        if (flg == kGrp - 1 || f == nt - 1) {  // source-major: 32 bytes per position
+          const int g0 = jg * (kGrp + 1) * NPG;
+#pragma unroll
+          for (int r = 0; r < PPL; ++r)
+            if (lane + 64 * r < NPG) {
+              const int u = lane + 64 * r;
+              st_wt4(nbr, g0 + 8 * u, nbd[r][0], nbd[r][1], nbd[r][2], nbd[r][3]);
+              st_wt4(nbr, g0 + 8 * u + 4, nbd[r][4], nbd[r][5], nbd[r][6], nbd[r][7]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) D = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], X[s], D, 0, 0, 0);
+    }
     // + Dg X: row kstep(r, h) of X times that state's blank self loop
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -739,6 +825,17 @@ LT_DEVINL unsigned flag_state(unsigned long long v, unsigned long long tag) {
 LT_DEVINL int prog_count(unsigned long long v, unsigned long long tag) {
   return (v & ~0xFFFFFFull) == tag ? (int)(v & 0xFFFFFF) : 0;
 }
+// L1-bypassing loads of another workgroup's data published in this launch
+// (LT_CK_NOACQ): 16 bytes, one float
+// (a buffer load: the compiler counts it in vmcnt, unlike an asm load)
+LT_DEVINL float4 ld_sc1x4(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0x10);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
+}
+LT_DEVINL float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 LT_DEVINL void acquire_agent() {
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -768,7 +865,7 @@ struct ChunkReady {
       take(v, lane, &c);
       if (c) {
         hi += c;
-        acquire_agent();
+        if (!kNoAcq) acquire_agent();
       } else if (spins > kSpinMax) {
         timeout();
       } else {
@@ -785,7 +882,7 @@ struct ChunkReady {
       take(v, lane, &c);
       if (c) {
         lo -= c;
-        acquire_agent();
+        if (!kNoAcq) acquire_agent();
       } else if (spins > kSpinMax) {
         timeout();
       } else {
@@ -953,8 +1050,15 @@ LT_DEVINL void num_walk(const CkArgs& a, int b, int lane, int nf, int Kl, int nl
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       const int uc = min(lane + 64 * r, NPG - 1);
-      g[r][0] = row[2 * uc];
-      g[r][1] = row[2 * uc + 1];
+      if constexpr (kNoAcq) {
+        const __amdgpu_buffer_rsrc_t rr =
+            __builtin_amdgcn_make_buffer_rsrc((void*)row, (short)0, 32 * NPG, 0x00020000);
+        g[r][0] = ld_sc1x4(rr, 32 * uc);
+        g[r][1] = ld_sc1x4(rr, 32 * uc + 16);
+      } else {
+        g[r][0] = row[2 * uc];
+        g[r][1] = row[2 * uc + 1];
+      }
     }
   };
   auto step = [&](float4 (*g)[2], int q, int qn) {
@@ -1087,7 +1191,7 @@ LT_DEVINL void combine_role(const CkArgs& a, int b, int wave, unsigned char* dyn
   auto issue_rec = [&](int k, int n) {  // step n's record k (clamped to [0, Kl)) -> slot n mod kWalkSlots
     const int kc = min(max(k, 0), Kl - 1);
     dma_issue((const unsigned char*)a.rec, ((long long)b * a.K + kc) * (kRec * 4), kRec * 4,
-              ring_a + (unsigned)((n % kWalkSlots) * kWalkSlot), kRecNi, lane);
+              ring_a + (unsigned)((n % kWalkSlots) * kWalkSlot), kRecNi, lane, 0, 1, kNoAcq);
   };
   // step n's record has landed: the ring's issues and each step's one
   // boundary-row store, in issue order (vmcnt counts both, in order; the
@@ -1496,7 +1600,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    acquire_agent();
+    if (!kNoAcq) acquire_agent();
     CK_STAMP(6);
     fl[2 * a.L + 2] = ok;
   }
@@ -1613,7 +1717,9 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     const int q = lane & 31, h = lane >> 5;
     const int qe = min(q, V - 1) + 1;
     const bool core = lane >= 1 && lane <= V;
-    const float x0 = lane < C ? a.abd[((long long)b * (a.K + 1) + k) * CP + lane] : -kInf;
+    const float* xp = a.abd + ((long long)b * (a.K + 1) + k) * CP + min(lane, C - 1);
+    const float xr = kNoAcq ? ld_sc1(xp) : *xp;
+    const float x0 = lane < C ? xr : -kInf;
     float a0 = first_lane(x0);
     float S = wmax_u(core ? x0 : -kInf);  // -inf: no core state reached yet
     float al = (core && S != -kInf) ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
@@ -1713,7 +1819,9 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
     const int j = lane & 31, h = lane >> 5;
     const int pe = min(j, V - 1) + 1;
     const bool core = lane >= 1 && lane <= V;
-    const float x0 = lane < C ? a.bbd[((long long)b * (a.K + 1) + k + 1) * CP + lane] : -kInf;
+    const float* xp = a.bbd + ((long long)b * (a.K + 1) + k + 1) * CP + min(lane, C - 1);
+    const float xr = kNoAcq ? ld_sc1(xp) : *xp;
+    const float x0 = lane < C ? xr : -kInf;
     float b0 = first_lane(x0);
     float S = safe_max(wmax_u(core ? x0 : -kInf));
     float be = core ? __builtin_amdgcn_exp2f(x0 - S) : 0.f;
@@ -1806,7 +1914,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       const int u = lane + 64 * r, uc = min(u, NPG - 1);
-      const float v = src[uc];  // log2, relative to the walk's offset
+      const float v = kNoAcq ? ld_sc1(src + uc) : src[uc];  // log2, relative to the walk's offset
       al[r] = u < NPG ? v : -kInf;
     }
     for (int f = 0; f < nt; ++f) {
@@ -1834,7 +1942,7 @@ __global__ __launch_bounds__(64 * kMargWaves, kMargWaves / 2) void ck_marg_kerne
 #pragma unroll
     for (int r = 0; r < PPL; ++r) {
       const int u = lane + 64 * r, uc = min(u, NPG - 1);
-      const float v = src[uc];
+      const float v = kNoAcq ? ld_sc1(src + uc) : src[uc];
       be[r] = u < NPG ? v : -kInf;
     }
     if (a.pf) {  // the chunk of the block about a.pf dispatches later, into L2

@@ -398,6 +398,23 @@ LT_DEVINL void glds16(const void* gsrc, unsigned lds_addr) {
       : "memory");
 }
 
+// glds16 with the sc1 cache policy: the 16 bytes come from L2 (past this
+// CU's L1), so data another CU published in the same launch is read fresh
+// without an agent-scope acquire (buffer_inv sc1) first
+LT_DEVINL void glds16_sc1(const void* gsrc, unsigned lds_addr) {
+  unsigned keep;
+  lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off sc1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
 #define LT_VMCNT_CASE(N) \
   case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
 LT_DEVINL void wait_vmcnt(int n) {
