@@ -104,6 +104,12 @@ constexpr unsigned kSpinMax = 1u << 20;
 #define LT_CK_NOACQ 1
 #endif
 constexpr bool kNoAcq = LT_CK_NOACQ != 0;
+#ifndef LT_CK_ALDS
+#define LT_CK_ALDS 0
+#endif
+constexpr bool kALds = LT_CK_ALDS != 0;  // phase A: frames through an LDS ring (two slots a wave)
+constexpr int kASlot = 5 * 1024;         // bytes per slot (a fp32 bigram frame: 5 DMA instructions)
+constexpr int kALdsBytes = 4 * 2 * kASlot;  // dynamic LDS of phase A's workgroups
 #ifndef LT_CK_BANDMIX
 #define LT_CK_BANDMIX 0
 #endif
@@ -445,6 +451,28 @@ LT_DEVINL void load_frame(const unsigned char* Wf, int bytes, const FrameOffs<PP
     f.gl[q] = ldb<BF16>(r, o.vgl[q], 0);
   }
 }
+// load_frame's values from a frame staged in LDS (LT_CK_ALDS: `fr` = the
+// frame's first byte in the wave's ring slot)
+template <bool BF16, int PPL, bool FULL>
+LT_DEVINL void lds_frame(const unsigned char* fr, const FrameOffs<PPL>& o,
+                         FrameRegs<BF16, PPL>& f) {
+  constexpr int es = BF16 ? 2 : 4;
+  auto rd = [&](int off) -> float {
+    if constexpr (BF16) return __uint_as_float((unsigned)*(const unsigned short*)(fr + off) << 16);
+    else return *(const float*)(fr + off);
+  };
+#pragma unroll
+  for (int s = 0; s < 16; ++s) f.w[s] = FULL ? rd(o.vb + krow(s) * 33 * es) : rd(o.vb + o.srow[s]);
+  f.wr0 = rd(o.vr0);
+  f.wbl = rd(o.vbl);
+  f.wdg = rd(o.vdg);
+  f.w00 = rd(0);
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) {
+    f.gb[q] = rd(o.vgb[q]);
+    f.gl[q] = rd(o.vgl[q]);
+  }
+}
 // the values load_frame read for nothing (FULL: V = 32, every core value live)
 template <bool BF16, int PPL, bool FULL>
 LT_DEVINL void mask_frame(int V, int lane, const int* boff, const int* loff,
@@ -551,6 +579,18 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
   FrameRegs<BF16, PPL> fr;
   FrameOffs<PPL> fo;
   frame_offsets<BF16, PPL>(a, lane, boff, loff, fo);
+  // LT_CK_ALDS: this wave's two ring slots in the launch's dynamic LDS
+  extern __shared__ __attribute__((aligned(16))) unsigned char ck_dyn[];
+  unsigned char* aring = ck_dyn + wave * 2 * kASlot;
+  float cfl_lane = 0.f;  // LT_CK_ALDS: lane f holds frame f's offset
+  auto goff = [&](int f) { return ((long long)b * a.T + t0 + f) * a.FB; };
+  auto aissue = [&](int f) {
+    dma_issue(a.W, goff(f), a.FB, lds_base_addr(aring) + (unsigned)((f & 1) * kASlot), a.a_ni, lane);
+  };
+  auto aframe = [&](int f) -> const unsigned char* {
+    return aring + (f & 1) * kASlot + (int)(goff(f) & 15);
+  };
+  (void)aissue; (void)aframe;
   auto frame_ptr = [&](int f) { return W0 + (long long)min(f, nt - 1) * a.FR * es; };
   auto frame_bytes = [&](int f) { return (nt - min(f, nt - 1)) * a.FR * (int)es; };
   auto step = [&](FrameRegs<BF16, PPL>& F, int f, bool reload) {
@@ -609,6 +649,14 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
       }
       __builtin_amdgcn_wave_barrier();
     }
+    if constexpr (kALds) {
+      // frame f + 2 into the slot frame f came through (its reads into F have
+      // returned: F was just used)
+      if (f + 2 < nt && !LT_ABL(a, 8192)) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        aissue(f + 2);
+      }
+    }
     // the frame's offset c = ceil(max W log2 e), an integer in log2 units
     // (masked values are -inf), so every sum of offsets is exact
     float mx = max3_raw(F.wr0, F.wbl, F.w[15]);
@@ -617,7 +665,8 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     mx = wmax_u(mx);
     const bool cfin = __builtin_isfinite(mx);
     const float cl = cfin ? ceilf(mx * kLog2e) : 0.f;
-    if (lane == 0) a.cf[(long long)b * a.T + t0 + f] = cl;
+    if constexpr (kALds) cfl_lane = lane == f ? cl : cfl_lane;  // stored after the frames
+    else if (lane == 0) a.cf[(long long)b * a.T + t0 + f] = cl;
     // E_t^T as the A operand: lane (i, h), k-step s -> E[k][i]. The core
     // diagonal's blank self loop (alignments.py:294-297) is added beside
     // the product (Dg X after the MFMAs, rt Dg in the state-0 row), which
@@ -657,8 +706,17 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     }
     const float w00 = F.w00;
     // (diagnostic builds: bit 8192 keeps the chunk's first frame -- timing only)
-    if (reload && !LT_ABL(a, 8192))
+    if constexpr (kALds) {
+      // frame f + 1 from its ring slot: its DMA was issued at the start of
+      // step f - 1; only frame f + 2's (issued at the start of this step)
+      // may still be in flight
+      if (reload && !LT_ABL(a, 8192)) {
+        wait_vmcnt(f + 2 < nt ? a.a_ni : 0);
+        lds_frame<BF16, PPL, FULL>(aframe(f + 1), fo, F);
+      }
+    } else if (reload && !LT_ABL(a, 8192)) {
       load_frame<BF16, PPL, FULL>(frame_ptr(f + kApf), frame_bytes(f + kApf), fo, F);
+    }
 
     // state-0 row: r' = p00 * e0 + r Ec (VALU, beside the MFMAs), scaled by
     // a power of two so that its largest entry sits in [1/2, 1)
@@ -754,7 +812,19 @@ LT_DEVINL void transfer_role(const CkArgs& a, int b, int k, int wave) {
     for (int r = 0; r < 16; ++r) X[r] = ldexpf(D[r], -e);
     ej += e;
   };
-  if constexpr (kApf == 1) {
+  if constexpr (kALds) {
+    // LT_CK_ALDS: the chunk's frames through a two-slot LDS ring per wave
+    // (LDS-DMA, 16 bytes a lane, a_ni wave instructions a frame) and into F
+    // one step ahead: frame f + 2's DMA is issued at the start of step f, so
+    // every frame has more than a step to land (the register prefetch gave
+    // it two thirds of one), with no registers held for it
+    aissue(0);
+    if (nt > 1) aissue(1);
+    wait_vmcnt(nt > 1 ? a.a_ni : 0);
+    lds_frame<BF16, PPL, FULL>(aframe(0), fo, fr);
+    for (int f = 0; f < nt; ++f) step(fr, f, f + 1 < nt);
+    if (lane < nt) a.cf[(long long)b * a.T + t0 + lane] = cfl_lane;
+  } else if constexpr (kApf == 1) {
     // one frame in registers ahead
     load_frame<BF16, PPL, FULL>(frame_ptr(0), frame_bytes(0), fo, fr);
     for (int f = 0; f < nt; ++f) step(fr, f, f + 1 < nt);
@@ -2374,7 +2444,7 @@ int ck_launch_ab(CkArgs& a, bool bf16, hipStream_t st) {
   const int at = ck_env("LT_CHUNK_WALK_AT", std::max(0, 100 - 4800 / std::max(a.B, 1)));
   a.wpos = (int)(nwa * std::min(std::max(at, 0), 100) / 100);
   int rc = ck_launch(ck_kernel_ab(a.PPL, bf16, a.V == 32), (int)(a.nc + nwa),
-                     fuse ? kWalkLdsBytes : 0, st, a);
+                     std::max(fuse ? kWalkLdsBytes : 0, kALds ? kALdsBytes : 0), st, a);
   if (rc || fuse) return rc;
   return ck_launch(ck_kernel_b(a.PPL), a.B, kWalkLdsBytes, st, a);
 }

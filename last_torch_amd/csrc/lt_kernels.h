@@ -494,6 +494,10 @@ struct KArgs {
   int gw0, gw1;                    // instructions per frame of loader wave 0 / 1
   int off_ring, off_a, off_na, off_ctx, off_ylab, off_dbuf, off_nbuf, off_misc;
   int off_tb;        // trigram V = 32 backward: the padded beta rows [2][kTriBPad]
+  // the trigram overlap (lt_tri.hip, tri_mix_kernel): nullable; [2B] frames
+  // whose checkpoint rows are final, published every kTriPub frames (forward:
+  // rows [0, p); backward: rows [nf - 1 - p, nf))
+  unsigned* prog;
 };
 
 // The kernel arguments re-read from the kernarg segment through a pointer
@@ -1009,6 +1013,53 @@ LT_DEVINL float den_fwd_loop(const KArgs& a, unsigned char* lds, float* abuf, in
 // image, three slots in rotation) to the next step, which subtracts its
 // floor (the same rounding scheme as den_sub_take, without a serial pass).
 // ---------------------------------------------------------------------------
+// 16-byte units of W / dW (marg_kernel, the trigram overlap's marginal role)
+template <bool BF16>
+LT_DEVINL void unpack_unit(const uint4 q, float* w) {
+  if constexpr (BF16) {
+    const unsigned u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w[2 * i] = __uint_as_float(u[i] << 16);
+      w[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  } else {
+    w[0] = __uint_as_float(q.x); w[1] = __uint_as_float(q.y);
+    w[2] = __uint_as_float(q.z); w[3] = __uint_as_float(q.w);
+  }
+}
+template <bool BF16>
+LT_DEVINL void store_unit(unsigned char* p, const float* v) {
+  uint4 q;
+  if constexpr (BF16) {
+    q.x = f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    q.y = f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    q.z = f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+    q.w = f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+  } else {
+    q.x = __float_as_uint(v[0]); q.y = __float_as_uint(v[1]);
+    q.z = __float_as_uint(v[2]); q.w = __float_as_uint(v[3]);
+  }
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  v4u qv = {q.x, q.y, q.z, q.w};
+  __builtin_nontemporal_store(qv, (v4u*)p);  // dW is written once: one 16-byte store
+}
+
+
+// The trigram overlap's progress words (KArgs::prog, tri_mix_kernel): every
+// kTriPub frames the waves that store checkpoint rows (den and numerator
+// roles) drain their stores before the frame's barrier, and thread 0
+// publishes the count after it (an sc1 store; the marginal workgroups on the
+// same XCD poll it with sc1 loads and read the rows with sc1 loads)
+constexpr int kTriPub = 64;
+LT_DEVINL bool tri_pub_frame(const KArgs& a, int i) { return a.prog && i > 0 && i % kTriPub == 0; }
+LT_DEVINL void tri_pub_drain(const KArgs& a, int i) {
+  if (tri_pub_frame(a, i)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+LT_DEVINL void tri_pub_store(const KArgs& a, int b, int dir, unsigned v) {
+  if (a.prog && threadIdx.x == 0)
+    __hip_atomic_store(a.prog + 2 * b + dir, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 constexpr int kTriDenWaves = 9;
 #ifndef LT_TRI_LOAD
 #define LT_TRI_LOAD 4
@@ -1054,7 +1105,9 @@ LT_DEVINL float den_fwd_tri(const KArgs& a, unsigned char* lds, float* abuf, int
   float* hist = a.alpha ? a.alpha + (long long)b * a.T * C : nullptr;
   float O = 0.f;
   for (int i = 0; i < nf; ++i) {
+    tri_pub_drain(a, i);
     lds_barrier();
+    if (tri_pub_frame(a, i)) tri_pub_store(a, b, 0, (unsigned)i);
     const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
     const float* acur = abuf + (i & 1) * C;
     float* anxt = abuf + ((i + 1) & 1) * C;
@@ -1136,6 +1189,7 @@ LT_DEVINL float num_fwd_loop(const KArgs& a, unsigned char* lds, float* nbuf, co
   float O = 0.f;  // Log: the vector's integer offset (MaxTropical / Real: 0, exact values)
   for (int i = 0; i < nf; ++i) {
     LT_STAMP(a, al == 0, 1, i, 0);
+    tri_pub_drain(a, i);
     lds_barrier();
     LT_STAMP(a, al == 0, 1, i, 1);
     const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
@@ -1220,7 +1274,10 @@ LT_DEVINL void fwd_body(const KArgs& a, const int b) {
       noff = num_fwd_loop<MODE, BF16, WST>(a, lds, nbuf, ctx, ylab, b, nf, al, aux_lanes);
     else idle_loop(nf);
   }
+  // the trigram overlap: every row final (the storing roles drain first)
+  if (a.prog && role != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
+  tri_pub_store(a, b, 0, (unsigned)nf);
 
   // ---- finalize: shortest distance = (+)_q alpha_T[q] (lattices.py:496)
   const int fin = nf & 1;
@@ -1539,7 +1596,9 @@ LT_DEVINL void den_bwd_tri32(const KArgs& a, unsigned char* lds, int b, int nf, 
   float* brow = a.beta ? a.beta + (t_last - 1) * C : nullptr;
   float Ob = 0.f;
   for (int i = 0; i < nf; ++i) {
+    tri_pub_drain(a, i);
     lds_barrier();
+    if (tri_pub_frame(a, i)) tri_pub_store(a, b, 1, (unsigned)i);
     const unsigned char* wrow = WST ? ring + cw.soff + cw.mis : a.W + cw.goff;
     const float* bcur = pbuf + (i & 1) * kTriBPad;
     float* bnxt = pbuf + ((i + 1) & 1) * kTriBPad;
@@ -1796,6 +1855,7 @@ LT_DEVINL void num_beta_loop(const KArgs& a, unsigned char* lds, float* nbb, con
   float Ob = 0.f;  // the vector's integer offset (num_sub_take); rows are Ob + value
   for (int i = 0; i < nf; ++i) {
     LT_STAMP(a, al == 0, 1, i, 0);
+    tri_pub_drain(a, i);
     lds_barrier();
     LT_STAMP(a, al == 0, 1, i, 1);
     const unsigned char* wrow = WST ? ringw + cw.soff + cw.mis : a.W + cw.goff;
@@ -1929,7 +1989,14 @@ LT_DEVINL void bwd_body(const KArgs& a, const int b) {
       idle_loop(nf);
     }
   }
-  if constexpr (CK) return;
+  if constexpr (CK) {
+    if (a.prog) {  // the trigram overlap: every row final (the storing roles drain first)
+      if (role != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      tri_pub_store(a, b, 1, (unsigned)nf);
+    }
+    return;
+  }
   lds_barrier();
   // padding frames get zero marginals (lattices.py:775-779)
   {
@@ -1976,6 +2043,48 @@ __global__ __launch_bounds__(1024) void fwdbwd_kernel(const KArgs af, const KArg
 }  // namespace
 
 namespace lt_impl {
+// The trigram overlap (lt_tri.hip, tri_mix_kernel): what its marginal
+// workgroups read and write besides the recursions' KArgs
+struct MixArgs {
+  const unsigned char* W;
+  const int* nfr;
+  const int* labels;
+  const float *alpha, *beta, *alpha_num, *beta_num;  // the recursions' checkpoint rows
+  const float* grad;  // nullable (ones)
+  void* dW;
+  unsigned* prog;     // [2B] the recursions' progress (KArgs::prog)
+  unsigned* xcc;      // [2B] XCD id + 1 of each recursion workgroup (0: not yet)
+  unsigned* ctr;      // [8 * 32] per-XCD job counters, one 128-byte line each
+  int* done;          // [B*T] frame done here (marg_kernel skips it)
+  int B, T, U;
+  NGram g;
+};
+
+// log Z and the string's weight of one utterance from its checkpoint rows at
+// a middle frame m: (+)_q alpha_m[q] beta_m[q] and (+)_u alpha^n_m[u] beta^n_m[u]
+// (any frame gives both: every path crosses it). One wave, a fixed lane order
+// and butterfly, so the trigram overlap's marginal role and marg_kernel get
+// the same bits; sc1: rows another workgroup of the same launch published.
+LT_DEVINL float2 tri_mid_norm(const float* ar, const float* br, const float* anr,
+                              const float* bnr, int C, int NP, int lane, bool sc1) {
+  auto ld = [&](const float* p) -> float {
+    return sc1 ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+  };
+  auto lse = [&](const float* x, const float* y, int n) {
+    float mx = -kInf;
+    for (int q = lane; q < n; q += 64) mx = fmaxf(mx, ld(x + q) + ld(y + q));
+    mx = gmax<6>(mx, 6);
+    const float c = __builtin_isfinite(mx) ? mx : 0.f;
+    float s = 0.f;
+    for (int q = lane; q < n; q += 64) s += lt_exp(ld(x + q) + ld(y + q) - c);
+    s = gsum<6>(s, 6);
+    return c + lt_log(s);
+  };
+  const float lz = lse(ar, br, C);
+  const float nm = lse(anr, bnr, NP);
+  return make_float2(lz, nm);
+}
+
 struct Plan {
   KArgs a;
   int lg;    // template LG (log2 lanes per group), -1 = runtime
@@ -2007,6 +2116,11 @@ inline bool stream_capturing(hipStream_t st) {
 }
 // lt_tri.hip: the trigram checkpointing pair (den_fwd_tri / den_bwd_tri roles)
 int launch_tri_fwdbwd(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStream_t st);
+// lt_tri.hip: the same recursions with marginal workgroups on the idle CUs
+// (tri_mix_kernel, V = 32); marg_kernel afterwards takes the frames not done
+int tri_mix_lds(const NGram& g, int U, int B);
+int launch_tri_mix(const Plan& pf, const Plan& pb, bool bf16, int nb, int marg_blocks,
+                   const MixArgs& mx, hipStream_t st);
 // lt_tri4.hip (diagnostic builds only): the V = 32 trigram recursions on
 // quads of four workgroups
 bool tri4_eligible(int V, int n, int B, int U, int cus);
@@ -2060,3 +2174,7 @@ int launch_pipe(const lt_problem* pb, int local_norm, const void* W, const int32
 size_t pipe_mid_workspace_bytes(const lt_problem* pb);
 bool pipe_mid_fits(const lt_problem* pb);
 }  // namespace lt_impl
+namespace {
+using lt_impl::MixArgs;
+using lt_impl::tri_mid_norm;
+}  // namespace

@@ -77,6 +77,10 @@ struct MgArgs {
   int nmode;
   int off_hm, off_hp, off_hv;
   int xcd;       // frame slices: the tpf slices of a frame on one XCD (blocks 8 apart)
+  // the trigram overlap (lt_tri.hip): frames its marginal workgroups did are
+  // skipped; every frame normalised by the middle-frame norm (tri_mid_norm)
+  const int* done;  // [B*T] nullable
+  int mid_norm;
 };
 
 // n / d from the magic m = ceil(2^32 / d), corrected to exact.
@@ -89,37 +93,6 @@ LT_DEVINL unsigned fdiv(unsigned n, unsigned d, unsigned m) {
 inline unsigned magic_of(unsigned d) { return (unsigned)((0x100000000ULL + d - 1) / d); }
 
 constexpr int kMgUnits = 5;  // 16-byte units of W per thread and tile
-
-template <bool BF16>
-LT_DEVINL void unpack_unit(const uint4 q, float* w) {
-  if constexpr (BF16) {
-    const unsigned u[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      w[2 * i] = __uint_as_float(u[i] << 16);
-      w[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
-    }
-  } else {
-    w[0] = __uint_as_float(q.x); w[1] = __uint_as_float(q.y);
-    w[2] = __uint_as_float(q.z); w[3] = __uint_as_float(q.w);
-  }
-}
-template <bool BF16>
-LT_DEVINL void store_unit(unsigned char* p, const float* v) {
-  uint4 q;
-  if constexpr (BF16) {
-    q.x = f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-    q.y = f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-    q.z = f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
-    q.w = f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
-  } else {
-    q.x = __float_as_uint(v[0]); q.y = __float_as_uint(v[1]);
-    q.z = __float_as_uint(v[2]); q.w = __float_as_uint(v[3]);
-  }
-  typedef unsigned v4u __attribute__((ext_vector_type(4)));
-  v4u qv = {q.x, q.y, q.z, q.w};
-  __builtin_nontemporal_store(qv, (v4u*)p);  // dW is written once: one 16-byte store
-}
 
 // One tile: F whole frames (small frames) or one slice of a frame.
 //   phase 0: the tile's W as 16-B units into registers; alpha/beta (+num)
@@ -156,8 +129,35 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   const int s0 = !SLICED ? 0 : tile % a.tpf;
   const int Fh = !SLICED ? min(a.F, a.T - t0) : 1;
   float gb = a.grad ? a.grad[b] : 1.f;
-  const float lz = a.do_den ? a.log_z[b] : 0.f;
-  const float nm = a.do_num ? a.num[b] : 0.f;
+  float lz = a.do_den ? a.log_z[b] : 0.f;
+  float nm = a.do_num ? a.num[b] : 0.f;
+  if constexpr (SLICED) {
+    // the trigram overlap: a frame its marginal workgroups did is skipped;
+    // the others take the same middle-frame norm they did
+    if (a.done && a.done[(long long)b * a.T + t0]) return;
+    if (a.mid_norm) {
+      __shared__ float s_mid[2];
+      int nf0 = a.nfr[b];
+      nf0 = nf0 < 0 ? 0 : (nf0 > a.T ? a.T : nf0);
+      if (nf0 >= 2) {
+        if (threadIdx.x < 64) {
+          const int mid = nf0 / 2, C0 = a.g.C, NP0 = a.U + 1;
+          const long long r0 = (long long)b * a.T;
+          const float2 zn = tri_mid_norm(a.alpha + (r0 + mid) * C0, a.beta + (r0 + mid - 1) * C0,
+                                         a.alpha_num + (r0 + mid) * NP0,
+                                         a.beta_num + (r0 + mid - 1) * NP0, C0, NP0,
+                                         threadIdx.x, false);
+          if (threadIdx.x == 0) {
+            s_mid[0] = zn.x;
+            s_mid[1] = zn.y;
+          }
+        }
+        __syncthreads();
+        lz = s_mid[0];
+        nm = s_mid[1];
+      }
+    }
+  }
   if ((a.do_num && !__builtin_isfinite(nm)) || (a.do_den && !__builtin_isfinite(lz))) gb = 0.f;
   const int Fl = max(0, min(Fh, nf - t0));  // live frames of the tile
   // slice sl: elements [e_lo, e_hi) of each of the tile's frames, contiguous
@@ -905,7 +905,7 @@ int cu_count() {
 // lt_loss_grad workspace: checkpoints, arc table and the recursion
 // backward's side buffer, each 256-byte aligned
 struct GradWs {
-  size_t alpha, beta, an, bn, arcs, side, total;
+  size_t alpha, beta, an, bn, arcs, side, mix, total;
 };
 GradWs grad_ws(const lt_problem* pb, int local_norm) {
   GradWs w;
@@ -920,9 +920,21 @@ GradWs grad_ws(const lt_problem* pb, int local_norm) {
   w.bn = o; o += up(4 * B * T * NP);
   w.arcs = o; o += up(4 * B * 4 * NP);
   w.side = o; o += up((long long)side_bytes(pb));
+  // the trigram overlap: progress words, XCD ids, per-XCD job counters, done flags
+  w.mix = o; o += g.n == 2 ? up(4 * (4 * B + 8 * 32 + B * T)) : 0;
   w.total = o;
   return w;
 }
+
+// The trigram overlap's hand-over from lt_loss_grad to the lt_loss_forward
+// / lt_loss_backward calls it makes (set only for their duration, this thread)
+struct MixReq {
+  MixArgs m;      // prog / xcc / ctr / done set; the rest filled at the launch
+  int blocks;     // marginal workgroups
+  bool launched;  // lt_loss_forward took the overlap route
+};
+thread_local MixReq* t_mix = nullptr;
+thread_local const int* t_mix_done = nullptr;
 
 }  // namespace
 
@@ -1156,6 +1168,18 @@ int lt_loss_forward(const lt_problem* pb, int32_t local_norm, const void* W,
       ka.gw1 = instr / ka.load_waves;
       pl->threads = 64 * (kTriDenWaves + ka.aux_waves + ka.load_waves);
     }
+    if (t_mix && g.V == 32 && pb->batch % 8 == 0) {
+      // lt_loss_grad's trigram route: marginal workgroups on the idle CUs in
+      // the same launch (lt_tri.hip, tri_mix_kernel)
+      pf.a.prog = pbk.a.prog = t_mix->m.prog;
+      MixArgs mx = t_mix->m;
+      mx.W = (const unsigned char*)W; mx.nfr = num_frames; mx.labels = labels;
+      mx.alpha = alpha; mx.beta = beta; mx.alpha_num = alpha_num; mx.beta_num = beta_num;
+      mx.B = pb->batch; mx.T = pb->max_frames; mx.U = pb->max_labels; mx.g = g;
+      if ((rc = lt_impl::launch_tri_mix(pf, pbk, bf16, pb->batch, t_mix->blocks, mx, st))) return rc;
+      t_mix->launched = true;
+      return LT_OK;
+    }
     return lt_impl::launch_tri_fwdbwd(pf, pbk, bf16, pb->batch, st);
   }
   // same geometry (the usual case): beta and alpha side by side in one
@@ -1225,6 +1249,8 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
     m.W = (const unsigned char*)W; m.nfr = num_frames;
     m.alpha = alpha; m.beta = beta; m.alpha_num = alpha_num; m.beta_num = beta_num;
     m.arcs = arcs; m.log_z = log_z; m.num = num; m.grad = grad; m.dW = dW;
+    m.done = t_mix_done;  // the trigram overlap's frames (lt_loss_grad only)
+    m.mid_norm = t_mix_done != nullptr;
     if (grid == 0) return LT_OK;
     hipStream_t st = (hipStream_t)stream;
     const bool bf = pb->weight_dtype == LT_DTYPE_BF16, sliced = m.tpf > 1;
@@ -1471,11 +1497,38 @@ int lt_loss_grad_ex(const lt_problem* pb, int32_t local_norm, int32_t design_in,
   // workgroups find CUs; with the pipelined bigram recursions up to 1.5 CUs
   // utterances (measured crossover ~1.75: tools/b256_check.py)
   if (design == LT_DESIGN_CHECKPOINTS || design == LT_DESIGN_FUSED_PIPE) {
-    if ((rc = lt_loss_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z,
-                              num, alpha, an, beta, bn, arcs, stream)))
-      return rc;
-    return lt_loss_backward(pb, local_norm, W, num_frames, labels, num_labels, log_z, num,
-                            alpha, an, beta, bn, arcs, nullptr, dW, nullptr, 0, stream);
+    // trigram V = 32: the recursions with marginal workgroups on the CUs they
+    // leave idle (lt_tri.hip), marg_kernel afterwards on the frames not done
+    const int cus = cu_count();
+    MixReq req;
+    const bool mix = g.n == 2 && g.V == 32 && !local_norm && pb->batch % 8 == 0 &&
+                     2 * pb->batch + 8 <= cus && pb->max_frames >= 2 && pb->max_frames < 65536 &&
+                     lt_impl::tune_int("LT_TRI_MIX", 1) != 0;
+    if (mix) {
+      memset(&req, 0, sizeof(req));
+      const long long B = pb->batch;
+      unsigned* mw = (unsigned*)(ws + w.mix);
+      req.m.prog = mw;
+      req.m.xcc = mw + 2 * B;
+      req.m.ctr = mw + 4 * B;
+      req.m.done = (int*)(mw + 4 * B + 8 * 32);
+      req.m.dW = dW;
+      req.blocks = cus - 2 * pb->batch;
+      if ((rc = hip_check(hipMemsetAsync(mw, 0, 4 * (size_t)(4 * B + 8 * 32 + B * pb->max_frames),
+                                         (hipStream_t)stream),
+                          "overlap memset")))
+        return rc;
+      t_mix = &req;
+    }
+    rc = lt_loss_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z, num,
+                         alpha, an, beta, bn, arcs, stream);
+    t_mix = nullptr;
+    if (rc) return rc;
+    t_mix_done = mix && req.launched ? req.m.done : nullptr;
+    rc = lt_loss_backward(pb, local_norm, W, num_frames, labels, num_labels, log_z, num, alpha,
+                          an, beta, bn, arcs, nullptr, dW, nullptr, 0, stream);
+    t_mix_done = nullptr;
+    return rc;
   }
   if ((rc = lt_loss_forward(pb, local_norm, W, num_frames, labels, num_labels, loss, log_z, num,
                             alpha, an, nullptr, nullptr, nullptr, stream)))

@@ -6,6 +6,25 @@
 // (backward), every term of a state in that lane's registers. The numerator
 // and loader roles are fwd_body / bwd_body's own. lattices.py:379-496 and
 // 686-799 (alignments.py:286-318, contexts.py:207-256).
+//
+// The overlap (tri_mix_kernel, lt_loss_grad's trigram V = 32 route, round 6):
+// the 2B recursion workgroups hold 2B CUs for the whole call while the rest of
+// the chip idles, and the marginal pass (marg_kernel) used to run only after
+// them. Here the launch also carries one marginal workgroup per idle CU. A
+// frame's marginals need alpha_t and beta_{t+1} only, so frames become ready
+// from the middle of the utterance outwards once both recursions have passed
+// it (alignments.py:300-318: each frame's marginals are the reference's
+// FrameDependent.backward of that frame). The recursions publish their
+// checkpoint rows every kTriPub frames (KArgs::prog); a marginal workgroup
+// takes the frames of the utterances whose two recursion workgroups share its
+// XCD (their plain row stores sit in that XCD's L2, which its sc1 loads read),
+// in the order they become ready, and marks each frame done. marg_kernel then
+// runs as before on the frames not done (the others return at once), so a
+// placement that shares no XCD or a wait that times out only moves work back
+// to it. Every frame is normalised by log Z and the string's weight taken
+// from the rows at the middle frame m = nf / 2 (alpha_m . beta_m,
+// tri_mid_norm: the same fixed-order wave reduction in both kernels), so the
+// result does not depend on which kernel took a frame.
 #include "lt_kernels.h"
 
 namespace {
@@ -18,6 +37,287 @@ __global__ __launch_bounds__(1024) void tri_fwdbwd_kernel(const KArgs af, const 
   } else if (!LT_ABL(af, 32)) {
     bwd_body<BF16, true, false, 2, 9, true, (int)sizeof(KArgs), VT>(ab, blockIdx.x - nb);
   }
+}
+
+LT_DEVINL unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+  return v;
+}
+LT_DEVINL unsigned ld_u32_sc1(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+LT_DEVINL float ld_f32_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr unsigned kMixSpins = 1u << 22;  // ~1 s of polling, then the frames go back to marg_kernel
+constexpr int kMixUnits = 5;              // 16-byte units of W in flight per thread
+
+}  // namespace
+
+namespace {
+
+template <bool BF16>
+LT_DEVINL void mix_stage_rows(const MixArgs& m, int b, int t, float* A, float* Bt, float* AN,
+                              float* BN, int tid, int nthr) {
+  const int C = m.g.C, NP = m.U + 1;
+  const long long rc = ((long long)b * m.T + t) * C, rn = ((long long)b * m.T + t) * NP;
+  for (int e = tid; e < C; e += nthr) {
+    A[e] = ld_f32_sc1(m.alpha + rc + e);
+    Bt[e] = ld_f32_sc1(m.beta + rc + e);
+  }
+  for (int e = tid; e < NP; e += nthr) {
+    AN[e] = ld_f32_sc1(m.alpha_num + rn + e);
+    BN[e] = ld_f32_sc1(m.beta_num + rn + e);
+  }
+}
+
+// One frame's marginals, the whole workgroup: den elements straight from the
+// staged rows (marg_tile's expressions), stored by 16-byte units; then the
+// string's chain heads rewrite their elements as den - num (marg_tile's
+// phase 2).
+template <bool BF16>
+LT_DEVINL void mix_frame(const MixArgs& m, int b, int t, float lz, float nm, const float* A,
+                         const float* Bt, const float* AN, const float* BN, const int* aoff,
+                         const int* alink, const int* nbt, int tid, int nthr) {
+  constexpr int VE = BF16 ? 8 : 4, ES = BF16 ? 2 : 4;
+  constexpr int V = 32, R = 33, C = 1 + 32 + 32 * 32, FR = C * R;
+  const int NP = m.U + 1, NK = 2 * NP;
+  const float gb = m.grad ? m.grad[b] : 1.f;
+  const long long base = ((long long)b * m.T + t) * FR;
+  const int h0 = (int)(((16 - ((base * ES) & 15)) & 15) / ES);
+  const int nunits = (FR - h0) / VE;
+  const int ntail = h0 + (FR - h0 - nunits * VE);
+  const unsigned char* Wu = m.W + (base + h0) * ES;
+  unsigned char* dWu = (unsigned char*)m.dW + (base + h0) * ES;
+  auto den_el = [&](int el, float w) {
+    const int p = el / R, y = el - p * R;
+    const int q = y == 0 ? p : nbt[p] + y;
+    return gb * lt_exp(A[p] + w + Bt[q] - lz);
+  };
+  for (int u0 = tid; u0 < nunits; u0 += kMixUnits * nthr) {
+    uint4 wq[kMixUnits];
+#pragma unroll
+    for (int r = 0; r < kMixUnits; ++r) {
+      const int u = u0 + r * nthr;
+      if (u < nunits) wq[r] = *(const uint4*)(Wu + (long long)u * 16);
+    }
+#pragma unroll
+    for (int r = 0; r < kMixUnits; ++r) {
+      const int u = u0 + r * nthr;
+      if (u >= nunits) break;
+      float w[VE], v[VE];
+      unpack_unit<BF16>(wq[r], w);
+      const int e0 = h0 + u * VE;
+      int p = e0 / R;
+      const int y = e0 - p * R;
+      // a unit spans at most two source rows (R >= VE)
+      const int p1 = min(p + 1, C - 1);
+      const float a0v = A[p], a1v = A[p1];
+      const int nb0 = nbt[p], nb1 = nbt[p1];
+#pragma unroll
+      for (int c = 0; c < VE; ++c) {
+        const int yc = y + c;
+        const bool w2 = yc >= R;
+        const int yy = w2 ? yc - R : yc;
+        const int pp = w2 ? p1 : p;
+        const int q = yy == 0 ? pp : (w2 ? nb1 : nb0) + yy;
+        const float av = w2 ? a1v : a0v;
+        v[c] = gb * lt_exp(av + w[c] + Bt[q] - lz);
+      }
+      store_unit<BF16>(dWu + (long long)u * 16, v);
+    }
+  }
+  for (int i = tid; i < ntail; i += nthr) {
+    const int e = i < h0 ? i : i + nunits * VE;
+    stw<BF16>(m.dW, base + e, den_el(e, ldw<BF16>(m.W + base * ES, e)));
+  }
+  // the chain heads rewrite their elements once every store of the frame
+  // has completed (same workgroup, same address, in order)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int k = tid; k < NK; k += nthr) {
+    const int o = aoff[k];
+    if (o < 0 || !(alink[k] >> 30)) continue;
+    const float wv = ldw<BF16>(m.W + base * ES, o);
+    float sacc = 0.f;
+    for (int kk = k; kk >= 0; kk = (alink[kk] & 0x3fffffff) - 1) {
+      const int u = kk >> 1;
+      const float bn = BN[(kk & 1) ? u + 1 : u];
+      sacc += lt_exp(AN[u] + wv + bn - nm);
+    }
+    stw<BF16>(m.dW, base + o, den_el(o, wv) - gb * sacc);
+  }
+  (void)V;
+}
+
+// The marginal role of tri_mix_kernel (blocks [2B, grid)).
+template <bool BF16>
+LT_DEVINL void mix_marg(const MixArgs& m, unsigned char* lds) {
+  const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63;
+  const int B = m.B, C = m.g.C, NP = m.U + 1, NK = 2 * NP;
+  // LDS carve (this workgroup's own: the recursions' layout does not apply)
+  float* A = (float*)lds;
+  float* Bt = A + C;
+  float* AN = Bt + C;
+  float* BN = AN + NP;
+  int* aoff = (int*)(BN + NP + 1);
+  int* alink = aoff + NK;
+  int* ctx = alink + NK;
+  int* ylab = ctx + NP + 1;
+  int* nbt = ylab + NP + 1;
+  int* list = nbt + C;     // [B] the utterances this XCD's marginal workgroups take
+  int* sh = list + B;      // [0] list length, [1] job, [2] abort, [3] cur utterance
+  float* shf = (float*)(sh + 4);  // [0] log Z, [1] num of the cur utterance
+  const unsigned own = xcc_id() + 1;
+  for (int p = tid; p < C; p += nthr) {
+    bool z;
+    nbt[p] = next_base(m.g, p, &z);
+  }
+  if (tid == 0) {
+    // the recursion workgroups' XCD ids (each writes its own at its start)
+    int n = 0, abort = 0;
+    for (int b = 0; b < B && !abort; ++b) {
+      unsigned xf = 0, xb = 0;
+      for (unsigned spins = 0; (xf == 0 || xb == 0) && spins < kMixSpins; ++spins) {
+        xf = ld_u32_sc1(m.xcc + b);
+        xb = ld_u32_sc1(m.xcc + B + b);
+        if (xf == 0 || xb == 0) __builtin_amdgcn_s_sleep(8);
+      }
+      if (xf == 0 || xb == 0) abort = 1;
+      int nf = m.nfr[b];
+      nf = nf < 0 ? 0 : (nf > m.T ? m.T : nf);
+      if (xf == own && xb == own && nf >= 2) list[n++] = b;
+    }
+    sh[0] = abort ? 0 : n;
+    sh[2] = 0;
+    sh[3] = -1;
+  }
+  __syncthreads();
+  const int n = sh[0];
+  if (n == 0) return;
+  const int smax = (m.T + 1) / 2;
+  unsigned* ctr = m.ctr + 32 * ((own - 1) & 7);  // this XCD's job counter (its own 128-byte line)
+  for (;;) {
+    if (tid == 0) {
+      // the next job of this XCD: step s outwards from the middle, utterance
+      // list[k], the frame after (side 0) or before (side 1) the middle
+      int j = 0, b = 0, t = -1, nf = 0, mid = 0;
+      for (;;) {
+        j = (int)atomicAdd(ctr, 1u);
+        const int s = j / (2 * n), r = j - s * 2 * n;
+        if (s >= smax) { t = -1; break; }
+        b = list[r >> 1];
+        nf = m.nfr[b];
+        nf = nf < 0 ? 0 : (nf > m.T ? m.T : nf);
+        mid = nf / 2;
+        t = (r & 1) ? mid - 1 - s : mid + s;
+        if (t >= 0 && t < nf) break;
+      }
+      sh[1] = t < 0 ? -1 : (b << 16 | t);
+      if (t >= 0) {
+        // frame t needs alpha row t and beta row t (beta_{t+1}); the middle
+        // norm needs alpha row mid and beta row mid - 1
+        const unsigned need_f = (unsigned)max(t + 1, mid + 1);
+        const unsigned need_b = (unsigned)max(nf - 1 - t, nf - mid);
+        unsigned spins = 0;
+        while ((ld_u32_sc1(m.prog + 2 * b) < need_f || ld_u32_sc1(m.prog + 2 * b + 1) < need_b) &&
+               ++spins < kMixSpins)
+          __builtin_amdgcn_s_sleep(8);
+        if (spins >= kMixSpins) sh[1] = -1;  // a recursion that never came: marg_kernel takes it
+      }
+    }
+    __syncthreads();
+    const int job = sh[1];
+    if (job < 0) return;
+    const int b = job >> 16, t = job & 0xffff;
+    if (b != sh[3]) {
+      // this utterance's string arc table (marg_kernel's, write_arc_table)
+      // and its middle norm, once per utterance
+      __syncthreads();
+      for (int u = tid; u < m.U; u += nthr) ylab[u] = m.labels[(long long)b * m.U + u];
+      __syncthreads();
+      if (tid == 0) {  // walk_states over the label string (contexts.py:109-146)
+        const int Rr = m.g.V + 1;
+        int c = 0;
+        for (int u = 0; u <= m.U; ++u) {
+          ctx[u] = c * Rr;
+          if (u < m.U) {
+            int y = ylab[u];
+            if (y < 0 || y > m.g.V) y = 0;
+            ylab[u] = y < 1 ? 1 : y;
+            if (y != 0) {
+              bool z;
+              const int nb = next_base(m.g, c, &z);
+              c = z ? 0 : nb + y;
+            }
+          } else {
+            ylab[u] = 1;
+          }
+        }
+      }
+      __syncthreads();
+      auto arc = [&](int k) {
+        const int u = k >> 1;
+        return (k & 1) == 0 ? ctx[u] : (u < m.U ? ctx[u] + ylab[u] : -1);
+      };
+      for (int k = tid; k < NK; k += nthr) {
+        const int o = arc(k);
+        int head = o >= 0 ? 1 : 0, nxt = -1;
+        if (o >= 0)
+          for (int k2 = 0; k2 < NK; ++k2) {
+            if (arc(k2) != o) continue;
+            if (k2 < k) head = 0;
+            else if (k2 > k && nxt < 0) nxt = k2;
+          }
+        aoff[k] = o;
+        alink[k] = (head << 30) | (nxt + 1);
+      }
+      if (tid < 64) {
+        int nf = m.nfr[b];
+        nf = nf < 0 ? 0 : (nf > m.T ? m.T : nf);
+        const int mid = nf / 2;
+        const long long r0 = (long long)b * m.T;
+        const float2 zn = tri_mid_norm(m.alpha + (r0 + mid) * C, m.beta + (r0 + mid - 1) * C,
+                                       m.alpha_num + (r0 + mid) * NP,
+                                       m.beta_num + (r0 + mid - 1) * NP, C, NP, lane, true);
+        if (lane == 0) {
+          shf[0] = zn.x;
+          shf[1] = zn.y;
+          sh[3] = b;
+        }
+      }
+      __syncthreads();
+    }
+    const float lz = shf[0], nm = shf[1];
+    if (__builtin_isfinite(lz) && __builtin_isfinite(nm)) {
+      mix_stage_rows<BF16>(m, b, t, A, Bt, AN, BN, tid, nthr);
+      __syncthreads();
+      mix_frame<BF16>(m, b, t, lz, nm, A, Bt, AN, BN, aoff, alink, nbt, tid, nthr);
+      if (tid == 0) m.done[(long long)b * m.T + t] = 1;
+    }
+    // (a frame whose norm is not finite -- an unreachable string, a dead
+    // lattice -- stays with marg_kernel, which zeroes it)
+    __syncthreads();
+  }
+}
+
+// The recursions and the marginal workgroups in one launch: blocks [0, nb)
+// forward, [nb, 2 nb) checkpointing backward (each publishing its XCD id and
+// its progress), [2 nb, grid) marginals.
+template <bool BF16>
+__global__ __launch_bounds__(1024) void tri_mix_kernel(const KArgs af, const KArgs ab, int nb,
+                                                       const MixArgs mx) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int x = blockIdx.x;
+  if (x < 2 * nb) {
+    if (threadIdx.x == 0)
+      __hip_atomic_store(mx.xcc + x, xcc_id() + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (x < nb) fwd_body<M_LOG, BF16, true, 2, 9, 32>(af, x);
+    else bwd_body<BF16, true, false, 2, 9, true, (int)sizeof(KArgs), 32>(ab, x - nb);
+    return;
+  }
+  mix_marg<BF16>(mx, lds);
 }
 }  // namespace
 
@@ -35,6 +335,33 @@ int launch_tri_fwdbwd(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStre
   KArgs af = pf.a, ab = pb.a;
   void* args[] = {(void*)&af, (void*)&ab, (void*)&nb};
   e = hipLaunchKernel(k, dim3(2 * nb), dim3(pf.threads), args, lds, st);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
+  return LT_OK;
+}
+
+// LDS bytes of the marginal role (mix_marg's carve)
+int tri_mix_lds(const NGram& g, int U, int B) {
+  const int NP = U + 1, NK = 2 * NP;
+  return 4 * (2 * g.C + 2 * NP + 1 + 2 * NK + 2 * (NP + 1) + g.C + B + 4 + 2) + 16;
+}
+
+int launch_tri_mix(const Plan& pf, const Plan& pb, bool bf16, int nb, int marg_blocks,
+                   const MixArgs& mx, hipStream_t st) {
+  if (nb == 0) return LT_OK;
+  if (!mx.W || !mx.nfr || !mx.alpha || !mx.beta || !mx.alpha_num || !mx.beta_num || !mx.dW ||
+      !mx.prog || !mx.xcc || !mx.ctr || !mx.done || (mx.U > 0 && !mx.labels) ||
+      pf.a.prog != mx.prog || pb.a.prog != mx.prog || mx.g.V != 32 || mx.g.n != 2 || mx.B != nb)
+    return set_error(LT_EINVAL, "trigram overlap: incomplete arguments");
+  const void* k = bf16 ? (const void*)tri_mix_kernel<true> : (const void*)tri_mix_kernel<false>;
+  int lds = pf.lds_bytes > pb.lds_bytes ? pf.lds_bytes : pb.lds_bytes;
+  lds = std::max(lds, tri_mix_lds(mx.g, mx.U, mx.B));
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
+  KArgs af = pf.a, ab = pb.a;
+  MixArgs m = mx;
+  void* args[] = {(void*)&af, (void*)&ab, (void*)&nb, (void*)&m};
+  e = hipLaunchKernel(k, dim3(2 * nb + marg_blocks), dim3(pf.threads), args, lds, st);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
   return LT_OK;

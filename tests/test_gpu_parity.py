@@ -268,6 +268,36 @@ def test_trigram_v32_short_and_empty_utterances(cuda):
                              rnum, True)
 
 
+@pytest.mark.parametrize('dt', ['bf16', 'f32'])
+def test_trigram_overlap_loss_grad_vs_oracle(cuda, dt):
+  """lt_loss_grad's trigram V = 32 route (lt_tri.hip, tri_mix_kernel): the
+  recursions with marginal workgroups on the CUs they leave idle, each taking
+  frames as both recursions pass them, then marg_kernel on the frames they
+  did not take. B = 8 (the route needs a multiple of 8), T = 160 (progress
+  published every 64 frames), lengths 0, 1, 2, 3, T - 1 and T, epsilon labels,
+  an unreachable string: loss and every dW element against the oracle, and a
+  second call bit-identical (which kernel takes a frame does not change it)."""
+  orc = _orc()
+  B, T, U, V, n = 8, 160, 12, 32, 2
+  W, _, lab, _ = _random_problem(B, T, U, V, n, seed=777)
+  nf = np.array([T, 0, 1, 2, T - 1, 150, 3, T], dtype=np.int32)
+  nl = np.array([U, 0, 1, 2, U - 1, U, 5, U], dtype=np.int32)  # utterance 6 unreachable
+  bf16 = dt == 'bf16'
+  if bf16:
+    W = torch.tensor(W).bfloat16().float().numpy()
+  Wd = torch.tensor(W).to(torch.bfloat16 if bf16 else torch.float32).to(cuda)
+  nfd, labd, nld = (torch.tensor(x).to(cuda) for x in (nf, lab, nl))
+  assert nat.loss_grad_design(B, T, U, V, n) == nat.DESIGN_CHECKPOINTS
+  loss, lz, num, dW = nat.loss_grad(Wd, nfd, labd, nld, V, n, False)
+  loss2, _, _, dW2 = nat.loss_grad(Wd, nfd, labd, nld, V, n, False)
+  torch.cuda.synchronize()
+  assert torch.equal(loss, loss2) and torch.equal(dW, dW2)
+  rl, rlz, rnum, rdW = orc.loss_grad(W, nf, lab, nl, V, n)
+  assert_loss_close(loss.cpu().numpy(), rl)
+  assert_grad_marginal_close(dW.float().cpu().numpy(), rdW, orc.den_grad(W, nf, V, n)[1], rlz,
+                             rnum, bf16)
+
+
 @pytest.mark.parametrize('B,T,U,V,n,dt', RANDOM)
 def test_random_vs_oracle(cuda, B, T, U, V, n, dt):
   orc = _orc()

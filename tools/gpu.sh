@@ -52,7 +52,7 @@ for step in "$@"; do
         > $out/smoke.log 2>&1 || exit $?
       ;;
     full) t_run full.log 500 tests/test_gpu_full_size.py -v ;;
-    k=*) t_run k_${step#k=}.log 500 tests -m gpu -v -k "${step#k=}" ;;
+    k=*) t_run k_$(echo "${step#k=}" | tr -c 'A-Za-z0-9_\n' _).log 500 tests -m gpu -v -k "${step#k=}" ;;
     bench)
       timeout -k 10 400 python -u bench.py --warmup 5 --steps 20 > $out/bench_driver_flags.json \
         2> $out/bench_driver_flags.err || exit $?
