@@ -105,7 +105,7 @@ constexpr unsigned kSpinMax = 1u << 20;
 #endif
 constexpr bool kNoAcq = LT_CK_NOACQ != 0;
 #ifndef LT_CK_ALDS
-#define LT_CK_ALDS 0
+#define LT_CK_ALDS 1
 #endif
 constexpr bool kALds = LT_CK_ALDS != 0;  // phase A: frames through an LDS ring (two slots a wave)
 constexpr int kASlot = 5 * 1024;         // bytes per slot (a fp32 bigram frame: 5 DMA instructions)

@@ -1051,7 +1051,10 @@ LT_DEVINL void store_unit(unsigned char* p, const float* v) {
 // roles) drain their stores before the frame's barrier, and thread 0
 // publishes the count after it (an sc1 store; the marginal workgroups on the
 // same XCD poll it with sc1 loads and read the rows with sc1 loads)
-constexpr int kTriPub = 64;
+#ifndef LT_TRI_PUB
+#define LT_TRI_PUB 64
+#endif
+constexpr int kTriPub = LT_TRI_PUB;
 LT_DEVINL bool tri_pub_frame(const KArgs& a, int i) { return a.prog && i > 0 && i % kTriPub == 0; }
 LT_DEVINL void tri_pub_drain(const KArgs& a, int i) {
   if (tri_pub_frame(a, i)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2057,6 +2060,11 @@ struct MixArgs {
   unsigned* ctr;      // [8 * 32] per-XCD job counters, one 128-byte line each
   int* done;          // [B*T] frame done here (marg_kernel skips it)
   int B, T, U;
+  int lds_bytes;      // the launch's dynamic LDS (the marginal waves' row regions)
+  int dbg;            // diagnostic builds (LT_TRI_MIX_DBG): 1 the marginal role does nothing,
+                      // 2 it waits for whole recursions, 4 it leaves every frame to marg_kernel,
+                      // 8 done = XCD id + 1, 16 done = completion time and ts the recursions' times
+  unsigned* ts;       // [4B] diagnostic (dbg 16): recursion start, end (s_memrealtime low bits)
   NGram g;
 };
 
@@ -2065,23 +2073,36 @@ struct MixArgs {
 // (any frame gives both: every path crosses it). One wave, a fixed lane order
 // and butterfly, so the trigram overlap's marginal role and marg_kernel get
 // the same bits; sc1: rows another workgroup of the same launch published.
+template <int NQ>  // values per lane: n <= 64 NQ
+LT_DEVINL float mid_lse(const float* x, const float* y, int n, int lane, bool sc1) {
+  float v[NQ];
+  // every load in flight before the first use: sc1 (L1-bypassing) buffer
+  // loads for rows another workgroup of the same launch wrote
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 4 * n, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, 4 * n, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = min(lane + 64 * i, n - 1);
+    const float a = sc1 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, 4 * q, 0, 0x10)) : x[q];
+    const float b = sc1 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, 4 * q, 0, 0x10)) : y[q];
+    v[i] = lane + 64 * i < n ? a + b : -kInf;
+  }
+  float mx = -kInf;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) mx = fmaxf(mx, v[i]);
+  mx = gmax<6>(mx, 6);
+  const float c = __builtin_isfinite(mx) ? mx : 0.f;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) s += lt_exp(v[i] - c);
+  s = gsum<6>(s, 6);
+  return c + lt_log(s);
+}
 LT_DEVINL float2 tri_mid_norm(const float* ar, const float* br, const float* anr,
                               const float* bnr, int C, int NP, int lane, bool sc1) {
-  auto ld = [&](const float* p) -> float {
-    return sc1 ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
-  };
-  auto lse = [&](const float* x, const float* y, int n) {
-    float mx = -kInf;
-    for (int q = lane; q < n; q += 64) mx = fmaxf(mx, ld(x + q) + ld(y + q));
-    mx = gmax<6>(mx, 6);
-    const float c = __builtin_isfinite(mx) ? mx : 0.f;
-    float s = 0.f;
-    for (int q = lane; q < n; q += 64) s += lt_exp(ld(x + q) + ld(y + q) - c);
-    s = gsum<6>(s, 6);
-    return c + lt_log(s);
-  };
-  const float lz = lse(ar, br, C);
-  const float nm = lse(anr, bnr, NP);
+  // C = 1057 (the V = 32 trigram), NP <= 128 (the overlap's shapes)
+  const float lz = mid_lse<17>(ar, br, C, lane, sc1);
+  const float nm = mid_lse<2>(anr, bnr, NP, lane, sc1);
   return make_float2(lz, nm);
 }
 

@@ -467,10 +467,33 @@ LT_DEVINL void marg_tile(const MgArgs& a, const int job, unsigned char* lds) {
   }
 }
 
+constexpr int kMgScan = 16;  // frames per cleanup workgroup after the trigram overlap
+
 template <bool BF16, bool SLICED>
 __global__ __launch_bounds__(256) void marg_kernel(const MgArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   int job = (int)blockIdx.x;
+  if (SLICED && a.done) {
+    // after the trigram overlap: each workgroup scans kMgScan frames' done
+    // flags in one load and takes the slices of the frames left (usually
+    // none: one short workgroup per kMgScan frames instead of one per slice)
+    __shared__ int s_list[kMgScan], s_n;
+    const long long nfr = (long long)a.B * a.T;
+    const long long f0 = (long long)blockIdx.x * kMgScan;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    if (threadIdx.x < kMgScan && f0 + threadIdx.x < nfr && !a.done[f0 + threadIdx.x])
+      s_list[atomicAdd(&s_n, 1)] = (int)threadIdx.x;
+    __syncthreads();
+    const int cnt = s_n;
+    for (int i = 0; i < cnt * a.tpf; ++i) {
+      const long long f = f0 + s_list[i / a.tpf];
+      const int b = (int)(f / a.T), t = (int)(f - (long long)b * a.T);
+      marg_tile<BF16, SLICED>(a, b * a.tiles + t * a.tpf + i % a.tpf, lds);
+      __syncthreads();  // the tile's LDS before the next tile's
+    }
+    return;
+  }
   if (SLICED && LT_MARG_OPTS && a.xcd) {
     // blocks 8 g tpf + 8 s + x take slice s of frame 8 g + x: a frame's
     // slices 8 block ids apart, so under round-robin dispatch they share one
@@ -921,7 +944,8 @@ GradWs grad_ws(const lt_problem* pb, int local_norm) {
   w.arcs = o; o += up(4 * B * 4 * NP);
   w.side = o; o += up((long long)side_bytes(pb));
   // the trigram overlap: progress words, XCD ids, per-XCD job counters, done flags
-  w.mix = o; o += g.n == 2 ? up(4 * (4 * B + 8 * 32 + B * T)) : 0;
+  // (and the diagnostic time stamps)
+  w.mix = o; o += g.n == 2 ? up(4 * (8 * B + 8 * 32 + B * T)) : 0;
   w.total = o;
   return w;
 }
@@ -1252,6 +1276,7 @@ int lt_loss_backward(const lt_problem* pb, int32_t local_norm, const void* W,
     m.done = t_mix_done;  // the trigram overlap's frames (lt_loss_grad only)
     m.mid_norm = t_mix_done != nullptr;
     if (grid == 0) return LT_OK;
+    if (m.done && m.tpf > 1) grid = ceil_div((long long)pb->batch * pb->max_frames, kMgScan);
     hipStream_t st = (hipStream_t)stream;
     const bool bf = pb->weight_dtype == LT_DTYPE_BF16, sliced = m.tpf > 1;
     const void* k = bf ? (sliced ? (const void*)marg_kernel<true, true>
@@ -1513,8 +1538,12 @@ int lt_loss_grad_ex(const lt_problem* pb, int32_t local_norm, int32_t design_in,
       req.m.ctr = mw + 4 * B;
       req.m.done = (int*)(mw + 4 * B + 8 * 32);
       req.m.dW = dW;
-      req.blocks = cus - 2 * pb->batch;
-      if ((rc = hip_check(hipMemsetAsync(mw, 0, 4 * (size_t)(4 * B + 8 * 32 + B * pb->max_frames),
+      req.m.dbg = lt_impl::tune_int("LT_TRI_MIX_DBG", 0);
+      req.m.ts = (unsigned*)(req.m.done + B * pb->max_frames);
+      // marginal workgroups for the idle CUs (LT_TRI_MIX_EXTRA more, queued
+      // for the recursions' CUs: measured 3.35 against 3.27 ms at cfg5 with 2B)
+      req.blocks = cus - 2 * pb->batch + lt_impl::tune_int("LT_TRI_MIX_EXTRA", 0);
+      if ((rc = hip_check(hipMemsetAsync(mw, 0, 4 * (size_t)(8 * B + 8 * 32 + B * pb->max_frames),
                                          (hipStream_t)stream),
                           "overlap memset")))
         return rc;

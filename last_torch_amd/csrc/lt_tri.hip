@@ -44,45 +44,61 @@ LT_DEVINL unsigned xcc_id() {
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
   return v;
 }
+// diagnostic time stamps: the low 30 bits of the 100 MHz real-time counter
+LT_DEVINL unsigned mix_rt() { return (unsigned)__builtin_amdgcn_s_memrealtime() & 0x3fffffffu; }
 LT_DEVINL unsigned ld_u32_sc1(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 LT_DEVINL float ld_f32_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// n <= 64 NQ floats of a row into LDS: NQ sc1 buffer loads per lane issued
+// together (a relaxed atomic load per element waits one latency each)
+template <int NQ>
+LT_DEVINL void row_sc1(const float* src, int n, float* dst, int lane) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 4 * n, 0x00020000);
+  float v[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i)
+    v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * (lane + 64 * i), 0, 0x10));
+#pragma unroll
+  for (int i = 0; i < NQ; ++i)
+    if (lane + 64 * i < n) dst[lane + 64 * i] = v[i];
+}
 constexpr unsigned kMixSpins = 1u << 22;  // ~1 s of polling, then the frames go back to marg_kernel
 constexpr int kMixUnits = 5;              // 16-byte units of W in flight per thread
+constexpr int kMixUtt = 8;                // utterances a marginal workgroup keeps arc tables for
 
 }  // namespace
 
 namespace {
 
+// One frame's marginals by ONE wave (every wave of a marginal workgroup takes
+// frames on its own: no workgroup barrier, so one wave's memory latency
+// hides behind the others): the frame's rows into the wave's LDS region, den
+// elements with marg_tile's expressions stored by 16-byte units, then the
+// string's chain heads rewrite their elements as den - num once the wave's
+// own stores of the frame have completed (marg_tile's phase 2).
 template <bool BF16>
-LT_DEVINL void mix_stage_rows(const MixArgs& m, int b, int t, float* A, float* Bt, float* AN,
-                              float* BN, int tid, int nthr) {
-  const int C = m.g.C, NP = m.U + 1;
-  const long long rc = ((long long)b * m.T + t) * C, rn = ((long long)b * m.T + t) * NP;
-  for (int e = tid; e < C; e += nthr) {
-    A[e] = ld_f32_sc1(m.alpha + rc + e);
-    Bt[e] = ld_f32_sc1(m.beta + rc + e);
-  }
-  for (int e = tid; e < NP; e += nthr) {
-    AN[e] = ld_f32_sc1(m.alpha_num + rn + e);
-    BN[e] = ld_f32_sc1(m.beta_num + rn + e);
-  }
-}
-
-// One frame's marginals, the whole workgroup: den elements straight from the
-// staged rows (marg_tile's expressions), stored by 16-byte units; then the
-// string's chain heads rewrite their elements as den - num (marg_tile's
-// phase 2).
-template <bool BF16>
-LT_DEVINL void mix_frame(const MixArgs& m, int b, int t, float lz, float nm, const float* A,
-                         const float* Bt, const float* AN, const float* BN, const int* aoff,
-                         const int* alink, const int* nbt, int tid, int nthr) {
+LT_DEVINL void mix_frame(const MixArgs& m, int b, int t, float lz, float nm, float* A, float* Bt,
+                         float* AN, float* BN, const int* aoff, const int* alink, const int* nbt,
+                         int lane) {
   constexpr int VE = BF16 ? 8 : 4, ES = BF16 ? 2 : 4;
-  constexpr int V = 32, R = 33, C = 1 + 32 + 32 * 32, FR = C * R;
+  constexpr int R = 33, C = 1 + 32 + 32 * 32, FR = C * R;
   const int NP = m.U + 1, NK = 2 * NP;
+  {
+    // the four rows by sc1 buffer loads (L1 bypassed: another workgroup of
+    // this launch wrote them), every load in flight before the first LDS write
+    const long long rc = ((long long)b * m.T + t) * C, rn = ((long long)b * m.T + t) * NP;
+    row_sc1<17>(m.alpha + rc, C, A, lane);
+    row_sc1<17>(m.beta + rc, C, Bt, lane);
+    row_sc1<2>(m.alpha_num + rn, NP, AN, lane);
+    row_sc1<2>(m.beta_num + rn, NP, BN, lane);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's row writes, before any lane reads them
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (m.dbg & 64) return;  // diagnostic: the rows only
   const float gb = m.grad ? m.grad[b] : 1.f;
   const long long base = ((long long)b * m.T + t) * FR;
   const int h0 = (int)(((16 - ((base * ES) & 15)) & 15) / ES);
@@ -95,21 +111,27 @@ LT_DEVINL void mix_frame(const MixArgs& m, int b, int t, float lz, float nm, con
     const int q = y == 0 ? p : nbt[p] + y;
     return gb * lt_exp(A[p] + w + Bt[q] - lz);
   };
-  for (int u0 = tid; u0 < nunits; u0 += kMixUnits * nthr) {
+  for (int u0 = lane; u0 < nunits; u0 += kMixUnits * 64) {
     uint4 wq[kMixUnits];
 #pragma unroll
     for (int r = 0; r < kMixUnits; ++r) {
-      const int u = u0 + r * nthr;
-      if (u < nunits) wq[r] = *(const uint4*)(Wu + (long long)u * 16);
+      const int u = min(u0 + r * 64, nunits - 1);  // every load issued (clamped): one wait
+      if (m.dbg & 256) wq[r] = make_uint4(u, u, u, u);  // diagnostic: no W loads
+      else if (m.dbg & 1024) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v4u q = __builtin_nontemporal_load((const v4u*)(Wu + (long long)u * 16));
+        wq[r] = make_uint4(q.x, q.y, q.z, q.w);
+      }
+      else wq[r] = *(const uint4*)(Wu + (long long)u * 16);
     }
 #pragma unroll
     for (int r = 0; r < kMixUnits; ++r) {
-      const int u = u0 + r * nthr;
+      const int u = u0 + r * 64;
       if (u >= nunits) break;
       float w[VE], v[VE];
       unpack_unit<BF16>(wq[r], w);
       const int e0 = h0 + u * VE;
-      int p = e0 / R;
+      const int p = e0 / R;
       const int y = e0 - p * R;
       // a unit spans at most two source rows (R >= VE)
       const int p1 = min(p + 1, C - 1);
@@ -125,18 +147,27 @@ LT_DEVINL void mix_frame(const MixArgs& m, int b, int t, float lz, float nm, con
         const float av = w2 ? a1v : a0v;
         v[c] = gb * lt_exp(av + w[c] + Bt[q] - lz);
       }
-      store_unit<BF16>(dWu + (long long)u * 16, v);
+      if (m.dbg & 128) {  // diagnostic: no dW stores (one conditional store keeps the math)
+        if (v[0] == 12345.f) store_unit<BF16>(dWu + (long long)u * 16, v);
+      } else if (BF16 && (m.dbg & 512)) {  // diagnostic: plain (temporal) stores
+        unsigned q[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          q[i] = f2bf(v[(2 * i) % VE]) | ((unsigned)f2bf(v[(2 * i + 1) % VE]) << 16);
+        *(uint4*)(dWu + (long long)u * 16) = make_uint4(q[0], q[1], q[2], q[3]);
+      } else {
+        store_unit<BF16>(dWu + (long long)u * 16, v);
+      }
     }
   }
-  for (int i = tid; i < ntail; i += nthr) {
+  for (int i = lane; i < ntail; i += 64) {
     const int e = i < h0 ? i : i + nunits * VE;
     stw<BF16>(m.dW, base + e, den_el(e, ldw<BF16>(m.W + base * ES, e)));
   }
-  // the chain heads rewrite their elements once every store of the frame
-  // has completed (same workgroup, same address, in order)
+  // the chain heads rewrite their elements once the wave's stores of the
+  // frame have completed (same wave, same address)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int k = tid; k < NK; k += nthr) {
+  for (int k = lane; k < NK; k += 64) {
     const int o = aoff[k];
     if (o < 0 || !(alink[k] >> 30)) continue;
     const float wv = ldw<BF16>(m.W + base * ES, o);
@@ -148,32 +179,41 @@ LT_DEVINL void mix_frame(const MixArgs& m, int b, int t, float lz, float nm, con
     }
     stw<BF16>(m.dW, base + o, den_el(o, wv) - gb * sacc);
   }
-  (void)V;
 }
 
-// The marginal role of tri_mix_kernel (blocks [2B, grid)).
+__host__ __device__ inline int al16i(int x) { return (x + 15) & ~15; }
+// the marginal role's shared LDS (the utterances' tables) and one wave's rows
+__host__ __device__ inline int mix_shared_bytes(int C, int NP, int B) {
+  return al16i(4 * (C + kMixUtt * 4 * NP + 2 * (NP + 1) + B + 4 + 2 * kMixUtt));
+}
+__host__ __device__ inline int mix_row_bytes(int C, int NP) { return al16i(4 * (2 * C + 2 * NP)); }
+
+// The marginal role of tri_mix_kernel (blocks [2B, grid)): the workgroup
+// builds the tables of the utterances on its XCD, then every wave takes
+// frames through the XCD's job counter on its own.
 template <bool BF16>
-LT_DEVINL void mix_marg(const MixArgs& m, unsigned char* lds) {
+LT_DEVINL void mix_marg(const MixArgs& m, unsigned char* lds, int lds_bytes) {
   const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int B = m.B, C = m.g.C, NP = m.U + 1, NK = 2 * NP;
-  // LDS carve (this workgroup's own: the recursions' layout does not apply)
-  float* A = (float*)lds;
-  float* Bt = A + C;
-  float* AN = Bt + C;
-  float* BN = AN + NP;
-  int* aoff = (int*)(BN + NP + 1);
-  int* alink = aoff + NK;
-  int* ctx = alink + NK;
-  int* ylab = ctx + NP + 1;
-  int* nbt = ylab + NP + 1;
-  int* list = nbt + C;     // [B] the utterances this XCD's marginal workgroups take
-  int* sh = list + B;      // [0] list length, [1] job, [2] abort, [3] cur utterance
-  float* shf = (float*)(sh + 4);  // [0] log Z, [1] num of the cur utterance
+  int* nbt = (int*)lds;                  // [C] next_base of each state
+  int* tabs = nbt + C;                   // [kMixUtt][2 NK] arc tables (offsets, links) by list slot
+  int* ctx = tabs + kMixUtt * 2 * NK;    // [NP + 1]
+  int* ylab = ctx + NP + 1;              // [NP + 1]
+  int* list = ylab + NP + 1;             // [B] the utterances this XCD's marginal workgroups take
+  int* sh = list + B;                    // [0] list length
+  float* shf = (float*)(sh + 4);         // [2 kMixUtt] log Z, num by list slot (NaN: not yet)
+  const int shared = mix_shared_bytes(C, NP, B), rowb = mix_row_bytes(C, NP);
+  int nwork = min(nthr >> 6, (lds_bytes - shared) / rowb);
+  if (m.dbg & 2048) nwork = min(nwork, 8);  // diagnostic: fewer marginal waves
+  if (m.dbg & 4096) nwork = min(nwork, 4);
+  if (m.dbg & 1) return;
   const unsigned own = xcc_id() + 1;
   for (int p = tid; p < C; p += nthr) {
     bool z;
     nbt[p] = next_base(m.g, p, &z);
   }
+  for (int i = tid; i < 2 * kMixUtt; i += nthr) shf[i] = __builtin_nanf("");
   if (tid == 0) {
     // the recursion workgroups' XCD ids (each writes its own at its start)
     int n = 0, abort = 0;
@@ -187,118 +227,132 @@ LT_DEVINL void mix_marg(const MixArgs& m, unsigned char* lds) {
       if (xf == 0 || xb == 0) abort = 1;
       int nf = m.nfr[b];
       nf = nf < 0 ? 0 : (nf > m.T ? m.T : nf);
-      if (xf == own && xb == own && nf >= 2) list[n++] = b;
+      if (xf == own && xb == own && nf >= 2 && n < kMixUtt) list[n++] = b;
     }
-    sh[0] = abort ? 0 : n;
-    sh[2] = 0;
-    sh[3] = -1;
+    sh[0] = abort ? 0 : n;  // (past kMixUtt on one XCD: marg_kernel takes the rest)
   }
   __syncthreads();
   const int n = sh[0];
-  if (n == 0) return;
+  if (n == 0 || nwork < 1) return;
+  // every listed utterance's string arc table (marg_kernel's,
+  // write_arc_table: contexts.py:109-146 walk, lattices.py:314-338 arcs)
+  for (int k2 = 0; k2 < n; ++k2) {
+    const int b = list[k2];
+    for (int u = tid; u < m.U; u += nthr) ylab[u] = m.labels[(long long)b * m.U + u];
+    __syncthreads();
+    if (tid == 0) {
+      const int Rr = m.g.V + 1;
+      int c = 0;
+      for (int u = 0; u <= m.U; ++u) {
+        ctx[u] = c * Rr;
+        if (u < m.U) {
+          int y = ylab[u];
+          if (y < 0 || y > m.g.V) y = 0;
+          ylab[u] = y < 1 ? 1 : y;
+          if (y != 0) {
+            bool z;
+            const int nb = next_base(m.g, c, &z);
+            c = z ? 0 : nb + y;
+          }
+        } else {
+          ylab[u] = 1;
+        }
+      }
+    }
+    __syncthreads();
+    auto arc = [&](int k) {
+      const int u = k >> 1;
+      return (k & 1) == 0 ? ctx[u] : (u < m.U ? ctx[u] + ylab[u] : -1);
+    };
+    int* aoff = tabs + k2 * 2 * NK;
+    int* alink = aoff + NK;
+    for (int k = tid; k < NK; k += nthr) {
+      const int o = arc(k);
+      int head = o >= 0 ? 1 : 0, nxt = -1;
+      if (o >= 0)
+        for (int kk = 0; kk < NK; ++kk) {
+          if (arc(kk) != o) continue;
+          if (kk < k) head = 0;
+          else if (kk > k && nxt < 0) nxt = kk;
+        }
+      aoff[k] = o;
+      alink[k] = (head << 30) | (nxt + 1);
+    }
+    __syncthreads();
+  }
+  if (wave >= nwork) return;
+  float* A = (float*)(lds + shared + wave * rowb);
+  float* Bt = A + C;
+  float* AN = Bt + C;
+  float* BN = AN + NP;
   const int smax = (m.T + 1) / 2;
   unsigned* ctr = m.ctr + 32 * ((own - 1) & 7);  // this XCD's job counter (its own 128-byte line)
   for (;;) {
-    if (tid == 0) {
+    int job = -1;
+    if (lane == 0) {
       // the next job of this XCD: step s outwards from the middle, utterance
-      // list[k], the frame after (side 0) or before (side 1) the middle
-      int j = 0, b = 0, t = -1, nf = 0, mid = 0;
+      // list[slot], the frame after (side 0) or before (side 1) the middle
+      int j = 0, b = 0, t = -1, nf = 0, mid = 0, slot = 0;
       for (;;) {
         j = (int)atomicAdd(ctr, 1u);
         const int s = j / (2 * n), r = j - s * 2 * n;
         if (s >= smax) { t = -1; break; }
-        b = list[r >> 1];
+        slot = r >> 1;
+        b = list[slot];
         nf = m.nfr[b];
         nf = nf < 0 ? 0 : (nf > m.T ? m.T : nf);
         mid = nf / 2;
         t = (r & 1) ? mid - 1 - s : mid + s;
         if (t >= 0 && t < nf) break;
       }
-      sh[1] = t < 0 ? -1 : (b << 16 | t);
       if (t >= 0) {
         // frame t needs alpha row t and beta row t (beta_{t+1}); the middle
-        // norm needs alpha row mid and beta row mid - 1
-        const unsigned need_f = (unsigned)max(t + 1, mid + 1);
-        const unsigned need_b = (unsigned)max(nf - 1 - t, nf - mid);
+        // norm alpha row mid and beta row mid - 1
+        unsigned need_f = (unsigned)max(t + 1, mid + 1);
+        unsigned need_b = (unsigned)max(nf - 1 - t, nf - mid);
+        if (m.dbg & 2) need_f = need_b = (unsigned)nf;  // diagnostic: wait for the whole recursions
         unsigned spins = 0;
         while ((ld_u32_sc1(m.prog + 2 * b) < need_f || ld_u32_sc1(m.prog + 2 * b + 1) < need_b) &&
-               ++spins < kMixSpins)
-          __builtin_amdgcn_s_sleep(8);
-        if (spins >= kMixSpins) sh[1] = -1;  // a recursion that never came: marg_kernel takes it
+               ++spins < kMixSpins) {
+          if (m.dbg & 32) __builtin_amdgcn_s_sleep(127);
+          else __builtin_amdgcn_s_sleep(8);
+        }
+        // a recursion that never came: marg_kernel takes the frame
+        job = spins >= kMixSpins ? -1 : (slot << 26 | b << 16 | t);
       }
     }
-    __syncthreads();
-    const int job = sh[1];
+    job = __builtin_amdgcn_readfirstlane(job);
     if (job < 0) return;
-    const int b = job >> 16, t = job & 0xffff;
-    if (b != sh[3]) {
-      // this utterance's string arc table (marg_kernel's, write_arc_table)
-      // and its middle norm, once per utterance
-      __syncthreads();
-      for (int u = tid; u < m.U; u += nthr) ylab[u] = m.labels[(long long)b * m.U + u];
-      __syncthreads();
-      if (tid == 0) {  // walk_states over the label string (contexts.py:109-146)
-        const int Rr = m.g.V + 1;
-        int c = 0;
-        for (int u = 0; u <= m.U; ++u) {
-          ctx[u] = c * Rr;
-          if (u < m.U) {
-            int y = ylab[u];
-            if (y < 0 || y > m.g.V) y = 0;
-            ylab[u] = y < 1 ? 1 : y;
-            if (y != 0) {
-              bool z;
-              const int nb = next_base(m.g, c, &z);
-              c = z ? 0 : nb + y;
-            }
-          } else {
-            ylab[u] = 1;
-          }
-        }
+    const int slot = job >> 26, b = (job >> 16) & 1023, t = job & 0xffff;
+    float lz = shf[2 * slot], nm = shf[2 * slot + 1];
+    if (__builtin_isnan(lz)) {
+      // this utterance's middle norm (its rows are final: the job's wait
+      // covered them); another wave may compute the same bits beside it
+      int nf = m.nfr[b];
+      nf = nf < 0 ? 0 : (nf > m.T ? m.T : nf);
+      const int mid = nf / 2;
+      const long long r0 = (long long)b * m.T;
+      const float2 zn = tri_mid_norm(m.alpha + (r0 + mid) * C, m.beta + (r0 + mid - 1) * C,
+                                     m.alpha_num + (r0 + mid) * NP,
+                                     m.beta_num + (r0 + mid - 1) * NP, C, NP, lane, true);
+      lz = zn.x;
+      nm = zn.y;
+      if (lane == 0) {
+        shf[2 * slot] = lz;
+        shf[2 * slot + 1] = nm;
       }
-      __syncthreads();
-      auto arc = [&](int k) {
-        const int u = k >> 1;
-        return (k & 1) == 0 ? ctx[u] : (u < m.U ? ctx[u] + ylab[u] : -1);
-      };
-      for (int k = tid; k < NK; k += nthr) {
-        const int o = arc(k);
-        int head = o >= 0 ? 1 : 0, nxt = -1;
-        if (o >= 0)
-          for (int k2 = 0; k2 < NK; ++k2) {
-            if (arc(k2) != o) continue;
-            if (k2 < k) head = 0;
-            else if (k2 > k && nxt < 0) nxt = k2;
-          }
-        aoff[k] = o;
-        alink[k] = (head << 30) | (nxt + 1);
-      }
-      if (tid < 64) {
-        int nf = m.nfr[b];
-        nf = nf < 0 ? 0 : (nf > m.T ? m.T : nf);
-        const int mid = nf / 2;
-        const long long r0 = (long long)b * m.T;
-        const float2 zn = tri_mid_norm(m.alpha + (r0 + mid) * C, m.beta + (r0 + mid - 1) * C,
-                                       m.alpha_num + (r0 + mid) * NP,
-                                       m.beta_num + (r0 + mid - 1) * NP, C, NP, lane, true);
-        if (lane == 0) {
-          shf[0] = zn.x;
-          shf[1] = zn.y;
-          sh[3] = b;
-        }
-      }
-      __syncthreads();
     }
-    const float lz = shf[0], nm = shf[1];
+    // a frame whose norm is not finite (an unreachable string, a dead
+    // lattice) stays with marg_kernel, which zeroes it
     if (__builtin_isfinite(lz) && __builtin_isfinite(nm)) {
-      mix_stage_rows<BF16>(m, b, t, A, Bt, AN, BN, tid, nthr);
-      __syncthreads();
-      mix_frame<BF16>(m, b, t, lz, nm, A, Bt, AN, BN, aoff, alink, nbt, tid, nthr);
-      if (tid == 0) m.done[(long long)b * m.T + t] = 1;
+      const int* aoff = tabs + slot * 2 * NK;
+      mix_frame<BF16>(m, b, t, lz, nm, A, Bt, AN, BN, aoff, aoff + NK, nbt, lane);
+      // (diagnostic dbg 4: the frame is left to marg_kernel all the same)
+      if (lane == 0 && !(m.dbg & 4))
+        m.done[(long long)b * m.T + t] =
+            (m.dbg & 8) ? (int)own
+                        : (m.dbg & 16) ? (int)(mix_rt() | 0x40000000u) : 1;
     }
-    // (a frame whose norm is not finite -- an unreachable string, a dead
-    // lattice -- stays with marg_kernel, which zeroes it)
-    __syncthreads();
   }
 }
 
@@ -311,13 +365,16 @@ __global__ __launch_bounds__(1024) void tri_mix_kernel(const KArgs af, const KAr
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int x = blockIdx.x;
   if (x < 2 * nb) {
+    const bool stamp = (mx.dbg & 16) && mx.ts && threadIdx.x == 0;
+    if (stamp) mx.ts[x] = mix_rt();
     if (threadIdx.x == 0)
       __hip_atomic_store(mx.xcc + x, xcc_id() + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (x < nb) fwd_body<M_LOG, BF16, true, 2, 9, 32>(af, x);
     else bwd_body<BF16, true, false, 2, 9, true, (int)sizeof(KArgs), 32>(ab, x - nb);
+    if (stamp) mx.ts[2 * nb + x] = mix_rt();
     return;
   }
-  mix_marg<BF16>(mx, lds);
+  mix_marg<BF16>(mx, lds, mx.lds_bytes);
 }
 }  // namespace
 
@@ -340,10 +397,11 @@ int launch_tri_fwdbwd(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStre
   return LT_OK;
 }
 
-// LDS bytes of the marginal role (mix_marg's carve)
+// LDS bytes the marginal role wants (mix_marg: its tables and a row region
+// for every wave of a 1024-thread workgroup, capped at the CU's 160 KB)
 int tri_mix_lds(const NGram& g, int U, int B) {
-  const int NP = U + 1, NK = 2 * NP;
-  return 4 * (2 * g.C + 2 * NP + 1 + 2 * NK + 2 * (NP + 1) + g.C + B + 4 + 2) + 16;
+  const int NP = U + 1;
+  return std::min(160 * 1024, mix_shared_bytes(g.C, NP, B) + 16 * mix_row_bytes(g.C, NP));
 }
 
 int launch_tri_mix(const Plan& pf, const Plan& pb, bool bf16, int nb, int marg_blocks,
@@ -360,6 +418,7 @@ int launch_tri_mix(const Plan& pf, const Plan& pb, bool bf16, int nb, int marg_b
   if (e != hipSuccess) return set_error(LT_EHIP, hipGetErrorString(e));
   KArgs af = pf.a, ab = pb.a;
   MixArgs m = mx;
+  m.lds_bytes = lds;
   void* args[] = {(void*)&af, (void*)&ab, (void*)&nb, (void*)&m};
   e = hipLaunchKernel(k, dim3(2 * nb + marg_blocks), dim3(pf.threads), args, lds, st);
   if (e == hipSuccess) e = hipGetLastError();
