@@ -46,6 +46,9 @@ LT_DEVINL unsigned xcc_id() {
 }
 // diagnostic time stamps: the low 30 bits of the 100 MHz real-time counter
 LT_DEVINL unsigned mix_rt() { return (unsigned)__builtin_amdgcn_s_memrealtime() & 0x3fffffffu; }
+LT_DEVINL float uniform_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
 LT_DEVINL unsigned ld_u32_sc1(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -89,14 +92,23 @@ LT_DEVINL void mix_frame(const MixArgs& m, int b, int t, float lz, float nm, flo
   const int NP = m.U + 1, NK = 2 * NP;
   {
     // the four rows by sc1 buffer loads (L1 bypassed: another workgroup of
-    // this launch wrote them), every load in flight before the first LDS write
+    // this launch wrote them), every load in flight before the first LDS write.
+    // Lanes read each other's row entries, so the hand-offs through the
+    // wave's LDS region are wavefront-scope fences (a wave barrier alone
+    // orders no memory for the compiler): the previous frame's reads before
+    // these writes, these writes before this frame's reads
     const long long rc = ((long long)b * m.T + t) * C, rn = ((long long)b * m.T + t) * NP;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     row_sc1<17>(m.alpha + rc, C, A, lane);
     row_sc1<17>(m.beta + rc, C, Bt, lane);
     row_sc1<2>(m.alpha_num + rn, NP, AN, lane);
     row_sc1<2>(m.beta_num + rn, NP, BN, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's row writes, before any lane reads them
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   if (m.dbg & 64) return;  // diagnostic: the rows only
   const float gb = m.grad ? m.grad[b] : 1.f;
@@ -184,7 +196,7 @@ LT_DEVINL void mix_frame(const MixArgs& m, int b, int t, float lz, float nm, flo
 __host__ __device__ inline int al16i(int x) { return (x + 15) & ~15; }
 // the marginal role's shared LDS (the utterances' tables) and one wave's rows
 __host__ __device__ inline int mix_shared_bytes(int C, int NP, int B) {
-  return al16i(4 * (C + kMixUtt * 4 * NP + 2 * (NP + 1) + B + 4 + 2 * kMixUtt));
+  return al16i(4 * (C + kMixUtt * 4 * NP + 2 * (NP + 1) + B + 4 + 16 * 2 * kMixUtt));
 }
 __host__ __device__ inline int mix_row_bytes(int C, int NP) { return al16i(4 * (2 * C + 2 * NP)); }
 
@@ -192,7 +204,15 @@ __host__ __device__ inline int mix_row_bytes(int C, int NP) { return al16i(4 * (
 // builds the tables of the utterances on its XCD, then every wave takes
 // frames through the XCD's job counter on its own.
 template <bool BF16>
-LT_DEVINL void mix_marg(const MixArgs& m, unsigned char* lds, int lds_bytes) {
+LT_DEVINL void mix_marg(const MixArgs& m_in, unsigned char* lds, int lds_bytes) {
+#ifdef LT_MIX_NODBG
+  // diagnostic: the switches folded away. This build gives wrong chain-head
+  // elements on every frame after a wave's first ("Open item")
+  MixArgs m = m_in;
+  m.dbg = 0;
+#else
+  const MixArgs& m = m_in;
+#endif
   const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int B = m.B, C = m.g.C, NP = m.U + 1, NK = 2 * NP;
@@ -202,7 +222,7 @@ LT_DEVINL void mix_marg(const MixArgs& m, unsigned char* lds, int lds_bytes) {
   int* ylab = ctx + NP + 1;              // [NP + 1]
   int* list = ylab + NP + 1;             // [B] the utterances this XCD's marginal workgroups take
   int* sh = list + B;                    // [0] list length
-  float* shf = (float*)(sh + 4);         // [2 kMixUtt] log Z, num by list slot (NaN: not yet)
+  float* shf = (float*)(sh + 4);         // [16][2 kMixUtt] per wave: log Z, num by slot (NaN: not yet)
   const int shared = mix_shared_bytes(C, NP, B), rowb = mix_row_bytes(C, NP);
   int nwork = min(nthr >> 6, (lds_bytes - shared) / rowb);
   if (m.dbg & 2048) nwork = min(nwork, 8);  // diagnostic: fewer marginal waves
@@ -213,7 +233,7 @@ LT_DEVINL void mix_marg(const MixArgs& m, unsigned char* lds, int lds_bytes) {
     bool z;
     nbt[p] = next_base(m.g, p, &z);
   }
-  for (int i = tid; i < 2 * kMixUtt; i += nthr) shf[i] = __builtin_nanf("");
+  for (int i = tid; i < 16 * 2 * kMixUtt; i += nthr) shf[i] = __builtin_nanf("");
   if (tid == 0) {
     // the recursion workgroups' XCD ids (each writes its own at its start)
     int n = 0, abort = 0;
@@ -324,10 +344,14 @@ LT_DEVINL void mix_marg(const MixArgs& m, unsigned char* lds, int lds_bytes) {
     job = __builtin_amdgcn_readfirstlane(job);
     if (job < 0) return;
     const int slot = job >> 26, b = (job >> 16) & 1023, t = job & 0xffff;
-    float lz = shf[2 * slot], nm = shf[2 * slot + 1];
-    if (__builtin_isnan(lz)) {
+    // the slot's norm as this wave computed it before (each wave keeps its
+    // own copy: no LDS word is written by one wave while another reads it),
+    // taken wave-uniform
+    float* wn = shf + wave * 2 * kMixUtt + 2 * slot;
+    float lz = uniform_f(wn[0]), nm = uniform_f(wn[1]);
+    if (__builtin_isnan(lz) || __builtin_isnan(nm)) {
       // this utterance's middle norm (its rows are final: the job's wait
-      // covered them); another wave may compute the same bits beside it
+      // covered them), once per wave and utterance
       int nf = m.nfr[b];
       nf = nf < 0 ? 0 : (nf > m.T ? m.T : nf);
       const int mid = nf / 2;
@@ -335,11 +359,11 @@ LT_DEVINL void mix_marg(const MixArgs& m, unsigned char* lds, int lds_bytes) {
       const float2 zn = tri_mid_norm(m.alpha + (r0 + mid) * C, m.beta + (r0 + mid - 1) * C,
                                      m.alpha_num + (r0 + mid) * NP,
                                      m.beta_num + (r0 + mid - 1) * NP, C, NP, lane, true);
-      lz = zn.x;
-      nm = zn.y;
+      lz = uniform_f(zn.x);
+      nm = uniform_f(zn.y);
       if (lane == 0) {
-        shf[2 * slot] = lz;
-        shf[2 * slot + 1] = nm;
+        wn[0] = lz;
+        wn[1] = nm;
       }
     }
     // a frame whose norm is not finite (an unreachable string, a dead
