@@ -43,6 +43,15 @@ def run(name, table, K, B, T, U, dtype=torch.float32):
   graph = nat.TableGraph(table, K, 'cuda')
   ms = timeit(lambda: nat.table_loss_grad(graph, W, nf, lab, nl, False))
   mv = timeit(lambda: nat.table_viterbi(graph, W, nf, 1))
+  if os.environ.get('BREAK') == '1':  # the four passes of the loss + gradient apart (Log)
+    d, a = nat.table_forward(graph, W, nf, nat.SEMIRING_LOG)
+    parts = {
+        'den_forward_ms': timeit(lambda: nat.table_forward(graph, W, nf, nat.SEMIRING_LOG)),
+        'num_forward_ms': timeit(lambda: nat.table_num_forward(graph, W, nf, lab, nl, nat.SEMIRING_LOG)),
+        'den_backward_ms': timeit(lambda: nat.table_den_backward(graph, W, nf, nat.SEMIRING_LOG, d, a)),
+        'num_backward_ms': timeit(lambda: nat.table_num_backward(graph, W, nf, lab, nl, nat.SEMIRING_LOG)),
+    }
+    print(json.dumps({'workload': name, 'parts': parts}), flush=True)
   es = 2 if dtype == torch.bfloat16 else 4
   byts = B * T * C * (V + 1) * (3 * es)
   print(json.dumps({'workload': name, 'B': B, 'T': T, 'U': U, 'C': int(C), 'V': int(V), 'K': K,
