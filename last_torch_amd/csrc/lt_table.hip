@@ -110,6 +110,9 @@ template <int SR>
 LT_DEVINL float t_times(float a, float b) { return SR == M_REAL ? a * b : a + b; }
 
 constexpr int kTabMaxThreads = 512;
+#ifndef LT_TAB_DENSE
+#define LT_TAB_DENSE 1  // the dense-bigram FrameLabelDependent kernels (diagnostic builds: 0 = generic)
+#endif
 
 // Log vectors are kept relative to an integer offset near their maximum
 // (exact in fp32), so a recursion over T frames rounds small numbers, not
@@ -652,6 +655,132 @@ LT_DEVINL void tab_fwd_k0_body(const TArgs& a, const int b, float* sm) {
   }
 }
 
+// ---- dense bigram context, FrameLabelDependent(K >= 1): one wave -----------
+// FullNGram bigram (contexts.py:207-256 with n = 1): C = V + 1 states, every
+// state p goes to state y on label y, so each lexical expansion of
+// FrameLabelDependent.forward (alignments.py:363-377) is v'[y] = (+)_p v[p] w[p][y]
+// over all C sources and nothing enters state 0. The generic kernel spends a
+// frame on seven barrier-separated sweeps (CSR gathers, shuffle merges); here
+// ONE wave keeps a frame in registers: lane (j, h) owns destination y = j + 1
+// and sources [17h, 17h + 17), the two halves' partial logsumexps swap by
+// permlane32, the vector goes between expansions through a 36-float LDS row.
+// The other waves of the workgroup leave at once (no barrier after the
+// dispatch). Decided by every thread from the next-state table.
+LT_DEVINL bool tab_dense_bigram(const TArgs& a) {
+  __shared__ int s_dense;
+  if (threadIdx.x == 0) s_dense = (a.C == a.V + 1 && a.V <= 32 && a.V >= 1) ? 1 : 0;
+  __syncthreads();
+  if (s_dense)
+    for (int e = threadIdx.x; e < a.C * a.V; e += blockDim.x)
+      if (a.table[e] != e % a.V + 1) s_dense = 0;  // (benign race: every writer stores 0)
+  __syncthreads();
+  const bool d = s_dense != 0;
+  __syncthreads();  // (s_dense is read by every thread before any can reuse it)
+  return d;
+}
+
+LT_DEVINL int tdslot(int p) { return p < 17 ? p : p + 3; }  // sources of half 1 at 20..
+
+template <bool BF16>
+LT_DEVINL void tab_fwd_dense(const TArgs& a, const int b, float* sm) {
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 31, h = lane >> 5;
+  const int V = a.V, C = a.C, R = a.R, K = a.K;
+  const int y = j + 1;
+  const bool live = y <= V;
+  const int ns = h ? C - 17 : (C < 17 ? C : 17);  // sources of this half
+  float* vb = sm;  // [40] the vector between expansions (slots tdslot(p)), -inf elsewhere
+  for (int e = lane; e < 40; e += 64) vb[e] = -kInf;
+  (void)ns;
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const long long FR = (long long)C * R;
+  const unsigned char* wb0 = a.W + (long long)b * a.T * FR * (BF16 ? 2 : 4);
+  // the lane's weights of a frame: its sources' arcs into y, y's blank, w[0][0]
+  float wc[17], wbl = 0.f, w00 = 0.f, nwc[17], nwbl = 0.f, nw00 = 0.f;
+  auto fetch = [&](int t, float* c, float& bl, float& z) {
+    const unsigned char* wf = wb0 + (long long)t * FR * (BF16 ? 2 : 4);
+#pragma unroll
+    for (int m = 0; m < 17; ++m)
+      c[m] = (m < ns && live) ? ldw<BF16>(wf, (long long)(17 * h + m) * R + y) : 0.f;
+    bl = live ? ldw<BF16>(wf, (long long)y * R) : 0.f;
+    z = ldw<BF16>(wf, 0);
+  };
+  if (nf > 0) fetch(0, nwc, nwbl, nw00);
+  float ay = -kInf, a0 = 0.f;  // alpha relative to the offset O (start state: one = 0)
+  float O = 0.f;
+  for (int t = 0; t < a.T; ++t) {
+    if (a.alpha) {
+      float* row = a.alpha + ((long long)b * a.T + t) * C;
+      if (h == 0 && live) row[y] = O + ay;
+      if (lane == 32) row[0] = O + a0;
+    }
+    if (t >= nf) continue;  // padding frames carry alpha (lattices.py:460-461)
+#pragma unroll
+    for (int m = 0; m < 17; ++m) wc[m] = nwc[m];
+    wbl = nwbl;
+    w00 = nw00;
+    if (t + 1 < nf) fetch(t + 1, nwc, nwbl, nw00);  // next frame under this one
+    // terminated[0] = alpha (x) blank; the chain starts at alpha
+    float acc = live ? ay + wbl : -kInf;
+    const float acc0 = a0 + w00;
+    float v = ay;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (h == 0 && live) vb[tdslot(y)] = v;
+    if (lane == 32) vb[0] = a0;
+    for (int i = 1; i <= K; ++i) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float x[17];
+      float mx = -kInf;
+#pragma unroll
+      for (int m = 0; m < 17; ++m) {
+        // every read unconditional (a read under a branch waits its own
+        // latency): slots past the sources hold -inf for good
+        x[m] = vb[20 * h + m] + wc[m];
+        mx = fmaxf(mx, x[m]);
+      }
+      const float ch = t_safe(mx);
+      float ss = 0.f;
+#pragma unroll
+      for (int m = 0; m < 17; ++m) ss += lt_exp(x[m] - ch);
+      // the other half's (max, sum) by permlane32 swap; the same expression on
+      // both halves (commuted operands), so both hold the same value
+      const auto pm = __builtin_amdgcn_permlane32_swap(__float_as_int(mx), __float_as_int(mx), false, false);
+      const auto ps = __builtin_amdgcn_permlane32_swap(__float_as_int(ss), __float_as_int(ss), false, false);
+      const float omx = __int_as_float(h ? pm[0] : pm[1]);
+      const float oss = __int_as_float(h ? ps[0] : ps[1]);
+      const float oc = t_safe(omx);
+      const float c = t_safe(fmaxf(mx, omx));
+      const float S = h ? oss * lt_exp(oc - c) + ss * lt_exp(ch - c) : ss * lt_exp(ch - c) + oss * lt_exp(oc - c);
+      v = live ? (S > 0.f ? c + lt_log_acc(S) : -kInf) : -kInf;
+      acc = live ? t_lae(acc, v + wbl) : -kInf;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (h == 0 && live) vb[tdslot(y)] = v;
+      if (lane == 32) vb[0] = -kInf;  // nothing enters the start state
+    }
+    // the new vector over a new integer offset (floor of its max)
+    float m = fmaxf(acc, acc0);
+    m = gmax<6>(m, 6);
+    const float sp = __builtin_isfinite(m) ? floorf(m) : 0.f;
+    ay = acc - sp;
+    a0 = acc0 - sp;
+    O += sp;
+  }
+  // (+)_q alpha_T[q] (lattices.py:496)
+  float m = fmaxf(h == 0 && live ? ay : -kInf, a0);
+  m = gmax<6>(m, 6);
+  const float c = t_safe(m);
+  float e = h == 0 && live ? lt_exp(ay - c) : 0.f;
+  if (lane == 32) e += lt_exp(a0 - c);
+  e = gsum<6>(e, 6);
+  if (lane == 0) a.dist[b] = e > 0.f ? O + c + lt_log_acc(e) : -kInf;
+}
+
 // ---- forward: den (NUM = false) or string (NUM = true) shortest distance ----
 // STAGE: the frame's weights are copied to LDS once (coalesced) and the
 // in-arc gathers read LDS; otherwise they read W from global memory.
@@ -664,6 +793,12 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
   if constexpr (!NUM) {
     if (a.K == 0) {
       tab_fwd_k0_body<BF16, SR, VIT, STAGE>(a, b, sm);
+      return;
+    }
+  }
+  if constexpr (!NUM && SR == M_LOG && !VIT) {
+    if (LT_TAB_DENSE && tab_dense_bigram(a)) {  // (a uniform decision: every thread took it)
+      if (threadIdx.x < 64) tab_fwd_dense<BF16>(a, b, sm);
       return;
     }
   }
@@ -1082,11 +1217,188 @@ LT_DEVINL void tab_bwd_den_k0_body(const TArgs& a, const int b, float* sm) {
   }
 }
 
+// The dense-bigram FrameLabelDependent(K) backward in ONE wave (Log; see
+// tab_fwd_dense): lane p owns state p's row of the frame -- its blank and its
+// V lexical weights in registers, its dW row accumulated in registers -- and,
+// for the lexical alphas L^i alpha_t recomputed from the history row, state p
+// as a destination (its column of the frame from an LDS copy). The same
+// recursion as tab_bwd_den_body: blank marginals over the K+1 alphas, then
+// the lexical levels j = K-1..0 with cur_j = bb (+) L(cur_{j+1}).
+constexpr int kTabDenseKMax = 4;
+template <bool BF16>
+LT_DEVINL void tab_bwd_den_dense(const TArgs& a, const int b, float* sm) {
+  const int p = threadIdx.x & 63;  // the lane's state (rows p < C)
+  const int C = a.C, V = a.V, R = a.R, K = a.K;
+  const bool row = p < C;
+  float* wf = sm;                    // [C * R] the frame (columns read by destination lanes)
+  float* vb = wf + ((C * R + 3) & ~3);  // [64] a vector broadcast
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const float lz = a.local ? 0.f : a.den_in[b];
+  const float nm = a.num_in[b];
+  const float gb = a.gin ? a.gin[b] : 1.f;
+  const bool live = !a.local && __builtin_isfinite(nm) && __builtin_isfinite(lz) && gb != 0.f;
+  const long long FR = (long long)C * R;
+  const unsigned char* wb0 = a.W + (long long)b * a.T * FR * (BF16 ? 2 : 4);
+  float wr[33], nwr[33];  // the lane's row: blank w[p][0], lexical w[p][1..V]
+  float hr = 0.f, nhr = 0.f;  // the history alpha_t[p]
+  auto fetch = [&](int t, float* w, float& hv) {
+    const unsigned char* f = wb0 + (long long)t * FR * (BF16 ? 2 : 4);
+#pragma unroll
+    for (int k = 0; k < 33; ++k) w[k] = (row && k < R) ? ldw<BF16>(f, (long long)p * R + k) : 0.f;
+    hv = row ? a.hist[((long long)b * a.T + t) * C + p] : -kInf;
+  };
+  if (live && nf > 0) fetch(nf - 1, nwr, nhr);
+  float beta = 0.f;  // beta_{t+1}[p] relative to Ob (every state final: one)
+  float Ob = 0.f;
+  for (int t = a.T - 1; t >= 0; --t) {
+    const long long fo = ((long long)b * a.T + t) * FR;
+    if (t >= nf || !live) {
+      for (long long e = p; e < FR; e += 64) a.dW[fo + e] = 0.f;
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < 33; ++k) wr[k] = nwr[k];
+    hr = nhr;
+    if (t >= 1) fetch(t - 1, nwr, nhr);  // the previous frame under this one
+    // the frame into LDS (row by row), then the lane's column as a destination
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (row)
+#pragma unroll
+      for (int k = 0; k < 33; ++k)
+        if (k < R) wf[p * R + k] = wr[k];
+    if (p < 64) vb[p] = row ? hr : -kInf;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool dest = p >= 1 && p <= V;  // lexical destinations (nothing enters state 0)
+    float col[33];
+    const int pc = p < R ? p : R - 1;  // (reads clamped in bounds, unconditional)
+#pragma unroll
+    for (int k = 0; k < 33; ++k) col[k] = wf[(k < C ? k : C - 1) * R + pc];
+    // lexical alphas: la[0] = alpha_t, la[i][p] = (+)_q la[i-1][q] w[q][p]
+    float la[kTabDenseKMax + 1];
+    la[0] = hr;
+#pragma unroll
+    for (int i = 1; i <= kTabDenseKMax; ++i) {
+      if (i > K) break;
+      float x[33], mx = -kInf;
+#pragma unroll
+      for (int k = 0; k < 33; ++k) {
+        // unconditional (a select would sink the read under a branch that
+        // waits its own latency): vb is -inf past C, non-destinations masked below
+        x[k] = vb[k] + col[k];
+        mx = fmaxf(mx, x[k]);
+      }
+      const float c = t_safe(mx);
+      float ss = 0.f;
+#pragma unroll
+      for (int k = 0; k < 33; ++k) ss += lt_exp(x[k] - c);
+      la[i] = dest && ss > 0.f ? c + lt_log_acc(ss) : -kInf;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      vb[p] = row ? la[i] : -kInf;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // blank marginals over the K + 1 alphas: exp((alpha - log_z) + Ob + w[p][0] + beta)
+    const float bb = wr[0] + beta;
+    float mb = 0.f;
+#pragma unroll
+    for (int i = 0; i <= kTabDenseKMax; ++i)
+      if (i <= K) mb += lt_exp(((la[i] - lz) + Ob) + bb) * gb;
+    float dacc[32];
+#pragma unroll
+    for (int y = 0; y < 32; ++y) dacc[y] = 0.f;
+    float cur = bb;  // level K: blank[K] + beta
+    for (int jj = K - 1; jj >= 0; --jj) {
+      // cur over the states by LDS, then the lane's row: lb = w[p][y] + cur[y]
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      vb[p] = row ? cur : -kInf;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float lj = -kInf;
+#pragma unroll
+      for (int i = 0; i < kTabDenseKMax; ++i)
+        if (i == jj) lj = la[i];
+      const float af = (lj - lz) + Ob;
+      float lb[32], mx = -kInf;
+#pragma unroll
+      for (int y = 0; y < 32; ++y) {
+        // unconditional reads: vb is -inf past C and wr 0 past R (rows past C
+        // have alpha -inf, so their sums are zero and never stored)
+        lb[y] = wr[y + 1] + vb[y + 1];
+        mx = fmaxf(mx, lb[y]);
+      }
+      const float c = t_safe(mx);
+      // one exponential per arc, shared by the sum and the marginal:
+      // exp(af + lb) = exp(lb - c) exp(af + c), and af + c is the log of the
+      // row's largest arc marginal (a probability: no overflow)
+      const float sc = lt_exp(af + c) * gb;
+      float ss = 0.f;
+#pragma unroll
+      for (int y = 0; y < 32; ++y) {
+        const float e = lt_exp(lb[y] - c);
+        ss += e;
+        dacc[y] += e * sc;
+      }
+      const float sv = ss > 0.f ? c + lt_log_acc(ss) : -kInf;
+      cur = row ? t_lae(bb, sv) : -kInf;
+      (void)V;
+    }
+    // the frame's dW through LDS (row p at p R, over the frame copy, whose
+    // columns every lane has read), then stored contiguously by all lanes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (row) {
+      wf[p * R] = mb;
+#pragma unroll
+      for (int y = 0; y < 32; ++y)
+        if (y < V) wf[p * R + y + 1] = dacc[y];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+      // the head up to a 16-byte boundary element by element, then float4s,
+      // then the tail
+      const int h0 = (int)((4 - (((unsigned long long)(a.dW + fo) >> 2) & 3)) & 3);
+      const int n4 = (int)((FR - h0) >> 2);
+      if (p < h0) a.dW[fo + p] = wf[p];
+      for (int i = p; i < n4; i += 64) {
+        const int e = h0 + 4 * i;
+        *(float4*)(a.dW + fo + e) = make_float4(wf[e], wf[e + 1], wf[e + 2], wf[e + 3]);
+      }
+      for (int e = h0 + 4 * n4 + p; e < FR; e += 64) a.dW[fo + e] = wf[e];
+    }
+    // beta_t over a new integer offset (floor of its max)
+    float m = row ? cur : -kInf;
+    m = gmax<6>(m, 6);
+    const float sp = __builtin_isfinite(m) ? floorf(m) : 0.f;
+    beta = cur - sp;
+    Ob += sp;
+  }
+}
+
 template <bool BF16, bool STAGE, int SR>
 LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
   if (a.K == 0) {
     tab_bwd_den_k0_body<BF16, STAGE, SR>(a, b, sm);
     return;
+  }
+  if constexpr (SR == M_LOG && STAGE) {  // (STAGE: the launch's LDS holds a frame and more)
+    if (LT_TAB_DENSE && a.K <= kTabDenseKMax && tab_dense_bigram(a)) {
+      if (threadIdx.x < 64) tab_bwd_den_dense<BF16>(a, b, sm);
+      return;
+    }
   }
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int C = a.C, V = a.V, R = a.R, K = a.K;

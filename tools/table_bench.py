@@ -49,7 +49,6 @@ def run(name, table, K, B, T, U, dtype=torch.float32):
         'den_forward_ms': timeit(lambda: nat.table_forward(graph, W, nf, nat.SEMIRING_LOG)),
         'num_forward_ms': timeit(lambda: nat.table_num_forward(graph, W, nf, lab, nl, nat.SEMIRING_LOG)),
         'den_backward_ms': timeit(lambda: nat.table_den_backward(graph, W, nf, nat.SEMIRING_LOG, d, a)),
-        'num_backward_ms': timeit(lambda: nat.table_num_backward(graph, W, nf, lab, nl, nat.SEMIRING_LOG)),
     }
     print(json.dumps({'workload': name, 'parts': parts}), flush=True)
   es = 2 if dtype == torch.bfloat16 else 4
