@@ -53,6 +53,10 @@ struct TArgs {
   // ntab [B,2S] (-1: none), subtracted from dW afterwards (tab_apply_kernel)
   float* nsub;
   int* ntab;
+  // dense-bigram FrameLabelDependent (lt_table_loss_grad): the lexical alphas
+  // L^i alpha_t, i = 1..K, [B,T,K,C], written by the forward and read by the
+  // backward instead of recomputed (nullable)
+  float* lx;
 };
 
 // Copies the graph arrays to LDS at g (ints: in_off [C+1], in_arc [C*V],
@@ -710,17 +714,26 @@ LT_DEVINL void tab_fwd_dense(const TArgs& a, const int b, float* sm) {
   float ay = -kInf, a0 = 0.f;  // alpha relative to the offset O (start state: one = 0)
   float O = 0.f;
   for (int t = 0; t < a.T; ++t) {
-    if (a.alpha) {
-      float* row = a.alpha + ((long long)b * a.T + t) * C;
-      if (h == 0 && live) row[y] = O + ay;
-      if (lane == 32) row[0] = O + a0;
+    // (the history row after this frame's weights are in and the next
+    // frame's loads issued: the wait for those at the next frame's top then
+    // covers this store too, a frame later, instead of stalling on it now)
+    auto hist_row = [&]() {
+      if (a.alpha) {
+        float* row = a.alpha + ((long long)b * a.T + t) * C;
+        if (h == 0 && live) row[y] = O + ay;
+        if (lane == 32) row[0] = O + a0;
+      }
+    };
+    if (t >= nf) {  // padding frames carry alpha (lattices.py:460-461)
+      hist_row();
+      continue;
     }
-    if (t >= nf) continue;  // padding frames carry alpha (lattices.py:460-461)
 #pragma unroll
     for (int m = 0; m < 17; ++m) wc[m] = nwc[m];
     wbl = nwbl;
     w00 = nw00;
     if (t + 1 < nf) fetch(t + 1, nwc, nwbl, nw00);  // next frame under this one
+    hist_row();
     // terminated[0] = alpha (x) blank; the chain starts at alpha
     float acc = live ? ay + wbl : -kInf;
     const float acc0 = a0 + w00;
@@ -734,18 +747,18 @@ LT_DEVINL void tab_fwd_dense(const TArgs& a, const int b, float* sm) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       float x[17];
-      float mx = -kInf;
 #pragma unroll
       for (int m = 0; m < 17; ++m) {
         // every read unconditional (a read under a branch waits its own
         // latency): slots past the sources hold -inf for good
         x[m] = vb[20 * h + m] + wc[m];
-        mx = fmaxf(mx, x[m]);
       }
+      const float mx = tree_max<17>(x);  // (balanced: short dependency chains)
       const float ch = t_safe(mx);
-      float ss = 0.f;
+      float ex[17];
 #pragma unroll
-      for (int m = 0; m < 17; ++m) ss += lt_exp(x[m] - ch);
+      for (int m = 0; m < 17; ++m) ex[m] = lt_exp(x[m] - ch);
+      const float ss = tree_sum<17>(ex);
       // the other half's (max, sum) by permlane32 swap; the same expression on
       // both halves (commuted operands), so both hold the same value
       const auto pm = __builtin_amdgcn_permlane32_swap(__float_as_int(mx), __float_as_int(mx), false, false);
@@ -757,6 +770,11 @@ LT_DEVINL void tab_fwd_dense(const TArgs& a, const int b, float* sm) {
       const float S = h ? oss * lt_exp(oc - c) + ss * lt_exp(ch - c) : ss * lt_exp(ch - c) + oss * lt_exp(oc - c);
       v = live ? (S > 0.f ? c + lt_log_acc(S) : -kInf) : -kInf;
       acc = live ? t_lae(acc, v + wbl) : -kInf;
+      if (a.lx) {
+        float* r = a.lx + (((long long)b * a.T + t) * K + (i - 1)) * C;
+        if (h == 0 && live) r[y] = O + v;
+        if (lane == 32) r[0] = -kInf;
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1232,6 +1250,7 @@ LT_DEVINL void tab_bwd_den_dense(const TArgs& a, const int b, float* sm) {
   const bool row = p < C;
   float* wf = sm;                    // [C * R] the frame (columns read by destination lanes)
   float* vb = wf + ((C * R + 3) & ~3);  // [64] a vector broadcast
+  float* dwb = vb + 64;              // [C * R] the previous frame's dW, stored a frame late
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const float lz = a.local ? 0.f : a.den_in[b];
@@ -1242,15 +1261,34 @@ LT_DEVINL void tab_bwd_den_dense(const TArgs& a, const int b, float* sm) {
   const unsigned char* wb0 = a.W + (long long)b * a.T * FR * (BF16 ? 2 : 4);
   float wr[33], nwr[33];  // the lane's row: blank w[p][0], lexical w[p][1..V]
   float hr = 0.f, nhr = 0.f;  // the history alpha_t[p]
+  float nla[kTabDenseKMax + 1], fla[kTabDenseKMax + 1];  // lexical alphas from a.lx
   auto fetch = [&](int t, float* w, float& hv) {
     const unsigned char* f = wb0 + (long long)t * FR * (BF16 ? 2 : 4);
 #pragma unroll
     for (int k = 0; k < 33; ++k) w[k] = (row && k < R) ? ldw<BF16>(f, (long long)p * R + k) : 0.f;
     hv = row ? a.hist[((long long)b * a.T + t) * C + p] : -kInf;
+#pragma unroll
+    for (int i = 1; i <= kTabDenseKMax; ++i)
+      fla[i] = (a.lx && row && i <= K) ? a.lx[(((long long)b * a.T + t) * K + (i - 1)) * C + p] : -kInf;
   };
   if (live && nf > 0) fetch(nf - 1, nwr, nhr);
   float beta = 0.f;  // beta_{t+1}[p] relative to Ob (every state final: one)
   float Ob = 0.f;
+  // frame tp's dW (in dwb) to memory: issued after the next frame's loads,
+  // so the wait for those (a frame later) covers these stores as well
+  long long pend = -1;
+  auto flush = [&]() {
+    if (pend < 0) return;
+    const int h0 = (int)((4 - (((unsigned long long)(a.dW + pend) >> 2) & 3)) & 3);
+    const int n4 = (int)((FR - h0) >> 2);
+    if (p < h0) a.dW[pend + p] = dwb[p];
+    for (int i = p; i < n4; i += 64) {
+      const int e = h0 + 4 * i;
+      *(float4*)(a.dW + pend + e) = make_float4(dwb[e], dwb[e + 1], dwb[e + 2], dwb[e + 3]);
+    }
+    for (int e = h0 + 4 * n4 + p; e < FR; e += 64) a.dW[pend + e] = dwb[e];
+    pend = -1;
+  };
   for (int t = a.T - 1; t >= 0; --t) {
     const long long fo = ((long long)b * a.T + t) * FR;
     if (t >= nf || !live) {
@@ -1260,12 +1298,15 @@ LT_DEVINL void tab_bwd_den_dense(const TArgs& a, const int b, float* sm) {
 #pragma unroll
     for (int k = 0; k < 33; ++k) wr[k] = nwr[k];
     hr = nhr;
+#pragma unroll
+    for (int i = 1; i <= kTabDenseKMax; ++i) nla[i] = fla[i];
     if (t >= 1) fetch(t - 1, nwr, nhr);  // the previous frame under this one
+    flush();  // frame t + 1's dW (its LDS reads in order before this frame's writes)
     // the frame into LDS (row by row), then the lane's column as a destination
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (row)
+    if (row && !a.lx)
 #pragma unroll
       for (int k = 0; k < 33; ++k)
         if (k < R) wf[p * R + k] = wr[k];
@@ -1274,28 +1315,32 @@ LT_DEVINL void tab_bwd_den_dense(const TArgs& a, const int b, float* sm) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const bool dest = p >= 1 && p <= V;  // lexical destinations (nothing enters state 0)
-    float col[33];
-    const int pc = p < R ? p : R - 1;  // (reads clamped in bounds, unconditional)
-#pragma unroll
-    for (int k = 0; k < 33; ++k) col[k] = wf[(k < C ? k : C - 1) * R + pc];
     // lexical alphas: la[0] = alpha_t, la[i][p] = (+)_q la[i-1][q] w[q][p]
+    // (lt_table_loss_grad: the forward's, from a.lx; else recomputed here)
     float la[kTabDenseKMax + 1];
     la[0] = hr;
 #pragma unroll
+    for (int i = 1; i <= kTabDenseKMax; ++i) la[i] = i <= K ? nla[i] : -kInf;
+    float col[33];
+    if (!a.lx) {
+      const int pc = p < R ? p : R - 1;  // (reads clamped in bounds, unconditional)
+#pragma unroll
+      for (int k = 0; k < 33; ++k) col[k] = wf[(k < C ? k : C - 1) * R + pc];
+    }
+#pragma unroll
     for (int i = 1; i <= kTabDenseKMax; ++i) {
-      if (i > K) break;
-      float x[33], mx = -kInf;
+      if (i > K || a.lx) break;
+      float x[33];
 #pragma unroll
       for (int k = 0; k < 33; ++k) {
         // unconditional (a select would sink the read under a branch that
         // waits its own latency): vb is -inf past C, non-destinations masked below
         x[k] = vb[k] + col[k];
-        mx = fmaxf(mx, x[k]);
       }
-      const float c = t_safe(mx);
-      float ss = 0.f;
+      const float c = t_safe(tree_max<33>(x));
 #pragma unroll
-      for (int k = 0; k < 33; ++k) ss += lt_exp(x[k] - c);
+      for (int k = 0; k < 33; ++k) x[k] = lt_exp(x[k] - c);
+      const float ss = tree_sum<33>(x);
       la[i] = dest && ss > 0.f ? c + lt_log_acc(ss) : -kInf;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -1329,56 +1374,43 @@ LT_DEVINL void tab_bwd_den_dense(const TArgs& a, const int b, float* sm) {
       for (int i = 0; i < kTabDenseKMax; ++i)
         if (i == jj) lj = la[i];
       const float af = (lj - lz) + Ob;
-      float lb[32], mx = -kInf;
+      float lb[32];
 #pragma unroll
       for (int y = 0; y < 32; ++y) {
         // unconditional reads: vb is -inf past C and wr 0 past R (rows past C
         // have alpha -inf, so their sums are zero and never stored)
         lb[y] = wr[y + 1] + vb[y + 1];
-        mx = fmaxf(mx, lb[y]);
       }
-      const float c = t_safe(mx);
+      const float c = t_safe(tree_max<32>(lb));
       // one exponential per arc, shared by the sum and the marginal:
       // exp(af + lb) = exp(lb - c) exp(af + c), and af + c is the log of the
       // row's largest arc marginal (a probability: no overflow)
       const float sc = lt_exp(af + c) * gb;
-      float ss = 0.f;
 #pragma unroll
       for (int y = 0; y < 32; ++y) {
-        const float e = lt_exp(lb[y] - c);
-        ss += e;
-        dacc[y] += e * sc;
+        lb[y] = lt_exp(lb[y] - c);
+        dacc[y] += lb[y] * sc;
       }
+      const float ss = tree_sum<32>(lb);
       const float sv = ss > 0.f ? c + lt_log_acc(ss) : -kInf;
       cur = row ? t_lae(bb, sv) : -kInf;
       (void)V;
     }
-    // the frame's dW through LDS (row p at p R, over the frame copy, whose
-    // columns every lane has read), then stored contiguously by all lanes
+    // the frame's dW rows into dwb (row p at p R), stored contiguously by
+    // every lane at the next frame's top (flush) or after the loop
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (row) {
-      wf[p * R] = mb;
+      dwb[p * R] = mb;
 #pragma unroll
       for (int y = 0; y < 32; ++y)
-        if (y < V) wf[p * R + y + 1] = dacc[y];
+        if (y < V) dwb[p * R + y + 1] = dacc[y];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    {
-      // the head up to a 16-byte boundary element by element, then float4s,
-      // then the tail
-      const int h0 = (int)((4 - (((unsigned long long)(a.dW + fo) >> 2) & 3)) & 3);
-      const int n4 = (int)((FR - h0) >> 2);
-      if (p < h0) a.dW[fo + p] = wf[p];
-      for (int i = p; i < n4; i += 64) {
-        const int e = h0 + 4 * i;
-        *(float4*)(a.dW + fo + e) = make_float4(wf[e], wf[e + 1], wf[e + 2], wf[e + 3]);
-      }
-      for (int e = h0 + 4 * n4 + p; e < FR; e += 64) a.dW[fo + e] = wf[e];
-    }
+    pend = fo;
     // beta_t over a new integer offset (floor of its max)
     float m = row ? cur : -kInf;
     m = gmax<6>(m, 6);
@@ -1386,6 +1418,7 @@ LT_DEVINL void tab_bwd_den_dense(const TArgs& a, const int b, float* sm) {
     beta = cur - sp;
     Ob += sp;
   }
+  flush();
 }
 
 template <bool BF16, bool STAGE, int SR>
@@ -1394,8 +1427,8 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
     tab_bwd_den_k0_body<BF16, STAGE, SR>(a, b, sm);
     return;
   }
-  if constexpr (SR == M_LOG && STAGE) {  // (STAGE: the launch's LDS holds a frame and more)
-    if (LT_TAB_DENSE && a.K <= kTabDenseKMax && tab_dense_bigram(a)) {
+  if constexpr (SR == M_LOG && STAGE) {  // (STAGE and acc: the launch's LDS holds two frames)
+    if (LT_TAB_DENSE && a.acc && a.K <= kTabDenseKMax && tab_dense_bigram(a)) {
       if (threadIdx.x < 64) tab_bwd_den_dense<BF16>(a, b, sm);
       return;
     }
@@ -2266,7 +2299,7 @@ int t_fwd(int sr, bool num, bool vit, const TArgs& a, bool bf16, hipStream_t st)
 }
 
 struct GradLayout {
-  size_t hd, hn, nsub, ntab, dwf, total;
+  size_t hd, hn, nsub, ntab, dwf, lx, total;
 };
 GradLayout grad_layout(const lt_graph* g, const lt_table_problem* pb) {
   auto up = [](long long x) { return (size_t)((x + 255) & ~255LL); };
@@ -2278,7 +2311,8 @@ GradLayout grad_layout(const lt_graph* g, const lt_table_problem* pb) {
   l.ntab = l.nsub + up(4 * BT * NK);
   l.dwf = l.ntab + up(4LL * pb->batch * NK);
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
-  l.total = l.dwf + (bf16 ? up(4 * BT * g->num_states * (g->vocab_size + 1)) : 0);
+  l.lx = l.dwf + (bf16 ? up(4 * BT * g->num_states * (g->vocab_size + 1)) : 0);
+  l.total = l.lx + (g->expansions > 0 ? up(4 * BT * g->expansions * g->num_states) : 0);
   return l;
 }
 
@@ -2369,6 +2403,7 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   TArgs ad = a, an = a;
   ad.dist = log_z;
   ad.alpha = hd;
+  ad.lx = (dW && K > 0) ? (float*)((char*)workspace + l.lx) : nullptr;
   an.dist = num;
   an.alpha = hn;
   if (!local_norm) {
@@ -2406,6 +2441,7 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   ad = a;
   an = a;
   ad.hist = hd;
+  ad.lx = (dW && K > 0) ? (float*)((char*)workspace + l.lx) : nullptr;
   ad.nsub = nullptr;
   ad.ntab = nullptr;
   an.hist = hn;
