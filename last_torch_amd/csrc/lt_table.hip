@@ -1421,6 +1421,135 @@ LT_DEVINL void tab_bwd_den_dense(const TArgs& a, const int b, float* sm) {
   flush();
 }
 
+// The same backward on TWO waves when the forward left its lexical alphas
+// (a.lx, lt_table_loss_grad): wave w takes labels y in [16w + 1, 16w + 16] of
+// every row (lane p = state p), so a lane forms half the arcs of a level;
+// the two halves' (max, sum) of each row's logsumexp meet through LDS at one
+// barrier a level, combined in a fixed order (both waves get the same bits).
+template <bool BF16>
+LT_DEVINL void tab_bwd_den_dense2(const TArgs& a, const int b, float* sm) {
+  const int w = threadIdx.x >> 6, p = threadIdx.x & 63;
+  const int C = a.C, R = a.R, K = a.K;
+  const bool row = p < C;
+  const int y0 = 16 * w;           // the wave's labels y0 + 1 .. y0 + 16
+  float* vb = sm;                  // [64] cur over the states (-inf past C)
+  float* part = vb + 64;           // [2 levels][2 waves][max, sum][64]
+  float* dwb = part + 512;         // [C R] the frame's dW, stored a frame late
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const float lz = a.local ? 0.f : a.den_in[b];
+  const float nm = a.num_in[b];
+  const float gb = a.gin ? a.gin[b] : 1.f;
+  const bool live = !a.local && __builtin_isfinite(nm) && __builtin_isfinite(lz) && gb != 0.f;
+  const long long FR = (long long)C * R;
+  const unsigned char* wb0 = a.W + (long long)b * a.T * FR * (BF16 ? 2 : 4);
+  float wr[17], nwr[17];  // w[p][0], then w[p][y0 + 1 .. y0 + 16]
+  float la[kTabDenseKMax + 1], nla[kTabDenseKMax + 1];
+  auto fetch = [&](int t, float* wv, float* lv) {
+    const unsigned char* f = wb0 + (long long)t * FR * (BF16 ? 2 : 4);
+    wv[0] = row ? ldw<BF16>(f, (long long)p * R) : 0.f;
+#pragma unroll
+    for (int k = 1; k < 17; ++k)
+      wv[k] = (row && y0 + k < R) ? ldw<BF16>(f, (long long)p * R + y0 + k) : 0.f;
+    lv[0] = row ? a.hist[((long long)b * a.T + t) * C + p] : -kInf;
+#pragma unroll
+    for (int i = 1; i <= kTabDenseKMax; ++i)
+      lv[i] = (row && i <= K) ? a.lx[(((long long)b * a.T + t) * K + (i - 1)) * C + p] : -kInf;
+  };
+  auto sync = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  if (live && nf > 0) fetch(nf - 1, nwr, nla);
+  float beta = 0.f, Ob = 0.f;  // beta_{t+1}[p] relative to Ob (every state final: one)
+  long long pend = -1;
+  auto flush = [&]() {  // frame pend's dW from dwb, all 128 lanes
+    if (pend < 0) return;
+    const int t2 = threadIdx.x;
+    const int h0 = (int)((4 - (((unsigned long long)(a.dW + pend) >> 2) & 3)) & 3);
+    const int n4 = (int)((FR - h0) >> 2);
+    if (t2 < h0) a.dW[pend + t2] = dwb[t2];
+    for (int i = t2; i < n4; i += 128) {
+      const int e = h0 + 4 * i;
+      *(float4*)(a.dW + pend + e) = make_float4(dwb[e], dwb[e + 1], dwb[e + 2], dwb[e + 3]);
+    }
+    for (int e = h0 + 4 * n4 + t2; e < FR; e += 128) a.dW[pend + e] = dwb[e];
+    pend = -1;
+  };
+  for (int t = a.T - 1; t >= 0; --t) {
+    const long long fo = ((long long)b * a.T + t) * FR;
+    if (t >= nf || !live) {
+      for (long long e = threadIdx.x; e < FR; e += 128) a.dW[fo + e] = 0.f;
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < 17; ++k) wr[k] = nwr[k];
+#pragma unroll
+    for (int i = 0; i <= kTabDenseKMax; ++i) la[i] = nla[i];
+    if (t >= 1) fetch(t - 1, nwr, nla);  // the previous frame under this one
+    flush();  // frame t + 1's dW (its dwb writes came before that frame's last barrier)
+    const float bb = wr[0] + beta;
+    float mb = 0.f;  // the blank marginal over the K + 1 alphas (wave 0 stores it)
+#pragma unroll
+    for (int i = 0; i <= kTabDenseKMax; ++i)
+      if (i <= K) mb += lt_exp(((la[i] - lz) + Ob) + bb) * gb;
+    float dacc[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dacc[k] = 0.f;
+    float cur = row ? bb : -kInf;  // level K: blank[K] + beta
+    for (int jj = K - 1; jj >= 0; --jj) {
+      if (w == 0) vb[p] = cur;  // (both waves hold the same cur)
+      sync();
+      float lj = -kInf;
+#pragma unroll
+      for (int i = 0; i < kTabDenseKMax; ++i)
+        if (i == jj) lj = la[i];
+      const float af = (lj - lz) + Ob;
+      float lb[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) lb[k] = wr[k + 1] + vb[y0 + k + 1];  // (unconditional)
+      const float mx = tree_max<16>(lb);
+      const float c = t_safe(mx);
+      // one exponential per arc for the sum and the marginal (af + c: the log
+      // of the half row's largest arc marginal, a probability)
+      const float sc = lt_exp(af + c) * gb;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        lb[k] = lt_exp(lb[k] - c);
+        dacc[k] += lb[k] * sc;
+      }
+      const float ss = tree_sum<16>(lb);
+      float* pl = part + (jj & 1) * 256;
+      pl[w * 128 + p] = mx;
+      pl[w * 128 + 64 + p] = ss;
+      sync();
+      // the row's logsumexp from the two halves, wave 0's first on both
+      const float m0 = pl[p], s0 = pl[64 + p], m1 = pl[128 + p], s1 = pl[192 + p];
+      const float cc = t_safe(fmaxf(m0, m1));
+      const float S = s0 * lt_exp(t_safe(m0) - cc) + s1 * lt_exp(t_safe(m1) - cc);
+      const float sv = S > 0.f ? cc + lt_log_acc(S) : -kInf;
+      cur = row ? t_lae(bb, sv) : -kInf;
+    }
+    // the frame's dW into dwb (each wave its labels, wave 0 the blank)
+    if (row) {
+      if (w == 0) dwb[p * R] = mb;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (y0 + k + 1 < R) dwb[p * R + y0 + k + 1] = dacc[k];
+    }
+    sync();
+    pend = fo;
+    // beta_t over a new integer offset (floor of its max); the same on both waves
+    float m = row ? cur : -kInf;
+    m = gmax<6>(m, 6);
+    const float sp = __builtin_isfinite(m) ? floorf(m) : 0.f;
+    beta = cur - sp;
+    Ob += sp;
+  }
+  flush();
+}
+
 template <bool BF16, bool STAGE, int SR>
 LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
   if (a.K == 0) {
@@ -1429,7 +1558,11 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
   }
   if constexpr (SR == M_LOG && STAGE) {  // (STAGE and acc: the launch's LDS holds two frames)
     if (LT_TAB_DENSE && a.acc && a.K <= kTabDenseKMax && tab_dense_bigram(a)) {
-      if (threadIdx.x < 64) tab_bwd_den_dense<BF16>(a, b, sm);
+      if (a.lx && a.V == 32 && blockDim.x >= 128) {
+        if (threadIdx.x < 128) tab_bwd_den_dense2<BF16>(a, b, sm);
+      } else if (threadIdx.x < 64) {
+        tab_bwd_den_dense<BF16>(a, b, sm);
+      }
       return;
     }
   }
