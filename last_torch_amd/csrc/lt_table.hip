@@ -799,6 +799,131 @@ LT_DEVINL void tab_fwd_dense(const TArgs& a, const int b, float* sm) {
   if (lane == 0) a.dist[b] = e > 0.f ? O + c + lt_log_acc(e) : -kInf;
 }
 
+// The dense forward on TWO waves (V = 32): wave w takes destinations
+// y = 16w + 1 .. 16w + 16, four lanes a destination, each over a quarter of
+// the sources (9); the quarters merge by two xor shuffles, the vector goes
+// between expansions through a double-buffered LDS row, one barrier each.
+template <bool BF16>
+LT_DEVINL void tab_fwd_dense2(const TArgs& a, const int b, float* sm) {
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int jj = lane & 15, qd = lane >> 4;
+  const int C = a.C, R = a.R, K = a.K;
+  const int y = 16 * w + jj + 1;  // the lane's destination (V = 32: always live)
+  float* vbuf = sm;               // [2][48] the vector (slot p), -inf past C
+  float* xch = vbuf + 96;         // [2 waves][4] partial maxima / sums
+  for (int e = tid; e < 96; e += 128) vbuf[e] = -kInf;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_s_barrier();
+  int nf = a.nfr[b];
+  nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
+  const long long FR = (long long)C * R;
+  const unsigned char* wb0 = a.W + (long long)b * a.T * FR * (BF16 ? 2 : 4);
+  float wc[9], wbl = 0.f, w00 = 0.f, nwc[9], nwbl = 0.f, nw00 = 0.f;
+  auto fetch = [&](int t, float* c, float& bl, float& z) {
+    const unsigned char* wf = wb0 + (long long)t * FR * (BF16 ? 2 : 4);
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+      const int p = 9 * qd + m;
+      c[m] = p < C ? ldw<BF16>(wf, (long long)p * R + y) : 0.f;
+    }
+    bl = ldw<BF16>(wf, (long long)y * R);
+    z = ldw<BF16>(wf, 0);
+  };
+  auto sync = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  // merge (m, s) running logsumexps over the four quarter lanes of a destination
+  auto merge4 = [&](float m, float s) {
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+      const float c = t_safe(fmaxf(m, m2));
+      s = s * lt_exp(t_safe(m) - c) + s2 * lt_exp(t_safe(m2) - c);
+      m = fmaxf(m, m2);
+    }
+    return s > 0.f ? t_safe(m) + lt_log_acc(s) : -kInf;
+  };
+  if (nf > 0) fetch(0, nwc, nwbl, nw00);
+  float ay = -kInf, a0 = 0.f, O = 0.f;  // alpha relative to O (start state: one = 0)
+  for (int t = 0; t < a.T; ++t) {
+    auto hist_row = [&]() {
+      if (a.alpha) {
+        float* row = a.alpha + ((long long)b * a.T + t) * C;
+        if (qd == 0) row[y] = O + ay;
+        if (tid == 0) row[0] = O + a0;
+      }
+    };
+    if (t >= nf) {  // padding frames carry alpha (lattices.py:460-461)
+      hist_row();
+      continue;
+    }
+#pragma unroll
+    for (int m = 0; m < 9; ++m) wc[m] = nwc[m];
+    wbl = nwbl;
+    w00 = nw00;
+    if (t + 1 < nf) fetch(t + 1, nwc, nwbl, nw00);
+    hist_row();
+    float acc = ay + wbl;
+    const float acc0 = a0 + w00;
+    if (qd == 0) vbuf[y] = ay;
+    if (tid == 0) vbuf[0] = a0;
+    sync();
+    for (int i = 1; i <= K; ++i) {
+      const float* src = vbuf + ((i - 1) & 1) * 48;
+      float x[9];
+#pragma unroll
+      for (int m = 0; m < 9; ++m) x[m] = src[9 * qd + m] + wc[m];  // (-inf past C)
+      const float mx = tree_max<9>(x);
+      const float ch = t_safe(mx);
+#pragma unroll
+      for (int m = 0; m < 9; ++m) x[m] = lt_exp(x[m] - ch);
+      const float v = merge4(mx, tree_sum<9>(x));
+      acc = t_lae(acc, v + wbl);
+      if (a.lx) {
+        float* r = a.lx + (((long long)b * a.T + t) * K + (i - 1)) * C;
+        if (qd == 0) r[y] = O + v;
+        if (tid == 0) r[0] = -kInf;
+      }
+      if (i < K) {
+        float* dst = vbuf + (i & 1) * 48;
+        if (qd == 0) dst[y] = v;
+        if (tid == 0) dst[0] = -kInf;  // nothing enters the start state
+        sync();
+      }
+    }
+    // the new vector over a new integer offset: the max over both waves
+    float m = fmaxf(acc, acc0);
+    m = gmax<6>(m, 6);
+    if (lane == 0) xch[(t & 1) * 2 + w] = m;
+    sync();
+    const float mall = fmaxf(xch[(t & 1) * 2], xch[(t & 1) * 2 + 1]);
+    const float sp = __builtin_isfinite(mall) ? floorf(mall) : 0.f;
+    ay = acc - sp;
+    a0 = acc0 - sp;
+    O += sp;
+  }
+  // (+)_q alpha_T[q] (lattices.py:496): partial (max, sum) by wave, then thread 0
+  float m = gmax<6>(ay, 6);
+  m = fmaxf(m, a0);
+  const float c = t_safe(m);
+  float e = qd == 0 ? lt_exp(ay - c) : 0.f;
+  e = gsum<6>(e, 6);
+  if (w == 0) e += lt_exp(a0 - c);
+  if (lane == 0) {
+    xch[4 + 2 * w] = m;
+    xch[5 + 2 * w] = e;
+  }
+  sync();
+  if (tid == 0) {
+    const float m0 = xch[4], e0 = xch[5], m1 = xch[6], e1 = xch[7];
+    const float cc = t_safe(fmaxf(m0, m1));
+    const float S = e0 * lt_exp(t_safe(m0) - cc) + e1 * lt_exp(t_safe(m1) - cc);
+    a.dist[b] = S > 0.f ? O + cc + lt_log_acc(S) : -kInf;
+  }
+}
+
 // ---- forward: den (NUM = false) or string (NUM = true) shortest distance ----
 // STAGE: the frame's weights are copied to LDS once (coalesced) and the
 // in-arc gathers read LDS; otherwise they read W from global memory.
@@ -816,7 +941,11 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
   }
   if constexpr (!NUM && SR == M_LOG && !VIT) {
     if (LT_TAB_DENSE && tab_dense_bigram(a)) {  // (a uniform decision: every thread took it)
-      if (threadIdx.x < 64) tab_fwd_dense<BF16>(a, b, sm);
+      if (a.V == 32 && blockDim.x >= 128) {
+        if (threadIdx.x < 128) tab_fwd_dense2<BF16>(a, b, sm);
+      } else if (threadIdx.x < 64) {
+        tab_fwd_dense<BF16>(a, b, sm);
+      }
       return;
     }
   }
