@@ -114,6 +114,9 @@ template <int SR>
 LT_DEVINL float t_times(float a, float b) { return SR == M_REAL ? a * b : a + b; }
 
 constexpr int kTabMaxThreads = 512;
+#ifndef LT_TAB_BWD_WAVES
+#define LT_TAB_BWD_WAVES 4  // waves of the dense FrameLabelDependent backward (2 or 4)
+#endif
 #ifndef LT_TAB_DENSE
 #define LT_TAB_DENSE 1  // the dense-bigram FrameLabelDependent kernels (diagnostic builds: 0 = generic)
 #endif
@@ -1555,15 +1558,16 @@ LT_DEVINL void tab_bwd_den_dense(const TArgs& a, const int b, float* sm) {
 // every row (lane p = state p), so a lane forms half the arcs of a level;
 // the two halves' (max, sum) of each row's logsumexp meet through LDS at one
 // barrier a level, combined in a fixed order (both waves get the same bits).
-template <bool BF16>
+template <bool BF16, int NW>
 LT_DEVINL void tab_bwd_den_dense2(const TArgs& a, const int b, float* sm) {
+  constexpr int L = 32 / NW;  // labels a lane
   const int w = threadIdx.x >> 6, p = threadIdx.x & 63;
   const int C = a.C, R = a.R, K = a.K;
   const bool row = p < C;
-  const int y0 = 16 * w;           // the wave's labels y0 + 1 .. y0 + 16
+  const int y0 = L * w;            // the wave's labels y0 + 1 .. y0 + L
   float* vb = sm;                  // [64] cur over the states (-inf past C)
-  float* part = vb + 64;           // [2 levels][2 waves][max, sum][64]
-  float* dwb = part + 512;         // [C R] the frame's dW, stored a frame late
+  float* part = vb + 64;           // [2 levels][NW waves][max, sum][64]
+  float* dwb = part + 2 * NW * 128;  // [C R] the frame's dW, stored a frame late
   int nf = a.nfr[b];
   nf = nf < 0 ? 0 : (nf > a.T ? a.T : nf);
   const float lz = a.local ? 0.f : a.den_in[b];
@@ -1572,13 +1576,13 @@ LT_DEVINL void tab_bwd_den_dense2(const TArgs& a, const int b, float* sm) {
   const bool live = !a.local && __builtin_isfinite(nm) && __builtin_isfinite(lz) && gb != 0.f;
   const long long FR = (long long)C * R;
   const unsigned char* wb0 = a.W + (long long)b * a.T * FR * (BF16 ? 2 : 4);
-  float wr[17], nwr[17];  // w[p][0], then w[p][y0 + 1 .. y0 + 16]
+  float wr[L + 1], nwr[L + 1];  // w[p][0], then w[p][y0 + 1 .. y0 + L]
   float la[kTabDenseKMax + 1], nla[kTabDenseKMax + 1];
   auto fetch = [&](int t, float* wv, float* lv) {
     const unsigned char* f = wb0 + (long long)t * FR * (BF16 ? 2 : 4);
     wv[0] = row ? ldw<BF16>(f, (long long)p * R) : 0.f;
 #pragma unroll
-    for (int k = 1; k < 17; ++k)
+    for (int k = 1; k <= L; ++k)
       wv[k] = (row && y0 + k < R) ? ldw<BF16>(f, (long long)p * R + y0 + k) : 0.f;
     lv[0] = row ? a.hist[((long long)b * a.T + t) * C + p] : -kInf;
 #pragma unroll
@@ -1593,27 +1597,27 @@ LT_DEVINL void tab_bwd_den_dense2(const TArgs& a, const int b, float* sm) {
   if (live && nf > 0) fetch(nf - 1, nwr, nla);
   float beta = 0.f, Ob = 0.f;  // beta_{t+1}[p] relative to Ob (every state final: one)
   long long pend = -1;
-  auto flush = [&]() {  // frame pend's dW from dwb, all 128 lanes
+  auto flush = [&]() {  // frame pend's dW from dwb, every lane of the NW waves
     if (pend < 0) return;
     const int t2 = threadIdx.x;
     const int h0 = (int)((4 - (((unsigned long long)(a.dW + pend) >> 2) & 3)) & 3);
     const int n4 = (int)((FR - h0) >> 2);
     if (t2 < h0) a.dW[pend + t2] = dwb[t2];
-    for (int i = t2; i < n4; i += 128) {
+    for (int i = t2; i < n4; i += 64 * NW) {
       const int e = h0 + 4 * i;
       *(float4*)(a.dW + pend + e) = make_float4(dwb[e], dwb[e + 1], dwb[e + 2], dwb[e + 3]);
     }
-    for (int e = h0 + 4 * n4 + t2; e < FR; e += 128) a.dW[pend + e] = dwb[e];
+    for (int e = h0 + 4 * n4 + t2; e < FR; e += 64 * NW) a.dW[pend + e] = dwb[e];
     pend = -1;
   };
   for (int t = a.T - 1; t >= 0; --t) {
     const long long fo = ((long long)b * a.T + t) * FR;
     if (t >= nf || !live) {
-      for (long long e = threadIdx.x; e < FR; e += 128) a.dW[fo + e] = 0.f;
+      for (long long e = threadIdx.x; e < FR; e += 64 * NW) a.dW[fo + e] = 0.f;
       continue;
     }
 #pragma unroll
-    for (int k = 0; k < 17; ++k) wr[k] = nwr[k];
+    for (int k = 0; k <= L; ++k) wr[k] = nwr[k];
 #pragma unroll
     for (int i = 0; i <= kTabDenseKMax; ++i) la[i] = nla[i];
     if (t >= 1) fetch(t - 1, nwr, nla);  // the previous frame under this one
@@ -1623,9 +1627,9 @@ LT_DEVINL void tab_bwd_den_dense2(const TArgs& a, const int b, float* sm) {
 #pragma unroll
     for (int i = 0; i <= kTabDenseKMax; ++i)
       if (i <= K) mb += lt_exp(((la[i] - lz) + Ob) + bb) * gb;
-    float dacc[16];
+    float dacc[L];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) dacc[k] = 0.f;
+    for (int k = 0; k < L; ++k) dacc[k] = 0.f;
     float cur = row ? bb : -kInf;  // level K: blank[K] + beta
     for (int jj = K - 1; jj >= 0; --jj) {
       if (w == 0) vb[p] = cur;  // (both waves hold the same cur)
@@ -1635,28 +1639,32 @@ LT_DEVINL void tab_bwd_den_dense2(const TArgs& a, const int b, float* sm) {
       for (int i = 0; i < kTabDenseKMax; ++i)
         if (i == jj) lj = la[i];
       const float af = (lj - lz) + Ob;
-      float lb[16];
+      float lb[L];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) lb[k] = wr[k + 1] + vb[y0 + k + 1];  // (unconditional)
-      const float mx = tree_max<16>(lb);
+      for (int k = 0; k < L; ++k) lb[k] = wr[k + 1] + vb[y0 + k + 1];  // (unconditional)
+      const float mx = tree_max<L>(lb);
       const float c = t_safe(mx);
       // one exponential per arc for the sum and the marginal (af + c: the log
       // of the half row's largest arc marginal, a probability)
       const float sc = lt_exp(af + c) * gb;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
+      for (int k = 0; k < L; ++k) {
         lb[k] = lt_exp(lb[k] - c);
         dacc[k] += lb[k] * sc;
       }
-      const float ss = tree_sum<16>(lb);
-      float* pl = part + (jj & 1) * 256;
+      const float ss = tree_sum<L>(lb);
+      float* pl = part + (jj & 1) * NW * 128;
       pl[w * 128 + p] = mx;
       pl[w * 128 + 64 + p] = ss;
       sync();
-      // the row's logsumexp from the two halves, wave 0's first on both
-      const float m0 = pl[p], s0 = pl[64 + p], m1 = pl[128 + p], s1 = pl[192 + p];
-      const float cc = t_safe(fmaxf(m0, m1));
-      const float S = s0 * lt_exp(t_safe(m0) - cc) + s1 * lt_exp(t_safe(m1) - cc);
+      // the row's logsumexp from the waves' parts, in wave order on every wave
+      float mm = -kInf;
+#pragma unroll
+      for (int v = 0; v < NW; ++v) mm = fmaxf(mm, pl[v * 128 + p]);
+      const float cc = t_safe(mm);
+      float S = 0.f;
+#pragma unroll
+      for (int v = 0; v < NW; ++v) S += pl[v * 128 + 64 + p] * lt_exp(t_safe(pl[v * 128 + p]) - cc);
       const float sv = S > 0.f ? cc + lt_log_acc(S) : -kInf;
       cur = row ? t_lae(bb, sv) : -kInf;
     }
@@ -1664,7 +1672,7 @@ LT_DEVINL void tab_bwd_den_dense2(const TArgs& a, const int b, float* sm) {
     if (row) {
       if (w == 0) dwb[p * R] = mb;
 #pragma unroll
-      for (int k = 0; k < 16; ++k)
+      for (int k = 0; k < L; ++k)
         if (y0 + k + 1 < R) dwb[p * R + y0 + k + 1] = dacc[k];
     }
     sync();
@@ -1687,8 +1695,8 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
   }
   if constexpr (SR == M_LOG && STAGE) {  // (STAGE and acc: the launch's LDS holds two frames)
     if (LT_TAB_DENSE && a.acc && a.K <= kTabDenseKMax && tab_dense_bigram(a)) {
-      if (a.lx && a.V == 32 && blockDim.x >= 128) {
-        if (threadIdx.x < 128) tab_bwd_den_dense2<BF16>(a, b, sm);
+      if (a.lx && a.V == 32 && blockDim.x >= 64 * LT_TAB_BWD_WAVES) {
+        if (threadIdx.x < 64 * LT_TAB_BWD_WAVES) tab_bwd_den_dense2<BF16, LT_TAB_BWD_WAVES>(a, b, sm);
       } else if (threadIdx.x < 64) {
         tab_bwd_den_dense<BF16>(a, b, sm);
       }
