@@ -942,16 +942,6 @@ LT_DEVINL void tab_fwd_body(const TArgs& a, const int b, float* sm) {
       return;
     }
   }
-  if constexpr (!NUM && SR == M_LOG && !VIT) {
-    if (LT_TAB_DENSE && tab_dense_bigram(a)) {  // (a uniform decision: every thread took it)
-      if (a.V == 32 && blockDim.x >= 128) {
-        if (threadIdx.x < 128) tab_fwd_dense2<BF16>(a, b, sm);
-      } else if (threadIdx.x < 64) {
-        tab_fwd_dense<BF16>(a, b, sm);
-      }
-      return;
-    }
-  }
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int S = NUM ? a.U + 1 : a.C, K = a.K, R = a.R;
   int* gsm = (int*)sm;  // graph copy (STAGE): C+1 + 2*C*V ints
@@ -1693,16 +1683,7 @@ LT_DEVINL void tab_bwd_den_body(const TArgs& a, const int b, float* sm) {
     tab_bwd_den_k0_body<BF16, STAGE, SR>(a, b, sm);
     return;
   }
-  if constexpr (SR == M_LOG && STAGE) {  // (STAGE and acc: the launch's LDS holds two frames)
-    if (LT_TAB_DENSE && a.acc && a.K <= kTabDenseKMax && tab_dense_bigram(a)) {
-      if (a.lx && a.V == 32 && blockDim.x >= 64 * LT_TAB_BWD_WAVES) {
-        if (threadIdx.x < 64 * LT_TAB_BWD_WAVES) tab_bwd_den_dense2<BF16, LT_TAB_BWD_WAVES>(a, b, sm);
-      } else if (threadIdx.x < 64) {
-        tab_bwd_den_dense<BF16>(a, b, sm);
-      }
-      return;
-    }
-  }
+
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int C = a.C, V = a.V, R = a.R, K = a.K;
   int* gsm = (int*)sm;
@@ -2208,6 +2189,60 @@ __global__ __launch_bounds__(kTabMaxThreads) void tab_bwd2_kernel(const TArgs ad
   else tab_bwd_num_body<BF16>(an, blk - ad.B, sm);
 }
 
+// The Log denominator of FrameLabelDependent(K >= 1) lattices: the dense-
+// bigram kernels (tab_fwd_dense*, tab_bwd_den_dense*) when the next-state
+// table is FullNGram's bigram, else the generic bodies. Kernels of their own,
+// chosen by the host for K >= 1, so the K = 0 kernels keep their code.
+template <bool BF16, bool STAGE>
+LT_DEVINL void tab_fwd_den_fld(const TArgs& a, const int b, float* sm) {
+  if (LT_TAB_DENSE && tab_dense_bigram(a)) {  // (a uniform decision: every thread took it)
+    if (a.V == 32 && blockDim.x >= 128) {
+      if (threadIdx.x < 128) tab_fwd_dense2<BF16>(a, b, sm);
+    } else if (threadIdx.x < 64) {
+      tab_fwd_dense<BF16>(a, b, sm);
+    }
+    return;
+  }
+  tab_fwd_body<BF16, M_LOG, false, false, STAGE>(a, b, sm);
+}
+template <bool BF16, bool STAGE>
+LT_DEVINL void tab_bwd_den_fld(const TArgs& a, const int b, float* sm) {
+  // (STAGE and acc: the launch's LDS holds two frames)
+  if (LT_TAB_DENSE && STAGE && a.acc && a.K <= kTabDenseKMax && tab_dense_bigram(a)) {
+    if (a.lx && a.V == 32 && blockDim.x >= 64 * LT_TAB_BWD_WAVES) {
+      if (threadIdx.x < 64 * LT_TAB_BWD_WAVES) tab_bwd_den_dense2<BF16, LT_TAB_BWD_WAVES>(a, b, sm);
+    } else if (threadIdx.x < 64) {
+      tab_bwd_den_dense<BF16>(a, b, sm);
+    }
+    return;
+  }
+  tab_bwd_den_body<BF16, STAGE, M_LOG>(a, b, sm);
+}
+template <bool BF16, bool STAGE>
+__global__ __launch_bounds__(kTabMaxThreads) void tab_fwd_fld_kernel(const TArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  tab_fwd_den_fld<BF16, STAGE>(a, (int)blockIdx.x, sm);
+}
+template <bool BF16, bool STAGE>
+__global__ __launch_bounds__(kTabMaxThreads) void tab_fwd2_fld_kernel(const TArgs ad, const TArgs an) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int blk = (int)blockIdx.x;
+  if (blk < ad.B) tab_fwd_den_fld<BF16, STAGE>(ad, blk, sm);
+  else tab_fwd_body<BF16, M_LOG, true, false, false>(an, blk - ad.B, sm);
+}
+template <bool BF16, bool STAGE>
+__global__ __launch_bounds__(kTabMaxThreads) void tab_bwd_den_fld_kernel(const TArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  tab_bwd_den_fld<BF16, STAGE>(a, (int)blockIdx.x, sm);
+}
+template <bool BF16, bool STAGE>
+__global__ __launch_bounds__(kTabMaxThreads) void tab_bwd2_fld_kernel(const TArgs ad, const TArgs an) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int blk = (int)blockIdx.x;
+  if (blk < ad.B) tab_bwd_den_fld<BF16, STAGE>(ad, blk, sm);
+  else tab_bwd_num_body<BF16>(an, blk - ad.B, sm);
+}
+
 // dW -= the numerator's chain-head sums (one writer per element and frame)
 __global__ __launch_bounds__(256) void tab_apply_kernel(const TArgs a) {
   const int NK = 2 * (a.U + 1);
@@ -2541,7 +2576,9 @@ int launch_t_fwd_s(int sr, bool num, bool vit, const TArgs& a, int lds, hipStrea
     if (sr == M_MAX) return t_launch(tab_fwd_kernel<BF16, M_MAX, true, false, false>, a.B, lds, st, a);
     return t_launch(tab_fwd_kernel<BF16, M_REAL, true, false, false>, a.B, lds, st, a);
   }
-  if (sr == M_LOG) return t_launch(tab_fwd_kernel<BF16, M_LOG, false, false, STG>, a.B, lds, st, a);
+  if (sr == M_LOG)
+    return a.K > 0 ? t_launch(tab_fwd_fld_kernel<BF16, STG>, a.B, lds, st, a)
+                   : t_launch(tab_fwd_kernel<BF16, M_LOG, false, false, STG>, a.B, lds, st, a);
   if (sr == M_MAX) return t_launch(tab_fwd_kernel<BF16, M_MAX, false, false, STG>, a.B, lds, st, a);
   return t_launch(tab_fwd_kernel<BF16, M_REAL, false, false, STG>, a.B, lds, st, a);
 }
@@ -2682,12 +2719,16 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
     const long long staged = (long long)ld + graph_lds(a) + (a.K == 0 ? 8 : 4) * FR;
     if (staged <= kStageBudget) {
       const int l2 = std::max((int)staged, ln);
-      rc = bf16 ? t_launch2(tab_fwd2_kernel<true, true>, 2 * a.B, l2, st, ad, an)
-                : t_launch2(tab_fwd2_kernel<false, true>, 2 * a.B, l2, st, ad, an);
+      rc = K > 0 ? (bf16 ? t_launch2(tab_fwd2_fld_kernel<true, true>, 2 * a.B, l2, st, ad, an)
+                         : t_launch2(tab_fwd2_fld_kernel<false, true>, 2 * a.B, l2, st, ad, an))
+                 : (bf16 ? t_launch2(tab_fwd2_kernel<true, true>, 2 * a.B, l2, st, ad, an)
+                         : t_launch2(tab_fwd2_kernel<false, true>, 2 * a.B, l2, st, ad, an));
     } else {
       const int l2 = std::max(ld, ln);
-      rc = bf16 ? t_launch2(tab_fwd2_kernel<true, false>, 2 * a.B, l2, st, ad, an)
-                : t_launch2(tab_fwd2_kernel<false, false>, 2 * a.B, l2, st, ad, an);
+      rc = K > 0 ? (bf16 ? t_launch2(tab_fwd2_fld_kernel<true, false>, 2 * a.B, l2, st, ad, an)
+                         : t_launch2(tab_fwd2_fld_kernel<false, false>, 2 * a.B, l2, st, ad, an))
+                 : (bf16 ? t_launch2(tab_fwd2_kernel<true, false>, 2 * a.B, l2, st, ad, an)
+                         : t_launch2(tab_fwd2_kernel<false, false>, 2 * a.B, l2, st, ad, an));
     }
     if (rc) return rc;
   } else {
@@ -2725,8 +2766,10 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
     ad.acc = K > 0 && lds_d + graph_lds(a) + 8 * FR <= kStageBudget;
     const int l2 =
         std::max((int)(lds_d + graph_lds(a) + ((ad.acc || K == 0) ? 8 : 4) * FR), lds_n);
-    rc = bf16 ? t_launch2(tab_bwd2_kernel<true, true>, 2 * a.B, l2, st, ad, an)
-              : t_launch2(tab_bwd2_kernel<false, true>, 2 * a.B, l2, st, ad, an);
+    rc = K > 0 ? (bf16 ? t_launch2(tab_bwd2_fld_kernel<true, true>, 2 * a.B, l2, st, ad, an)
+                       : t_launch2(tab_bwd2_fld_kernel<false, true>, 2 * a.B, l2, st, ad, an))
+               : (bf16 ? t_launch2(tab_bwd2_kernel<true, true>, 2 * a.B, l2, st, ad, an)
+                       : t_launch2(tab_bwd2_kernel<false, true>, 2 * a.B, l2, st, ad, an));
   } else {
     const int l2 = std::max(lds_d, lds_n);
     rc = bf16 ? t_launch2(tab_bwd2_kernel<true, false>, 2 * a.B, l2, st, ad, an)
@@ -2830,8 +2873,10 @@ int lt_table_den_backward(const lt_graph* g, const lt_table_problem* pb, int32_t
       a.acc = K > 0 && lds_d + graph_lds(a) + 8 * FR <= kStageBudget;
       const int lds = (int)(lds_d + graph_lds(a) + ((a.acc || K == 0) ? 8 : 4) * FR);
       if (semiring == M_LOG)
-        rc = bf16 ? t_launch(tab_bwd_den_kernel<true, true, M_LOG>, a.B, lds, st, a)
-                  : t_launch(tab_bwd_den_kernel<false, true, M_LOG>, a.B, lds, st, a);
+        rc = a.K > 0 ? (bf16 ? t_launch(tab_bwd_den_fld_kernel<true, true>, a.B, lds, st, a)
+                             : t_launch(tab_bwd_den_fld_kernel<false, true>, a.B, lds, st, a))
+                     : (bf16 ? t_launch(tab_bwd_den_kernel<true, true, M_LOG>, a.B, lds, st, a)
+                             : t_launch(tab_bwd_den_kernel<false, true, M_LOG>, a.B, lds, st, a));
       else
         rc = bf16 ? t_launch(tab_bwd_den_kernel<true, true, M_REAL>, a.B, lds, st, a)
                   : t_launch(tab_bwd_den_kernel<false, true, M_REAL>, a.B, lds, st, a);
