@@ -529,6 +529,8 @@ LT_DEVINL void tab_str_fwd_log(const TArgs& a, const int b, float* sm) {
         for (int u = tid; u < S; u += nthr) {
           il[u] = ia[u];
           fl[u] = fa[u];
+          // (lt_table_loss_grad: L^i alpha kept for the string backward)
+          if (a.lx) a.lx[(((long long)b * a.T + t) * K + (i - 1)) * S + u] = ia[u] + fa[u];
           lae_split(ic[u], fc[u], ia[u], fa[u] + wl[2 * u], ic[u], fc[u]);
         }
         __syncthreads();
@@ -2096,12 +2098,18 @@ LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
                                           : 0.f;
     };
   };
+  // the forward's lexical alphas L^i alpha_t (lt_table_loss_grad), [K][S] a frame
+  auto ldx = [&](int t) {
+    return [=](int e) { return a.lx[((long long)b * a.T + t) * K * S + e]; };
+  };
   RegStage<1> hs;
   RegStage<2> cs, ds;
+  RegStage<2> xs;
   if (nf > 0) {
     hs.fetch(S, ldh(nf - 1));
     cs.fetch(2 * S, ldc(nf - 1));
     ds.fetch(NK, ldd(nf - 1));
+    if (a.lx) xs.fetch(K * S, ldx(nf - 1));
   }
   // a string arc's marginal exp(alpha + w + beta' - num), beta' = (i, f):
   // the large terms first, ((alpha - num) + i) + (f + w)
@@ -2111,12 +2119,14 @@ LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
     hs.store(la, S, ldh(t));
     cs.store(wc, 2 * S, ldc(t));
     ds.store(dh, NK, ldd(t));
+    if (a.lx) xs.store(la + S, K * S, ldx(t));
     hs.fetch(t >= 1 ? S : 0, ldh(t - 1));
     cs.fetch(t >= 1 ? 2 * S : 0, ldc(t - 1));
     ds.fetch(t >= 1 ? NK : 0, ldd(t - 1));
+    if (a.lx) xs.fetch(t >= 1 ? K * S : 0, ldx(t - 1));
     auto wr = [&](int i) { return wc[i]; };
     __syncthreads();
-    for (int i = 1; i <= K; ++i) {
+    for (int i = 1; i <= K && !a.lx; ++i) {  // (recomputed without the forward's)
       for (int u = tid; u < S; u += nthr)
         la[(long long)i * S + u] = t_reduce<M_LOG>(ng, u, la + (long long)(i - 1) * S, wr, nullptr);
       __syncthreads();
@@ -2164,10 +2174,13 @@ LT_DEVINL void tab_bwd_num_body(const TArgs& a, const int b, float* sm) {
       if (a.nsub) a.nsub[((long long)b * a.T + t) * NK + k] = s;
       else stw<false>(a.dW, fo + elem(k), dh[k] - s);
     }
-    __syncthreads();
-    for (int u = tid; u < S; u += nthr) {
-      bi[u] = pi[u];
-      bf[u] = pf[u];
+    // beta_t: the last level's buffers become beta (their roles swap, no copy)
+    if (pi == ai) {
+      ai = bi; bi = pi;
+      af = bf; bf = pf;
+    } else {
+      ci = bi; bi = pi;
+      cf = bf; bf = pf;
     }
     __syncthreads();
   }
@@ -2606,7 +2619,7 @@ int t_fwd(int sr, bool num, bool vit, const TArgs& a, bool bf16, hipStream_t st)
 }
 
 struct GradLayout {
-  size_t hd, hn, nsub, ntab, dwf, lx, total;
+  size_t hd, hn, nsub, ntab, dwf, lx, lxn, total;
 };
 GradLayout grad_layout(const lt_graph* g, const lt_table_problem* pb) {
   auto up = [](long long x) { return (size_t)((x + 255) & ~255LL); };
@@ -2619,7 +2632,8 @@ GradLayout grad_layout(const lt_graph* g, const lt_table_problem* pb) {
   l.dwf = l.ntab + up(4LL * pb->batch * NK);
   const bool bf16 = pb->weight_dtype == LT_DTYPE_BF16;
   l.lx = l.dwf + (bf16 ? up(4 * BT * g->num_states * (g->vocab_size + 1)) : 0);
-  l.total = l.lx + (g->expansions > 0 ? up(4 * BT * g->expansions * g->num_states) : 0);
+  l.lxn = l.lx + (g->expansions > 0 ? up(4 * BT * g->expansions * g->num_states) : 0);
+  l.total = l.lxn + (g->expansions > 0 ? up(4 * BT * g->expansions * (pb->max_labels + 1)) : 0);
   return l;
 }
 
@@ -2713,6 +2727,7 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   ad.lx = (dW && K > 0) ? (float*)((char*)workspace + l.lx) : nullptr;
   an.dist = num;
   an.alpha = hn;
+  an.lx = (dW && K > 0) ? (float*)((char*)workspace + l.lxn) : nullptr;
   if (!local_norm) {
     const int ln = fwd_lds(S) + 16 * S;
     const int ld = fwd_lds(C);
@@ -2752,6 +2767,7 @@ int lt_table_loss_grad(const lt_graph* g, const lt_table_problem* pb, int32_t lo
   ad = a;
   an = a;
   ad.hist = hd;
+  an.lx = (dW && K > 0) ? (float*)((char*)workspace + l.lxn) : nullptr;
   ad.lx = (dW && K > 0) ? (float*)((char*)workspace + l.lx) : nullptr;
   ad.nsub = nullptr;
   ad.ntab = nullptr;
