@@ -1052,7 +1052,7 @@ LT_DEVINL void store_unit(unsigned char* p, const float* v) {
 // publishes the count after it (an sc1 store; the marginal workgroups on the
 // same XCD poll it with sc1 loads and read the rows with sc1 loads)
 #ifndef LT_TRI_PUB
-#define LT_TRI_PUB 64
+#define LT_TRI_PUB 16  // (64: 3.28-3.29 ms at cfg5, 16: 3.25-3.26, 8: 3.36-3.39; profiles/r06_tri_pub_ab.txt)
 #endif
 constexpr int kTriPub = LT_TRI_PUB;
 LT_DEVINL bool tri_pub_frame(const KArgs& a, int i) { return a.prog && i > 0 && i % kTriPub == 0; }
