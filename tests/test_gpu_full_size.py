@@ -248,8 +248,9 @@ def test_viterbi_long_utterances_backtrace_routes(cuda, T):
 
 def test_cfg5_trigram_bf16(cuda):
   """cfg5: trigram (|ctx| = 1057) bf16 arc weights at B=32, T=1000, U=100
-  (the product build runs the one-workgroup recursions of lt_tri.hip and
-  marg_kernel; the quad design, lt_tri4.hip, is diagnostic-only and covered by
+  (lt_loss_grad's trigram overlap: the one-workgroup recursions of lt_tri.hip
+  with marginal waves on the idle CUs, tri_mix_kernel, then marg_kernel on the
+  frames left; the quad design, lt_tri4.hip, is diagnostic-only and covered by
   test_gpu_diag.py): losses and every dW element of sixteen utterances spread
   over the batch against the oracle on the bf16-rounded weights; per-frame
   marginal sums of the whole batch."""
@@ -266,6 +267,24 @@ def test_cfg5_trigram_bf16(cuda):
   _, den = orc.den_grad(Wc, nfc, V, n)
   assert_loss_close(loss[idx].cpu().numpy(), rl)
   assert_grad_marginal_close(dW[idx].float().cpu().numpy(), rdW, den, rlz, rnum, bf16=True)
+
+
+def test_trigram_overlap_b8_t1000_every_utterance(cuda):
+  """The trigram overlap with one utterance per XCD, so that each marginal
+  wave takes many frames of its utterance (B = 8, T = 1000: cus - 2B marginal
+  workgroups for 8000 frames): every dW element of every utterance against the
+  oracle. A build that computed only each wave's first frame right (DESIGN.md
+  3d, the open item) fails here."""
+  V, n = 32, 2
+  W, nf, lab, nl = _bench_inputs(8, 1000, 100, V, n, cuda, seed=11, dtype=torch.bfloat16)
+  assert nat.loss_grad_design(8, 1000, 100, V, n) == nat.DESIGN_CHECKPOINTS
+  loss, lz, num, dW = nat.loss_grad(W, nf, lab, nl, V, n, False)
+  orc = _orc()
+  Wc, nfc, labc, nlc = _np(W, nf, lab, nl)
+  rl, rlz, rnum, rdW = orc.loss_grad(Wc, nfc, labc, nlc, V, n)
+  _, den = orc.den_grad(Wc, nfc, V, n)
+  assert_loss_close(loss.cpu().numpy(), rl)
+  assert_grad_marginal_close(dW.float().cpu().numpy(), rdW, den, rlz, rnum, bf16=True)
 
 
 @pytest.mark.parametrize('B', [8, 64, 120, 160, 176, 177, 192, 256, 512])

@@ -274,7 +274,7 @@ def test_trigram_overlap_loss_grad_vs_oracle(cuda, dt):
   recursions with marginal workgroups on the CUs they leave idle, each taking
   frames as both recursions pass them, then marg_kernel on the frames they
   did not take. B = 8 (the route needs a multiple of 8), T = 160 (progress
-  published every 64 frames), lengths 0, 1, 2, 3, T - 1 and T, epsilon labels,
+  published every 16 frames), lengths 0, 1, 2, 3, T - 1 and T, epsilon labels,
   an unreachable string: loss and every dW element against the oracle, and a
   second call bit-identical (which kernel takes a frame does not change it)."""
   orc = _orc()
