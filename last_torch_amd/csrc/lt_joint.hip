@@ -259,7 +259,7 @@ __global__ __launch_bounds__(64 * (NW < 2 ? 2 : NW), 2) void jf_marg_kernel(cons
   f32x16 dwo0 = {}, dwo1 = {};
   float dbias = 0.f;  // thread tid < R: sum of g[:, tid]
   JSTAMP(a, 1, JCLK());
-  long long tf = 0, tc = 0, tb = 0, tw = 0;  // wave 0: W tile, marginals, barrier, backward
+  [[maybe_unused]] long long tf = 0, tc = 0, tb = 0, tw = 0;  // wave 0: W tile, marginals, barrier, backward
 
   for (int c = 0, buf = 0; c < C; ++c, buf ^= 1) {
     float* g = gt + buf * 32 * GS;

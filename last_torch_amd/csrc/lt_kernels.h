@@ -2139,7 +2139,6 @@ inline bool stream_capturing(hipStream_t st) {
 int launch_tri_fwdbwd(const Plan& pf, const Plan& pb, bool bf16, int nb, hipStream_t st);
 // lt_tri.hip: the same recursions with marginal workgroups on the idle CUs
 // (tri_mix_kernel, V = 32); marg_kernel afterwards takes the frames not done
-int tri_mix_lds(const NGram& g, int U, int B);
 int launch_tri_mix(const Plan& pf, const Plan& pb, bool bf16, int nb, int marg_blocks,
                    const MixArgs& mx, hipStream_t st);
 // lt_tri4.hip (diagnostic builds only): the V = 32 trigram recursions on
