@@ -233,16 +233,28 @@ LT_DEVINL void backtrace_body(const VbtArgs& a, int b, int tid, int nth, unsigne
 #ifndef LT_VIT_NAP
 #define LT_VIT_NAP 4  // s_sleep count of the followers' progress polls
 #endif
+// the rings' depths: the slack the loader and the chain have on the
+// backpointer waves, which lag the chain by jitter more than by throughput
+// (cfg4: kTw 16 -> 22 and kSAl 16 -> 32 with kRing 10 -> 8, 0.602 -> 0.565 ms;
+// a third backpointer wave or a deeper DMA ring did not help); the
+// diagnostic build's stamp buffer takes 4 KB of the LDS
 #ifndef LT_VIT_TW
-#define LT_VIT_TW 16
+#ifdef LT_DIAG
+#define LT_VIT_TW 20
+#else
+#define LT_VIT_TW 22
+#endif
 #endif
 #ifndef LT_VIT_SAL
-#define LT_VIT_SAL 16
+#define LT_VIT_SAL 32
 #endif
 #ifndef LT_VIT_BT_FUSE
 #define LT_VIT_BT_FUSE 1  // the backtrace in the forward's launch when it fits
 #endif
-constexpr int kRing = 10;          // raw frames: kRing - 2 in flight, taken in pairs
+#ifndef LT_VIT_RING
+#define LT_VIT_RING 8
+#endif
+constexpr int kRing = LT_VIT_RING;  // raw frames: kRing - 2 in flight, taken in pairs
 constexpr int kTw = LT_VIT_TW;     // transposed frames
 constexpr int kSAl = LT_VIT_SAL;   // alpha rows
 constexpr int kPub = LT_VIT_PUB;   // the chain publishes its progress every kPub frames
